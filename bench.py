@@ -1,0 +1,182 @@
+#!/usr/bin/env python3
+"""Benchmark of the RRDB-23 + CEM ×4 super-resolution hot path on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N --steps K --warmup W]        (N>1: launched by torch.distributed.run, one rank per GPU)
+
+A step = one forward of CEM_PyTorch(RRDBNet-23) in eval mode (CEM pre-pad, the reference's test path
+SRRaGANModel.test(), SRRaGAN_model.py:577-584) over one batch of B synthetic 128×128 LR images already resident in
+HBM, producing B 512×512 HR images.  Multi-GPU: images are independent, so each rank runs its own batch (weak scaling,
+no collective in the data path); timing is barrier + synchronize bracketed and the max over ranks is reported.
+
+One JSON line on rank 0: value = HR Mpixels/s over all ranks; `roofline` = the dominant kernel (the 3×3 conv
+instantiation that takes the most time) from HIP events around every launch in the timed region; `cpu_baseline` =
+the CPU oracle restatement (oracle/esr_oracle.py, PyTorch-CPU oneDNN convs) on a bounded sample, rank 0 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, 'explorable-super-resolution_old_amd'))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = json.load(open(os.path.join(REPO, 'BASELINE.json')))['metric']
+FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix = vector peak (f32-input MFMA)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=10)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--batch', type=int, default=32, help='images per GPU (BASELINE config 2: 32)')
+    ap.add_argument('--lr-size', type=int, default=128)
+    ap.add_argument('--nb', type=int, default=23)
+    ap.add_argument('--variant', choices=['plain', 'latent'], default='plain')
+    ap.add_argument('--no-cem', action='store_true', help='bare RRDBNet (no CEM, no pre-pad)')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-images', type=int, default=8, help='images in the bounded CPU-baseline sample')
+    return ap.parse_args()
+
+
+def build_model(args, dev):
+    import esr_amd
+    from esr_amd import CEMnet as C
+    latent = args.variant == 'latent'
+    torch.manual_seed(1234)
+    net = esr_amd.RRDBNet(3, 3, 64, args.nb, latent_input='all_layers_HR_downscaled' if latent else None,
+                          num_latent_channels=3 if latent else 0)
+    model = net if args.no_cem else C.CEMnet(C.Get_CEM_Config(4)).WrapArchitecture_PyTorch(net)
+    esr_amd.init_weights(model, 'kaiming', scale=0.1)  # define_G's training-time init (networks.py:97-98)
+    with torch.no_grad():  # nonzero biases so the epilogue is exercised
+        for n, p in model.named_parameters():
+            if n.endswith('bias'):
+                p.uniform_(-0.01, 0.01)
+    model.eval()
+    return model.to(dev)
+
+
+def make_input(args, dev, rank):
+    g = torch.Generator().manual_seed(100 + rank)
+    B, h = args.batch, args.lr_size
+    x = torch.rand(B, 3, h, h, generator=g)
+    if args.variant == 'latent':  # per-image constant Z (training-time feed_data), raw HR view (ConcatLatent)
+        z = (2 * torch.rand(B, 3, 1, 1, generator=g) - 1).expand(B, 3, 4 * h, 4 * h).contiguous()
+        x = torch.cat([z.view(B, 48, h, h), x], 1)
+    return x.to(dev)
+
+
+def cpu_baseline(args, model, x_gpu, out_gpu):
+    """The CPU oracle on a bounded sample of the same workload (same weights, same images), rank 0 only."""
+    from oracle import esr_oracle as O
+    threads = min(os.cpu_count() or 1, 16)  # the GPU box gives one GPU a 16-CPU share
+    torch.set_num_threads(threads)
+    sd = {k: v.detach().float().cpu() for k, v in model.state_dict().items()}
+    P = O.strip_prefix({k: v for k, v in sd.items() if 'Filter' not in k})
+    design = None if args.no_cem else O.cem_design(4)
+    n = max(1, min(args.cpu_images, x_gpu.shape[0]))
+    xs = x_gpu[:n].cpu()
+    latent = args.variant == 'latent'
+    with torch.no_grad():
+        O.sr_forward(xs[:1], P, args.nb, latent, design, pre_pad=design is not None)  # warm-up
+        t0 = time.perf_counter()
+        outs = [O.sr_forward(xs[i:i + 1], P, args.nb, latent, design, pre_pad=design is not None) for i in range(n)]
+        dt = time.perf_counter() - t0
+    ref = torch.cat(outs)
+    got = out_gpu[:n].cpu().double()
+    err = float((got - ref.double()).abs().max() / ref.double().abs().max())
+    mse = float(((got - ref.double()) ** 2).mean())
+    hr = 4 * args.lr_size
+    return ({'value': round(n * hr * hr / dt / 1e6, 4), 'unit': 'HR Mpixels/s', 'cores': threads, 'kind': 'port',
+             'sample': '%d image(s) of 128x128 LR -> 512x512, same weights/inputs as the GPU run, PyTorch-CPU '
+                       '(oneDNN) restatement oracle/esr_oracle.py, %d threads' % (n, threads)},
+            {'normwise_rel_err_vs_cpu_ref': err, 'psnr_vs_ref_db': (10 * np.log10(1.0 / mse)) if mse > 0 else None,
+             'images_compared': n})
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=dev)
+    from esr_amd import engine
+    model = build_model(args, dev)
+    x = make_input(args, dev, rank)
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            out = model(x)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        prof = []
+        engine._PROFILE = prof
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = model(x)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        engine._PROFILE = None
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.barrier()
+        dt = float(t.item())
+    hr = 4 * args.lr_size
+    total_px = world * args.batch * hr * hr * args.steps
+    value = total_px / dt / 1e6
+    # roofline of the dominant kernel from the per-launch events
+    per = {}
+    for tag, flops, s, e in prof:
+        ms = s.elapsed_time(e)
+        a = per.setdefault(tag, [0, 0.0, 0.0])
+        a[0] += 1
+        a[1] += flops
+        a[2] += ms
+    dom = max(per, key=lambda k: per[k][2])
+    n_l, fl, ms = per[dom]
+    achieved = (fl / n_l) / (ms / n_l / 1e3) / 1e12
+    kernels = {k: {'launches_per_step': v[0] // args.steps, 'avg_us': round(v[2] / v[0] * 1e3, 2),
+                   'tflops': round(v[1] / (v[2] / 1e3) / 1e12, 2), 'share_of_gpu_time': None}
+               for k, v in per.items()}
+    tot = sum(v[2] for v in per.values())
+    for k in kernels:
+        kernels[k]['share_of_gpu_time'] = round(per[k][2] / (dt * 1e3), 3)
+    rec = {
+        'metric': METRIC, 'value': round(value, 3), 'unit': 'HR Mpixels/s', 'n_gpus': world, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': round(dt / args.steps * 1e3, 3), 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
+        'config': {'workload': 'RRDB-23 x4 %s%s, batch %d x %dx%d LR -> %dx%d HR per GPU (BASELINE config 2 shape)'
+                               % (args.variant, '' if args.no_cem else ' + CEM (eval, LR pre-pad 10)', args.batch,
+                                  args.lr_size, args.lr_size, hr, hr),
+                   'global_batch': world * args.batch, 'nb': args.nb, 'parallelism': 'dp%d (image sharding, no '
+                   'data-path collective)' % world},
+        'roofline': {'bound': 'mfma', 'kernel': dom, 'achieved': round(achieved, 2), 'peak': FP32_PEAK_TFLOPS,
+                     'unit': 'TFLOP/s', 'frac': round(achieved / FP32_PEAK_TFLOPS, 4), 'traffic': None,
+                     'flops_per_launch': fl / n_l, 'avg_launch_us': round(ms / n_l * 1e3, 2)},
+        'kernels': kernels,
+        'gpu_busy_frac': round(tot / (dt * 1e3), 3),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cb, parity = cpu_baseline(args, model, x, out)
+        rec['cpu_baseline'] = cb
+        rec['parity'] = parity
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

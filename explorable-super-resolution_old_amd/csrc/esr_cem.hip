@@ -1,0 +1,227 @@
+// esr_cem.hip — Consistency Enforcing Module (CEM) stencils and model-input preparation for gfx950.
+//
+// The CEM step (CEMnet.py:184-190) is  out = Up(Inv(LR)) + gen - Up(Inv(Down(gen)))  with three fixed depthwise
+// filters.  By linearity it equals  gen + Up(Inv(LR - Down(gen))),  which we evaluate as three HBM-bound stencil
+// passes with exact reference indexing:
+//   esr_cem_down   : r = LR - Down(gen)            polyphase: only the sf-strided phase of the ×sf grid is computed
+//   esr_cem_inv    : q = Inv(r)                    replicate-padded depthwise xcorr at LR resolution
+//   esr_cem_up_add : out = crop(gen + Up(q))       zero-stuffed ×sf grid never materialised; only taps that land on
+//                                                 a stuffed sample are visited
+// Replicate padding is realised as index clamping (ReplicationPad2d, CEMnet.py:63-64,150,158).
+#include <hip/hip_runtime.h>
+#include "esr_amd.h"
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int MAXK = 64;  // largest supported filter side
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+__global__ __launch_bounds__(NT) void cem_down_kernel(const float *__restrict__ gen, const float *__restrict__ lr,
+                                                      float *__restrict__ r, int B, int H, int W, int sf, int ph,
+                                                      const float *__restrict__ wd, int kd, int negate) {
+    __shared__ float sw[MAXK * MAXK];
+    for (int i = threadIdx.x; i < kd * kd; i += NT) sw[i] = wd[i];
+    __syncthreads();
+    const long long total = (long long)B * 3 * H * W;
+    const long long idx = (long long)blockIdx.x * NT + threadIdx.x;
+    if (idx >= total) return;
+    const int j = idx % W;
+    const int i = (idx / W) % H;
+    const long long plane = idx / ((long long)H * W);  // b*3 + c
+    const int HH = sf * H, WW = sf * W;
+    const float *g = gen + plane * HH * WW;
+    const int pd = kd / 2;
+    const int ry = sf * i + ph - pd, rx = sf * j + ph - pd;
+    float acc = 0.f;
+    for (int u = 0; u < kd; ++u) {
+        const float *grow = g + (long long)clampi(ry + u, 0, HH - 1) * WW;
+        const float *wrow = sw + u * kd;
+        for (int v = 0; v < kd; ++v) acc += wrow[v] * grow[clampi(rx + v, 0, WW - 1)];
+    }
+    float out = (lr ? lr[idx] : 0.f) - acc;
+    r[idx] = negate ? -out : out;
+}
+
+__global__ __launch_bounds__(NT) void cem_inv_kernel(const float *__restrict__ rin, float *__restrict__ q, int B,
+                                                     int H, int W, const float *__restrict__ wi, int ki) {
+    __shared__ float sw[MAXK * MAXK];
+    for (int i = threadIdx.x; i < ki * ki; i += NT) sw[i] = wi[i];
+    __syncthreads();
+    const long long total = (long long)B * 3 * H * W;
+    const long long idx = (long long)blockIdx.x * NT + threadIdx.x;
+    if (idx >= total) return;
+    const int j = idx % W;
+    const int i = (idx / W) % H;
+    const long long plane = idx / ((long long)H * W);
+    const float *src = rin + plane * H * W;
+    const int pd = ki / 2;
+    float acc = 0.f;
+    for (int u = 0; u < ki; ++u) {
+        const float *row = src + (long long)clampi(i + u - pd, 0, H - 1) * W;
+        const float *wrow = sw + u * ki;
+        for (int v = 0; v < ki; ++v) acc += wrow[v] * row[clampi(j + v - pd, 0, W - 1)];
+    }
+    q[idx] = acc;
+}
+
+__global__ __launch_bounds__(NT) void cem_up_add_kernel(const float *__restrict__ q, const float *__restrict__ gen,
+                                                        float *__restrict__ out, int B, int H, int W, int sf, int ph,
+                                                        const float *__restrict__ wu, int kd, int M) {
+    __shared__ float sw[MAXK * MAXK];
+    for (int i = threadIdx.x; i < kd * kd; i += NT) sw[i] = wu[i];
+    __syncthreads();
+    const int HH = sf * H, WW = sf * W;
+    const int OH = HH - 2 * M, OW = WW - 2 * M;
+    const long long total = (long long)B * 3 * OH * OW;
+    const long long idx = (long long)blockIdx.x * NT + threadIdx.x;
+    if (idx >= total) return;
+    const int X = idx % OW;
+    const int Y = (idx / OW) % OH;
+    const long long plane = idx / ((long long)OH * OW);
+    const float *qp = q + plane * H * W;
+    const int pd = kd / 2;
+    float acc = 0.f;
+    for (int u = 0; u < kd; ++u) {
+        const int py = clampi(Y + M + u - pd, 0, HH - 1) - ph;  // position in the stuffed grid, relative to phase
+        if (py < 0 || py % sf) continue;
+        const float *qrow = qp + (long long)(py / sf) * W;
+        const float *wrow = sw + u * kd;
+        for (int v = 0; v < kd; ++v) {
+            const int px = clampi(X + M + v - pd, 0, WW - 1) - ph;
+            if (px < 0 || px % sf) continue;
+            acc += wrow[v] * qrow[px / sf];
+        }
+    }
+    out[idx] = gen[(plane * HH + Y + M) * WW + X + M] + acc;
+}
+
+// ---- model-input preparation ----
+
+struct PrepParams {
+    const float *x;
+    int B, nz, h, w, sf, m;
+    float *lr_nchw;
+    float *first;
+    int first_cp, first_lr_off;
+    float *zlr[4];
+    int zlr_cp[4];
+    int n_zlr;
+    float *zhr[4];
+    int zhr_cp[4];
+    int n_zhr;
+};
+
+// Z_HR (replicate-padded by sf*m) at padded-HR coords (Y, X), channel c.
+__device__ __forceinline__ float zhr_at(const PrepParams &p, int b, int c, int Y, int X) {
+    const int Hs = p.sf * p.h, Ws = p.sf * p.w;
+    const int yy = clampi(Y - p.sf * p.m, 0, Hs - 1), xx = clampi(X - p.sf * p.m, 0, Ws - 1);
+    const long long bstride = (long long)(p.nz * p.sf * p.sf + 3) * p.h * p.w;
+    return p.x[b * bstride + (long long)c * Hs * Ws + (long long)yy * Ws + xx];
+}
+
+__global__ __launch_bounds__(NT) void prep_lr_kernel(PrepParams p) {
+    const int H = p.h + 2 * p.m, W = p.w + 2 * p.m;
+    const long long total = (long long)p.B * H * W;
+    const long long idx = (long long)blockIdx.x * NT + threadIdx.x;
+    if (idx >= total) return;
+    const int x = idx % W;
+    const int y = (idx / W) % H;
+    const int b = idx / ((long long)H * W);
+    const long long pix = ((long long)b * (H + 2) + y + 1) * (W + 2) + x + 1;
+    const long long bstride = (long long)(p.nz * p.sf * p.sf + 3) * p.h * p.w;
+    const int sy = clampi(y - p.m, 0, p.h - 1), sx = clampi(x - p.m, 0, p.w - 1);
+    const float *lr = p.x + b * bstride + (long long)p.nz * p.sf * p.sf * p.h * p.w;
+    for (int c = 0; c < 3; ++c) {
+        const float v = lr[(long long)c * p.h * p.w + (long long)sy * p.w + sx];
+        if (p.lr_nchw) p.lr_nchw[(((long long)b * 3 + c) * H + y) * W + x] = v;
+        if (p.first) p.first[pix * p.first_cp + p.first_lr_off + c] = v;
+    }
+    if (p.nz == 0) return;
+    // F.interpolate(scale 1/sf, bilinear, align_corners=False): src = (d+0.5)*sf-0.5
+    const float fy = (y + 0.5f) * p.sf - 0.5f, fx = (x + 0.5f) * p.sf - 0.5f;
+    const int Hs = p.sf * H, Ws = p.sf * W;
+    const int y0 = (int)fy, x0 = (int)fx;
+    const int y1 = min(y0 + 1, Hs - 1), x1 = min(x0 + 1, Ws - 1);
+    const float ly = fy - y0, lx = fx - x0;
+    const float hy0 = 1.f - ly, hx0 = 1.f - lx;
+    for (int c = 0; c < p.nz; ++c) {
+        const float v = hy0 * (hx0 * zhr_at(p, b, c, y0, x0) + lx * zhr_at(p, b, c, y0, x1)) +
+                        ly * (hx0 * zhr_at(p, b, c, y1, x0) + lx * zhr_at(p, b, c, y1, x1));
+        if (p.first) p.first[pix * p.first_cp + c] = v;
+        for (int k = 0; k < p.n_zlr; ++k) p.zlr[k][pix * p.zlr_cp[k] + c] = v;
+    }
+}
+
+__global__ __launch_bounds__(NT) void prep_hr_kernel(PrepParams p) {
+    const int Hs = p.sf * (p.h + 2 * p.m), Ws = p.sf * (p.w + 2 * p.m);
+    const long long total = (long long)p.B * Hs * Ws;
+    const long long idx = (long long)blockIdx.x * NT + threadIdx.x;
+    if (idx >= total) return;
+    const int X = idx % Ws;
+    const int Y = (idx / Ws) % Hs;
+    const int b = idx / ((long long)Hs * Ws);
+    const long long pix = ((long long)b * (Hs + 2) + Y + 1) * (Ws + 2) + X + 1;
+    for (int c = 0; c < p.nz; ++c) {
+        const float v = zhr_at(p, b, c, Y, X);
+        for (int k = 0; k < p.n_zhr; ++k) p.zhr[k][pix * p.zhr_cp[k] + c] = v;
+    }
+}
+
+inline unsigned nblocks(long long n) { return (unsigned)((n + NT - 1) / NT); }
+inline int launched() { return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH; }
+
+}  // namespace
+
+extern "C" int esr_cem_down(const float *gen, const float *lr, float *r, int32_t B, int32_t H, int32_t W, int32_t sf,
+                            int32_t ph, const float *w_down, int32_t kd, int32_t negate, esr_stream_t stream) {
+    if (!gen || !r || !w_down || B <= 0 || H <= 0 || W <= 0 || sf <= 0 || kd <= 0 || kd > MAXK || !(kd & 1) ||
+        ph < 0 || ph >= sf)
+        return ESR_EINVAL;
+    hipLaunchKernelGGL(cem_down_kernel, dim3(nblocks((long long)B * 3 * H * W)), dim3(NT), 0, (hipStream_t)stream,
+                       gen, lr, r, B, H, W, sf, ph, w_down, kd, negate);
+    return launched();
+}
+
+extern "C" int esr_cem_inv(const float *r, float *q, int32_t B, int32_t H, int32_t W, const float *w_inv, int32_t ki,
+                           esr_stream_t stream) {
+    if (!r || !q || !w_inv || B <= 0 || H <= 0 || W <= 0 || ki <= 0 || ki > MAXK || !(ki & 1)) return ESR_EINVAL;
+    hipLaunchKernelGGL(cem_inv_kernel, dim3(nblocks((long long)B * 3 * H * W)), dim3(NT), 0, (hipStream_t)stream, r,
+                       q, B, H, W, w_inv, ki);
+    return launched();
+}
+
+extern "C" int esr_cem_up_add(const float *q, const float *gen, float *out, int32_t B, int32_t H, int32_t W,
+                              int32_t sf, int32_t ph, const float *w_up, int32_t kd, int32_t M, esr_stream_t stream) {
+    if (!q || !gen || !out || !w_up || B <= 0 || H <= 0 || W <= 0 || sf <= 0 || kd <= 0 || kd > MAXK || !(kd & 1) ||
+        ph < 0 || ph >= sf || M < 0 || 2 * M >= sf * H || 2 * M >= sf * W)
+        return ESR_EINVAL;
+    const long long n = (long long)B * 3 * (sf * H - 2 * M) * (sf * W - 2 * M);
+    hipLaunchKernelGGL(cem_up_add_kernel, dim3(nblocks(n)), dim3(NT), 0, (hipStream_t)stream, q, gen, out, B, H, W, sf,
+                       ph, w_up, kd, M);
+    return launched();
+}
+
+extern "C" int esr_prep_input(const float *x, int32_t B, int32_t nz, int32_t h, int32_t w, int32_t sf, int32_t m,
+                              float *lr_nchw, float *first, int32_t first_cp, int32_t first_lr_off,
+                              float *const *zlr_dst, const int32_t *zlr_cp, int32_t n_zlr, float *const *zhr_dst,
+                              const int32_t *zhr_cp, int32_t n_zhr, esr_stream_t stream) {
+    if (!x || B <= 0 || h <= 0 || w <= 0 || sf <= 0 || m < 0 || nz < 0 || n_zlr < 0 || n_zlr > 4 || n_zhr < 0 ||
+        n_zhr > 4)
+        return ESR_EINVAL;
+    PrepParams p = {};
+    p.x = x; p.B = B; p.nz = nz; p.h = h; p.w = w; p.sf = sf; p.m = m;
+    p.lr_nchw = lr_nchw; p.first = first; p.first_cp = first_cp; p.first_lr_off = first_lr_off;
+    p.n_zlr = nz ? n_zlr : 0;
+    p.n_zhr = nz ? n_zhr : 0;
+    for (int i = 0; i < p.n_zlr; ++i) { p.zlr[i] = zlr_dst[i]; p.zlr_cp[i] = zlr_cp[i]; }
+    for (int i = 0; i < p.n_zhr; ++i) { p.zhr[i] = zhr_dst[i]; p.zhr_cp[i] = zhr_cp[i]; }
+    const int H = h + 2 * m, W = w + 2 * m;
+    hipLaunchKernelGGL(prep_lr_kernel, dim3(nblocks((long long)B * H * W)), dim3(NT), 0, (hipStream_t)stream, p);
+    int rc = launched();
+    if (rc || !p.n_zhr) return rc;
+    hipLaunchKernelGGL(prep_hr_kernel, dim3(nblocks((long long)B * sf * H * sf * W)), dim3(NT), 0,
+                       (hipStream_t)stream, p);
+    return launched();
+}

@@ -1,0 +1,82 @@
+"""ctypes binding of libesr_amd.so (C ABI declared in include/esr_amd.h).
+
+The library is built in-tree (`make -C explorable-super-resolution_old_amd/csrc` or `__graft_entry__.build()`).  There
+is no fallback: if the library cannot be loaded, or a caller hands it a non-ROCm tensor, we raise.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get('ESR_AMD_LIB', os.path.join(_HERE, 'libesr_amd.so'))
+ABI_VERSION = 1
+
+c_int = ctypes.c_int32
+c_float = ctypes.c_float
+c_void_p = ctypes.c_void_p
+c_fp = ctypes.POINTER(ctypes.c_float)
+
+
+class ConvOut(ctypes.Structure):
+    """Mirror of `esr_conv_out` (include/esr_amd.h)."""
+    _fields_ = [('out', c_void_p),
+                ('out_cp', c_int), ('out_coff', c_int), ('out_h', c_int), ('out_w', c_int),
+                ('out_sy', c_int), ('out_sx', c_int), ('out_oy', c_int), ('out_ox', c_int), ('out_planar', c_int),
+                ('lrelu', c_int),
+                ('r1', c_void_p), ('r1_cp', c_int), ('r1_coff', c_int), ('s1', c_float),
+                ('r2', c_void_p), ('r2_cp', c_int), ('r2_coff', c_int), ('s2', c_float),
+                ('out2', c_void_p), ('out2_cp', c_int), ('out2_coff', c_int)]
+
+
+# name -> argtypes (all return int32 status)
+_SIGNATURES = {
+    'esr_conv3x3_fwd': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
+                        ctypes.POINTER(ConvOut), c_void_p],
+    'esr_upconv2x_phase_fwd': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
+                               ctypes.POINTER(ConvOut), c_void_p],
+    'esr_prep_input': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int,
+                       ctypes.POINTER(c_void_p), ctypes.POINTER(c_int), c_int,
+                       ctypes.POINTER(c_void_p), ctypes.POINTER(c_int), c_int, c_void_p],
+    'esr_cem_down': [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int,
+                     c_void_p],
+    'esr_cem_inv': [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p],
+    'esr_cem_up_add': [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int,
+                       c_void_p],
+    'esr_abi_version': [],
+}
+EXPORTED = tuple(_SIGNATURES)
+
+_lib = None
+
+
+class ESRLibraryError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libesr_amd.so once and bind prototypes.  Raises ESRLibraryError if absent or ABI-incompatible."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ESRLibraryError('libesr_amd.so not found at %s: build it with `make -C explorable-super-resolution_old_amd'
+                              '/csrc` (or __graft_entry__.build()); there is no non-HIP fallback' % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, argtypes in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = c_int
+    v = lib.esr_abi_version()
+    if v != ABI_VERSION:
+        raise ESRLibraryError('libesr_amd.so ABI %d != expected %d (stale build?)' % (v, ABI_VERSION))
+    _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != 0:
+        raise RuntimeError('%s failed with esr_status %d' % (what, rc))
+
+
+def ptr(t):
+    """Device pointer of a tensor (None → NULL)."""
+    return None if t is None else ctypes.c_void_p(t.data_ptr())

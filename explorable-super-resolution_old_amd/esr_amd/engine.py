@@ -1,0 +1,301 @@
+"""HIP executor for the RRDB ×4 generator (+ CEM) forward.
+
+Replaces the PyTorch op graph of RRDBNet.forward (architecture.py:151-175) and CEM_PyTorch.forward (CEMnet.py:169-190)
+with a fixed sequence of libesr_amd launches over preallocated padded-NHWC workspaces.
+
+Memory plan (per (device, B, H, W, latent) — H×W is the LR grid the generator runs on, i.e. after CEM pre-pad):
+  ZC = 8 latent channels slot (3 used, 5 zero) in latent mode, 0 otherwise; XOFF = ZC.
+  first [B][H+2][W+2][16|8]   conv_first input: Z_LR at 0..2, LR at 8..10 (latent) | LR at 0..2 (plain)
+  fea   [B][H+2][W+2][64]     conv_first output, the ShortcutBlock skip (block.py:96)
+  P0..2 [B][H+2][W+2][ZC+192] RDB concat buffers: [Z | x(64) | x1 | x2 | x3 | x4 (32 each)].  conv_i of an RDB reads
+                              the channel prefix [0, ZC+64+32i) and writes its 32 growth channels right after it, so
+                              torch.cat (block.py:234,265,92) never happens.  RRDB k: P0 -RDB1-> P1.x -RDB2-> P2.x
+                              -RDB3-> P0.x (in place, pointwise residual), P0.x carrying the trunk.
+  U0    [B][H+2][W+2][64]     LR_conv + skip output
+  U1    [B][2H+2][2W+2][64]   upconv-1 output
+  HR0/1 [B][4H+2][4W+2][ZC+64] upconv-2 / HR_conv0 outputs with Z_HR in the slot
+  gen   [B][3][4H][4W]        HR_conv1 output (NCHW, consumed by the CEM stencils)
+Halos and unused channels are zero from allocation and never written.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+
+SF = 4
+CEM_PHASE = SF - SF // 2 - 1  # calc_strides(None, 4) pre_stride (imresize_CEM.py:83-85)
+_FOLD = (((1., 0., 0.), (0., 1., 1.)), ((1., 1., 0.), (0., 0., 1.)))  # nearest-×2 polyphase tap folding, phase 0/1
+
+
+# Optional per-launch profiling (bench.py): a list collecting (tag, algorithmic FLOPs, start event, end event).
+_PROFILE = None
+
+
+def _prof_begin(prof, tag, flops):
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    start.record()
+    prof.append((tag, flops, start, end))
+    return end
+
+
+def _require_device(t, what):
+    if not t.is_cuda:
+        raise RuntimeError('esr_amd: %s must be a ROCm device tensor (this build has no CPU path)' % what)
+    if t.dtype != torch.float32:
+        raise RuntimeError('esr_amd: %s must be float32 (got %s)' % (what, t.dtype))
+
+
+def pack_conv_weight(w, cmap, n_pad):
+    """[Cout][Cin_ref][k][k] -> packed [nchunk][k*k][n_pad][32] (include/esr_amd.h); cmap[c] = reference input channel
+    feeding buffer channel c, or -1 for a zero (padding) channel."""
+    cout, cin_ref, kh, kw = w.shape
+    T = kh * kw
+    nch = (len(cmap) + 31) // 32
+    src = w.detach().permute(1, 2, 3, 0).reshape(cin_ref, T, cout)
+    out = torch.zeros(nch * 32, T, n_pad, device=w.device, dtype=torch.float32)
+    cm = np.asarray(cmap)
+    dst_idx = np.nonzero(cm >= 0)[0]
+    out[torch.as_tensor(dst_idx, device=w.device), :, :cout] = src[torch.as_tensor(cm[dst_idx], device=w.device)]
+    return out.view(nch, 32, T, n_pad).permute(0, 2, 3, 1).contiguous()
+
+
+def fold_upconv_phase(w, py, px):
+    """Nearest-×2 upsample then 3×3 conv == per output phase (py,px) a 2×2 conv on the LR grid whose taps are sums of
+    the 3×3 taps landing on the same source pixel (block.py:294-301)."""
+    F = torch.tensor(_FOLD, dtype=w.dtype, device=w.device)
+    return torch.einsum('ay,bx,oiyx->oiab', F[py], F[px], w.detach())
+
+
+class _Packed:
+    """Packed weights of one generator, rebuilt when any parameter changes (data_ptr or in-place version)."""
+
+    def __init__(self, net, latent):
+        zc = 8 if latent else 0
+
+        def lr_map(n_feat):  # [Z(3) pad(5)] + features, reference order [Z, features]
+            if not latent:
+                return list(range(n_feat))
+            return [0, 1, 2] + [-1] * 5 + [3 + c for c in range(n_feat)]
+
+        m = net.model
+        first_w = m[0].weight
+        if latent:
+            first_map = [0, 1, 2] + [-1] * 5 + [3, 4, 5] + [-1] * 5
+        else:
+            first_map = [0, 1, 2] + [-1] * 5
+        self.first = (pack_conv_weight(first_w, first_map, 64), m[0].bias)
+        self.rdb = []
+        for k in range(net.nb):
+            rr = m[1].sub[k]
+            for rdb in (rr.RDB1, rr.RDB2, rr.RDB3):
+                convs = []
+                for i in range(5):
+                    c = rdb.convs[i][0]
+                    convs.append((pack_conv_weight(c.weight, lr_map(64 + 32 * i), 32 if i < 4 else 64), c.bias))
+                self.rdb.append(convs)
+        lrc = m[1].sub[net.nb]
+        self.lr_conv = (pack_conv_weight(lrc.weight, lr_map(64), 64), lrc.bias)
+        self.up = []
+        for j in (2, 3):
+            c = m[j][1]
+            ph = [pack_conv_weight(fold_upconv_phase(c.weight, py, px), list(range(64)), 64)
+                  for py in (0, 1) for px in (0, 1)]
+            self.up.append((ph, c.bias))
+        self.hr0 = (pack_conv_weight(m[4].weight, lr_map(64), 64), m[4].bias)
+        self.hr1 = (pack_conv_weight(m[6].weight, lr_map(64), 32), m[6].bias)
+        self.zc = zc
+
+
+def _param_key(net):
+    return tuple((p.data_ptr(), p._version) for p in net.parameters())
+
+
+def _packed(net, latent):
+    key = (_param_key(net), latent)
+    c = net._esr_cache.get('packed')
+    if c is None or c[0] != key:
+        with torch.no_grad():
+            c = (key, _Packed(net, latent))
+        net._esr_cache['packed'] = c
+    return c[1]
+
+
+class _Workspace:
+    def __init__(self, dev, B, H, W, latent):
+        zc = 8 if latent else 0
+        z = lambda *s: torch.zeros(*s, device=dev, dtype=torch.float32)  # noqa: E731
+        self.B, self.H, self.W, self.zc = B, H, W, zc
+        self.first_cp = 16 if latent else 8
+        self.first_lr_off = 8 if latent else 0
+        self.cp = zc + 192
+        self.hr_cp = zc + 64
+        self.first = z(B, H + 2, W + 2, self.first_cp)
+        self.fea = z(B, H + 2, W + 2, 64)
+        self.P = [z(B, H + 2, W + 2, self.cp) for _ in range(3)]
+        self.U0 = z(B, H + 2, W + 2, 64)
+        self.U1 = z(B, 2 * H + 2, 2 * W + 2, 64)
+        self.HR = [z(B, 4 * H + 2, 4 * W + 2, self.hr_cp) for _ in range(2)]
+        self.lr = z(B, 3, H, W)
+
+
+def _workspace(net, dev, B, H, W, latent):
+    key = (str(dev), B, H, W, latent)
+    c = net._esr_cache.get('ws')
+    if c is None or c[0] != key:
+        net._esr_cache.pop('ws', None)  # free the previous shape's buffers first
+        c = (key, _Workspace(dev, B, H, W, latent))
+        net._esr_cache['ws'] = c
+    return c[1]
+
+
+def _conv_out(out, cp, coff, oh, ow, lrelu, sy=1, sx=1, oy=0, ox=0, planar=0, r1=None, r1_cp=0, r1_coff=0, s1=1.0,
+              r2=None, r2_cp=0, r2_coff=0, s2=1.0, out2=None, out2_cp=0, out2_coff=0):
+    return _lib.ConvOut(out.data_ptr(), cp, coff, oh, ow, sy, sx, oy, ox, planar, int(lrelu),
+                        None if r1 is None else r1.data_ptr(), r1_cp, r1_coff, s1,
+                        None if r2 is None else r2.data_ptr(), r2_cp, r2_coff, s2,
+                        None if out2 is None else out2.data_ptr(), out2_cp, out2_coff)
+
+
+def generator_forward(net, x, cem=None):
+    """RRDBNet.forward, optionally wrapped by CEM_PyTorch.forward (cem = the CEM_PyTorch module)."""
+    lib = _lib.load()
+    _require_device(x, 'generator input')
+    if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in net.parameters())):
+        raise RuntimeError('esr_amd: the HIP generator is forward-only in this build; run under torch.no_grad() '
+                           '(or freeze parameters and the input)')
+    x = x.contiguous()
+    latent = net.latent_input is not None
+    nz = net.nl if latent else 0
+    Bn, C, h, w = x.shape
+    if C != 3 + nz * SF * SF:
+        raise RuntimeError('esr_amd: expected %d input channels (3 LR + %d rearranged HR latent), got %d'
+                           % (3 + nz * SF * SF, nz * SF * SF, C))
+    if latent and nz != 3:
+        raise NotImplementedError('esr_amd latent path is built for 3 latent channels')
+    pre_pad = cem is not None and cem.pre_pad
+    m = int(cem.margins_LR) if pre_pad else 0
+    H, W = h + 2 * m, w + 2 * m
+    dev = x.device
+    ws = _workspace(net, dev, Bn, H, W, latent)
+    pk = _packed(net, latent)
+    for p in (pk.first[1],):
+        _require_device(p, 'generator parameters')
+    stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    zc, cp, hcp = ws.zc, ws.cp, ws.hr_cp
+    P0, P1, P2 = ws.P
+    HR0, HR1 = ws.HR
+
+    zlr = (ctypes.c_void_p * 3)(*[t.data_ptr() for t in ws.P])
+    zlr_cp = (ctypes.c_int32 * 3)(cp, cp, cp)
+    zhr = (ctypes.c_void_p * 2)(HR0.data_ptr(), HR1.data_ptr())
+    zhr_cp = (ctypes.c_int32 * 2)(hcp, hcp)
+    _lib.check(lib.esr_prep_input(x.data_ptr(), Bn, nz, h, w, SF, m, ws.lr.data_ptr(), ws.first.data_ptr(),
+                                  ws.first_cp, ws.first_lr_off, zlr, zlr_cp, 3 if nz else 0, zhr, zhr_cp,
+                                  2 if nz else 0, stream), 'esr_prep_input')
+
+    prof = _PROFILE
+
+    def conv(inp, h_, w_, in_cp, cin, wb, cout, o, cin_ref=None):
+        if prof is not None:
+            ev = _prof_begin(prof, 'conv3x3_n%d' % (32 if cout <= 32 else 64),
+                             2.0 * Bn * h_ * w_ * 9 * (cin_ref if cin_ref is not None else cin) * cout)
+        _lib.check(lib.esr_conv3x3_fwd(inp.data_ptr(), Bn, h_, w_, in_cp, cin, wb[0].data_ptr(), wb[1].data_ptr(),
+                                       cout, ctypes.byref(o), stream), 'esr_conv3x3_fwd')
+        if prof is not None:
+            ev.record()
+
+    # conv_first -> P0.x and fea
+    nl = 3 if latent else 0  # reference latent channels concatenated into a conv input (FLOP accounting)
+    conv(ws.first, H, W, ws.first_cp, ws.first_cp, pk.first, 64,
+         _conv_out(P0, cp, zc, H, W, False, out2=ws.fea, out2_cp=64, out2_coff=0), cin_ref=3 + nl)
+    # 23 RRDBs
+    chain = ((P0, P1), (P1, P2), (P2, P0))
+    for k in range(net.nb):
+        for r, (pin, pout) in enumerate(chain):
+            convs = pk.rdb[3 * k + r]
+            for i in range(4):
+                coff = zc + 64 + 32 * i
+                conv(pin, H, W, cp, coff, convs[i], 32, _conv_out(pin, cp, coff, H, W, True), cin_ref=nl + 64 + 32 * i)
+            o = _conv_out(pout, cp, zc, H, W, False, r1=pin, r1_cp=cp, r1_coff=zc, s1=0.2,
+                          r2=P0 if r == 2 else None, r2_cp=cp, r2_coff=zc, s2=0.2)
+            conv(pin, H, W, cp, zc + 192, convs[4], 64, o, cin_ref=nl + 192)
+    # LR_conv + trunk skip
+    conv(P0, H, W, cp, zc + 64, pk.lr_conv, 64, _conv_out(ws.U0, 64, 0, H, W, False, r1=ws.fea, r1_cp=64, s1=1.0),
+         cin_ref=nl + 64)
+    # two nearest-×2 upconvs, four phases each
+    for (src, sh, sw, dst, dcp, dcoff), (phw, bias) in zip(
+            ((ws.U0, H, W, ws.U1, 64, 0), (ws.U1, 2 * H, 2 * W, HR0, hcp, zc)), pk.up):
+        for ph, wph in enumerate(phw):
+            py, px = ph // 2, ph % 2
+            o = _conv_out(dst, dcp, dcoff, 2 * sh, 2 * sw, True, sy=2, sx=2, oy=py, ox=px)
+            if prof is not None:  # reference FLOPs: a 3×3 conv at 2× resolution, a quarter of it per phase
+                ev = _prof_begin(prof, 'upconv2x_phase', 2.0 * Bn * (2 * sh) * (2 * sw) * 9 * 64 * 64 / 4)
+            _lib.check(lib.esr_upconv2x_phase_fwd(src.data_ptr(), Bn, sh, sw, 64, 64, wph.data_ptr(),
+                                                  bias.data_ptr(), 64, py, px, ctypes.byref(o), stream),
+                       'esr_upconv2x_phase_fwd')
+            if prof is not None:
+                ev.record()
+    HH, WW = SF * H, SF * W
+    conv(HR0, HH, WW, hcp, hcp, pk.hr0, 64, _conv_out(HR1, hcp, zc, HH, WW, True), cin_ref=nl + 64)
+    gen = torch.empty(Bn, 3, HH, WW, device=dev, dtype=torch.float32)
+    conv(HR1, HH, WW, hcp, hcp, pk.hr1, 3, _conv_out(gen, 0, 0, HH, WW, False, planar=1), cin_ref=nl + 64)
+    if cem is None:
+        return gen
+    return cem_apply(lib, cem, gen, ws.lr, Bn, H, W, SF * m if pre_pad else 0, stream)
+
+
+def cem_apply(lib, cem, gen, lr, Bn, H, W, M, stream):
+    """out = crop_M(gen + Up(Inv(lr - Down(gen))))  ==  CEMnet.py:186-190."""
+    dev = gen.device
+    wd = cem.DownscaleOP.Filter_OP.weight
+    wi = cem.Conv_LR_with_Inv_hTh_OP.Filter_OP.weight
+    wu = cem.Upscale_OP.Filter_OP.weight
+    for t, n in ((wd, 'DownscaleOP'), (wi, 'Conv_LR_with_Inv_hTh_OP'), (wu, 'Upscale_OP')):
+        _require_device(t, n + ' filter')
+    kd, ki = wd.shape[-1], wi.shape[-1]
+    r = torch.empty(Bn, 3, H, W, device=dev, dtype=torch.float32)
+    q = torch.empty_like(r)
+    out = torch.empty(Bn, 3, SF * H - 2 * M, SF * W - 2 * M, device=dev, dtype=torch.float32)
+    _lib.check(lib.esr_cem_down(gen.data_ptr(), lr.data_ptr(), r.data_ptr(), Bn, H, W, SF, CEM_PHASE,
+                                wd[0, 0].contiguous().data_ptr(), kd, 0, stream), 'esr_cem_down')
+    _lib.check(lib.esr_cem_inv(r.data_ptr(), q.data_ptr(), Bn, H, W, wi[0, 0].contiguous().data_ptr(), ki, stream),
+               'esr_cem_inv')
+    _lib.check(lib.esr_cem_up_add(q.data_ptr(), gen.data_ptr(), out.data_ptr(), Bn, H, W, SF, CEM_PHASE,
+                                  wu[0, 0].contiguous().data_ptr(), kd, M, stream), 'esr_cem_up_add')
+    return out
+
+
+def cem_filter_op(layer, x):
+    """A single CEM Filter_Layer applied on its own (CEMnet.py:139-140), e.g. `netG.module.DownscaleOP(HR)` from the
+    GUI (GUI.py:1289,1900).  kind 'down': replicate-pad, xcorr, keep the stride phase (NCHW [B,3,sf*h,sf*w] ->
+    [B,3,h,w]); 'inv': replicate-padded xcorr at LR; 'up': zero-stuff ×sf then xcorr ([B,3,h,w] -> [B,3,sf*h,sf*w])."""
+    lib = _lib.load()
+    _require_device(x, 'CEM filter input')
+    if x.dim() != 4 or x.shape[1] != 3:
+        raise RuntimeError('esr_amd: CEM filters take [B,3,H,W] input')
+    x = x.contiguous()
+    w = layer.Filter_OP.weight
+    _require_device(w, 'CEM filter weight')
+    k = w.shape[-1]
+    wk = w[0, 0].contiguous()
+    stream = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+    Bn, _, Hx, Wx = x.shape
+    if layer.kind == 'down':
+        if Hx % SF or Wx % SF:
+            raise RuntimeError('esr_amd: DownscaleOP input size must be divisible by %d' % SF)
+        out = torch.empty(Bn, 3, Hx // SF, Wx // SF, device=x.device, dtype=torch.float32)
+        _lib.check(lib.esr_cem_down(x.data_ptr(), None, out.data_ptr(), Bn, Hx // SF, Wx // SF, SF, CEM_PHASE,
+                                    wk.data_ptr(), k, 1, stream), 'esr_cem_down')
+    elif layer.kind == 'inv':
+        out = torch.empty_like(x)
+        _lib.check(lib.esr_cem_inv(x.data_ptr(), out.data_ptr(), Bn, Hx, Wx, wk.data_ptr(), k, stream), 'esr_cem_inv')
+    elif layer.kind == 'up':
+        zero = torch.zeros(Bn, 3, SF * Hx, SF * Wx, device=x.device, dtype=torch.float32)
+        out = torch.empty_like(zero)
+        _lib.check(lib.esr_cem_up_add(x.data_ptr(), zero.data_ptr(), out.data_ptr(), Bn, Hx, Wx, SF, CEM_PHASE,
+                                      wk.data_ptr(), k, 0, stream), 'esr_cem_up_add')
+    else:
+        raise ValueError(layer.kind)
+    return out

@@ -1,0 +1,62 @@
+"""Generator factory — counterpart of reference codes/models/networks.py (define_G, init_weights).
+
+`define_G(opt, CEM=None, num_latent_channels=None)` reads the same option keys (network_G.*, scale, gpu_ids,
+is_train, datasets.train.patch_size) and returns the same object shape: CEM_PyTorch(RRDBNet) when network_G.CEM_arch,
+initialised with kaiming×0.1 when training (networks.py:95-98), wrapped so that `.module` reaches it when gpu_ids is
+set (networks.py:99-101).  Multi-GPU in this build is one process per GPU (torch.distributed over RCCL), so the
+wrapper is a single-device nn.DataParallel on the process's current device, never a multi-device replicate/scatter.
+"""
+import functools
+
+import torch
+import torch.nn as nn
+from torch.nn import init
+
+from . import architecture as arch
+
+
+def weights_init_kaiming(m, scale=1):
+    """networks.py:28-44 (CEM filter layers are skipped)."""
+    if getattr(m, 'filter_layer', False):
+        return
+    classname = m.__class__.__name__
+    if classname.find('Conv') != -1 or classname.find('Linear') != -1:
+        init.kaiming_normal_(m.weight.data, a=0, mode='fan_in')
+        m.weight.data *= scale
+        if m.bias is not None:
+            m.bias.data.zero_()
+    elif classname.find('BatchNorm2d') != -1:
+        init.constant_(m.weight.data, 1.0)
+        init.constant_(m.bias.data, 0.0)
+
+
+def init_weights(net, init_type='kaiming', scale=1, std=0.02):
+    if init_type != 'kaiming':
+        raise NotImplementedError('only the kaiming initialisation used by define_G/define_D is provided')
+    net.apply(functools.partial(weights_init_kaiming, scale=scale))
+
+
+def define_G(opt, CEM=None, num_latent_channels=None):
+    gpu_ids = opt['gpu_ids']
+    opt_net = opt['network_G']
+    which_model = opt_net['which_model_G']
+    latent = opt_net.get('latent_input')
+    latent = latent if latent not in (None, 'None') else None
+    opt_net['latent_input'] = latent
+    if which_model != 'RRDB_net':
+        raise NotImplementedError('Generator model [{:s}] not recognized'.format(which_model))
+    netG = arch.RRDBNet(in_nc=opt_net['in_nc'], out_nc=opt_net['out_nc'], nf=opt_net['nf'], nb=opt_net['nb'],
+                        gc=opt_net['gc'], upscale=opt_net['scale'] if 'scale' in opt_net else opt['scale'],
+                        norm_type=opt_net.get('norm_type'), act_type='leakyrelu', mode=opt_net.get('mode', 'CNA'),
+                        upsample_mode='upconv',
+                        latent_input=(latent + '_' + opt_net['latent_input_domain']) if latent is not None else None,
+                        num_latent_channels=num_latent_channels)
+    if opt_net.get('CEM_arch'):
+        netG = CEM.WrapArchitecture_PyTorch(netG, opt['datasets']['train']['patch_size'] if opt['is_train'] else None)
+    if opt['is_train']:
+        init_weights(netG, init_type='kaiming', scale=0.1)
+    if gpu_ids:
+        assert torch.cuda.is_available()
+        dev = torch.cuda.current_device()
+        netG = nn.DataParallel(netG.to(dev), device_ids=[dev])
+    return netG

@@ -1,0 +1,117 @@
+/*
+ * esr_amd.h — C ABI of the MI355X-native RRDB-23 + CEM ×4 super-resolution hot path (libesr_amd.so).
+ *
+ * Every entry point is `extern "C"`, takes plain pointers / sizes, enqueues on the given HIP stream and returns 0 or a
+ * negative esr_status.  Buffers are caller-allocated device memory; the library holds no persistent allocations and
+ * is re-entrant across streams.
+ *
+ * Reference = YuvalBahat/Explorable-Super-Resolution_old, paths relative to codes/.  Each entry cites the reference
+ * interface it replaces.  The Python host layer (explorable-super-resolution_old_amd/esr_amd) binds these through
+ * ctypes behind the reference's RRDBNet / CEM_PyTorch / define_G API.
+ *
+ * Feature-map layout ("padded NHWC"): fp32 [B][H+2][W+2][cp], a one-pixel zero halo around the H×W interior, `cp`
+ * floats per pixel (channel pitch, multiple of 4).  Interior pixel (b, y, x), channel c lives at
+ *     ((b*(H+2) + y+1)*(W+2) + x+1)*cp + c.
+ * A convolution reads the channel PREFIX [0, cin) of its input pixels, which is how the dense concatenations of the
+ * residual dense block (block.py:233-235) are realised without copies: each conv writes its growth channels into a
+ * slice of the same buffer.
+ */
+#ifndef ESR_AMD_H
+#define ESR_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void *esr_stream_t; /* hipStream_t (0 = legacy default stream) */
+
+enum esr_status {
+    ESR_OK = 0,
+    ESR_EINVAL = -1,   /* bad shape / alignment / unsupported combination */
+    ESR_ELAUNCH = -2,  /* kernel launch failed (hipGetLastError after launch) */
+};
+
+/* Packed conv weights: [nchunk][taps][n_pad][32] fp32, nchunk = ceil(cin/32), n_pad = 32*ceil(cout/32); channel c of
+ * chunk j is input channel 32*j + c (zero where >= cin).  Bias: fp32 [cout]. */
+
+/* Output/epilogue descriptor of a convolution.
+ *   v = acc + bias[n]; if (lrelu) v = v > 0 ? v : 0.2*v        (conv_block CNA + act, block.py:10-23,141-146)
+ *   if (r1) v = s1*v + r1[pixel, r1_coff + n]                  (RDB / trunk residuals, block.py:96,235,270)
+ *   if (r2) v = s2*v + r2[pixel, r2_coff + n]
+ *   out[pixel, out_coff + n] = v   (and out2 likewise when out2 != NULL)
+ * Output pixel of input-grid position (y, x) is (out_sy*y + out_oy, out_sx*x + out_ox) in the out grid (out_h × out_w,
+ * padded NHWC), which is how the four polyphase phases of the nearest-×2 upconv scatter into the 2× grid.
+ * out_planar = 1 writes NCHW [B][cout][out_h][out_w] without halo instead (the generator output fed to CEM).
+ * r1/r2/out2 use the out grid geometry with their own channel pitch/offset. */
+typedef struct esr_conv_out {
+    float *out;
+    int32_t out_cp, out_coff, out_h, out_w, out_sy, out_sx, out_oy, out_ox, out_planar;
+    int32_t lrelu;
+    const float *r1;
+    int32_t r1_cp, r1_coff;
+    float s1;
+    const float *r2;
+    int32_t r2_cp, r2_coff;
+    float s2;
+    float *out2;
+    int32_t out2_cp, out2_coff;
+} esr_conv_out;
+
+/* 3×3 stride-1 zero-pad-1 convolution + bias + LeakyReLU/residual epilogue, fp32 (f32-input MFMA, exact fp32 FMA
+ * chain).  Replaces nn.Conv2d(k=3, padding=1) + act in conv_block (block.py:129-156), i.e. every generator conv of
+ * RRDBNet (architecture.py:122-141): conv_first, the 345 RDB convs (block.py:212-217), LR_conv, HR_conv0/1.
+ * in: padded NHWC [B][H+2][W+2][in_cp], reads channels [0, cin); cin % 8 == 0; cout <= 64. */
+int esr_conv3x3_fwd(const float *in, int32_t B, int32_t H, int32_t W, int32_t in_cp, int32_t cin,
+                    const float *w_packed, const float *bias, int32_t cout, const esr_conv_out *o, esr_stream_t stream);
+
+/* One polyphase phase (py, px) in {0,1}² of the nearest-×2 upsample + 3×3 conv (upconv_blcok, block.py:294-301;
+ * used twice by RRDBNet, networks.py:91): out[2y+py, 2x+px] = Σ_{a,b∈{0,1}} Wp[a][b] · in[y+py+a-1, x+px+b-1], with
+ * Wp the 3×3 taps summed per source pixel (folded on the host, see esr_amd/ops.py).  w_packed: [nchunk][4][n_pad][32].
+ * Set o->out_sy = o->out_sx = 2, o->out_oy = py, o->out_ox = px. */
+int esr_upconv2x_phase_fwd(const float *in, int32_t B, int32_t H, int32_t W, int32_t in_cp, int32_t cin,
+                           const float *w_packed, const float *bias, int32_t cout, int32_t py, int32_t px,
+                           const esr_conv_out *o, esr_stream_t stream);
+
+/* Model-input preparation (SRRaGANModel.ConcatLatent SRRaGAN_model.py:249-255, CEM_PyTorch pre-pad CEMnet.py:170-181,
+ * RRDBNet latent split + bilinear ↓sf architecture.py:153-160).
+ * x: NCHW fp32 [B][nz*sf*sf + 3][h][w] (nz = 0 plain, 3 latent; the HR latent travels as a raw view).
+ * Writes, for the padded LR grid H = h+2m, W = w+2m (m = pre-pad margin, 0 in train mode), replicate padding:
+ *   lr_nchw  [B][3][H][W]                   padded LR image (CEM input, CEMnet.py:184)
+ *   first    padded NHWC [B][H+2][W+2][first_cp]: Z_LR at channels 0..nz-1, LR at channels first_lr_off..+2
+ *   zlr_dst[i] padded NHWC LR-grid buffers with their own pitch zlr_cp[i]: Z_LR at channels 0..nz-1 (i < n_zlr)
+ *   zhr_dst[i] padded NHWC HR-grid buffers (sf*H × sf*W), pitch zhr_cp[i]: Z_HR (replicate pad sf*m) at 0..nz-1
+ * Z_LR = F.interpolate(Z_HR_padded, 1/sf, bilinear, align_corners=False). */
+int esr_prep_input(const float *x, int32_t B, int32_t nz, int32_t h, int32_t w, int32_t sf, int32_t m,
+                   float *lr_nchw, float *first, int32_t first_cp, int32_t first_lr_off,
+                   float *const *zlr_dst, const int32_t *zlr_cp, int32_t n_zlr,
+                   float *const *zhr_dst, const int32_t *zhr_cp, int32_t n_zhr, esr_stream_t stream);
+
+/* CEM step 1, fused DownscaleOP + LR residual (CEMnet.py:152,157-162,186-189):
+ *   r[b,c,i,j] = (lr ? lr[b,c,i,j] : 0) - Σ_{u,v<kd} w_down[u][v] · gen[b,c, clamp(sf*i+ph+u-kd/2), clamp(sf*j+ph+v-kd/2)]
+ * gen: NCHW [B][3][sf*H][sf*W]; lr, r: NCHW [B][3][H][W]; w_down = rot180(ds_kernel) (the Filter_OP weight),
+ * kd odd; ph = the stride phase (calc_strides pre_stride, imresize_CEM.py:83-85).  With lr == NULL this is
+ * -DownscaleOP(gen) (GUI.py:1289,1900 use DownscaleOP alone; pass negate=1 to get +DownscaleOP). */
+int esr_cem_down(const float *gen, const float *lr, float *r, int32_t B, int32_t H, int32_t W, int32_t sf, int32_t ph,
+                 const float *w_down, int32_t kd, int32_t negate, esr_stream_t stream);
+
+/* CEM step 2, Conv_LR_with_Inv_hTh_OP (CEMnet.py:149-151): q = xcorr(replicate_pad(r, ki/2), w_inv), NCHW LR grid,
+ * C = 3 channels, ki odd. */
+int esr_cem_inv(const float *r, float *q, int32_t B, int32_t H, int32_t W, const float *w_inv, int32_t ki,
+                esr_stream_t stream);
+
+/* CEM step 3, Upscale_OP + back-projection + HR unpad (CEMnet.py:153-159,186-190):
+ *   out[b,c,Y,X] = gen[b,c,Y+M,X+M] + Σ_{u,v<kd} w_up[u][v] · S[clamp(Y+M+u-kd/2), clamp(X+M+v-kd/2)]
+ * S = q zero-stuffed at phase ph on the sf× grid; M = HR crop margin (0 in train mode).
+ * out: NCHW [B][3][sf*H-2M][sf*W-2M]; w_up = sf²·ds_kernel. */
+int esr_cem_up_add(const float *q, const float *gen, float *out, int32_t B, int32_t H, int32_t W, int32_t sf,
+                   int32_t ph, const float *w_up, int32_t kd, int32_t M, esr_stream_t stream);
+
+/* Library / ABI version (bumped on any signature change). */
+int esr_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ESR_AMD_H */

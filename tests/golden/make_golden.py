@@ -1,0 +1,201 @@
+"""Generate the golden fixtures under tests/golden/ by importing the REFERENCE (read-only at /root/reference) in this
+container.  Run once here; only the small .npz outputs are committed.  The reference never travels to the GPU box.
+
+    python tests/golden/make_golden.py
+
+The reference does not import cleanly on this image; these in-memory shims make it importable without
+writing anything under /root/reference:
+  1. `cv2` is absent.  Only `cv2.resize(delta, INTER_CUBIC)` is used on the hot path (imresize_CEM.py:88-94,
+     Cubic_Kernel).  We restate OpenCV's published INTER_CUBIC (OpenCV 4.x imgproc/resize.cpp: A = -0.75, half-pixel
+     source coordinate fx = (x+0.5)*in/out - 0.5, 4 taps, BORDER_REFLECT_101).  For a delta image at scale 4 every
+     coefficient is a dyadic rational, so float32/float64 evaluation is exact.
+  2. `scipy.signal.gaussian` moved to `scipy.signal.windows.gaussian` in SciPy 1.15.
+  3. `torchvision` is absent; architecture.py only imports it at module top.
+  4. `torch.cuda.FloatTensor` is used to cast CEM filters (CEMnet.py:74,134); mapped to the CPU type.
+Bytecode: the reference directory carries __pycache__/*.pyc files; we never load them (pycache_prefix redirect) and
+never write any (dont_write_bytecode).
+"""
+import json
+import os
+import sys
+import types
+
+sys.dont_write_bytecode = True
+sys.pycache_prefix = '/tmp/esr_golden_pycache'
+
+import numpy as np
+import scipy.signal
+import scipy.signal.windows
+import torch
+import torch.nn as nn
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = '/root/reference/codes'
+sys.path.insert(0, REPO)
+from oracle.recipe import seeded_params, seeded_inputs, synthetic_learned_kernel  # noqa: E402
+
+
+def _cv2_resize_cubic(img, dsize, interpolation=None):
+    """OpenCV INTER_CUBIC restated (see module docstring). img: 2-D float array; dsize=(W, H)."""
+    A = -0.75
+    img = np.asarray(img, dtype=np.float64)
+
+    def coeffs(t):
+        w0 = ((A * (t + 1) - 5 * A) * (t + 1) + 8 * A) * (t + 1) - 4 * A
+        w1 = ((A + 2) * t - (A + 3)) * t * t + 1
+        w2 = ((A + 2) * (1 - t) - (A + 3)) * (1 - t) * (1 - t) + 1
+        return np.array([w0, w1, w2, 1.0 - w0 - w1 - w2])
+
+    def reflect101(i, n):
+        if n == 1:
+            return 0
+        while i < 0 or i >= n:
+            i = -i if i < 0 else 2 * n - 2 - i
+        return i
+
+    def resize_1d(src_len, dst_len):
+        m = np.zeros((dst_len, src_len))
+        scale = src_len / dst_len
+        for x in range(dst_len):
+            fx = (x + 0.5) * scale - 0.5
+            sx = int(np.floor(fx))
+            c = coeffs(fx - sx)
+            for k in range(4):
+                m[x, reflect101(sx - 1 + k, src_len)] += c[k]
+        return m
+
+    W, H = dsize
+    my = resize_1d(img.shape[0], H)
+    mx = resize_1d(img.shape[1], W)
+    return my @ img @ mx.T
+
+
+def install_shims():
+    cv2 = types.ModuleType('cv2')
+    cv2.INTER_CUBIC = 2
+    cv2.resize = _cv2_resize_cubic
+    sys.modules['cv2'] = cv2
+    scipy.signal.gaussian = scipy.signal.windows.gaussian
+    tv = types.ModuleType('torchvision')
+    sys.modules['torchvision'] = tv
+    torch.cuda.FloatTensor = torch.FloatTensor
+    torch.cuda.DoubleTensor = torch.DoubleTensor
+    sys.path.insert(0, REF)
+
+
+class FixedGen(nn.Module):
+    """Stand-in generator for CEM-only fixtures: returns a preset HR tensor (CEMnet.py:183 calls it once)."""
+
+    def __init__(self, out):
+        super().__init__()
+        self.out = out
+        self.num_latent_channels = 0
+        self.upscale = 4
+
+    def forward(self, x):
+        return self.out
+
+
+def cem_fixture(CEMnet, name, kernel):
+    conf = CEMnet.Get_CEM_Config(4)
+    cem = CEMnet.CEMnet(conf, upscale_kernel=kernel)
+    d = dict(ds_kernel=np.asarray(cem.ds_kernel), inv_hTh=np.asarray(cem.inv_hTh),
+             ds_half=np.int64(cem.ds_kernel_invalidity_half_size_LR), inv_half=np.int64(cem.inv_hTh_invalidity_half_size),
+             margins_LR=np.int64(cem.invalidity_margins_LR), margins_HR=np.int64(cem.invalidity_margins_HR))
+    if isinstance(kernel, np.ndarray):
+        d['input_kernel'] = kernel
+    mLR = int(cem.invalidity_margins_LR)
+    # CEM forward on fixed (gen, LR) pairs, train mode (no pre-pad) and eval mode (pre-pad), non-square on purpose.
+    B, h, w = 2, 20, 24
+    lr, _ = seeded_inputs(100, (B, 3, h, w))
+    rng = np.random.default_rng(101)
+    gen_train = rng.random((B, 3, 4 * h, 4 * w)).astype(np.float32)
+    gen_eval = rng.random((B, 3, 4 * (h + 2 * mLR), 4 * (w + 2 * mLR))).astype(np.float32)
+    for mode, gen in (('train', gen_train), ('eval', gen_eval)):
+        m = cem.WrapArchitecture_PyTorch(FixedGen(torch.from_numpy(gen)))
+        m.train(mode == 'train')
+        with torch.no_grad():
+            out = m(torch.from_numpy(lr)).numpy()
+        d['fwd_%s_lr' % mode] = lr
+        d['fwd_%s_gen' % mode] = gen
+        d['fwd_%s_out' % mode] = out
+    m = cem.WrapArchitecture_PyTorch(FixedGen(None))
+    d['w_inv'] = m.Conv_LR_with_Inv_hTh_OP.Filter_OP.weight.detach().numpy()
+    d['w_up'] = m.Upscale_OP.Filter_OP.weight.detach().numpy()
+    d['w_down'] = m.DownscaleOP.Filter_OP.weight.detach().numpy()
+    # DownscaleOP alone on an HR image (GUI.py:1289,1900 call it directly)
+    hr = rng.random((B, 3, 4 * h, 4 * w)).astype(np.float32)
+    with torch.no_grad():
+        d['down_hr'] = hr
+        d['down_out'] = m.DownscaleOP(torch.from_numpy(hr)).numpy()
+    np.savez_compressed(os.path.join(HERE, 'cem_%s.npz' % name), **d)
+    print('cem_%s: ds %s inv %s margins %d/%d' % (name, d['ds_kernel'].shape, d['inv_hTh'].shape, mLR,
+                                                  int(cem.invalidity_margins_HR)))
+    return cem
+
+
+def rrdb_fixture(arch, CEMnet, name, nb, latent, lr_shape, seed, w_scale, cem_mode=None, z_mode='pixel', kernel=None):
+    nl = 3 if latent else 0
+    net = arch.RRDBNet(in_nc=3, out_nc=3, nf=64, nb=nb, gc=32, upscale=4, norm_type=None, act_type='leakyrelu',
+                       mode='CNA', upsample_mode='upconv',
+                       latent_input='all_layers_HR_downscaled' if latent else None, num_latent_channels=nl)
+    model = net
+    cem = None
+    if cem_mode is not None:
+        cem = CEMnet.CEMnet(CEMnet.Get_CEM_Config(4), upscale_kernel=kernel)
+        model = cem.WrapArchitecture_PyTorch(net)
+    sd = model.state_dict()
+    named_shapes = [(k, tuple(v.shape)) for k, v in sd.items()]
+    params = seeded_params(named_shapes, seed, w_scale=w_scale)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=False)
+    B, _, h, w = lr_shape
+    lr, z = seeded_inputs(seed + 1, lr_shape, (B, 3, 4 * h, 4 * w) if latent else None, z_mode=z_mode)
+    x = torch.from_numpy(lr)
+    if latent:  # SRRaGANModel.ConcatLatent (SRRaGAN_model.py:249-255): raw view of HR Z into 48 LR-sized channels
+        zt = torch.from_numpy(z)
+        x = torch.cat([zt.contiguous().view(B, 3 * 16, h, w), x], 1)
+    if cem is not None:
+        model.train(cem_mode == 'train')
+    else:
+        model.eval()
+    with torch.no_grad():
+        out = model(x).numpy()
+    d = dict(lr=lr, out=out, nb=np.int64(nb), latent=np.int64(latent), seed=np.int64(seed), w_scale=np.float64(w_scale),
+             cem_mode=np.str_(cem_mode or 'none'), keys=np.str_(json.dumps(named_shapes)))
+    if z is not None:
+        d['z'] = z
+    if isinstance(kernel, np.ndarray):
+        d['kernel'] = kernel
+    np.savez_compressed(os.path.join(HERE, 'rrdb_%s.npz' % name), **d)
+    print('rrdb_%s: in %s out %s |out| %.4f params %d' % (name, tuple(x.shape), out.shape, np.abs(out).mean(),
+                                                          sum(int(np.prod(s)) for _, s in named_shapes)))
+
+
+def main():
+    install_shims()
+    import CEM.CEMnet as CEMnet
+    import models.modules.architecture as arch
+    torch.set_num_threads(8)
+    # --- CEM filter design + CEM forward, bicubic default then a learned (non-bicubic) kernel ---
+    cem_fixture(CEMnet, 'bicubic', None)
+    # --- RRDBNet plain / latent, bare and CEM-wrapped (bicubic kernel) ---
+    rrdb_fixture(arch, CEMnet, 'plain_nb2', 2, False, (2, 3, 12, 16), 1, 0.1)
+    rrdb_fixture(arch, CEMnet, 'plain_nb2_s1', 2, False, (2, 3, 12, 16), 2, 1.0)
+    rrdb_fixture(arch, CEMnet, 'latent_nb2', 2, True, (2, 3, 12, 16), 3, 0.1)
+    rrdb_fixture(arch, CEMnet, 'latent_nb2_s1', 2, True, (2, 3, 10, 14), 4, 1.0, z_mode='image')
+    rrdb_fixture(arch, CEMnet, 'plain_nb1_cem_eval', 1, False, (1, 3, 12, 12), 5, 0.5, cem_mode='eval')
+    rrdb_fixture(arch, CEMnet, 'plain_nb1_cem_train', 1, False, (2, 3, 12, 12), 6, 0.5, cem_mode='train')
+    rrdb_fixture(arch, CEMnet, 'latent_nb1_cem_eval', 1, True, (1, 3, 12, 12), 7, 0.5, cem_mode='eval')
+    rrdb_fixture(arch, CEMnet, 'latent_nb1_cem_train', 1, True, (2, 3, 12, 16), 8, 0.5, cem_mode='train')
+    rrdb_fixture(arch, CEMnet, 'plain_nb23', 23, False, (1, 3, 16, 16), 9, 0.1)
+    rrdb_fixture(arch, CEMnet, 'latent_nb23_cem_eval', 23, True, (1, 3, 16, 16), 10, 0.1, cem_mode='eval')
+    rrdb_fixture(arch, CEMnet, 'plain_nb23_s1_cem_eval', 23, False, (1, 3, 16, 16), 11, 1.0, cem_mode='eval')
+    # --- learned kernel last: imresize.kernels is process-global and sticky (imresize_CEM.py:9,23-42) ---
+    k = synthetic_learned_kernel()
+    cem_fixture(CEMnet, 'learned13', k)
+    rrdb_fixture(arch, CEMnet, 'latent_nb1_cem_eval_learned', 1, True, (1, 3, 12, 12), 12, 0.5, cem_mode='eval', kernel=k)
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,136 @@
+"""Host-side logic of the product package, CPU only: CEM filter design vs golden, module/state_dict layout vs the
+reference, weight packing / upconv folding algebra, C-ABI library exports, and loud failure without a GPU."""
+import ctypes
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import REPO, golden, golden_names
+
+import esr_amd
+from esr_amd import CEMnet as C
+from esr_amd import engine
+from esr_amd import _lib
+
+
+@pytest.mark.parametrize('name', ['cem_bicubic', 'cem_learned13'])
+def test_product_cem_design_exact(name):
+    d = golden(name)
+    cem = C.CEMnet(C.Get_CEM_Config(4), upscale_kernel=d['input_kernel'] if 'input_kernel' in d else None)
+    np.testing.assert_array_equal(cem.ds_kernel, d['ds_kernel'])
+    np.testing.assert_array_equal(cem.inv_hTh, d['inv_hTh'])
+    assert int(cem.invalidity_margins_LR) == int(d['margins_LR'])
+    assert int(cem.invalidity_margins_HR) == int(d['margins_HR'])
+    m = cem.WrapArchitecture_PyTorch(torch.nn.Identity())
+    np.testing.assert_array_equal(m.Conv_LR_with_Inv_hTh_OP.Filter_OP.weight.numpy(), d['w_inv'])
+    np.testing.assert_array_equal(m.Upscale_OP.Filter_OP.weight.numpy(), d['w_up'])
+    np.testing.assert_array_equal(m.DownscaleOP.Filter_OP.weight.numpy(), d['w_down'])
+    assert cem.OP_names == ['Conv_LR_with_Inv_hTh_OP.Filter_OP', 'Upscale_OP.Filter_OP', 'DownscaleOP.Filter_OP']
+
+
+def test_blurry_cubic_kernel_is_honoured():
+    """The reference's sticky kernel cache ignores 'blurry_cubic_1' after a default init; here the
+    kernel is an explicit argument, so it must change the design."""
+    a = C.CEMnet(C.Get_CEM_Config(4))
+    b = C.CEMnet(C.Get_CEM_Config(4), upscale_kernel='blurry_cubic_1')
+    assert b.ds_kernel.shape[0] > a.ds_kernel.shape[0]
+    assert abs(b.ds_kernel.sum() - 1) < 1e-6
+
+
+def _build(nb, latent, cem_mode):
+    net = esr_amd.RRDBNet(3, 3, 64, nb, latent_input='all_layers_HR_downscaled' if latent else None,
+                          num_latent_channels=3 if latent else 0)
+    if cem_mode == 'none':
+        return net
+    return C.CEMnet(C.Get_CEM_Config(4)).WrapArchitecture_PyTorch(net)
+
+
+@pytest.mark.parametrize('name', golden_names('rrdb_'))
+def test_state_dict_layout_matches_reference(name):
+    d = golden(name)
+    if 'kernel' in d:
+        pytest.skip('layout identical to the bicubic case; filter sizes covered by the design test')
+    ref = json.loads(str(d['keys']))
+    m = _build(int(d['nb']), bool(int(d['latent'])), str(d['cem_mode']))
+    ours = [(k, list(v.shape)) for k, v in m.state_dict().items()]
+    assert ours == [(k, list(s)) for k, s in ref]
+
+
+def test_define_G_from_shipped_config():
+    opt = {'gpu_ids': None, 'is_train': False, 'scale': 4,
+           'network_G': {'which_model_G': 'RRDB_net', 'CEM_arch': 1, 'latent_input': 'all_layers',
+                         'latent_input_domain': 'HR_downscaled', 'latent_channels': 3, 'norm_type': None,
+                         'mode': 'CNA', 'nf': 64, 'nb': 23, 'in_nc': 3, 'out_nc': 3, 'gc': 32, 'group': 1},
+           'datasets': {'train': {'patch_size': 256}}}
+    cem = C.CEMnet(C.Get_CEM_Config(4))
+    g = esr_amd.define_G(opt, CEM=cem, num_latent_channels=3)
+    assert isinstance(g, C.CEM_PyTorch)
+    assert sum(p.numel() for p in g.parameters()) == 17064869  # = reference latent RRDB-23 + CEM (fixture keys)
+    g.eval()
+    assert g.pre_pad
+    g.train()
+    assert not g.pre_pad
+
+
+def test_pack_conv_weight_layout():
+    torch.manual_seed(0)
+    w = torch.randn(32, 67, 3, 3)
+    cmap = [0, 1, 2] + [-1] * 5 + [3 + c for c in range(64)]
+    pk = engine.pack_conv_weight(w, cmap, 32)
+    assert pk.shape == (3, 9, 32, 32)
+    for c in range(len(cmap)):
+        j, cc = divmod(c, 32)
+        for t in (0, 4, 8):
+            if cmap[c] < 0:
+                assert torch.all(pk[j, t, :, cc] == 0)
+            else:
+                assert torch.equal(pk[j, t, :, cc], w[:, cmap[c], t // 3, t % 3])
+    assert torch.all(pk[2, :, :, 8:] == 0)  # channels >= 72 of the last chunk are padding
+
+
+def test_upconv_polyphase_fold_equals_nearest_then_conv():
+    """nearest-×2 then conv3×3 (block.py:294-301) == four 2×2 phase convs on the LR grid with folded taps."""
+    torch.manual_seed(1)
+    x = torch.randn(2, 5, 7, 6, dtype=torch.float64)
+    w = torch.randn(4, 5, 3, 3, dtype=torch.float64)
+    ref = F.conv2d(F.interpolate(x, scale_factor=2, mode='nearest'), w, padding=1)
+    out = torch.zeros_like(ref)
+    xp = F.pad(x, (1, 1, 1, 1))
+    for py in (0, 1):
+        for px in (0, 1):
+            wp = engine.fold_upconv_phase(w, py, px).to(torch.float64)
+            # phase tap (a,b) reads LR offset (py+a-1, px+b-1): crop the padded input accordingly
+            o = F.conv2d(xp[:, :, py:py + x.shape[2] + 1, px:px + x.shape[3] + 1], wp)
+            out[:, :, py::2, px::2] = o
+    assert torch.allclose(out, ref, atol=1e-12)
+
+
+def test_library_exports_every_header_symbol():
+    hdr = open(os.path.join(REPO, 'include', 'esr_amd.h')).read()
+    declared = sorted(set(re.findall(r'^int\s+(esr_\w+)\s*\(', hdr, flags=re.M)))
+    assert declared and set(declared) == set(_lib.EXPORTED)
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    for s in declared:
+        assert hasattr(lib, s), s
+    assert _lib.load().esr_abi_version() == _lib.ABI_VERSION
+
+
+def test_product_path_refuses_cpu_tensors():
+    net = _build(1, False, 'none')
+    with torch.no_grad(), pytest.raises(RuntimeError, match='ROCm device'):
+        net(torch.rand(1, 3, 8, 8))
+    cem = _build(1, False, 'cem')
+    with torch.no_grad(), pytest.raises(RuntimeError, match='ROCm device'):
+        cem.DownscaleOP(torch.rand(1, 3, 8, 8))
+
+
+def test_missing_library_fails_loudly(monkeypatch):
+    monkeypatch.setattr(_lib, '_lib', None)
+    monkeypatch.setattr(_lib, 'LIB_PATH', '/nonexistent/libesr_amd.so')
+    with pytest.raises(_lib.ESRLibraryError):
+        _lib.load()

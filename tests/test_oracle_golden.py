@@ -1,0 +1,64 @@
+"""Pin the CPU oracle (oracle/esr_oracle.py) against the golden vectors produced by the reference itself
+(tests/golden/make_golden.py).  CPU only."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import fixture_input, fixture_params, golden, golden_names, normwise_rel
+from oracle import esr_oracle as O
+
+
+@pytest.mark.parametrize('name', ['cem_bicubic', 'cem_learned13'])
+def test_cem_design_exact(name):
+    d = golden(name)
+    g = O.cem_design(4, d['input_kernel'] if 'input_kernel' in d else None)
+    for k in ('ds_kernel', 'inv_hTh'):
+        assert g[k].shape == d[k].shape
+        np.testing.assert_array_equal(np.asarray(g[k]), d[k])
+    for k in ('ds_half', 'inv_half', 'margins_LR', 'margins_HR'):
+        assert int(g[k]) == int(d[k]), k
+
+
+def test_cubic_kernel_taps():
+    """The 16 OpenCV INTER_CUBIC ×4 taps: [-21,-135,-225,-147,235,873,1535,1981,...]/8192."""
+    t = np.outer(*(2 * [np.array([-21, -135, -225, -147, 235, 873, 1535, 1981, 1981, 1535, 873, 235, -147, -225,
+                                   -135, -21]) / 8192.0])) * 16
+    np.testing.assert_allclose(O.cubic_upscale_kernel(4), t, rtol=0, atol=1e-15)
+
+
+@pytest.mark.parametrize('name', ['cem_bicubic', 'cem_learned13'])
+@pytest.mark.parametrize('mode', ['train', 'eval'])
+def test_cem_forward(name, mode):
+    d = golden(name)
+    design = O.cem_design(4, d['input_kernel'] if 'input_kernel' in d else None)
+    gen = torch.from_numpy(d['fwd_%s_gen' % mode])
+    lr = torch.from_numpy(d['fwd_%s_lr' % mode])
+    out = O.cem_forward(gen, lr, design, pre_pad=mode == 'eval')
+    assert normwise_rel(out.numpy(), d['fwd_%s_out' % mode]) < 1e-6
+
+
+@pytest.mark.parametrize('name', ['cem_bicubic', 'cem_learned13'])
+def test_downscale_op(name):
+    d = golden(name)
+    design = O.cem_design(4, d['input_kernel'] if 'input_kernel' in d else None)
+    out = O.cem_downscale(torch.from_numpy(d['down_hr']), design['ds_kernel'])
+    assert normwise_rel(out.numpy(), d['down_out']) < 1e-6
+
+
+@pytest.mark.parametrize('name', golden_names('rrdb_'))
+def test_rrdbnet_forward(name):
+    d = golden(name)
+    _, params = fixture_params(d)
+    P = O.strip_prefix(params)
+    mode = str(d['cem_mode'])
+    design = None if mode == 'none' else O.cem_design(4, d['kernel'] if 'kernel' in d else None)
+    with torch.no_grad():
+        out = O.sr_forward(fixture_input(d), P, int(d['nb']), bool(int(d['latent'])), design, pre_pad=mode == 'eval')
+    assert out.shape == d['out'].shape
+    assert normwise_rel(out.numpy(), d['out']) < 1e-5
+
+
+def test_bilinear_down4_matches_interpolate():
+    z = torch.rand(2, 3, 32, 24) * 2 - 1
+    ref = torch.nn.functional.interpolate(z, scale_factor=0.25, mode='bilinear', align_corners=False)
+    assert torch.allclose(O.bilinear_down4(z), ref, rtol=0, atol=1e-6)
