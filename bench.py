@@ -101,6 +101,21 @@ def cpu_baseline(args, model, x_gpu, out_gpu):
              'images_compared': n})
 
 
+def pmc_traffic(kernel_tag):
+    """HBM bytes per launch of `kernel_tag` from the committed rocprofv3 PMC passes (profiles/pmc_latest.json, made
+    by tools/prof_summary.py from separate --pmc FETCH_SIZE / WRITE_SIZE runs of this same default bench command,
+    FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM).  PMC counters cannot be read live from inside the process."""
+    path = os.path.join(REPO, 'profiles', 'pmc_latest.json')
+    if not os.path.exists(path):
+        return None
+    d = json.load(open(path))
+    for r in d['kernels']:
+        if r['kernel'] == kernel_tag and r['hbm_read_bytes_per_launch'] is not None:
+            return (r['hbm_read_bytes_per_launch'] + (r['hbm_write_bytes_per_launch'] or 0.0),
+                    '%s (%s)' % (os.path.relpath(path, REPO), d['source']))
+    return None
+
+
 def main():
     args = parse()
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -168,6 +183,10 @@ def main():
         'kernels': kernels,
         'gpu_busy_frac': round(tot / (dt * 1e3), 3),
     }
+    traffic = pmc_traffic(dom)
+    if traffic is not None:
+        rec['roofline']['traffic'] = traffic[0]
+        rec['roofline']['traffic_source'] = traffic[1]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb, parity = cpu_baseline(args, model, x, out)
         rec['cpu_baseline'] = cb
