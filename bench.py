@@ -28,6 +28,12 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = json.load(open(os.path.join(REPO, 'BASELINE.json')))['metric']
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix = vector peak (f32-input MFMA)
+F16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 MFMA ~2.5 PF dense (spec)
+PEAKS = {  # fp32-equivalent peak of each precision mode, in reference (fp32) FLOPs
+    'f32': (FP32_PEAK_TFLOPS, 'f32-input MFMA = f32 vector peak'),
+    'x3': (F16_DENSE_PEAK_TFLOPS / 3, '2.5 PFLOP/s dense f16 MFMA / 3 f16 products per fp32 product'),
+}
+DTYPES = {'f32': 'f32', 'x3': 'f32 (x3: f16 hi/lo split operands, 3 f16 MFMA products, fp32 accumulate)'}
 HBM_PEAK_GBS = 8000.0
 
 
@@ -42,6 +48,7 @@ def parse():
     ap.add_argument('--variant', choices=['plain', 'latent'], default='plain')
     ap.add_argument('--no-cem', action='store_true', help='bare RRDBNet (no CEM, no pre-pad)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--precision', choices=['x3', 'f32'], default='x3')
     ap.add_argument('--cpu-images', type=int, default=8, help='images in the bounded CPU-baseline sample')
     return ap.parse_args()
 
@@ -60,6 +67,8 @@ def build_model(args, dev):
             if n.endswith('bias'):
                 p.uniform_(-0.01, 0.01)
     model.eval()
+    from esr_amd import engine
+    engine.set_precision(model, args.precision)
     return model.to(dev)
 
 
@@ -162,6 +171,7 @@ def main():
     dom = max(per, key=lambda k: per[k][2])
     n_l, fl, ms = per[dom]
     achieved = (fl / n_l) / (ms / n_l / 1e3) / 1e12
+    peak, peak_note = PEAKS[args.precision]
     kernels = {k: {'launches_per_step': v[0] // args.steps, 'avg_us': round(v[2] / v[0] * 1e3, 2),
                    'tflops': round(v[1] / (v[2] / 1e3) / 1e12, 2), 'share_of_gpu_time': None}
                for k, v in per.items()}
@@ -171,14 +181,14 @@ def main():
     rec = {
         'metric': METRIC, 'value': round(value, 3), 'unit': 'HR Mpixels/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': round(dt / args.steps * 1e3, 3), 'higher_is_better': True,
-        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': DTYPES[args.precision], 'data': 'synthetic',
         'config': {'workload': 'RRDB-23 x4 %s%s, batch %d x %dx%d LR -> %dx%d HR per GPU (BASELINE config 2 shape)'
                                % (args.variant, '' if args.no_cem else ' + CEM (eval, LR pre-pad 10)', args.batch,
                                   args.lr_size, args.lr_size, hr, hr),
                    'global_batch': world * args.batch, 'nb': args.nb, 'parallelism': 'dp%d (image sharding, no '
                    'data-path collective)' % world},
-        'roofline': {'bound': 'mfma', 'kernel': dom, 'achieved': round(achieved, 2), 'peak': FP32_PEAK_TFLOPS,
-                     'unit': 'TFLOP/s', 'frac': round(achieved / FP32_PEAK_TFLOPS, 4), 'traffic': None,
+        'roofline': {'bound': 'mfma', 'kernel': dom, 'achieved': round(achieved, 2), 'peak': round(peak, 1),
+                     'peak_basis': peak_note, 'unit': 'TFLOP/s', 'frac': round(achieved / peak, 4), 'traffic': None,
                      'flops_per_launch': fl / n_l, 'avg_launch_us': round(ms / n_l * 1e3, 2)},
         'kernels': kernels,
         'gpu_busy_frac': round(tot / (dt * 1e3), 3),

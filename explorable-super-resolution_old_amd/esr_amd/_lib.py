@@ -8,7 +8,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('ESR_AMD_LIB', os.path.join(_HERE, 'libesr_amd.so'))
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 c_int = ctypes.c_int32
 c_float = ctypes.c_float
@@ -35,7 +35,11 @@ _SIGNATURES = {
                                ctypes.POINTER(ConvOut), c_void_p],
     'esr_prep_input': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int,
                        ctypes.POINTER(c_void_p), ctypes.POINTER(c_int), c_int,
-                       ctypes.POINTER(c_void_p), ctypes.POINTER(c_int), c_int, c_void_p],
+                       ctypes.POINTER(c_void_p), ctypes.POINTER(c_int), c_int, c_int, c_void_p],
+    'esr_conv3x3_fwd_x3': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_int,
+                           ctypes.POINTER(ConvOut), c_void_p, c_void_p],
+    'esr_upconv2x_phase_fwd_x3': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_int,
+                                  c_int, c_int, ctypes.POINTER(ConvOut), c_void_p, c_void_p],
     'esr_cem_down': [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int,
                      c_void_p],
     'esr_cem_inv': [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p],

@@ -3,6 +3,12 @@
 Replaces the PyTorch op graph of RRDBNet.forward (architecture.py:151-175) and CEM_PyTorch.forward (CEMnet.py:169-190)
 with a fixed sequence of libesr_amd launches over preallocated padded-NHWC workspaces.
 
+Precision modes (per call: `net.esr_precision`, default env ESR_PRECISION or 'x3'):
+  'x3'  activations carried as f16 hi/lo pairs, products on f16 MFMA with fp32 accumulation (esr_conv_x3.hip);
+        ~1e-6 relative error, 5.3× the MFMA rate of exact fp32.  If any activation leaves the f16 range the call is
+        transparently recomputed in 'f32' (the overflow flag is checked once per forward).
+  'f32' exact fp32 MFMA (esr_conv.hip).
+
 Memory plan (per (device, B, H, W, latent) — H×W is the LR grid the generator runs on, i.e. after CEM pre-pad):
   ZC = 8 latent channels slot (3 used, 5 zero) in latent mode, 0 otherwise; XOFF = ZC.
   first [B][H+2][W+2][16|8]   conv_first input: Z_LR at 0..2, LR at 8..10 (latent) | LR at 0..2 (plain)
@@ -14,10 +20,13 @@ Memory plan (per (device, B, H, W, latent) — H×W is the LR grid the generator
   U0    [B][H+2][W+2][64]     LR_conv + skip output
   U1    [B][2H+2][2W+2][64]   upconv-1 output
   HR0/1 [B][4H+2][4W+2][ZC+64] upconv-2 / HR_conv0 outputs with Z_HR in the slot
-  gen   [B][3][4H][4W]        HR_conv1 output (NCHW, consumed by the CEM stencils)
-Halos and unused channels are zero from allocation and never written.
+  gen   [B][3][4H][4W]        HR_conv1 output (fp32 NCHW, consumed by the CEM stencils)
+Every buffer holds 4 bytes per channel in either mode (fp32, or an f16 hi/lo pair).  Halos and unused channels are
+zero from allocation and never written.
 """
 import ctypes
+import math
+import os
 
 import numpy as np
 import torch
@@ -27,10 +36,13 @@ from . import _lib
 SF = 4
 CEM_PHASE = SF - SF // 2 - 1  # calc_strides(None, 4) pre_stride (imresize_CEM.py:83-85)
 _FOLD = (((1., 0., 0.), (0., 1., 1.)), ((1., 1., 0.), (0., 0., 1.)))  # nearest-×2 polyphase tap folding, phase 0/1
-
+DEFAULT_PRECISION = os.environ.get('ESR_PRECISION', 'x3')
+PRECISIONS = ('x3', 'f32')
 
 # Optional per-launch profiling (bench.py): a list collecting (tag, algorithmic FLOPs, start event, end event).
 _PROFILE = None
+# Number of forwards recomputed in f32 after an f16-range overflow (observability; tests read it).
+OVERFLOW_RERUNS = 0
 
 
 def _prof_begin(prof, tag, flops):
@@ -47,6 +59,9 @@ def _require_device(t, what):
         raise RuntimeError('esr_amd: %s must be float32 (got %s)' % (what, t.dtype))
 
 
+# ----------------------------------------------------------------------------------------------------------------------
+# weight packing
+# ----------------------------------------------------------------------------------------------------------------------
 def pack_conv_weight(w, cmap, n_pad):
     """[Cout][Cin_ref][k][k] -> packed [nchunk][k*k][n_pad][32] (include/esr_amd.h); cmap[c] = reference input channel
     feeding buffer channel c, or -1 for a zero (padding) channel."""
@@ -54,11 +69,45 @@ def pack_conv_weight(w, cmap, n_pad):
     T = kh * kw
     nch = (len(cmap) + 31) // 32
     src = w.detach().permute(1, 2, 3, 0).reshape(cin_ref, T, cout)
-    out = torch.zeros(nch * 32, T, n_pad, device=w.device, dtype=torch.float32)
+    out = torch.zeros(nch * 32, T, n_pad, device=w.device, dtype=w.dtype)
     cm = np.asarray(cmap)
     dst_idx = np.nonzero(cm >= 0)[0]
     out[torch.as_tensor(dst_idx, device=w.device), :, :cout] = src[torch.as_tensor(cm[dst_idx], device=w.device)]
     return out.view(nch, 32, T, n_pad).permute(0, 2, 3, 1).contiguous()
+
+
+def split_f16(x):
+    """fp32 -> (hi, lo) f16 with hi = f16(x), lo = f16(x - hi)."""
+    hi = x.half()
+    return hi, (x - hi.float()).half()
+
+
+def pack_x3(packed):
+    """fp32 packed weights [nch][T][n_pad][32] -> split layout [nch][T][n_pad][4 groups][hi 8 | lo 8] (f16), scaled by
+    a power of two so that max|w|·scale lies in [2^14, 2^15) (lo parts stay out of the f16 subnormal range)."""
+    amax = float(packed.abs().max())
+    e = 0 if amax == 0.0 else 14 - math.floor(math.log2(amax))
+    scale = 2.0 ** e
+    hi, lo = split_f16(packed * scale)
+    sh = packed.shape[:3] + (4, 1, 8)
+    out = torch.cat([hi.reshape(sh), lo.reshape(sh)], dim=4).contiguous()
+    return out, scale
+
+
+def to_split(x_nhwc):
+    """fp32 [..., C] (C % 8 == 0) -> split-f16 layout with the same byte size, returned as float32 storage."""
+    hi, lo = split_f16(x_nhwc)
+    sh = x_nhwc.shape[:-1] + (x_nhwc.shape[-1] // 8, 1, 8)
+    return torch.cat([hi.reshape(sh), lo.reshape(sh)], dim=-2).reshape(x_nhwc.shape[:-1] + (x_nhwc.shape[-1] * 2,)) \
+        .view(torch.float32)
+
+
+def from_split(buf):
+    """Inverse of to_split: float32-storage [..., C] in split layout -> fp32 values."""
+    h = buf.contiguous().view(torch.float16)
+    sh = buf.shape[:-1] + (buf.shape[-1] // 8, 2, 8)
+    h = h.reshape(sh).float()
+    return (h[..., 0, :] + h[..., 1, :]).reshape(buf.shape)
 
 
 def fold_upconv_phase(w, py, px):
@@ -68,44 +117,47 @@ def fold_upconv_phase(w, py, px):
     return torch.einsum('ay,bx,oiyx->oiab', F[py], F[px], w.detach())
 
 
+class _ConvW:
+    """One conv's packed weights in both precisions (x3 built lazily) + its bias parameter."""
+    __slots__ = ('f32', 'bias', '_x3')
+
+    def __init__(self, f32, bias):
+        self.f32, self.bias, self._x3 = f32, bias, None
+
+    def x3(self):
+        if self._x3 is None:
+            self._x3 = pack_x3(self.f32)
+        return self._x3
+
+
 class _Packed:
     """Packed weights of one generator, rebuilt when any parameter changes (data_ptr or in-place version)."""
 
     def __init__(self, net, latent):
-        zc = 8 if latent else 0
-
         def lr_map(n_feat):  # [Z(3) pad(5)] + features, reference order [Z, features]
             if not latent:
                 return list(range(n_feat))
             return [0, 1, 2] + [-1] * 5 + [3 + c for c in range(n_feat)]
 
         m = net.model
-        first_w = m[0].weight
-        if latent:
-            first_map = [0, 1, 2] + [-1] * 5 + [3, 4, 5] + [-1] * 5
-        else:
-            first_map = [0, 1, 2] + [-1] * 5
-        self.first = (pack_conv_weight(first_w, first_map, 64), m[0].bias)
+        first_map = ([0, 1, 2] + [-1] * 5 + [3, 4, 5] + [-1] * 5) if latent else ([0, 1, 2] + [-1] * 5)
+        self.first = _ConvW(pack_conv_weight(m[0].weight, first_map, 64), m[0].bias)
         self.rdb = []
         for k in range(net.nb):
             rr = m[1].sub[k]
             for rdb in (rr.RDB1, rr.RDB2, rr.RDB3):
-                convs = []
-                for i in range(5):
-                    c = rdb.convs[i][0]
-                    convs.append((pack_conv_weight(c.weight, lr_map(64 + 32 * i), 32 if i < 4 else 64), c.bias))
-                self.rdb.append(convs)
+                self.rdb.append([_ConvW(pack_conv_weight(rdb.convs[i][0].weight, lr_map(64 + 32 * i),
+                                                         32 if i < 4 else 64), rdb.convs[i][0].bias)
+                                 for i in range(5)])
         lrc = m[1].sub[net.nb]
-        self.lr_conv = (pack_conv_weight(lrc.weight, lr_map(64), 64), lrc.bias)
+        self.lr_conv = _ConvW(pack_conv_weight(lrc.weight, lr_map(64), 64), lrc.bias)
         self.up = []
         for j in (2, 3):
             c = m[j][1]
-            ph = [pack_conv_weight(fold_upconv_phase(c.weight, py, px), list(range(64)), 64)
-                  for py in (0, 1) for px in (0, 1)]
-            self.up.append((ph, c.bias))
-        self.hr0 = (pack_conv_weight(m[4].weight, lr_map(64), 64), m[4].bias)
-        self.hr1 = (pack_conv_weight(m[6].weight, lr_map(64), 32), m[6].bias)
-        self.zc = zc
+            self.up.append([_ConvW(pack_conv_weight(fold_upconv_phase(c.weight, py, px), list(range(64)), 64), c.bias)
+                            for py in (0, 1) for px in (0, 1)])
+        self.hr0 = _ConvW(pack_conv_weight(m[4].weight, lr_map(64), 64), m[4].bias)
+        self.hr1 = _ConvW(pack_conv_weight(m[6].weight, lr_map(64), 32), m[6].bias)
 
 
 def _param_key(net):
@@ -138,10 +190,12 @@ class _Workspace:
         self.U1 = z(B, 2 * H + 2, 2 * W + 2, 64)
         self.HR = [z(B, 4 * H + 2, 4 * W + 2, self.hr_cp) for _ in range(2)]
         self.lr = z(B, 3, H, W)
+        self.overflow = torch.zeros(1, device=dev, dtype=torch.int32)
 
 
-def _workspace(net, dev, B, H, W, latent):
-    key = (str(dev), B, H, W, latent)
+def _workspace(net, dev, B, H, W, latent, precision):
+    # keyed by precision too: the zero padding channels of an fp32 workspace are not zero when read as split-f16 pairs
+    key = (str(dev), B, H, W, latent, precision)
     c = net._esr_cache.get('ws')
     if c is None or c[0] != key:
         net._esr_cache.pop('ws', None)  # free the previous shape's buffers first
@@ -158,14 +212,31 @@ def _conv_out(out, cp, coff, oh, ow, lrelu, sy=1, sx=1, oy=0, ox=0, planar=0, r1
                         None if out2 is None else out2.data_ptr(), out2_cp, out2_coff)
 
 
+# ----------------------------------------------------------------------------------------------------------------------
+# forward
+# ----------------------------------------------------------------------------------------------------------------------
 def generator_forward(net, x, cem=None):
     """RRDBNet.forward, optionally wrapped by CEM_PyTorch.forward (cem = the CEM_PyTorch module)."""
-    lib = _lib.load()
+    global OVERFLOW_RERUNS
     _require_device(x, 'generator input')
     if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in net.parameters())):
         raise RuntimeError('esr_amd: the HIP generator is forward-only in this build; run under torch.no_grad() '
                            '(or freeze parameters and the input)')
-    x = x.contiguous()
+    precision = getattr(net, 'esr_precision', None) or DEFAULT_PRECISION
+    if precision not in PRECISIONS:
+        raise ValueError('esr_precision must be one of %s' % (PRECISIONS,))
+    out, ws = _forward(net, x.contiguous(), cem, precision)
+    if precision == 'x3':
+        if int(ws.overflow.item()):  # one 4-byte D2H per forward
+            OVERFLOW_RERUNS += 1
+            ws.overflow.zero_()
+            out, _ = _forward(net, x.contiguous(), cem, 'f32')
+    return out
+
+
+def _forward(net, x, cem, precision):
+    lib = _lib.load()
+    x3 = precision == 'x3'
     latent = net.latent_input is not None
     nz = net.nl if latent else 0
     Bn, C, h, w = x.shape
@@ -178,14 +249,14 @@ def generator_forward(net, x, cem=None):
     m = int(cem.margins_LR) if pre_pad else 0
     H, W = h + 2 * m, w + 2 * m
     dev = x.device
-    ws = _workspace(net, dev, Bn, H, W, latent)
+    ws = _workspace(net, dev, Bn, H, W, latent, precision)
     pk = _packed(net, latent)
-    for p in (pk.first[1],):
-        _require_device(p, 'generator parameters')
+    _require_device(pk.first.bias, 'generator parameters')
     stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     zc, cp, hcp = ws.zc, ws.cp, ws.hr_cp
     P0, P1, P2 = ws.P
     HR0, HR1 = ws.HR
+    ovf = ws.overflow.data_ptr()
 
     zlr = (ctypes.c_void_p * 3)(*[t.data_ptr() for t in ws.P])
     zlr_cp = (ctypes.c_int32 * 3)(cp, cp, cp)
@@ -193,57 +264,67 @@ def generator_forward(net, x, cem=None):
     zhr_cp = (ctypes.c_int32 * 2)(hcp, hcp)
     _lib.check(lib.esr_prep_input(x.data_ptr(), Bn, nz, h, w, SF, m, ws.lr.data_ptr(), ws.first.data_ptr(),
                                   ws.first_cp, ws.first_lr_off, zlr, zlr_cp, 3 if nz else 0, zhr, zhr_cp,
-                                  2 if nz else 0, stream), 'esr_prep_input')
-
+                                  2 if nz else 0, int(x3), stream), 'esr_prep_input')
     prof = _PROFILE
+    tagp = 'x3_' if x3 else ''
 
-    def conv(inp, h_, w_, in_cp, cin, wb, cout, o, cin_ref=None):
+    def conv(inp, h_, w_, in_cp, cin, cw, cout, o, cin_ref):
         if prof is not None:
-            ev = _prof_begin(prof, 'conv3x3_n%d' % (32 if cout <= 32 else 64),
-                             2.0 * Bn * h_ * w_ * 9 * (cin_ref if cin_ref is not None else cin) * cout)
-        _lib.check(lib.esr_conv3x3_fwd(inp.data_ptr(), Bn, h_, w_, in_cp, cin, wb[0].data_ptr(), wb[1].data_ptr(),
-                                       cout, ctypes.byref(o), stream), 'esr_conv3x3_fwd')
+            ev = _prof_begin(prof, '%sconv3x3_n%d' % (tagp, 32 if cout <= 32 else 64), 2.0 * Bn * h_ * w_ * 9 * cin_ref * cout)
+        if x3:
+            wx, scale = cw.x3()
+            rc = lib.esr_conv3x3_fwd_x3(inp.data_ptr(), Bn, h_, w_, in_cp, cin, wx.data_ptr(), cw.bias.data_ptr(),
+                                        scale, cout, ctypes.byref(o), ovf, stream)
+        else:
+            rc = lib.esr_conv3x3_fwd(inp.data_ptr(), Bn, h_, w_, in_cp, cin, cw.f32.data_ptr(), cw.bias.data_ptr(),
+                                     cout, ctypes.byref(o), stream)
+        _lib.check(rc, 'esr_conv3x3_fwd' + ('_x3' if x3 else ''))
         if prof is not None:
             ev.record()
 
-    # conv_first -> P0.x and fea
     nl = 3 if latent else 0  # reference latent channels concatenated into a conv input (FLOP accounting)
+    # conv_first -> P0.x and fea
     conv(ws.first, H, W, ws.first_cp, ws.first_cp, pk.first, 64,
-         _conv_out(P0, cp, zc, H, W, False, out2=ws.fea, out2_cp=64, out2_coff=0), cin_ref=3 + nl)
-    # 23 RRDBs
+         _conv_out(P0, cp, zc, H, W, False, out2=ws.fea, out2_cp=64, out2_coff=0), 3 + nl)
+    # nb RRDBs
     chain = ((P0, P1), (P1, P2), (P2, P0))
     for k in range(net.nb):
         for r, (pin, pout) in enumerate(chain):
             convs = pk.rdb[3 * k + r]
             for i in range(4):
                 coff = zc + 64 + 32 * i
-                conv(pin, H, W, cp, coff, convs[i], 32, _conv_out(pin, cp, coff, H, W, True), cin_ref=nl + 64 + 32 * i)
+                conv(pin, H, W, cp, coff, convs[i], 32, _conv_out(pin, cp, coff, H, W, True), nl + 64 + 32 * i)
             o = _conv_out(pout, cp, zc, H, W, False, r1=pin, r1_cp=cp, r1_coff=zc, s1=0.2,
                           r2=P0 if r == 2 else None, r2_cp=cp, r2_coff=zc, s2=0.2)
-            conv(pin, H, W, cp, zc + 192, convs[4], 64, o, cin_ref=nl + 192)
+            conv(pin, H, W, cp, zc + 192, convs[4], 64, o, nl + 192)
     # LR_conv + trunk skip
     conv(P0, H, W, cp, zc + 64, pk.lr_conv, 64, _conv_out(ws.U0, 64, 0, H, W, False, r1=ws.fea, r1_cp=64, s1=1.0),
-         cin_ref=nl + 64)
+         nl + 64)
     # two nearest-×2 upconvs, four phases each
-    for (src, sh, sw, dst, dcp, dcoff), (phw, bias) in zip(
+    for (src, sh, sw, dst, dcp, dcoff), phw in zip(
             ((ws.U0, H, W, ws.U1, 64, 0), (ws.U1, 2 * H, 2 * W, HR0, hcp, zc)), pk.up):
-        for ph, wph in enumerate(phw):
+        for ph, cw in enumerate(phw):
             py, px = ph // 2, ph % 2
             o = _conv_out(dst, dcp, dcoff, 2 * sh, 2 * sw, True, sy=2, sx=2, oy=py, ox=px)
             if prof is not None:  # reference FLOPs: a 3×3 conv at 2× resolution, a quarter of it per phase
-                ev = _prof_begin(prof, 'upconv2x_phase', 2.0 * Bn * (2 * sh) * (2 * sw) * 9 * 64 * 64 / 4)
-            _lib.check(lib.esr_upconv2x_phase_fwd(src.data_ptr(), Bn, sh, sw, 64, 64, wph.data_ptr(),
-                                                  bias.data_ptr(), 64, py, px, ctypes.byref(o), stream),
-                       'esr_upconv2x_phase_fwd')
+                ev = _prof_begin(prof, tagp + 'upconv2x_phase', 2.0 * Bn * (2 * sh) * (2 * sw) * 9 * 64 * 64 / 4)
+            if x3:
+                wx, scale = cw.x3()
+                rc = lib.esr_upconv2x_phase_fwd_x3(src.data_ptr(), Bn, sh, sw, 64, 64, wx.data_ptr(),
+                                                   cw.bias.data_ptr(), scale, 64, py, px, ctypes.byref(o), ovf, stream)
+            else:
+                rc = lib.esr_upconv2x_phase_fwd(src.data_ptr(), Bn, sh, sw, 64, 64, cw.f32.data_ptr(),
+                                                cw.bias.data_ptr(), 64, py, px, ctypes.byref(o), stream)
+            _lib.check(rc, 'esr_upconv2x_phase_fwd')
             if prof is not None:
                 ev.record()
     HH, WW = SF * H, SF * W
-    conv(HR0, HH, WW, hcp, hcp, pk.hr0, 64, _conv_out(HR1, hcp, zc, HH, WW, True), cin_ref=nl + 64)
+    conv(HR0, HH, WW, hcp, hcp, pk.hr0, 64, _conv_out(HR1, hcp, zc, HH, WW, True), nl + 64)
     gen = torch.empty(Bn, 3, HH, WW, device=dev, dtype=torch.float32)
-    conv(HR1, HH, WW, hcp, hcp, pk.hr1, 3, _conv_out(gen, 0, 0, HH, WW, False, planar=1), cin_ref=nl + 64)
+    conv(HR1, HH, WW, hcp, hcp, pk.hr1, 3, _conv_out(gen, 0, 0, HH, WW, False, planar=1), nl + 64)
     if cem is None:
-        return gen
-    return cem_apply(lib, cem, gen, ws.lr, Bn, H, W, SF * m if pre_pad else 0, stream)
+        return gen, ws
+    return cem_apply(lib, cem, gen, ws.lr, Bn, H, W, SF * m if pre_pad else 0, stream), ws
 
 
 def cem_apply(lib, cem, gen, lr, Bn, H, W, M, stream):
@@ -299,3 +380,13 @@ def cem_filter_op(layer, x):
     else:
         raise ValueError(layer.kind)
     return out
+
+
+def set_precision(module, precision):
+    """Select 'x3' or 'f32' for every RRDBNet inside `module` (CEM_PyTorch, DataParallel wrappers included)."""
+    if precision not in PRECISIONS:
+        raise ValueError('precision must be one of %s' % (PRECISIONS,))
+    for m in module.modules():
+        if hasattr(m, '_esr_cache'):
+            m.esr_precision = precision
+    return module

@@ -82,11 +82,12 @@ int esr_upconv2x_phase_fwd(const float *in, int32_t B, int32_t H, int32_t W, int
  *   first    padded NHWC [B][H+2][W+2][first_cp]: Z_LR at channels 0..nz-1, LR at channels first_lr_off..+2
  *   zlr_dst[i] padded NHWC LR-grid buffers with their own pitch zlr_cp[i]: Z_LR at channels 0..nz-1 (i < n_zlr)
  *   zhr_dst[i] padded NHWC HR-grid buffers (sf*H × sf*W), pitch zhr_cp[i]: Z_HR (replicate pad sf*m) at 0..nz-1
- * Z_LR = F.interpolate(Z_HR_padded, 1/sf, bilinear, align_corners=False). */
+ * Z_LR = F.interpolate(Z_HR_padded, 1/sf, bilinear, align_corners=False).
+ * split = 1 writes `first` and the Z slots in the split-f16 layout of the x3 path (below), 0 in fp32. */
 int esr_prep_input(const float *x, int32_t B, int32_t nz, int32_t h, int32_t w, int32_t sf, int32_t m,
                    float *lr_nchw, float *first, int32_t first_cp, int32_t first_lr_off,
                    float *const *zlr_dst, const int32_t *zlr_cp, int32_t n_zlr,
-                   float *const *zhr_dst, const int32_t *zhr_cp, int32_t n_zhr, esr_stream_t stream);
+                   float *const *zhr_dst, const int32_t *zhr_cp, int32_t n_zhr, int32_t split, esr_stream_t stream);
 
 /* CEM step 1, fused DownscaleOP + LR residual (CEMnet.py:152,157-162,186-189):
  *   r[b,c,i,j] = (lr ? lr[b,c,i,j] : 0) - Σ_{u,v<kd} w_down[u][v] · gen[b,c, clamp(sf*i+ph+u-kd/2), clamp(sf*j+ph+v-kd/2)]
@@ -107,6 +108,21 @@ int esr_cem_inv(const float *r, float *q, int32_t B, int32_t H, int32_t W, const
  * out: NCHW [B][3][sf*H-2M][sf*W-2M]; w_up = sf²·ds_kernel. */
 int esr_cem_up_add(const float *q, const float *gen, float *out, int32_t B, int32_t H, int32_t W, int32_t sf,
                    int32_t ph, const float *w_up, int32_t kd, int32_t M, esr_stream_t stream);
+
+/* ---- split-precision ("x3") path --------------------------------------------------------------------------------
+ * Split activation layout: padded NHWC as above, 4 bytes per channel, channels in groups of 8; group g of a pixel is
+ * 32 bytes: f16 hi[8] then f16 lo[8] with hi = f16(v), lo = f16(v - hi) (|v - hi - lo| <= 2^-22 |v|).  cp, cin and
+ * every channel offset are multiples of 8.  Packed x3 weights: [nchunk][taps][n_pad][32 channels as 4 split groups]
+ * (128 B per (tap, n)), scaled by `w_scale` (a power of two the epilogue divides out exactly).
+ * Products are a_hi·b_hi + a_hi·b_lo + a_lo·b_hi on v_mfma_f32_32x32x16_f16 with fp32 accumulation.
+ * Outputs are split unless o->out_planar (fp32 NCHW).  r1/r2 residual inputs are split.  *overflow is OR-ed with 1
+ * if any split output is not representable (|v| >= 65504), in which case the caller reruns the exact-fp32 path. */
+int esr_conv3x3_fwd_x3(const void *in, int32_t B, int32_t H, int32_t W, int32_t in_cp, int32_t cin,
+                       const void *w_packed, const float *bias, float w_scale, int32_t cout, const esr_conv_out *o,
+                       int32_t *overflow, esr_stream_t stream);
+int esr_upconv2x_phase_fwd_x3(const void *in, int32_t B, int32_t H, int32_t W, int32_t in_cp, int32_t cin,
+                              const void *w_packed, const float *bias, float w_scale, int32_t cout, int32_t py,
+                              int32_t px, const esr_conv_out *o, int32_t *overflow, esr_stream_t stream);
 
 /* Library / ABI version (bumped on any signature change). */
 int esr_abi_version(void);

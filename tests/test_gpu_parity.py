@@ -142,7 +142,7 @@ def test_cem_step_vs_golden(gpu_device, name, mode):
     assert normwise_rel(out.cpu(), d['fwd_%s_out' % mode]) < 1e-5
 
 
-def _product_model(d, dev):
+def _product_model(d, dev, precision):
     keys, params = fixture_params(d)
     latent = bool(int(d['latent']))
     net = esr_amd.RRDBNet(3, 3, 64, int(d['nb']), latent_input='all_layers_HR_downscaled' if latent else None,
@@ -156,13 +156,15 @@ def _product_model(d, dev):
     assert not unexpected and all('Filter' in k for k in missing)
     model.to(dev)
     model.train(mode == 'train')
+    engine.set_precision(model, precision)
     return model
 
 
+@pytest.mark.parametrize('precision', ['f32', 'x3'])
 @pytest.mark.parametrize('name', golden_names('rrdb_'))
-def test_generator_vs_reference_golden(gpu_device, name):
+def test_generator_vs_reference_golden(gpu_device, name, precision):
     d = golden(name)
-    model = _product_model(d, gpu_device)
+    model = _product_model(d, gpu_device, precision)
     with torch.no_grad():
         out = model(fixture_input(d).to(gpu_device))
     torch.cuda.synchronize()
@@ -170,7 +172,7 @@ def test_generator_vs_reference_golden(gpu_device, name):
     assert normwise_rel(out.cpu(), d['out']) < 1e-4
 
 
-def _big_model(nb, latent, dev, seed=21, w_scale=0.5):
+def _big_model(nb, latent, dev, precision, seed=21, w_scale=0.5):
     from oracle.recipe import seeded_params
     net = esr_amd.RRDBNet(3, 3, 64, nb, latent_input='all_layers_HR_downscaled' if latent else None,
                           num_latent_channels=3 if latent else 0)
@@ -178,13 +180,15 @@ def _big_model(nb, latent, dev, seed=21, w_scale=0.5):
     sd = model.state_dict()
     params = seeded_params([(k, tuple(v.shape)) for k, v in sd.items()], seed, w_scale=w_scale)
     model.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=False)
+    engine.set_precision(model, precision)
     return model.to(dev), params
 
 
+@pytest.mark.parametrize('precision', ['f32', 'x3'])
 @pytest.mark.parametrize('latent', [False, True])
-def test_full_size_rrdb23_cem_vs_oracle(gpu_device, latent):
+def test_full_size_rrdb23_cem_vs_oracle(gpu_device, latent, precision):
     """C1 shape (128² LR -> 512², RRDB-23 + CEM eval pre-pad) against the CPU oracle: the north_star 1e-3 bar."""
-    model, params = _big_model(23, latent, gpu_device)
+    model, params = _big_model(23, latent, gpu_device, precision)
     model.eval()
     from oracle.recipe import seeded_inputs
     lr, z = seeded_inputs(22, (1, 3, 128, 128), (1, 3, 512, 512) if latent else None)
@@ -196,18 +200,19 @@ def test_full_size_rrdb23_cem_vs_oracle(gpu_device, latent):
         design = O.cem_design(4)
         ref = O.sr_forward(x, O.strip_prefix(params), 23, latent, design, pre_pad=True)
     err = normwise_rel(out, ref)
-    print('full-size normwise rel err (latent=%s): %.3e' % (latent, err))
-    assert err < 1e-3
-    # PSNR-vs-ref delta on [0,1] range: |PSNR(ours, ref)| is what the metric reports
     mse = float(((out.double() - ref.double()) ** 2).mean())
+    print('full-size normwise rel err (latent=%s, %s): %.3e, PSNR vs ref %.1f dB'
+          % (latent, precision, err, 10 * np.log10(1 / max(mse, 1e-30))))
+    assert err < 1e-3
     assert mse < 1e-8
 
 
-def test_cem_consistency_and_batch_invariance(gpu_device):
+@pytest.mark.parametrize('precision', ['f32', 'x3'])
+def test_cem_consistency_and_batch_invariance(gpu_device, precision):
     """Size-independent properties at a larger batch: (1) CEM consistency — DownscaleOP(SR) reproduces the LR input in
     the valid interior (the module's defining property, CEMnet.py:186-189); (2) every image of a batch equals the same
     image run alone, bitwise; (3) two runs are bitwise identical."""
-    model, _ = _big_model(2, False, gpu_device, seed=31)
+    model, _ = _big_model(2, False, gpu_device, precision, seed=31)
     model.train(False)
     x = torch.rand(4, 3, 64, 80, generator=torch.Generator().manual_seed(32)).to(gpu_device)
     with torch.no_grad():
@@ -220,3 +225,91 @@ def test_cem_consistency_and_batch_invariance(gpu_device):
     m = 12  # stay clear of the CEM invalidity margin (10 LR px for the bicubic kernel)
     err = (lr_back - x)[:, :, m:-m, m:-m].abs().max().item()
     assert err < 1e-4, err
+
+
+def test_x3_overflow_falls_back_to_exact_f32(gpu_device):
+    """Activations beyond the f16 range must not corrupt the x3 path: the overflow flag triggers an exact-fp32 rerun."""
+    model, _ = _big_model(1, False, gpu_device, 'x3', seed=41, w_scale=1.0)
+    with torch.no_grad():
+        model.generated_image_model.model[0].weight.mul_(2.0e5)  # conv_first output far beyond 65504
+    model.eval()
+    x = torch.rand(1, 3, 16, 16, generator=torch.Generator().manual_seed(42)).to(gpu_device)
+    before = engine.OVERFLOW_RERUNS
+    with torch.no_grad():
+        y = model(x)
+        engine.set_precision(model, 'f32')
+        ref = model(x)
+    assert engine.OVERFLOW_RERUNS == before + 1
+    assert torch.equal(y, ref)
+
+
+@pytest.mark.parametrize('cin,cout,H,W', [(8, 64, 5, 7), (72, 32, 13, 37), (200, 64, 9, 33), (64, 32, 17, 31),
+                                          (136, 32, 8, 32), (16, 64, 1, 1), (104, 32, 33, 70)])
+def test_conv3x3_layer_x3(gpu_device, cin, cout, H, W):
+    lib = _lib.load()
+    B = 2
+    cp = cin + 8
+    xf = _padded(B, H, W, cp, cin, gpu_device, 11)
+    xf[..., cin:] = 0
+    g = torch.Generator().manual_seed(12)
+    w = torch.randn(cout, cin, 3, 3, generator=g) * 0.1
+    b = torch.rand(cout, generator=g) - 0.5
+    wx, scale = engine.pack_x3(engine.pack_conv_weight(w.to(gpu_device), list(range(cin)), 32 if cout <= 32 else 64))
+    res = _padded(B, H, W, 80, 80, gpu_device, 13)
+    out = torch.zeros(B, H + 2, W + 2, 80, device=gpu_device)
+    out2 = torch.zeros(B, H + 2, W + 2, 64, device=gpu_device)
+    ovf = torch.zeros(1, dtype=torch.int32, device=gpu_device)
+    xs, rs = engine.to_split(xf), engine.to_split(res)
+    o = engine._conv_out(out, 80, 8, H, W, True, r1=rs, r1_cp=80, r1_coff=0, s1=0.2, r2=rs, r2_cp=80, r2_coff=8,
+                         s2=0.5, out2=out2, out2_cp=64, out2_coff=0)
+    _lib.check(lib.esr_conv3x3_fwd_x3(xs.data_ptr(), B, H, W, cp, cin, wx.data_ptr(), b.to(gpu_device).data_ptr(),
+                                      scale, cout, ctypes.byref(o), ovf.data_ptr(), _stream()), 'conv_x3')
+    torch.cuda.synchronize()
+    got = engine.from_split(out)
+    ref = F.leaky_relu(F.conv2d(_nchw(engine.from_split(xs), 0, cin), w.double(), b.double(), padding=1), 0.2)
+    rsv = engine.from_split(rs)
+    ref = 0.5 * (0.2 * ref + _nchw(rsv, 0, cout)) + _nchw(rsv, 8, 8 + cout)
+    err = normwise_rel(_nchw(got, 8, 8 + cout), ref)
+    assert err < 1e-5, err
+    assert torch.equal(out2[:, 1:-1, 1:-1, :cout], out[:, 1:-1, 1:-1, 8:8 + cout])
+    assert torch.all(out[..., :8] == 0) and torch.all(out[..., 8 + cout:] == 0)
+    assert torch.all(out[:, 0] == 0) and torch.all(out[:, -1] == 0) and torch.all(out[:, :, 0] == 0)
+    assert int(ovf.item()) == 0
+
+
+def test_conv3x3_x3_planar_output(gpu_device):
+    lib = _lib.load()
+    B, H, W, cin = 2, 19, 45, 72
+    x = engine.to_split(_padded(B, H, W, cin, cin, gpu_device, 14))
+    w = torch.randn(3, cin, 3, 3, generator=torch.Generator().manual_seed(15)) * 0.05
+    b = torch.tensor([0.1, -0.2, 0.3])
+    wx, scale = engine.pack_x3(engine.pack_conv_weight(w.to(gpu_device), list(range(cin)), 32))
+    out = torch.full((B, 3, H, W), 7.0, device=gpu_device)
+    o = engine._conv_out(out, 0, 0, H, W, False, planar=1)
+    _lib.check(lib.esr_conv3x3_fwd_x3(x.data_ptr(), B, H, W, cin, cin, wx.data_ptr(), b.to(gpu_device).data_ptr(),
+                                      scale, 3, ctypes.byref(o), None, _stream()), 'conv_x3')
+    torch.cuda.synchronize()
+    ref = F.conv2d(_nchw(engine.from_split(x), 0, cin), w.double(), b.double(), padding=1)
+    assert normwise_rel(out.cpu(), ref) < 1e-5
+
+
+@pytest.mark.parametrize('H,W', [(6, 9), (16, 40)])
+def test_upconv2x_phases_x3(gpu_device, H, W):
+    lib = _lib.load()
+    B = 2
+    x = engine.to_split(_padded(B, H, W, 64, 64, gpu_device, 16))
+    w = torch.randn(64, 64, 3, 3, generator=torch.Generator().manual_seed(17)) * 0.05
+    b = torch.randn(64, generator=torch.Generator().manual_seed(18)) * 0.1
+    out = torch.zeros(B, 2 * H + 2, 2 * W + 2, 64, device=gpu_device)
+    bd = b.to(gpu_device)
+    for py in (0, 1):
+        for px in (0, 1):
+            wx, scale = engine.pack_x3(engine.pack_conv_weight(engine.fold_upconv_phase(w.to(gpu_device), py, px),
+                                                               list(range(64)), 64))
+            o = engine._conv_out(out, 64, 0, 2 * H, 2 * W, True, sy=2, sx=2, oy=py, ox=px)
+            _lib.check(lib.esr_upconv2x_phase_fwd_x3(x.data_ptr(), B, H, W, 64, 64, wx.data_ptr(), bd.data_ptr(),
+                                                     scale, 64, py, px, ctypes.byref(o), None, _stream()), 'up_x3')
+    torch.cuda.synchronize()
+    ref = F.leaky_relu(F.conv2d(F.interpolate(_nchw(engine.from_split(x), 0, 64), scale_factor=2, mode='nearest'),
+                                w.double(), b.double(), padding=1), 0.2)
+    assert normwise_rel(_nchw(engine.from_split(out), 0, 64), ref) < 1e-5

@@ -2,6 +2,7 @@
 reference, weight packing / upconv folding algebra, C-ABI library exports, and loud failure without a GPU."""
 import ctypes
 import json
+import math
 import os
 import re
 
@@ -134,3 +135,19 @@ def test_missing_library_fails_loudly(monkeypatch):
     monkeypatch.setattr(_lib, 'LIB_PATH', '/nonexistent/libesr_amd.so')
     with pytest.raises(_lib.ESRLibraryError):
         _lib.load()
+
+
+def test_split_f16_roundtrip_and_x3_packing():
+    torch.manual_seed(3)
+    x = torch.randn(2, 3, 5, 24) * 10
+    back = engine.from_split(engine.to_split(x))
+    assert back.shape == x.shape
+    # |v - hi - lo| <= 2^-22 |v|, or the f16 subnormal step (2^-24) once lo underflows
+    assert bool(((back - x).abs() <= torch.maximum(2 ** -22 * x.abs(), torch.full_like(x, 2 ** -24))).all())
+    w = torch.randn(32, 67, 3, 3) * 0.02
+    pk = engine.pack_conv_weight(w, [0, 1, 2] + [-1] * 5 + [3 + c for c in range(64)], 32)
+    px, scale = engine.pack_x3(pk)
+    assert px.dtype == torch.float16 and px.shape == (3, 9, 32, 4, 2, 8)
+    assert math.log2(scale).is_integer() and 2 ** 14 <= float(pk.abs().max()) * scale < 2 ** 15
+    rec = (px[..., 0, :].float() + px[..., 1, :].float()).reshape(pk.shape) / scale
+    assert float((rec - pk).abs().max()) <= 2 ** -22 * float(pk.abs().max())
