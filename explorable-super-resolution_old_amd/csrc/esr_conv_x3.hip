@@ -1,24 +1,31 @@
 // esr_conv_x3.hip — 3×3 convolution / polyphase upconv on f16 matrix cores with fp32-level accuracy ("x3" path).
 //
-// Every fp32 value v is carried as an f16 pair (hi = f16(v), lo = f16(v - hi)), |v - hi - lo| <= 2^-22 |v| (absolute
-// 2^-25 below the f16 normal range).  A product a·b is evaluated as a_hi·b_hi + a_hi·b_lo + a_lo·b_hi on
+// Numerics.  Every fp32 value v is carried as an f16 pair (hi = f16(v), lo = f16(v - hi)), |v - hi - lo| <= 2^-22 |v|
+// (absolute 2^-25 below the f16 normal range).  A product a·b is evaluated as a_hi·b_hi + a_hi·b_lo + a_lo·b_hi on
 // v_mfma_f32_32x32x16_f16 with fp32 accumulation; the dropped a_lo·b_lo term is <= 2^-22 |ab|.  Three f16 MFMAs
-// (3 × 32 cycles per 32×32×16 block) replace eight f32 MFMAs (8 × 64 cycles per 32×32×16): 5.3× the MFMA throughput
-// of the exact-fp32 path (esr_conv.hip) at ~1e-6 relative error.
+// (3 × 32 cycles per 32×32×16 block) replace eight f32 MFMAs (8 × 64 cycles): 5.3× the MFMA throughput of the
+// exact-fp32 path (esr_conv.hip) at ~1e-6 relative error.
 //
-// "Split" activation layout (include/esr_amd.h): per pixel, channels in groups of 8, each group 32 bytes =
-// 8 × f16 hi then 8 × f16 lo.  Same 4 bytes per channel as fp32, so HBM traffic is unchanged, and the producer's
-// epilogue writes the split form once instead of every consumer splitting it again.
-// Weights: packed [chunk][tap][n_pad][32 channels as 4 split groups] (128 B per (tap, n)), pre-scaled by a power of
-// two (w_scale) so their lo parts stay normal; the epilogue multiplies by 1/w_scale (exact).
+// Layouts.  Split activations (include/esr_amd.h): per pixel, channels in groups of 8, each group 32 bytes =
+// 8 × f16 hi then 8 × f16 lo — 4 bytes per channel like fp32, written once by the producer's epilogue.  Weights:
+// packed [chunk16][tap][n_pad][2 groups × 32 B] (64 B per (tap, n)), pre-scaled by a power of two (w_scale) so their lo
+// parts stay normal; the epilogue multiplies by 1/w_scale (exact).
 //
-// Workgroup: 256 threads (4 waves), output tile 8 rows × 32 cols, all N.  Wave w owns rows {2w, 2w+1} (two 32-pixel
-// M-tiles) × NT 32-channel N-tiles.  Per 32-channel K chunk the halo tile (10×34 pixels × 128 B) and the chunk's
-// weights are copied to LDS at a 144-byte pitch (9 16-byte slots: the 16 lanes of a ds_read_b128 group hit 16 distinct
-// slots), the next chunk is prefetched into registers while the MFMAs run.  MFMA K-step s of a chunk: lane half h
-// consumes channel group 2s+h (its 8 channels are the fragment's 8 K elements): one ds_read_b128 per plane per operand.
-// Epilogue: accumulators are re-staged through LDS as fp32 [pixel][channel] so each thread finishes whole 8-channel
-// groups: bias, LeakyReLU, residuals (split inputs), split + 16-byte stores, fp32 planar stores for the CEM input.
+// Tiling.  The batch is treated as one tall padded image of B·(H+2) rows (the zero halo rows between images are the
+// vertical zero padding), so a tile may straddle two images and no per-image row remainder is wasted; output rows that
+// fall on halo rows are computed and dropped (2 of H+2).  Tiles are 16 rows × 32 columns, plus one remainder column
+// tile of width W % 32 whose 32-pixel M-tiles run row-major across its rows (W = 148 -> 4 full + one 20-wide tile,
+// instead of padding to 160).  Workgroup = 512 threads (8 waves, 2 per SIMD); wave w owns M-tiles 2w, 2w+1 × NT
+// 32-channel N-tiles.
+//
+// Pipeline.  K is walked in 16-channel chunks (one 32×32×16 MFMA step per tap).  Each chunk's halo tile (18 × 34
+// records of 64 B) and weights are copied HBM/L2 -> LDS by LDS-DMA (global_load_lds_dwordx4: no VGPR round trip, no
+// ds_write) into one of two LDS stages while the MFMAs consume the other stage.  Records are 64 B (4 × 16-B slots)
+// with the slot index XOR-swizzled by (record>>2)&3, applied on the DMA source address (the DMA destination is
+// lane-linear), so the 16 lanes of every ds_read_b128 group hit 16 distinct slots.  Out-of-range halo pixels and
+// the channels past cin of a partial chunk are fetched from a zero page.
+// Epilogue: accumulators are re-staged through LDS as fp32 [pixel][channel]; each thread finishes 8-channel groups:
+// 1/w_scale, bias, LeakyReLU, residuals (split inputs), split + 16-byte stores, or fp32 planar stores for CEM.
 #include <hip/hip_runtime.h>
 #include "esr_amd.h"
 
@@ -27,13 +34,17 @@ namespace {
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) const void glob_void;
 
-constexpr int TH = 8, TW = 32, HY = TH + 2, HX = TW + 2;
-constexpr int PIXB = 144;  // LDS bytes per staged pixel / weight row: 128 data + 16 pad
-constexpr int NTHR = 256;
-constexpr int IN_PIECES = HY * HX * 8;  // 16-byte pieces of a full 32-channel input chunk
-constexpr int IN_IT = (IN_PIECES + NTHR - 1) / NTHR;
+constexpr int TH = 16, TWF = 32;
+constexpr int HY = TH + 2, HXF = TWF + 2;
+constexpr int REC = 64;                            // bytes per staged record (16 channels, split)
+constexpr int IN_RECS = (HY * HXF + 15) / 16 * 16;  // 624: whole 16-record DMA wave-instructions
+constexpr int NTHR = 512;
+constexpr int NWAVES = NTHR / 64;
+
+__device__ __attribute__((aligned(16))) unsigned char g_zero_page[64];
 
 struct X3Params {
     const unsigned char *in;
@@ -49,7 +60,6 @@ struct X3Params {
 
 __device__ __forceinline__ float lrelu(float v) { return v > 0.f ? v : 0.2f * v; }
 
-// load one split 8-channel group (32 B) and reconstruct fp32
 __device__ __forceinline__ void load_group(const unsigned char *p, float v[8]) {
     const f16x8 hi = *reinterpret_cast<const f16x8 *>(p);
     const f16x8 lo = *reinterpret_cast<const f16x8 *>(p + 16);
@@ -71,20 +81,19 @@ __device__ __forceinline__ bool store_group(unsigned char *p, const float v[8]) 
     return ok;
 }
 
+// byte offset of logical 16-B slot s of record r inside a stage region
+__device__ __forceinline__ int slot_off(int r, int s) { return r * REC + ((s ^ ((r >> 2) & 3)) << 4); }
+
 template <int NT, int TS>
-__global__ __launch_bounds__(NTHR, 1) void conv_x3_kernel(X3Params p) {
+__global__ __launch_bounds__(NTHR, 2) void conv_x3_kernel(X3Params p) {
     constexpr int T = TS * TS;
     constexpr int N = NT * 32;
-    constexpr int IN_BYTES = HY * HX * PIXB;
-    constexpr int W_PIECES = T * N * 8;
-    constexpr int W_IT = (W_PIECES + NTHR - 1) / NTHR;
-    constexpr int EP_P = N + 4;  // fp32 pitch of the epilogue tile
-    constexpr int MAIN_BYTES = IN_BYTES + T * N * PIXB;
-    constexpr int EP_BYTES = TH * TW * EP_P * 4;
-    constexpr int LDS_BYTES = MAIN_BYTES > EP_BYTES ? MAIN_BYTES : EP_BYTES;
+    constexpr int W_RECS = T * N;  // multiple of 16
+    constexpr int STAGE = (IN_RECS + W_RECS) * REC;
+    constexpr int EP_P = N + 4;
+    constexpr int EP_BYTES = TH * TWF * EP_P * 4;
+    constexpr int LDS_BYTES = 2 * STAGE > EP_BYTES ? 2 * STAGE : EP_BYTES;
     __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
-    unsigned char *s_in = lds;
-    unsigned char *s_w = lds + IN_BYTES;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -92,66 +101,55 @@ __global__ __launch_bounds__(NTHR, 1) void conv_x3_kernel(X3Params p) {
     const int hl = lane >> 5;
     const int ml = lane & 31;
 
-    int t = blockIdx.x;
-    const int tx = t % p.tiles_x;
-    t /= p.tiles_x;
-    const int ty = t % p.tiles_y;
-    const int b = t / p.tiles_y;
-    const int y0 = ty * TH, x0 = tx * TW;
+    const int tx = blockIdx.x % p.tiles_x;
+    const int ty = blockIdx.x / p.tiles_x;
+    const int x0 = tx * TWF;
+    const int tw = min(TWF, p.W - x0);  // tile width (32, or the remainder)
+    const int hx = tw + 2;              // halo tile row length
+    const int r0 = ty * TH;             // tall padded row of halo row 0
+    const int rows_tot = p.B * (p.H + 2);
+    const int nq = TH * tw;             // output pixels in the tile
+    const int nmt = (nq + 31) >> 5;     // 32-pixel M-tiles
 
     const long long rowp = (long long)(p.W + 2);
-    const long long pixb = 4LL * p.in_cp;  // bytes per pixel
-    const unsigned char *in_b = p.in + (long long)b * (p.H + 2) * rowp * pixb;
-    const int nchunk = (p.cin + 31) / 32;
+    const long long pixb = 4LL * p.in_cp;
+    const int nchunk = (p.cin + 15) >> 4;
 
-    u32x4 rin[IN_IT];
-    u32x4 rw[W_IT];
-
-    auto load_chunk = [&](int j) {
-        const int kc = min(32, p.cin - 32 * j);
-        const int kc16 = (kc + 15) & ~15;
-        const int sh = kc16 == 32 ? 3 : 2;  // log2(pieces per pixel)
-        const int real = kc >> 2;           // real pieces per pixel (kc*4 bytes / 16)
-        const int cnt = HY * HX << sh;
-        const unsigned char *base = in_b + 128LL * j;
-#pragma unroll
-        for (int k = 0; k < IN_IT; ++k) {
-            const int idx = tid + k * NTHR;
-            u32x4 v = {0u, 0u, 0u, 0u};
-            if (idx < cnt) {
-                const int px = idx >> sh;
-                const int pc = idx & ((1 << sh) - 1);
-                const int hy = px / HX, hx = px - hy * HX;
-                const int gy = y0 + hy, gx = x0 + hx;
-                if (pc < real && gy < p.H + 2 && gx < p.W + 2)
-                    v = *reinterpret_cast<const u32x4 *>(base + (gy * rowp + gx) * pixb + pc * 16);
-            }
-            rin[k] = v;
+    // ---- LDS-DMA of chunk j into stage st ----
+    auto dma = [&](int j, int st) {
+        unsigned char *base = lds + st * STAGE;
+        const int groups = min(16, p.cin - 16 * j) >> 3;  // real 8-channel groups in this chunk (1 or 2)
+        const int sub = lane >> 2, ps = lane & 3;
+        for (int k = wave; k < IN_RECS / 16; k += NWAVES) {
+            const int r = 16 * k + sub;
+            const int s = ps ^ ((r >> 2) & 3);
+            const int hy = r / hx, hxi = r - (r / hx) * hx;
+            const int gy = r0 + hy, gx = x0 + hxi;
+            const void *src = g_zero_page;
+            if (r < HY * hx && gy < rows_tot && gx < p.W + 2 && (s >> 1) < groups)
+                src = p.in + (gy * rowp + gx) * pixb + 64LL * j + (s << 4);
+            __builtin_amdgcn_global_load_lds((glob_void *)src, (lds_void *)(base + k * 1024), 16, 0, 0);
         }
-        const unsigned char *wj = p.w + (long long)j * W_PIECES * 16;
-#pragma unroll
-        for (int k = 0; k < W_IT; ++k) {
-            const int idx = tid + k * NTHR;
-            if (idx < W_PIECES) rw[k] = *reinterpret_cast<const u32x4 *>(wj + idx * 16);
+        const unsigned char *wj = p.w + (long long)j * W_RECS * REC;
+        for (int k = wave; k < W_RECS / 16; k += NWAVES) {
+            const int r = 16 * k + sub;
+            const int s = ps ^ ((r >> 2) & 3);
+            __builtin_amdgcn_global_load_lds((glob_void *)(wj + r * REC + (s << 4)),
+                                             (lds_void *)(base + (IN_RECS + 16 * k) * REC), 16, 0, 0);
         }
     };
-    auto store_chunk = [&](int j) {
-        const int kc = min(32, p.cin - 32 * j);
-        const int kc16 = (kc + 15) & ~15;
-        const int sh = kc16 == 32 ? 3 : 2;
-        const int cnt = HY * HX << sh;
+
+    // per-lane A-fragment record of each of the wave's two M-tiles (tap 0)
+    int rec0[2];
+    bool mvalid[2];
 #pragma unroll
-        for (int k = 0; k < IN_IT; ++k) {
-            const int idx = tid + k * NTHR;
-            if (idx < cnt)
-                *reinterpret_cast<u32x4 *>(s_in + (idx >> sh) * PIXB + (idx & ((1 << sh) - 1)) * 16) = rin[k];
-        }
-#pragma unroll
-        for (int k = 0; k < W_IT; ++k) {
-            const int idx = tid + k * NTHR;
-            if (idx < W_PIECES) *reinterpret_cast<u32x4 *>(s_w + (idx >> 3) * PIXB + (idx & 7) * 16) = rw[k];
-        }
-    };
+    for (int mt = 0; mt < 2; ++mt) {
+        const int jm = 2 * wave + mt;
+        mvalid[mt] = jm < nmt;  // wave-uniform
+        int q = 32 * jm + ml;
+        if (q >= nq) q = 0;
+        rec0[mt] = (q / tw) * hx + q % tw;
+    }
 
     f32x16 acc[2][NT];
 #pragma unroll
@@ -161,39 +159,38 @@ __global__ __launch_bounds__(NTHR, 1) void conv_x3_kernel(X3Params p) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.f;
 
-    load_chunk(0);
+    dma(0, 0);
     for (int j = 0; j < nchunk; ++j) {
-        __syncthreads();
-        store_chunk(j);
-        __syncthreads();
-        if (j + 1 < nchunk) load_chunk(j + 1);
-        const int kc = min(32, p.cin - 32 * j);
-        const int nsteps = (kc + 15) >> 4;
+        __syncthreads();  // chunk j landed (vmcnt(0) of every wave), stage (j+1)&1 no longer read
+        if (j + 1 < nchunk) dma(j + 1, (j + 1) & 1);
+        const unsigned char *s_in = lds + (j & 1) * STAGE;
+        const unsigned char *s_w = s_in + IN_RECS * REC;
+        if (!mvalid[0]) continue;
 #pragma unroll
         for (int tap = 0; tap < T; ++tap) {
-            const int dy = p.tap_y0 + tap / TS, dx = p.tap_x0 + tap % TS;
-            const unsigned char *a0 = s_in + ((2 * wave + dy) * HX + ml + dx) * PIXB + hl * 32;
-            const unsigned char *bw = s_w + (tap * N + ml) * PIXB + hl * 32;
-            for (int s = 0; s < nsteps; ++s) {
-                f16x8 ah[2], al[2], bh[NT], bl[NT];
+            const int off = (p.tap_y0 + tap / TS) * hx + p.tap_x0 + tap % TS;
+            f16x8 ah[2], al[2], bh[NT], bl[NT];
 #pragma unroll
-                for (int mt = 0; mt < 2; ++mt) {
-                    ah[mt] = *reinterpret_cast<const f16x8 *>(a0 + mt * HX * PIXB + s * 64);
-                    al[mt] = *reinterpret_cast<const f16x8 *>(a0 + mt * HX * PIXB + s * 64 + 16);
-                }
+            for (int mt = 0; mt < 2; ++mt) {
+                const int r = rec0[mt] + off;
+                ah[mt] = *reinterpret_cast<const f16x8 *>(s_in + slot_off(r, 2 * hl));
+                al[mt] = *reinterpret_cast<const f16x8 *>(s_in + slot_off(r, 2 * hl + 1));
+            }
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                const int r = tap * N + nt * 32 + ml;
+                bh[nt] = *reinterpret_cast<const f16x8 *>(s_w + slot_off(r, 2 * hl));
+                bl[nt] = *reinterpret_cast<const f16x8 *>(s_w + slot_off(r, 2 * hl + 1));
+            }
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                if (!mvalid[mt]) continue;
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt) {
-                    bh[nt] = *reinterpret_cast<const f16x8 *>(bw + nt * 32 * PIXB + s * 64);
-                    bl[nt] = *reinterpret_cast<const f16x8 *>(bw + nt * 32 * PIXB + s * 64 + 16);
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[mt], bh[nt], acc[mt][nt], 0, 0, 0);
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mt], bl[nt], acc[mt][nt], 0, 0, 0);
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mt], bh[nt], acc[mt][nt], 0, 0, 0);
                 }
-#pragma unroll
-                for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-                    for (int nt = 0; nt < NT; ++nt) {
-                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[mt], bh[nt], acc[mt][nt], 0, 0, 0);
-                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mt], bl[nt], acc[mt][nt], 0, 0, 0);
-                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mt], bh[nt], acc[mt][nt], 0, 0, 0);
-                    }
             }
         }
     }
@@ -202,58 +199,64 @@ __global__ __launch_bounds__(NTHR, 1) void conv_x3_kernel(X3Params p) {
     __syncthreads();
     float *s_ep = reinterpret_cast<float *>(lds);
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < 2; ++mt) {
+        if (!mvalid[mt]) continue;
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int pix = (2 * wave + mt) * TW + (r & 3) + 8 * (r >> 2) + 4 * hl;
-                s_ep[pix * EP_P + nt * 32 + ml] = acc[mt][nt][r];
+                const int q = 32 * (2 * wave + mt) + (r & 3) + 8 * (r >> 2) + 4 * hl;
+                if (q < nq) s_ep[q * EP_P + nt * 32 + ml] = acc[mt][nt][r];
             }
+    }
     __syncthreads();
 
     const esr_conv_out &o = p.o;
     const long long orow = (long long)(o.out_w + 2);
     constexpr int GROUPS = N / 8;
     bool ok = true;
-    for (int u = tid; u < TH * TW * GROUPS; u += NTHR) {
-        const int pix = u / GROUPS, g = u - (u / GROUPS) * GROUPS;
+    for (int u = tid; u < nq * GROUPS; u += NTHR) {
+        const int q = u / GROUPS, g = u - (u / GROUPS) * GROUPS;
         const int c = 8 * g;
         if (c >= p.cout) continue;
-        const int y = y0 + pix / TW, x = x0 + pix % TW;
-        if (y >= p.H || x >= p.W) continue;
+        const int R = r0 + 1 + q / tw;  // tall padded row of this output pixel
+        const int b = R / (p.H + 2);
+        const int y = R - b * (p.H + 2) - 1;
+        if (b >= p.B || y < 0 || y >= p.H) continue;
+        const int x = x0 + q % tw;
         const int oy = o.out_sy * y + o.out_oy, ox = o.out_sx * x + o.out_ox;
         const long long opix = ((long long)b * (o.out_h + 2) + oy + 1) * orow + ox + 1;
         float v[8];
-        const f32x4 v0 = *reinterpret_cast<const f32x4 *>(s_ep + pix * EP_P + c);
-        const f32x4 v1 = *reinterpret_cast<const f32x4 *>(s_ep + pix * EP_P + c + 4);
+        const f32x4 v0 = *reinterpret_cast<const f32x4 *>(s_ep + q * EP_P + c);
+        const f32x4 v1 = *reinterpret_cast<const f32x4 *>(s_ep + q * EP_P + c + 4);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) { v[j] = v0[j]; v[j + 4] = v1[j]; }
+        for (int k = 0; k < 4; ++k) { v[k] = v0[k]; v[k + 4] = v1[k]; }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const float bj = (c + j < p.cout) ? p.bias[c + j] : 0.f;
-            v[j] = v[j] * p.w_scale_inv + bj;
-            if (o.lrelu) v[j] = lrelu(v[j]);
+        for (int k = 0; k < 8; ++k) {
+            const float bk = (c + k < p.cout) ? p.bias[c + k] : 0.f;
+            v[k] = v[k] * p.w_scale_inv + bk;
+            if (o.lrelu) v[k] = lrelu(v[k]);
         }
         if (o.r1) {
             float r[8];
             load_group(reinterpret_cast<const unsigned char *>(o.r1) + (opix * o.r1_cp + o.r1_coff + c) * 4, r);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = o.s1 * v[j] + r[j];
+            for (int k = 0; k < 8; ++k) v[k] = o.s1 * v[k] + r[k];
         }
         if (o.r2) {
             float r[8];
             load_group(reinterpret_cast<const unsigned char *>(o.r2) + (opix * o.r2_cp + o.r2_coff + c) * 4, r);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = o.s2 * v[j] + r[j];
+            for (int k = 0; k < 8; ++k) v[k] = o.s2 * v[k] + r[k];
         }
         if (o.out_planar) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j)
-                if (c + j < p.cout) o.out[(((long long)b * p.cout + c + j) * o.out_h + oy) * o.out_w + ox] = v[j];
+            for (int k = 0; k < 8; ++k)
+                if (c + k < p.cout) o.out[(((long long)b * p.cout + c + k) * o.out_h + oy) * o.out_w + ox] = v[k];
         } else {
             ok &= store_group(reinterpret_cast<unsigned char *>(o.out) + (opix * o.out_cp + o.out_coff + c) * 4, v);
-            if (o.out2) store_group(reinterpret_cast<unsigned char *>(o.out2) + (opix * o.out2_cp + o.out2_coff + c) * 4, v);
+            if (o.out2)
+                store_group(reinterpret_cast<unsigned char *>(o.out2) + (opix * o.out2_cp + o.out2_coff + c) * 4, v);
         }
     }
     if (!ok && p.overflow) atomicOr(p.overflow, 1);
@@ -277,11 +280,11 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
     p.w = static_cast<const unsigned char *>(w);
     p.bias = bias; p.w_scale_inv = 1.f / w_scale; p.cout = cout;
     p.tap_y0 = ty0; p.tap_x0 = tx0;
-    p.tiles_x = (W + TW - 1) / TW;
-    p.tiles_y = (H + TH - 1) / TH;
+    p.tiles_x = (W + TWF - 1) / TWF;
+    p.tiles_y = (B * (H + 2) - 2 + TH - 1) / TH;
     p.overflow = overflow;
     p.o = *o;
-    const dim3 grid((unsigned)(p.tiles_x * p.tiles_y * B)), block(NTHR);
+    const dim3 grid((unsigned)(p.tiles_x * p.tiles_y)), block(NTHR);
     if (taps_side == 3) {
         if (cout > 32) hipLaunchKernelGGL((conv_x3_kernel<2, 3>), grid, block, 0, stream, p);
         else hipLaunchKernelGGL((conv_x3_kernel<1, 3>), grid, block, 0, stream, p);

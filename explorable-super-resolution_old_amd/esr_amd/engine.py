@@ -83,13 +83,16 @@ def split_f16(x):
 
 
 def pack_x3(packed):
-    """fp32 packed weights [nch][T][n_pad][32] -> split layout [nch][T][n_pad][4 groups][hi 8 | lo 8] (f16), scaled by
-    a power of two so that max|w|·scale lies in [2^14, 2^15) (lo parts stay out of the f16 subnormal range)."""
+    """fp32 packed weights [nch32][T][n_pad][32] -> x3 layout [nch16][T][n_pad][2 groups][hi 8 | lo 8] (f16): 16-channel
+    K chunks (esr_conv_x3.hip), scaled by a power of two so that max|w|·scale lies in [2^14, 2^15) (lo parts stay out
+    of the f16 subnormal range)."""
     amax = float(packed.abs().max())
     e = 0 if amax == 0.0 else 14 - math.floor(math.log2(amax))
     scale = 2.0 ** e
-    hi, lo = split_f16(packed * scale)
-    sh = packed.shape[:3] + (4, 1, 8)
+    n32, T, n_pad, _ = packed.shape
+    p16 = packed.view(n32, T, n_pad, 2, 16).permute(0, 3, 1, 2, 4).reshape(2 * n32, T, n_pad, 16)
+    hi, lo = split_f16(p16 * scale)
+    sh = (2 * n32, T, n_pad, 2, 1, 8)
     out = torch.cat([hi.reshape(sh), lo.reshape(sh)], dim=4).contiguous()
     return out, scale
 

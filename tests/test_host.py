@@ -147,7 +147,8 @@ def test_split_f16_roundtrip_and_x3_packing():
     w = torch.randn(32, 67, 3, 3) * 0.02
     pk = engine.pack_conv_weight(w, [0, 1, 2] + [-1] * 5 + [3 + c for c in range(64)], 32)
     px, scale = engine.pack_x3(pk)
-    assert px.dtype == torch.float16 and px.shape == (3, 9, 32, 4, 2, 8)
+    assert px.dtype == torch.float16 and px.shape == (6, 9, 32, 2, 2, 8)  # 16-channel K chunks
     assert math.log2(scale).is_integer() and 2 ** 14 <= float(pk.abs().max()) * scale < 2 ** 15
-    rec = (px[..., 0, :].float() + px[..., 1, :].float()).reshape(pk.shape) / scale
+    rec16 = (px[..., 0, :].float() + px[..., 1, :].float()).reshape(6, 9, 32, 16) / scale
+    rec = rec16.view(3, 2, 9, 32, 16).permute(0, 2, 3, 1, 4).reshape(pk.shape)
     assert float((rec - pk).abs().max()) <= 2 ** -22 * float(pk.abs().max())
