@@ -1,0 +1,356 @@
+// esr_train.hip — backward-pass kernels of the RRDB generator + CEM for gfx950 (training step, Z optimisation).
+//
+// The data gradient of a 3×3 conv is itself a 3×3 conv (rot180, in/out channels swapped) and runs on
+// esr_conv3x3_fwd with repacked weights.  This file adds what has no forward counterpart:
+//   esr_conv3x3_wgrad  weight (+bias) gradient: dW[tap][ci][co] = Σ_pixels in[p + tap][ci] · dout[p][co], a GEMM with
+//                      K = pixels, on v_mfma_f32_32x32x2_f32 (exact fp32); split-K over pixel tiles into
+//                      deterministic per-split partials, then esr_wgrad_reduce (fixed summation order, no atomics).
+//   esr_lrelu_bwd      d *= (y > 0 ? 1 : 0.2) from the saved LeakyReLU output (block.py:10-23)
+//   esr_axpby          y = a·x1 + b·x2 on channel slices of padded NHWC buffers (residual fan-in, block.py:96,235,270)
+//   esr_sum2x2         adjoint of nearest ×2 upsampling (block.py:298)
+//   esr_nchw_to_padded layout adapter between NCHW images and padded NHWC feature maps
+//   esr_cem_adjoint    exact adjoint of the CEM stencils with replicate padding (CEMnet.py:149-162):
+//                      for F(x)[o] = Σ_u w[u] x[clamp(s·o + c + u - p)] it gathers
+//                      F^T(g)[k] = Σ_{(o,u): clamp(s·o + c + u - p) = k} w[u] g[o]   (2-D, separable clamp)
+#include <hip/hip_runtime.h>
+#include "esr_amd.h"
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int NT = 256;
+inline unsigned nblocks(long long n) { return (unsigned)((n + NT - 1) / NT); }
+inline int launched() { return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH; }
+
+// ---------------------------------------------------------------------------------------------------------------------
+// weight gradient
+// ---------------------------------------------------------------------------------------------------------------------
+constexpr int WT_TH = 8, WT_TW = 32, WT_HY = WT_TH + 2, WT_HX = WT_TW + 2;
+constexpr int WT_IP = 36;  // LDS pitch of a staged input pixel (32 channels)
+constexpr int WT_DP = 68;  // LDS pitch of a staged output-gradient pixel (64 channels)
+constexpr int WT_MAXP = 5; // (tap, co-tile) pairs per wave: 9 taps × 2 co-tiles over 4 waves
+
+struct WgradParams {
+    const float *in;
+    int in_cp, cin, up2;
+    const float *dout;
+    int dout_cp, dout_coff, cout, cout_pad;
+    int B, H, W, tiles_x, tiles_y, splits, cin_pad;
+    float *partial;  // [splits][9*cin_pad*cout_pad + cout_pad]
+};
+
+__global__ __launch_bounds__(256, 1) void wgrad_kernel(WgradParams p) {
+    __shared__ __attribute__((aligned(16))) float s_in[WT_HY * WT_HX * WT_IP];
+    __shared__ __attribute__((aligned(16))) float s_d[WT_TH * WT_TW * WT_DP];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hl = lane >> 5, ml = lane & 31;
+    const int chunk = blockIdx.x % (p.cin_pad / 32);
+    const int split = blockIdx.x / (p.cin_pad / 32);
+    const int ntiles = p.B * p.tiles_y * p.tiles_x;
+    const int t_begin = (int)((long long)ntiles * split / p.splits);
+    const int t_end = (int)((long long)ntiles * (split + 1) / p.splits);
+    const int nct = p.cout_pad / 32;
+    const int npairs = 9 * nct;
+    const int c0 = chunk * 32;
+    const int kc = min(32, p.cin - c0);
+
+    f32x16 acc[WT_MAXP];
+#pragma unroll
+    for (int i = 0; i < WT_MAXP; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+    float bsum = 0.f;  // bias partial: thread (co = tid & 63) over pixels tid>>6 (+4)
+
+    const int Hi = p.up2 ? p.H / 2 : p.H, Wi = p.up2 ? p.W / 2 : p.W;  // input grid
+    for (int t = t_begin; t < t_end; ++t) {
+        const int tx = t % p.tiles_x, ty = (t / p.tiles_x) % p.tiles_y, b = t / (p.tiles_x * p.tiles_y);
+        const int y0 = ty * WT_TH, x0 = tx * WT_TW;
+        __syncthreads();
+        // input halo tile (output-grid coordinates, zero outside)
+        for (int idx = tid; idx < WT_HY * WT_HX * 8; idx += 256) {
+            const int px = idx >> 3, c4 = idx & 7;
+            const int hy = px / WT_HX, hx = px - hy * WT_HX;
+            const int Y = y0 + hy - 1, X = x0 + hx - 1;  // output-grid coords of this halo pixel
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (Y >= 0 && Y < p.H && X >= 0 && X < p.W && c4 * 4 < kc) {
+                const int sy = p.up2 ? Y / 2 : Y, sx = p.up2 ? X / 2 : X;
+                const float *src = p.in + (((long long)b * (Hi + 2) + sy + 1) * (Wi + 2) + sx + 1) * p.in_cp + c0 + c4 * 4;
+                v = *reinterpret_cast<const f32x4 *>(src);
+            }
+            *reinterpret_cast<f32x4 *>(s_in + px * WT_IP + c4 * 4) = v;
+        }
+        // output-gradient tile
+        for (int idx = tid; idx < WT_TH * WT_TW * 16; idx += 256) {
+            const int px = idx >> 4, c4 = idx & 15;
+            const int y = y0 + px / WT_TW, x = x0 + px % WT_TW;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (y < p.H && x < p.W && c4 * 4 < p.cout) {
+                const float *src = p.dout + (((long long)b * (p.H + 2) + y + 1) * (p.W + 2) + x + 1) * p.dout_cp +
+                                   p.dout_coff + c4 * 4;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) v[k] = (c4 * 4 + k < p.cout) ? src[k] : 0.f;
+            }
+            *reinterpret_cast<f32x4 *>(s_d + px * WT_DP + c4 * 4) = v;
+        }
+        __syncthreads();
+        if (chunk == 0 && tid < 64 * 4)
+            for (int px = tid >> 6; px < WT_TH * WT_TW; px += 4) bsum += s_d[px * WT_DP + (tid & 63)];
+        // K loop: pixel pairs; lane half h takes pixel 2s+h
+        for (int s = 0; s < WT_TH * WT_TW / 2; ++s) {
+            const int px = 2 * s + hl;
+            const int py = px / WT_TW, pxx = px % WT_TW;
+#pragma unroll
+            for (int i = 0; i < WT_MAXP; ++i) {
+                const int pr = wave + 4 * i;
+                if (pr >= npairs) break;
+                const int tap = pr / nct, ct = pr - (pr / nct) * nct;
+                const int hp = (py + tap / 3) * WT_HX + pxx + tap % 3;
+                const float a = s_in[hp * WT_IP + ml];
+                const float bb = s_d[px * WT_DP + ct * 32 + ml];
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bb, acc[i], 0, 0, 0);
+            }
+        }
+    }
+    // D layout: lane column j = co (ml), rows i = ci = (r&3) + 8*(r>>2) + 4*hl
+    float *part = p.partial + (long long)split * (9LL * p.cin_pad * p.cout_pad + p.cout_pad);
+#pragma unroll
+    for (int i = 0; i < WT_MAXP; ++i) {
+        const int pr = wave + 4 * i;
+        if (pr >= npairs) break;
+        const int tap = pr / nct, ct = pr - (pr / nct) * nct;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int ci = c0 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+            part[((long long)tap * p.cin_pad + ci) * p.cout_pad + ct * 32 + ml] = acc[i][r];
+        }
+    }
+    // bias partial (chunk-0 workgroups): reduce the 4 pixel-phase partials through LDS
+    if (chunk == 0) {
+        __syncthreads();
+        s_d[tid] = bsum;
+        __syncthreads();
+        if (tid < p.cout_pad) {
+            float v = 0.f;
+            if (tid < 64) v = s_d[tid] + s_d[64 + tid] + s_d[128 + tid] + s_d[192 + tid];
+            part[9LL * p.cin_pad * p.cout_pad + tid] = v;
+        }
+    }
+}
+
+__global__ void wgrad_reduce_kernel(const float *partial, int splits, long long n, float scale, float *out) {
+    const long long i = (long long)blockIdx.x * NT + threadIdx.x;
+    if (i >= n) return;
+    float s = 0.f;
+    for (int k = 0; k < splits; ++k) s += partial[(long long)k * n + i];
+    out[i] = scale * s;
+}
+
+// ---------------------------------------------------------------------------------------------------------------------
+// elementwise helpers on padded NHWC channel slices
+// ---------------------------------------------------------------------------------------------------------------------
+__device__ __forceinline__ long long pix_index(long long idx, int C, int B, int H, int W, int *c) {
+    *c = idx % C;
+    long long q = idx / C;
+    const int x = q % W;
+    q /= W;
+    const int y = q % H;
+    const int b = q / H;
+    return ((long long)b * (H + 2) + y + 1) * (W + 2) + x + 1;
+}
+
+__global__ void lrelu_bwd_kernel(float *d, int d_cp, int d_coff, const float *y, int y_cp, int y_coff, int C, int B,
+                                 int H, int W) {
+    const long long idx = (long long)blockIdx.x * NT + threadIdx.x;
+    if (idx >= (long long)B * H * W * C) return;
+    int c;
+    const long long pix = pix_index(idx, C, B, H, W, &c);
+    if (!(y[pix * y_cp + y_coff + c] > 0.f)) d[pix * d_cp + d_coff + c] *= 0.2f;
+}
+
+__global__ void axpby_kernel(float *out, int o_cp, int o_coff, float a, const float *x1, int x1_cp, int x1_coff,
+                             float b, const float *x2, int x2_cp, int x2_coff, int C, int B, int H, int W) {
+    const long long idx = (long long)blockIdx.x * NT + threadIdx.x;
+    if (idx >= (long long)B * H * W * C) return;
+    int c;
+    const long long pix = pix_index(idx, C, B, H, W, &c);
+    float v = a * x1[pix * x1_cp + x1_coff + c];
+    if (x2) v += b * x2[pix * x2_cp + x2_coff + c];
+    out[pix * o_cp + o_coff + c] = v;
+}
+
+// out (grid H×W) = Σ over each 2×2 block of src (grid 2H×2W)
+__global__ void sum2x2_kernel(float *out, int o_cp, int o_coff, const float *src, int s_cp, int s_coff, int C, int B,
+                              int H, int W) {
+    const long long idx = (long long)blockIdx.x * NT + threadIdx.x;
+    if (idx >= (long long)B * H * W * C) return;
+    const int c = idx % C;
+    long long q = idx / C;
+    const int x = q % W;
+    q /= W;
+    const int y = q % H;
+    const int b = q / H;
+    float v = 0.f;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+            v += src[(((long long)b * (2 * H + 2) + 2 * y + a + 1) * (2 * W + 2) + 2 * x + e + 1) * s_cp + s_coff + c];
+    out[(((long long)b * (H + 2) + y + 1) * (W + 2) + x + 1) * o_cp + o_coff + c] = v;
+}
+
+__global__ void nchw_to_padded_kernel(const float *src, int C, int B, int H, int W, float *dst, int d_cp, int d_coff,
+                                      int to_nchw) {
+    const long long idx = (long long)blockIdx.x * NT + threadIdx.x;
+    if (idx >= (long long)B * C * H * W) return;
+    const int x = idx % W;
+    const int y = (idx / W) % H;
+    const int c = (idx / ((long long)W * H)) % C;
+    const int b = idx / ((long long)W * H * C);
+    const long long pix = ((long long)b * (H + 2) + y + 1) * (W + 2) + x + 1;
+    if (to_nchw) const_cast<float *>(src)[idx] = dst[pix * d_cp + d_coff + c];
+    else dst[pix * d_cp + d_coff + c] = src[idx];
+}
+
+// ---------------------------------------------------------------------------------------------------------------------
+// CEM adjoint
+// ---------------------------------------------------------------------------------------------------------------------
+// (o, u) pairs of one dimension with clamp(s*o + c + u - pd, 0, L-1) == k: for a fixed u, an o-range [lo, hi].
+__device__ __forceinline__ bool o_range(int k, int u, int s, int c, int pd, int L, int O, int *lo, int *hi) {
+    const int base = c + u - pd;  // position = s*o + base
+    int a, b;
+    if (k > 0 && k < L - 1) {
+        const int t = k - base;
+        if (t < 0 || t % s) return false;
+        a = b = t / s;
+    } else if (k == 0) {  // s*o + base <= 0
+        a = 0;
+        const int t = -base;
+        if (t < 0) return false;
+        b = t / s;
+        if (L == 1) b = O - 1;
+    } else {  // k == L-1: s*o + base >= L-1
+        const int t = L - 1 - base;
+        a = t <= 0 ? 0 : (t + s - 1) / s;
+        b = O - 1;
+    }
+    if (a < 0) a = 0;
+    if (b > O - 1) b = O - 1;
+    if (a > b) return false;
+    *lo = a;
+    *hi = b;
+    return true;
+}
+
+struct AdjParams {
+    const float *g;   // [B*C][Oy][Ox]
+    float *out;       // [B*C][Ny][Nx] with Ny = ceil(Ly/os) sampled at k = os*i + oc
+    const float *w;   // [K][K] forward taps
+    int K, s, c, Ly, Lx, Oy, Ox, os, oc, Ny, Nx, planes;
+    float alpha;      // out = alpha * F^T(g) (+ beta * out when accumulate)
+    int accumulate;
+};
+
+__global__ __launch_bounds__(NT) void cem_adjoint_kernel(AdjParams p) {
+    __shared__ float sw[64 * 64];
+    for (int i = threadIdx.x; i < p.K * p.K; i += NT) sw[i] = p.w[i];
+    __syncthreads();
+    const long long idx = (long long)blockIdx.x * NT + threadIdx.x;
+    if (idx >= (long long)p.planes * p.Ny * p.Nx) return;
+    const int j = idx % p.Nx, i = (idx / p.Nx) % p.Ny;
+    const long long plane = idx / ((long long)p.Nx * p.Ny);
+    const int ky = p.os * i + p.oc, kx = p.os * j + p.oc;
+    const float *g = p.g + plane * p.Oy * p.Ox;
+    const int pd = p.K / 2;
+    float acc = 0.f;
+    for (int uy = 0; uy < p.K; ++uy) {
+        int ylo, yhi;
+        if (!o_range(ky, uy, p.s, p.c, pd, p.Ly, p.Oy, &ylo, &yhi)) continue;
+        for (int ux = 0; ux < p.K; ++ux) {
+            int xlo, xhi;
+            if (!o_range(kx, ux, p.s, p.c, pd, p.Lx, p.Ox, &xlo, &xhi)) continue;
+            const float wv = sw[uy * p.K + ux];
+            float sg = 0.f;
+            for (int oy = ylo; oy <= yhi; ++oy)
+                for (int ox = xlo; ox <= xhi; ++ox) sg += g[(long long)oy * p.Ox + ox];
+            acc += wv * sg;
+        }
+    }
+    float *o = p.out + plane * p.Ny * p.Nx + (long long)i * p.Nx + j;
+    *o = p.accumulate ? *o + p.alpha * acc : p.alpha * acc;
+}
+
+}  // namespace
+
+extern "C" int esr_conv3x3_wgrad(const float *in, int32_t in_cp, int32_t cin, int32_t up2, const float *dout,
+                                 int32_t dout_cp, int32_t dout_coff, int32_t cout, int32_t B, int32_t H, int32_t W,
+                                 int32_t splits, float *partial, esr_stream_t stream) {
+    if (!in || !dout || !partial || cin <= 0 || cin % 4 || in_cp % 4 || cout <= 0 || cout > 64 || B <= 0 ||
+        H <= 0 || W <= 0 || splits <= 0 || (up2 && (H % 2 || W % 2)))
+        return ESR_EINVAL;
+    WgradParams p;
+    p.in = in; p.in_cp = in_cp; p.cin = cin; p.up2 = up2;
+    p.dout = dout; p.dout_cp = dout_cp; p.dout_coff = dout_coff; p.cout = cout; p.cout_pad = cout > 32 ? 64 : 32;
+    p.B = B; p.H = H; p.W = W;
+    p.tiles_x = (W + WT_TW - 1) / WT_TW; p.tiles_y = (H + WT_TH - 1) / WT_TH;
+    p.splits = splits; p.cin_pad = (cin + 31) / 32 * 32;
+    p.partial = partial;
+    hipLaunchKernelGGL(wgrad_kernel, dim3((unsigned)(p.cin_pad / 32 * splits)), dim3(256), 0, (hipStream_t)stream, p);
+    return launched();
+}
+
+extern "C" int esr_wgrad_reduce(const float *partial, int32_t splits, int64_t n, float scale, float *out,
+                                esr_stream_t stream) {
+    if (!partial || !out || splits <= 0 || n <= 0) return ESR_EINVAL;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(nblocks(n)), dim3(NT), 0, (hipStream_t)stream, partial, splits, n,
+                       scale, out);
+    return launched();
+}
+
+extern "C" int esr_lrelu_bwd(float *d, int32_t d_cp, int32_t d_coff, const float *y, int32_t y_cp, int32_t y_coff,
+                             int32_t C, int32_t B, int32_t H, int32_t W, esr_stream_t stream) {
+    if (!d || !y || C <= 0 || B <= 0 || H <= 0 || W <= 0) return ESR_EINVAL;
+    hipLaunchKernelGGL(lrelu_bwd_kernel, dim3(nblocks((long long)B * H * W * C)), dim3(NT), 0, (hipStream_t)stream, d,
+                       d_cp, d_coff, y, y_cp, y_coff, C, B, H, W);
+    return launched();
+}
+
+extern "C" int esr_axpby(float *out, int32_t o_cp, int32_t o_coff, float a, const float *x1, int32_t x1_cp,
+                         int32_t x1_coff, float b, const float *x2, int32_t x2_cp, int32_t x2_coff, int32_t C,
+                         int32_t B, int32_t H, int32_t W, esr_stream_t stream) {
+    if (!out || !x1 || C <= 0 || B <= 0 || H <= 0 || W <= 0) return ESR_EINVAL;
+    hipLaunchKernelGGL(axpby_kernel, dim3(nblocks((long long)B * H * W * C)), dim3(NT), 0, (hipStream_t)stream, out,
+                       o_cp, o_coff, a, x1, x1_cp, x1_coff, b, x2, x2_cp, x2_coff, C, B, H, W);
+    return launched();
+}
+
+extern "C" int esr_sum2x2(float *out, int32_t o_cp, int32_t o_coff, const float *src, int32_t s_cp, int32_t s_coff,
+                          int32_t C, int32_t B, int32_t H, int32_t W, esr_stream_t stream) {
+    if (!out || !src || C <= 0 || B <= 0 || H <= 0 || W <= 0) return ESR_EINVAL;
+    hipLaunchKernelGGL(sum2x2_kernel, dim3(nblocks((long long)B * H * W * C)), dim3(NT), 0, (hipStream_t)stream, out,
+                       o_cp, o_coff, src, s_cp, s_coff, C, B, H, W);
+    return launched();
+}
+
+extern "C" int esr_nchw_to_padded(const float *src, int32_t C, int32_t B, int32_t H, int32_t W, float *dst,
+                                  int32_t d_cp, int32_t d_coff, int32_t to_nchw, esr_stream_t stream) {
+    if (!src || !dst || C <= 0 || B <= 0 || H <= 0 || W <= 0 || d_coff + C > d_cp) return ESR_EINVAL;
+    hipLaunchKernelGGL(nchw_to_padded_kernel, dim3(nblocks((long long)B * C * H * W)), dim3(NT), 0,
+                       (hipStream_t)stream, src, C, B, H, W, dst, d_cp, d_coff, to_nchw);
+    return launched();
+}
+
+extern "C" int esr_cem_adjoint(const float *g, int32_t planes, int32_t Oy, int32_t Ox, const float *w, int32_t K,
+                               int32_t s, int32_t c, int32_t Ly, int32_t Lx, int32_t os, int32_t oc, float alpha,
+                               int32_t accumulate, float *out, esr_stream_t stream) {
+    if (!g || !w || !out || planes <= 0 || Oy <= 0 || Ox <= 0 || K <= 0 || K > 64 || !(K & 1) || s <= 0 ||
+        Ly <= 0 || Lx <= 0 || os <= 0 || oc < 0 || oc >= os)
+        return ESR_EINVAL;
+    AdjParams p;
+    p.g = g; p.out = out; p.w = w; p.K = K; p.s = s; p.c = c; p.Ly = Ly; p.Lx = Lx; p.Oy = Oy; p.Ox = Ox;
+    p.os = os; p.oc = oc; p.Ny = (Ly - oc + os - 1) / os; p.Nx = (Lx - oc + os - 1) / os; p.planes = planes;
+    p.alpha = alpha; p.accumulate = accumulate;
+    hipLaunchKernelGGL(cem_adjoint_kernel, dim3(nblocks((long long)planes * p.Ny * p.Nx)), dim3(NT), 0,
+                       (hipStream_t)stream, p);
+    return launched();
+}

@@ -45,6 +45,16 @@ _SIGNATURES = {
     'esr_cem_inv': [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p],
     'esr_cem_up_add': [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int,
                        c_void_p],
+    'esr_conv3x3_wgrad': [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                          c_void_p, c_void_p],
+    'esr_wgrad_reduce': [c_void_p, c_int, ctypes.c_int64, c_float, c_void_p, c_void_p],
+    'esr_lrelu_bwd': [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    'esr_axpby': [c_void_p, c_int, c_int, c_float, c_void_p, c_int, c_int, c_float, c_void_p, c_int, c_int, c_int,
+                  c_int, c_int, c_int, c_void_p],
+    'esr_sum2x2': [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    'esr_nchw_to_padded': [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p],
+    'esr_cem_adjoint': [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                        c_float, c_int, c_void_p, c_void_p],
     'esr_abi_version': [],
 }
 EXPORTED = tuple(_SIGNATURES)

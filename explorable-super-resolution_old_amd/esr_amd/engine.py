@@ -222,9 +222,11 @@ def generator_forward(net, x, cem=None):
     """RRDBNet.forward, optionally wrapped by CEM_PyTorch.forward (cem = the CEM_PyTorch module)."""
     global OVERFLOW_RERUNS
     _require_device(x, 'generator input')
-    if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in net.parameters())):
-        raise RuntimeError('esr_amd: the HIP generator is forward-only in this build; run under torch.no_grad() '
-                           '(or freeze parameters and the input)')
+    if torch.is_grad_enabled() and x.requires_grad:
+        raise NotImplementedError('esr_amd: gradients w.r.t. the generator input (Z optimisation) are not built yet')
+    if torch.is_grad_enabled() and any(p.requires_grad for p in net.parameters()):
+        from . import train_engine  # training step: retained activations + HIP backward (exact fp32)
+        return train_engine.generator_forward_train(net, x.contiguous(), cem)
     precision = getattr(net, 'esr_precision', None) or DEFAULT_PRECISION
     if precision not in PRECISIONS:
         raise ValueError('esr_precision must be one of %s' % (PRECISIONS,))
@@ -237,7 +239,9 @@ def generator_forward(net, x, cem=None):
     return out
 
 
-def _forward(net, x, cem, precision):
+def _forward(net, x, cem, precision, train_ws=None):
+    """One generator (+CEM) forward.  With `train_ws` (esr_amd.train_engine) every RDB's concat buffer is kept for
+    the backward pass instead of the inference ping-pong, and the workspace comes from the caller."""
     lib = _lib.load()
     x3 = precision == 'x3'
     latent = net.latent_input is not None
@@ -252,22 +256,38 @@ def _forward(net, x, cem, precision):
     m = int(cem.margins_LR) if pre_pad else 0
     H, W = h + 2 * m, w + 2 * m
     dev = x.device
-    ws = _workspace(net, dev, Bn, H, W, latent, precision)
+    ws = train_ws if train_ws is not None else _workspace(net, dev, Bn, H, W, latent, precision)
     pk = _packed(net, latent)
     _require_device(pk.first.bias, 'generator parameters')
     stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     zc, cp, hcp = ws.zc, ws.cp, ws.hr_cp
-    P0, P1, P2 = ws.P
     HR0, HR1 = ws.HR
     ovf = ws.overflow.data_ptr()
+    if train_ws is None:
+        P0, P1, P2 = ws.P
 
-    zlr = (ctypes.c_void_p * 3)(*[t.data_ptr() for t in ws.P])
-    zlr_cp = (ctypes.c_int32 * 3)(cp, cp, cp)
+        def rrdb_bufs(k):  # (RRDB input, RDB1 out, RDB2 out, RRDB output): ping-pong, output in place
+            return P0, P1, P2, P0
+        lr_bufs = ws.P
+    else:
+        Q = ws.Q
+
+        def rrdb_bufs(k):
+            return Q[3 * k], Q[3 * k + 1], Q[3 * k + 2], Q[3 * k + 3]
+        lr_bufs = Q
+
+    # every concat buffer carries Z_LR in its slot; prep writes up to 4 destinations per call
     zhr = (ctypes.c_void_p * 2)(HR0.data_ptr(), HR1.data_ptr())
     zhr_cp = (ctypes.c_int32 * 2)(hcp, hcp)
-    _lib.check(lib.esr_prep_input(x.data_ptr(), Bn, nz, h, w, SF, m, ws.lr.data_ptr(), ws.first.data_ptr(),
-                                  ws.first_cp, ws.first_lr_off, zlr, zlr_cp, 3 if nz else 0, zhr, zhr_cp,
-                                  2 if nz else 0, int(x3), stream), 'esr_prep_input')
+    groups = [lr_bufs[i:i + 4] for i in range(0, len(lr_bufs), 4)] if nz else [[]]
+    for gi, grp in enumerate(groups):
+        zlr = (ctypes.c_void_p * 4)(*([t.data_ptr() for t in grp] + [None] * (4 - len(grp))))
+        zlr_cp = (ctypes.c_int32 * 4)(*([cp] * 4))
+        first = gi == 0
+        _lib.check(lib.esr_prep_input(x.data_ptr(), Bn, nz, h, w, SF, m, ws.lr.data_ptr() if first else None,
+                                      ws.first.data_ptr() if first else None, ws.first_cp, ws.first_lr_off, zlr,
+                                      zlr_cp, len(grp), zhr, zhr_cp, 2 if (nz and first) else 0, int(x3), stream),
+                   'esr_prep_input')
     prof = _PROFILE
     tagp = 'x3_' if x3 else ''
 
@@ -286,22 +306,23 @@ def _forward(net, x, cem, precision):
             ev.record()
 
     nl = 3 if latent else 0  # reference latent channels concatenated into a conv input (FLOP accounting)
-    # conv_first -> P0.x and fea
+    # conv_first -> (RRDB 0 input).x and fea
     conv(ws.first, H, W, ws.first_cp, ws.first_cp, pk.first, 64,
-         _conv_out(P0, cp, zc, H, W, False, out2=ws.fea, out2_cp=64, out2_coff=0), 3 + nl)
+         _conv_out(rrdb_bufs(0)[0], cp, zc, H, W, False, out2=ws.fea, out2_cp=64, out2_coff=0), 3 + nl)
     # nb RRDBs
-    chain = ((P0, P1), (P1, P2), (P2, P0))
     for k in range(net.nb):
-        for r, (pin, pout) in enumerate(chain):
+        xin, b1, b2, xout = rrdb_bufs(k)
+        for r, (pin, pout) in enumerate(((xin, b1), (b1, b2), (b2, xout))):
             convs = pk.rdb[3 * k + r]
             for i in range(4):
                 coff = zc + 64 + 32 * i
                 conv(pin, H, W, cp, coff, convs[i], 32, _conv_out(pin, cp, coff, H, W, True), nl + 64 + 32 * i)
             o = _conv_out(pout, cp, zc, H, W, False, r1=pin, r1_cp=cp, r1_coff=zc, s1=0.2,
-                          r2=P0 if r == 2 else None, r2_cp=cp, r2_coff=zc, s2=0.2)
+                          r2=xin if r == 2 else None, r2_cp=cp, r2_coff=zc, s2=0.2)
             conv(pin, H, W, cp, zc + 192, convs[4], 64, o, nl + 192)
     # LR_conv + trunk skip
-    conv(P0, H, W, cp, zc + 64, pk.lr_conv, 64, _conv_out(ws.U0, 64, 0, H, W, False, r1=ws.fea, r1_cp=64, s1=1.0),
+    trunk = rrdb_bufs(net.nb - 1)[3] if net.nb > 0 else rrdb_bufs(0)[0]
+    conv(trunk, H, W, cp, zc + 64, pk.lr_conv, 64, _conv_out(ws.U0, 64, 0, H, W, False, r1=ws.fea, r1_cp=64, s1=1.0),
          nl + 64)
     # two nearest-×2 upconvs, four phases each
     for (src, sh, sw, dst, dcp, dcoff), phw in zip(

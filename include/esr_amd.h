@@ -124,6 +124,44 @@ int esr_upconv2x_phase_fwd_x3(const void *in, int32_t B, int32_t H, int32_t W, i
                               const void *w_packed, const float *bias, float w_scale, int32_t cout, int32_t py,
                               int32_t px, const esr_conv_out *o, int32_t *overflow, esr_stream_t stream);
 
+/* ---- training / Z-optimisation backward (esr_train.hip) ------------------------------------------------------------
+ * The data gradient of every conv is esr_conv3x3_fwd run with rot180, in/out-swapped packed weights (host-side
+ * repacking), i.e. the backward of conv_block (block.py:129-156) for loss.backward() in
+ * SRRaGANModel.optimize_parameters (SRRaGAN_model.py:529) and Z_optimizer.optimize (Z_optimization.py:633). */
+
+/* Weight + bias gradient of a 3×3 zero-padded conv on the H×W output grid:
+ *   partial[s][tap][ci][co] = Σ_{pixels of split s} in[p + tap][ci] · dout[p][co],   partial[s][9*cin_pad*cout_pad + co]
+ *   = Σ dout[p][co] (bias), cin_pad = 32·ceil(cin/32), cout_pad = 32·ceil(cout/32).
+ * in: padded NHWC fp32, channels [0, cin) (cin % 4 == 0); with up2 = 1 the conv input is the nearest-×2 upsampling of
+ * an (H/2)×(W/2) `in` grid (the upconv of block.py:294-301).  dout: padded NHWC fp32 on the H×W grid, channels
+ * [dout_coff, dout_coff + cout), cout <= 64.  Deterministic: reduce the `splits` partials with esr_wgrad_reduce. */
+int esr_conv3x3_wgrad(const float *in, int32_t in_cp, int32_t cin, int32_t up2, const float *dout, int32_t dout_cp,
+                      int32_t dout_coff, int32_t cout, int32_t B, int32_t H, int32_t W, int32_t splits, float *partial,
+                      esr_stream_t stream);
+/* out[i] = scale · Σ_s partial[s·n + i], fixed summation order. */
+int esr_wgrad_reduce(const float *partial, int32_t splits, int64_t n, float scale, float *out, esr_stream_t stream);
+/* LeakyReLU(0.2) backward from the saved output y: d *= (y > 0 ? 1 : 0.2) on a C-channel slice. */
+int esr_lrelu_bwd(float *d, int32_t d_cp, int32_t d_coff, const float *y, int32_t y_cp, int32_t y_coff, int32_t C,
+                  int32_t B, int32_t H, int32_t W, esr_stream_t stream);
+/* out = a·x1 + b·x2 (x2 may be NULL) on C-channel slices of padded NHWC buffers (in place allowed, pointwise). */
+int esr_axpby(float *out, int32_t o_cp, int32_t o_coff, float a, const float *x1, int32_t x1_cp, int32_t x1_coff,
+              float b, const float *x2, int32_t x2_cp, int32_t x2_coff, int32_t C, int32_t B, int32_t H, int32_t W,
+              esr_stream_t stream);
+/* Adjoint of nearest ×2 upsampling: out (H×W grid) = Σ over each 2×2 block of src (2H×2W grid). */
+int esr_sum2x2(float *out, int32_t o_cp, int32_t o_coff, const float *src, int32_t s_cp, int32_t s_coff, int32_t C,
+               int32_t B, int32_t H, int32_t W, esr_stream_t stream);
+/* NCHW [B][C][H][W] <-> padded NHWC channel slice (to_nchw = 0: src -> dst; 1: dst -> src). */
+int esr_nchw_to_padded(const float *src, int32_t C, int32_t B, int32_t H, int32_t W, float *dst, int32_t d_cp,
+                       int32_t d_coff, int32_t to_nchw, esr_stream_t stream);
+/* Exact adjoint of a replicate-padded strided depthwise stencil F(x)[o] = Σ_u w[u] x[clamp(s·o + c + u - K/2)]
+ * (2-D, same s/c per dimension; x is Ly×Lx, g = F's output shape Oy×Ox, `planes` = B·C images):
+ *   out[i][j] (+)= alpha · F^T(g)[os·i + oc][os·j + oc]
+ * Used with (s, c, os, oc) = (1, 0, sf, ph) for Upscale_OP (adjoint sampled on the stuffed phase), (1, 0, 1, 0) for
+ * Conv_LR_with_Inv_hTh_OP and (sf, ph, 1, 0) for DownscaleOP (CEMnet.py:149-162). */
+int esr_cem_adjoint(const float *g, int32_t planes, int32_t Oy, int32_t Ox, const float *w, int32_t K, int32_t s,
+                    int32_t c, int32_t Ly, int32_t Lx, int32_t os, int32_t oc, float alpha, int32_t accumulate,
+                    float *out, esr_stream_t stream);
+
 /* Library / ABI version (bumped on any signature change). */
 int esr_abi_version(void);
 

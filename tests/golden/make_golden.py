@@ -172,6 +172,43 @@ def rrdb_fixture(arch, CEMnet, name, nb, latent, lr_shape, seed, w_scale, cem_mo
                                                           sum(int(np.prod(s)) for _, s in named_shapes)))
 
 
+GRAD_KEYS = ('model.0.weight', 'model.0.bias', 'model.1.sub.0.RDB1.convs.0.0.weight', 'model.1.sub.0.RDB1.convs.4.0.weight',
+             'model.1.sub.0.RDB3.convs.2.0.weight', 'model.1.sub.0.RDB3.convs.4.0.bias', 'model.1.sub.1.weight',
+             'model.2.1.weight', 'model.3.1.bias', 'model.4.weight', 'model.6.weight', 'model.6.bias')
+
+
+def grad_fixture(arch, CEMnet, name, latent, lr_shape, seed, w_scale):
+    """Training-step gradients (SRRaGAN_model.py:347-348, 529): CEM-wrapped RRDBNet(nb=1) in train mode, loss =
+    Σ out·R with a seeded R; dumps the gradients of GRAD_KEYS (prefixed 'generated_image_model.')."""
+    nl = 3 if latent else 0
+    net = arch.RRDBNet(in_nc=3, out_nc=3, nf=64, nb=1, gc=32, upscale=4, norm_type=None, act_type='leakyrelu',
+                       mode='CNA', upsample_mode='upconv',
+                       latent_input='all_layers_HR_downscaled' if latent else None, num_latent_channels=nl)
+    model = CEMnet.CEMnet(CEMnet.Get_CEM_Config(4)).WrapArchitecture_PyTorch(net)
+    sd = model.state_dict()
+    named_shapes = [(k, tuple(v.shape)) for k, v in sd.items()]
+    params = seeded_params(named_shapes, seed, w_scale=w_scale)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=False)
+    model.train(True)
+    B, _, h, w = lr_shape
+    lr, z = seeded_inputs(seed + 1, lr_shape, (B, 3, 4 * h, 4 * w) if latent else None, z_mode='image')
+    x = torch.from_numpy(lr)
+    if latent:
+        x = torch.cat([torch.from_numpy(z).contiguous().view(B, 48, h, w), x], 1)
+    out = model(x)
+    R = torch.from_numpy(np.random.default_rng(seed + 2).standard_normal(tuple(out.shape)).astype(np.float32))
+    (out * R).sum().backward()
+    named = dict(model.named_parameters())
+    d = dict(lr=lr, R=R.numpy(), out=out.detach().numpy(), latent=np.int64(latent), seed=np.int64(seed),
+             w_scale=np.float64(w_scale), keys=np.str_(json.dumps(named_shapes)), nb=np.int64(1))
+    if z is not None:
+        d['z'] = z
+    for k in GRAD_KEYS:
+        d['grad:' + k] = named['generated_image_model.' + k].grad.numpy()
+    np.savez_compressed(os.path.join(HERE, 'grad_%s.npz' % name), **d)
+    print('grad_%s: %d grads, |g conv_first| %.3e' % (name, len(GRAD_KEYS), np.abs(d['grad:model.0.weight']).mean()))
+
+
 def main():
     install_shims()
     import CEM.CEMnet as CEMnet
@@ -191,6 +228,9 @@ def main():
     rrdb_fixture(arch, CEMnet, 'plain_nb23', 23, False, (1, 3, 16, 16), 9, 0.1)
     rrdb_fixture(arch, CEMnet, 'latent_nb23_cem_eval', 23, True, (1, 3, 16, 16), 10, 0.1, cem_mode='eval')
     rrdb_fixture(arch, CEMnet, 'plain_nb23_s1_cem_eval', 23, False, (1, 3, 16, 16), 11, 1.0, cem_mode='eval')
+    # --- training-step gradients (bicubic CEM, train mode) ---
+    grad_fixture(arch, CEMnet, 'plain_nb1', False, (2, 3, 12, 16), 13, 0.5)
+    grad_fixture(arch, CEMnet, 'latent_nb1', True, (2, 3, 12, 12), 14, 0.5)
     # --- learned kernel last: imresize.kernels is process-global and sticky (imresize_CEM.py:9,23-42) ---
     k = synthetic_learned_kernel()
     cem_fixture(CEMnet, 'learned13', k)

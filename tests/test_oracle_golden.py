@@ -62,3 +62,17 @@ def test_bilinear_down4_matches_interpolate():
     z = torch.rand(2, 3, 32, 24) * 2 - 1
     ref = torch.nn.functional.interpolate(z, scale_factor=0.25, mode='bilinear', align_corners=False)
     assert torch.allclose(O.bilinear_down4(z), ref, rtol=0, atol=1e-6)
+
+
+@pytest.mark.parametrize('name', golden_names('grad_'))
+def test_oracle_training_gradients(name):
+    """Autograd through the oracle's CEM + RRDBNet (train mode) reproduces the reference's training gradients."""
+    d = golden(name)
+    _, params = fixture_params(d)
+    P = {k: v.requires_grad_(True) for k, v in O.strip_prefix(params).items()}
+    latent = bool(int(d['latent']))
+    out = O.sr_forward(fixture_input(d), P, int(d['nb']), latent, O.cem_design(4), pre_pad=False)
+    assert normwise_rel(out.detach().numpy(), d['out']) < 1e-5
+    (out * torch.from_numpy(d['R'])).sum().backward()
+    for k in [f[len('grad:'):] for f in d.files if f.startswith('grad:')]:
+        assert normwise_rel(P[k].grad.numpy(), d['grad:' + k]) < 1e-5, k
