@@ -1,0 +1,107 @@
+#!/usr/bin/env python3
+"""Training-step benchmark (BASELINE.json configs 3 and 4): one SRRaGANModel.optimize_parameters() with a D step and
+a G step, RRDB-23 (latent all_layers/HR_downscaled) + CEM generator on the HIP path (forward + hand-written fp32
+backward), Discriminator_VGG_128_(nb=6) + WGAN-GP (gp 10) + range loss (5000), Adam on both.
+
+    python bench_train.py [--gpus N --steps K --warmup W]     (N>1 via torch.distributed.run: DP over RCCL, B per rank)
+
+One JSON line on rank 0: value = HR Mpixels/s of training images (all ranks), step time = max over ranks.  The VGG
+feature loss of the config-3 wording is off in the shipped config (feature_weight 0) and broken in the reference.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, 'explorable-super-resolution_old_amd'))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def make_opt(args):
+    patch = 4 * args.lr_size
+    return {
+        'is_train': True, 'scale': 4, 'gpu_ids': [0], 'range': [0, 1],
+        'datasets': {'train': {'patch_size': patch, 'batch_size': args.batch}},
+        'network_G': {'which_model_G': 'RRDB_net', 'CEM_arch': 1, 'latent_input': 'all_layers' if args.latent else None,
+                      'latent_input_domain': 'HR_downscaled', 'latent_channels': 'SVDinNormedOut_structure_tensor',
+                      'norm_type': None, 'mode': 'CNA', 'nf': 64, 'nb': args.nb, 'in_nc': 3, 'out_nc': 3, 'gc': 32},
+        'network_D': {'which_model_D': 'discriminator_vgg_128', 'relativistic': 0, 'decomposed_input': 0,
+                      'norm_type': 'batch', 'act_type': 'leakyrelu', 'mode': 'CNA', 'n_layers': 6, 'nf': 64,
+                      'in_nc': 3},
+        'train': {'lr_G': 1e-5, 'weight_decay_G': 0, 'beta1_G': 0.9, 'lr_D': 1e-5, 'weight_decay_D': 0,
+                  'beta1_D': 0.9, 'lr_steps': [50000], 'lr_gamma': 0.5, 'gan_type': 'wgan-gp', 'gan_weight': 1,
+                  'gp_weigth': 10, 'range_weight': 5000, 'D_update_ratio': 1, 'D_verification': None,
+                  'D_init_iters': 0, 'pixel_weight': 0, 'feature_weight': 0, 'latent_weight': 0,
+                  'optimalZ_loss_weight': 0},
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--batch', type=int, default=16)
+    ap.add_argument('--lr-size', type=int, default=96)
+    ap.add_argument('--nb', type=int, default=23)
+    ap.add_argument('--no-latent', dest='latent', action='store_false')
+    args = ap.parse_args()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=dev)
+    from esr_amd.SRRaGAN_model import SRRaGANModel
+    torch.manual_seed(1000 + rank)
+    model = SRRaGANModel(make_opt(args), device=dev)
+    if world > 1:  # identical initial weights on every rank (DataParallel replicates rank 0's)
+        for p in list(model.netG.parameters()) + list(model.netD.parameters()):
+            dist.broadcast(p.data, 0)
+    g = torch.Generator(device='cpu').manual_seed(7 + rank)
+    hr = 4 * args.lr_size
+    data = {'LR': torch.rand(args.batch, 3, args.lr_size, args.lr_size, generator=g).to(dev),
+            'HR': torch.rand(args.batch, 3, hr, hr, generator=g).to(dev)}
+    gsteps = 0
+    for _ in range(args.warmup):
+        model.feed_data(data)
+        model.optimize_parameters()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        model.feed_data(data)
+        model.optimize_parameters()
+        gsteps += int(model.generator_step)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    value = world * args.batch * hr * hr * args.steps / dt / 1e6
+    rec = {'metric': 'training HR Mpixels/s (RRDB-23 + CEM G fwd+bwd, VGG128_ D + WGAN-GP, Adam)', 'value': round(value, 4),
+           'unit': 'HR Mpixels/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+           'ms_per_step': round(dt / args.steps * 1e3, 2), 'higher_is_better': True, 'scaling': 'weak',
+           'dtype': 'f32', 'data': 'synthetic', 'generator_steps_in_timed_region': gsteps,
+           'config': {'workload': 'BASELINE config %s: batch %d/GPU of %dx%d LR crops (%dx%d HR, D on %dx%d after CEM '
+                                  'unpad), nb=%d, latent=%s' % ('4' if world > 1 else '3', args.batch, args.lr_size,
+                                                                 args.lr_size, hr, hr, hr - 80, hr - 80, args.nb,
+                                                                 args.latent),
+                      'global_batch': world * args.batch, 'parallelism': 'dp%d (RCCL all-reduce of G/D grads)' % world},
+           'last_losses': {k: v[-1][1] for k, v in model.log_dict.items() if v}}
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

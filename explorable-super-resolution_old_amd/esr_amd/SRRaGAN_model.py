@@ -1,0 +1,345 @@
+"""SRRaGANModel — counterpart of reference codes/models/SRRaGAN_model.py (the north_star's "SRGAN_model").
+
+Keeps the interface the reference's drivers use — `feed_data`, `ConcatLatent`, `GetLatent`, `optimize_parameters`,
+`test`, `get_current_visuals`, attributes `netG`, `netD`, `CEM_net`, `fake_H`, `var_L`, `var_H`, `model_input`,
+`num_latent_channels`, `Z_size_factor`, `log_dict`, `step` — for the configuration the shipped JSONs select:
+CEM_arch, latent `all_layers`/`HR_downscaled` (or no latent), WGAN-GP (non-relativistic), range loss, D_verification
+'past'/None, gradient accumulation.  Options the shipped configs switch off (VGG feature loss — broken in the
+reference, pixel/high-pass/shift-invariant/optimal-Z/latent losses, encoder, decomposed D input) raise
+NotImplementedError instead of silently differing.  Logging to files, checkpoint rotation and plotting are out of
+scope.
+
+Multi-GPU: one process per GPU (torch.distributed, RCCL).  The reference's nn.DataParallel computes every loss on the
+gathered global batch; with equal per-rank batches the average of per-rank gradients equals that gradient, so after
+each backward the G / D gradients are all-reduced (average, one flat bucket per network).  BatchNorm statistics stay
+per-replica (as DataParallel's) and the running buffers are broadcast from rank 0 (DataParallel keeps replica 0's).
+The per-image D statistics that gate the generator step are all-reduced so that every rank takes the same branch.
+"""
+import math
+from collections import OrderedDict
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import CEMnet
+from . import networks
+from .loss import CreateRangeLoss, GANLoss, GradientPenaltyLoss
+
+
+def Latent_channels_desc_2_num_channels(desc):
+    """loss.py:14-21."""
+    if isinstance(desc, int):
+        return desc
+    if desc == 'STD_1dir':
+        return 2
+    if desc == 'STD_directional' or 'structure_tensor' in desc:
+        return 3
+    raise ValueError(desc)
+
+
+def SVD_2_LatentZ(SVD_values, max_lambda=1):
+    """utils/util.py:137-143: (lambda0, lambda1, theta) -> structure-tensor latent channels."""
+    l0, l1, th = SVD_values[:, 0, ...], SVD_values[:, 1, ...], SVD_values[:, -1, ...]
+    s, c = torch.sin(th) ** 2, torch.cos(th) ** 2
+    return torch.stack([2 * max_lambda * (l1 * s + l0 * c) - max_lambda,
+                        2 * max_lambda * (l0 * s + l1 * c) - max_lambda,
+                        2 * (l0 - l1) * torch.sin(th) * torch.cos(th)], 1)
+
+
+def _world():
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
+def _allreduce_grads(params):
+    """Average the .grad of `params` over ranks in one flat bucket (RCCL all-reduce over xGMI)."""
+    if _world() == 1:
+        return
+    grads = [p.grad for p in params if p.grad is not None]
+    if not grads:
+        return
+    flat = torch.cat([g.reshape(-1) for g in grads])
+    dist.all_reduce(flat)
+    flat /= _world()
+    o = 0
+    for g in grads:
+        n = g.numel()
+        g.copy_(flat[o:o + n].view_as(g))
+        o += n
+
+
+def _broadcast_buffers(module):
+    if _world() == 1:
+        return
+    for b in module.buffers():
+        dist.broadcast(b, 0)
+
+
+class SRRaGANModel:
+    def __init__(self, opt, accumulation_steps_per_batch=1, kernel=None, device=None):
+        self.opt = opt
+        self.is_train = bool(opt['is_train'])
+        self.device = device if device is not None else torch.device('cuda', torch.cuda.current_device())
+        opt_G = opt['network_G']
+        li = opt_G.get('latent_input')
+        self.latent_input = li if li not in (None, 'None') else None
+        self.latent_input_domain = opt_G.get('latent_input_domain')
+        self.num_latent_channels = Latent_channels_desc_2_num_channels(opt_G.get('latent_channels', 0) or 0) \
+            if self.latent_input is not None else 0
+        if self.latent_input is not None:
+            self.Z_size_factor = opt['scale'] if 'HR' in self.latent_input_domain else 1
+        self.CEM_arch = bool(opt_G.get('CEM_arch'))
+        self.step = 0
+        self.generator_step = False
+        self.CEM_net = None
+        if self.CEM_arch or self.latent_input is not None:
+            conf = CEMnet.Get_CEM_Config(opt['scale'])
+            conf.input_range = np.array(opt.get('range', [0, 1]))
+            test_opt = opt.get('test') or {}
+            if test_opt.get('kernel') == 'estimated':
+                conf.lower_magnitude_bound = 0.1
+            k = kernel if kernel is not None else test_opt.get('kernel')
+            if isinstance(k, str) and k == 'estimated':
+                k = None
+            self.CEM_net = CEMnet.CEMnet(conf, upscale_kernel=k)
+            if not self.CEM_arch:
+                self.CEM_net.WrapArchitecture_PyTorch(only_padders=True)
+        self.netG = networks.define_G(opt, CEM=self.CEM_net, num_latent_channels=self.num_latent_channels)
+        self.netG.to(self.device)
+        keys = ['l_g_range', 'l_g_gan', 'l_d_real', 'l_d_fake', 'l_d_real_fake', 'D_real', 'D_fake', 'D_logits_diff',
+                'D_update_ratio', 'Correctly_distinguished', 'l_d_gp']
+        self.log_dict = OrderedDict((k, []) for k in keys)
+        if self.is_train:
+            self._init_training(opt, accumulation_steps_per_batch)
+
+    # ------------------------------------------------------------------------------------------------------------------
+    def _init_training(self, opt, accumulation_steps_per_batch):
+        t = opt['train']
+        for k in ('pixel_weight', 'feature_weight', 'latent_weight', 'optimalZ_loss_weight', 'highpass_weight',
+                  'shift_invariant_weight'):
+            if t.get(k):
+                raise NotImplementedError('%s > 0 is not part of the built training path (shipped configs use 0)' % k)
+        if opt['network_D'].get('decomposed_input') or opt['network_D'].get('relativistic') not in (0, None, False):
+            if opt['network_D'].get('decomposed_input'):
+                raise NotImplementedError('decomposed D input')
+        self.relativistic_D = bool(opt['network_D'].get('relativistic'))
+        self.D_verification = t.get('D_verification')
+        assert self.D_verification in ['current', 'past', None]
+        self.grad_accumulation_steps_G = t.get('grad_accumulation_steps_G', 1)
+        self.grad_accumulation_steps_D = t.get('grad_accumulation_steps_D', 1)
+        self.max_accumulation_steps = accumulation_steps_per_batch
+        self.l_gan_w = t['gan_weight']
+        self.D_exists = self.l_gan_w > 0
+        self.netG.train()
+        self.cri_range = CreateRangeLoss(opt.get('range', [0, 1])) if t.get('range_weight', 0) > 0 else None
+        self.l_range_w = t.get('range_weight', 0)
+        self.optimizers = []
+        gparams = [p for p in self.netG.parameters() if p.requires_grad]
+        self.optimizer_G = torch.optim.Adam(gparams, lr=t['lr_G'], weight_decay=t.get('weight_decay_G') or 0,
+                                            betas=(t['beta1_G'], 0.999))
+        self.optimizers.append(self.optimizer_G)
+        if self.D_exists:
+            self.netD = networks.define_D(opt, CEM=self.CEM_net).to(self.device)
+            self.netD.train()
+            self.cri_gan = GANLoss(t['gan_type'], 1.0, 0.0)
+            self.global_D_update_ratio = t.get('D_update_ratio') or 1
+            self.D_init_iters = t.get('D_init_iters') or 0
+            if t['gan_type'] == 'wgan-gp':
+                self.cri_gp = GradientPenaltyLoss(device=self.device)
+                self.l_gp_w = t['gp_weigth']
+            self.optimizer_D = torch.optim.Adam(self.netD.parameters(), lr=t['lr_D'],
+                                                weight_decay=t.get('weight_decay_D') or 0, betas=(t['beta1_D'], 0.999))
+            self.optimizers.append(self.optimizer_D)
+        else:
+            self.global_D_update_ratio, self.D_init_iters = 1, 0
+        self.schedulers = [torch.optim.lr_scheduler.MultiStepLR(o, t['lr_steps'], t['lr_gamma'])
+                           for o in self.optimizers]
+
+    # ------------------------------------------------------------------------------------------------------------------
+    def ConcatLatent(self, LR_image, latent_input):
+        """SRRaGAN_model.py:249-255: the HR latent is carried as a raw view into sf² LR-sized channels."""
+        if latent_input is not None:
+            if LR_image.size()[2:] != latent_input.size()[2:]:
+                latent_input = latent_input.contiguous().view([latent_input.size(0)] + [
+                    latent_input.size(1) * self.opt['scale'] ** 2] + list(LR_image.size()[2:]))
+            self.model_input = torch.cat([latent_input, LR_image], dim=1)
+        else:
+            self.model_input = 1 * LR_image
+
+    def GetLatent(self):
+        latent = 1 * self.model_input[:, :-3, ...]
+        if latent.size(1) != self.num_latent_channels:
+            latent = latent.view([latent.size(0)] + [self.num_latent_channels] +
+                                 [self.opt['scale'] * v for v in list(latent.size()[2:])])
+        return latent
+
+    def feed_data(self, data, need_HR=True):
+        """SRRaGAN_model.py:269-302."""
+        self.var_L = data['LR'].to(self.device)
+        cur_Z = None
+        if self.latent_input is not None:
+            B = self.var_L.size(0)
+            if 'Z' in data:
+                cur_Z = data['Z']
+            else:
+                lc = self.opt['network_G']['latent_channels']
+                cur_Z = torch.rand([B, self.num_latent_channels, 1, 1])
+                if lc in ['SVD_structure_tensor', 'SVDinNormedOut_structure_tensor']:
+                    cur_Z[:, -1, ...] = 2 * np.pi * cur_Z[:, -1, ...]
+                    cur_Z = SVD_2_LatentZ(cur_Z).detach()
+                else:
+                    cur_Z = 2 * cur_Z - 1
+            hw = [self.Z_size_factor * v for v in list(self.var_L.size()[2:])]
+            if isinstance(cur_Z, (int, float)) or (not torch.is_tensor(cur_Z) and np.ndim(cur_Z) < 4):
+                cur_Z = cur_Z * np.ones([1, self.num_latent_channels] + hw)
+            elif torch.is_tensor(cur_Z) and cur_Z.size(2) == 1:
+                cur_Z = cur_Z * torch.ones([1, 1] + hw)
+            if not torch.is_tensor(cur_Z):
+                cur_Z = torch.from_numpy(np.asarray(cur_Z, dtype=np.float32))
+            cur_Z = cur_Z.float().to(self.device)
+        self.ConcatLatent(LR_image=self.var_L, latent_input=cur_Z)
+        if need_HR:
+            self.var_H = data['HR'].to(self.device)
+            self.var_ref = (data['ref'] if 'ref' in data else data['HR']).to(self.device)
+
+    # ------------------------------------------------------------------------------------------------------------------
+    def _d_statistics(self, pred_real, pred_fake):
+        """Per-image D logit differences, summed over ranks (global-batch semantics of DataParallel)."""
+        diff = torch.mean(pred_real.detach() - pred_fake.detach(), dim=list(range(1, pred_real.dim())))
+        s = torch.stack([diff.sum(), (diff > 0).float().sum(), torch.tensor(float(diff.numel()), device=diff.device),
+                         pred_real.detach().mean(), pred_fake.detach().mean()])
+        if _world() > 1:
+            dist.all_reduce(s)
+            s[3:] /= _world()
+        return float(s[0] / s[2]), float(s[1] / s[2]), float(s[3]), float(s[4])
+
+    def optimize_parameters(self):
+        """SRRaGAN_model.py:307-575 for the shipped training configuration."""
+        t = self.opt['train']
+        self.gradient_step_num = self.step // self.max_accumulation_steps
+        first_acc_G = self.step % self.grad_accumulation_steps_G == 0
+        last_acc_G = self.step % self.grad_accumulation_steps_G == self.grad_accumulation_steps_G - 1
+        first_acc_D = self.step % self.grad_accumulation_steps_D == 0
+        last_acc_D = self.step % self.grad_accumulation_steps_D == self.grad_accumulation_steps_D - 1
+        if first_acc_D:
+            self.cur_D_update_ratio = self.global_D_update_ratio
+        G_grads_retained = first_acc_D or self.generator_step
+        for p in self.netG.parameters():
+            if not getattr(p, '_esr_frozen', False):
+                p.requires_grad = G_grads_retained
+        if self.CEM_net is not None:
+            self.var_H, self.var_ref = self.CEM_net.HR_unpadder(self.var_H), self.CEM_net.HR_unpadder(self.var_ref)
+        static_Z = self.GetLatent() if self.latent_input is not None else None
+        self.ConcatLatent(LR_image=self.var_L, latent_input=static_Z)
+        self.fake_H = self.netG(self.model_input)
+        if self.CEM_net is not None:
+            self.fake_H = self.CEM_net.HR_unpadder(self.fake_H)
+        # ---- D step ----
+        if not self.D_exists:
+            self.generator_step = self.gradient_step_num > 0
+        elif self.gradient_step_num % max(1, math.ceil(1 / self.cur_D_update_ratio)) == 0 and \
+                self.gradient_step_num > -self.D_init_iters:
+            for p in self.netD.parameters():
+                p.requires_grad = True
+            if first_acc_D:
+                self.optimizer_D.zero_grad()
+                self._d_logs = []
+            pred_d_real = self.netD(self.var_ref)
+            pred_d_fake = self.netD(self.fake_H.detach())
+            if self.relativistic_D:
+                l_d_real = self.cri_gan(pred_d_real - torch.mean(pred_d_fake), True)
+                l_d_fake = self.cri_gan(pred_d_fake - torch.mean(pred_d_real), False)
+            else:
+                l_d_real = 2 * self.cri_gan(pred_d_real, True)
+                l_d_fake = 2 * self.cri_gan(pred_d_fake, False)
+            l_d_total = (l_d_real + l_d_fake) / 2
+            l_d_gp = None
+            if t['gan_type'] == 'wgan-gp':
+                rp = torch.rand(self.var_ref.size(0), 1, 1, 1, device=self.device)
+                interp = rp * self.fake_H.detach() + (1 - rp) * self.var_ref
+                interp.requires_grad = True
+                l_d_gp = self.l_gp_w * self.cri_gp(interp, self.netD(interp))
+                l_d_total = l_d_total + l_d_gp
+            diff, correct, d_real, d_fake = self._d_statistics(pred_d_real, pred_d_fake)
+            self._d_logs.append((l_d_real.item(), l_d_fake.item(), d_real, d_fake, diff, correct))
+            if first_acc_D:
+                self.generator_step = (self.gradient_step_num % max(1, self.cur_D_update_ratio) == 0 and
+                                       self.gradient_step_num > self.D_init_iters)
+                self.generator_step = self.generator_step and self.step % self.grad_accumulation_steps_D >= \
+                    self.grad_accumulation_steps_D - self.grad_accumulation_steps_G
+                if self.generator_step and self.D_verification == 'past' and t.get('D_valid_Steps_4_G_update', 0) > 0:
+                    n = t['D_valid_Steps_4_G_update']
+                    self.generator_step = len(self.log_dict['D_logits_diff']) >= n and \
+                        all(v[1] > np.log(t['min_D_prob_ratio_4_G']) for v in self.log_dict['D_logits_diff'][-n:]) and \
+                        all(v[1] > t['min_mean_D_correct'] for v in self.log_dict['Correctly_distinguished'][-n:])
+            if self.D_verification == 'current' and self.generator_step:
+                self.generator_step = correct == 1.0 and diff > np.log(t['min_D_prob_ratio_4_G'])
+            if G_grads_retained and not self.generator_step:
+                self.fake_H = self.fake_H.detach()
+            (l_d_total / self.grad_accumulation_steps_D).backward(retain_graph=self.generator_step)
+            if last_acc_D:
+                _allreduce_grads(list(self.netD.parameters()))
+                self.optimizer_D.step()
+                _broadcast_buffers(self.netD)
+                a = np.mean(np.array(self._d_logs), axis=0)
+                g = self.gradient_step_num
+                for k, v in (('l_d_real', a[0]), ('l_d_fake', a[1]), ('l_d_real_fake', a[0] + a[1]), ('D_real', a[2]),
+                             ('D_fake', a[3]), ('D_logits_diff', a[4]), ('Correctly_distinguished', a[5]),
+                             ('D_update_ratio', self.cur_D_update_ratio)):
+                    self.log_dict[k].append((g, float(v)))
+                if l_d_gp is not None:
+                    self.log_dict['l_d_gp'].append((g, l_d_gp.item()))
+        # ---- G step ----
+        if self.generator_step:
+            if self.D_exists:
+                for p in self.netD.parameters():
+                    p.requires_grad = False
+            if first_acc_G:
+                self.optimizer_G.zero_grad()
+            l_g_total = 0
+            if self.cri_range is not None:
+                l_g_range = self.cri_range(self.fake_H)
+                l_g_total = l_g_total + self.l_range_w * l_g_range / self.grad_accumulation_steps_G
+            if self.D_exists:
+                pred_g_fake = self.netD(self.fake_H)
+                if self.relativistic_D:
+                    pred_d_real = self.netD(self.var_ref).detach()
+                    l_g_gan = self.l_gan_w * (self.cri_gan(pred_d_real - torch.mean(pred_g_fake), False) +
+                                              self.cri_gan(pred_g_fake - torch.mean(pred_d_real), True)) / 2
+                else:
+                    l_g_gan = self.l_gan_w * self.cri_gan(pred_g_fake, True)
+                l_g_total = l_g_total + l_g_gan / self.grad_accumulation_steps_G
+            l_g_total.backward()
+            if last_acc_G:
+                _allreduce_grads([p for p in self.netG.parameters() if p.requires_grad])
+                self.optimizer_G.step()
+                g = self.gradient_step_num
+                if self.cri_range is not None:
+                    self.log_dict['l_g_range'].append((g, l_g_range.item()))
+                if self.D_exists:
+                    self.log_dict['l_g_gan'].append((g, l_g_gan.item()))
+        self.step += 1
+
+    def update_learning_rate(self):
+        for s in self.schedulers:
+            s.step()
+
+    # ------------------------------------------------------------------------------------------------------------------
+    def test(self, prevent_grads_calc=True):
+        """SRRaGAN_model.py:577-584 (leaves the net in train mode afterwards, like the reference)."""
+        self.netG.eval()
+        if prevent_grads_calc:
+            with torch.no_grad():
+                self.fake_H = self.netG(self.model_input)
+        else:
+            self.fake_H = self.netG(self.model_input)
+        self.netG.train()
+
+    def get_current_visuals(self, need_HR=True, entire_batch=False):
+        out = OrderedDict()
+        sel = slice(None) if entire_batch else 0
+        out['LR'] = self.var_L.detach()[sel].float().cpu()
+        out['SR'] = self.fake_H.detach()[sel].float().cpu()
+        if need_HR:
+            out['HR'] = self.var_H.detach()[sel].float().cpu()
+        return out

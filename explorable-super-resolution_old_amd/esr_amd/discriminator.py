@@ -1,0 +1,55 @@
+"""Discriminator_VGG_128_ — counterpart of reference codes/models/modules/architecture.py:222-284.
+
+The patch ("pseudo-FC") VGG discriminator the shipped training config uses (network_D: n_layers 6, nf 64, batch norm,
+leakyrelu, CNA; train_esrgan_CEM.json).  As shipped, `define_D` builds `Discriminator_VGG_128` and passes `nb=`, which
+that class does not accept (TypeError, networks.py:115-120 vs architecture.py:183-184); the class that takes `nb` is
+this one — `define_D` here builds it (SURVEY.md §7 "training path is broken as shipped").  Same module tree, hence the
+same state_dict keys and order as the reference (tests/golden/disc_*.npz).
+
+This round the discriminator runs on PyTorch-ROCm (MIOpen convolutions, autograd incl. the WGAN-GP double backward);
+moving its dense 3×3/4×4/8×8 convolutions onto hand-written MFMA kernels is SURVEY.md §8(f) item 2.
+"""
+import torch.nn as nn
+
+LRELU = 0.2
+
+
+def _conv_block(in_nc, out_nc, k, stride=1, norm=True, act=True, zero_pad=True):
+    """conv_block(mode='CNA') of block.py:129-156 flattened the way `sequential` does (block.py:106-126)."""
+    pad = (k - 1) // 2 if zero_pad else 0  # get_valid_padding; pad_type=None means no padding at all
+    mods = [nn.Conv2d(in_nc, out_nc, kernel_size=k, stride=stride, padding=pad, bias=True)]
+    if norm:
+        mods.append(nn.BatchNorm2d(out_nc, affine=True))
+    if act:
+        mods.append(nn.LeakyReLU(LRELU, True))
+    return mods
+
+
+class Discriminator_VGG_128_(nn.Module):
+    def __init__(self, in_nc, base_nf, norm_type='batch', act_type='leakyrelu', mode='CNA', input_patch_size=128,
+                 num_2_strides=5, nb=10):
+        super().__init__()
+        if norm_type != 'batch' or act_type != 'leakyrelu' or mode != 'CNA':
+            raise NotImplementedError('Discriminator_VGG_128_ is built for the shipped batch/leakyrelu/CNA config')
+        assert num_2_strides <= 5
+        self.num_2_strides = num_2_strides
+        nf = base_nf
+        plan = [(in_nc, nf, 3, 1, False), (nf, nf, 4, 2, True), (nf, 2 * nf, 3, 1, True), (2 * nf, 2 * nf, 4, 2, True),
+                (2 * nf, 4 * nf, 3, 1, True), (4 * nf, 4 * nf, 4, 2, True), (4 * nf, 8 * nf, 3, 1, True),
+                (8 * nf, 8 * nf, 4, 2, True), (8 * nf, 8 * nf, 3, 1, True), (8 * nf, 8 * nf, 4, 2, True)]
+        strides_left = num_2_strides
+        mods = []
+        for i, (ci, co, k, s, norm) in enumerate(plan[:nb]):
+            if s == 2:
+                s = 2 if strides_left > 0 else 1
+                strides_left -= 1
+            mods += _conv_block(ci, co, k, s, norm=norm)
+        self.features = nn.Sequential(*mods)
+        self.last_FC_layers = False
+        nfeat = [m for m in self.features.children()][-2].num_features
+        self.classifier = nn.Sequential(nn.Sequential(*_conv_block(nfeat, min(100, nfeat), 8, zero_pad=False)),
+                                        nn.LeakyReLU(LRELU, False),
+                                        nn.Sequential(*_conv_block(min(100, nfeat), 1, 1)))
+
+    def forward(self, x):
+        return self.classifier(self.features(x))

@@ -36,6 +36,28 @@ def init_weights(net, init_type='kaiming', scale=1, std=0.02):
     net.apply(functools.partial(weights_init_kaiming, scale=scale))
 
 
+def define_D(opt, CEM=None):
+    """networks.py:105-127.  The shipped `discriminator_vgg_128` + `n_layers` combination builds
+    Discriminator_VGG_128_(nb=n_layers) (the reference's define_G passes nb= to the class without it: TypeError)."""
+    from .discriminator import Discriminator_VGG_128_
+    gpu_ids = opt['gpu_ids']
+    opt_net = opt['network_D']
+    if opt_net['which_model_D'] != 'discriminator_vgg_128':
+        raise NotImplementedError('Discriminator model [{:s}] not recognized'.format(opt_net['which_model_D']))
+    patch = opt['datasets']['train']['patch_size']
+    if CEM is not None:
+        patch -= 2 * int(CEM.invalidity_margins_HR)
+    kwargs = {'num_2_strides': opt_net['num_2_strides']} if 'num_2_strides' in opt_net else {}
+    netD = Discriminator_VGG_128_(in_nc=opt_net['in_nc'], base_nf=opt_net['nf'], norm_type=opt_net['norm_type'],
+                                  act_type=opt_net['act_type'], mode=opt_net['mode'], input_patch_size=patch,
+                                  nb=opt_net['n_layers'], **kwargs)
+    init_weights(netD, init_type='kaiming', scale=1)
+    if gpu_ids:
+        dev = torch.cuda.current_device()
+        netD = nn.DataParallel(netD.to(dev), device_ids=[dev])
+    return netD
+
+
 def define_G(opt, CEM=None, num_latent_channels=None):
     gpu_ids = opt['gpu_ids']
     opt_net = opt['network_G']

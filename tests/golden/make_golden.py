@@ -209,6 +209,50 @@ def grad_fixture(arch, CEMnet, name, latent, lr_shape, seed, w_scale):
     print('grad_%s: %d grads, |g conv_first| %.3e' % (name, len(GRAD_KEYS), np.abs(d['grad:model.0.weight']).mean()))
 
 
+def disc_fixture(arch, loss_mod, name, seed):
+    """Discriminator_VGG_128_ (architecture.py:222-284) with nb = n_layers = 6 as the shipped train config builds it
+    once define_D's TypeError is resolved, plus one WGAN-GP discriminator loss + gradients exactly as
+    optimize_parameters forms them (SRRaGAN_model.py:378-399, non-relativistic, loss.py:202-263)."""
+    torch.manual_seed(seed)
+    D = arch.Discriminator_VGG_128_(in_nc=3, base_nf=64, norm_type='batch', act_type='leakyrelu', mode='CNA',
+                                    input_patch_size=80, nb=6)
+    sd = D.state_dict()
+    named_shapes = [(k, tuple(v.shape)) for k, v in sd.items()]
+    params = seeded_params([(k, s) for k, s in named_shapes if 'running' not in k and 'num_batches' not in k],
+                           seed, w_scale=1.0)
+    D.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=False)
+    D.train()
+    rng = np.random.default_rng(seed + 1)
+    real = torch.from_numpy(rng.random((3, 3, 80, 72)).astype(np.float32))
+    fake = torch.from_numpy(rng.random((3, 3, 80, 72)).astype(np.float32))
+    rp = torch.from_numpy(rng.random((3, 1, 1, 1)).astype(np.float32))
+    cri_gan = loss_mod.GANLoss('wgan-gp', 1.0, 0.0)
+    cri_gp = loss_mod.GradientPenaltyLoss()
+    pred_real = D(real)
+    pred_fake = D(fake)
+    l_d_real = 2 * cri_gan(pred_real, True)
+    l_d_fake = 2 * cri_gan(pred_fake, False)
+    interp = rp * fake + (1 - rp) * real
+    interp.requires_grad = True
+    l_d_gp = 10 * cri_gp(interp, D(interp))
+    l_d_total = (l_d_real + l_d_fake) / 2 + l_d_gp
+    l_d_total.backward()
+    range_loss = loss_mod.CreateRangeLoss([0, 1])(torch.from_numpy((rng.random((2, 3, 8, 8)) * 1.6 - 0.3)
+                                                                   .astype(np.float32)))
+    d = dict(real=real.numpy(), fake=fake.numpy(), rp=rp.numpy(), pred_real=pred_real.detach().numpy(),
+             pred_fake=pred_fake.detach().numpy(), l_d_real=l_d_real.item(), l_d_fake=l_d_fake.item(),
+             l_d_gp=l_d_gp.item(), l_d_total=l_d_total.item(), range_loss=range_loss.item(), seed=np.int64(seed),
+             keys=np.str_(json.dumps(named_shapes)), range_seed=np.int64(seed + 1))
+    for k, p in D.named_parameters():
+        d['grad:' + k] = p.grad.numpy()
+    for k, v in D.state_dict().items():
+        if 'running' in k:
+            d['buf:' + k] = v.numpy()
+    np.savez_compressed(os.path.join(HERE, 'disc_%s.npz' % name), **d)
+    print('disc_%s: out %s, l_d_total %.5f (gp %.5f), %d params' % (name, pred_real.shape, l_d_total.item(),
+                                                                   l_d_gp.item(), len(named_shapes)))
+
+
 def main():
     install_shims()
     import CEM.CEMnet as CEMnet
@@ -228,6 +272,9 @@ def main():
     rrdb_fixture(arch, CEMnet, 'plain_nb23', 23, False, (1, 3, 16, 16), 9, 0.1)
     rrdb_fixture(arch, CEMnet, 'latent_nb23_cem_eval', 23, True, (1, 3, 16, 16), 10, 0.1, cem_mode='eval')
     rrdb_fixture(arch, CEMnet, 'plain_nb23_s1_cem_eval', 23, False, (1, 3, 16, 16), 11, 1.0, cem_mode='eval')
+    # --- discriminator + WGAN-GP / range losses ---
+    import models.modules.loss as loss_mod
+    disc_fixture(arch, loss_mod, 'vgg128_nb6', 15)
     # --- training-step gradients (bicubic CEM, train mode) ---
     grad_fixture(arch, CEMnet, 'plain_nb1', False, (2, 3, 12, 16), 13, 0.5)
     grad_fixture(arch, CEMnet, 'latent_nb1', True, (2, 3, 12, 12), 14, 0.5)

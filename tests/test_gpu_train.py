@@ -81,3 +81,36 @@ def test_training_step_is_deterministic(gpu_device):
         grads.append([p.grad.clone() for p in model.parameters() if p.requires_grad])
     for a, b in zip(*grads):
         assert torch.equal(a, b)
+
+
+def test_optimize_parameters_training_step(gpu_device):
+    """SRRaGANModel.optimize_parameters on the HIP generator: D step (WGAN-GP) every step, G step from step 1 on;
+    both networks move, losses are finite, the generator output keeps the reference shape contract."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location('bench_train', os.path.join(os.path.dirname(__file__), '..',
+                                                                              'bench_train.py'))
+    bt = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bt)
+    from esr_amd.SRRaGAN_model import SRRaGANModel
+
+    class A:
+        batch, lr_size, nb, latent = 2, 40, 1, True
+    torch.manual_seed(0)
+    model = SRRaGANModel(bt.make_opt(A), device=gpu_device)
+    g0 = [p.detach().clone() for p in model.netG.parameters() if p.requires_grad]
+    d0 = [p.detach().clone() for p in model.netD.parameters()]
+    data = {'LR': torch.rand(2, 3, 40, 40, device=gpu_device), 'HR': torch.rand(2, 3, 160, 160, device=gpu_device)}
+    steps = []
+    for _ in range(3):
+        model.feed_data(data)
+        model.optimize_parameters()
+        steps.append(model.generator_step)
+    assert steps == [False, True, True]
+    assert tuple(model.fake_H.shape) == (2, 3, 80, 80)
+    assert any(not torch.equal(a, b) for a, b in zip(g0, [p for p in model.netG.parameters() if p.requires_grad]))
+    assert any(not torch.equal(a, b) for a, b in zip(d0, model.netD.parameters()))
+    for k in ('l_d_real', 'l_d_fake', 'l_d_gp', 'l_g_gan', 'l_g_range'):
+        assert model.log_dict[k] and np.isfinite(model.log_dict[k][-1][1]), k
+    model.test()
+    assert tuple(model.fake_H.shape) == (2, 3, 160, 160)

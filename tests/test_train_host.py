@@ -1,0 +1,101 @@
+"""CPU tests of the training-step host side: discriminator layout + forward/GP/range losses vs the reference's golden
+vector, and the multi-process (gloo, world size 2) gradient / statistics reductions of SRRaGANModel."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import golden, normwise_rel
+
+from esr_amd.discriminator import Discriminator_VGG_128_
+from esr_amd import loss as L
+from esr_amd import SRRaGAN_model as M
+from oracle.recipe import seeded_params
+
+
+def _disc_from_fixture(d):
+    D = Discriminator_VGG_128_(in_nc=3, base_nf=64, norm_type='batch', act_type='leakyrelu', mode='CNA',
+                               input_patch_size=80, nb=6)
+    ref_keys = json.loads(str(d['keys']))
+    assert [(k, list(v.shape)) for k, v in D.state_dict().items()] == [(k, list(s)) for k, s in ref_keys]
+    params = seeded_params([(k, s) for k, s in ref_keys if 'running' not in k and 'num_batches' not in k],
+                           int(d['seed']), w_scale=1.0)
+    D.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=False)
+    return D.train()
+
+
+def test_discriminator_and_wgan_gp_losses_match_reference():
+    d = golden('disc_vgg128_nb6')
+    D = _disc_from_fixture(d)
+    real, fake, rp = (torch.from_numpy(d[k]) for k in ('real', 'fake', 'rp'))
+    cri_gan, cri_gp = L.GANLoss('wgan-gp'), L.GradientPenaltyLoss()
+    pred_real, pred_fake = D(real), D(fake)
+    assert normwise_rel(pred_real.detach(), d['pred_real']) < 1e-5
+    assert normwise_rel(pred_fake.detach(), d['pred_fake']) < 1e-5
+    l_d_real, l_d_fake = 2 * cri_gan(pred_real, True), 2 * cri_gan(pred_fake, False)
+    interp = rp * fake + (1 - rp) * real
+    interp.requires_grad = True
+    l_d_gp = 10 * cri_gp(interp, D(interp))
+    l_d_total = (l_d_real + l_d_fake) / 2 + l_d_gp
+    l_d_total.backward()
+    for k in ('l_d_real', 'l_d_fake', 'l_d_gp', 'l_d_total'):
+        assert abs(float(locals()[k]) - float(d[k])) <= 1e-5 * max(1.0, abs(float(d[k]))), k
+    for k, p in D.named_parameters():
+        assert normwise_rel(p.grad, d['grad:' + k]) < 1e-4, k
+    for k, v in D.state_dict().items():
+        if 'running' in k:
+            assert normwise_rel(v, d['buf:' + k]) < 1e-5, k
+
+
+def test_range_loss_matches_reference():
+    d = golden('disc_vgg128_nb6')
+    rng = np.random.default_rng(int(d['range_seed']))
+    for name in ('real', 'fake', 'rp'):  # advance the stream exactly as the generator did
+        rng.random(d[name].shape)
+    x = torch.from_numpy((rng.random((2, 3, 8, 8)) * 1.6 - 0.3).astype(np.float32))
+    assert abs(float(L.CreateRangeLoss([0, 1])(x)) - float(d['range_loss'])) < 1e-7
+
+
+def _dist_worker(rank, world, port, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        torch.manual_seed(rank)
+        p = [torch.nn.Parameter(torch.zeros(3, 4)), torch.nn.Parameter(torch.zeros(5))]
+        p[0].grad = torch.full((3, 4), float(rank + 1))
+        p[1].grad = torch.arange(5, dtype=torch.float32) * (rank + 1)
+        M._allreduce_grads(p)
+        m = M.SRRaGANModel.__new__(M.SRRaGANModel)
+        pred_real = torch.full((2, 1, 3, 3), 1.0 + rank)          # per-image diffs: rank 0: (+1,+1)
+        pred_fake = torch.tensor([0.0, 3.0 + rank]).view(2, 1, 1, 1).expand(2, 1, 3, 3)  # rank 1: (+2,-2)
+        diff, correct, d_real, d_fake = m._d_statistics(pred_real, pred_fake)
+        q.put((rank, p[0].grad.clone(), p[1].grad.clone(), diff, correct, d_real, d_fake))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ddp_gradient_average_and_consistent_statistics():
+    """World size 2 over gloo: grads are averaged over ranks, and the D statistics that decide generator_step are the
+    global-batch values on every rank (DataParallel semantics, SRRaGAN_model.py:400-431)."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = 29500 + (os.getpid() % 2000)
+    procs = [ctx.Process(target=_dist_worker, args=(r, 2, port, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda t: t[0])
+    for pr in procs:
+        pr.join(60)
+        assert pr.exitcode == 0
+    for r in res:
+        assert torch.equal(r[1], torch.full((3, 4), 1.5))
+        assert torch.allclose(r[2], torch.arange(5, dtype=torch.float32) * 1.5)
+    # images: rank0 diffs (1-0, 1-3) = (1,-2); rank1 (2-0, 2-4) = (2,-2) -> mean -0.25, correct 0.5
+    for r in res:
+        assert abs(r[3] - (-0.25)) < 1e-6 and abs(r[4] - 0.5) < 1e-6
+    assert res[0][3:] == res[1][3:]
