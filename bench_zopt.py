@@ -1,0 +1,106 @@
+#!/usr/bin/env python3
+"""Z-optimisation benchmark (BASELINE.json config 5): CEM-wrapped latent RRDB-23 with a learned (non-bicubic) 13×13
+blur kernel, batch 8 of 128×128 LR, eval mode (CEM pre-pad), Z_optimizer('max_STD') iterations — each one a
+generator forward with retained activations + the HIP input-gradient sweep to Z + Adam on Z.
+
+    python bench_zopt.py [--gpus N --steps K --warmup W]      (N>1 via torch.distributed.run: images sharded)
+
+value = HR Mpixels/s of delivered (cropped) images per Z iteration summed over ranks; step = one Z iteration.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, 'explorable-super-resolution_old_amd'))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def learned_kernel(size=13, sigma=(1.6, 2.6), theta=np.pi / 6):
+    """Synthetic anisotropic Gaussian standing in for a KernelGAN estimate (no dataset / network here)."""
+    r = np.arange(size) - (size - 1) / 2
+    X, Y = np.meshgrid(r, r)
+    c, s = np.cos(theta), np.sin(theta)
+    u, v = c * X + s * Y, -s * X + c * Y
+    k = np.exp(-0.5 * ((u / sigma[0]) ** 2 + (v / sigma[1]) ** 2))
+    return k / k.sum()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--batch', type=int, default=8)
+    ap.add_argument('--lr-size', type=int, default=128)
+    ap.add_argument('--nb', type=int, default=23)
+    ap.add_argument('--objective', default='max_STD')
+    args = ap.parse_args()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=dev)
+    from esr_amd.SRRaGAN_model import SRRaGANModel
+    from esr_amd.Z_optimization import Z_optimizer
+    from esr_amd import networks
+    opt = {'is_train': False, 'scale': 4, 'gpu_ids': [0], 'range': [0, 1],
+           'network_G': {'which_model_G': 'RRDB_net', 'CEM_arch': 1, 'latent_input': 'all_layers',
+                         'latent_input_domain': 'HR_downscaled', 'latent_channels': 'SVDinNormedOut_structure_tensor',
+                         'norm_type': None, 'mode': 'CNA', 'nf': 64, 'nb': args.nb, 'in_nc': 3, 'out_nc': 3,
+                         'gc': 32}}
+    torch.manual_seed(1234)  # same generator weights on every rank
+    model = SRRaGANModel(opt, kernel=learned_kernel(), device=dev)
+    networks.init_weights(model.netG.module, scale=0.1)
+    g = torch.Generator().manual_seed(99 + rank)
+    B, h = args.batch, args.lr_size
+    data = {'LR': torch.rand(B, 3, h, h, generator=g).to(dev),
+            'Z': (torch.rand(B, 3, 4 * h, 4 * h, generator=g) * 2 - 1).to(dev)}
+    model.feed_data(data, need_HR=False)
+    model.test()
+    model.netG.eval()
+    cem = model.netG.module
+    zo = Z_optimizer(args.objective, [4 * h, 4 * h], model, 1.0, args.warmup, data=data, initial_LR=0.01,
+                     batch_size=B)
+    zo.optimize()  # warmup iterations (workspace allocation, weight packing)
+    zo.max_iters = args.steps
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    zo.optimize()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    m = int(cem.margins_LR)
+    flop_iter = 2 * 2 * 18316944 * (h + 2 * m) ** 2 * B  # fwd + input dgrad, SURVEY.md §8(d) latent MAC/LR-px
+    rec = {'metric': 'Z-optimisation HR Mpixels/s per iteration (latent RRDB-23 + learned-kernel CEM, fwd + dZ + Adam)',
+           'value': round(world * B * (4 * h) ** 2 * args.steps / dt / 1e6, 4), 'unit': 'HR Mpixels/s',
+           'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+           'ms_per_step': round(dt / args.steps * 1e3, 2), 'higher_is_better': True, 'scaling': 'weak',
+           'dtype': 'f32', 'data': 'synthetic',
+           'achieved_TFLOPs': round(flop_iter * args.steps / dt / 1e12, 2),
+           'config': {'workload': 'BASELINE config 5: batch %d/GPU of %dx%d LR, learned 13x13 kernel (CEM margins '
+                                  '%d/%d, G at %dx%d), objective %s, nb=%d' % (B, h, h, m, 4 * m, h + 2 * m,
+                                                                               h + 2 * m, args.objective, args.nb),
+                      'global_batch': world * B, 'parallelism': 'images sharded, no collective'},
+           'final_loss': zo.loss_values[-1]}
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -282,6 +282,38 @@ __global__ __launch_bounds__(NT) void cem_adjoint_kernel(AdjParams p) {
 
 }  // namespace
 
+// ---------------------------------------------------------------------------------------------------------------------
+// generator input adjoint (Z optimisation): replicate pre-pad adjoint + bilinear ↓sf adjoint
+// ---------------------------------------------------------------------------------------------------------------------
+__global__ void input_adjoint_kernel(const float *d_hr, int hr_cp, int hr_coff, const float *d_lr, int lr_cp,
+                                     int lr_coff, int sf, const float *d_pl, int C, int B, int Hp, int Wp, int M,
+                                     float *out) {
+    const int Ho = Hp - 2 * M, Wo = Wp - 2 * M;
+    const long long idx = (long long)blockIdx.x * NT + threadIdx.x;
+    if (idx >= (long long)B * C * Ho * Wo) return;
+    const int X = idx % Wo;
+    const int Y = (idx / Wo) % Ho;
+    const int c = (idx / ((long long)Wo * Ho)) % C;
+    const int b = idx / ((long long)Wo * Ho * C);
+    // padded positions that the replicate pad clamps onto (Y, X)
+    const int y0 = Y == 0 ? 0 : Y + M, y1 = Y == Ho - 1 ? Hp - 1 : Y + M;
+    const int x0 = X == 0 ? 0 : X + M, x1 = X == Wo - 1 ? Wp - 1 : X + M;
+    const int Hl = sf > 0 ? Hp / sf : 0, Wl = sf > 0 ? Wp / sf : 0;
+    float v = 0.f;
+    for (int yp = y0; yp <= y1; ++yp)
+        for (int xp = x0; xp <= x1; ++xp) {
+            if (d_hr) v += d_hr[(((long long)b * (Hp + 2) + yp + 1) * (Wp + 2) + xp + 1) * hr_cp + hr_coff + c];
+            if (d_pl) v += d_pl[(((long long)b * C + c) * Hp + yp) * Wp + xp];
+            if (d_lr) {  // bilinear ↓sf, align_corners=False, sf = 4: mean of the central 2×2 of each 4×4 block
+                const int ry = yp % sf, rx = xp % sf;
+                if ((ry == sf / 2 - 1 || ry == sf / 2) && (rx == sf / 2 - 1 || rx == sf / 2))
+                    v += 0.25f * d_lr[(((long long)b * (Hl + 2) + yp / sf + 1) * (Wl + 2) + xp / sf + 1) * lr_cp +
+                                      lr_coff + c];
+            }
+        }
+    out[idx] = v;
+}
+
 extern "C" int esr_conv3x3_wgrad(const float *in, int32_t in_cp, int32_t cin, int32_t up2, const float *dout,
                                  int32_t dout_cp, int32_t dout_coff, int32_t cout, int32_t B, int32_t H, int32_t W,
                                  int32_t splits, float *partial, esr_stream_t stream) {
@@ -352,5 +384,17 @@ extern "C" int esr_cem_adjoint(const float *g, int32_t planes, int32_t Oy, int32
     p.alpha = alpha; p.accumulate = accumulate;
     hipLaunchKernelGGL(cem_adjoint_kernel, dim3(nblocks((long long)planes * p.Ny * p.Nx)), dim3(NT), 0,
                        (hipStream_t)stream, p);
+    return launched();
+}
+
+extern "C" int esr_input_adjoint(const float *d_hr, int32_t hr_cp, int32_t hr_coff, const float *d_lr, int32_t lr_cp,
+                                 int32_t lr_coff, int32_t sf, const float *d_pl, int32_t C, int32_t B, int32_t Hp,
+                                 int32_t Wp, int32_t M, float *out, esr_stream_t stream) {
+    if (!out || C <= 0 || B <= 0 || M < 0 || Hp - 2 * M <= 0 || Wp - 2 * M <= 0) return ESR_EINVAL;
+    if (d_hr && hr_coff + C > hr_cp) return ESR_EINVAL;
+    if (d_lr && (sf != 4 || Hp % sf || Wp % sf || lr_coff + C > lr_cp)) return ESR_EINVAL;
+    const long long n = (long long)B * C * (Hp - 2 * M) * (Wp - 2 * M);
+    hipLaunchKernelGGL(input_adjoint_kernel, dim3(nblocks(n)), dim3(NT), 0, (hipStream_t)stream, d_hr, hr_cp, hr_coff,
+                       d_lr, lr_cp, lr_coff, sf, d_pl, C, B, Hp, Wp, M, out);
     return launched();
 }

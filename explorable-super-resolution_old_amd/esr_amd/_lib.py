@@ -8,7 +8,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('ESR_AMD_LIB', os.path.join(_HERE, 'libesr_amd.so'))
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 c_int = ctypes.c_int32
 c_float = ctypes.c_float
@@ -55,6 +55,8 @@ _SIGNATURES = {
     'esr_nchw_to_padded': [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p],
     'esr_cem_adjoint': [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                         c_float, c_int, c_void_p, c_void_p],
+    'esr_input_adjoint': [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int,
+                          c_int, c_void_p, c_void_p],
     'esr_abi_version': [],
 }
 EXPORTED = tuple(_SIGNATURES)

@@ -133,8 +133,58 @@ class _ConvW:
         return self._x3
 
 
+class GatherPlan:
+    """Every packed weight layout of a network as ONE gather from its flattened parameters.
+
+    The layouts (channel maps, padding, rot180/transpose for the data gradient, 0.2 residual scales) are pure
+    permutations with zero fill, so they are derived once by running the packing code on *index images* of the
+    parameters (float64 tensors holding 1-based flat positions; 0 = zero fill; +k·N selects the k-th scaled copy).
+    `refresh()` then rebuilds all packed tensors in place after an optimiser step with one cat + one index_select,
+    instead of thousands of small copies per step."""
+
+    def __init__(self, params, scales=(1.0,)):
+        self.params = list(params)
+        self.scales = tuple(scales)
+        self.N = sum(p.numel() for p in self.params)
+        self._img, off = {}, 1
+        for p in self.params:
+            self._img[id(p)] = torch.arange(off, off + p.numel(), dtype=torch.float64).view(p.shape)
+            off += p.numel()
+        self._parts = []
+        self.buf = self.idx = None
+
+    def w(self, p):
+        return self._img[id(p)]
+
+    def scaled(self, t, s):
+        k = self.scales.index(s)
+        return t if k == 0 else torch.where(t > 0, t + k * self.N, t)
+
+    def reg(self, t):
+        self._parts.append(t)
+        return t
+
+    def finalize(self, dev):
+        """Allocate the packed buffer; returns {id(index tensor): device view} for the caller to swap in."""
+        n = sum(t.numel() for t in self._parts)
+        self.buf = torch.empty(n, device=dev, dtype=torch.float32)
+        self.idx = torch.cat([t.reshape(-1) for t in self._parts]).to(torch.int64).to(dev)
+        views, o = {}, 0
+        for t in self._parts:
+            views[id(t)] = self.buf[o:o + t.numel()].view(t.shape)
+            o += t.numel()
+        self._parts = None
+        return views
+
+    def refresh(self):
+        flat = torch.cat([p.detach().reshape(-1) for p in self.params])
+        ext = torch.cat([flat.new_zeros(1)] + [flat * s if s != 1.0 else flat for s in self.scales])
+        torch.index_select(ext, 0, self.idx, out=self.buf)
+
+
 class _Packed:
-    """Packed weights of one generator, rebuilt when any parameter changes (data_ptr or in-place version)."""
+    """Packed weights of one generator: built once per parameter set (GatherPlan), refreshed in place when any
+    parameter changes (in-place version bump, e.g. an optimiser step or load_state_dict)."""
 
     def __init__(self, net, latent):
         def lr_map(n_feat):  # [Z(3) pad(5)] + features, reference order [Z, features]
@@ -142,39 +192,62 @@ class _Packed:
                 return list(range(n_feat))
             return [0, 1, 2] + [-1] * 5 + [3 + c for c in range(n_feat)]
 
+        self.net = net
+        plan = self.plan = GatherPlan(net.parameters())
+        pk = lambda conv, cmap, n_pad: plan.reg(pack_conv_weight(plan.w(conv.weight), cmap, n_pad))  # noqa: E731
         m = net.model
         first_map = ([0, 1, 2] + [-1] * 5 + [3, 4, 5] + [-1] * 5) if latent else ([0, 1, 2] + [-1] * 5)
-        self.first = _ConvW(pack_conv_weight(m[0].weight, first_map, 64), m[0].bias)
+        self.first = _ConvW(pk(m[0], first_map, 64), m[0].bias)
         self.rdb = []
         for k in range(net.nb):
             rr = m[1].sub[k]
             for rdb in (rr.RDB1, rr.RDB2, rr.RDB3):
-                self.rdb.append([_ConvW(pack_conv_weight(rdb.convs[i][0].weight, lr_map(64 + 32 * i),
-                                                         32 if i < 4 else 64), rdb.convs[i][0].bias)
-                                 for i in range(5)])
+                self.rdb.append([_ConvW(pk(rdb.convs[i][0], lr_map(64 + 32 * i), 32 if i < 4 else 64),
+                                        rdb.convs[i][0].bias) for i in range(5)])
         lrc = m[1].sub[net.nb]
-        self.lr_conv = _ConvW(pack_conv_weight(lrc.weight, lr_map(64), 64), lrc.bias)
+        self.lr_conv = _ConvW(pk(lrc, lr_map(64), 64), lrc.bias)
+        self.hr0 = _ConvW(pk(m[4], lr_map(64), 64), m[4].bias)
+        self.hr1 = _ConvW(pk(m[6], lr_map(64), 32), m[6].bias)
+        views = plan.finalize(net.model[0].weight.device)
+        self.planned = [self.first, self.lr_conv, self.hr0, self.hr1] + [cw for r in self.rdb for cw in r]
+        for cw in self.planned:
+            cw.f32 = views[id(cw.f32)]
+        self.up = None
+
+    def refresh(self):
+        self.plan.refresh()
+        for cw in self.planned:
+            cw._x3 = None
+        # the upsampler phases are sums of taps (not a permutation): packed directly, 8 small tensors
+        m = self.net.model
         self.up = []
         for j in (2, 3):
             c = m[j][1]
             self.up.append([_ConvW(pack_conv_weight(fold_upconv_phase(c.weight, py, px), list(range(64)), 64), c.bias)
                             for py in (0, 1) for px in (0, 1)])
-        self.hr0 = _ConvW(pack_conv_weight(m[4].weight, lr_map(64), 64), m[4].bias)
-        self.hr1 = _ConvW(pack_conv_weight(m[6].weight, lr_map(64), 32), m[6].bias)
 
 
 def _param_key(net):
     return tuple((p.data_ptr(), p._version) for p in net.parameters())
 
 
+def _struct_key(net):
+    return tuple((p.data_ptr(), tuple(p.shape)) for p in net.parameters())
+
+
 def _packed(net, latent):
-    key = (_param_key(net), latent)
+    skey, vkey = (_struct_key(net), latent), _param_key(net)
     c = net._esr_cache.get('packed')
-    if c is None or c[0] != key:
+    if c is None or c[0] != skey:
+        net._esr_cache.pop('packed', None)
         with torch.no_grad():
-            c = (key, _Packed(net, latent))
+            c = [skey, None, _Packed(net, latent)]
         net._esr_cache['packed'] = c
-    return c[1]
+    if c[1] != vkey:
+        with torch.no_grad():
+            c[2].refresh()
+        c[1] = vkey
+    return c[2]
 
 
 class _Workspace:
@@ -222,10 +295,9 @@ def generator_forward(net, x, cem=None):
     """RRDBNet.forward, optionally wrapped by CEM_PyTorch.forward (cem = the CEM_PyTorch module)."""
     global OVERFLOW_RERUNS
     _require_device(x, 'generator input')
-    if torch.is_grad_enabled() and x.requires_grad:
-        raise NotImplementedError('esr_amd: gradients w.r.t. the generator input (Z optimisation) are not built yet')
-    if torch.is_grad_enabled() and any(p.requires_grad for p in net.parameters()):
-        from . import train_engine  # training step: retained activations + HIP backward (exact fp32)
+    if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in net.parameters())):
+        # training step / Z optimisation: retained activations + HIP backward (exact fp32)
+        from . import train_engine
         return train_engine.generator_forward_train(net, x.contiguous(), cem)
     precision = getattr(net, 'esr_precision', None) or DEFAULT_PRECISION
     if precision not in PRECISIONS:

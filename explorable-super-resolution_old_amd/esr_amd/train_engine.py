@@ -54,9 +54,12 @@ class TrainWorkspace:
         self.dUp1 = _z(dev, B, 2 * H + 2, 2 * W + 2, 64)
         self.dHR = [_z(dev, B, 4 * H + 2, 4 * W + 2, 64) for _ in range(2)]
         self.dgen_p = _z(dev, B, 4 * H + 2, 4 * W + 2, 8)
+        # generator-input gradient (Z optimisation)
+        self.dZl = _z(dev, B, H + 2, W + 2, 8)
+        self.dFirst = _z(dev, B, H + 2, W + 2, self.first_cp)
+        self.dZh = _z(dev, B, 4 * H + 2, 4 * W + 2, 8) if latent else None
         self.wg_n_max = 9 * 224 * 64 + 64
         self.partial = torch.empty(WG_SPLITS_MAX * self.wg_n_max, device=dev, dtype=torch.float32)
-        self.dw = torch.empty(self.wg_n_max, device=dev, dtype=torch.float32)
 
 
 def _train_workspace(net, dev, B, H, W, latent):
@@ -73,29 +76,45 @@ def _train_workspace(net, dev, B, H, W, latent):
 # backward weight packing
 # ----------------------------------------------------------------------------------------------------------------------
 class _BwdConv:
-    """Backward data of one conv: the forward-buffer channel map, dgrad weight slices and the wgrad index map."""
+    """Backward data of one conv: the forward-buffer channel map, dgrad weight slices (GatherPlan index images until
+    finalised) and the location of its weight gradient in the flat wgrad buffer."""
 
-    def __init__(self, conv, cmap, scale=1.0, cin_k=None, dgrad_from=0):
-        w = conv.weight.detach()
+    def __init__(self, plan, conv, cmap, scale=1.0, cin_k=None, dgrad_from=0, in_width=0):
+        w = plan.w(conv.weight)
         cout, cin_ref = w.shape[:2]
         self.conv, self.cout, self.cmap, self.cin_buf = conv, cout, list(cmap), len(cmap)
         wf = w.flip(2, 3).transpose(0, 1)  # [Cin_ref][Cout][3][3]: rot180, swapped
         k = cin_k if cin_k is not None else cout  # channels of the gradient the dgrad reads (padded to 8)
         kmap = list(range(cout)) + [-1] * (k - cout)
+        def dslice(n0, nw):
+            rows = torch.tensor(self.cmap[n0:n0 + nw])
+            wt = torch.zeros(nw, cout, 3, 3, dtype=w.dtype)
+            wt[rows >= 0] = wf[rows[rows >= 0]]
+            return n0, nw, plan.reg(E.pack_conv_weight(plan.scaled(wt, scale), kmap, 32 if nw <= 32 else 64))
+
         self.slices = []  # (first buffer channel, width, packed weights)
         n0 = dgrad_from  # input-gradient channels below this (the latent Z slot) are not needed
         while n0 < self.cin_buf:
             nw = min(64, self.cin_buf - n0)
-            wt = torch.zeros(nw, cout, 3, 3, device=w.device, dtype=w.dtype)
-            for o in range(nw):
-                r = self.cmap[n0 + o]
-                if r >= 0:
-                    wt[o] = wf[r]
-            self.slices.append((n0, nw, E.pack_conv_weight(wt * scale, kmap, 32 if nw <= 32 else 64)))
+            self.slices.append(dslice(n0, nw))
             n0 += nw
-        dev = w.device
-        self.ref_to_buf = torch.tensor([self.cmap.index(r) for r in range(cin_ref)], device=dev, dtype=torch.long)
-        self.zero_bias = torch.zeros(64, device=dev)
+        # generator-input gradient (Z optimisation): the channels below dgrad_from (latent Z slot / conv_first input)
+        self.in_slices = [dslice(0, in_width)] if in_width else []
+        self.ref_to_buf = [self.cmap.index(r) for r in range(cin_ref)]
+        self.cin_pad = (self.cin_buf + 31) // 32 * 32
+        self.cout_pad = 32 if cout <= 32 else 64
+        self.wg_n = 9 * self.cin_pad * self.cout_pad + self.cout_pad
+        self.wg_off = 0
+
+    def grad_index(self):
+        """Positions in this conv's wgrad region ([9][cin_pad][cout_pad] + bias[cout_pad]) of the reference-layout
+        weight [Cout][Cin_ref][3][3] and bias [Cout]."""
+        co = torch.arange(self.cout).view(-1, 1, 1)
+        ci = torch.tensor(self.ref_to_buf).view(1, -1, 1)
+        tap = torch.arange(9).view(1, 1, 9)
+        wi = self.wg_off + (tap * self.cin_pad + ci) * self.cout_pad + co
+        bi = self.wg_off + 9 * self.cin_pad * self.cout_pad + torch.arange(self.cout)
+        return wi.reshape(-1), bi
 
 
 class _BwdPacked:
@@ -104,40 +123,65 @@ class _BwdPacked:
             return list(range(n)) if not latent else [0, 1, 2] + [-1] * 5 + [3 + c for c in range(n)]
         m = net.model
         zc = 8 if latent else 0
+        plan = self.plan = E.GatherPlan(net.parameters(), scales=(1.0, 0.2))
         first_map = ([0, 1, 2] + [-1] * 5 + [3, 4, 5] + [-1] * 5) if latent else ([0, 1, 2] + [-1] * 5)
-        self.first = _BwdConv(m[0], first_map, dgrad_from=len(first_map))  # no input gradient needed
+        self.first = _BwdConv(plan, m[0], first_map, dgrad_from=len(first_map), in_width=len(first_map))
         self.rdb = []
         for k in range(net.nb):
             rr = m[1].sub[k]
             for rdb in (rr.RDB1, rr.RDB2, rr.RDB3):
-                self.rdb.append([_BwdConv(rdb.convs[i][0], lr_map(64 + 32 * i), 0.2 if i == 4 else 1.0,
-                                          dgrad_from=zc) for i in range(5)])
-        self.lr_conv = _BwdConv(m[1].sub[net.nb], lr_map(64), dgrad_from=zc)
-        self.up = [_BwdConv(m[j][1], list(range(64))) for j in (2, 3)]
-        self.hr0 = _BwdConv(m[4], lr_map(64), dgrad_from=zc)
-        self.hr1 = _BwdConv(m[6], lr_map(64), cin_k=8, dgrad_from=zc)
+                self.rdb.append([_BwdConv(plan, rdb.convs[i][0], lr_map(64 + 32 * i), 0.2 if i == 4 else 1.0,
+                                          dgrad_from=zc, in_width=zc) for i in range(5)])
+        self.lr_conv = _BwdConv(plan, m[1].sub[net.nb], lr_map(64), dgrad_from=zc, in_width=zc)
+        self.up = [_BwdConv(plan, m[j][1], list(range(64))) for j in (2, 3)]
+        self.hr0 = _BwdConv(plan, m[4], lr_map(64), dgrad_from=zc, in_width=zc)
+        self.hr1 = _BwdConv(plan, m[6], lr_map(64), cin_k=8, dgrad_from=zc, in_width=zc)
+        convs = [self.first, self.lr_conv, self.hr0, self.hr1] + self.up + [c for r in self.rdb for c in r]
+        dev = m[0].weight.device
+        views = plan.finalize(dev)
+        off = 0
+        for c in convs:
+            c.slices = [(n0, nw, views[id(t)]) for n0, nw, t in c.slices]
+            c.in_slices = [(n0, nw, views[id(t)]) for n0, nw, t in c.in_slices]
+            c.wg_off = off
+            off += c.wg_n
+        self.zero_bias = torch.zeros(64, device=dev)
+        self.dw = torch.empty(off, device=dev, dtype=torch.float32)  # every conv's reduced wgrad, packed layout
+        by_param = {}
+        for c in convs:
+            wi, bi = c.grad_index()
+            by_param[id(c.conv.weight)], by_param[id(c.conv.bias)] = wi, bi
+        self.params = plan.params
+        assert all(id(p) in by_param for p in self.params), 'generator parameter without a backward rule'
+        self.gidx = torch.cat([by_param[id(p)] for p in self.params]).to(dev)
 
 
 def _bwd_packed(net, latent):
-    key = (E._param_key(net), latent)
+    skey, vkey = (E._struct_key(net), latent), E._param_key(net)
     c = net._esr_cache.get('packed_bwd')
-    if c is None or c[0] != key:
+    if c is None or c[0] != skey:
+        net._esr_cache.pop('packed_bwd', None)
         with torch.no_grad():
-            c = (key, _BwdPacked(net, latent))
+            c = [skey, None, _BwdPacked(net, latent)]
         net._esr_cache['packed_bwd'] = c
-    return c[1]
+    if c[1] != vkey:
+        with torch.no_grad():
+            c[2].plan.refresh()
+        c[1] = vkey
+    return c[2]
 
 
 # ----------------------------------------------------------------------------------------------------------------------
 # backward sweep
 # ----------------------------------------------------------------------------------------------------------------------
 class _Runner:
-    def __init__(self, ws, stream):
+    def __init__(self, ws, bp, stream, need_params=True, need_input=False):
         self.lib = _lib.load()
         self.ws = ws
+        self.bp = bp
         self.B = ws.B
         self.stream = stream
-        self.grads = {}
+        self.need_params, self.need_input = need_params, need_input
 
     def dgrad(self, bc, src, src_cp, src_coff, cin_k, h, w, dst, dst_cp, dst_base, accumulate, res=None):
         """dst[:, n0-dst_base ...] (+)= conv(src slice, rot180 W^T) for every output slice; `res` = (buf, cp, coff)
@@ -151,29 +195,34 @@ class _Runner:
             o = E._conv_out(dst, dst_cp, coff, h, w, False, r1=r1, r1_cp=r1_cp, r1_coff=r1_coff, s1=1.0)
             inp = src.data_ptr() + 4 * src_coff
             _lib.check(self.lib.esr_conv3x3_fwd(inp, self.B, h, w, src_cp, cin_k, wpk.data_ptr(),
-                                                bc.zero_bias.data_ptr(), nw, ctypes.byref(o), self.stream), 'dgrad')
+                                                self.bp.zero_bias.data_ptr(), nw, ctypes.byref(o), self.stream),
+                       'dgrad')
+
+    def dgrad_in(self, bc, src, src_cp, src_coff, cin_k, h, w, dst, dst_cp):
+        """Generator-input gradient: dst[:, 0:nw] += conv(src slice, rot180 W^T) restricted to the input channels
+        below the feature channels (latent Z slot; conv_first's [Z | LR] input)."""
+        if not self.need_input:
+            return
+        for n0, nw, wpk in bc.in_slices:
+            o = E._conv_out(dst, dst_cp, 0, h, w, False, r1=dst, r1_cp=dst_cp, r1_coff=0, s1=1.0)
+            _lib.check(self.lib.esr_conv3x3_fwd(src.data_ptr() + 4 * src_coff, self.B, h, w, src_cp, cin_k,
+                                                wpk.data_ptr(), self.bp.zero_bias.data_ptr(), nw, ctypes.byref(o),
+                                                self.stream), 'dgrad_in')
 
     def wgrad(self, bc, inp, in_cp, cin, up2, dout, d_cp, d_coff, h, w, scale=1.0):
-        ws = self.ws
-        cin_pad = (cin + 31) // 32 * 32
-        cout_pad = 32 if bc.cout <= 32 else 64
-        n = 9 * cin_pad * cout_pad + cout_pad
-        chunks = cin_pad // 32
+        """Weight + bias gradient of one conv into its region of the flat packed-layout buffer bp.dw."""
+        if not self.need_params:
+            return
+        assert cin == bc.cin_buf
+        chunks = bc.cin_pad // 32
         ntiles = self.B * ((h + 7) // 8) * ((w + 31) // 32)
         splits = max(1, min(WG_SPLITS_MAX, -(-1024 // chunks), ntiles))
+        assert splits * bc.wg_n <= self.ws.partial.numel()
         _lib.check(self.lib.esr_conv3x3_wgrad(inp.data_ptr(), in_cp, cin, up2, dout.data_ptr(), d_cp, d_coff,
-                                              bc.cout, self.B, h, w, splits, ws.partial.data_ptr(), self.stream),
+                                              bc.cout, self.B, h, w, splits, self.ws.partial.data_ptr(), self.stream),
                    'wgrad')
-        _lib.check(self.lib.esr_wgrad_reduce(ws.partial.data_ptr(), splits, n, scale, ws.dw.data_ptr(),
-                                             self.stream), 'wgrad_reduce')
-        dw = ws.dw[:9 * cin_pad * cout_pad].view(9, cin_pad, cout_pad)
-        g = dw[:, bc.ref_to_buf, :bc.cout].permute(2, 1, 0).reshape(bc.conv.weight.shape)
-        self._acc(bc.conv.weight, g)
-        self._acc(bc.conv.bias, ws.dw[9 * cin_pad * cout_pad:9 * cin_pad * cout_pad + bc.cout])
-
-    def _acc(self, p, g):
-        prev = self.grads.get(p)
-        self.grads[p] = g.clone() if prev is None else prev + g
+        _lib.check(self.lib.esr_wgrad_reduce(self.ws.partial.data_ptr(), splits, bc.wg_n, scale,
+                                             self.bp.dw.data_ptr() + 4 * bc.wg_off, self.stream), 'wgrad_reduce')
 
     def lrelu(self, d, d_cp, d_coff, y, y_cp, y_coff, C, h, w):
         _lib.check(self.lib.esr_lrelu_bwd(d.data_ptr(), d_cp, d_coff, y.data_ptr(), y_cp, y_coff, C, self.B, h, w,
@@ -191,21 +240,29 @@ def _rdb_backward(R, P, dout, dcat, convs, zc, cp, H, W):
     dbuf, dcp, dcoff = dout
     # conv4 (0.2 folded into its packed dgrad weights and its wgrad scale); the x slice also receives dL/dh
     R.wgrad(convs[4], P, cp, zc + 192, 0, dbuf, dcp, dcoff, H, W, scale=0.2)
+    R.dgrad_in(convs[4], dbuf, dcp, dcoff, 64, H, W, R.ws.dZl, 8)
     R.dgrad(convs[4], dbuf, dcp, dcoff, 64, H, W, dcat, cp, 0, accumulate=False, res=(dbuf, dcp, dcoff))
     for i in (3, 2, 1, 0):
         s = zc + 64 + 32 * i
         R.lrelu(dcat, cp, s, P, cp, s, 32, H, W)
         R.wgrad(convs[i], P, cp, s, 0, dcat, cp, s, H, W)
+        R.dgrad_in(convs[i], dcat, cp, s, 32, H, W, R.ws.dZl, 8)
         R.dgrad(convs[i], dcat, cp, s, 32, H, W, dcat, cp, 0, accumulate=True)
 
 
-def generator_backward(net, cem, ws, d_out, latent, M):
-    """dL/dparams of RRDBNet (+ CEM in train or eval mode) given dL/dout; returns {param: grad}."""
+def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_input=False):
+    """dL/dparams of RRDBNet (+ CEM in train or eval mode) and/or dL/dinput given dL/dout.
+    Returns ({param: grad} or {}, input gradient [B, C_in, h, w] or None)."""
     dev = d_out.device
     stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-    R = _Runner(ws, stream)
-    lib = R.lib
     bp = _bwd_packed(net, latent)
+    R = _Runner(ws, bp, stream, need_params, need_input)
+    lib = R.lib
+    if need_input:
+        ws.dZl.zero_()
+        ws.dFirst.zero_()
+        if latent:
+            ws.dZh.zero_()
     Bn, H, W, zc, cp, hcp = ws.B, ws.H, ws.W, ws.zc, ws.cp, ws.hr_cp
     HH, WW = E.SF * H, E.SF * W
     # ---- CEM adjoint: out = crop_M(gen + Up(Inv(LR - Down(gen)))) ----
@@ -237,10 +294,12 @@ def generator_backward(net, cem, ws, d_out, latent, M):
     dA, dB = ws.dHR
     # HR_conv1 (no act): input HR1 = [Z_HR | x]
     R.wgrad(bp.hr1, HR1, hcp, hcp, 0, ws.dgen_p, 8, 0, HH, WW)
+    R.dgrad_in(bp.hr1, ws.dgen_p, 8, 0, 8, HH, WW, ws.dZh, 8)
     R.dgrad(bp.hr1, ws.dgen_p, 8, 0, 8, HH, WW, dA, 64, zc, accumulate=False)
     # HR_conv0 + LReLU: output HR1.x
     R.lrelu(dA, 64, 0, HR1, hcp, zc, 64, HH, WW)
     R.wgrad(bp.hr0, HR0, hcp, hcp, 0, dA, 64, 0, HH, WW)
+    R.dgrad_in(bp.hr0, dA, 64, 0, 64, HH, WW, ws.dZh, 8)
     R.dgrad(bp.hr0, dA, 64, 0, 64, HH, WW, dB, 64, zc, accumulate=False)
     # upconv 2: HR0.x = lrelu(conv(nearest2(U1)))
     R.lrelu(dB, 64, 0, HR0, hcp, zc, 64, HH, WW)
@@ -256,6 +315,7 @@ def generator_backward(net, cem, ws, d_out, latent, M):
     Q = ws.Q
     trunk = Q[3 * net.nb]
     R.wgrad(bp.lr_conv, trunk, cp, zc + 64, 0, ws.dU0, 64, 0, H, W)
+    R.dgrad_in(bp.lr_conv, ws.dU0, 64, 0, 64, H, W, ws.dZl, 8)
     R.dgrad(bp.lr_conv, ws.dU0, 64, 0, 64, H, W, ws.GA, 64, zc, accumulate=False)
     # RRDBs, last to first: o = 0.2·RDB3(RDB2(RDB1(x))) + x
     D0, D1 = ws.D
@@ -268,7 +328,31 @@ def generator_backward(net, cem, ws, d_out, latent, M):
     # conv_first: dL/dfea = trunk gradient + LR_conv skip
     R.axpby(ws.GA, 64, 0, 1.0, ws.GA, 64, 0, 1.0, ws.dU0, 64, 0, C=64, h=H, w=W)
     R.wgrad(bp.first, ws.first, ws.first_cp, ws.first_cp, 0, ws.GA, 64, 0, H, W)
-    return R.grads
+    grads = {}
+    if need_params:
+        flat = bp.dw.index_select(0, bp.gidx)  # all parameter gradients, reference layout, parameter order
+        o = 0
+        for p in bp.params:
+            grads[p] = flat[o:o + p.numel()].view(p.shape)
+            o += p.numel()
+    dx = None
+    if need_input:
+        R.dgrad_in(bp.first, ws.GA, 64, 0, 64, H, W, ws.dFirst, ws.first_cp)
+        m = M // E.SF
+        h, w = H - 2 * m, W - 2 * m
+        d_lr = torch.empty(Bn, 3, h, w, device=dev)
+        _lib.check(lib.esr_input_adjoint(ws.dFirst.data_ptr(), ws.first_cp, ws.first_lr_off, None, 0, 0, 0,
+                                         a2.data_ptr() if cem is not None else None, 3, Bn, H, W, m,
+                                         d_lr.data_ptr(), stream), 'input_adjoint lr')
+        if latent:  # Z_LR = bilinear↓4(Z_HR) feeds conv_first and every LR conv; Z_HR feeds HR_conv0/1
+            R.axpby(ws.dZl, 8, 0, 1.0, ws.dZl, 8, 0, 1.0, ws.dFirst, ws.first_cp, 0, C=8, h=H, w=W)
+            d_z = torch.empty(Bn, 3, E.SF * h, E.SF * w, device=dev)
+            _lib.check(lib.esr_input_adjoint(ws.dZh.data_ptr(), 8, 0, ws.dZl.data_ptr(), 8, 0, E.SF, None, 3, Bn,
+                                             HH, WW, M, d_z.data_ptr(), stream), 'input_adjoint z')
+            dx = torch.cat([d_z.view(Bn, 3 * E.SF * E.SF, h, w), d_lr], 1)  # raw view, SRRaGAN_model.py:252
+        else:
+            dx = d_lr
+    return grads, dx
 
 
 class _GeneratorFn(torch.autograd.Function):
@@ -286,8 +370,10 @@ class _GeneratorFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, d_out):
-        grads = generator_backward(ctx.net, ctx.cem, ctx.ws, d_out, ctx.latent, ctx.M)
-        return (None, None, None) + tuple(grads.get(p) for p in ctx.params)
+        need_params = any(ctx.needs_input_grad[3:])
+        grads, dx = generator_backward(ctx.net, ctx.cem, ctx.ws, d_out, ctx.latent, ctx.M, need_params=need_params,
+                                       need_input=ctx.needs_input_grad[0])
+        return (dx, None, None) + tuple(grads.get(p) for p in ctx.params)
 
 
 def generator_forward_train(net, x, cem):

@@ -146,7 +146,8 @@ def cem_design(sf=4, kernel=None, lower_magnitude_bound=0.01, perturbation_limit
 # ----------------------------------------------------------------------------------------------------------------------
 def _dw(x, k, pad):
     """Depthwise (groups=3) cross-correlation with replicate padding (Filter_Layer, CEMnet.py:130-140)."""
-    w = torch.as_tensor(np.ascontiguousarray(k), dtype=torch.float32)[None, None].repeat(x.shape[1], 1, 1, 1)
+    # the reference casts its filters to float32 (CEMnet.py:134); a float64 input (conditioning checks) keeps those values
+    w = torch.as_tensor(np.ascontiguousarray(k), dtype=torch.float32).to(x.dtype)[None, None].repeat(x.shape[1], 1, 1, 1)
     return F.conv2d(F.pad(x, (pad, pad, pad, pad), mode='replicate'), w, groups=x.shape[1])
 
 

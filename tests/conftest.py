@@ -56,3 +56,47 @@ def gpu_device():
     if not torch.cuda.is_available():
         pytest.skip('no ROCm device')
     return torch.device('cuda:0')
+
+
+def l2_rel(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return float(np.sqrt(((a - b) ** 2).sum() / max((b ** 2).sum(), 1e-300)))
+
+
+def grad_parity(a, exact, base, factor=5.0, floor=1e-4):
+    """Gradient parity "as accurate as the reference's own fp32": relative L2 error of `a` against the float64
+    oracle `exact` must be within `factor`× that of an independent fp32 evaluation `base` (the reference's golden
+    values or the oracle in fp32), with an absolute floor (1e-4: either side may be the one that flips a kink).
+    The max-norm is not used for gradients: a pre-activation within fp32 rounding of 0 takes LeakyReLU slope 1 in
+    one evaluation and 0.2 in another, and each such kink flip
+    changes the gradient of its whole receptive field by O(1) locally (tests/test_oracle_golden.py::
+    test_fp32_gradients_have_kink_flips: the oracle's own fp32 vs fp64 input gradient differs by 7e-3 max-norm, 1.7e-3
+    L2 at 40x40 LR)."""
+    e, eb = l2_rel(a, exact), l2_rel(base, exact)
+    return e <= max(floor, factor * eb), 'l2 %.2e (fp32 reference %.2e, max-norm %.2e)' % (e, eb, normwise_rel(a, exact))
+
+
+def oracle_grads(params, lr, z, R, nb, latent, design, pre_pad, dtype, want_params=True):
+    """Gradients of Σ out·R through the oracle (CEM_PyTorch ∘ RRDBNet) in `dtype`: {'param:<key>', 'dz', 'dlr'}.
+    `params` are reference-keyed numpy arrays (prefix stripped here); lr/z numpy NCHW (z = HR latent or None)."""
+    import torch
+    from oracle import esr_oracle as O
+    P = {k: torch.as_tensor(v).to(dtype).requires_grad_(want_params) for k, v in O.strip_prefix(params).items()}
+    lr_t = torch.as_tensor(lr).to(dtype).requires_grad_(True)
+    B, _, h, w = lr_t.shape
+    x = lr_t
+    z_t = None
+    if latent:
+        z_t = torch.as_tensor(z).to(dtype).requires_grad_(True)
+        x = torch.cat([z_t.reshape(B, -1, h, w), lr_t], 1)
+    out = O.sr_forward(x, P, nb, latent, design, pre_pad=pre_pad)
+    (out * torch.as_tensor(R).to(dtype)).sum().backward()
+    g = {'dlr': lr_t.grad.double().numpy()}
+    if z_t is not None:
+        g['dz'] = z_t.grad.double().numpy()
+    if want_params:
+        for k, v in P.items():
+            if v.grad is not None:
+                g['param:' + k] = v.grad.double().numpy()
+    return g

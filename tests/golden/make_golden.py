@@ -209,6 +209,36 @@ def grad_fixture(arch, CEMnet, name, latent, lr_shape, seed, w_scale):
     print('grad_%s: %d grads, |g conv_first| %.3e' % (name, len(GRAD_KEYS), np.abs(d['grad:model.0.weight']).mean()))
 
 
+def zgrad_fixture(arch, CEMnet, name, cem_mode, lr_shape, seed, w_scale, kernel=None):
+    """Z-optimisation gradients (Z_optimization.py:545-553, 574-630): generator frozen (requires_grad False), latent
+    RRDBNet(nb=1) CEM-wrapped in `cem_mode`, loss = Σ out·R; dumps dL/dZ (HR latent, [B,3,4h,4w]) and dL/dLR."""
+    net = arch.RRDBNet(in_nc=3, out_nc=3, nf=64, nb=1, gc=32, upscale=4, norm_type=None, act_type='leakyrelu',
+                       mode='CNA', upsample_mode='upconv', latent_input='all_layers_HR_downscaled',
+                       num_latent_channels=3)
+    model = CEMnet.CEMnet(CEMnet.Get_CEM_Config(4), upscale_kernel=kernel).WrapArchitecture_PyTorch(net)
+    sd = model.state_dict()
+    named_shapes = [(k, tuple(v.shape)) for k, v in sd.items()]
+    params = seeded_params(named_shapes, seed, w_scale=w_scale)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=False)
+    model.train(cem_mode == 'train')
+    for q in model.parameters():
+        q.requires_grad = False
+    B, _, h, w = lr_shape
+    lr, z = seeded_inputs(seed + 1, lr_shape, (B, 3, 4 * h, 4 * w), z_mode='pixel')
+    zt = torch.from_numpy(z).requires_grad_(True)
+    lt = torch.from_numpy(lr).requires_grad_(True)
+    out = model(torch.cat([zt.view(B, 48, h, w), lt], 1))
+    R = torch.from_numpy(np.random.default_rng(seed + 2).standard_normal(tuple(out.shape)).astype(np.float32))
+    (out * R).sum().backward()
+    d = dict(lr=lr, z=z, R=R.numpy(), out=out.detach().numpy(), dz=zt.grad.numpy(), dlr=lt.grad.numpy(),
+             seed=np.int64(seed), w_scale=np.float64(w_scale), cem_mode=np.str_(cem_mode),
+             keys=np.str_(json.dumps(named_shapes)), nb=np.int64(1), latent=np.int64(1))
+    if isinstance(kernel, np.ndarray):
+        d['kernel'] = kernel
+    np.savez_compressed(os.path.join(HERE, 'zgrad_%s.npz' % name), **d)
+    print('zgrad_%s: |dz| %.3e |dlr| %.3e' % (name, np.abs(d['dz']).mean(), np.abs(d['dlr']).mean()))
+
+
 def disc_fixture(arch, loss_mod, name, seed):
     """Discriminator_VGG_128_ (architecture.py:222-284) with nb = n_layers = 6 as the shipped train config builds it
     once define_D's TypeError is resolved, plus one WGAN-GP discriminator loss + gradients exactly as
@@ -278,10 +308,14 @@ def main():
     # --- training-step gradients (bicubic CEM, train mode) ---
     grad_fixture(arch, CEMnet, 'plain_nb1', False, (2, 3, 12, 16), 13, 0.5)
     grad_fixture(arch, CEMnet, 'latent_nb1', True, (2, 3, 12, 12), 14, 0.5)
+    # --- Z-optimisation input gradients (frozen G) ---
+    zgrad_fixture(arch, CEMnet, 'eval', 'eval', (2, 3, 12, 12), 16, 0.5)
+    zgrad_fixture(arch, CEMnet, 'train', 'train', (2, 3, 12, 16), 17, 0.5)
     # --- learned kernel last: imresize.kernels is process-global and sticky (imresize_CEM.py:9,23-42) ---
     k = synthetic_learned_kernel()
     cem_fixture(CEMnet, 'learned13', k)
     rrdb_fixture(arch, CEMnet, 'latent_nb1_cem_eval_learned', 1, True, (1, 3, 12, 12), 12, 0.5, cem_mode='eval', kernel=k)
+    zgrad_fixture(arch, CEMnet, 'eval_learned', 'eval', (1, 3, 12, 12), 18, 0.5, kernel=k)
 
 
 if __name__ == '__main__':

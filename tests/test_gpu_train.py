@@ -1,11 +1,13 @@
 """GPU parity of the training path: HIP forward with retained activations + hand-written backward (exact fp32)
 against the reference's own training gradients (golden) and the oracle's autograd (all parameters).
-Tolerance: normwise 1e-4 (fp32 with different summation order; observed ~1e-6)."""
+Forward outputs: normwise 1e-5.  Gradients: conftest.grad_parity — relative L2 error against the float64 oracle within
+5× that of the reference's own fp32 evaluation (floor 1e-4, a tenth of the 1e-3 bar; an indexing or layout bug
+shows as O(1e-1) errors), which is robust to LeakyReLU kink flips."""
 import numpy as np
 import pytest
 import torch
 
-from conftest import fixture_input, fixture_params, golden, golden_names, normwise_rel
+from conftest import fixture_input, fixture_params, golden, golden_names, grad_parity, normwise_rel, oracle_grads
 
 import esr_amd
 from esr_amd import CEMnet as C
@@ -31,11 +33,14 @@ def test_training_gradients_vs_reference_golden(gpu_device, name):
     out = model(fixture_input(d).to(gpu_device))
     assert normwise_rel(out.detach().cpu(), d['out']) < 1e-5
     (out * torch.from_numpy(d['R']).to(gpu_device)).sum().backward()
+    exact = oracle_grads(params, d['lr'], d['z'] if 'z' in d.files else None, d['R'], int(d['nb']),
+                         bool(int(d['latent'])), O.cem_design(4), False, torch.float64)
     named = dict(model.named_parameters())
     for k in [f[len('grad:'):] for f in d.files if f.startswith('grad:')]:
         g = named['generated_image_model.' + k].grad
         assert g is not None, k
-        assert normwise_rel(g.cpu(), d['grad:' + k]) < 1e-4, k
+        ok, msg = grad_parity(g.cpu(), exact['param:' + k], d['grad:' + k])
+        assert ok, (k, msg)
 
 
 @pytest.mark.parametrize('latent', [False, True])
@@ -55,19 +60,18 @@ def test_all_parameter_gradients_vs_oracle(gpu_device, latent):
     R = torch.from_numpy(np.random.default_rng(53).standard_normal((B, 3, 4 * h, 4 * w)).astype(np.float32))
     out = model(x.to(gpu_device))
     (out * R.to(gpu_device)).sum().backward()
-    P = {k: v.requires_grad_(True) for k, v in O.strip_prefix(params).items()}
-    ref = O.sr_forward(x, P, nb, latent, O.cem_design(4), pre_pad=False)
-    (ref * R).sum().backward()
-    assert normwise_rel(out.detach().cpu(), ref.detach()) < 1e-5
-    worst = 0.0
+    P = O.strip_prefix(params)
+    with torch.no_grad():
+        ref = O.sr_forward(x, P, nb, latent, O.cem_design(4), pre_pad=False)
+    assert normwise_rel(out.detach().cpu(), ref) < 1e-5
+    exact, base = (oracle_grads(params, lr, z, R, nb, latent, O.cem_design(4), False, dt)
+                   for dt in (torch.float64, torch.float32))
     for n, p in model.named_parameters():
         if not p.requires_grad:
             continue
-        k = n[len('generated_image_model.'):]
-        e = normwise_rel(p.grad.cpu(), P[k].grad)
-        worst = max(worst, e)
-        assert e < 1e-4, (n, e)
-    print('worst normwise grad error (latent=%s): %.2e' % (latent, worst))
+        k = 'param:' + n[len('generated_image_model.'):]
+        ok, msg = grad_parity(p.grad.cpu(), exact[k], base[k])
+        assert ok, (n, msg)
 
 
 def test_training_step_is_deterministic(gpu_device):
@@ -114,3 +118,55 @@ def test_optimize_parameters_training_step(gpu_device):
         assert model.log_dict[k] and np.isfinite(model.log_dict[k][-1][1]), k
     model.test()
     assert tuple(model.fake_H.shape) == (2, 3, 160, 160)
+
+
+@pytest.mark.parametrize('name', golden_names('zgrad_'))
+def test_z_gradients_vs_reference_golden(gpu_device, name):
+    """Z optimisation (Z_optimization.py:545-630): generator frozen, gradient w.r.t. the model input only —
+    replicate pre-pad adjoint (eval), bilinear ↓4 adjoint, Z slots of every conv, CEM's LR path."""
+    d = golden(name)
+    _, params = fixture_params(d)
+    net = esr_amd.RRDBNet(3, 3, 64, 1, latent_input='all_layers_HR_downscaled', num_latent_channels=3)
+    cem = C.CEMnet(C.Get_CEM_Config(4), upscale_kernel=d['kernel'] if 'kernel' in d.files else None)
+    model = cem.WrapArchitecture_PyTorch(net)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=False)
+    model = model.to(gpu_device).train(str(d['cem_mode']) == 'train')
+    for p in model.parameters():
+        p.requires_grad = False
+    z = torch.from_numpy(d['z']).to(gpu_device).requires_grad_(True)
+    lr = torch.from_numpy(d['lr']).to(gpu_device).requires_grad_(True)
+    B, _, h, w = lr.shape
+    out = model(torch.cat([z.view(B, 48, h, w), lr], 1))
+    assert normwise_rel(out.detach().cpu(), d['out']) < 1e-5
+    (out * torch.from_numpy(d['R']).to(gpu_device)).sum().backward()
+    design = O.cem_design(4, d['kernel'] if 'kernel' in d.files else None)
+    exact = oracle_grads(params, d['lr'], d['z'], d['R'], 1, True, design, str(d['cem_mode']) == 'eval',
+                         torch.float64, want_params=False)
+    for g, k in ((z.grad, 'dz'), (lr.grad, 'dlr')):
+        ok, msg = grad_parity(g.cpu(), exact[k], d[k])
+        assert ok, (k, msg)
+
+
+@pytest.mark.parametrize('mode', ['eval', 'train'])
+def test_input_and_parameter_gradients_together_vs_oracle(gpu_device, mode):
+    """Both gradient kinds in one backward (nb=2, latent, pixel Z) against the oracle's autograd."""
+    nb = 2
+    net = esr_amd.RRDBNet(3, 3, 64, nb, latent_input='all_layers_HR_downscaled', num_latent_channels=3)
+    model = C.CEMnet(C.Get_CEM_Config(4)).WrapArchitecture_PyTorch(net)
+    params = seeded_params([(k, tuple(v.shape)) for k, v in model.state_dict().items()], 61, w_scale=0.7)
+    model = _model(nb, True, params, gpu_device).train(mode == 'train')
+    B, h, w = 2, 12, 10
+    lr, z = seeded_inputs(62, (B, 3, h, w), (B, 3, 4 * h, 4 * w), z_mode='pixel')
+    zt = torch.from_numpy(z).to(gpu_device).requires_grad_(True)
+    out = model(torch.cat([zt.view(B, 48, h, w), torch.from_numpy(lr).to(gpu_device)], 1))
+    R = torch.from_numpy(np.random.default_rng(63).standard_normal(tuple(out.shape)).astype(np.float32))
+    (out * R.to(gpu_device)).sum().backward()
+    exact, base = (oracle_grads(params, lr, z, R, nb, True, O.cem_design(4), mode == 'eval', dt)
+                   for dt in (torch.float64, torch.float32))
+    ok, msg = grad_parity(zt.grad.cpu(), exact['dz'], base['dz'])
+    assert ok, msg
+    for n, p in model.named_parameters():
+        if p.requires_grad:
+            k = 'param:' + n[len('generated_image_model.'):]
+            ok, msg = grad_parity(p.grad.cpu(), exact[k], base[k])
+            assert ok, (n, msg)

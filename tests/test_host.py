@@ -152,3 +152,52 @@ def test_split_f16_roundtrip_and_x3_packing():
     rec16 = (px[..., 0, :].float() + px[..., 1, :].float()).reshape(6, 9, 32, 16) / scale
     rec = rec16.view(3, 2, 9, 32, 16).permute(0, 2, 3, 1, 4).reshape(pk.shape)
     assert float((rec - pk).abs().max()) <= 2 ** -22 * float(pk.abs().max())
+
+
+@pytest.mark.parametrize('latent', [False, True])
+def test_gather_plan_equals_direct_packing(latent):
+    """The one-gather packing (GatherPlan) reproduces the per-conv packing for the forward weights, the rot180 /
+    transposed / 0.2-scaled data-gradient weights, and maps the flat wgrad buffer back to reference-layout grads."""
+    from esr_amd import train_engine as T
+    torch.manual_seed(0)
+    net = esr_amd.RRDBNet(3, 3, 64, 1, gc=32, latent_input='all_layers_HR_downscaled' if latent else None,
+                          num_latent_channels=3 if latent else 0)
+    for p in net.parameters():
+        p.data.normal_()
+    zc = 8 if latent else 0
+    lr_map = (lambda n: list(range(n))) if not latent else (lambda n: [0, 1, 2] + [-1] * 5 + [3 + c for c in range(n)])
+    pk = engine._packed(net, latent)
+    conv = net.model[1].sub[0].RDB2.convs[3][0]
+    assert torch.equal(pk.rdb[1][3].f32, engine.pack_conv_weight(conv.weight, lr_map(64 + 96), 32))
+    assert torch.equal(pk.hr1.f32, engine.pack_conv_weight(net.model[6].weight, lr_map(64), 32))
+    # refresh after an in-place update
+    with torch.no_grad():
+        conv.weight.mul_(3.0)
+    pk = engine._packed(net, latent)
+    assert torch.equal(pk.rdb[1][3].f32, engine.pack_conv_weight(conv.weight, lr_map(64 + 96), 32))
+    bp = T._bwd_packed(net, latent)
+    c4 = net.model[1].sub[0].RDB3.convs[4][0]
+    bc = bp.rdb[2][4]
+    wf = c4.weight.detach().flip(2, 3).transpose(0, 1)
+    n0, nw, wpk = bc.slices[-1]
+    cmap = lr_map(64 + 128)
+    wt = torch.zeros(nw, 64, 3, 3)
+    for o in range(nw):
+        if cmap[n0 + o] >= 0:
+            wt[o] = wf[cmap[n0 + o]]
+    assert bc.slices[0][0] == zc
+    assert torch.allclose(wpk, engine.pack_conv_weight(wt * 0.2, list(range(64)), 32 if nw <= 32 else 64), rtol=0,
+                          atol=0)
+    # wgrad buffer -> reference-layout gradient
+    ref = {p: torch.randn_like(p) for p in net.parameters()}
+    for b in [bp.first, bp.lr_conv, bp.hr0, bp.hr1] + bp.up + [c for r in bp.rdb for c in r]:
+        g = ref[b.conv.weight]
+        reg = torch.zeros(9, b.cin_pad, b.cout_pad)
+        reg[:, b.ref_to_buf, :b.cout] = g.reshape(b.cout, -1, 9).permute(2, 1, 0)
+        bp.dw[b.wg_off:b.wg_off + 9 * b.cin_pad * b.cout_pad] = reg.reshape(-1)
+        bp.dw[b.wg_off + 9 * b.cin_pad * b.cout_pad:b.wg_off + 9 * b.cin_pad * b.cout_pad + b.cout] = ref[b.conv.bias]
+    flat = bp.dw.index_select(0, bp.gidx)
+    o = 0
+    for p in bp.params:
+        assert torch.equal(flat[o:o + p.numel()].view(p.shape), ref[p])
+        o += p.numel()
