@@ -20,11 +20,7 @@
 //
 // Pipeline.  K is walked in 16-channel chunks (one 32×32×16 MFMA step per tap).  Each chunk's halo tile (18 × 34
 // records of 64 B) and weights are copied HBM/L2 -> LDS by LDS-DMA (global_load_lds_dwordx4: no VGPR round trip, no
-// ds_write) into one of two LDS stages while the MFMAs consume the other stage.  LDS is laid out [in0|in1|w0|w1] and
-// the chunk loop is unrolled by two, so every fragment address is a per-lane register computed once per workgroup
-// plus an immediate offset (no address arithmetic per tap); DMA source offsets are also computed once.  Fragments
-// of tap t+1 are read while tap t's MFMAs run, and the MFMAs are issued product-major over the independent
-// accumulators.  Records are 64 B (4 × 16-B slots)
+// ds_write) into one of two LDS stages while the MFMAs consume the other stage.  Records are 64 B (4 × 16-B slots)
 // with the slot index XOR-swizzled by (record>>2)&3, applied on the DMA source address (the DMA destination is
 // lane-linear), so the 16 lanes of every ds_read_b128 group hit 16 distinct slots.  Out-of-range halo pixels and
 // the channels past cin of a partial chunk are fetched from a zero page.
@@ -88,18 +84,15 @@ __device__ __forceinline__ bool store_group(unsigned char *p, const float v[8]) 
 // byte offset of logical 16-B slot s of record r inside a stage region
 __device__ __forceinline__ int slot_off(int r, int s) { return r * REC + ((s ^ ((r >> 2) & 3)) << 4); }
 
-template <int NT, int TS>
-__global__ __launch_bounds__(NTHR, 1) void conv_x3_kernel(X3Params p) {
+template <int NT, int TS, int MODE>
+__global__ __launch_bounds__(NTHR, (MODE >= 4 ? 1 : 2)) void conv_x3_kernel(X3Params p) {
     constexpr int T = TS * TS;
     constexpr int N = NT * 32;
-    constexpr int W_RECS = T * N;
-    constexpr int IN_B = IN_RECS * REC;
-    constexpr int W_B = W_RECS * REC;
+    constexpr int W_RECS = T * N;  // multiple of 16
+    constexpr int STAGE = (IN_RECS + W_RECS) * REC;
     constexpr int EP_P = N + 4;
     constexpr int EP_BYTES = TH * TWF * EP_P * 4;
-    constexpr int LDS_BYTES = 2 * (IN_B + W_B) > EP_BYTES ? 2 * (IN_B + W_B) : EP_BYTES;
-    constexpr int KIN = (IN_RECS / 16 + NWAVES - 1) / NWAVES;
-    constexpr int KW = (W_RECS / 16 + NWAVES - 1) / NWAVES;
+    constexpr int LDS_BYTES = 2 * STAGE > EP_BYTES ? 2 * STAGE : EP_BYTES;
     __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
 
     const int tid = threadIdx.x;
@@ -111,73 +104,52 @@ __global__ __launch_bounds__(NTHR, 1) void conv_x3_kernel(X3Params p) {
     const int tx = blockIdx.x % p.tiles_x;
     const int ty = blockIdx.x / p.tiles_x;
     const int x0 = tx * TWF;
-    const int tw = min(TWF, p.W - x0);
-    const int hx = tw + 2;
-    const int r0 = ty * TH;
+    const int tw = min(TWF, p.W - x0);  // tile width (32, or the remainder)
+    const int hx = tw + 2;              // halo tile row length
+    const int r0 = ty * TH;             // tall padded row of halo row 0
     const int rows_tot = p.B * (p.H + 2);
-    const int nq = TH * tw;
-    const int nmt = (nq + 31) >> 5;
+    const int nq = TH * tw;             // output pixels in the tile
+    const int nmt = (nq + 31) >> 5;     // 32-pixel M-tiles
+
     const long long rowp = (long long)(p.W + 2);
     const long long pixb = 4LL * p.in_cp;
     const int nchunk = (p.cin + 15) >> 4;
 
-    const int sub = lane >> 2, ps = lane & 3;
-    long long in_src[KIN];
-    int in_hi[KIN];
-#pragma unroll
-    for (int i = 0; i < KIN; ++i) {
-        const int k = wave + NWAVES * i;
-        const int r = 16 * k + sub;
-        const int s = ps ^ ((r >> 2) & 3);
-        const int hy = r / hx, hxi = r - (r / hx) * hx;
-        const int gy = r0 + hy, gx = x0 + hxi;
-        in_hi[i] = -1;
-        in_src[i] = 0;
-        if (k < IN_RECS / 16 && r < HY * hx && gy < rows_tot && gx < p.W + 2) {
-            in_src[i] = (gy * rowp + gx) * pixb + (s << 4);
-            in_hi[i] = s >> 1;
-        }
-    }
+    // ---- LDS-DMA of chunk j into stage st ----
     auto dma = [&](int j, int st) {
-        const int groups = min(16, p.cin - 16 * j) >> 3;
-#pragma unroll
-        for (int i = 0; i < KIN; ++i) {
-            const int k = wave + NWAVES * i;
-            if (k >= IN_RECS / 16) break;
-            const void *src = (in_hi[i] >= 0 && in_hi[i] < groups) ? (const void *)(p.in + in_src[i] + 64LL * j)
-                                                                   : (const void *)g_zero_page;
-            __builtin_amdgcn_global_load_lds((glob_void *)src, (lds_void *)(lds + st * IN_B + k * 1024), 16, 0, 0);
+        unsigned char *base = lds + st * STAGE;
+        const int groups = min(16, p.cin - 16 * j) >> 3;  // real 8-channel groups in this chunk (1 or 2)
+        const int sub = lane >> 2, ps = lane & 3;
+        for (int k = wave; k < IN_RECS / 16; k += NWAVES) {
+            const int r = 16 * k + sub;
+            const int s = ps ^ ((r >> 2) & 3);
+            const int hy = r / hx, hxi = r - (r / hx) * hx;
+            const int gy = r0 + hy, gx = x0 + hxi;
+            const void *src = g_zero_page;
+            if (r < HY * hx && gy < rows_tot && gx < p.W + 2 && (s >> 1) < groups)
+                src = p.in + (gy * rowp + gx) * pixb + 64LL * j + (s << 4);
+            __builtin_amdgcn_global_load_lds((glob_void *)src, (lds_void *)(base + k * 1024), 16, 0, 0);
         }
-        const unsigned char *wj = p.w + (long long)j * W_B;
-#pragma unroll
-        for (int i = 0; i < KW; ++i) {
-            const int k = wave + NWAVES * i;
-            if (k >= W_RECS / 16) break;
+        const unsigned char *wj = p.w + (long long)j * W_RECS * REC;
+        for (int k = wave; k < W_RECS / 16; k += NWAVES) {
             const int r = 16 * k + sub;
             const int s = ps ^ ((r >> 2) & 3);
             __builtin_amdgcn_global_load_lds((glob_void *)(wj + r * REC + (s << 4)),
-                                             (lds_void *)(lds + 2 * IN_B + st * W_B + k * 1024), 16, 0, 0);
+                                             (lds_void *)(base + (IN_RECS + 16 * k) * REC), 16, 0, 0);
         }
     };
 
-    int aoff[T][2][2];
+    // per-lane A-fragment record of each of the wave's two M-tiles (tap 0)
+    int rec0[2];
     bool mvalid[2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
         const int jm = 2 * wave + mt;
-        mvalid[mt] = jm < nmt;
+        mvalid[mt] = jm < nmt;  // wave-uniform
         int q = 32 * jm + ml;
         if (q >= nq) q = 0;
-        const int rec0 = (q / tw) * hx + q % tw;
-#pragma unroll
-        for (int tap = 0; tap < T; ++tap) {
-            const int r = rec0 + (p.tap_y0 + tap / TS) * hx + p.tap_x0 + tap % TS;
-            aoff[tap][mt][0] = slot_off(r, 2 * hl);
-            aoff[tap][mt][1] = slot_off(r, 2 * hl + 1);
-        }
+        rec0[mt] = (q / tw) * hx + q % tw;
     }
-    const int bsw = (ml >> 2) & 3;
-    const int boff0 = ml * REC + (((2 * hl) ^ bsw) << 4), boff1 = ml * REC + (((2 * hl + 1) ^ bsw) << 4);
 
     f32x16 acc[2][NT];
 #pragma unroll
@@ -187,52 +159,76 @@ __global__ __launch_bounds__(NTHR, 1) void conv_x3_kernel(X3Params p) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.f;
 
-    auto compute = [&](const unsigned char *s_in, const unsigned char *s_w) {
-        f16x8 ah[2][2], al[2][2], bh[2][NT], bl[2][NT];
-        auto ld = [&](int tap, int buf) {
+    dma(0, 0);
+    for (int j = 0; j < nchunk; ++j) {
+        __syncthreads();  // chunk j landed (vmcnt(0) of every wave), stage (j+1)&1 no longer read
+        if (j + 1 < nchunk && MODE != 1) dma(j + 1, (j + 1) & 1);
+        const unsigned char *s_in = lds + (j & 1) * STAGE;
+        const unsigned char *s_w = s_in + IN_RECS * REC;
+        if (!mvalid[0] || MODE == 2) continue;
+        if (MODE >= 3) {
+            // software-pipelined: fragments of tap t+1 are read from LDS while tap t's MFMAs run
+            f16x8 ah[2][2], al[2][2], bh[2][NT], bl[2][NT];
+            auto ld = [&](int tap, int buf) {
+                const int off = (p.tap_y0 + tap / TS) * hx + p.tap_x0 + tap % TS;
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt) {
+                    const int r = rec0[mt] + off;
+                    ah[buf][mt] = *reinterpret_cast<const f16x8 *>(s_in + slot_off(r, 2 * hl));
+                    al[buf][mt] = *reinterpret_cast<const f16x8 *>(s_in + slot_off(r, 2 * hl + 1));
+                }
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) {
+                    const int r = tap * N + nt * 32 + ml;
+                    bh[buf][nt] = *reinterpret_cast<const f16x8 *>(s_w + slot_off(r, 2 * hl));
+                    bl[buf][nt] = *reinterpret_cast<const f16x8 *>(s_w + slot_off(r, 2 * hl + 1));
+                }
+            };
+            ld(0, 0);
+#pragma unroll
+            for (int tap = 0; tap < T; ++tap) {
+                const int cb = tap & 1;
+                if (tap + 1 < T) ld(tap + 1, cb ^ 1);
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt) {
+                    if (!mvalid[mt]) continue;
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt) {
+                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[cb][mt], bh[cb][nt], acc[mt][nt], 0, 0, 0);
+                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[cb][mt], bl[cb][nt], acc[mt][nt], 0, 0, 0);
+                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[cb][mt], bh[cb][nt], acc[mt][nt], 0, 0, 0);
+                    }
+                }
+            }
+            continue;
+        }
+#pragma unroll
+        for (int tap = 0; tap < T; ++tap) {
+            const int off = (p.tap_y0 + tap / TS) * hx + p.tap_x0 + tap % TS;
+            f16x8 ah[2], al[2], bh[NT], bl[NT];
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
-                ah[buf][mt] = *reinterpret_cast<const f16x8 *>(s_in + aoff[tap][mt][0]);
-                al[buf][mt] = *reinterpret_cast<const f16x8 *>(s_in + aoff[tap][mt][1]);
+                const int r = rec0[mt] + off;
+                ah[mt] = *reinterpret_cast<const f16x8 *>(s_in + slot_off(r, 2 * hl));
+                al[mt] = *reinterpret_cast<const f16x8 *>(s_in + slot_off(r, 2 * hl + 1));
             }
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) {
-                bh[buf][nt] = *reinterpret_cast<const f16x8 *>(s_w + (tap * N + nt * 32) * REC + boff0);
-                bl[buf][nt] = *reinterpret_cast<const f16x8 *>(s_w + (tap * N + nt * 32) * REC + boff1);
+                const int r = tap * N + nt * 32 + ml;
+                bh[nt] = *reinterpret_cast<const f16x8 *>(s_w + slot_off(r, 2 * hl));
+                bl[nt] = *reinterpret_cast<const f16x8 *>(s_w + slot_off(r, 2 * hl + 1));
             }
-        };
-        ld(0, 0);
 #pragma unroll
-        for (int tap = 0; tap < T; ++tap) {
-            const int cb = tap & 1;
-            if (tap + 1 < T) ld(tap + 1, cb ^ 1);
+            for (int mt = 0; mt < 2; ++mt) {
+                if (!mvalid[mt]) continue;
 #pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt)
-                    if (mvalid[mt]) acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[cb][mt], bh[cb][nt], acc[mt][nt], 0, 0, 0);
-#pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt)
-                    if (mvalid[mt]) acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[cb][mt], bl[cb][nt], acc[mt][nt], 0, 0, 0);
-#pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt)
-                    if (mvalid[mt]) acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[cb][mt], bh[cb][nt], acc[mt][nt], 0, 0, 0);
+                for (int nt = 0; nt < NT; ++nt) {
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[mt], bh[nt], acc[mt][nt], 0, 0, 0);
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mt], bl[nt], acc[mt][nt], 0, 0, 0);
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mt], bh[nt], acc[mt][nt], 0, 0, 0);
+                }
+            }
         }
-    };
-
-    dma(0, 0);
-    for (int j = 0; j < nchunk; j += 2) {
-        __syncthreads();
-        if (j + 1 < nchunk) dma(j + 1, 1);
-        if (mvalid[0]) compute(lds, lds + 2 * IN_B);
-        if (j + 1 >= nchunk) break;
-        __syncthreads();
-        if (j + 2 < nchunk) dma(j + 2, 0);
-        if (mvalid[0]) compute(lds + IN_B, lds + 2 * IN_B + W_B);
     }
 
     // ---- epilogue: restage fp32 accumulators as [pixel][channel] ----
@@ -302,53 +298,26 @@ __global__ __launch_bounds__(NTHR, 1) void conv_x3_kernel(X3Params p) {
     if (!ok && p.overflow) atomicOr(p.overflow, 1);
 }
 
-int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const void *w, const float *bias,
-              float w_scale, int cout, int taps_side, int ty0, int tx0, const esr_conv_out *o, int *overflow,
-              hipStream_t stream) {
-    if (!in || !w || !bias || !o || !o->out) return ESR_EINVAL;
-    if (B <= 0 || H <= 0 || W <= 0 || cin <= 0 || cout <= 0 || cout > 64 || !(w_scale > 0.f)) return ESR_EINVAL;
-    if (cin % 8 || in_cp % 8 || in_cp < cin) return ESR_EINVAL;
-    if (!o->out_planar && (cout % 8 || o->out_cp % 8 || o->out_coff % 8 || o->out_coff + cout > o->out_cp))
-        return ESR_EINVAL;
-    if ((o->r1 && (o->r1_cp % 8 || o->r1_coff % 8)) || (o->r2 && (o->r2_cp % 8 || o->r2_coff % 8)) ||
-        (o->out2 && (o->out2_cp % 8 || o->out2_coff % 8)))
-        return ESR_EINVAL;
-    if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(w)) & 15) return ESR_EINVAL;
+
+}  // namespace
+
+extern "C" int x3exp_conv(int mode, const void *in, int B, int H, int W, int in_cp, int cin, const void *w,
+                          const float *bias, float w_scale, int cout, const esr_conv_out *o, int *overflow,
+                          void *stream) {
     X3Params p;
     p.in = static_cast<const unsigned char *>(in);
     p.B = B; p.H = H; p.W = W; p.in_cp = in_cp; p.cin = cin;
     p.w = static_cast<const unsigned char *>(w);
     p.bias = bias; p.w_scale_inv = 1.f / w_scale; p.cout = cout;
-    p.tap_y0 = ty0; p.tap_x0 = tx0;
+    p.tap_y0 = 0; p.tap_x0 = 0;
     p.tiles_x = (W + TWF - 1) / TWF;
     p.tiles_y = (B * (H + 2) - 2 + TH - 1) / TH;
     p.overflow = overflow;
     p.o = *o;
     const dim3 grid((unsigned)(p.tiles_x * p.tiles_y)), block(NTHR);
-    if (taps_side == 3) {
-        if (cout > 32) hipLaunchKernelGGL((conv_x3_kernel<2, 3>), grid, block, 0, stream, p);
-        else hipLaunchKernelGGL((conv_x3_kernel<1, 3>), grid, block, 0, stream, p);
-    } else {
-        if (cout > 32) hipLaunchKernelGGL((conv_x3_kernel<2, 2>), grid, block, 0, stream, p);
-        else hipLaunchKernelGGL((conv_x3_kernel<1, 2>), grid, block, 0, stream, p);
-    }
-    return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
-}
-
-}  // namespace
-
-extern "C" int esr_conv3x3_fwd_x3(const void *in, int32_t B, int32_t H, int32_t W, int32_t in_cp, int32_t cin,
-                                  const void *w_packed, const float *bias, float w_scale, int32_t cout,
-                                  const esr_conv_out *o, int32_t *overflow, esr_stream_t stream) {
-    return launch_x3(in, B, H, W, in_cp, cin, w_packed, bias, w_scale, cout, 3, 0, 0, o, overflow,
-                     (hipStream_t)stream);
-}
-
-extern "C" int esr_upconv2x_phase_fwd_x3(const void *in, int32_t B, int32_t H, int32_t W, int32_t in_cp, int32_t cin,
-                                         const void *w_packed, const float *bias, float w_scale, int32_t cout,
-                                         int32_t py, int32_t px, const esr_conv_out *o, int32_t *overflow,
-                                         esr_stream_t stream) {
-    if (py < 0 || py > 1 || px < 0 || px > 1) return ESR_EINVAL;
-    return launch_x3(in, B, H, W, in_cp, cin, w_packed, bias, w_scale, cout, 2, py, px, o, overflow,
-                     (hipStream_t)stream);
+    hipStream_t s = (hipStream_t)stream;
+#define L(NT_, M_) hipLaunchKernelGGL((conv_x3_kernel<NT_, 3, M_>), grid, block, 0, s, p)
+    if (cout > 32) { if (mode == 0) L(2, 0); else if (mode == 1) L(2, 1); else if (mode == 2) L(2, 2); else if (mode == 3) L(2, 3); else L(2, 4); }
+    else { if (mode == 0) L(1, 0); else if (mode == 1) L(1, 1); else if (mode == 2) L(1, 2); else if (mode == 3) L(1, 3); else L(1, 4); }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }

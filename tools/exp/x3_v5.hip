@@ -20,11 +20,7 @@
 //
 // Pipeline.  K is walked in 16-channel chunks (one 32×32×16 MFMA step per tap).  Each chunk's halo tile (18 × 34
 // records of 64 B) and weights are copied HBM/L2 -> LDS by LDS-DMA (global_load_lds_dwordx4: no VGPR round trip, no
-// ds_write) into one of two LDS stages while the MFMAs consume the other stage.  LDS is laid out [in0|in1|w0|w1] and
-// the chunk loop is unrolled by two, so every fragment address is a per-lane register computed once per workgroup
-// plus an immediate offset (no address arithmetic per tap); DMA source offsets are also computed once.  Fragments
-// of tap t+1 are read while tap t's MFMAs run, and the MFMAs are issued product-major over the independent
-// accumulators.  Records are 64 B (4 × 16-B slots)
+// ds_write) into one of two LDS stages while the MFMAs consume the other stage.  Records are 64 B (4 × 16-B slots)
 // with the slot index XOR-swizzled by (record>>2)&3, applied on the DMA source address (the DMA destination is
 // lane-linear), so the 16 lanes of every ds_read_b128 group hit 16 distinct slots.  Out-of-range halo pixels and
 // the channels past cin of a partial chunk are fetched from a zero page.
@@ -88,8 +84,8 @@ __device__ __forceinline__ bool store_group(unsigned char *p, const float v[8]) 
 // byte offset of logical 16-B slot s of record r inside a stage region
 __device__ __forceinline__ int slot_off(int r, int s) { return r * REC + ((s ^ ((r >> 2) & 3)) << 4); }
 
-template <int NT, int TS>
-__global__ __launch_bounds__(NTHR, 1) void conv_x3_kernel(X3Params p) {
+template <int NT, int TS, int MODE>
+__global__ __launch_bounds__(NTHR, 1) void conv_x3_v5(X3Params p) {
     constexpr int T = TS * TS;
     constexpr int N = NT * 32;
     constexpr int W_RECS = T * N;
@@ -227,11 +223,11 @@ __global__ __launch_bounds__(NTHR, 1) void conv_x3_kernel(X3Params p) {
     dma(0, 0);
     for (int j = 0; j < nchunk; j += 2) {
         __syncthreads();
-        if (j + 1 < nchunk) dma(j + 1, 1);
+        if (j + 1 < nchunk && MODE != 1) dma(j + 1, 1);
         if (mvalid[0]) compute(lds, lds + 2 * IN_B);
         if (j + 1 >= nchunk) break;
         __syncthreads();
-        if (j + 2 < nchunk) dma(j + 2, 0);
+        if (j + 2 < nchunk && MODE != 1) dma(j + 2, 0);
         if (mvalid[0]) compute(lds + IN_B, lds + 2 * IN_B + W_B);
     }
 
@@ -299,56 +295,32 @@ __global__ __launch_bounds__(NTHR, 1) void conv_x3_kernel(X3Params p) {
                 store_group(reinterpret_cast<unsigned char *>(o.out2) + (opix * o.out2_cp + o.out2_coff + c) * 4, v);
         }
     }
-    if (!ok && p.overflow) atomicOr(p.overflow, 1);
+    if (!ok && p.overflow && MODE != 1) atomicOr(p.overflow, 1);
 }
 
-int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const void *w, const float *bias,
-              float w_scale, int cout, int taps_side, int ty0, int tx0, const esr_conv_out *o, int *overflow,
-              hipStream_t stream) {
-    if (!in || !w || !bias || !o || !o->out) return ESR_EINVAL;
-    if (B <= 0 || H <= 0 || W <= 0 || cin <= 0 || cout <= 0 || cout > 64 || !(w_scale > 0.f)) return ESR_EINVAL;
-    if (cin % 8 || in_cp % 8 || in_cp < cin) return ESR_EINVAL;
-    if (!o->out_planar && (cout % 8 || o->out_cp % 8 || o->out_coff % 8 || o->out_coff + cout > o->out_cp))
-        return ESR_EINVAL;
-    if ((o->r1 && (o->r1_cp % 8 || o->r1_coff % 8)) || (o->r2 && (o->r2_cp % 8 || o->r2_coff % 8)) ||
-        (o->out2 && (o->out2_cp % 8 || o->out2_coff % 8)))
-        return ESR_EINVAL;
-    if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(w)) & 15) return ESR_EINVAL;
+}  // namespace
+
+extern "C" int x3exp_conv(int mode, const void *in, int B, int H, int W, int in_cp, int cin, const void *w,
+                          const float *bias, float w_scale, int cout, const esr_conv_out *o, int *overflow,
+                          void *stream) {
     X3Params p;
     p.in = static_cast<const unsigned char *>(in);
     p.B = B; p.H = H; p.W = W; p.in_cp = in_cp; p.cin = cin;
     p.w = static_cast<const unsigned char *>(w);
     p.bias = bias; p.w_scale_inv = 1.f / w_scale; p.cout = cout;
-    p.tap_y0 = ty0; p.tap_x0 = tx0;
+    p.tap_y0 = 0; p.tap_x0 = 0;
     p.tiles_x = (W + TWF - 1) / TWF;
     p.tiles_y = (B * (H + 2) - 2 + TH - 1) / TH;
     p.overflow = overflow;
     p.o = *o;
     const dim3 grid((unsigned)(p.tiles_x * p.tiles_y)), block(NTHR);
-    if (taps_side == 3) {
-        if (cout > 32) hipLaunchKernelGGL((conv_x3_kernel<2, 3>), grid, block, 0, stream, p);
-        else hipLaunchKernelGGL((conv_x3_kernel<1, 3>), grid, block, 0, stream, p);
+    hipStream_t s = (hipStream_t)stream;
+    if (mode == 1) {
+        if (cout > 32) hipLaunchKernelGGL((conv_x3_v5<2, 3, 1>), grid, block, 0, s, p);
+        else hipLaunchKernelGGL((conv_x3_v5<1, 3, 1>), grid, block, 0, s, p);
     } else {
-        if (cout > 32) hipLaunchKernelGGL((conv_x3_kernel<2, 2>), grid, block, 0, stream, p);
-        else hipLaunchKernelGGL((conv_x3_kernel<1, 2>), grid, block, 0, stream, p);
+        if (cout > 32) hipLaunchKernelGGL((conv_x3_v5<2, 3, 0>), grid, block, 0, s, p);
+        else hipLaunchKernelGGL((conv_x3_v5<1, 3, 0>), grid, block, 0, s, p);
     }
-    return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
-}
-
-}  // namespace
-
-extern "C" int esr_conv3x3_fwd_x3(const void *in, int32_t B, int32_t H, int32_t W, int32_t in_cp, int32_t cin,
-                                  const void *w_packed, const float *bias, float w_scale, int32_t cout,
-                                  const esr_conv_out *o, int32_t *overflow, esr_stream_t stream) {
-    return launch_x3(in, B, H, W, in_cp, cin, w_packed, bias, w_scale, cout, 3, 0, 0, o, overflow,
-                     (hipStream_t)stream);
-}
-
-extern "C" int esr_upconv2x_phase_fwd_x3(const void *in, int32_t B, int32_t H, int32_t W, int32_t in_cp, int32_t cin,
-                                         const void *w_packed, const float *bias, float w_scale, int32_t cout,
-                                         int32_t py, int32_t px, const esr_conv_out *o, int32_t *overflow,
-                                         esr_stream_t stream) {
-    if (py < 0 || py > 1 || px < 0 || px > 1) return ESR_EINVAL;
-    return launch_x3(in, B, H, W, in_cp, cin, w_packed, bias, w_scale, cout, 2, py, px, o, overflow,
-                     (hipStream_t)stream);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
