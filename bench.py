@@ -9,7 +9,8 @@ HBM, producing B 512×512 HR images.  Multi-GPU: images are independent, so each
 no collective in the data path); timing is barrier + synchronize bracketed and the max over ranks is reported.
 
 One JSON line on rank 0: value = HR Mpixels/s over all ranks; `roofline` = the dominant kernel (the 3×3 conv
-instantiation that takes the most time) from HIP events around every launch in the timed region; `cpu_baseline` =
+instantiation that takes the most time) from HIP events around every launch in the timed region (recorded natively by
+the op-list executor esr_run_ops, so the timing adds no host round trips); `cpu_baseline` =
 the CPU oracle restatement (oracle/esr_oracle.py, PyTorch-CPU oneDNN convs) on a bounded sample, rank 0 only.
 """
 import argparse
@@ -162,8 +163,7 @@ def main():
     value = total_px / dt / 1e6
     # roofline of the dominant kernel from the per-launch events
     per = {}
-    for tag, flops, s, e in prof:
-        ms = s.elapsed_time(e)
+    for tag, flops, ms in engine.profile_records(prof):
         a = per.setdefault(tag, [0, 0.0, 0.0])
         a[0] += 1
         a[1] += flops

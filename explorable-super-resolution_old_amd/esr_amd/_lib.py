@@ -8,7 +8,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('ESR_AMD_LIB', os.path.join(_HERE, 'libesr_amd.so'))
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 c_int = ctypes.c_int32
 c_float = ctypes.c_float
@@ -27,7 +27,15 @@ class ConvOut(ctypes.Structure):
                 ('out2', c_void_p), ('out2_cp', c_int), ('out2_coff', c_int)]
 
 
-# name -> argtypes (all return int32 status)
+class EsrOp(ctypes.Structure):
+    """Mirror of `esr_op` (include/esr_amd.h): one recorded launch of an op list (esr_run_ops)."""
+    _fields_ = [('kind', c_int), ('tag', c_int), ('p', c_void_p * 10), ('i', c_int * 20), ('f', c_float * 2),
+                ('o', ConvOut)]
+
+
+OP_CONV3X3, OP_CONV3X3_X3, OP_UPCONV, OP_UPCONV_X3, OP_PREP, OP_CEM_DOWN, OP_CEM_INV, OP_CEM_UP_ADD = range(1, 9)
+
+# name -> argtypes (all return int32 status unless listed in _RESTYPES)
 _SIGNATURES = {
     'esr_conv3x3_fwd': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
                         ctypes.POINTER(ConvOut), c_void_p],
@@ -57,8 +65,14 @@ _SIGNATURES = {
                         c_float, c_int, c_void_p, c_void_p],
     'esr_input_adjoint': [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int,
                           c_int, c_void_p, c_void_p],
+    'esr_timer_create': [c_int],
+    'esr_timer_elapsed': [c_void_p, c_fp],
+    'esr_timer_destroy': [c_void_p],
+    'esr_run_ops': [ctypes.POINTER(EsrOp), c_int, c_void_p, c_void_p],
+    'esr_op_size': [],
     'esr_abi_version': [],
 }
+_RESTYPES = {'esr_timer_create': c_void_p, 'esr_timer_destroy': None}
 EXPORTED = tuple(_SIGNATURES)
 
 _lib = None
@@ -80,10 +94,13 @@ def load():
     for name, argtypes in _SIGNATURES.items():
         fn = getattr(lib, name)
         fn.argtypes = argtypes
-        fn.restype = c_int
+        fn.restype = _RESTYPES.get(name, c_int)
     v = lib.esr_abi_version()
     if v != ABI_VERSION:
         raise ESRLibraryError('libesr_amd.so ABI %d != expected %d (stale build?)' % (v, ABI_VERSION))
+    if lib.esr_op_size() != ctypes.sizeof(EsrOp):
+        raise ESRLibraryError('esr_op layout mismatch: C %d bytes, binding %d' % (lib.esr_op_size(),
+                                                                                  ctypes.sizeof(EsrOp)))
     _lib = lib
     return lib
 

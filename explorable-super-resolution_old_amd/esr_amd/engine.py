@@ -216,6 +216,7 @@ class _Packed:
 
     def refresh(self):
         self.plan.refresh()
+        self.version = getattr(self, 'version', 0) + 1  # invalidates recorded op lists (new x3 weight tensors)
         for cw in self.planned:
             cw._x3 = None
         # the upsampler phases are sums of taps (not a permutation): packed directly, 8 small tensors
@@ -289,6 +290,152 @@ def _conv_out(out, cp, coff, oh, ow, lrelu, sy=1, sx=1, oy=0, ox=0, planar=0, r1
 
 
 # ----------------------------------------------------------------------------------------------------------------------
+# op lists: a forward recorded once, replayed natively (esr_run_ops)
+# ----------------------------------------------------------------------------------------------------------------------
+class _Recorder:
+    """Stands in for the library inside `_forward`: every launch becomes an esr_op record (include/esr_amd.h) instead
+    of being issued.  Tensors allocated during recording are kept alive by the recorder (`keep`)."""
+
+    def __init__(self):
+        self.ops, self.tags, self.keep = [], [], []
+        self._tag = None
+
+    def tag(self, name, flops):
+        self._tag = (name, flops)
+
+    def _add(self, kind, p, i, f=(), o=None):
+        op = _lib.EsrOp()
+        op.kind = kind
+        for k, v in enumerate(p):
+            op.p[k] = v
+        for k, v in enumerate(i):
+            op.i[k] = v
+        for k, v in enumerate(f):
+            op.f[k] = v
+        if o is not None:
+            op.o = o._obj if hasattr(o, '_obj') else o
+        self.ops.append(op)
+        self.tags.append(self._tag)
+        self._tag = None
+        return 0
+
+    def esr_conv3x3_fwd(self, inp, B, H, W, in_cp, cin, w, bias, cout, o, stream):
+        return self._add(_lib.OP_CONV3X3, [inp, w, bias], [B, H, W, in_cp, cin, cout], o=o)
+
+    def esr_conv3x3_fwd_x3(self, inp, B, H, W, in_cp, cin, w, bias, w_scale, cout, o, ovf, stream):
+        return self._add(_lib.OP_CONV3X3_X3, [inp, w, bias, ovf], [B, H, W, in_cp, cin, cout], [w_scale], o=o)
+
+    def esr_upconv2x_phase_fwd(self, inp, B, H, W, in_cp, cin, w, bias, cout, py, px, o, stream):
+        return self._add(_lib.OP_UPCONV, [inp, w, bias], [B, H, W, in_cp, cin, cout, py, px], o=o)
+
+    def esr_upconv2x_phase_fwd_x3(self, inp, B, H, W, in_cp, cin, w, bias, w_scale, cout, py, px, o, ovf, stream):
+        return self._add(_lib.OP_UPCONV_X3, [inp, w, bias, ovf], [B, H, W, in_cp, cin, cout, py, px], [w_scale], o=o)
+
+    def esr_prep_input(self, x, B, nz, h, w, sf, m, lr, first, first_cp, first_lr_off, zlr, zlr_cp, n_zlr, zhr,
+                       zhr_cp, n_zhr, split, stream):
+        return self._add(_lib.OP_PREP, [x, lr, first] + [zlr[k] for k in range(4)] + [zhr[k] for k in range(2)],
+                         [B, nz, h, w, sf, m, first_cp, first_lr_off] + [zlr_cp[k] for k in range(4)] + [n_zlr] +
+                         [zhr_cp[k] for k in range(2)] + [n_zhr, split])
+
+    def esr_cem_down(self, gen, lr, r, B, H, W, sf, ph, w, kd, negate, stream):
+        return self._add(_lib.OP_CEM_DOWN, [gen, lr, r, w], [B, H, W, sf, ph, kd, negate])
+
+    def esr_cem_inv(self, r, q, B, H, W, w, ki, stream):
+        return self._add(_lib.OP_CEM_INV, [r, q, w], [B, H, W, ki])
+
+    def esr_cem_up_add(self, q, gen, out, B, H, W, sf, ph, w, kd, M, stream):
+        return self._add(_lib.OP_CEM_UP_ADD, [q, gen, out, w], [B, H, W, sf, ph, kd, M])
+
+
+class _OpPlan:
+    """One recorded inference forward.  Between calls only the model-input pointer and the output pointer change;
+    they are patched in place and the whole list runs in one esr_run_ops call."""
+
+    def __init__(self, key, net, x, cem, precision):
+        rec = _Recorder()
+        out, ws = _forward(net, x, cem, precision, rec=rec)
+        self.key, self.ws, self.keep, self.tags = key, ws, rec.keep, rec.tags
+        self.n = len(rec.ops)
+        self.ops = (_lib.EsrOp * self.n)(*rec.ops)
+        self.out_shape = tuple(out.shape)
+        xp, op_ = x.data_ptr(), out.data_ptr()
+        self.x_sites, self.out_sites = [], []
+        for k in range(self.n):
+            for j in range(10):
+                if self.ops[k].p[j] == xp:
+                    self.x_sites.append((k, j))
+                elif self.ops[k].p[j] == op_:
+                    self.out_sites.append((k, j))
+            if self.ops[k].o.out == op_:
+                self.out_sites.append((k, -1))
+        if not self.x_sites or not self.out_sites:
+            raise RuntimeError('esr_amd: op-list recording did not find the input/output of the forward')
+
+    def run(self, x):
+        lib = _lib.load()
+        out = torch.empty(self.out_shape, device=x.device, dtype=torch.float32)
+        for k, j in self.x_sites:
+            self.ops[k].p[j] = x.data_ptr()
+        for k, j in self.out_sites:
+            if j < 0:
+                self.ops[k].o.out = out.data_ptr()
+            else:
+                self.ops[k].p[j] = out.data_ptr()
+        timer = None
+        if _PROFILE is not None:
+            timer = lib.esr_timer_create(self.n)
+            if not timer:
+                raise RuntimeError('esr_amd: esr_timer_create failed')
+            _PROFILE.append(('ops', self.tags, timer, self.n))
+        stream = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+        _lib.check(lib.esr_run_ops(self.ops, self.n, timer, stream), 'esr_run_ops')
+        return out
+
+
+def profile_records(prof):
+    """(tag, flops, ms) of every profiled launch in `prof` (engine._PROFILE list): op-list entries are read from
+    their native HIP-event timers (and the timers freed), direct-launch entries from torch events."""
+    lib = _lib.load()
+    for entry in prof:
+        if entry[0] == 'ops':
+            _, tags, timer, n = entry
+            ms = (ctypes.c_float * n)()
+            _lib.check(lib.esr_timer_elapsed(timer, ms), 'esr_timer_elapsed')
+            lib.esr_timer_destroy(timer)
+            for k in range(n):
+                if tags[k] is not None:
+                    yield tags[k][0], tags[k][1], ms[k]
+        else:
+            tag, flops, start, end = entry
+            yield tag, flops, start.elapsed_time(end)
+
+
+USE_OP_LISTS = os.environ.get('ESR_OP_LISTS', '1') != '0'
+
+
+def _plan_key(net, x, cem, precision, pk):
+    pre_pad = cem is not None and cem.pre_pad
+    cem_key = None
+    if cem is not None:
+        cem_key = (id(cem), pre_pad, int(cem.margins_LR),
+                   cem.DownscaleOP.Filter_OP.weight.data_ptr(), cem.Conv_LR_with_Inv_hTh_OP.Filter_OP.weight.data_ptr(),
+                   cem.Upscale_OP.Filter_OP.weight.data_ptr())
+    return (id(pk), getattr(pk, 'version', 0), precision, tuple(x.shape), str(x.device), cem_key)
+
+
+def _planned_forward(net, x, cem, precision):
+    pk = _packed(net, net.latent_input is not None)
+    key = _plan_key(net, x, cem, precision, pk)
+    plans = net._esr_cache.setdefault('plans', {})
+    plan = plans.get(precision)
+    if plan is None or plan.key != key:
+        plans.pop(precision, None)
+        plan = _OpPlan(key, net, x, cem, precision)
+        plans[precision] = plan
+    return plan.run(x), plan.ws
+
+
+# ----------------------------------------------------------------------------------------------------------------------
 # forward
 # ----------------------------------------------------------------------------------------------------------------------
 def generator_forward(net, x, cem=None):
@@ -302,19 +449,24 @@ def generator_forward(net, x, cem=None):
     precision = getattr(net, 'esr_precision', None) or DEFAULT_PRECISION
     if precision not in PRECISIONS:
         raise ValueError('esr_precision must be one of %s' % (PRECISIONS,))
-    out, ws = _forward(net, x.contiguous(), cem, precision)
+    x = x.contiguous()
+    if USE_OP_LISTS:
+        out, ws = _planned_forward(net, x, cem, precision)
+    else:
+        out, ws = _forward(net, x, cem, precision)
     if precision == 'x3':
         if int(ws.overflow.item()):  # one 4-byte D2H per forward
             OVERFLOW_RERUNS += 1
             ws.overflow.zero_()
-            out, _ = _forward(net, x.contiguous(), cem, 'f32')
+            out, _ = _forward(net, x, cem, 'f32')
     return out
 
 
-def _forward(net, x, cem, precision, train_ws=None):
+def _forward(net, x, cem, precision, train_ws=None, rec=None):
     """One generator (+CEM) forward.  With `train_ws` (esr_amd.train_engine) every RDB's concat buffer is kept for
-    the backward pass instead of the inference ping-pong, and the workspace comes from the caller."""
-    lib = _lib.load()
+    the backward pass instead of the inference ping-pong, and the workspace comes from the caller.  With `rec` (a
+    _Recorder) the launches are recorded as an op list instead of issued."""
+    lib = rec if rec is not None else _lib.load()
     x3 = precision == 'x3'
     latent = net.latent_input is not None
     nz = net.nl if latent else 0
@@ -364,7 +516,10 @@ def _forward(net, x, cem, precision, train_ws=None):
     tagp = 'x3_' if x3 else ''
 
     def conv(inp, h_, w_, in_cp, cin, cw, cout, o, cin_ref):
-        if prof is not None:
+        ev = None
+        if rec is not None:
+            rec.tag('%sconv3x3_n%d' % (tagp, 32 if cout <= 32 else 64), 2.0 * Bn * h_ * w_ * 9 * cin_ref * cout)
+        elif prof is not None:
             ev = _prof_begin(prof, '%sconv3x3_n%d' % (tagp, 32 if cout <= 32 else 64), 2.0 * Bn * h_ * w_ * 9 * cin_ref * cout)
         if x3:
             wx, scale = cw.x3()
@@ -374,7 +529,7 @@ def _forward(net, x, cem, precision, train_ws=None):
             rc = lib.esr_conv3x3_fwd(inp.data_ptr(), Bn, h_, w_, in_cp, cin, cw.f32.data_ptr(), cw.bias.data_ptr(),
                                      cout, ctypes.byref(o), stream)
         _lib.check(rc, 'esr_conv3x3_fwd' + ('_x3' if x3 else ''))
-        if prof is not None:
+        if ev is not None:
             ev.record()
 
     nl = 3 if latent else 0  # reference latent channels concatenated into a conv input (FLOP accounting)
@@ -402,7 +557,10 @@ def _forward(net, x, cem, precision, train_ws=None):
         for ph, cw in enumerate(phw):
             py, px = ph // 2, ph % 2
             o = _conv_out(dst, dcp, dcoff, 2 * sh, 2 * sw, True, sy=2, sx=2, oy=py, ox=px)
-            if prof is not None:  # reference FLOPs: a 3×3 conv at 2× resolution, a quarter of it per phase
+            ev = None  # reference FLOPs: a 3×3 conv at 2× resolution, a quarter of it per phase
+            if rec is not None:
+                rec.tag(tagp + 'upconv2x_phase', 2.0 * Bn * (2 * sh) * (2 * sw) * 9 * 64 * 64 / 4)
+            elif prof is not None:
                 ev = _prof_begin(prof, tagp + 'upconv2x_phase', 2.0 * Bn * (2 * sh) * (2 * sw) * 9 * 64 * 64 / 4)
             if x3:
                 wx, scale = cw.x3()
@@ -412,11 +570,13 @@ def _forward(net, x, cem, precision, train_ws=None):
                 rc = lib.esr_upconv2x_phase_fwd(src.data_ptr(), Bn, sh, sw, 64, 64, cw.f32.data_ptr(),
                                                 cw.bias.data_ptr(), 64, py, px, ctypes.byref(o), stream)
             _lib.check(rc, 'esr_upconv2x_phase_fwd')
-            if prof is not None:
+            if ev is not None:
                 ev.record()
     HH, WW = SF * H, SF * W
     conv(HR0, HH, WW, hcp, hcp, pk.hr0, 64, _conv_out(HR1, hcp, zc, HH, WW, True), nl + 64)
     gen = torch.empty(Bn, 3, HH, WW, device=dev, dtype=torch.float32)
+    if rec is not None:
+        rec.keep.append(gen)
     conv(HR1, HH, WW, hcp, hcp, pk.hr1, 3, _conv_out(gen, 0, 0, HH, WW, False, planar=1), nl + 64)
     if cem is None:
         return gen, ws
@@ -434,6 +594,8 @@ def cem_apply(lib, cem, gen, lr, Bn, H, W, M, stream):
     kd, ki = wd.shape[-1], wi.shape[-1]
     r = torch.empty(Bn, 3, H, W, device=dev, dtype=torch.float32)
     q = torch.empty_like(r)
+    if hasattr(lib, 'keep'):  # recording an op list: the intermediates must outlive this call
+        lib.keep += [r, q]
     out = torch.empty(Bn, 3, SF * H - 2 * M, SF * W - 2 * M, device=dev, dtype=torch.float32)
     _lib.check(lib.esr_cem_down(gen.data_ptr(), lr.data_ptr(), r.data_ptr(), Bn, H, W, SF, CEM_PHASE,
                                 wd[0, 0].contiguous().data_ptr(), kd, 0, stream), 'esr_cem_down')

@@ -112,8 +112,8 @@ int esr_cem_up_add(const float *q, const float *gen, float *out, int32_t B, int3
 /* ---- split-precision ("x3") path --------------------------------------------------------------------------------
  * Split activation layout: padded NHWC as above, 4 bytes per channel, channels in groups of 8; group g of a pixel is
  * 32 bytes: f16 hi[8] then f16 lo[8] with hi = f16(v), lo = f16(v - hi) (|v - hi - lo| <= 2^-22 |v|).  cp, cin and
- * every channel offset are multiples of 8.  Packed x3 weights: [nchunk][taps][n_pad][32 channels as 4 split groups]
- * (128 B per (tap, n)), scaled by `w_scale` (a power of two the epilogue divides out exactly).
+ * every channel offset are multiples of 8.  Packed x3 weights: [nchunk16][taps][n_pad][16 channels as 2 split groups]
+ * (64 B per (tap, n)), scaled by `w_scale` (a power of two the epilogue divides out exactly).
  * Products are a_hi·b_hi + a_hi·b_lo + a_lo·b_hi on v_mfma_f32_32x32x16_f16 with fp32 accumulation.
  * Outputs are split unless o->out_planar (fp32 NCHW).  r1/r2 residual inputs are split.  *overflow is OR-ed with 1
  * if any split output is not representable (|v| >= 65504), in which case the caller reruns the exact-fp32 path. */
@@ -171,6 +171,45 @@ int esr_cem_adjoint(const float *g, int32_t planes, int32_t Oy, int32_t Ox, cons
 int esr_input_adjoint(const float *d_hr, int32_t hr_cp, int32_t hr_coff, const float *d_lr, int32_t lr_cp,
                       int32_t lr_coff, int32_t sf, const float *d_pl, int32_t C, int32_t B, int32_t Hp, int32_t Wp,
                       int32_t M, float *out, esr_stream_t stream);
+
+/* ---- op lists (host-side executor, esr_plan.hip) -----------------------------------------------------------------
+ * A generator (+CEM) forward is a fixed sequence of the launches above (≈360 for RRDB-23).  The host layer records it
+ * once per (workspace, weights, shape) as an array of esr_op and replays it with one esr_run_ops call, patching only
+ * the input / output pointers between calls; esr_run_ops optionally brackets every op with HIP events (esr_timer_*)
+ * for per-kernel timing inside the benchmark's timed region.  Argument order per kind (p = pointers, i = int32s):
+ *   CONV3X3     p: in, w, bias           i: B, H, W, in_cp, cin, cout              + o
+ *   CONV3X3_X3  p: in, w, bias, overflow i: B, H, W, in_cp, cin, cout   f0: w_scale + o
+ *   UPCONV      p: in, w, bias           i: B, H, W, in_cp, cin, cout, py, px      + o
+ *   UPCONV_X3   p: in, w, bias, overflow i: B, H, W, in_cp, cin, cout, py, px  f0 + o
+ *   PREP        p: x, lr_nchw, first, zlr[4], zhr[2]
+ *               i: B, nz, h, w, sf, m, first_cp, first_lr_off, zlr_cp[4], n_zlr, zhr_cp[2], n_zhr, split
+ *   CEM_DOWN    p: gen, lr, r, w_down    i: B, H, W, sf, ph, kd, negate
+ *   CEM_INV     p: r, q, w_inv           i: B, H, W, ki
+ *   CEM_UP_ADD  p: q, gen, out, w_up     i: B, H, W, sf, ph, kd, M                              */
+enum esr_op_kind {
+    ESR_OP_CONV3X3 = 1,
+    ESR_OP_CONV3X3_X3 = 2,
+    ESR_OP_UPCONV = 3,
+    ESR_OP_UPCONV_X3 = 4,
+    ESR_OP_PREP = 5,
+    ESR_OP_CEM_DOWN = 6,
+    ESR_OP_CEM_INV = 7,
+    ESR_OP_CEM_UP_ADD = 8,
+};
+typedef struct esr_op {
+    int32_t kind;
+    int32_t tag; /* caller's label (profiling) */
+    const void *p[10];
+    int32_t i[20];
+    float f[2];
+    esr_conv_out o;
+} esr_op;
+typedef void *esr_timer_t;
+esr_timer_t esr_timer_create(int32_t n_ops);            /* n_ops + 1 HIP events; NULL on failure */
+int esr_timer_elapsed(esr_timer_t timer, float *ms);    /* waits; ms[k] = duration of op k of the last run */
+void esr_timer_destroy(esr_timer_t timer);
+int esr_run_ops(const esr_op *ops, int32_t n, esr_timer_t timer, esr_stream_t stream);
+int esr_op_size(void);                                  /* sizeof(esr_op), checked by the binding */
 
 /* Library / ABI version (bumped on any signature change). */
 int esr_abi_version(void);

@@ -113,12 +113,13 @@ def test_upconv_polyphase_fold_equals_nearest_then_conv():
 
 def test_library_exports_every_header_symbol():
     hdr = open(os.path.join(REPO, 'include', 'esr_amd.h')).read()
-    declared = sorted(set(re.findall(r'^int\s+(esr_\w+)\s*\(', hdr, flags=re.M)))
+    declared = sorted(set(re.findall(r'^(?:int|void|esr_timer_t)\s+(esr_\w+)\s*\(', hdr, flags=re.M)))
     assert declared and set(declared) == set(_lib.EXPORTED)
     lib = ctypes.CDLL(_lib.LIB_PATH)
     for s in declared:
         assert hasattr(lib, s), s
     assert _lib.load().esr_abi_version() == _lib.ABI_VERSION
+    assert lib.esr_op_size() == ctypes.sizeof(_lib.EsrOp)  # op-list record layout matches the binding
 
 
 def test_product_path_refuses_cpu_tensors():
