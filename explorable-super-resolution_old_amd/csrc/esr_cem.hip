@@ -97,6 +97,81 @@ __global__ __launch_bounds__(NT) void cem_up_add_kernel(const float *__restrict_
     out[idx] = gen[(plane * HH + Y + M) * WW + X + M] + acc;
 }
 
+// ---- tiled forms (the launchers use these; the direct kernels above remain for the general stride phase) ----------
+// Down: a 16×16 block of LR outputs of one plane stages its replicate-clamped HR window ((15·sf+kd)² values) in LDS,
+// de-interleaved by column phase (x mod sf) so that lanes reading columns sf·j + v hit consecutive words.
+template <int sf>
+__global__ __launch_bounds__(256) void cem_down_tiled(const float *__restrict__ gen, const float *__restrict__ lr,
+                                                      float *__restrict__ r, int H, int W, int ph,
+                                                      const float *__restrict__ wd, int kd, int negate) {
+    extern __shared__ float smem[];
+    const int WH = 15 * sf + kd;              // window rows = cols
+    const int P = (WH + sf - 1) / sf + 1;     // de-interleaved row pitch (+1: bank spread)
+    float *sw = smem;                         // kd*kd weights
+    float *s = smem + ((kd * kd + 3) & ~3);   // [sf][WH][P]
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    const int j0 = blockIdx.x * 16, i0 = blockIdx.y * 16;
+    const long long plane = blockIdx.z;
+    const int HH = sf * H, WW = sf * W, pd = kd / 2;
+    const float *g = gen + plane * HH * WW;
+    for (int k = threadIdx.x; k < kd * kd; k += 256) sw[k] = wd[k];
+    const int Y0 = sf * i0 + ph - pd, X0 = sf * j0 + ph - pd;
+    for (int k = threadIdx.x; k < WH * WH; k += 256) {
+        const int y = k / WH, x = k - y * WH;
+        const float v = g[(long long)clampi(Y0 + y, 0, HH - 1) * WW + clampi(X0 + x, 0, WW - 1)];
+        s[((x % sf) * WH + y) * P + x / sf] = v;
+    }
+    __syncthreads();
+    const int i = i0 + ty, j = j0 + tx;
+    if (i >= H || j >= W) return;
+    float acc = 0.f;
+    for (int u = 0; u < kd; ++u) {
+        const float *wrow = sw + u * kd;
+        const float *srow = s + (sf * ty + u) * P + tx;
+        for (int v0 = 0; v0 < kd; v0 += sf) {  // v = v0 + ph_: phase ph_, de-interleaved index v0/sf
+#pragma unroll
+            for (int ph_ = 0; ph_ < sf; ++ph_)
+                if (v0 + ph_ < kd) acc += wrow[v0 + ph_] * srow[ph_ * WH * P + v0 / sf];
+        }
+    }
+    const long long idx = (plane * H + i) * W + j;
+    const float out = (lr ? lr[idx] : 0.f) - acc;
+    r[idx] = negate ? -out : out;
+}
+
+// Up + back-projection + crop, for stride phases whose clamped border rows/columns are not stuffed rows
+// (0 < ph < sf-1: replicate padding of the zero-stuffed grid then reads zeros): only the ≈(kd/sf)² taps that land on
+// stuffed samples are visited, with no modulo in the tap loops.
+template <int sf>
+__global__ __launch_bounds__(256) void cem_up_add_phase(const float *__restrict__ q, const float *__restrict__ gen,
+                                                        float *__restrict__ out, int H, int W, int ph,
+                                                        const float *__restrict__ wu, int kd, int M) {
+    __shared__ float sw[MAXK * MAXK];
+    for (int k = threadIdx.x; k < kd * kd; k += 256) sw[k] = wu[k];
+    __syncthreads();
+    const int HH = sf * H, WW = sf * W, OH = HH - 2 * M, OW = WW - 2 * M;
+    const int X = blockIdx.x * 64 + (threadIdx.x & 63), Y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const long long plane = blockIdx.z;
+    if (X >= OW || Y >= OH) return;
+    const int pd = kd / 2, Yp = Y + M, Xp = X + M;
+    // first tap on a stuffed row/column: (Yp + u - pd - ph) ≡ 0 (mod sf); the +sf·kd keeps the operand positive
+    const int u0 = (pd + ph - Yp + sf * (Yp + kd)) % sf, v0 = (pd + ph - Xp + sf * (Xp + kd)) % sf;
+    const float *qp = q + plane * H * W;
+    float acc = 0.f;
+    for (int u = u0; u < kd; u += sf) {
+        const int py = Yp + u - pd;
+        if (py < 0 || py >= HH) continue;
+        const float *qrow = qp + (long long)((py - ph) / sf) * W;
+        const float *wrow = sw + u * kd;
+        for (int v = v0; v < kd; v += sf) {
+            const int px = Xp + v - pd;
+            if (px < 0 || px >= WW) continue;
+            acc += wrow[v] * qrow[(px - ph) / sf];
+        }
+    }
+    out[(plane * OH + Y) * OW + X] = gen[(plane * HH + Yp) * WW + Xp] + acc;
+}
+
 // ---- model-input preparation ----
 
 struct PrepParams {
@@ -191,8 +266,15 @@ extern "C" int esr_cem_down(const float *gen, const float *lr, float *r, int32_t
     if (!gen || !r || !w_down || B <= 0 || H <= 0 || W <= 0 || sf <= 0 || kd <= 0 || kd > MAXK || !(kd & 1) ||
         ph < 0 || ph >= sf)
         return ESR_EINVAL;
-    hipLaunchKernelGGL(cem_down_kernel, dim3(nblocks((long long)B * 3 * H * W)), dim3(NT), 0, (hipStream_t)stream,
-                       gen, lr, r, B, H, W, sf, ph, w_down, kd, negate);
+    const int WH = 15 * sf + kd, P = (WH + sf - 1) / sf + 1;
+    const size_t lds = 4 * (((kd * kd + 3) & ~3) + (size_t)sf * WH * P);
+    if (sf == 4 && lds <= 64 * 1024) {
+        hipLaunchKernelGGL(cem_down_tiled<4>, dim3((W + 15) / 16, (H + 15) / 16, B * 3), dim3(256), lds,
+                           (hipStream_t)stream, gen, lr, r, H, W, ph, w_down, kd, negate);
+    } else {
+        hipLaunchKernelGGL(cem_down_kernel, dim3(nblocks((long long)B * 3 * H * W)), dim3(NT), 0, (hipStream_t)stream,
+                           gen, lr, r, B, H, W, sf, ph, w_down, kd, negate);
+    }
     return launched();
 }
 
@@ -209,9 +291,14 @@ extern "C" int esr_cem_up_add(const float *q, const float *gen, float *out, int3
     if (!q || !gen || !out || !w_up || B <= 0 || H <= 0 || W <= 0 || sf <= 0 || kd <= 0 || kd > MAXK || !(kd & 1) ||
         ph < 0 || ph >= sf || M < 0 || 2 * M >= sf * H || 2 * M >= sf * W)
         return ESR_EINVAL;
-    const long long n = (long long)B * 3 * (sf * H - 2 * M) * (sf * W - 2 * M);
-    hipLaunchKernelGGL(cem_up_add_kernel, dim3(nblocks(n)), dim3(NT), 0, (hipStream_t)stream, q, gen, out, B, H, W, sf,
-                       ph, w_up, kd, M);
+    if (sf == 4 && ph > 0 && ph < sf - 1) {
+        hipLaunchKernelGGL(cem_up_add_phase<4>, dim3((sf * W - 2 * M + 63) / 64, (sf * H - 2 * M + 3) / 4, B * 3),
+                           dim3(256), 0, (hipStream_t)stream, q, gen, out, H, W, ph, w_up, kd, M);
+    } else {
+        const long long n = (long long)B * 3 * (sf * H - 2 * M) * (sf * W - 2 * M);
+        hipLaunchKernelGGL(cem_up_add_kernel, dim3(nblocks(n)), dim3(NT), 0, (hipStream_t)stream, q, gen, out, B, H,
+                           W, sf, ph, w_up, kd, M);
+    }
     return launched();
 }
 
