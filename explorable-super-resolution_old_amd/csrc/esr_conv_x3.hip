@@ -88,6 +88,108 @@ __device__ __forceinline__ bool store_group(unsigned char *p, const float v[8]) 
 // byte offset of logical 16-B slot s of record r inside a stage region
 __device__ __forceinline__ int slot_off(int r, int s) { return r * REC + ((s ^ ((r >> 2) & 3)) << 4); }
 
+// Epilogue store phase shared by both kernels.  s_ep holds the tile's fp32 accumulators as [pixel q][channel] (pitch
+// N + 4); r_first is the tall padded row of the tile's first output row.  Each thread owns one 8-channel group (so its
+// bias is loaded once) and a fixed list of ITERS pixels; the loop is fully unrolled so every residual / LDS load of the
+// tile is in flight before the first value is finished (the store phase is load-latency-bound otherwise), and the
+// pixel -> (image, row) mapping walks the tall image without per-pixel divisions.  Planar fp32 output (HR_conv1 ->
+// CEM): consecutive lanes take consecutive pixels of one channel plane.  Returns false if a split output left the
+// f16 range.
+__device__ __forceinline__ float split_at(const float *buf, long long pix, int cp, int ch) {
+    const _Float16 *g = reinterpret_cast<const _Float16 *>(buf + pix * cp + (ch & ~7));
+    return (float)g[ch & 7] + (float)g[8 + (ch & 7)];
+}
+
+template <int N>
+__device__ __forceinline__ bool store_tile(const X3Params &p, const float *s_ep, int r_first, int x0, int tw, int nq,
+                                           int tid) {
+    constexpr int EP_P = N + 4;
+    constexpr int GROUPS = N / 8;
+    constexpr int PPI = NTHR / GROUPS;         // pixels per iteration
+    constexpr int ITERS = TH * TWF / PPI;      // 4 (N = 32) or 8 (N = 64)
+    const esr_conv_out &o = p.o;
+    const long long orow = (long long)(o.out_w + 2);
+    const int HP = p.H + 2;
+    const int b0 = r_first / HP;
+    auto locate = [&](int q, long long &opix, int &b, int &oy, int &ox) {
+        const int row = (tw == TWF) ? (q >> 5) : q / tw;
+        const int col = q - row * tw;
+        int yy = r_first + 1 + row - b0 * HP;
+        b = b0;
+        while (yy >= HP) {
+            yy -= HP;
+            ++b;
+        }
+        const int y = yy - 1;
+        oy = o.out_sy * y + o.out_oy;
+        ox = o.out_sx * (x0 + col) + o.out_ox;
+        opix = ((long long)b * (o.out_h + 2) + oy + 1) * orow + ox + 1;
+        return q < nq && b < p.B && y >= 0 && y < p.H;
+    };
+    if (o.out_planar) {
+        for (int u = tid; u < nq * p.cout; u += NTHR) {
+            const int c = u / nq, q = u - c * nq;
+            long long opix;
+            int b, oy, ox;
+            if (!locate(q, opix, b, oy, ox)) continue;
+            float v = s_ep[q * EP_P + c] * p.w_scale_inv + p.bias[c];
+            if (o.lrelu) v = lrelu(v);
+            if (o.r1) v = o.s1 * v + split_at(o.r1, opix, o.r1_cp, o.r1_coff + c);
+            if (o.r2) v = o.s2 * v + split_at(o.r2, opix, o.r2_cp, o.r2_coff + c);
+            o.out[(((long long)b * p.cout + c) * o.out_h + oy) * o.out_w + ox] = v;
+        }
+        return true;
+    }
+    const int g = tid % GROUPS;
+    const int c = 8 * g;
+    if (c >= p.cout) return true;
+    float bk[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bk[j] = (c + j < p.cout) ? p.bias[c + j] : 0.f;
+    long long opix[ITERS];
+    bool val[ITERS];
+#pragma unroll
+    for (int k = 0; k < ITERS; ++k) {
+        int b, oy, ox;
+        val[k] = locate(tid / GROUPS + k * PPI, opix[k], b, oy, ox);
+    }
+    float r1v[ITERS][8], r2v[ITERS][8];
+    if (o.r1) {
+#pragma unroll
+        for (int k = 0; k < ITERS; ++k)
+            if (val[k]) load_group(reinterpret_cast<const unsigned char *>(o.r1) + (opix[k] * o.r1_cp + o.r1_coff + c) * 4,
+                                   r1v[k]);
+    }
+    if (o.r2) {
+#pragma unroll
+        for (int k = 0; k < ITERS; ++k)
+            if (val[k]) load_group(reinterpret_cast<const unsigned char *>(o.r2) + (opix[k] * o.r2_cp + o.r2_coff + c) * 4,
+                                   r2v[k]);
+    }
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < ITERS; ++k) {
+        if (!val[k]) continue;
+        const int q = tid / GROUPS + k * PPI;
+        float v[8];
+        const f32x4 v0 = *reinterpret_cast<const f32x4 *>(s_ep + q * EP_P + c);
+        const f32x4 v1 = *reinterpret_cast<const f32x4 *>(s_ep + q * EP_P + c + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { v[j] = v0[j]; v[j + 4] = v1[j]; }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            v[j] = v[j] * p.w_scale_inv + bk[j];
+            if (o.lrelu) v[j] = lrelu(v[j]);
+            if (o.r1) v[j] = o.s1 * v[j] + r1v[k][j];
+            if (o.r2) v[j] = o.s2 * v[j] + r2v[k][j];
+        }
+        ok &= store_group(reinterpret_cast<unsigned char *>(o.out) + (opix[k] * o.out_cp + o.out_coff + c) * 4, v);
+        if (o.out2)
+            store_group(reinterpret_cast<unsigned char *>(o.out2) + (opix[k] * o.out2_cp + o.out2_coff + c) * 4, v);
+    }
+    return ok;
+}
+
 template <int NT, int TS>
 __global__ __launch_bounds__(NTHR, 1) void conv_x3_kernel(X3Params p) {
     constexpr int T = TS * TS;
@@ -251,56 +353,256 @@ __global__ __launch_bounds__(NTHR, 1) void conv_x3_kernel(X3Params p) {
     }
     __syncthreads();
 
-    const esr_conv_out &o = p.o;
-    const long long orow = (long long)(o.out_w + 2);
-    constexpr int GROUPS = N / 8;
-    bool ok = true;
-    for (int u = tid; u < nq * GROUPS; u += NTHR) {
-        const int q = u / GROUPS, g = u - (u / GROUPS) * GROUPS;
-        const int c = 8 * g;
-        if (c >= p.cout) continue;
-        const int R = r0 + 1 + q / tw;  // tall padded row of this output pixel
-        const int b = R / (p.H + 2);
-        const int y = R - b * (p.H + 2) - 1;
-        if (b >= p.B || y < 0 || y >= p.H) continue;
-        const int x = x0 + q % tw;
-        const int oy = o.out_sy * y + o.out_oy, ox = o.out_sx * x + o.out_ox;
-        const long long opix = ((long long)b * (o.out_h + 2) + oy + 1) * orow + ox + 1;
-        float v[8];
-        const f32x4 v0 = *reinterpret_cast<const f32x4 *>(s_ep + q * EP_P + c);
-        const f32x4 v1 = *reinterpret_cast<const f32x4 *>(s_ep + q * EP_P + c + 4);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) { v[k] = v0[k]; v[k + 4] = v1[k]; }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const float bk = (c + k < p.cout) ? p.bias[c + k] : 0.f;
-            v[k] = v[k] * p.w_scale_inv + bk;
-            if (o.lrelu) v[k] = lrelu(v[k]);
-        }
-        if (o.r1) {
-            float r[8];
-            load_group(reinterpret_cast<const unsigned char *>(o.r1) + (opix * o.r1_cp + o.r1_coff + c) * 4, r);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = o.s1 * v[k] + r[k];
-        }
-        if (o.r2) {
-            float r[8];
-            load_group(reinterpret_cast<const unsigned char *>(o.r2) + (opix * o.r2_cp + o.r2_coff + c) * 4, r);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = o.s2 * v[k] + r[k];
-        }
-        if (o.out_planar) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-                if (c + k < p.cout) o.out[(((long long)b * p.cout + c + k) * o.out_h + oy) * o.out_w + ox] = v[k];
-        } else {
-            ok &= store_group(reinterpret_cast<unsigned char *>(o.out) + (opix * o.out_cp + o.out_coff + c) * 4, v);
-            if (o.out2)
-                store_group(reinterpret_cast<unsigned char *>(o.out2) + (opix * o.out2_cp + o.out2_coff + c) * 4, v);
-        }
-    }
+    const bool ok = store_tile<N>(p, s_ep, r0, x0, tw, nq, tid);
     if (!ok && p.overflow) atomicOr(p.overflow, 1);
 }
+
+// ---- ring variant (N = 32, 3×3): two vertically adjacent tiles per workgroup, 3-deep input ring -------------------
+//
+// The classic kernel above re-stages each chunk's weights for every 512-pixel tile and waits for each chunk's DMA one
+// compute phase after issuing it (two stages is all the LDS allows).  Here a workgroup owns tiles (tx, 2p) and
+// (tx, 2p+1) and walks "units" u = (chunk u/2, tile u&1): the weights of a chunk are staged once for both tiles (half
+// the weight bytes per FLOP), and LDS holds a 2-slot weight ring + a 3-slot input ring (2·18 KB + 3·39 KB = 153 KB), so
+// every input tile and every weight chunk is fetched two units ahead.  The DMAs stay in flight across the barriers:
+// each wave waits with a COUNTED vmcnt for exactly the data the next unit reads (all waves issue the same number of
+// LDS-DMA instructions: short waves re-issue the last piece, rewriting identical bytes), then a raw s_barrier.
+// Per accumulator the MFMA sequence is the classic kernel's, so the two kernels agree bit for bit.
+constexpr int IN_PIECES = IN_RECS / 16;  // 1-KB LDS-DMA wave-instructions per input stage (39)
+
+template <int VM>
+__device__ __forceinline__ void wait_vm_lgkm0() {
+    static_assert(VM >= 0 && VM < 64, "vmcnt");
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(VM) : "memory");
+}
+
+__device__ __forceinline__ void raw_barrier() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// DBG bits (diagnostic builds, esr_x3_set_kernel >= 3; outputs are garbage): 1 = no LDS-DMA in the main loop,
+// 2 = no compute, 4 = fragment reads but no MFMAs, 8 = no barriers, 16 = slot 0 always (immediate LDS offsets),
+// 32 = MFMAs not predicated on mvalid, 64 = no epilogue stores (accumulators kept live), 128 = no epilogue at all.
+template <int NIN, bool STAG, int DBG = 0>
+__global__ __launch_bounds__(NTHR, 1) void conv_x3_ring_kernel(X3Params p) {
+    constexpr int T = 9;
+    constexpr int N = 32;
+    constexpr int W_RECS = T * N;
+    constexpr int IN_B = IN_RECS * REC;
+    constexpr int W_B = W_RECS * REC;
+    constexpr int W_PIECES = W_RECS / 16;
+    constexpr int EP_P = N + 4;
+    constexpr int EP_BYTES = TH * TWF * EP_P * 4;
+    constexpr int RING_BYTES = 2 * W_B + NIN * IN_B;
+    constexpr int LDS_BYTES = RING_BYTES > EP_BYTES ? RING_BYTES : EP_BYTES;
+    constexpr int KIN = (IN_PIECES + NWAVES - 1) / NWAVES;
+    constexpr int KW = (W_PIECES + NWAVES - 1) / NWAVES;
+    static_assert(LDS_BYTES <= 163840, "LDS");
+    __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int hl = lane >> 5;
+    const int ml = lane & 31;
+
+    const int tx = blockIdx.x % p.tiles_x;
+    const int tp = blockIdx.x / p.tiles_x;  // tile pair: tiles 2tp, 2tp+1
+    const int x0 = tx * TWF;
+    const int tw = min(TWF, p.W - x0);
+    const int hx = tw + 2;
+    const int r0 = 2 * tp * TH;
+    const int rows_tot = p.B * (p.H + 2);
+    const int nq = TH * tw;
+    const int nmt = (nq + 31) >> 5;
+    const long long rowp = (long long)(p.W + 2);
+    const long long pixb = 4LL * p.in_cp;
+    const long long tile_step = TH * rowp * pixb;
+    const int nchunk = (p.cin + 15) >> 4;
+    const int nunits = 2 * nchunk;
+
+    const int sub = lane >> 2, ps = lane & 3;
+    long long in_src[KIN];
+    int in_hi[KIN], in_gy[KIN];
+#pragma unroll
+    for (int i = 0; i < KIN; ++i) {
+        const int k = min(wave + NWAVES * i, IN_PIECES - 1);
+        const int r = 16 * k + sub;
+        const int s = ps ^ ((r >> 2) & 3);
+        const int hy = r / hx, hxi = r - (r / hx) * hx;
+        const int gy = r0 + hy, gx = x0 + hxi;
+        in_hi[i] = -1;
+        in_src[i] = 0;
+        in_gy[i] = gy;
+        if (r < HY * hx && gx < p.W + 2) {
+            in_src[i] = (gy * rowp + gx) * pixb + (s << 4);
+            in_hi[i] = s >> 1;
+        }
+    }
+    auto dma_in = [&](int u, int slot) {
+        const int j = u >> 1, t = u & 1;
+        const int groups = min(16, p.cin - 16 * j) >> 3;
+        unsigned char *dst = lds + 2 * W_B + slot * IN_B;
+#pragma unroll
+        for (int i = 0; i < KIN; ++i) {
+            const int k = min(wave + NWAVES * i, IN_PIECES - 1);
+            const bool ok = in_hi[i] >= 0 && in_hi[i] < groups && in_gy[i] + t * TH < rows_tot;
+            const void *src =
+                ok ? (const void *)(p.in + in_src[i] + t * tile_step + 64LL * j) : (const void *)g_zero_page;
+            __builtin_amdgcn_global_load_lds((glob_void *)src, (lds_void *)(dst + k * 1024), 16, 0, 0);
+        }
+    };
+    auto dma_w = [&](int j, int slot) {
+        const unsigned char *wj = p.w + (long long)j * W_B;
+        unsigned char *dst = lds + slot * W_B;
+#pragma unroll
+        for (int i = 0; i < KW; ++i) {
+            const int k = min(wave + NWAVES * i, W_PIECES - 1);
+            const int r = 16 * k + sub;
+            const int s = ps ^ ((r >> 2) & 3);
+            __builtin_amdgcn_global_load_lds((glob_void *)(wj + r * REC + (s << 4)), (lds_void *)(dst + k * 1024), 16,
+                                             0, 0);
+        }
+    };
+
+    int aoff[T][2][2];
+    bool mvalid[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+        const int jm = 2 * wave + mt;
+        mvalid[mt] = jm < nmt;
+        int q = 32 * jm + ml;
+        if (q >= nq) q = 0;
+        const int rec0 = (q / tw) * hx + q % tw;
+#pragma unroll
+        for (int tap = 0; tap < T; ++tap) {
+            const int r = rec0 + (tap / 3) * hx + tap % 3;
+            aoff[tap][mt][0] = slot_off(r, 2 * hl);
+            aoff[tap][mt][1] = slot_off(r, 2 * hl + 1);
+        }
+    }
+    const int bsw = (ml >> 2) & 3;
+    const int boff0 = ml * REC + (((2 * hl) ^ bsw) << 4), boff1 = ml * REC + (((2 * hl + 1) ^ bsw) << 4);
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[t][mt][r] = 0.f;
+
+    auto compute = [&](const unsigned char *s_in, const unsigned char *s_w, f32x16(&ac)[2]) {
+        f16x8 ah[2][2], al[2][2], bh[2], bl[2];
+        auto ld = [&](int tap, int buf) {
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                ah[buf][mt] = *reinterpret_cast<const f16x8 *>(s_in + aoff[tap][mt][0]);
+                al[buf][mt] = *reinterpret_cast<const f16x8 *>(s_in + aoff[tap][mt][1]);
+            }
+            bh[buf] = *reinterpret_cast<const f16x8 *>(s_w + tap * N * REC + boff0);
+            bl[buf] = *reinterpret_cast<const f16x8 *>(s_w + tap * N * REC + boff1);
+        };
+        ld(0, 0);
+#pragma unroll
+        for (int tap = 0; tap < T; ++tap) {
+            const int cb = tap & 1;
+            if (tap + 1 < T) ld(tap + 1, cb ^ 1);
+            if (DBG & 4) {
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt) asm volatile("" ::"v"(ah[cb][mt]), "v"(al[cb][mt]));
+                asm volatile("" ::"v"(bh[cb]), "v"(bl[cb]));
+                continue;
+            }
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+                if ((DBG & 32) || mvalid[mt]) ac[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[cb][mt], bh[cb], ac[mt], 0, 0, 0);
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+                if ((DBG & 32) || mvalid[mt]) ac[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[cb][mt], bl[cb], ac[mt], 0, 0, 0);
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+                if ((DBG & 32) || mvalid[mt]) ac[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[cb][mt], bh[cb], ac[mt], 0, 0, 0);
+        }
+    };
+
+    // Unit u: barrier; issue the input of unit u+NIN-1 (into the slot unit u-1 freed) and, on a tile-0 unit, the
+    // weights of the next chunk (into the slot the previous chunk freed); compute; then wait until everything but
+    // this unit's own batch has landed (NIN = 3: the next unit's input was issued one unit earlier), or (NIN = 2) all
+    // but the weight prefetch.
+    auto unit = [&](int u, f32x16(&ac)[2]) {
+        if (!(DBG & 8)) raw_barrier();
+        const bool bi = u + NIN - 1 < nunits;
+        const bool bw = !(u & 1) && (u >> 1) + 1 < nchunk;
+        auto issue = [&]() {
+            if (DBG & 1) return;
+            if (bi) dma_in(u + NIN - 1, (u + NIN - 1) % NIN);
+            if (bw) dma_w((u >> 1) + 1, ((u >> 1) + 1) & 1);
+        };
+        // STAG: the two waves sharing a SIMD (w, w+4) issue their DMAs at opposite ends of the unit, so each one's
+        // LDS-DMA issue runs beside the other's MFMAs (the batch is still >= one unit ahead of its consumer)
+        const bool late = STAG && __builtin_amdgcn_readfirstlane(wave) >= NWAVES / 2;
+        if (!late) issue();
+        if (!(DBG & 2) && (mvalid[0] || (DBG & 32)))
+            compute(lds + 2 * W_B + ((DBG & 16) ? 0 : (u % NIN)) * IN_B, lds + ((DBG & 16) ? 0 : ((u >> 1) & 1)) * W_B, ac);
+        if (late) issue();
+        if (u + 1 < nunits) {
+            if (NIN == 3) {
+                if (bi && bw) wait_vm_lgkm0<KIN + KW>();
+                else if (bi) wait_vm_lgkm0<KIN>();
+                else if (bw) wait_vm_lgkm0<KW>();
+                else wait_vm_lgkm0<0>();
+            } else {
+                if (bw) wait_vm_lgkm0<KW>();
+                else wait_vm_lgkm0<0>();
+            }
+        }
+    };
+
+    dma_in(0, 0);
+    dma_w(0, 0);
+    if (NIN == 3) {
+        dma_in(1, 1);
+        wait_vm_lgkm0<KIN>();
+    } else {
+        wait_vm_lgkm0<0>();
+    }
+    for (int j = 0; j < nchunk; ++j) {
+        unit(2 * j, acc[0]);
+        unit(2 * j + 1, acc[1]);
+    }
+
+    if (DBG & 128) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) asm volatile("" ::"v"(acc[t][mt]));
+        return;
+    }
+    // ---- epilogue: restage both tiles' fp32 accumulators as [pixel][channel] (2 x 72 KB), then store ----
+    static_assert(2 * EP_BYTES <= LDS_BYTES, "epilogue staging");
+    float *s_ep = reinterpret_cast<float *>(lds);
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+            if (!mvalid[mt]) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int q = 32 * (2 * wave + mt) + (r & 3) + 8 * (r >> 2) + 4 * hl;
+                if (q < nq) s_ep[t * (EP_BYTES / 4) + q * EP_P + ml] = acc[t][mt][r];
+            }
+        }
+    __syncthreads();
+    if (DBG & 64) return;
+    bool ok = store_tile<N>(p, s_ep, r0, x0, tw, nq, tid);
+    ok &= store_tile<N>(p, s_ep + EP_BYTES / 4, r0 + TH, x0, tw, nq, tid);
+    if (!ok && p.overflow) atomicOr(p.overflow, 1);
+}
+
+int g_x3_kernel = 1;  // esr_x3_set_kernel (include/esr_amd.h)
 
 int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const void *w, const float *bias,
               float w_scale, int cout, int taps_side, int ty0, int tx0, const esr_conv_out *o, int *overflow,
@@ -324,7 +626,41 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
     p.tiles_y = (B * (H + 2) - 2 + TH - 1) / TH;
     p.overflow = overflow;
     p.o = *o;
-    const dim3 grid((unsigned)(p.tiles_x * p.tiles_y)), block(NTHR);
+    const dim3 block(NTHR);
+    // Ring kernel for N <= 32 when its halved grid still fills the chip: a ring workgroup does two tiles in ~1.8x the
+    // time of a classic one, so compare ceil(pairs/CUs) * 1.8 with ceil(tiles/CUs) (measured at config 2 / 3 shapes).
+    const int tiles = p.tiles_x * p.tiles_y, pairs = p.tiles_x * ((p.tiles_y + 1) / 2);
+    static int n_cu = 0;
+    if (!n_cu) {
+        int dev = 0, v = 0;
+        n_cu = (hipGetDevice(&dev) == hipSuccess &&
+                hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
+    }
+    const bool ring_pays = 18 * ((pairs + n_cu - 1) / n_cu) < 10 * ((tiles + n_cu - 1) / n_cu);
+    if (taps_side == 3 && cout <= 32 && g_x3_kernel >= 1 && (ring_pays || g_x3_kernel >= 2)) {
+        const dim3 grid2((unsigned)pairs);
+#define RING_DBG(v, bits) \
+    case v: hipLaunchKernelGGL((conv_x3_ring_kernel<3, true, bits>), grid2, block, 0, stream, p); break;
+        switch (g_x3_kernel) {
+        case 15: hipLaunchKernelGGL((conv_x3_ring_kernel<3, true>), grid2, block, 0, stream, p); break;
+        RING_DBG(3, 1)
+        RING_DBG(4, 2)
+        RING_DBG(5, 4)
+        RING_DBG(6, 1 | 8)
+        RING_DBG(7, 1 | 16)
+        RING_DBG(8, 1 | 32)
+        RING_DBG(9, 1 | 8 | 16 | 32)
+        RING_DBG(10, 4 | 1)
+        RING_DBG(11, 4 | 1 | 64)
+        RING_DBG(12, 4 | 1 | 128)
+        RING_DBG(13, 64)
+        RING_DBG(14, 2 | 128)
+        default: hipLaunchKernelGGL((conv_x3_ring_kernel<3, false>), grid2, block, 0, stream, p);
+        }
+#undef RING_DBG
+        return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+    }
+    const dim3 grid((unsigned)(p.tiles_x * p.tiles_y));
     if (taps_side == 3) {
         if (cout > 32) hipLaunchKernelGGL((conv_x3_kernel<2, 3>), grid, block, 0, stream, p);
         else hipLaunchKernelGGL((conv_x3_kernel<1, 3>), grid, block, 0, stream, p);
@@ -342,6 +678,13 @@ extern "C" int esr_conv3x3_fwd_x3(const void *in, int32_t B, int32_t H, int32_t 
                                   const esr_conv_out *o, int32_t *overflow, esr_stream_t stream) {
     return launch_x3(in, B, H, W, in_cp, cin, w_packed, bias, w_scale, cout, 3, 0, 0, o, overflow,
                      (hipStream_t)stream);
+}
+
+extern "C" int esr_x3_set_kernel(int32_t variant) {
+    if (variant < 0 || variant > 15) return ESR_EINVAL;
+    const int prev = g_x3_kernel;
+    g_x3_kernel = variant;
+    return prev;
 }
 
 extern "C" int esr_upconv2x_phase_fwd_x3(const void *in, int32_t B, int32_t H, int32_t W, int32_t in_cp, int32_t cin,

@@ -48,6 +48,7 @@ _SIGNATURES = {
                            ctypes.POINTER(ConvOut), c_void_p, c_void_p],
     'esr_upconv2x_phase_fwd_x3': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_int,
                                   c_int, c_int, ctypes.POINTER(ConvOut), c_void_p, c_void_p],
+    'esr_x3_set_kernel': [c_int],
     'esr_cem_down': [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int,
                      c_void_p],
     'esr_cem_inv': [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p],

@@ -123,6 +123,12 @@ int esr_conv3x3_fwd_x3(const void *in, int32_t B, int32_t H, int32_t W, int32_t 
 int esr_upconv2x_phase_fwd_x3(const void *in, int32_t B, int32_t H, int32_t W, int32_t in_cp, int32_t cin,
                               const void *w_packed, const float *bias, float w_scale, int32_t cout, int32_t py,
                               int32_t px, const esr_conv_out *o, int32_t *overflow, esr_stream_t stream);
+/* Kernel selection for esr_conv3x3_fwd_x3 with cout <= 32 (process-wide; for A/B tests and benchmarks):
+ * 1 (default) = ring kernel (two tiles per workgroup, 3-deep LDS-DMA input ring) where its halved grid still fills the
+ * chip, else the classic two-stage kernel; 0 = classic only; 2 = ring always; 15 = ring always with staggered DMA issue;
+ * 3..14 = diagnostic ablations of the ring kernel (garbage outputs).  0..2 give bitwise-identical results.  Returns the previous setting,
+ * or ESR_EINVAL. */
+int esr_x3_set_kernel(int32_t variant);
 
 /* ---- training / Z-optimisation backward (esr_train.hip) ------------------------------------------------------------
  * The data gradient of every conv is esr_conv3x3_fwd run with rot180, in/out-swapped packed weights (host-side

@@ -277,6 +277,40 @@ def test_conv3x3_layer_x3(gpu_device, cin, cout, H, W):
     assert int(ovf.item()) == 0
 
 
+@pytest.mark.parametrize('cin,cout,B,H,W', [(64, 32, 3, 40, 148), (136, 32, 5, 17, 45), (104, 24, 2, 33, 70),
+                                            (16, 32, 1, 1, 1), (160, 32, 4, 96, 33)])
+def test_x3_ring_kernel_bitwise_equals_classic(gpu_device, cin, cout, B, H, W):
+    """The N<=32 ring kernel (two tiles per workgroup, 3-deep LDS-DMA ring, counted vmcnt) runs the classic kernel's
+    MFMA sequence per accumulator: outputs, residual epilogue and out2 must agree bit for bit, including odd tile
+    counts (the second tile of the last pair is beyond the batch) and partial column tiles."""
+    lib = _lib.load()
+    cp = cin + 8
+    xs = engine.to_split(_padded(B, H, W, cp, cin, gpu_device, 21))
+    g = torch.Generator().manual_seed(22)
+    w = torch.randn(cout, cin, 3, 3, generator=g) * 0.1
+    b = (torch.rand(cout, generator=g) - 0.5).to(gpu_device)
+    wx, scale = engine.pack_x3(engine.pack_conv_weight(w.to(gpu_device), list(range(cin)), 32))
+    rs = engine.to_split(_padded(B, H, W, 40, 40, gpu_device, 23))
+    outs = []
+    try:
+        for variant in (0, 2):  # classic only, ring always
+            lib.esr_x3_set_kernel(variant)
+            out = torch.zeros(B, H + 2, W + 2, 40, device=gpu_device)
+            out2 = torch.zeros(B, H + 2, W + 2, 32, device=gpu_device)
+            o = engine._conv_out(out, 40, 8, H, W, True, r1=rs, r1_cp=40, r1_coff=0, s1=0.2, out2=out2, out2_cp=32,
+                                 out2_coff=0)
+            _lib.check(lib.esr_conv3x3_fwd_x3(xs.data_ptr(), B, H, W, cp, cin, wx.data_ptr(), b.data_ptr(), scale,
+                                              cout, ctypes.byref(o), None, _stream()), 'conv_x3')
+            torch.cuda.synchronize()
+            outs.append((out, out2))
+    finally:
+        lib.esr_x3_set_kernel(1)
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    ref = F.leaky_relu(F.conv2d(_nchw(engine.from_split(xs), 0, cin), w.double(), b.cpu().double(), padding=1), 0.2)
+    ref = 0.2 * ref + _nchw(engine.from_split(rs), 0, cout)
+    assert normwise_rel(_nchw(engine.from_split(outs[1][0]), 8, 8 + cout), ref) < 1e-5
+
+
 def test_conv3x3_x3_planar_output(gpu_device):
     lib = _lib.load()
     B, H, W, cin = 2, 19, 45, 72
