@@ -47,6 +47,9 @@ constexpr int REC = 64;                            // bytes per staged record (1
 constexpr int IN_RECS = (HY * HXF + 15) / 16 * 16;  // 624: whole 16-record DMA wave-instructions
 constexpr int NTHR = 512;
 constexpr int NWAVES = NTHR / 64;
+#ifndef X3_PF
+#define X3_PF 2   // fragment prefetch distance (taps) of the classic kernel
+#endif
 
 __device__ __attribute__((aligned(16))) unsigned char g_zero_page[64];
 
@@ -289,8 +292,12 @@ __global__ __launch_bounds__(NTHR, 1) void conv_x3_kernel(X3Params p) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.f;
 
+    // Fragments are read X3_PF taps ahead of their MFMAs (X3_PF + 1 register sets): with one tap of lookahead the
+    // reads of 8 waves (6-8 ds_read_b128 each) were covered by only ~5 of the wave's own MFMAs, and LDS latency
+    // added to the matrix time instead of hiding under it.
     auto compute = [&](const unsigned char *s_in, const unsigned char *s_w) {
-        f16x8 ah[2][2], al[2][2], bh[2][NT], bl[2][NT];
+        constexpr int NBUF = X3_PF + 1;
+        f16x8 ah[NBUF][2], al[NBUF][2], bh[NBUF][NT], bl[NBUF][NT];
         auto ld = [&](int tap, int buf) {
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
@@ -303,11 +310,13 @@ __global__ __launch_bounds__(NTHR, 1) void conv_x3_kernel(X3Params p) {
                 bl[buf][nt] = *reinterpret_cast<const f16x8 *>(s_w + (tap * N + nt * 32) * REC + boff1);
             }
         };
-        ld(0, 0);
+#pragma unroll
+        for (int k = 0; k < X3_PF; ++k)
+            if (k < T) ld(k, k);
 #pragma unroll
         for (int tap = 0; tap < T; ++tap) {
-            const int cb = tap & 1;
-            if (tap + 1 < T) ld(tap + 1, cb ^ 1);
+            const int cb = tap % NBUF;
+            if (tap + X3_PF < T) ld(tap + X3_PF, (tap + X3_PF) % NBUF);
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt)
 #pragma unroll

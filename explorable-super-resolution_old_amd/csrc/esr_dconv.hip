@@ -1,0 +1,317 @@
+// esr_dconv.hip — convolutions of the patch discriminator on exact-fp32 MFMA, forward and both gradients.
+//
+// Discriminator_VGG_128_ (architecture.py:222-284) is conv_block(CNA) layers (block.py:129-156) with k = 3 / 4 / 8 / 1,
+// stride 1 / 2, zero padding k//2-ish or none, on channels-last tensors.  The D step of optimize_parameters
+// (SRRaGAN_model.py:360-433) needs the forward, the data gradient and the weight gradient, and the WGAN-GP penalty
+// (loss.py:244-263, autograd.grad(create_graph=True)) differentiates the data gradient again — which is again one of the
+// three.  All three are one gather-GEMM over NHWC tensors:
+//
+//   esr_dconv_fwd    out[b, omy·Y+oay, omx·X+oax, n] = bias[n] + Σ_t Σ_c src[b, smy·Y+offy[t], smx·X+offx[t], c]·w[t][c][n]
+//                    M = B·MH·MW output pixels, N = output channels, K = taps × channels; out-of-range source pixels
+//                    are the conv's zero padding.  A forward conv is (smy = stride, offy[t] = ky - pad).  The data
+//                    gradient of a stride-s conv is s² launches, one per input phase class (cy, cx): a stride-1 gather
+//                    over the taps with ky ≡ cy + pad (mod s), written to pixels (s·Y'+cy, s·X'+cx) — the transposed
+//                    conv without a zero-stuffed grid.
+//   esr_dconv_wgrad  partial[split][t][ci][co] = Σ_{pixels of split} src[.., tap t, ..][ci] · dy[pixel][co]
+//                    M = input channels, N = output channels, K = pixels; split-K into `splits` partial slabs that
+//                    esr_wgrad_reduce sums in a fixed order (deterministic).
+//
+// Tiling (fwd): workgroup = 256 threads (4 waves, one per SIMD), 256 pixels × 64 channels; wave w owns M-tiles 2w,
+// 2w+1 × two 32-wide N-tiles of v_mfma_f32_32x32x2_f32.  K steps of 32 channels of one tap: the 256 gathered pixel rows
+// (128 B each, coalesced per pixel) and the 64×32 weight slab are staged in LDS (row pitch 36 floats: the 16 lanes of a
+// ds_read_b128 group hit 16 distinct slots) while the next step is prefetched into registers.  Lane half h consumes
+// channels [16h, 16h+16) of the step four at a time (one ds_read_b128 each for A and B, four MFMAs).
+// Numerics: v_mfma_f32_32x32x2_f32 is an exact fp32 FMA chain; only the summation order differs from a CPU conv.
+#include <hip/hip_runtime.h>
+#include "esr_amd.h"
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int NTH = 256;
+constexpr int MT = 256;                  // pixels per workgroup
+constexpr int NB = 64;                   // output channels per workgroup
+constexpr int KC = 32;                   // channels per K step
+constexpr int PS = 36;                   // LDS row pitch (floats)
+constexpr int A_IT = MT * KC / 4 / NTH;  // float4 per thread per step: 8
+constexpr int B_IT = NB * KC / 4 / NTH;  // 2
+constexpr int MAXT = ESR_DCONV_MAX_TAPS;
+
+struct FwdParams {
+    const float *src;
+    int B, Hs, Ws, sp, kc, vec;  // source NHWC [B][Hs][Ws][sp], channels [0, kc); vec: 16-B loads allowed
+    const float *w;              // packed [T][nck][n_pad][32]
+    int nck, n_pad;
+    const float *bias;           // [n] or null
+    float *out;
+    int Ho, Wo, op, n;           // out NHWC [B][Ho][Wo][op], channels [0, n)
+    int MH, MW;
+    int omy, oay, omx, oax, smy, smx;
+    int T;
+    int offy[MAXT], offx[MAXT];
+};
+
+__device__ __forceinline__ f32x4 load4(const float *row, int c, int kc, bool vec) {
+    if (vec && c + 4 <= kc) return *reinterpret_cast<const f32x4 *>(row + c);
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+        if (c + e < kc) v[e] = row[c + e];
+    return v;
+}
+
+__global__ __launch_bounds__(NTH, 2) void dconv_fwd_kernel(FwdParams p) {
+    __shared__ __attribute__((aligned(16))) float lds[(MT + NB) * PS];
+    float *s_a = lds, *s_b = lds + MT * PS;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hl = lane >> 5, ml = lane & 31;
+    const int per_img = p.MH * p.MW;
+    const long long M = (long long)p.B * per_img;
+    const long long m0 = (long long)blockIdx.x * MT;
+    const int n0 = blockIdx.y * NB;
+    const int cg = tid & 7;  // this thread's 4-channel group of every staged pixel row
+    const bool vec = p.vec != 0;
+
+    int pb[A_IT], py[A_IT], px[A_IT];
+#pragma unroll
+    for (int k = 0; k < A_IT; ++k) {
+        const long long m = m0 + (tid >> 3) + 32 * k;
+        pb[k] = -1;
+        py[k] = 0;
+        px[k] = 0;
+        if (m < M) {
+            const int b = (int)(m / per_img), r = (int)(m - (long long)b * per_img);
+            pb[k] = b;
+            py[k] = r / p.MW;
+            px[k] = r - py[k] * p.MW;
+        }
+    }
+    f32x4 ra[A_IT], rb[B_IT];
+    const int nsteps = p.T * p.nck;
+    auto load = [&](int step) {
+        const int t = step / p.nck, j = step - t * p.nck;
+        const int c = j * KC + cg * 4;
+        const int oy = p.offy[t], ox = p.offx[t];
+#pragma unroll
+        for (int k = 0; k < A_IT; ++k) {
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            const int sy = p.smy * py[k] + oy, sx = p.smx * px[k] + ox;
+            if (pb[k] >= 0 && c < p.kc && sy >= 0 && sy < p.Hs && sx >= 0 && sx < p.Ws)
+                v = load4(p.src + (((long long)pb[k] * p.Hs + sy) * p.Ws + sx) * p.sp, c, p.kc, vec);
+            ra[k] = v;
+        }
+        const float *wj = p.w + ((long long)(t * p.nck + j) * p.n_pad + n0) * KC;
+#pragma unroll
+        for (int k = 0; k < B_IT; ++k) rb[k] = *reinterpret_cast<const f32x4 *>(wj + (tid + k * NTH) * 4);
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int k = 0; k < A_IT; ++k) *reinterpret_cast<f32x4 *>(s_a + ((tid >> 3) + 32 * k) * PS + cg * 4) = ra[k];
+#pragma unroll
+        for (int k = 0; k < B_IT; ++k) {
+            const int idx = tid + k * NTH;
+            *reinterpret_cast<f32x4 *>(s_b + (idx >> 3) * PS + (idx & 7) * 4) = rb[k];
+        }
+    };
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.f;
+
+    load(0);
+    for (int step = 0; step < nsteps; ++step) {
+        __syncthreads();
+        store();
+        __syncthreads();
+        if (step + 1 < nsteps) load(step + 1);
+        const float *a0 = s_a + (64 * wave + ml) * PS + 16 * hl;
+        const float *a1 = a0 + 32 * PS;
+        const float *b0 = s_b + ml * PS + 16 * hl;
+        const float *b1 = b0 + 32 * PS;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const f32x4 av0 = *reinterpret_cast<const f32x4 *>(a0 + 4 * g);
+            const f32x4 av1 = *reinterpret_cast<const f32x4 *>(a1 + 4 * g);
+            const f32x4 bv0 = *reinterpret_cast<const f32x4 *>(b0 + 4 * g);
+            const f32x4 bv1 = *reinterpret_cast<const f32x4 *>(b1 + 4 * g);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av0[s], bv0[s], acc[0][0], 0, 0, 0);
+                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av0[s], bv1[s], acc[0][1], 0, 0, 0);
+                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av1[s], bv0[s], acc[1][0], 0, 0, 0);
+                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av1[s], bv1[s], acc[1][1], 0, 0, 0);
+            }
+        }
+    }
+
+    // D layout (32x32 f32 MFMA): lane holds column n = lane & 31, rows m = (r&3) + 8(r>>2) + 4(lane>>5)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+        const int n = n0 + nt * 32 + ml;
+        if (n >= p.n) continue;
+        const float bn = p.bias ? p.bias[n] : 0.f;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const long long m = m0 + 64 * wave + 32 * mt + (r & 3) + 8 * (r >> 2) + 4 * hl;
+                if (m >= M) continue;
+                const int b = (int)(m / per_img), rr = (int)(m - (long long)b * per_img);
+                const int Y = rr / p.MW, X = rr - (rr / p.MW) * p.MW;
+                const int oy = p.omy * Y + p.oay, ox = p.omx * X + p.oax;
+                p.out[(((long long)b * p.Ho + oy) * p.Wo + ox) * p.op + n] = acc[mt][nt][r] + bn;
+            }
+    }
+}
+
+// ---- weight gradient ------------------------------------------------------------------------------------------------
+constexpr int WKP = 64;   // pixels per K step
+constexpr int WPS = 68;   // LDS row pitch (floats) of the [pixel][64 channels] tiles
+
+struct WgradParams {
+    const float *src;
+    int B, Hs, Ws, sp, cin, svec;
+    const float *dy;
+    int MH, MW, dp, cout, dvec;
+    int smy, smx, T;
+    int ci_blocks, co_blocks;
+    long long pix_per_split;
+    float *partial;
+    int offy[MAXT], offx[MAXT];
+};
+
+__global__ __launch_bounds__(NTH, 2) void dconv_wgrad_kernel(WgradParams p) {
+    __shared__ __attribute__((aligned(16))) float lds[2 * WKP * WPS];
+    float *s_a = lds, *s_b = lds + WKP * WPS;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hl = lane >> 5, ml = lane & 31;
+    int bid = blockIdx.x;
+    const int cob = bid % p.co_blocks;
+    bid /= p.co_blocks;
+    const int cib = bid % p.ci_blocks;
+    const int t = bid / p.ci_blocks;
+    const int split = blockIdx.y;
+    const int per_img = p.MH * p.MW;
+    const long long P = (long long)p.B * per_img;
+    const long long k0 = (long long)split * p.pix_per_split;
+    const long long k1 = min(P, k0 + p.pix_per_split);
+    const int ci0 = cib * 64, co0 = cob * 64;
+    const int oy = p.offy[t], ox = p.offx[t];
+    const int c4 = tid & 15;  // 4-channel group staged by this thread (the same for all of its pixel rows)
+    const bool svec = p.svec != 0, dvec = p.dvec != 0;
+    f32x4 ra[4], rb[4];
+    auto load = [&](long long kb) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const long long m = kb + (tid >> 4) + 16 * k;
+            f32x4 va = {0.f, 0.f, 0.f, 0.f}, vb = {0.f, 0.f, 0.f, 0.f};
+            if (m < k1) {
+                const int b = (int)(m / per_img), r = (int)(m - (long long)b * per_img);
+                const int Y = r / p.MW, X = r - (r / p.MW) * p.MW;
+                const int ci = ci0 + 4 * c4, co = co0 + 4 * c4;
+                const int sy = p.smy * Y + oy, sx = p.smx * X + ox;
+                if (ci < p.cin && sy >= 0 && sy < p.Hs && sx >= 0 && sx < p.Ws)
+                    va = load4(p.src + (((long long)b * p.Hs + sy) * p.Ws + sx) * p.sp, ci, p.cin, svec);
+                if (co < p.cout) vb = load4(p.dy + (((long long)b * p.MH + Y) * p.MW + X) * p.dp, co, p.cout, dvec);
+            }
+            ra[k] = va;
+            rb[k] = vb;
+        }
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int pp = (tid >> 4) + 16 * k;
+            *reinterpret_cast<f32x4 *>(s_a + pp * WPS + 4 * c4) = ra[k];
+            *reinterpret_cast<f32x4 *>(s_b + pp * WPS + 4 * c4) = rb[k];
+        }
+    };
+    const int mt = wave >> 1, nt = wave & 1;
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    if (k0 < k1) load(k0);
+    for (long long kb = k0; kb < k1; kb += WKP) {
+        __syncthreads();
+        store();
+        __syncthreads();
+        if (kb + WKP < k1) load(kb + WKP);
+        // A[m = ci][k = pixel] from s_a[pixel][ci], B[k = pixel][n = co] from s_b[pixel][co]; lane half = pixel parity
+#pragma unroll 8
+        for (int s = 0; s < WKP / 2; ++s) {
+            const float a = s_a[(2 * s + hl) * WPS + 32 * mt + ml];
+            const float b = s_b[(2 * s + hl) * WPS + 32 * nt + ml];
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+        }
+    }
+    const int cin_pad = 64 * p.ci_blocks, cout_pad = 64 * p.co_blocks;
+    float *dst = p.partial + ((long long)split * p.T + t) * cin_pad * cout_pad;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int ci = ci0 + 32 * mt + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        const int co = co0 + 32 * nt + ml;
+        dst[(long long)ci * cout_pad + co] = acc[r];
+    }
+}
+
+bool aligned16(const void *ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; }
+
+}  // namespace
+
+extern "C" int esr_dconv_fwd(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t src_pitch, int32_t kc,
+                             const float *w_packed, int32_t nck, int32_t n_pad, const float *bias, float *out,
+                             int32_t Ho, int32_t Wo, int32_t out_pitch, int32_t n, int32_t MH, int32_t MW, int32_t omy,
+                             int32_t oay, int32_t omx, int32_t oax, int32_t smy, int32_t smx, int32_t T,
+                             const int32_t *offy, const int32_t *offx, esr_stream_t stream) {
+    if (!src || !w_packed || !out || !offy || !offx) return ESR_EINVAL;
+    if (B <= 0 || Hs <= 0 || Ws <= 0 || kc <= 0 || src_pitch < kc || n <= 0 || out_pitch < n || MH <= 0 || MW <= 0)
+        return ESR_EINVAL;
+    if (T <= 0 || T > ESR_DCONV_MAX_TAPS || nck != (kc + KC - 1) / KC || n_pad % NB || n_pad < n) return ESR_EINVAL;
+    if (!aligned16(w_packed)) return ESR_EINVAL;
+    // every output pixel the grid writes must lie inside the output tensor
+    if (oay < 0 || oax < 0 || omy * (MH - 1) + oay >= Ho || omx * (MW - 1) + oax >= Wo) return ESR_EINVAL;
+    FwdParams p;
+    p.src = src; p.B = B; p.Hs = Hs; p.Ws = Ws; p.sp = src_pitch; p.kc = kc;
+    p.vec = (src_pitch % 4 == 0 && aligned16(src)) ? 1 : 0;
+    p.w = w_packed; p.nck = nck; p.n_pad = n_pad; p.bias = bias;
+    p.out = out; p.Ho = Ho; p.Wo = Wo; p.op = out_pitch; p.n = n;
+    p.MH = MH; p.MW = MW; p.omy = omy; p.oay = oay; p.omx = omx; p.oax = oax; p.smy = smy; p.smx = smx;
+    p.T = T;
+    for (int t = 0; t < T; ++t) { p.offy[t] = offy[t]; p.offx[t] = offx[t]; }
+    const long long M = (long long)B * MH * MW;
+    const long long gx = (M + MT - 1) / MT;
+    if (gx > 0x7fffffff) return ESR_EINVAL;
+    const dim3 grid((unsigned)gx, (unsigned)((n + NB - 1) / NB)), block(NTH);
+    hipLaunchKernelGGL(dconv_fwd_kernel, grid, block, 0, (hipStream_t)stream, p);
+    return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+}
+
+extern "C" int esr_dconv_wgrad(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t src_pitch, int32_t cin,
+                               const float *dy, int32_t MH, int32_t MW, int32_t dy_pitch, int32_t cout, int32_t smy,
+                               int32_t smx, int32_t T, const int32_t *offy, const int32_t *offx, int32_t splits,
+                               float *partial, esr_stream_t stream) {
+    if (!src || !dy || !partial || !offy || !offx) return ESR_EINVAL;
+    if (B <= 0 || Hs <= 0 || Ws <= 0 || cin <= 0 || src_pitch < cin || MH <= 0 || MW <= 0 || cout <= 0 ||
+        dy_pitch < cout || T <= 0 || T > ESR_DCONV_MAX_TAPS || splits <= 0)
+        return ESR_EINVAL;
+    WgradParams p;
+    p.src = src; p.B = B; p.Hs = Hs; p.Ws = Ws; p.sp = src_pitch; p.cin = cin;
+    p.svec = (src_pitch % 4 == 0 && aligned16(src)) ? 1 : 0;
+    p.dy = dy; p.MH = MH; p.MW = MW; p.dp = dy_pitch; p.cout = cout;
+    p.dvec = (dy_pitch % 4 == 0 && aligned16(dy)) ? 1 : 0;
+    p.smy = smy; p.smx = smx; p.T = T;
+    p.ci_blocks = (cin + 63) / 64;
+    p.co_blocks = (cout + 63) / 64;
+    const long long P = (long long)B * MH * MW;
+    p.pix_per_split = ((P + splits - 1) / splits + WKP - 1) / WKP * WKP;
+    p.partial = partial;
+    for (int t = 0; t < T; ++t) { p.offy[t] = offy[t]; p.offx[t] = offx[t]; }
+    const long long gx = (long long)T * p.ci_blocks * p.co_blocks;
+    const dim3 grid((unsigned)gx, (unsigned)splits), block(NTH);
+    hipLaunchKernelGGL(dconv_wgrad_kernel, grid, block, 0, (hipStream_t)stream, p);
+    return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+}

@@ -8,7 +8,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('ESR_AMD_LIB', os.path.join(_HERE, 'libesr_amd.so'))
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 c_int = ctypes.c_int32
 c_float = ctypes.c_float
@@ -66,6 +66,11 @@ _SIGNATURES = {
                         c_float, c_int, c_void_p, c_void_p],
     'esr_input_adjoint': [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int,
                           c_int, c_void_p, c_void_p],
+    'esr_dconv_fwd': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                      c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                      ctypes.POINTER(c_int), ctypes.POINTER(c_int), c_void_p],
+    'esr_dconv_wgrad': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                        c_int, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int), c_int, c_void_p, c_void_p],
     'esr_timer_create': [c_int],
     'esr_timer_elapsed': [c_void_p, c_fp],
     'esr_timer_destroy': [c_void_p],

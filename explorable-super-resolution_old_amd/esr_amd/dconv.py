@@ -1,0 +1,221 @@
+"""Discriminator convolutions on the HIP gather-GEMM kernels (csrc/esr_dconv.hip), differentiable to any order.
+
+Discriminator_VGG_128_ (architecture.py:222-284) is built from conv_block(CNA) layers (block.py:129-156): Conv2d with
+k = 3 / 4 / 8 / 1, stride 1 / 2, then BatchNorm + LeakyReLU.  The D step (SRRaGAN_model.py:360-433) needs their forward,
+data gradient and weight gradient, and the WGAN-GP penalty (loss.py:244-263: autograd.grad(create_graph=True) followed
+by .backward()) differentiates the data gradient once more.  The three maps
+
+    conv  (x, w)  -> y        DConvFn
+    dgrad (gy, w) -> gx       DgradFn     (adjoint of conv in x)
+    wgrad (x, gy) -> gw       WgradFn     (adjoint of conv in w)
+
+are bilinear and each one's backward is made of the other two, so autograd can differentiate through them any number
+of times with every convolution running on the MFMA kernels.  Tensors are channels-last: the module-level wrapper
+HipConv2d takes/returns NCHW tensors with NHWC storage (torch.channels_last), which BatchNorm / LeakyReLU accept as is.
+There is no CPU path: a CPU tensor raises.
+"""
+import ctypes
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+
+MAX_TAPS = 64
+_WG_SPLIT_TARGET = 1024          # workgroups a weight-gradient launch aims for (split-K over pixels)
+_WG_PARTIAL_MAX = 64 << 20       # floats of split-K partials per launch
+
+
+def _stream(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _i32(vals):
+    return (ctypes.c_int32 * max(1, len(vals)))(*vals)
+
+
+def _check_dev(*ts):
+    for t in ts:
+        if t is not None and (not t.is_cuda or t.dtype != torch.float32):
+            raise RuntimeError('esr_amd.dconv: discriminator tensors must be float32 on a ROCm device '
+                               '(this build has no CPU path)')
+
+
+def out_size(n, k, s, p):
+    return (n + 2 * p - k) // s + 1
+
+
+def _pack(wt, n_out):
+    """wt [T][K][N] -> packed [T][nck][n_pad][32] (esr_dconv_fwd's weight layout)."""
+    T, K, N = wt.shape
+    nck = (K + 31) // 32
+    n_pad = 64 * ((n_out + 63) // 64)
+    buf = wt.new_zeros(T, nck * 32, n_pad)
+    buf[:, :K, :N] = wt
+    return buf.view(T, nck, 32, n_pad).permute(0, 1, 3, 2).contiguous(), nck, n_pad
+
+
+def _gather(src, wt, bias, out, MH, MW, omy, oay, omx, oax, smy, smx, offy, offx):
+    """One esr_dconv_fwd launch: src [B][Hs][Ws][C] and out [B][Ho][Wo][N] contiguous NHWC, wt [T][C][N]."""
+    B, Hs, Ws, C = src.shape
+    _, Ho, Wo, N = out.shape
+    wp, nck, n_pad = _pack(wt, N)
+    lib = _lib.load()
+    _lib.check(lib.esr_dconv_fwd(src.data_ptr(), B, Hs, Ws, C, C, wp.data_ptr(), nck, n_pad,
+                                 None if bias is None else bias.data_ptr(), out.data_ptr(), Ho, Wo, N, N, MH, MW,
+                                 omy, oay, omx, oax, smy, smx, len(offy), _i32(offy), _i32(offx), _stream(src)),
+               'esr_dconv_fwd')
+
+
+def conv_forward(x, w, b, k, s, p):
+    """y = conv2d(x, w, b, stride s, zero padding p) on NHWC x [B][H][W][Ci]; w [Co][Ci][k][k]."""
+    _check_dev(x, w, b)
+    B, H, W, Ci = x.shape
+    Co = w.shape[0]
+    Ho, Wo = out_size(H, k, s, p), out_size(W, k, s, p)
+    y = torch.empty(B, Ho, Wo, Co, device=x.device, dtype=torch.float32)
+    wt = w.detach().permute(2, 3, 1, 0).reshape(k * k, Ci, Co)
+    taps = [(ky, kx) for ky in range(k) for kx in range(k)]
+    _gather(x, wt, None if b is None else b.detach().contiguous(), y, Ho, Wo, 1, 0, 1, 0, s, s,
+            [ky - p for ky, _ in taps], [kx - p for _, kx in taps])
+    return y
+
+
+def conv_dgrad(gy, w, k, s, p, H, W):
+    """gx = conv_transpose of gy (NHWC [B][Ho][Wo][Co]) back to the [B][H][W][Ci] input grid: one launch per phase
+    class (cy, cx) of the stride, each gathering over the taps that land on that class."""
+    _check_dev(gy, w)
+    B, Ho, Wo, Co = gy.shape
+    Ci = w.shape[1]
+    wd = w.detach()
+    classes = []
+    full = True
+    for cy in range(s):
+        for cx in range(s):
+            MH, MW = (H - cy + s - 1) // s, (W - cx + s - 1) // s
+            tys = [ky for ky in range(k) if (cy + p - ky) % s == 0]
+            txs = [kx for kx in range(k) if (cx + p - kx) % s == 0]
+            if MH <= 0 or MW <= 0:
+                continue
+            if not tys or not txs:
+                full = False
+                continue
+            classes.append((cy, cx, MH, MW, [(ky, kx) for ky in tys for kx in txs]))
+    gx = (torch.empty if full else torch.zeros)(B, H, W, Ci, device=gy.device, dtype=torch.float32)
+    for cy, cx, MH, MW, taps in classes:
+        wt = torch.stack([wd[:, :, ky, kx] for ky, kx in taps])  # [T][Co][Ci]
+        _gather(gy, wt, None, gx, MH, MW, s, cy, s, cx, 1, 1,
+                [(cy + p - ky) // s for ky, _ in taps], [(cx + p - kx) // s for _, kx in taps])
+    return gx
+
+
+def conv_wgrad(x, gy, k, s, p):
+    """gw [Co][Ci][k][k] = sum over pixels of x (gathered per tap) * gy; split-K over pixels + deterministic reduce."""
+    _check_dev(x, gy)
+    B, H, W, Ci = x.shape
+    _, Ho, Wo, Co = gy.shape
+    T = k * k
+    cin_pad, cout_pad = 64 * ((Ci + 63) // 64), 64 * ((Co + 63) // 64)
+    n = T * cin_pad * cout_pad
+    tiles = T * (cin_pad // 64) * (cout_pad // 64)
+    P = B * Ho * Wo
+    splits = max(1, min(-(-_WG_SPLIT_TARGET // tiles), -(-P // 256), _WG_PARTIAL_MAX // n))
+    partial = torch.empty(splits * n, device=x.device, dtype=torch.float32)
+    red = torch.empty(n, device=x.device, dtype=torch.float32)
+    taps = [(ky, kx) for ky in range(k) for kx in range(k)]
+    lib = _lib.load()
+    st = _stream(x)
+    _lib.check(lib.esr_dconv_wgrad(x.data_ptr(), B, H, W, Ci, Ci, gy.data_ptr(), Ho, Wo, Co, Co, s, s, T,
+                                   _i32([ky - p for ky, _ in taps]), _i32([kx - p for _, kx in taps]), splits,
+                                   partial.data_ptr(), st), 'esr_dconv_wgrad')
+    _lib.check(lib.esr_wgrad_reduce(partial.data_ptr(), splits, n, 1.0, red.data_ptr(), st), 'esr_wgrad_reduce')
+    return red.view(k, k, cin_pad, cout_pad)[:, :, :Ci, :Co].permute(3, 2, 0, 1).contiguous()
+
+
+class DConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, k, s, p):
+        ctx.save_for_backward(x, w)
+        ctx.geom = (k, s, p)
+        ctx.has_bias = b is not None
+        return conv_forward(x, w, b, k, s, p)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        k, s, p = ctx.geom
+        gy = gy.contiguous()
+        gx = DgradFn.apply(gy, w, k, s, p, x.shape[1], x.shape[2]) if ctx.needs_input_grad[0] else None
+        gw = WgradFn.apply(x, gy, k, s, p) if ctx.needs_input_grad[1] else None
+        gb = gy.sum((0, 1, 2)) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        return gx, gw, gb, None, None, None
+
+
+class DgradFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gy, w, k, s, p, H, W):
+        ctx.save_for_backward(gy, w)
+        ctx.geom = (k, s, p)
+        return conv_dgrad(gy, w, k, s, p, H, W)
+
+    @staticmethod
+    def backward(ctx, ggx):
+        gy, w = ctx.saved_tensors
+        k, s, p = ctx.geom
+        ggx = ggx.contiguous()
+        g_gy = DConvFn.apply(ggx, w, None, k, s, p) if ctx.needs_input_grad[0] else None
+        g_w = WgradFn.apply(ggx, gy, k, s, p) if ctx.needs_input_grad[1] else None
+        return g_gy, g_w, None, None, None, None, None
+
+
+class WgradFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gy, k, s, p):
+        ctx.save_for_backward(x, gy)
+        ctx.geom = (k, s, p)
+        return conv_wgrad(x, gy, k, s, p)
+
+    @staticmethod
+    def backward(ctx, ggw):
+        x, gy = ctx.saved_tensors
+        k, s, p = ctx.geom
+        ggw = ggw.contiguous()
+        g_x = DgradFn.apply(gy, ggw, k, s, p, x.shape[1], x.shape[2]) if ctx.needs_input_grad[0] else None
+        g_gy = DConvFn.apply(x, ggw, None, k, s, p) if ctx.needs_input_grad[1] else None
+        return g_x, g_gy, None, None, None
+
+
+class _ToNHWC(torch.autograd.Function):
+    """NCHW-contiguous -> NHWC copy whose gradient comes back NCHW-contiguous (the discriminator's input gradient is
+    used with .view() by GradientPenaltyLoss, loss.py:255-263, as in the reference)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.permute(0, 2, 3, 1).contiguous()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.permute(0, 3, 1, 2).contiguous()
+
+
+class HipConv2d(nn.Conv2d):
+    """nn.Conv2d of the discriminator (same parameters, state_dict and init) whose forward runs esr_dconv.
+
+    Square kernel, equal stride and zero padding in both dimensions, no dilation / groups (what conv_block builds).
+    Input: NCHW tensor (any memory format; channels-last avoids a copy); output: NCHW with channels-last storage."""
+
+    def __init__(self, *args, **kwargs):
+        super().__init__(*args, **kwargs)
+        k, s, p = self.kernel_size, self.stride, self.padding
+        if k[0] != k[1] or s[0] != s[1] or p[0] != p[1] or self.dilation != (1, 1) or self.groups != 1 or \
+                self.padding_mode != 'zeros' or k[0] * k[1] > MAX_TAPS:
+            raise NotImplementedError('HipConv2d: square zero-padded dense convolutions with <= %d taps' % MAX_TAPS)
+
+    def forward(self, x):
+        _check_dev(x)
+        if x.is_contiguous(memory_format=torch.channels_last):
+            xh = x.permute(0, 2, 3, 1)  # a view: NHWC storage already
+        else:
+            xh = _ToNHWC.apply(x)
+        y = DConvFn.apply(xh, self.weight, self.bias, self.kernel_size[0], self.stride[0], self.padding[0])
+        return y.permute(0, 3, 1, 2)

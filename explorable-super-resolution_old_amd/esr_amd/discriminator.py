@@ -6,10 +6,14 @@ that class does not accept (TypeError, networks.py:115-120 vs architecture.py:18
 this one — `define_D` here builds it (SURVEY.md §7 "training path is broken as shipped").  Same module tree, hence the
 same state_dict keys and order as the reference (tests/golden/disc_*.npz).
 
-This round the discriminator runs on PyTorch-ROCm (MIOpen convolutions, autograd incl. the WGAN-GP double backward);
-moving its dense 3×3/4×4/8×8 convolutions onto hand-written MFMA kernels is SURVEY.md §8(f) item 2.
+Every convolution (3×3 s1, 4×4 s2, the 8×8 "pseudo-FC" and the 1×1 head) is a HipConv2d: forward, data gradient
+and weight gradient on the exact-fp32 MFMA gather-GEMM kernels of csrc/esr_dconv.hip, differentiable to any order, so
+the D step and the WGAN-GP double backward (loss.py:244-263) run every convolution on HIP.  BatchNorm and LeakyReLU
+stay PyTorch elementwise ops on the channels-last activations the convolutions produce.
 """
 import torch.nn as nn
+
+from .dconv import HipConv2d
 
 LRELU = 0.2
 
@@ -17,7 +21,7 @@ LRELU = 0.2
 def _conv_block(in_nc, out_nc, k, stride=1, norm=True, act=True, zero_pad=True):
     """conv_block(mode='CNA') of block.py:129-156 flattened the way `sequential` does (block.py:106-126)."""
     pad = (k - 1) // 2 if zero_pad else 0  # get_valid_padding; pad_type=None means no padding at all
-    mods = [nn.Conv2d(in_nc, out_nc, kernel_size=k, stride=stride, padding=pad, bias=True)]
+    mods = [HipConv2d(in_nc, out_nc, kernel_size=k, stride=stride, padding=pad, bias=True)]
     if norm:
         mods.append(nn.BatchNorm2d(out_nc, affine=True))
     if act:

@@ -178,6 +178,35 @@ int esr_input_adjoint(const float *d_hr, int32_t hr_cp, int32_t hr_coff, const f
                       int32_t lr_coff, int32_t sf, const float *d_pl, int32_t C, int32_t B, int32_t Hp, int32_t Wp,
                       int32_t M, float *out, esr_stream_t stream);
 
+/* ---- discriminator convolutions (esr_dconv.hip) -----------------------------------------------------------------
+ * Discriminator_VGG_128_ (architecture.py:222-284): the conv_block convolutions (block.py:129-156; k = 3/4/8/1,
+ * stride 1/2) of the D step and of the WGAN-GP double backward (SRRaGAN_model.py:360-433, loss.py:244-263), exact fp32
+ * (v_mfma_f32_32x32x2_f32), on channels-last (NHWC, no halo) tensors.
+ *
+ * esr_dconv_fwd: gather-GEMM
+ *   out[b, omy*Y+oay, omx*X+oax, n] = bias[n] + sum_t sum_{c<kc} src[b, smy*Y+offy[t], smx*X+offx[t], c] * W[t][c][n]
+ * for Y < MH, X < MW, n < n_out; source pixels outside [0,Hs)x[0,Ws) read as zero (the conv's zero padding).
+ *   forward conv (k, s, pad):  MH x MW = output grid, omy = omx = 1, oay = oax = 0, smy = smx = s, offy = ky - pad
+ *   data gradient:             one call per input phase class (cy, cx) of the stride: src = dL/dout, W[t] = w[:, :, ky,
+ *                              kx] (K = Cout, N = Cin) for the taps with (cy + pad - ky) % s == 0, offy = (cy+pad-ky)/s,
+ *                              smy = 1, omy = s, oay = cy (pixels of other classes are not written)
+ * w_packed: [T][nck][n_pad][32] fp32 (nck = ceil(kc/32), n_pad = 64*ceil(n_out/64)); channel k of chunk j is 32j + k,
+ * zero beyond kc / n_out.  bias may be NULL.  T <= ESR_DCONV_MAX_TAPS. */
+#define ESR_DCONV_MAX_TAPS 64
+int esr_dconv_fwd(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t src_pitch, int32_t kc,
+                  const float *w_packed, int32_t nck, int32_t n_pad, const float *bias, float *out, int32_t Ho,
+                  int32_t Wo, int32_t out_pitch, int32_t n_out, int32_t MH, int32_t MW, int32_t omy, int32_t oay,
+                  int32_t omx, int32_t oax, int32_t smy, int32_t smx, int32_t T, const int32_t *offy,
+                  const int32_t *offx, esr_stream_t stream);
+/* esr_dconv_wgrad: weight gradient of the forward conv above (src = its input, dy = dL/dout on the MH x MW grid):
+ *   partial[s][t][ci][co] = sum over the pixels of split s of src[b, smy*Y+offy[t], smx*X+offx[t], ci] * dy[b, Y, X, co]
+ * partial: [splits][T][cin_pad][cout_pad], cin_pad = 64*ceil(cin/64), cout_pad = 64*ceil(cout/64); reduce the splits
+ * with esr_wgrad_reduce (fixed order, deterministic). */
+int esr_dconv_wgrad(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t src_pitch, int32_t cin,
+                    const float *dy, int32_t MH, int32_t MW, int32_t dy_pitch, int32_t cout, int32_t smy, int32_t smx,
+                    int32_t T, const int32_t *offy, const int32_t *offx, int32_t splits, float *partial,
+                    esr_stream_t stream);
+
 /* ---- op lists (host-side executor, esr_plan.hip) -----------------------------------------------------------------
  * A generator (+CEM) forward is a fixed sequence of the launches above (≈360 for RRDB-23).  The host layer records it
  * once per (workspace, weights, shape) as an array of esr_op and replays it with one esr_run_ops call, patching only

@@ -280,3 +280,45 @@ def sr_forward(x, P, nb, latent, design=None, pre_pad=False, sf=4):
 def strip_prefix(params):
     return {k[len('generated_image_model.'):] if k.startswith('generated_image_model.') else k: torch.as_tensor(v)
             for k, v in params.items()}
+
+
+# ----------------------------------------------------------------------------------------------------------------------
+# Discriminator_VGG_128_ (architecture.py:222-284) — the patch D of the training step, on torch.nn CPU convolutions
+# ----------------------------------------------------------------------------------------------------------------------
+def reference_discriminator(in_nc=3, nf=64, nb=6, num_2_strides=5):
+    """The module tree of Discriminator_VGG_128_(norm 'batch', act 'leakyrelu', mode 'CNA'): conv_block layers
+    (block.py:129-156: Conv2d, BatchNorm2d except the first, LeakyReLU(0.2)) with the 3x3-s1 / 4x4-s2 plan
+    (architecture.py:226-260), then the pseudo-FC head conv 8x8 valid + BN + LReLU, LReLU, conv 1x1 + BN + LReLU
+    (architecture.py:262-276).  Same state_dict keys as the reference; plain nn.Conv2d (CPU/any device)."""
+    import torch.nn as nn
+
+    def block(ci, co, k, s, norm, pad):
+        mods = [nn.Conv2d(ci, co, kernel_size=k, stride=s, padding=pad, bias=True)]
+        if norm:
+            mods.append(nn.BatchNorm2d(co, affine=True))
+        mods.append(nn.LeakyReLU(LRELU, True))
+        return mods
+
+    plan = [(in_nc, nf, 3, 1, False), (nf, nf, 4, 2, True), (nf, 2 * nf, 3, 1, True), (2 * nf, 2 * nf, 4, 2, True),
+            (2 * nf, 4 * nf, 3, 1, True), (4 * nf, 4 * nf, 4, 2, True), (4 * nf, 8 * nf, 3, 1, True),
+            (8 * nf, 8 * nf, 4, 2, True), (8 * nf, 8 * nf, 3, 1, True), (8 * nf, 8 * nf, 4, 2, True)]
+    left = num_2_strides
+    mods = []
+    for ci, co, k, s, norm in plan[:nb]:
+        if s == 2:
+            s = 2 if left > 0 else 1
+            left -= 1
+        mods += block(ci, co, k, s, norm, (k - 1) // 2)
+    nfeat = [m for m in mods if isinstance(m, nn.BatchNorm2d)][-1].num_features
+
+    class _D(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.features = nn.Sequential(*mods)
+            self.classifier = nn.Sequential(nn.Sequential(*block(nfeat, min(100, nfeat), 8, 1, True, 0)),
+                                            nn.LeakyReLU(LRELU, False),
+                                            nn.Sequential(*block(min(100, nfeat), 1, 1, 1, True, 0)))
+
+        def forward(self, x):
+            return self.classifier(self.features(x))
+    return _D()

@@ -1,0 +1,144 @@
+"""GPU parity of the discriminator on the HIP gather-GEMM convolutions (csrc/esr_dconv.hip, esr_amd/dconv.py).
+
+  single conv forward / data gradient / weight gradient vs float64 CPU (torch.nn.grad):   1e-5 normwise
+  Discriminator_VGG_128_ D step (forward, wgan losses, WGAN-GP double backward, BN buffers)
+      vs the reference's golden vector (tests/golden/disc_vgg128_nb6.npz):               same bars as the CPU oracle
+  the same D step at another size vs the float64 oracle D (torch.nn, CPU):              1e-4 (gradients: max-norm
+      relative to each parameter's gradient, floored at 1e-3 of the model's largest gradient — see _grad_errors)
+"""
+import json
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import golden, normwise_rel
+
+from esr_amd import dconv
+from esr_amd import loss as L
+from esr_amd.discriminator import Discriminator_VGG_128_
+from oracle.esr_oracle import reference_discriminator
+from oracle.recipe import seeded_params
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize('ci,co,k,s,p,H,W', [
+    (3, 64, 3, 1, 1, 20, 18),      # conv0 (3 input channels: scalar-gather path)
+    (64, 64, 4, 2, 1, 19, 22),     # 4x4 stride 2, odd size: all four dgrad phase classes
+    (64, 128, 3, 1, 1, 9, 11),
+    (256, 100, 8, 1, 0, 12, 10),   # pseudo-FC 8x8 valid, 100 outputs (two N blocks, partial)
+    (100, 1, 1, 1, 0, 5, 7),       # 1x1 head: 100 channels in, 1 out (unaligned pitches)
+    (130, 70, 4, 2, 1, 8, 9),      # partial K chunks and N blocks
+])
+def test_dconv_ops_vs_float64(gpu_device, ci, co, k, s, p, H, W):
+    g = torch.Generator().manual_seed(ci * 1000 + co)
+    B = 3
+    x = torch.randn(B, ci, H, W, generator=g)
+    w = torch.randn(co, ci, k, k, generator=g) / np.sqrt(ci * k * k)
+    b = torch.randn(co, generator=g) * 0.1
+    Ho, Wo = dconv.out_size(H, k, s, p), dconv.out_size(W, k, s, p)
+    gy = torch.randn(B, co, Ho, Wo, generator=g)
+    nhwc = lambda t: t.permute(0, 2, 3, 1).contiguous().to(gpu_device)  # noqa: E731
+    back = lambda t: t.permute(0, 3, 1, 2).double().cpu()  # noqa: E731
+    wd, bd = w.to(gpu_device), b.to(gpu_device)
+    y = dconv.conv_forward(nhwc(x), wd, bd, k, s, p)
+    gx = dconv.conv_dgrad(nhwc(gy), wd, k, s, p, H, W)
+    gw = dconv.conv_wgrad(nhwc(x), nhwc(gy), k, s, p)
+    torch.cuda.synchronize()
+    xd, wdd, gyd = x.double(), w.double(), gy.double()
+    assert normwise_rel(back(y), F.conv2d(xd, wdd, b.double(), stride=s, padding=p)) < 1e-5
+    assert normwise_rel(back(gx), torch.nn.grad.conv2d_input(xd.shape, wdd, gyd, stride=s, padding=p)) < 1e-5
+    assert normwise_rel(gw.double().cpu(), torch.nn.grad.conv2d_weight(xd, wdd.shape, gyd, stride=s, padding=p)) < 1e-5
+
+
+def _grad_errors(named_grads, ref):
+    """Per-parameter max|g - ref| / max(max|ref|, 1e-3 * the largest reference gradient of the model).  The floor only
+    matters for the conv biases in front of a BatchNorm (training mode): their exact gradient is 0, and both sides
+    carry rounding noise there, which a pure relative metric would turn into O(1)."""
+    gmax = max(float(np.abs(np.asarray(r, dtype=np.float64)).max()) for r in ref.values())
+    errs = {}
+    for k, g in named_grads:
+        a, b = np.asarray(g.detach().cpu(), dtype=np.float64), np.asarray(ref[k], dtype=np.float64)
+        errs[k] = float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-3 * gmax))
+    return errs
+
+
+def _load(D, d):
+    ref_keys = json.loads(str(d['keys']))
+    params = seeded_params([(k, s) for k, s in ref_keys if 'running' not in k and 'num_batches' not in k],
+                           int(d['seed']), w_scale=1.0)
+    D.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=False)
+    return D.train()
+
+
+def _d_step(D, real, fake, rp):
+    """SRRaGAN_model.py:360-433 D losses with the wgan-gp GAN type (l_gp_w = 10) and their backward."""
+    cri_gan, cri_gp = L.GANLoss('wgan-gp'), L.GradientPenaltyLoss(device=real.device)
+    pred_real, pred_fake = D(real), D(fake)
+    l_d_real, l_d_fake = 2 * cri_gan(pred_real, True), 2 * cri_gan(pred_fake, False)
+    interp = rp * fake + (1 - rp) * real
+    interp.requires_grad = True
+    l_d_gp = 10 * cri_gp(interp, D(interp))
+    l_d_total = (l_d_real + l_d_fake) / 2 + l_d_gp
+    l_d_total.backward()
+    return pred_real, pred_fake, dict(l_d_real=l_d_real, l_d_fake=l_d_fake, l_d_gp=l_d_gp, l_d_total=l_d_total)
+
+
+def test_discriminator_d_step_vs_reference_golden(gpu_device):
+    d = golden('disc_vgg128_nb6')
+    D = _load(Discriminator_VGG_128_(in_nc=3, base_nf=64, norm_type='batch', act_type='leakyrelu', mode='CNA',
+                                     input_patch_size=80, nb=6), d).to(gpu_device)
+    real, fake, rp = (torch.from_numpy(d[k]).to(gpu_device) for k in ('real', 'fake', 'rp'))
+    pred_real, pred_fake, losses = _d_step(D, real, fake, rp)
+    assert normwise_rel(pred_real.detach().cpu(), d['pred_real']) < 1e-5
+    assert normwise_rel(pred_fake.detach().cpu(), d['pred_fake']) < 1e-5
+    for k, v in losses.items():
+        assert abs(float(v) - float(d[k])) <= 1e-5 * max(1.0, abs(float(d[k]))), k
+    # gradients: against the float64 truth (the oracle D in float64 on the fixture's weights and inputs), within 5x
+    # the reference's own fp32 error or 1e-4 (conftest.grad_parity's rule: a LeakyReLU pre-activation within rounding
+    # of 0 takes slope 1 in one fp32 evaluation and 0.2 in another)
+    Dr = _load(reference_discriminator(nb=6), d).double()
+    _d_step(Dr, *(torch.from_numpy(d[k]).double() for k in ('real', 'fake', 'rp')))
+    truth = {k: p.grad for k, p in Dr.named_parameters()}
+    e_hip = _grad_errors([(k, p.grad) for k, p in D.named_parameters()], truth)
+    e_ref = _grad_errors([(k, torch.from_numpy(d['grad:' + k])) for k, _ in D.named_parameters()], truth)
+    bad = {k: (e_hip[k], e_ref[k]) for k in e_hip if e_hip[k] > max(1e-4, 5 * e_ref[k])}
+    assert not bad, bad
+    for k, v in D.state_dict().items():
+        if 'running' in k:
+            assert normwise_rel(v.cpu(), d['buf:' + k]) < 1e-5, k
+
+
+def test_discriminator_d_step_vs_float64_oracle(gpu_device):
+    """Batch 4 at 96x96 (classifier output 5x5), kaiming-initialised D: predictions, losses and every parameter gradient
+    of the D step, WGAN-GP double backward included, against the oracle D in float64 on the CPU with the same weights,
+    within 5x the error of the same oracle run in fp32 (or 1e-4)."""
+    torch.manual_seed(5)
+    Dh = Discriminator_VGG_128_(in_nc=3, base_nf=64, norm_type='batch', act_type='leakyrelu', mode='CNA',
+                                input_patch_size=96, nb=6)
+    g = torch.Generator().manual_seed(6)
+    real, fake = torch.rand(4, 3, 96, 96, generator=g), torch.rand(4, 3, 96, 96, generator=g)
+    rp = torch.rand(4, 1, 1, 1, generator=g)
+    runs = {}
+    for name, dtype in (('f64', torch.float64), ('f32', torch.float32)):
+        Dr = reference_discriminator(nb=6)
+        Dr.load_state_dict(Dh.state_dict())
+        Dr.to(dtype).train()
+        pr, _, lr_ = _d_step(Dr, real.to(dtype), fake.to(dtype), rp.to(dtype))
+        runs[name] = (pr.detach(), {k: float(v) for k, v in lr_.items()}, {k: p.grad for k, p in Dr.named_parameters()})
+    Dh.to(gpu_device).train()
+    ph, _, lh = _d_step(Dh, real.to(gpu_device), fake.to(gpu_device), rp.to(gpu_device))
+    p64, l64, g64 = runs['f64']
+    p32, l32, g32 = runs['f32']
+    assert normwise_rel(ph.detach().cpu(), p64) < max(1e-5, 5 * normwise_rel(p32, p64))
+    for k in lh:
+        e, e32 = abs(float(lh[k]) - l64[k]), abs(l32[k] - l64[k])
+        assert e <= max(1e-5 * max(1.0, abs(l64[k])), 5 * e32), (k, e, e32)
+    e_hip = _grad_errors([(k, p.grad) for k, p in Dh.named_parameters()], g64)
+    e_32 = _grad_errors(list(g32.items()), g64)
+    # 10x here (5x against the fixture above): with kaiming-scale weights the penalty is ~1e3 and the BatchNorm shift
+    # gradients are sums that cancel to ~1e-3 of their terms, so their fp32 error is summation-order noise
+    bad = {k: (e_hip[k], e_32[k]) for k in e_hip if e_hip[k] > max(1e-4, 10 * e_32[k])}
+    assert not bad, bad

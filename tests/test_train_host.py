@@ -17,9 +17,11 @@ from esr_amd import SRRaGAN_model as M
 from oracle.recipe import seeded_params
 
 
-def _disc_from_fixture(d):
-    D = Discriminator_VGG_128_(in_nc=3, base_nf=64, norm_type='batch', act_type='leakyrelu', mode='CNA',
-                               input_patch_size=80, nb=6)
+def _disc_from_fixture(d, D=None):
+    """The fixture's seeded parameters loaded into D (default: the oracle's torch.nn restatement, CPU)."""
+    if D is None:
+        from oracle.esr_oracle import reference_discriminator
+        D = reference_discriminator(nb=6)
     ref_keys = json.loads(str(d['keys']))
     assert [(k, list(v.shape)) for k, v in D.state_dict().items()] == [(k, list(s)) for k, s in ref_keys]
     params = seeded_params([(k, s) for k, s in ref_keys if 'running' not in k and 'num_batches' not in k],
@@ -49,6 +51,20 @@ def test_discriminator_and_wgan_gp_losses_match_reference():
     for k, v in D.state_dict().items():
         if 'running' in k:
             assert normwise_rel(v, d['buf:' + k]) < 1e-5, k
+
+
+def test_hip_discriminator_module_tree_and_no_cpu_path():
+    """esr_amd's Discriminator_VGG_128_ keeps the reference's state_dict keys/shapes/order (positional checkpoint
+    loading, base_model.py:117-141) with HipConv2d convolutions, and refuses CPU tensors (no silent fallback)."""
+    d = golden('disc_vgg128_nb6')
+    D = Discriminator_VGG_128_(in_nc=3, base_nf=64, norm_type='batch', act_type='leakyrelu', mode='CNA',
+                               input_patch_size=80, nb=6)
+    ref_keys = json.loads(str(d['keys']))
+    assert [(k, list(v.shape)) for k, v in D.state_dict().items()] == [(k, list(s)) for k, s in ref_keys]
+    convs = [m for m in D.modules() if isinstance(m, torch.nn.Conv2d)]
+    assert len(convs) == 8 and all(type(m).__name__ == 'HipConv2d' for m in convs)
+    with pytest.raises(RuntimeError, match='no CPU path'):
+        D(torch.zeros(1, 3, 80, 80))
 
 
 def test_range_loss_matches_reference():
