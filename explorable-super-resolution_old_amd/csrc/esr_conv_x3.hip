@@ -103,13 +103,15 @@ __device__ __forceinline__ float split_at(const float *buf, long long pix, int c
     return (float)g[ch & 7] + (float)g[8 + (ch & 7)];
 }
 
-template <int N>
-__device__ __forceinline__ bool store_tile(const X3Params &p, const float *s_ep, int r_first, int x0, int tw, int nq,
-                                           int tid) {
+// store_px: NTH_ cooperating threads (thread index t) store NPX consecutive pixels q0 .. q0+NPX-1 of the tile, whose
+// accumulators s_ep holds in rows 0 .. NPX-1 (a whole tile by the workgroup, or one 32-pixel M-tile by its wave).
+template <int N, int NTH_, int NPX>
+__device__ __forceinline__ bool store_px(const X3Params &p, const float *s_ep, int q0, int r_first, int x0, int tw,
+                                         int nq, int t) {
     constexpr int EP_P = N + 4;
     constexpr int GROUPS = N / 8;
-    constexpr int PPI = NTHR / GROUPS;         // pixels per iteration
-    constexpr int ITERS = TH * TWF / PPI;      // 4 (N = 32) or 8 (N = 64)
+    constexpr int PPI = NTH_ / GROUPS;         // pixels per iteration
+    constexpr int ITERS = NPX / PPI;
     const esr_conv_out &o = p.o;
     const long long orow = (long long)(o.out_w + 2);
     const int HP = p.H + 2;
@@ -130,12 +132,12 @@ __device__ __forceinline__ bool store_tile(const X3Params &p, const float *s_ep,
         return q < nq && b < p.B && y >= 0 && y < p.H;
     };
     if (o.out_planar) {
-        for (int u = tid; u < nq * p.cout; u += NTHR) {
-            const int c = u / nq, q = u - c * nq;
+        for (int it = t; it < NPX * p.cout; it += NTH_) {
+            const int c = it / NPX, qq = it - c * NPX;
             long long opix;
             int b, oy, ox;
-            if (!locate(q, opix, b, oy, ox)) continue;
-            float v = s_ep[q * EP_P + c] * p.w_scale_inv + p.bias[c];
+            if (!locate(q0 + qq, opix, b, oy, ox)) continue;
+            float v = s_ep[qq * EP_P + c] * p.w_scale_inv + p.bias[c];
             if (o.lrelu) v = lrelu(v);
             if (o.r1) v = o.s1 * v + split_at(o.r1, opix, o.r1_cp, o.r1_coff + c);
             if (o.r2) v = o.s2 * v + split_at(o.r2, opix, o.r2_cp, o.r2_coff + c);
@@ -143,7 +145,7 @@ __device__ __forceinline__ bool store_tile(const X3Params &p, const float *s_ep,
         }
         return true;
     }
-    const int g = tid % GROUPS;
+    const int g = t % GROUPS;
     const int c = 8 * g;
     if (c >= p.cout) return true;
     float bk[8];
@@ -154,7 +156,7 @@ __device__ __forceinline__ bool store_tile(const X3Params &p, const float *s_ep,
 #pragma unroll
     for (int k = 0; k < ITERS; ++k) {
         int b, oy, ox;
-        val[k] = locate(tid / GROUPS + k * PPI, opix[k], b, oy, ox);
+        val[k] = locate(q0 + t / GROUPS + k * PPI, opix[k], b, oy, ox);
     }
     float r1v[ITERS][8], r2v[ITERS][8];
     if (o.r1) {
@@ -173,10 +175,10 @@ __device__ __forceinline__ bool store_tile(const X3Params &p, const float *s_ep,
 #pragma unroll
     for (int k = 0; k < ITERS; ++k) {
         if (!val[k]) continue;
-        const int q = tid / GROUPS + k * PPI;
+        const int qq = t / GROUPS + k * PPI;
         float v[8];
-        const f32x4 v0 = *reinterpret_cast<const f32x4 *>(s_ep + q * EP_P + c);
-        const f32x4 v1 = *reinterpret_cast<const f32x4 *>(s_ep + q * EP_P + c + 4);
+        const f32x4 v0 = *reinterpret_cast<const f32x4 *>(s_ep + qq * EP_P + c);
+        const f32x4 v1 = *reinterpret_cast<const f32x4 *>(s_ep + qq * EP_P + c + 4);
 #pragma unroll
         for (int j = 0; j < 4; ++j) { v[j] = v0[j]; v[j + 4] = v1[j]; }
 #pragma unroll
@@ -191,6 +193,12 @@ __device__ __forceinline__ bool store_tile(const X3Params &p, const float *s_ep,
             store_group(reinterpret_cast<unsigned char *>(o.out2) + (opix[k] * o.out2_cp + o.out2_coff + c) * 4, v);
     }
     return ok;
+}
+
+template <int N>
+__device__ __forceinline__ bool store_tile(const X3Params &p, const float *s_ep, int r_first, int x0, int tw, int nq,
+                                           int tid) {
+    return store_px<N, NTHR, TH * TWF>(p, s_ep, 0, r_first, x0, tw, nq, tid);
 }
 
 template <int NT, int TS>
@@ -611,6 +619,229 @@ __global__ __launch_bounds__(NTHR, 1) void conv_x3_ring_kernel(X3Params p) {
     if (!ok && p.overflow) atomicOr(p.overflow, 1);
 }
 
+// ---- persistent ring kernel (N = 32, 3×3) ---------------------------------------------------------------------------
+//
+// The ring kernel above still pays, per workgroup, a cold prologue (its first tiles come from HBM with nothing to
+// overlap) and an epilogue whose 16 KB per wave of stores issue at ~7 B/cycle/CU while the matrix pipe idles; with three
+// rounds of workgroups per launch that was ~15-20 % of an RDB conv (ablation in DESIGN.md §5).  Here one workgroup per
+// CU walks its tile pairs (blockIdx.x, +gridDim.x, ...) as ONE stream of units: the 3-slot input ring and the 2-slot
+// weight ring prefetch across pair boundaries (the next pair's first two input tiles and first weight chunk are in
+// flight while the current pair finishes), and a pair's epilogue runs per wave — each wave restages its own 32-pixel
+// M-tiles in the input slot the pair's last unit released and issues their stores, which then drain behind the next
+// pair's MFMAs.  Fragments are read PF taps ahead; DMA addresses are 32-bit offsets from the fetched pair's first row
+// and the lo halves of the A/B fragments are at offset ^ 16, which pays for the deeper fragment ring in registers.
+// Per accumulator the MFMA sequence is the classic kernel's: results are bitwise identical.
+// Measured (tools/x3_ring_ab.py, config-2 shapes): within ±3 % of the non-persistent ring kernel (prefetch 2) and
+// slower at 96² — the store issue of the epilogue, not the cold prologue, is what the ring kernel loses per pair — so
+// it is not selected by default (esr_x3_set_kernel 16 / 17).
+template <int PF>
+__global__ __launch_bounds__(NTHR, 1) void conv_x3_pring_kernel(X3Params p) {
+    constexpr int NIN = 3;
+    constexpr int T = 9;
+    constexpr int N = 32;
+    constexpr int W_RECS = T * N;
+    constexpr int IN_B = IN_RECS * REC;
+    constexpr int W_B = W_RECS * REC;
+    constexpr int W_PIECES = W_RECS / 16;
+    constexpr int EP_P = N + 4;
+    constexpr int EPW_FLOATS = 32 * EP_P;  // one wave's restage area: one M-tile of 32 pixels
+    constexpr int LDS_BYTES = 2 * W_B + NIN * IN_B;
+    constexpr int KIN = (IN_PIECES + NWAVES - 1) / NWAVES;
+    constexpr int KW = (W_PIECES + NWAVES - 1) / NWAVES;
+    static_assert(NWAVES * EPW_FLOATS * 4 <= IN_B, "per-wave epilogue areas fit in one input slot");
+    static_assert(LDS_BYTES <= 163840, "LDS");
+    __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int hl = lane >> 5;
+    const int ml = lane & 31;
+    const int sub = lane >> 2, ps = lane & 3;
+    const int npairs = p.tiles_x * ((p.tiles_y + 1) / 2);
+    const int my_pairs = (npairs - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+    if (my_pairs <= 0) return;
+    const int nchunk = (p.cin + 15) >> 4;
+    const int upp = 2 * nchunk;  // units per pair
+    const int nunits = my_pairs * upp;
+    const int rows_tot = p.B * (p.H + 2);
+    const long long rowp = (long long)(p.W + 2);
+    const long long pixb = 4LL * p.in_cp;
+    const long long tile_step = TH * rowp * pixb;
+
+    auto pair_geo = [&](int i, int &x0, int &tw, int &r0) {
+        const int pr = (int)blockIdx.x + i * (int)gridDim.x;
+        x0 = (pr % p.tiles_x) * TWF;
+        tw = min(TWF, p.W - x0);
+        r0 = 2 * (pr / p.tiles_x) * TH;
+    };
+
+    // LDS-DMA addressing of the pair being fetched (switches to the next pair ahead of the compute pair)
+    int in_off[KIN], in_code[KIN];  // code = (halo row << 2) | (split group of the slot + 1); 0 = zero page
+    int dma_pair = -1, dma_r0 = 0;
+    auto set_dma = [&](int i) {
+        int x0, tw, r0;
+        pair_geo(i, x0, tw, r0);
+        const int hx = tw + 2;
+#pragma unroll
+        for (int k = 0; k < KIN; ++k) {
+            const int pc = min(wave + NWAVES * k, IN_PIECES - 1);
+            const int r = 16 * pc + sub;
+            const int s = ps ^ ((r >> 2) & 3);
+            const int hy = r / hx;
+            const int gx = x0 + r - hy * hx;
+            const bool v = r < HY * hx && gx < p.W + 2;
+            in_off[k] = v ? (int)((hy * rowp + gx) * pixb + (s << 4)) : 0;
+            in_code[k] = v ? ((hy << 2) | ((s >> 1) + 1)) : 0;
+        }
+        dma_pair = i;
+        dma_r0 = r0;
+    };
+    auto dma_in = [&](int v, int slot) {  // input of global unit v
+        const int i = v / upp;
+        if (i != dma_pair) set_dma(i);
+        const int lv = v - i * upp;
+        const int j = lv >> 1, t = lv & 1;
+        const int groups = min(16, p.cin - 16 * j) >> 3;
+        const unsigned char *base = p.in + (long long)dma_r0 * rowp * pixb + t * tile_step + 64LL * j;
+        unsigned char *dst = lds + 2 * W_B + slot * IN_B;
+#pragma unroll
+        for (int k = 0; k < KIN; ++k) {
+            const int pc = min(wave + NWAVES * k, IN_PIECES - 1);
+            const int code = in_code[k];
+            const bool ok = code != 0 && (code & 3) - 1 < groups && dma_r0 + (code >> 2) + t * TH < rows_tot;
+            const void *src = ok ? (const void *)(base + in_off[k]) : (const void *)g_zero_page;
+            __builtin_amdgcn_global_load_lds((glob_void *)src, (lds_void *)(dst + pc * 1024), 16, 0, 0);
+        }
+    };
+    auto dma_w = [&](int c, int slot) {  // weights of global chunk c (= chunk c % nchunk of every pair)
+        const unsigned char *wj = p.w + (long long)(c % nchunk) * W_B;
+        unsigned char *dst = lds + slot * W_B;
+#pragma unroll
+        for (int i = 0; i < KW; ++i) {
+            const int k = min(wave + NWAVES * i, W_PIECES - 1);
+            const int r = 16 * k + sub;
+            const int s = ps ^ ((r >> 2) & 3);
+            __builtin_amdgcn_global_load_lds((glob_void *)(wj + r * REC + (s << 4)), (lds_void *)(dst + k * 1024), 16,
+                                             0, 0);
+        }
+    };
+
+    // geometry of the pair being computed; fragment offsets of the hi halves (lo = offset ^ 16)
+    int aoff[T][2];
+    bool mvalid[2];
+    int cx0 = 0, ctw = TWF, cr0 = 0, cnq = TH * TWF;
+    auto set_geo = [&](int i) {
+        pair_geo(i, cx0, ctw, cr0);
+        const int hx = ctw + 2;
+        cnq = TH * ctw;
+        const int nmt = (cnq + 31) >> 5;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+            const int jm = 2 * wave + mt;
+            mvalid[mt] = jm < nmt;
+            int q = 32 * jm + ml;
+            if (q >= cnq) q = 0;
+            const int rec0 = (q / ctw) * hx + q % ctw;
+#pragma unroll
+            for (int tap = 0; tap < T; ++tap) aoff[tap][mt] = slot_off(rec0 + (tap / 3) * hx + tap % 3, 2 * hl);
+        }
+    };
+    const int boff = ml * REC + (((2 * hl) ^ ((ml >> 2) & 3)) << 4);
+
+    f32x16 acc[2][2];
+    auto zero_acc = [&]() {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[t][mt][r] = 0.f;
+    };
+
+    auto compute = [&](const unsigned char *s_in, const unsigned char *s_w, f32x16(&ac)[2]) {
+        constexpr int NBUF = PF + 1;
+        f16x8 ah[NBUF][2], al[NBUF][2], bh[NBUF], bl[NBUF];
+        auto ld = [&](int tap, int buf) {
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                ah[buf][mt] = *reinterpret_cast<const f16x8 *>(s_in + aoff[tap][mt]);
+                al[buf][mt] = *reinterpret_cast<const f16x8 *>(s_in + (aoff[tap][mt] ^ 16));
+            }
+            bh[buf] = *reinterpret_cast<const f16x8 *>(s_w + tap * N * REC + boff);
+            bl[buf] = *reinterpret_cast<const f16x8 *>(s_w + tap * N * REC + (boff ^ 16));
+        };
+#pragma unroll
+        for (int k = 0; k < PF; ++k) ld(k, k);
+#pragma unroll
+        for (int tap = 0; tap < T; ++tap) {
+            const int cb = tap % NBUF;
+            if (tap + PF < T) ld(tap + PF, (tap + PF) % NBUF);
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+                if (mvalid[mt]) ac[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[cb][mt], bh[cb], ac[mt], 0, 0, 0);
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+                if (mvalid[mt]) ac[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[cb][mt], bl[cb], ac[mt], 0, 0, 0);
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+                if (mvalid[mt]) ac[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[cb][mt], bh[cb], ac[mt], 0, 0, 0);
+        }
+    };
+
+    auto unit = [&](int u, f32x16(&ac)[2]) {
+        raw_barrier();
+        const bool bi = u + NIN - 1 < nunits;
+        if (bi) dma_in(u + NIN - 1, (u + NIN - 1) % NIN);
+        const bool bw = !(u & 1) && (u >> 1) + 1 < (nunits >> 1);
+        if (bw) dma_w((u >> 1) + 1, ((u >> 1) + 1) & 1);
+        if (mvalid[0]) compute(lds + 2 * W_B + (u % NIN) * IN_B, lds + ((u >> 1) & 1) * W_B, ac);
+        if (u + 1 < nunits) {
+            if (bi && bw) wait_vm_lgkm0<KIN + KW>();
+            else if (bi) wait_vm_lgkm0<KIN>();
+            else if (bw) wait_vm_lgkm0<KW>();
+            else wait_vm_lgkm0<0>();
+        }
+    };
+
+    // per-wave epilogue of the pair just computed, staged in input slot `slot` (free: its unit has been consumed by
+    // every wave, and its next DMA is issued only after the next unit's barrier)
+    auto epilogue = [&](int slot) {
+        float *s_ep = reinterpret_cast<float *>(lds + 2 * W_B + slot * IN_B) + wave * EPW_FLOATS;
+        bool ok = true;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                if (!mvalid[mt]) continue;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) s_ep[((r & 3) + 8 * (r >> 2) + 4 * hl) * EP_P + ml] = acc[t][mt][r];
+                ok &= store_px<N, 64, 32>(p, s_ep, 32 * (2 * wave + mt), cr0 + t * TH, cx0, ctw, cnq, lane);
+            }
+        if (!ok && p.overflow) atomicOr(p.overflow, 1);
+    };
+
+    set_dma(0);
+    dma_in(0, 0);
+    dma_w(0, 0);
+    dma_in(1, 1);
+    wait_vm_lgkm0<KIN>();
+    set_geo(0);
+    zero_acc();
+    for (int u = 0; u < nunits; u += 2) {
+        unit(u, acc[0]);
+        unit(u + 1, acc[1]);
+        if ((u + 2) % upp == 0) {
+            raw_barrier();
+            epilogue((u + 1) % NIN);
+            if (u + 2 < nunits) {
+                set_geo((u + 2) / upp);
+                zero_acc();
+            }
+        }
+    }
+}
+
 int g_x3_kernel = 1;  // esr_x3_set_kernel (include/esr_amd.h)
 
 int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const void *w, const float *bias,
@@ -646,7 +877,13 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
                 hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
     }
     const bool ring_pays = 18 * ((pairs + n_cu - 1) / n_cu) < 10 * ((tiles + n_cu - 1) / n_cu);
-    if (taps_side == 3 && cout <= 32 && g_x3_kernel >= 1 && (ring_pays || g_x3_kernel >= 2)) {
+    if (taps_side == 3 && cout <= 32 && (g_x3_kernel == 16 || g_x3_kernel == 17)) {
+        const dim3 gridp((unsigned)min(pairs, n_cu));
+        if (g_x3_kernel == 16) hipLaunchKernelGGL((conv_x3_pring_kernel<1>), gridp, block, 0, stream, p);
+        else hipLaunchKernelGGL((conv_x3_pring_kernel<2>), gridp, block, 0, stream, p);
+        return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+    }
+    if (taps_side == 3 && cout <= 32 && (g_x3_kernel >= 2 || (g_x3_kernel == 1 && ring_pays))) {
         const dim3 grid2((unsigned)pairs);
 #define RING_DBG(v, bits) \
     case v: hipLaunchKernelGGL((conv_x3_ring_kernel<3, true, bits>), grid2, block, 0, stream, p); break;
@@ -690,7 +927,7 @@ extern "C" int esr_conv3x3_fwd_x3(const void *in, int32_t B, int32_t H, int32_t 
 }
 
 extern "C" int esr_x3_set_kernel(int32_t variant) {
-    if (variant < 0 || variant > 15) return ESR_EINVAL;
+    if (variant < 0 || variant > 17) return ESR_EINVAL;
     const int prev = g_x3_kernel;
     g_x3_kernel = variant;
     return prev;

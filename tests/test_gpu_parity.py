@@ -280,9 +280,10 @@ def test_conv3x3_layer_x3(gpu_device, cin, cout, H, W):
 @pytest.mark.parametrize('cin,cout,B,H,W', [(64, 32, 3, 40, 148), (136, 32, 5, 17, 45), (104, 24, 2, 33, 70),
                                             (16, 32, 1, 1, 1), (160, 32, 4, 96, 33)])
 def test_x3_ring_kernel_bitwise_equals_classic(gpu_device, cin, cout, B, H, W):
-    """The N<=32 ring kernel (two tiles per workgroup, 3-deep LDS-DMA ring, counted vmcnt) runs the classic kernel's
-    MFMA sequence per accumulator: outputs, residual epilogue and out2 must agree bit for bit, including odd tile
-    counts (the second tile of the last pair is beyond the batch) and partial column tiles."""
+    """The N<=32 ring kernels (two tiles per workgroup, 3-deep LDS-DMA ring, counted vmcnt; and the persistent variant
+    that streams several tile pairs per workgroup with a per-wave epilogue) run the classic kernel's MFMA sequence per
+    accumulator: outputs, residual epilogue and out2 must agree bit for bit, including odd tile counts (the second tile
+    of the last pair is beyond the batch) and partial column tiles."""
     lib = _lib.load()
     cp = cin + 8
     xs = engine.to_split(_padded(B, H, W, cp, cin, gpu_device, 21))
@@ -293,7 +294,7 @@ def test_x3_ring_kernel_bitwise_equals_classic(gpu_device, cin, cout, B, H, W):
     rs = engine.to_split(_padded(B, H, W, 40, 40, gpu_device, 23))
     outs = []
     try:
-        for variant in (0, 2):  # classic only, ring always
+        for variant in (0, 2, 17):  # classic only, ring always, persistent ring always
             lib.esr_x3_set_kernel(variant)
             out = torch.zeros(B, H + 2, W + 2, 40, device=gpu_device)
             out2 = torch.zeros(B, H + 2, W + 2, 32, device=gpu_device)
@@ -305,7 +306,8 @@ def test_x3_ring_kernel_bitwise_equals_classic(gpu_device, cin, cout, B, H, W):
             outs.append((out, out2))
     finally:
         lib.esr_x3_set_kernel(1)
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    for k in (1, 2):
+        assert torch.equal(outs[0][0], outs[k][0]) and torch.equal(outs[0][1], outs[k][1]), k
     ref = F.leaky_relu(F.conv2d(_nchw(engine.from_split(xs), 0, cin), w.double(), b.cpu().double(), padding=1), 0.2)
     ref = 0.2 * ref + _nchw(engine.from_split(rs), 0, cout)
     assert normwise_rel(_nchw(engine.from_split(outs[1][0]), 8, 8 + cout), ref) < 1e-5
