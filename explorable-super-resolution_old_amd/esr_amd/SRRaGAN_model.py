@@ -6,8 +6,11 @@ Keeps the interface the reference's drivers use — `feed_data`, `ConcatLatent`,
 CEM_arch, latent `all_layers`/`HR_downscaled` (or no latent), WGAN-GP (non-relativistic), range loss, D_verification
 'past'/None, gradient accumulation.  Options the shipped configs switch off (VGG feature loss — broken in the
 reference, pixel/high-pass/shift-invariant/optimal-Z/latent losses, encoder, decomposed D input) raise
-NotImplementedError instead of silently differing.  Logging to files, checkpoint rotation and plotting are out of
-scope.
+NotImplementedError instead of silently differing.  Checkpoints and logs keep the reference's formats
+(base_model.py:86-144; SRRaGAN_model.py:695-719, 766-813): `{step}_G.pth` / `{step}_D.pth` dicts with
+model_state_dict + optimizer_state_dict, the positional key-remapping loader with the latent-channel zero-prepend, and
+logs.npz / lr.npz; checkpoints are read with torch.load(weights_only=True).  Checkpoint rotation, plotting and
+TensorBoard are out of scope.
 
 Multi-GPU: one process per GPU (torch.distributed, RCCL).  The reference's nn.DataParallel computes every loss on the
 gathered global batch; with equal per-rank batches the average of per-rank gradients equals that gradient, so after
@@ -15,7 +18,11 @@ each backward the G / D gradients are all-reduced (average, one flat bucket per 
 per-replica (as DataParallel's) and the running buffers are broadcast from rank 0 (DataParallel keeps replica 0's).
 The per-image D statistics that gate the generator step are all-reduced so that every rank takes the same branch.
 """
+import collections
 import math
+import os
+import re
+import warnings
 from collections import OrderedDict
 
 import numpy as np
@@ -90,8 +97,12 @@ class SRRaGANModel:
             self.Z_size_factor = opt['scale'] if 'HR' in self.latent_input_domain else 1
         self.CEM_arch = bool(opt_G.get('CEM_arch'))
         self.step = 0
+        self.gradient_step_num = 0
         self.generator_step = False
         self.CEM_net = None
+        paths = opt.get('path') or {}
+        self.save_dir = paths.get('models')
+        self.log_path = paths.get('log')
         if self.CEM_arch or self.latent_input is not None:
             conf = CEMnet.Get_CEM_Config(opt['scale'])
             conf.input_range = np.array(opt.get('range', [0, 1]))
@@ -135,7 +146,15 @@ class SRRaGANModel:
         self.l_range_w = t.get('range_weight', 0)
         self.optimizers = []
         gparams = [p for p in self.netG.parameters() if p.requires_grad]
-        self.optimizer_G = torch.optim.Adam(gparams, lr=t['lr_G'], weight_decay=t.get('weight_decay_G') or 0,
+        lr_G, lr_D = t['lr_G'], t.get('lr_D')
+        lr_file = os.path.join(self.log_path, 'lr.npz') if self.log_path else None
+        if lr_file and os.path.isfile(lr_file):  # SRRaGAN_model.py:212-216: learning rates decayed by a resumed run
+            with np.load(lr_file) as f:
+                lr_G, lr_D = float(f['lr_G']), float(f['lr_D'])
+        if self.latent_input is not None:  # SRRaGAN_model.py:79-80
+            self.latent_grads_multiplier = t['lr_latent'] / t['lr_G'] if t.get('lr_latent') else 1
+            self.channels_idx_4_grad_amplification = [[] for _ in self.netG.parameters()]
+        self.optimizer_G = torch.optim.Adam(gparams, lr=lr_G, weight_decay=t.get('weight_decay_G') or 0,
                                             betas=(t['beta1_G'], 0.999))
         self.optimizers.append(self.optimizer_G)
         if self.D_exists:
@@ -147,7 +166,7 @@ class SRRaGANModel:
             if t['gan_type'] == 'wgan-gp':
                 self.cri_gp = GradientPenaltyLoss(device=self.device)
                 self.l_gp_w = t['gp_weigth']
-            self.optimizer_D = torch.optim.Adam(self.netD.parameters(), lr=t['lr_D'],
+            self.optimizer_D = torch.optim.Adam(self.netD.parameters(), lr=lr_D,
                                                 weight_decay=t.get('weight_decay_D') or 0, betas=(t['beta1_D'], 0.999))
             self.optimizers.append(self.optimizer_D)
         else:
@@ -165,6 +184,10 @@ class SRRaGANModel:
             self.model_input = torch.cat([latent_input, LR_image], dim=1)
         else:
             self.model_input = 1 * LR_image
+
+    def AssignLatent(self, latent_input):
+        """SRRaGAN_model.py:260-261."""
+        self.netG.module.generated_image_model.Z = latent_input
 
     def GetLatent(self):
         latent = 1 * self.model_input[:, :-3, ...]
@@ -312,6 +335,10 @@ class SRRaGANModel:
             l_g_total.backward()
             if last_acc_G:
                 _allreduce_grads([p for p in self.netG.parameters() if p.requires_grad])
+                if self.latent_input is not None and self.latent_grads_multiplier != 1:  # :543-546
+                    for idx, p in zip(self.channels_idx_4_grad_amplification, self.netG.parameters()):
+                        for c in idx:
+                            p.grad[:, c, ...] *= self.latent_grads_multiplier
                 self.optimizer_G.step()
                 g = self.gradient_step_num
                 if self.cri_range is not None:
@@ -343,3 +370,133 @@ class SRRaGANModel:
         if need_HR:
             out['HR'] = self.var_H.detach()[sel].float().cpu()
         return out
+
+    # ------------------------------------------------------------------------------------------------------------------
+    # checkpoints and logs (base_model.py:86-144; SRRaGAN_model.py:695-719, 766-813)
+    # ------------------------------------------------------------------------------------------------------------------
+    def save_network(self, save_dir, network, network_label, iter_label, optimizer):
+        """base_model.py:86-97: `{iter}_{label}.pth` = {'model_state_dict' (CPU tensors), 'optimizer_state_dict'}."""
+        path = os.path.join(save_dir, '{}_{}.pth'.format(iter_label, network_label))
+        if hasattr(network, 'module'):
+            network = network.module
+        sd = network.state_dict()
+        for k in sd:
+            sd[k] = sd[k].cpu()
+        torch.save({'model_state_dict': sd, 'optimizer_state_dict': optimizer.state_dict()}, path)
+        return path
+
+    def load_network(self, load_path, network, strict=False, optimizer=None):
+        """base_model.py:100-111.  Plain state dicts (pretrained ESRGAN files) and {model, optimizer} dicts both load;
+        the file is read with torch.load(weights_only=True) (no pickled code is executed)."""
+        if hasattr(network, 'module'):
+            network = network.module
+        loaded = torch.load(load_path, map_location='cpu', weights_only=True)
+        if 'optimizer_state_dict' in loaded:
+            if optimizer is not None:
+                optimizer.load_state_dict(loaded['optimizer_state_dict'])
+            loaded = loaded['model_state_dict']
+        if self.CEM_arch:
+            loaded = CEMnet.Adjust_State_Dict_Keys(loaded, network.state_dict())
+        loaded = self.process_loaded_state_dict(loaded_state_dict=loaded, current_state_dict=network.state_dict())
+        network.load_state_dict(loaded, strict=strict)  # bumps the parameter versions: packed weights refresh
+
+    def process_loaded_state_dict(self, loaded_state_dict, current_state_dict):
+        """base_model.py:113-144: keys are matched by POSITION (old non-ModuleList checkpoints have other names; the
+        shapes must agree up to the input-channel dim).  A weight whose current input-channel count is the loaded one
+        plus num_latent_channels (× 1 or × scale²) gets zero weights prepended for the latent channels
+        (LATENT_WEIGHTS_RELATIVE_STD = 0) and its channels recorded for latent gradient amplification.  CEM filter
+        weights are never loaded (the current design is kept)."""
+        out = collections.OrderedDict()
+        cur_keys = list(current_state_dict.keys())
+        assert len(cur_keys) == len(loaded_state_dict), 'Loaded model and current one should have the same number of ' \
+                                                        'parameters'
+        renamed = 0
+        op_names = getattr(self.CEM_net, 'OP_names', []) if self.CEM_net is not None else []
+        for i, key in enumerate(loaded_state_dict.keys()):
+            ck = cur_keys[i]
+            lv, cv = loaded_state_dict[key], current_state_dict[ck]
+            ls, cs = tuple(lv.size()), tuple(cv.size())
+            if key != ck:
+                assert ls[:1] + ls[2:] == cs[:1] + cs[2:], 'Unmatching parameter sizes after changing parameter key name'
+                renamed += 1
+            if self.latent_input is not None and 'weight' in key and lv.dim() > 1 and \
+                    cs[1] in list(ls[1] + self.num_latent_channels * np.array([1, self.opt['scale'] ** 2])):
+                extra = cs[1] - ls[1]
+                out[ck] = torch.cat([torch.zeros((cs[0], extra) + cs[2:], dtype=lv.dtype), lv.cpu()], 1)
+                if hasattr(self, 'channels_idx_4_grad_amplification'):
+                    self.channels_idx_4_grad_amplification[i] = list(range(extra))
+            elif self.CEM_arch and any(op in key for op in op_names):
+                continue
+            else:
+                out[ck] = lv
+        if renamed:
+            warnings.warn('Modified %d key names due to the change to using ModuleLists' % renamed)
+        return out
+
+    @staticmethod
+    def _step_of(name):
+        return int(re.search(r'(\d)+(?=_G.pth)', name).group(0))
+
+    def load(self, max_step=None, resume_train=None):
+        """SRRaGAN_model.py:766-805: the latest (or latest <= max_step) `{step}_G.pth` under path.models when resuming
+        or testing, else path.pretrain_model_G / _D."""
+        resume = resume_train if resume_train is not None else (self.is_train and self.opt['train'].get('resume'))
+        paths = self.opt.get('path') or {}
+        if max_step is not None or resume or not self.is_train:
+            names = sorted([n for n in os.listdir(self.save_dir) if '_G.pth' in n], key=self._step_of)
+            if max_step is not None:
+                names = [n for n in names if self._step_of(n) <= max_step]
+            name = names[-1]
+            step = self._step_of(name)
+            if self.is_train:
+                self.step = (step + 1) * self.max_accumulation_steps
+                self.load_network(os.path.join(self.save_dir, name), self.netG, optimizer=self.optimizer_G)
+                if self.log_path and os.path.isfile(os.path.join(self.log_path, 'logs.npz')):
+                    self.load_log(max_step=step)
+                if self.D_exists:
+                    self.load_network(os.path.join(self.save_dir, '%d_D.pth' % step), self.netD,
+                                      optimizer=self.optimizer_D)
+            else:
+                self.load_network(os.path.join(self.save_dir, name), self.netG)
+                if getattr(self, 'netD', None) is not None:
+                    self.load_network(os.path.join(self.save_dir, name.replace('_G', '_D')), self.netD)
+                self.gradient_step_num = step
+        else:
+            if paths.get('pretrain_model_G') is not None:
+                self.load_network(paths['pretrain_model_G'], self.netG)
+            if self.is_train and paths.get('pretrain_model_D') is not None and getattr(self, 'netD', None) is not None:
+                self.load_network(paths['pretrain_model_D'], self.netD, optimizer=self.optimizer_D)
+
+    def save(self, iter_label):
+        """SRRaGAN_model.py:807-813."""
+        path = self.save_network(self.save_dir, self.netG, 'G', iter_label, self.optimizer_G)
+        if getattr(self, 'D_exists', False):
+            self.save_network(self.save_dir, self.netD, 'D', iter_label, self.optimizer_D)
+        return path
+
+    def save_log(self):
+        """SRRaGAN_model.py:695-698: logs.npz, one array of (step, value) rows per log key."""
+        np.savez(os.path.join(self.log_path, 'logs.npz'), **{k: np.asarray(v, dtype=np.float64).reshape(-1, 2)
+                                                                 for k, v in self.log_dict.items()})
+
+    def save_lr(self, step_num):
+        """The lr.npz the reference writes when it decays the learning rates (SRRaGAN_model.py:676-681), read back by
+        the optimizer set-up of a resumed run."""
+        np.savez(os.path.join(self.log_path, 'lr.npz'), step_num=step_num, lr_G=self.optimizer_G.param_groups[0]['lr'],
+                 lr_D=self.optimizer_D.param_groups[0]['lr'])
+
+    def load_log(self, max_step=None):
+        """SRRaGAN_model.py:700-714 (logs entries the reference stored as pickled objects are skipped: the file is read
+        with allow_pickle=False)."""
+        self.log_dict = OrderedDict((k, []) for k in self.log_dict)
+        with np.load(os.path.join(self.log_path, 'logs.npz')) as f:
+            for key in f.files:
+                try:
+                    arr = f[key]
+                except ValueError:
+                    warnings.warn('logs.npz: skipping %r (object array)' % key)
+                    continue
+                rows = [tuple(r) for r in np.asarray(arr).reshape(len(arr), -1).tolist()] if len(arr) else []
+                if max_step is not None:
+                    rows = [r for r in rows if r[0] <= max_step]
+                self.log_dict[key] = rows

@@ -1,8 +1,8 @@
-"""CEM kernel helpers (host-side, NumPy float64) — counterpart of reference codes/CEM/imresize_CEM.py.
+"""CEM resampling — counterpart of reference codes/CEM/imresize_CEM.py.
 
-Only what the CEM filter design needs: the upscale kernel of a given scale factor (bicubic default, blurred bicubic,
-or a custom/learned kernel re-centred with Center_Mass) and the zero-padded integer downscale used to measure the
-ds_kernel's invalid margin.
+Host side (NumPy float64, filter design only): the upscale kernel of a given scale factor (bicubic default, blurred
+bicubic, or a custom/learned kernel re-centred with Center_Mass) and the zero-padded integer downscale used to measure
+the ds_kernel's invalid margin.  `imresize` itself runs on the device (esr_amd/cem_ops.py stencils).
 
 Behavioural difference by design: the reference caches the kernel in a process-global dict
 (`imresize.kernels`, imresize_CEM.py:9,23-42) so the first kernel of a scale factor silently wins; here the kernel is an
@@ -137,3 +137,61 @@ def downscale_zero_padded(im, sf, up_kernel):
     pre, _ = calc_strides(im, 1 / sf)
     aa = np.rot90(up_kernel * (1 / sf) ** 2, 2)
     return convolve2d(im, aa, mode='same')[pre[0]::sf, pre[1]::sf]
+
+
+def _to_device(im, device):
+    """NumPy HW / HWC image -> float32 device tensor [C, H, W] (C = 1 for HW) and a function mapping results back."""
+    import torch
+    if isinstance(im, torch.Tensor):
+        return im, lambda t: t
+    if device is None:
+        if not torch.cuda.is_available():
+            raise RuntimeError('esr_amd.imresize: needs a ROCm device (this build has no CPU path)')
+        device = torch.device('cuda', torch.cuda.current_device())
+    a = np.asarray(im)
+    hw = a.ndim < 3
+    t = torch.from_numpy(np.ascontiguousarray(a[None] if hw else np.moveaxis(a, -1, 0), dtype=np.float32)).to(device)
+
+    def back(y):
+        y = y.cpu().numpy()
+        return y[0] if hw else np.squeeze(np.moveaxis(y, 0, -1))
+    return t, back
+
+
+def imresize(im, scale_factor=None, output_shape=None, kernel=None, align_center=False, return_upscale_kernel=False,
+             use_zero_padding=False, antialiasing=True, kernel_shift_flag=False, device=None):
+    """imresize_CEM.py:7-71 on the device: integer down- or up-scaling of an image with the CEM anti-aliasing kernel.
+
+    `im`: NumPy HW or HWC array (returned as a float32 NumPy array of the reference's shape — np.squeeze'd, :71) or a
+    float32 ROCm tensor [..., H, W] (batched; returned on the device, e.g. on-the-fly LR for LRHR_dataset.py:87).
+    `kernel`: None / 'cubic' / 'reset_2_default' (bicubic), 'blurry_cubic_<sigma>', or a custom DOWNSCALE kernel
+    ndarray; unlike the reference it is not cached between calls (Appendix B of SURVEY.md), so pass the same kernel to
+    every call that should use it.  `antialiasing` and `kernel_shift_flag` are accepted and unused, as in the
+    reference.  align_center=True is the reference's hTh alias-sampling convention, not used with images: rejected.
+    """
+    if scale_factor is None:
+        scale_factor = [output_shape[0] / im.shape[0]]
+    elif not isinstance(scale_factor, (list, tuple)):
+        scale_factor = [scale_factor]
+    assert len(scale_factor) == 1 or scale_factor[0] == scale_factor[1]
+    s = scale_factor[0]
+    assert np.round(s) == s or np.round(1 / s) == 1 / s, 'Only supporting integer downsampling or upsampling rates'
+    sf = int(np.maximum(s, 1 / s))
+    k_up = upscale_kernel(sf, kernel)
+    aa = k_up if s >= 1 else np.rot90(k_up * s ** 2, 2)
+    if return_upscale_kernel:
+        return aa
+    if align_center:
+        raise NotImplementedError('imresize: align_center=True is not supported for images')
+    import torch
+    from . import cem_ops
+    x, back = _to_device(im, device)
+    if output_shape is not None:
+        assert np.all(s * np.array(x.shape[-2:]) == np.asarray(output_shape)[:2])
+    if s >= 1:
+        w = torch.from_numpy(np.ascontiguousarray(np.rot90(k_up, 2), dtype=np.float32)).to(x.device)
+        y = cem_ops.upscale(x, w, sf, zero_pad=use_zero_padding)
+    else:
+        w = torch.from_numpy(np.ascontiguousarray(k_up / sf ** 2, dtype=np.float32)).to(x.device)
+        y = cem_ops.downscale(x, w, sf, zero_pad=use_zero_padding)
+    return back(y)

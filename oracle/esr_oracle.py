@@ -138,7 +138,8 @@ def cem_design(sf=4, kernel=None, lower_magnitude_bound=0.01, perturbation_limit
     if drop > 0:
         inv = inv[drop:-drop, drop:-drop]
     m_lr = 2 * ds_half + inv_half
-    return dict(ds_kernel=ds, inv_hTh=inv, ds_half=ds_half, inv_half=inv_half, margins_LR=m_lr, margins_HR=sf * m_lr)
+    return dict(ds_kernel=ds, inv_hTh=inv, ds_half=ds_half, inv_half=inv_half, margins_LR=m_lr, margins_HR=sf * m_lr,
+                k_up=k_up, sf=sf)
 
 
 # ----------------------------------------------------------------------------------------------------------------------
@@ -184,6 +185,75 @@ def cem_forward(gen, lr, design, pre_pad, sf=4):
         M = design['margins_HR']
         out = out[:, :, M:-M, M:-M]
     return out
+
+
+# ----------------------------------------------------------------------------------------------------------------------
+# CEM NumPy image helpers (CEMnet.py:44-57, 88-100; imresize_CEM.py:7-71), HWC float64 like the reference
+# ----------------------------------------------------------------------------------------------------------------------
+def imresize_np(im, scale, k_up, use_zero_padding=False):
+    """imresize_CEM.py:7-71 for an integer up (scale = sf) or down (scale = 1/sf) factor, align_center=False, with the
+    padded upscale kernel k_up passed explicitly (the reference reads it from its process-global cache)."""
+    sf = int(round(max(scale, 1 / scale)))
+    post = sf // 2
+    pre = sf - post - 1
+    aa = k_up if scale > 1 else np.rot90(k_up * scale ** 2, 2)                        # :43-45
+    pad = np.array(aa.shape) // 2                                                      # :49
+    squeeze = im.ndim < 3
+    im = im[:, :, None] if squeeze else im
+    out = []
+    for c in range(im.shape[2]):
+        x = im[:, :, c]
+        if scale > 1:                                                                  # :57-63 zero-stuff, filter
+            s = np.zeros((sf * x.shape[0], sf * x.shape[1]))
+            s[pre::sf, pre::sf] = x
+            x = s
+        if use_zero_padding:
+            y = convolve2d(x, aa, mode='same')
+        else:
+            y = convolve2d(np.pad(x, ((pad[0], pad[0]), (pad[1], pad[1])), mode='edge'), aa, mode='valid')
+        out.append(y if scale > 1 else y[pre::sf, pre::sf])                            # :70
+    out = np.stack(out, -1)
+    return out[:, :, 0] if squeeze else out
+
+
+def dt_satisfying_upscale(lr, design):
+    """CEMnet.DT_Satisfying_Upscale (CEMnet.py:53-57): edge-pad, zero-padded 'same' convolution with inv_hTh,
+    imresize ×sf (edge padding), unpad."""
+    sf = design['sf']
+    m = 2 * design['inv_half'] + design['ds_half']
+    x = np.pad(lr, ((m, m), (m, m), (0, 0)), mode='edge')                              # Pad_Image, :221-222
+    x = np.stack([convolve2d(x[:, :, c], design['inv_hTh'], mode='same') for c in range(x.shape[-1])], -1)
+    y = imresize_np(x, sf, design['k_up'])
+    M = sf * m
+    return y[M:-M, M:-M, :]                                                            # Unpad_Image, :224-225
+
+
+def project_2_kernel_subspace(hr, design):
+    """CEMnet.py:98-100."""
+    return dt_satisfying_upscale(imresize_np(hr, 1 / design['sf'], design['k_up']), design)
+
+
+def enforce_dt_on_image_pair(lr_source, hr_input, design):
+    """CEMnet.py:88-96: the image closest to hr_input whose downscale is lr_source (LR or already HR-sized)."""
+    sf = design['sf']
+    same = [a == b for a, b in zip(lr_source.shape, hr_input.shape)]
+    lrs = [sf * a == b for a, b in zip(lr_source.shape, hr_input.shape)]
+    assert all(a or b for a, b in zip(same, lrs))
+    src = dt_satisfying_upscale(lr_source, design) if any(lrs) else project_2_kernel_subspace(lr_source, design)
+    return hr_input - project_2_kernel_subspace(hr_input, design) + src
+
+
+def pad_lr_batch(batch, m, num_recursion=1):
+    """CEMnet.py:44-47 (NHWC, edge padding by the LR invalidity margin, repeated)."""
+    for _ in range(num_recursion):
+        batch = 1.0 * np.pad(batch, ((0, 0), (m, m), (m, m), (0, 0)), mode='edge')
+    return batch
+
+
+def unpad_hr_batch(batch, m, sf, num_recursion=1):
+    """CEMnet.py:49-51 (Python slice semantics: an over-large margin yields an empty batch)."""
+    r = sf ** num_recursion * m * num_recursion
+    return batch[:, r:-r, r:-r, :]
 
 
 # ----------------------------------------------------------------------------------------------------------------------

@@ -283,9 +283,45 @@ def disc_fixture(arch, loss_mod, name, seed):
                                                                    l_d_gp.item(), len(named_shapes)))
 
 
+def cem_np_fixture(CEMnet, name, kernel):
+    """The reference's NumPy image helpers (CEMnet.py:44-57,88-100; imresize_CEM.py:7-71) on HWC float64 images.
+    Must run while imresize.kernels holds this CEMnet's kernel (the CEMnet constructor puts it there)."""
+    from CEM.imresize_CEM import imresize
+    cem = CEMnet.CEMnet(CEMnet.Get_CEM_Config(4), upscale_kernel=kernel)
+    rng = np.random.default_rng(300 if kernel is None else 301)
+    f32 = lambda *s: rng.random(s).astype(np.float32).astype(np.float64)  # noqa: E731 (exact in fp32)
+    h, w = 20, 24
+    lr, hr, hr2, gray = f32(h, w, 3), f32(4 * h, 4 * w, 3), f32(4 * h, 4 * w, 3), f32(4 * h, 4 * w)
+    m = int(cem.invalidity_margins_LR)
+    lr_b, hr_b = f32(2, h, w, 3), f32(2, 4 * (h + 4 * m), 4 * (w + 4 * m), 3)
+    d = dict(lr=lr, hr=hr, hr2=hr2, gray=gray, lr_b=lr_b, hr_b=hr_b)
+    d['down'] = imresize(hr, [1 / 4])
+    d['down_zp'] = imresize(hr, [1 / 4], use_zero_padding=True)
+    d['down_gray'] = imresize(gray, [1 / 4])
+    d['up'] = imresize(lr, [4])
+    d['up_zp'] = imresize(lr, [4], use_zero_padding=True)
+    d['up_shape'] = imresize(lr, output_shape=[4 * h, 4 * w])
+    d['dt_up'] = cem.DT_Satisfying_Upscale(lr)
+    d['project'] = cem.Project_2_kernel_subspace(hr)
+    d['enforce'] = cem.Enforce_DT_on_Image_Pair(lr, hr)
+    d['enforce_same'] = cem.Enforce_DT_on_Image_Pair(hr2, hr)
+    d['pad1'] = cem.Pad_LR_Batch(lr_b)
+    d['pad2'] = cem.Pad_LR_Batch(lr_b, num_recursion=2)
+    d['unpad1'] = cem.Unpad_HR_Batch(hr_b)
+    d['unpad2'] = cem.Unpad_HR_Batch(hr_b, num_recursion=2)
+    d['aa_up'] = imresize(None, [4], return_upscale_kernel=True)
+    d['aa_down'] = imresize(None, [1 / 4], return_upscale_kernel=True)
+    np.savez_compressed(os.path.join(HERE, 'cem_np_%s.npz' % name), **d)
+    print('cem_np_%s: %s' % (name, {k: v.shape for k, v in d.items()}))
+
+
 def main():
     install_shims()
     import CEM.CEMnet as CEMnet
+    if sys.argv[1:] == ['cem_np']:  # only the NumPy-helper fixtures (bicubic first: imresize.kernels is sticky)
+        cem_np_fixture(CEMnet, 'bicubic', None)
+        cem_np_fixture(CEMnet, 'learned13', synthetic_learned_kernel())
+        return
     import models.modules.architecture as arch
     torch.set_num_threads(8)
     # --- CEM filter design + CEM forward, bicubic default then a learned (non-bicubic) kernel ---

@@ -202,3 +202,52 @@ def test_gather_plan_equals_direct_packing(latent):
     for p in bp.params:
         assert torch.equal(flat[o:o + p.numel()].view(p.shape), ref[p])
         o += p.numel()
+
+
+@pytest.mark.parametrize('name', ['bicubic', 'learned13'])
+def test_cem_batch_padding_and_kernels_match_reference(name):
+    """Host parts of the CEM NumPy helpers: Pad_LR_Batch / Unpad_HR_Batch (data movement) and
+    imresize(return_upscale_kernel=True), against the reference's outputs; the image resampling itself is a device
+    path (tests/test_gpu_cem_np.py) and refuses to run without a GPU."""
+    from esr_amd import imresize_CEM as I
+    from oracle.recipe import synthetic_learned_kernel
+    d = golden('cem_np_' + name)
+    k = synthetic_learned_kernel() if name == 'learned13' else None
+    cem = C.CEMnet(C.Get_CEM_Config(4), upscale_kernel=k)
+    for key, v in (('pad1', cem.Pad_LR_Batch(d['lr_b'])), ('pad2', cem.Pad_LR_Batch(d['lr_b'], num_recursion=2)),
+                   ('unpad1', cem.Unpad_HR_Batch(d['hr_b'])), ('unpad2', cem.Unpad_HR_Batch(d['hr_b'], 2)),
+                   ('aa_up', I.imresize(None, [4], kernel=k, return_upscale_kernel=True)),
+                   ('aa_down', I.imresize(None, [1 / 4], kernel=k, return_upscale_kernel=True))):
+        assert v.shape == d[key].shape, key
+        np.testing.assert_array_equal(v, d[key], err_msg=key)
+    if not torch.cuda.is_available():
+        with pytest.raises(RuntimeError, match='no CPU path'):
+            I.imresize(d['hr'], [1 / 4], kernel=k)
+        with pytest.raises(RuntimeError, match='no CPU path'):
+            cem.Project_2_kernel_subspace(d['hr'])
+
+
+def test_cem_set_upscale_kernel_equals_fresh_design():
+    from oracle.recipe import synthetic_learned_kernel
+    k = synthetic_learned_kernel()
+    a = C.CEMnet(C.Get_CEM_Config(4)).Set_Upscale_Kernel(k)
+    b = C.CEMnet(C.Get_CEM_Config(4), upscale_kernel=k)
+    for attr in ('ds_kernel', 'inv_hTh', 'invalidity_margins_LR', 'invalidity_margins_HR'):
+        np.testing.assert_array_equal(getattr(a, attr), getattr(b, attr))
+    net = esr_amd.RRDBNet(3, 3, 64, 1, num_latent_channels=0)
+    cem = C.CEMnet(C.Get_CEM_Config(4))
+    model = cem.WrapArchitecture_PyTorch(net, training_patch_size=384)
+    cem.Set_Upscale_Kernel(k)
+    model.Update_Filters(cem)
+    fresh = C.CEMnet(C.Get_CEM_Config(4), upscale_kernel=k).WrapArchitecture_PyTorch(
+        esr_amd.RRDBNet(3, 3, 64, 1, num_latent_channels=0), training_patch_size=384)
+    sd, sf = model.state_dict(), fresh.state_dict()
+    assert list(sd) == list(sf)
+    for key in sd:
+        if 'Filter' in key:
+            np.testing.assert_array_equal(sd[key].numpy(), sf[key].numpy())
+    assert (model.margins_LR, model.margins_HR) == (int(fresh.margins_LR), int(fresh.margins_HR)) != (10, 40)
+    M = int(fresh.margins_HR)
+    assert int(cem.loss_mask.sum()) == (384 - 2 * M) ** 2
+    x = torch.arange(2 * 3 * 5 * 5, dtype=torch.float32).view(2, 3, 5, 5)
+    assert torch.equal(model.LR_padder(x), fresh.LR_padder(x))

@@ -116,3 +116,25 @@ def test_fp32_gradients_have_kink_flips():
         g[dt] = x.grad.double()
     assert normwise_rel(g[torch.float32], g[torch.float64]) > 1e-3      # max-norm: kink flips dominate
     assert l2_rel(g[torch.float32], g[torch.float64]) < 1e-2
+
+
+@pytest.mark.parametrize('name', ['bicubic', 'learned13'])
+def test_cem_numpy_helpers(name):
+    """imresize (edge / zero padding, up / down, HW and HWC), DT_Satisfying_Upscale, Project_2_kernel_subspace,
+    Enforce_DT_on_Image_Pair (LR- and HR-sized sources), Pad_LR_Batch / Unpad_HR_Batch: bit-exact with the
+    reference's outputs (same float64 NumPy/SciPy arithmetic)."""
+    from oracle.recipe import synthetic_learned_kernel
+    d = golden('cem_np_' + name)
+    D = O.cem_design(4, synthetic_learned_kernel() if name == 'learned13' else None)
+    k, m = D['k_up'], D['margins_LR']
+    got = dict(down=O.imresize_np(d['hr'], 1 / 4, k), down_zp=O.imresize_np(d['hr'], 1 / 4, k, True),
+               down_gray=O.imresize_np(d['gray'], 1 / 4, k), up=O.imresize_np(d['lr'], 4, k),
+               up_zp=O.imresize_np(d['lr'], 4, k, True), up_shape=O.imresize_np(d['lr'], 4, k),
+               dt_up=O.dt_satisfying_upscale(d['lr'], D), project=O.project_2_kernel_subspace(d['hr'], D),
+               enforce=O.enforce_dt_on_image_pair(d['lr'], d['hr'], D),
+               enforce_same=O.enforce_dt_on_image_pair(d['hr2'], d['hr'], D),
+               pad1=O.pad_lr_batch(d['lr_b'], m), pad2=O.pad_lr_batch(d['lr_b'], m, 2),
+               unpad1=O.unpad_hr_batch(d['hr_b'], m, 4), unpad2=O.unpad_hr_batch(d['hr_b'], m, 4, 2))
+    for key, v in got.items():
+        assert v.shape == d[key].shape, key
+        np.testing.assert_array_equal(v, d[key], err_msg=key)
