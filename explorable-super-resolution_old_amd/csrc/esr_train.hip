@@ -138,6 +138,166 @@ __global__ __launch_bounds__(256, 1) void wgrad_kernel(WgradParams p) {
     }
 }
 
+// wgrad2: the same GEMM with 12 waves (3 per SIMD) instead of 4, so LDS and MFMA latencies of one wave hide behind
+// the others.  Wave w owns the three taps of tap column tg = w % 3 (dy = 0..2, dx = tg) for one output-channel tile
+// ct and one pixel class q (NCT = 1: four classes; NCT = 2: ct = (w/3) & 1 and two classes), i.e. 3 accumulators;
+// per pixel pair it reads one output-gradient fragment (reused by its 3 taps) and one input fragment per tap.  The
+// next pixel tile's global loads are issued into registers before the current tile is consumed.  The pixel classes
+// are summed through LDS at the end (fixed order).  blockIdx is remapped so that the chunks of one split run on the
+// same XCD and share its L2 for the output-gradient tile.
+constexpr int W2_NT = 768;
+constexpr int W2_IN_F = WT_HY * WT_HX * WT_IP, W2_D_F = WT_TH * WT_TW * WT_DP;
+constexpr int W2_IN_V4 = WT_HY * WT_HX * 8, W2_D_V4 = WT_TH * WT_TW * 16;
+constexpr int W2_IN_PT = (W2_IN_V4 + W2_NT - 1) / W2_NT, W2_D_PT = (W2_D_V4 + W2_NT - 1) / W2_NT;
+
+template <int NCT>
+__global__ __launch_bounds__(W2_NT, 1) void wgrad2_kernel(WgradParams p) {
+    constexpr int NQ = 4 / NCT;  // pixel classes
+    __shared__ __attribute__((aligned(16))) float smem[W2_IN_F + W2_D_F];
+    float *s_in = smem, *s_d = smem + W2_IN_F;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hl = lane >> 5, ml = lane & 31;
+    const int tg = wave % 3, r4 = wave / 3;
+    const int ct = NCT == 2 ? (r4 & 1) : 0, q = NCT == 2 ? (r4 >> 1) : r4;
+    const int nchunks = p.cin_pad / 32;
+    const int total = nchunks * p.splits;
+    // XCD-aware logical id: the hardware dispatches blockIdx round-robin over the 8 XCDs
+    const int per_xcd = (total + 7) / 8;
+    const int L = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+    if (L >= total) return;
+    const int chunk = L % nchunks, split = L / nchunks;
+    const int ntiles = p.B * p.tiles_y * p.tiles_x;
+    const int t_begin = (int)((long long)ntiles * split / p.splits);
+    const int t_end = (int)((long long)ntiles * (split + 1) / p.splits);
+    const int c0 = chunk * 32;
+    const int kc = min(32, p.cin - c0);
+    const int Hi = p.up2 ? p.H / 2 : p.H, Wi = p.up2 ? p.W / 2 : p.W;
+    const bool vec_d = ((p.dout_cp | p.dout_coff) & 3) == 0;  // 16-B aligned output-gradient pixels
+
+    f32x16 acc[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    float bsum = 0.f;
+
+    f32x4 rin[W2_IN_PT], rd[W2_D_PT];
+    auto load_tile = [&](int t) {
+        const int tx = t % p.tiles_x, ty = (t / p.tiles_x) % p.tiles_y, b = t / (p.tiles_x * p.tiles_y);
+        const int y0 = ty * WT_TH, x0 = tx * WT_TW;
+#pragma unroll
+        for (int k = 0; k < W2_IN_PT; ++k) {
+            const int idx = tid + k * W2_NT;
+            const int px = idx >> 3, c4 = idx & 7;
+            const int hy = px / WT_HX, hx = px - hy * WT_HX;
+            const int Y = y0 + hy - 1, X = x0 + hx - 1;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (idx < W2_IN_V4 && Y >= 0 && Y < p.H && X >= 0 && X < p.W && c4 * 4 < kc) {
+                const int sy = p.up2 ? Y / 2 : Y, sx = p.up2 ? X / 2 : X;
+                v = *reinterpret_cast<const f32x4 *>(
+                    p.in + (((long long)b * (Hi + 2) + sy + 1) * (Wi + 2) + sx + 1) * p.in_cp + c0 + c4 * 4);
+            }
+            rin[k] = v;
+        }
+#pragma unroll
+        for (int k = 0; k < W2_D_PT; ++k) {
+            const int idx = tid + k * W2_NT;
+            const int px = idx >> 4, c4 = idx & 15;
+            const int y = y0 + (px >> 5), x = x0 + (px & 31);
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (idx < W2_D_V4 && c4 < 8 * NCT && y < p.H && x < p.W && c4 * 4 < p.cout) {
+                const float *src = p.dout + (((long long)b * (p.H + 2) + y + 1) * (p.W + 2) + x + 1) * p.dout_cp +
+                                   p.dout_coff + c4 * 4;
+                if (vec_d && c4 * 4 + 4 <= p.cout) {
+                    v = *reinterpret_cast<const f32x4 *>(src);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = (c4 * 4 + e < p.cout) ? src[e] : 0.f;
+                }
+            }
+            rd[k] = v;
+        }
+    };
+    auto store_tile = [&]() {
+#pragma unroll
+        for (int k = 0; k < W2_IN_PT; ++k) {
+            const int idx = tid + k * W2_NT;
+            if (idx < W2_IN_V4) *reinterpret_cast<f32x4 *>(s_in + (idx >> 3) * WT_IP + (idx & 7) * 4) = rin[k];
+        }
+#pragma unroll
+        for (int k = 0; k < W2_D_PT; ++k) {
+            const int idx = tid + k * W2_NT;
+            if (idx < W2_D_V4 && (idx & 15) < 8 * NCT)
+                *reinterpret_cast<f32x4 *>(s_d + (idx >> 4) * WT_DP + (idx & 15) * 4) = rd[k];
+        }
+    };
+
+    if (t_begin < t_end) load_tile(t_begin);
+    for (int t = t_begin; t < t_end; ++t) {
+        __syncthreads();
+        store_tile();
+        __syncthreads();
+        if (t + 1 < t_end) load_tile(t + 1);
+        if (chunk == 0 && tid < 256)
+            for (int px = tid >> 6; px < WT_TH * WT_TW; px += 4) bsum += s_d[px * WT_DP + (tid & 63)];
+        // pixel pairs s = NQ*k + q; lane half hl takes pixel 2s + hl
+#pragma unroll 4
+        for (int k = 0; k < WT_TH * WT_TW / (2 * NQ); ++k) {
+            const int px = 2 * (NQ * k + q) + hl;
+            const int py = px >> 5, pxx = px & 31;
+            const float bb = s_d[px * WT_DP + ct * 32 + ml];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const float a = s_in[((py + j) * WT_HX + pxx + tg) * WT_IP + ml];
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bb, acc[j], 0, 0, 0);
+            }
+        }
+    }
+    // sum the pixel classes into class 0 (fixed order 1, 2, ...), through LDS
+    constexpr int PER_WAVE = 3 * 16 * 64;
+    static_assert(3 * NCT * PER_WAVE <= W2_IN_F + W2_D_F, "class reduction does not fit in LDS");
+    const int slot = tg * NCT + ct;
+    for (int r = 1; r < NQ; ++r) {
+        __syncthreads();
+        if (q == r) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) smem[slot * PER_WAVE + (j * 16 + e) * 64 + lane] = acc[j][e];
+        }
+        __syncthreads();
+        if (q == 0) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) acc[j][e] += smem[slot * PER_WAVE + (j * 16 + e) * 64 + lane];
+        }
+    }
+    float *part = p.partial + (long long)split * (9LL * p.cin_pad * p.cout_pad + p.cout_pad);
+    if (q == 0) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int tap = 3 * j + tg;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int ci = c0 + (e & 3) + 8 * (e >> 2) + 4 * hl;
+                part[((long long)tap * p.cin_pad + ci) * p.cout_pad + ct * 32 + ml] = acc[j][e];
+            }
+        }
+    }
+    if (chunk == 0) {
+        __syncthreads();
+        if (tid < 256) smem[tid] = bsum;
+        __syncthreads();
+        if (tid < p.cout_pad) {
+            float v = 0.f;
+            if (tid < 64) v = smem[tid] + smem[64 + tid] + smem[128 + tid] + smem[192 + tid];
+            part[9LL * p.cin_pad * p.cout_pad + tid] = v;
+        }
+    }
+}
+
+int g_wgrad_kernel = 1;  // 0 = wgrad_kernel (4 waves), 1 = wgrad2_kernel (12 waves)
+
 __global__ void wgrad_reduce_kernel(const float *partial, int splits, long long n, float scale, float *out) {
     const long long i = (long long)blockIdx.x * NT + threadIdx.x;
     if (i >= n) return;
@@ -327,8 +487,24 @@ extern "C" int esr_conv3x3_wgrad(const float *in, int32_t in_cp, int32_t cin, in
     p.tiles_x = (W + WT_TW - 1) / WT_TW; p.tiles_y = (H + WT_TH - 1) / WT_TH;
     p.splits = splits; p.cin_pad = (cin + 31) / 32 * 32;
     p.partial = partial;
-    hipLaunchKernelGGL(wgrad_kernel, dim3((unsigned)(p.cin_pad / 32 * splits)), dim3(256), 0, (hipStream_t)stream, p);
+    const unsigned total = (unsigned)(p.cin_pad / 32 * splits);
+    if (g_wgrad_kernel == 1) {
+        const unsigned grid = 8 * ((total + 7) / 8);  // whole XCD rounds; the surplus workgroups exit at once
+        if (p.cout_pad == 64)
+            hipLaunchKernelGGL(wgrad2_kernel<2>, dim3(grid), dim3(W2_NT), 0, (hipStream_t)stream, p);
+        else
+            hipLaunchKernelGGL(wgrad2_kernel<1>, dim3(grid), dim3(W2_NT), 0, (hipStream_t)stream, p);
+    } else {
+        hipLaunchKernelGGL(wgrad_kernel, dim3(total), dim3(256), 0, (hipStream_t)stream, p);
+    }
     return launched();
+}
+
+extern "C" int esr_wgrad_set_kernel(int32_t variant) {
+    if (variant < 0 || variant > 1) return ESR_EINVAL;
+    const int prev = g_wgrad_kernel;
+    g_wgrad_kernel = variant;
+    return prev;
 }
 
 extern "C" int esr_wgrad_reduce(const float *partial, int32_t splits, int64_t n, float scale, float *out,

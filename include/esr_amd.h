@@ -147,6 +147,10 @@ int esr_conv3x3_wgrad(const float *in, int32_t in_cp, int32_t cin, int32_t up2, 
                       esr_stream_t stream);
 /* out[i] = scale · Σ_s partial[s·n + i], fixed summation order. */
 int esr_wgrad_reduce(const float *partial, int32_t splits, int64_t n, float scale, float *out, esr_stream_t stream);
+/* Kernel selection for esr_conv3x3_wgrad (process-wide, for A/B tests and benchmarks): 1 (default) = 12-wave
+ * kernel (three waves per SIMD, next tile prefetched into registers, XCD-grouped chunks), 0 = the 4-wave kernel.
+ * Both are deterministic; they sum the pixels in different orders.  Returns the previous setting, or ESR_EINVAL. */
+int esr_wgrad_set_kernel(int32_t variant);
 /* LeakyReLU(0.2) backward from the saved output y: d *= (y > 0 ? 1 : 0.2) on a C-channel slice. */
 int esr_lrelu_bwd(float *d, int32_t d_cp, int32_t d_coff, const float *y, int32_t y_cp, int32_t y_coff, int32_t C,
                   int32_t B, int32_t H, int32_t W, esr_stream_t stream);

@@ -170,3 +170,50 @@ def test_input_and_parameter_gradients_together_vs_oracle(gpu_device, mode):
             k = 'param:' + n[len('generated_image_model.'):]
             ok, msg = grad_parity(p.grad.cpu(), exact[k], base[k])
             assert ok, (n, msg)
+
+
+@pytest.mark.parametrize('variant', [0, 1])
+@pytest.mark.parametrize('cin,in_cp,cout,dout_cp,dout_coff,up2,B,H,W,splits', [
+    (64, 64, 32, 192, 64, 0, 2, 20, 40, 7),      # RDB growth conv: dout a channel slice of a concat buffer
+    (72, 80, 64, 64, 0, 0, 3, 13, 33, 5),        # latent-slot input, cout 64, ragged tiles
+    (64, 64, 64, 72, 8, 1, 2, 24, 64, 16),       # upconv: nearest x2 input read on the fly
+    (64, 64, 3, 8, 0, 0, 1, 17, 35, 3),          # HR_conv1: cout 3 (scalar output-gradient loads)
+    (200, 200, 32, 32, 0, 0, 2, 8, 32, 1),       # partial last input chunk (cin_pad 224), one split
+    (64, 64, 32, 36, 2, 0, 2, 9, 31, 4),         # unaligned output-gradient pitch / offset
+])
+def test_weight_gradient_kernels_vs_float64(gpu_device, variant, cin, in_cp, cout, dout_cp, dout_coff, up2, B, H, W,
+                                            splits):
+    """esr_conv3x3_wgrad (both kernels) + esr_wgrad_reduce against torch.nn.grad.conv2d_weight in float64."""
+    import ctypes
+    from esr_amd import _lib
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(cin * 7 + cout)
+    Hi, Wi = (H // 2, W // 2) if up2 else (H, W)
+    x = torch.randn(B, cin, Hi, Wi, generator=g)
+    dy = torch.randn(B, cout, H, W, generator=g)
+    xin = torch.zeros(B, Hi + 2, Wi + 2, in_cp)
+    xin[:, 1:-1, 1:-1, :cin] = x.permute(0, 2, 3, 1)
+    dbuf = torch.randn(B, H + 2, W + 2, dout_cp, generator=g)  # junk around the slice must be ignored
+    dbuf[:, 1:-1, 1:-1, dout_coff:dout_coff + cout] = dy.permute(0, 2, 3, 1)
+    cin_pad, cout_pad = 32 * ((cin + 31) // 32), 64 if cout > 32 else 32
+    n = 9 * cin_pad * cout_pad + cout_pad
+    xin, dbuf = xin.to(gpu_device), dbuf.to(gpu_device)
+    partial = torch.full((splits * n,), float('nan'), device=gpu_device)
+    out = torch.empty(n, device=gpu_device)
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    prev = lib.esr_wgrad_set_kernel(variant)
+    try:
+        _lib.check(lib.esr_conv3x3_wgrad(xin.data_ptr(), in_cp, cin, up2, dbuf.data_ptr(), dout_cp, dout_coff, cout,
+                                         B, H, W, splits, partial.data_ptr(), st), 'wgrad')
+        _lib.check(lib.esr_wgrad_reduce(partial.data_ptr(), splits, n, 1.0, out.data_ptr(), st), 'reduce')
+        torch.cuda.synchronize()
+    finally:
+        lib.esr_wgrad_set_kernel(prev)
+    out = out.cpu().double()
+    xr = x.double()
+    if up2:
+        xr = xr.repeat_interleave(2, 2).repeat_interleave(2, 3)
+    ref_w = torch.nn.grad.conv2d_weight(xr, (cout, cin, 3, 3), dy.double(), padding=1)  # [co][ci][ky][kx]
+    got_w = out[:9 * cin_pad * cout_pad].view(3, 3, cin_pad, cout_pad)[:, :, :cin, :cout].permute(3, 2, 0, 1)
+    assert normwise_rel(got_w, ref_w) < 1e-5
+    assert normwise_rel(out[9 * cin_pad * cout_pad:][:cout], dy.double().sum((0, 2, 3))) < 1e-5
