@@ -176,10 +176,13 @@ __global__ __launch_bounds__(NTHREADS, 1) void conv_fwd_kernel(ConvParams p) {
                 if (x >= p.W) continue;
                 const int ox = o.out_sx * x + o.out_ox;
                 float v = acc[mt][nt][r] + bn;
-                if (o.lrelu) v = v > 0.f ? v : 0.2f * v;
+                if (o.lrelu == 1) v = v > 0.f ? v : 0.2f * v;
                 const long long pix = ((long long)b * (o.out_h + 2) + oy + 1) * orow + ox + 1;
                 if (o.r1) v = o.s1 * v + o.r1[pix * o.r1_cp + o.r1_coff + n];
-                if (o.r2) v = o.s2 * v + o.r2[pix * o.r2_cp + o.r2_coff + n];
+                if (o.lrelu == 2)
+                    v = o.r2[pix * o.r2_cp + o.r2_coff + n] > 0.f ? v : 0.2f * v;
+                else if (o.r2)
+                    v = o.s2 * v + o.r2[pix * o.r2_cp + o.r2_coff + n];
                 if (o.out_planar)
                     o.out[(((long long)b * p.cout + n) * o.out_h + oy) * o.out_w + ox] = v;
                 else
@@ -195,6 +198,7 @@ int launch_conv(const float *in, int B, int H, int W, int in_cp, int cin, const 
     if (!in || !w || !bias || !o || !o->out) return ESR_EINVAL;
     if (B <= 0 || H <= 0 || W <= 0 || cin <= 0 || cout <= 0 || cout > 64) return ESR_EINVAL;
     if (cin % 8 || in_cp % 4 || in_cp < cin) return ESR_EINVAL;
+    if (o->lrelu < 0 || o->lrelu > 2 || (o->lrelu == 2 && !o->r2)) return ESR_EINVAL;
     if (!o->out_planar && o->out_coff + cout > o->out_cp) return ESR_EINVAL;
     if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(w)) & 15) return ESR_EINVAL;
     ConvParams p;

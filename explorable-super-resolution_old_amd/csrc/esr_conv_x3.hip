@@ -849,7 +849,7 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
               hipStream_t stream) {
     if (!in || !w || !bias || !o || !o->out) return ESR_EINVAL;
     if (B <= 0 || H <= 0 || W <= 0 || cin <= 0 || cout <= 0 || cout > 64 || !(w_scale > 0.f)) return ESR_EINVAL;
-    if (cin % 8 || in_cp % 8 || in_cp < cin) return ESR_EINVAL;
+    if (cin % 8 || in_cp % 8 || in_cp < cin || o->lrelu < 0 || o->lrelu > 1) return ESR_EINVAL;
     if (!o->out_planar && (cout % 8 || o->out_cp % 8 || o->out_coff % 8 || o->out_coff + cout > o->out_cp))
         return ESR_EINVAL;
     if ((o->r1 && (o->r1_cp % 8 || o->r1_coff % 8)) || (o->r2 && (o->r2_cp % 8 || o->r2_coff % 8)) ||

@@ -5,8 +5,10 @@ step: `fake_H = netG(model_input)` then `l_g_total.backward()`, SRRaGAN_model.py
 CEM is one torch.autograd.Function whose backward runs libesr_amd kernels (exact fp32):
 
   CEM (train mode)      d gen = g - Down^T Inv^T Up^T g        esr_cem_adjoint ×3 (exact replicate-pad adjoints)
-  conv data gradient    esr_conv3x3_fwd with rot180, in/out-swapped packed weights, in 64-channel output slices,
-                        accumulating into a concat-gradient buffer (the adjoint of the dense concatenations)
+  conv data gradient    esr_conv3x3_fwd with rot180, in/out-swapped packed weights; inside an RDB one conv per
+                        concat slice over the stacked output gradients of every conv that reads it (fused K),
+                        LeakyReLU backward in its epilogue (the adjoint of the dense concatenations); elsewhere in
+                        64-channel output slices
   conv weight gradient  esr_conv3x3_wgrad (split-K over pixel tiles) + esr_wgrad_reduce (deterministic)
   LeakyReLU / residuals esr_lrelu_bwd, esr_axpby;  nearest ×2 adjoint: esr_sum2x2
 The reference's residual scales (0.2 in RDB and RRDB, block.py:235, 270) are folded into the packed backward weights
@@ -46,9 +48,11 @@ class TrainWorkspace:
         self.lr = _z(dev, B, 3, H, W)
         self.overflow = torch.zeros(1, device=dev, dtype=torch.int32)
         # backward
-        self.D = [_z(dev, B, H + 2, W + 2, self.cp) for _ in range(2)]
+        # concat-gradient buffers: [Z | x | d_0 .. d_3 | d_4] with d_i = dL/d(conv i output) (after the LeakyReLU
+        # backward) and d_4 = dL/d(RDB output), contiguous so that every slice's data gradient is ONE conv
+        self.dcp = zc + 256
+        self.D = [_z(dev, B, H + 2, W + 2, self.dcp) for _ in range(2)]
         self.GA = _z(dev, B, H + 2, W + 2, 64)
-        self.G3 = _z(dev, B, H + 2, W + 2, 64)
         self.dU0 = _z(dev, B, H + 2, W + 2, 64)
         self.dU1 = _z(dev, B, 2 * H + 2, 2 * W + 2, 64)
         self.dUp1 = _z(dev, B, 2 * H + 2, 2 * W + 2, 64)
@@ -92,6 +96,7 @@ class _BwdConv:
             wt[rows >= 0] = wf[rows[rows >= 0]]
             return n0, nw, plan.reg(E.pack_conv_weight(plan.scaled(wt, scale), kmap, 32 if nw <= 32 else 64))
 
+        self.wf = wf
         self.slices = []  # (first buffer channel, width, packed weights)
         n0 = dgrad_from  # input-gradient channels below this (the latent Z slot) are not needed
         while n0 < self.cin_buf:
@@ -126,12 +131,14 @@ class _BwdPacked:
         plan = self.plan = E.GatherPlan(net.parameters(), scales=(1.0, 0.2))
         first_map = ([0, 1, 2] + [-1] * 5 + [3, 4, 5] + [-1] * 5) if latent else ([0, 1, 2] + [-1] * 5)
         self.first = _BwdConv(plan, m[0], first_map, dgrad_from=len(first_map), in_width=len(first_map))
-        self.rdb = []
+        self.rdb, self.rdb_fused = [], []
         for k in range(net.nb):
             rr = m[1].sub[k]
             for rdb in (rr.RDB1, rr.RDB2, rr.RDB3):
-                self.rdb.append([_BwdConv(plan, rdb.convs[i][0], lr_map(64 + 32 * i), 0.2 if i == 4 else 1.0,
-                                          dgrad_from=zc, in_width=zc) for i in range(5)])
+                cv = [_BwdConv(plan, rdb.convs[i][0], lr_map(64 + 32 * i), 0.2 if i == 4 else 1.0,
+                               dgrad_from=zc + 64 + 32 * i) for i in range(5)]  # data gradient: fused below
+                self.rdb.append(cv)
+                self.rdb_fused.append(_fused_rdb_weights(plan, cv, zc))
         self.lr_conv = _BwdConv(plan, m[1].sub[net.nb], lr_map(64), dgrad_from=zc, in_width=zc)
         self.up = [_BwdConv(plan, m[j][1], list(range(64))) for j in (2, 3)]
         self.hr0 = _BwdConv(plan, m[4], lr_map(64), dgrad_from=zc, in_width=zc)
@@ -143,8 +150,10 @@ class _BwdPacked:
         for c in convs:
             c.slices = [(n0, nw, views[id(t)]) for n0, nw, t in c.slices]
             c.in_slices = [(n0, nw, views[id(t)]) for n0, nw, t in c.in_slices]
+            c.wf = None
             c.wg_off = off
             off += c.wg_n
+        self.rdb_fused = [{k: views[id(t)] for k, t in f.items()} for f in self.rdb_fused]
         self.zero_bias = torch.zeros(64, device=dev)
         self.dw = torch.empty(off, device=dev, dtype=torch.float32)  # every conv's reduced wgrad, packed layout
         by_param = {}
@@ -154,6 +163,31 @@ class _BwdPacked:
         self.params = plan.params
         assert all(id(p) in by_param for p in self.params), 'generator parameter without a backward rule'
         self.gidx = torch.cat([by_param[id(p)] for p in self.params]).to(dev)
+
+
+def _fused_rdb_weights(plan, convs, zc):
+    """Data-gradient weights of one RDB in the fused form: the gradient of concat slice t (buffer channels
+    [t0, t0+nw)) is  sum over the convs i that read t of conv_i^T(d_i),  one conv over the contiguous d_i channels
+    [d_lo, zc+256) of the concat-gradient buffer with the rot180/transposed weights of those convs stacked along K
+    (conv 4 scaled by its 0.2 residual factor).  Targets: 'm1'..'m4' = x_1..x_4 (32 channels, from d_m..d_4),
+    'x' = the block input (64 channels, from d_0..d_4), 'z' = the latent slot (zc channels, from d_0..d_4)."""
+    def slice_w(t0, nw, i_lo):
+        blocks = []
+        for i in range(i_lo, 5):
+            c = convs[i]
+            blk = torch.zeros(nw, c.cout, 3, 3, dtype=c.wf.dtype)
+            for r in range(nw):
+                t = t0 + r
+                if t < len(c.cmap) and c.cmap[t] >= 0:
+                    blk[r] = c.wf[c.cmap[t]]
+            blocks.append(plan.scaled(blk, 0.2) if i == 4 else blk)
+        wt = torch.cat(blocks, 1)
+        return plan.reg(E.pack_conv_weight(wt, list(range(wt.shape[1])), 32 if nw <= 32 else 64))
+    out = {'m%d' % m: slice_w(zc + 64 + 32 * (m - 1), 32, m) for m in (1, 2, 3, 4)}
+    out['x'] = slice_w(zc, 64, 0)
+    if zc:
+        out['z'] = slice_w(0, zc, 0)
+    return out
 
 
 def _bwd_packed(net, latent):
@@ -198,6 +232,21 @@ class _Runner:
                                                 self.bp.zero_bias.data_ptr(), nw, ctypes.byref(o), self.stream),
                        'dgrad')
 
+    def dgrad_fused(self, wpk, src, src_cp, src_coff, cin_k, h, w, dst, dst_cp, dst_coff, nw, res=None, mask=None):
+        """dst[:, dst_coff:+nw] = conv(src channels [src_coff, +cin_k), fused weights) (+ res) (then LeakyReLU
+        backward through the saved activation `mask` = (buf, cp, coff)); res = (buf, cp, coff) or 'acc'."""
+        r1, r1_cp, r1_coff = (None, 0, 0)
+        if res == 'acc':
+            r1, r1_cp, r1_coff = dst, dst_cp, dst_coff
+        elif res is not None:
+            r1, r1_cp, r1_coff = res
+        r2, r2_cp, r2_coff = mask if mask is not None else (None, 0, 0)
+        o = E._conv_out(dst, dst_cp, dst_coff, h, w, 2 if mask is not None else 0, r1=r1, r1_cp=r1_cp,
+                        r1_coff=r1_coff, s1=1.0, r2=r2, r2_cp=r2_cp, r2_coff=r2_coff)
+        _lib.check(self.lib.esr_conv3x3_fwd(src.data_ptr() + 4 * src_coff, self.B, h, w, src_cp, cin_k, wpk.data_ptr(),
+                                            self.bp.zero_bias.data_ptr(), nw, ctypes.byref(o), self.stream),
+                   'dgrad_fused')
+
     def dgrad_in(self, bc, src, src_cp, src_coff, cin_k, h, w, dst, dst_cp):
         """Generator-input gradient: dst[:, 0:nw] += conv(src slice, rot180 W^T) restricted to the input channels
         below the feature channels (latent Z slot; conv_first's [Z | LR] input)."""
@@ -234,20 +283,21 @@ class _Runner:
                                       self.stream), 'axpby')
 
 
-def _rdb_backward(R, P, dout, dcat, convs, zc, cp, H, W):
+def _rdb_backward(R, P, dcat, convs, fused, zc, cp, H, W, dx):
     """One ResidualDenseBlock_5C (block.py:230-235): h = 0.2·conv4(cat) + x, cat = [x, x1..x4], x_{i+1} =
-    lrelu(conv_i(cat_{<=i})).  dout = (buffer, pitch, offset) of dL/dh.  On return dcat[zc:zc+64) = dL/dx."""
-    dbuf, dcp, dcoff = dout
-    # conv4 (0.2 folded into its packed dgrad weights and its wgrad scale); the x slice also receives dL/dh
-    R.wgrad(convs[4], P, cp, zc + 192, 0, dbuf, dcp, dcoff, H, W, scale=0.2)
-    R.dgrad_in(convs[4], dbuf, dcp, dcoff, 64, H, W, R.ws.dZl, 8)
-    R.dgrad(convs[4], dbuf, dcp, dcoff, 64, H, W, dcat, cp, 0, accumulate=False, res=(dbuf, dcp, dcoff))
-    for i in (3, 2, 1, 0):
-        s = zc + 64 + 32 * i
-        R.lrelu(dcat, cp, s, P, cp, s, 32, H, W)
-        R.wgrad(convs[i], P, cp, s, 0, dcat, cp, s, H, W)
-        R.dgrad_in(convs[i], dcat, cp, s, 32, H, W, R.ws.dZl, 8)
-        R.dgrad(convs[i], dcat, cp, s, 32, H, W, dcat, cp, 0, accumulate=True)
+    lrelu(conv_i(cat_{<=i})).  On entry dcat[zc+192 : zc+256) = d_4 = dL/dh.  For m = 4..1 one fused conv computes
+    dL/dx_m from d_m..d_4 and its epilogue applies the LeakyReLU backward, giving d_{m-1} in place; then one conv gives
+    dL/dx (+ d_4 through the residual) into dx = (buffer, pitch, offset)."""
+    dcp = R.ws.dcp
+    d4 = zc + 192
+    R.wgrad(convs[4], P, cp, zc + 192, 0, dcat, dcp, d4, H, W, scale=0.2)
+    for m in (4, 3, 2, 1):
+        s_in, t = zc + 64 + 32 * m, zc + 64 + 32 * (m - 1)
+        R.dgrad_fused(fused['m%d' % m], dcat, dcp, s_in, zc + 256 - s_in, H, W, dcat, dcp, t, 32, mask=(P, cp, t))
+        R.wgrad(convs[m - 1], P, cp, t, 0, dcat, dcp, t, H, W)
+    if R.need_input and zc:
+        R.dgrad_fused(fused['z'], dcat, dcp, zc + 64, 192, H, W, R.ws.dZl, 8, 0, zc, res='acc')
+    R.dgrad_fused(fused['x'], dcat, dcp, zc + 64, 192, H, W, dx[0], dx[1], dx[2], 64, res=(dcat, dcp, d4))
 
 
 def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_input=False):
@@ -319,12 +369,12 @@ def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_in
     R.dgrad(bp.lr_conv, ws.dU0, 64, 0, 64, H, W, ws.GA, 64, zc, accumulate=False)
     # RRDBs, last to first: o = 0.2·RDB3(RDB2(RDB1(x))) + x
     D0, D1 = ws.D
+    dcp, d4 = ws.dcp, zc + 192
     for k in reversed(range(net.nb)):
-        R.axpby(ws.G3, 64, 0, 0.2, ws.GA, 64, 0, C=64, h=H, w=W)
-        _rdb_backward(R, Q[3 * k + 2], (ws.G3, 64, 0), D0, bp.rdb[3 * k + 2], zc, cp, H, W)
-        _rdb_backward(R, Q[3 * k + 1], (D0, cp, zc), D1, bp.rdb[3 * k + 1], zc, cp, H, W)
-        _rdb_backward(R, Q[3 * k], (D1, cp, zc), D0, bp.rdb[3 * k], zc, cp, H, W)
-        R.axpby(ws.GA, 64, 0, 1.0, ws.GA, 64, 0, 1.0, D0, cp, zc, C=64, h=H, w=W)
+        R.axpby(D0, dcp, d4, 0.2, ws.GA, 64, 0, C=64, h=H, w=W)
+        for j, (dc, dn) in zip((2, 1, 0), ((D0, D1), (D1, D0), (D0, D1))):
+            _rdb_backward(R, Q[3 * k + j], dc, bp.rdb[3 * k + j], bp.rdb_fused[3 * k + j], zc, cp, H, W, (dn, dcp, d4))
+        R.axpby(ws.GA, 64, 0, 1.0, ws.GA, 64, 0, 1.0, D1, dcp, d4, C=64, h=H, w=W)
     # conv_first: dL/dfea = trunk gradient + LR_conv skip
     R.axpby(ws.GA, 64, 0, 1.0, ws.GA, 64, 0, 1.0, ws.dU0, 64, 0, C=64, h=H, w=W)
     R.wgrad(bp.first, ws.first, ws.first_cp, ws.first_cp, 0, ws.GA, 64, 0, H, W)

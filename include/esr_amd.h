@@ -37,9 +37,11 @@ enum esr_status {
  * chunk j is input channel 32*j + c (zero where >= cin).  Bias: fp32 [cout]. */
 
 /* Output/epilogue descriptor of a convolution.
- *   v = acc + bias[n]; if (lrelu) v = v > 0 ? v : 0.2*v        (conv_block CNA + act, block.py:10-23,141-146)
+ *   v = acc + bias[n]; if (lrelu == 1) v = v > 0 ? v : 0.2*v   (conv_block CNA + act, block.py:10-23,141-146)
  *   if (r1) v = s1*v + r1[pixel, r1_coff + n]                  (RDB / trunk residuals, block.py:96,235,270)
- *   if (r2) v = s2*v + r2[pixel, r2_coff + n]
+ *   if (lrelu == 2) v = r2[pixel, r2_coff + n] > 0 ? v : 0.2*v (LeakyReLU backward through the saved activation r2;
+ *                                                               exact-fp32 convs only, r2 required)
+ *   else if (r2) v = s2*v + r2[pixel, r2_coff + n]
  *   out[pixel, out_coff + n] = v   (and out2 likewise when out2 != NULL)
  * Output pixel of input-grid position (y, x) is (out_sy*y + out_oy, out_sx*x + out_ox) in the out grid (out_h × out_w,
  * padded NHWC), which is how the four polyphase phases of the nearest-×2 upconv scatter into the 2× grid.

@@ -177,18 +177,23 @@ def test_gather_plan_equals_direct_packing(latent):
     pk = engine._packed(net, latent)
     assert torch.equal(pk.rdb[1][3].f32, engine.pack_conv_weight(conv.weight, lr_map(64 + 96), 32))
     bp = T._bwd_packed(net, latent)
-    c4 = net.model[1].sub[0].RDB3.convs[4][0]
-    bc = bp.rdb[2][4]
-    wf = c4.weight.detach().flip(2, 3).transpose(0, 1)
-    n0, nw, wpk = bc.slices[-1]
-    cmap = lr_map(64 + 128)
-    wt = torch.zeros(nw, 64, 3, 3)
-    for o in range(nw):
-        if cmap[n0 + o] >= 0:
-            wt[o] = wf[cmap[n0 + o]]
-    assert bc.slices[0][0] == zc
-    assert torch.allclose(wpk, engine.pack_conv_weight(wt * 0.2, list(range(64)), 32 if nw <= 32 else 64), rtol=0,
-                          atol=0)
+    # fused RDB data-gradient weights: slice t's rows of rot180/transposed W_i, stacked over the convs i that read t
+    rdb = net.model[1].sub[0].RDB3
+    wfs = [rdb.convs[i][0].weight.detach().flip(2, 3).transpose(0, 1) for i in range(5)]
+    for key, t0, nw, i_lo in (('x', zc, 64, 0), ('m3', zc + 128, 32, 3), ('m1', zc + 64, 32, 1)):
+        blocks = []
+        for i in range(i_lo, 5):
+            cmap = lr_map(64 + 32 * i)
+            blk = torch.zeros(nw, wfs[i].shape[1], 3, 3)
+            for o in range(nw):
+                if t0 + o < len(cmap) and cmap[t0 + o] >= 0:
+                    blk[o] = wfs[i][cmap[t0 + o]]
+            blocks.append(blk * 0.2 if i == 4 else blk)
+        wt = torch.cat(blocks, 1)
+        assert wt.shape[1] == 64 + 32 * (4 - i_lo)
+        want = engine.pack_conv_weight(wt, list(range(wt.shape[1])), 32 if nw <= 32 else 64)
+        assert torch.equal(bp.rdb_fused[2][key], want), key
+    assert bp.rdb[2][4].slices == [] and ('z' in bp.rdb_fused[2]) == latent
     # wgrad buffer -> reference-layout gradient
     ref = {p: torch.randn_like(p) for p in net.parameters()}
     for b in [bp.first, bp.lr_conv, bp.hr0, bp.hr1] + bp.up + [c for r in bp.rdb for c in r]:
