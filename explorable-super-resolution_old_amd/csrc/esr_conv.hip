@@ -1,9 +1,9 @@
 // esr_conv.hip — 3×3 convolution (and polyphase nearest-×2 upconv) for gfx950, fp32 via f32-input MFMA.
 //
 // Implicit GEMM: M = output pixels, N = output channels (32 or 64), K = taps × input channels.
-// Workgroup = 256 threads (4 waves, one per SIMD), output tile TH×TW = 8 rows × 32 columns of one image, all N.
-// Each wave owns two tile rows (two 32-pixel M-tiles) × NT 32-channel N-tiles: 2·NT accumulators of
-// v_mfma_f32_32x32x2_f32 (16 f32 per lane each).
+// Workgroup = 256 threads (4 waves, one per SIMD), output tile TH×TW = 4·MT rows × 32 columns of one image, all N.
+// Each wave owns MT tile rows (32-pixel M-tiles) × NT 32-channel N-tiles: MT·NT accumulators of
+// v_mfma_f32_32x32x2_f32 (16 f32 per lane each).  MT = 2 by default; MT = 1 for small grids (see launch_conv).
 // K loop: input channels in chunks of ≤32.  Per chunk the (TH+2)×(TW+2) halo tile of the chunk's channels and the
 // chunk's packed weights [taps][N][32] are staged in LDS (pixel/row pitch 36 floats: 16-byte slots of the 32 lanes of a
 // ds_read_b128 group land on 16 distinct slots); the next chunk is prefetched into registers while MFMAs run.
@@ -20,13 +20,12 @@ namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int TH = 8, TW = 32;
-constexpr int HY = TH + 2, HX = TW + 2;
+// Tile: 4 waves × MT rows × 32 columns (MT = 2: 8×32, the default; MT = 1: 4×32 for grids that would otherwise
+// leave the last round of workgroups mostly idle, and small enough in LDS for two workgroups per CU when N = 32).
+constexpr int TW = 32, HX = TW + 2;
 constexpr int KC = 32;
 constexpr int PS = 36;  // LDS pitch (floats) of a staged pixel / weight row
 constexpr int NTHREADS = 256;
-constexpr int IN_F4 = HY * HX * (KC / 4);                       // float4s of a full input chunk
-constexpr int IN_ITERS = (IN_F4 + NTHREADS - 1) / NTHREADS;     // 11
 
 struct ConvParams {
     const float *in;
@@ -39,8 +38,11 @@ struct ConvParams {
     esr_conv_out o;
 };
 
-template <int NT, int TS>
-__global__ __launch_bounds__(NTHREADS, 1) void conv_fwd_kernel(ConvParams p) {
+template <int NT, int TS, int MT>
+__global__ __launch_bounds__(NTHREADS, (MT == 1 && NT == 1) ? 2 : 1) void conv_fwd_kernel(ConvParams p) {
+    constexpr int TH = 4 * MT, HY = TH + 2;
+    constexpr int IN_F4 = HY * HX * (KC / 4);                    // float4s of a full input chunk
+    constexpr int IN_ITERS = (IN_F4 + NTHREADS - 1) / NTHREADS;
     constexpr int T = TS * TS;
     constexpr int N = NT * 32;
     constexpr int W_F4 = T * N * (KC / 4);
@@ -115,9 +117,9 @@ __global__ __launch_bounds__(NTHREADS, 1) void conv_fwd_kernel(ConvParams p) {
         }
     };
 
-    f32x16 acc[2][NT];
+    f32x16 acc[MT][NT];
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
@@ -135,22 +137,21 @@ __global__ __launch_bounds__(NTHREADS, 1) void conv_fwd_kernel(ConvParams p) {
 #pragma unroll
         for (int tap = 0; tap < T; ++tap) {
             const int dy = p.tap_y0 + tap / TS, dx = p.tap_x0 + tap % TS;
-            const float *a0 = s_in + ((2 * wave + dy) * HX + ml + dx) * PS + hl * half;
-            const float *a1 = a0 + HX * PS;
+            const float *a0 = s_in + ((MT * wave + dy) * HX + ml + dx) * PS + hl * half;
             const float *bw = s_w + (tap * N + ml) * PS + hl * half;
             for (int g = 0; g < ngroups; ++g) {
-                const f32x4 av0 = *reinterpret_cast<const f32x4 *>(a0 + 4 * g);
-                const f32x4 av1 = *reinterpret_cast<const f32x4 *>(a1 + 4 * g);
-                f32x4 bv[NT];
+                f32x4 av[MT], bv[NT];
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt) av[mt] = *reinterpret_cast<const f32x4 *>(a0 + mt * HX * PS + 4 * g);
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt) bv[nt] = *reinterpret_cast<const f32x4 *>(bw + nt * 32 * PS + 4 * g);
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
 #pragma unroll
-                    for (int nt = 0; nt < NT; ++nt) {
-                        acc[0][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av0[s], bv[nt][s], acc[0][nt], 0, 0, 0);
-                        acc[1][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av1[s], bv[nt][s], acc[1][nt], 0, 0, 0);
-                    }
+                    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                        for (int mt = 0; mt < MT; ++mt)
+                            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mt][s], bv[nt][s], acc[mt][nt], 0, 0, 0);
                 }
             }
         }
@@ -166,8 +167,8 @@ __global__ __launch_bounds__(NTHREADS, 1) void conv_fwd_kernel(ConvParams p) {
         if (n >= p.cout) continue;
         const float bn = p.bias[n];
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-            const int y = y0 + 2 * wave + mt;
+        for (int mt = 0; mt < MT; ++mt) {
+            const int y = y0 + MT * wave + mt;
             if (y >= p.H) continue;
             const int oy = o.out_sy * y + o.out_oy;
 #pragma unroll
@@ -193,6 +194,18 @@ __global__ __launch_bounds__(NTHREADS, 1) void conv_fwd_kernel(ConvParams p) {
     }
 }
 
+int g_conv_tile = 0;  // esr_conv_set_tile: 0 = automatic, 4 or 8 output rows per workgroup
+
+int n_cus() {
+    static int n = 0;
+    if (!n) {
+        int dev = 0, v = 0;
+        n = (hipGetDevice(&dev) == hipSuccess &&
+             hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
+    }
+    return n;
+}
+
 int launch_conv(const float *in, int B, int H, int W, int in_cp, int cin, const float *w, const float *bias, int cout,
                 int taps_side, int ty0, int tx0, const esr_conv_out *o, hipStream_t stream) {
     if (!in || !w || !bias || !o || !o->out) return ESR_EINVAL;
@@ -205,16 +218,30 @@ int launch_conv(const float *in, int B, int H, int W, int in_cp, int cin, const 
     p.in = in; p.B = B; p.H = H; p.W = W; p.in_cp = in_cp; p.cin = cin;
     p.w = w; p.bias = bias; p.cout = cout; p.tap_y0 = ty0; p.tap_x0 = tx0;
     p.tiles_x = (W + TW - 1) / TW;
-    p.tiles_y = (H + TH - 1) / TH;
+    // 4-row tiles for N = 32 (two workgroups per CU fit in LDS: measured 8-35 % faster, profiles/r1_conv_tile_ab.txt)
+    // and for N = 64 when 8-row tiles would fill fewer than 8 rounds of one workgroup per CU (the last, partly idle
+    // round then costs up to an eighth; at 8+ rounds the 8-row tile's better weight reuse wins); esr_conv_set_tile
+    // overrides
+    const int tiles8 = p.tiles_x * ((H + 7) / 8) * B;
+    const int mt = g_conv_tile == 4 ? 1 : g_conv_tile == 8 ? 2 : ((cout <= 32 || tiles8 < 8 * n_cus()) ? 1 : 2);
+    p.tiles_y = (H + 4 * mt - 1) / (4 * mt);
     p.o = *o;
     const dim3 grid((unsigned)(p.tiles_x * p.tiles_y * B)), block(NTHREADS);
-    if (taps_side == 3) {
-        if (cout > 32) hipLaunchKernelGGL((conv_fwd_kernel<2, 3>), grid, block, 0, stream, p);
-        else hipLaunchKernelGGL((conv_fwd_kernel<1, 3>), grid, block, 0, stream, p);
+#define ESR_CONV_LAUNCH(NT_, TS_, MT_) hipLaunchKernelGGL((conv_fwd_kernel<NT_, TS_, MT_>), grid, block, 0, stream, p)
+    if (mt == 1) {
+        if (taps_side == 3) {
+            if (cout > 32) ESR_CONV_LAUNCH(2, 3, 1); else ESR_CONV_LAUNCH(1, 3, 1);
+        } else {
+            if (cout > 32) ESR_CONV_LAUNCH(2, 2, 1); else ESR_CONV_LAUNCH(1, 2, 1);
+        }
     } else {
-        if (cout > 32) hipLaunchKernelGGL((conv_fwd_kernel<2, 2>), grid, block, 0, stream, p);
-        else hipLaunchKernelGGL((conv_fwd_kernel<1, 2>), grid, block, 0, stream, p);
+        if (taps_side == 3) {
+            if (cout > 32) ESR_CONV_LAUNCH(2, 3, 2); else ESR_CONV_LAUNCH(1, 3, 2);
+        } else {
+            if (cout > 32) ESR_CONV_LAUNCH(2, 2, 2); else ESR_CONV_LAUNCH(1, 2, 2);
+        }
     }
+#undef ESR_CONV_LAUNCH
     return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
 }
 
@@ -233,4 +260,11 @@ extern "C" int esr_upconv2x_phase_fwd(const float *in, int32_t B, int32_t H, int
     return launch_conv(in, B, H, W, in_cp, cin, w_packed, bias, cout, 2, py, px, o, (hipStream_t)stream);
 }
 
-extern "C" int esr_abi_version(void) { return 6; }
+extern "C" int esr_conv_set_tile(int32_t rows) {
+    if (rows != 0 && rows != 4 && rows != 8) return ESR_EINVAL;
+    const int prev = g_conv_tile;
+    g_conv_tile = rows;
+    return prev;
+}
+
+extern "C" int esr_abi_version(void) { return 7; }

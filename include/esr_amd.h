@@ -67,6 +67,10 @@ typedef struct esr_conv_out {
  * in: padded NHWC [B][H+2][W+2][in_cp], reads channels [0, cin); cin % 8 == 0; cout <= 64. */
 int esr_conv3x3_fwd(const float *in, int32_t B, int32_t H, int32_t W, int32_t in_cp, int32_t cin,
                     const float *w_packed, const float *bias, int32_t cout, const esr_conv_out *o, esr_stream_t stream);
+/* Tile height of the exact-fp32 convs (esr_conv3x3_fwd, esr_upconv2x_phase_fwd), process-wide: 0 (default) =
+ * automatic (4 output rows per workgroup for cout <= 32, and for cout > 32 when 8-row tiles would fill fewer than 8
+ * rounds of the CUs; else 8), or force 4 / 8.  Results are identical either way.  Returns the previous setting, or ESR_EINVAL. */
+int esr_conv_set_tile(int32_t rows);
 
 /* One polyphase phase (py, px) in {0,1}² of the nearest-×2 upsample + 3×3 conv (upconv_blcok, block.py:294-301;
  * used twice by RRDBNet, networks.py:91): out[2y+py, 2x+px] = Σ_{a,b∈{0,1}} Wp[a][b] · in[y+py+a-1, x+px+b-1], with
