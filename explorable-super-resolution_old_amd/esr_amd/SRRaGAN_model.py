@@ -213,10 +213,14 @@ class SRRaGANModel:
                 else:
                     cur_Z = 2 * cur_Z - 1
             hw = [self.Z_size_factor * v for v in list(self.var_L.size()[2:])]
-            if isinstance(cur_Z, (int, float)) or (not torch.is_tensor(cur_Z) and np.ndim(cur_Z) < 4):
+            # the spatial broadcasts happen on the device (the reference builds them on the host: a 28 MB CPU tensor
+            # per step at config 3)
+            if isinstance(cur_Z, (int, float)):
+                cur_Z = torch.full([1, self.num_latent_channels] + hw, float(cur_Z), device=self.device)
+            elif not torch.is_tensor(cur_Z) and np.ndim(cur_Z) < 4:
                 cur_Z = cur_Z * np.ones([1, self.num_latent_channels] + hw)
             elif torch.is_tensor(cur_Z) and cur_Z.size(2) == 1:
-                cur_Z = cur_Z * torch.ones([1, 1] + hw)
+                cur_Z = cur_Z.to(self.device).float().expand(-1, -1, *hw).contiguous()
             if not torch.is_tensor(cur_Z):
                 cur_Z = torch.from_numpy(np.asarray(cur_Z, dtype=np.float32))
             cur_Z = cur_Z.float().to(self.device)

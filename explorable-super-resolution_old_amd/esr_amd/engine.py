@@ -219,13 +219,21 @@ class _Packed:
         self.version = getattr(self, 'version', 0) + 1  # invalidates recorded op lists (new x3 weight tensors)
         for cw in self.planned:
             cw._x3 = None
-        # the upsampler phases are sums of taps (not a permutation): packed directly, 8 small tensors
+        # the upsampler phases are sums of taps (not a permutation): packed directly, 8 small tensors, updated in place
+        # after the first build so that recorded op lists and captured HIP graphs keep valid pointers
         m = self.net.model
-        self.up = []
+        up = []
         for j in (2, 3):
             c = m[j][1]
-            self.up.append([_ConvW(pack_conv_weight(fold_upconv_phase(c.weight, py, px), list(range(64)), 64), c.bias)
-                            for py in (0, 1) for px in (0, 1)])
+            up.append([_ConvW(pack_conv_weight(fold_upconv_phase(c.weight, py, px), list(range(64)), 64), c.bias)
+                       for py in (0, 1) for px in (0, 1)])
+        if self.up is None:
+            self.up = up
+        else:
+            for old_row, new_row in zip(self.up, up):
+                for o, n in zip(old_row, new_row):
+                    o.f32.copy_(n.f32)
+                    o._x3 = None
 
 
 def _param_key(net):

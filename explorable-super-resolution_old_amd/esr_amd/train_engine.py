@@ -15,6 +15,7 @@ The reference's residual scales (0.2 in RDB and RRDB, block.py:235, 270) are fol
 and the reduction scales.
 """
 import ctypes
+import os
 
 import torch
 
@@ -22,6 +23,10 @@ from . import _lib
 from . import engine as E
 
 WG_SPLITS_MAX = 128
+# The training forward and the backward sweep are ~400 and ~1200 launches per step; after a shape/flag combination has
+# run once eagerly, it is captured into a HIP graph and replayed (one launch), with the parameter repack (GatherPlan
+# refresh) kept outside the graph.  ESR_TRAIN_GRAPHS=0 keeps everything eager.
+USE_GRAPHS = os.environ.get('ESR_TRAIN_GRAPHS', '1') != '0'
 
 
 def _z(dev, *s):
@@ -64,6 +69,7 @@ class TrainWorkspace:
         self.dZh = _z(dev, B, 4 * H + 2, 4 * W + 2, 8) if latent else None
         self.wg_n_max = 9 * 224 * 64 + 64
         self.partial = torch.empty(WG_SPLITS_MAX * self.wg_n_max, device=dev, dtype=torch.float32)
+        self.graphs = {}
 
 
 def _train_workspace(net, dev, B, H, W, latent):
@@ -378,13 +384,7 @@ def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_in
     # conv_first: dL/dfea = trunk gradient + LR_conv skip
     R.axpby(ws.GA, 64, 0, 1.0, ws.GA, 64, 0, 1.0, ws.dU0, 64, 0, C=64, h=H, w=W)
     R.wgrad(bp.first, ws.first, ws.first_cp, ws.first_cp, 0, ws.GA, 64, 0, H, W)
-    grads = {}
-    if need_params:
-        flat = bp.dw.index_select(0, bp.gidx)  # all parameter gradients, reference layout, parameter order
-        o = 0
-        for p in bp.params:
-            grads[p] = flat[o:o + p.numel()].view(p.shape)
-            o += p.numel()
+    flat = bp.dw.index_select(0, bp.gidx) if need_params else None  # all parameter gradients, reference layout
     dx = None
     if need_input:
         R.dgrad_in(bp.first, ws.GA, 64, 0, 64, H, W, ws.dFirst, ws.first_cp)
@@ -402,7 +402,45 @@ def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_in
             dx = torch.cat([d_z.view(Bn, 3 * E.SF * E.SF, h, w), d_lr], 1)  # raw view, SRRaGAN_model.py:252
         else:
             dx = d_lr
-    return grads, dx
+    return flat, dx
+
+
+def _split_grads(bp, flat):
+    grads, o = {}, 0
+    for p in bp.params:
+        grads[p] = flat[o:o + p.numel()].view(p.shape)
+        o += p.numel()
+    return grads
+
+
+def _run_graphed(ws, key, fn, *inputs):
+    """fn(*inputs) eagerly the first time `key` is seen; captured into a HIP graph (static copies of the inputs) the
+    second time; replayed from then on.  Returns fn's outputs, which for a graph live in its private pool (the caller
+    clones what must outlive the next replay)."""
+    if not USE_GRAPHS:
+        return fn(*inputs), False
+    ent = ws.graphs.get(key)
+    if ent is None:
+        ws.graphs[key] = 'seen'
+        return fn(*inputs), False
+    if ent == 'seen':
+        static = [t.detach().clone() for t in inputs]
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = fn(*static)
+        ent = ws.graphs[key] = (g, static, out)
+    g, static, out = ent
+    for st, t in zip(static, inputs):
+        st.copy_(t)
+    g.replay()
+    return out, True
+
+
+def _cem_key(cem):
+    if cem is None:
+        return None
+    return (id(cem), bool(cem.pre_pad), int(cem.margins_LR), cem.DownscaleOP.Filter_OP.weight.data_ptr(),
+            cem.Conv_LR_with_Inv_hTh_OP.Filter_OP.weight.data_ptr(), cem.Upscale_OP.Filter_OP.weight.data_ptr())
 
 
 class _GeneratorFn(torch.autograd.Function):
@@ -413,16 +451,28 @@ class _GeneratorFn(torch.autograd.Function):
         m = int(cem.margins_LR) if pre_pad else 0
         Bn, _, h, w = x.shape
         ws = _train_workspace(net, x.device, Bn, h + 2 * m, w + 2 * m, latent)
-        out, _ = E._forward(net, x.detach().contiguous(), cem, 'f32', train_ws=ws)
+        pk = E._packed(net, latent)  # parameter repack, outside any graph
+        key = ('fwd', tuple(x.shape), _cem_key(cem), id(pk))
+        out, graphed = _run_graphed(ws, key, lambda xs: E._forward(net, xs, cem, 'f32', train_ws=ws)[0],
+                                    x.detach().contiguous())
         ctx.net, ctx.cem, ctx.ws, ctx.latent, ctx.M = net, cem, ws, latent, E.SF * m
         ctx.params = params
-        return out
+        return out.clone() if graphed else out
 
     @staticmethod
     def backward(ctx, d_out):
         need_params = any(ctx.needs_input_grad[3:])
-        grads, dx = generator_backward(ctx.net, ctx.cem, ctx.ws, d_out, ctx.latent, ctx.M, need_params=need_params,
-                                       need_input=ctx.needs_input_grad[0])
+        need_input = ctx.needs_input_grad[0]
+        bp = _bwd_packed(ctx.net, ctx.latent)  # parameter repack, outside any graph
+        key = ('bwd', tuple(d_out.shape), _cem_key(ctx.cem), ctx.M, need_params, need_input, id(bp))
+        (flat, dx), graphed = _run_graphed(
+            ctx.ws, key, lambda g: generator_backward(ctx.net, ctx.cem, ctx.ws, g, ctx.latent, ctx.M,
+                                                      need_params=need_params, need_input=need_input),
+            d_out.contiguous())
+        if graphed:
+            flat = flat.clone() if flat is not None else None
+            dx = dx.clone() if dx is not None else None
+        grads = _split_grads(bp, flat) if flat is not None else {}
         return (dx, None, None) + tuple(grads.get(p) for p in ctx.params)
 
 

@@ -217,3 +217,45 @@ def test_weight_gradient_kernels_vs_float64(gpu_device, variant, cin, in_cp, cou
     got_w = out[:9 * cin_pad * cout_pad].view(3, 3, cin_pad, cout_pad)[:, :, :cin, :cout].permute(3, 2, 0, 1)
     assert normwise_rel(got_w, ref_w) < 1e-5
     assert normwise_rel(out[9 * cin_pad * cout_pad:][:cout], dy.double().sum((0, 2, 3))) < 1e-5
+
+
+@pytest.mark.parametrize('latent', [False, True])
+def test_graph_replay_equals_eager(gpu_device, latent):
+    """The HIP-graph replay of the training forward/backward (captured on the second call of a shape) gives bitwise the
+    eager results over several optimiser steps (the parameter repack runs outside the graph), for parameter and
+    input gradients."""
+    from esr_amd import train_engine as T
+    from oracle.recipe import seeded_params
+    net0 = esr_amd.RRDBNet(3, 3, 64, 1, latent_input='all_layers_HR_downscaled' if latent else None,
+                           num_latent_channels=3 if latent else 0)
+    shapes = [(k, tuple(v.shape)) for k, v in C.CEMnet(C.Get_CEM_Config(4)).WrapArchitecture_PyTorch(net0)
+              .state_dict().items() if 'Filter' not in k]
+    params = seeded_params(shapes, 61, w_scale=0.5)
+    lr, z = seeded_inputs(62, (2, 3, 12, 16), (2, 3, 48, 64) if latent else None)
+    x = torch.from_numpy(lr)
+    if latent:
+        x = torch.cat([torch.from_numpy(z).reshape(2, 48, 12, 16), x], 1)
+    R = torch.from_numpy(np.random.default_rng(63).standard_normal((2, 3, 48, 64)).astype(np.float32))
+    runs = {}
+    prev = T.USE_GRAPHS
+    try:
+        for graphs in (False, True):
+            T.USE_GRAPHS = graphs
+            model = _model(1, latent, params, gpu_device)
+            opt = torch.optim.SGD([p for p in model.parameters() if p.requires_grad], lr=1e-3)
+            xin = x.to(gpu_device).requires_grad_(True)
+            rec = []
+            for _ in range(4):
+                opt.zero_grad()
+                xin.grad = None
+                out = model(xin)
+                (out * R.to(gpu_device)).sum().backward()
+                rec.append([out.detach().clone(), xin.grad.clone()] +
+                           [p.grad.clone() for p in model.parameters() if p.requires_grad])
+                opt.step()
+            runs[graphs] = rec
+    finally:
+        T.USE_GRAPHS = prev
+    for step, (a, b) in enumerate(zip(runs[False], runs[True])):
+        for i, (u, v) in enumerate(zip(a, b)):
+            assert torch.equal(u, v), (step, i)
