@@ -20,22 +20,24 @@ NAMES = {0: 'classic', 1: 'auto', 2: 'ring', 15: 'ring+stagger', 3: 'dbg:no-dma'
          6: 'nodma+nobar', 7: 'nodma+slot0', 8: 'nodma+nopred', 9: 'nodma+all3', 10: 'nodma+nomfma',
          11: 'reads+restage', 12: 'reads only', 13: 'no-ep-stores', 14: 'dma only,no ep', 16: 'pring pf1',
          17: 'pring pf2'}
+COUT = int(os.environ.get('AB_COUT', '32'))
+REPS = int(os.environ.get('AB_REPS', '50'))
 for H, W in ((148, 148), (96, 96)):
-    for cin in (64, 128, 160):
-        cout, cp = 32, 192
+    for cin in ((64, 128, 160) if COUT <= 32 else (192,)):
+        cout, cp = COUT, 192
         g = torch.Generator(device='cpu').manual_seed(cin)
         x = torch.zeros(B, H + 2, W + 2, cp)
         x[:, 1:-1, 1:-1, :cin] = torch.rand(B, H, W, cin, generator=g) * 2 - 1
         x = x.to(dev)
         w = (torch.randn(cout, cin, 3, 3, generator=g) * 0.05).to(dev)
         b = (torch.rand(cout, generator=g) * 0.02 - 0.01).to(dev)
-        wx, scale = engine.pack_x3(engine.pack_conv_weight(w, list(range(cin)), 32))
+        wx, scale = engine.pack_x3(engine.pack_conv_weight(w, list(range(cin)), 32 if cout <= 32 else 64))
         xs = engine.to_split(x)
         res = {}
         for variant in VARIANTS:
             lib.esr_x3_set_kernel(variant)
             out = torch.zeros(B, H + 2, W + 2, cp, device=dev)
-            o = engine._conv_out(out, cp, cin, H, W, True)
+            o = engine._conv_out(out, cp, cin if cin + cout <= cp else 0, H, W, True)
 
             def run():
                 return lib.esr_conv3x3_fwd_x3(xs.data_ptr(), B, H, W, cp, cin, wx.data_ptr(), b.data_ptr(), scale,
@@ -44,19 +46,19 @@ for H, W in ((148, 148), (96, 96)):
                 _lib.check(run(), 'conv_x3')
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
-            for _ in range(20):
+            for _ in range(REPS):
                 run()
             e.record()
             torch.cuda.synchronize()
-            us = s.elapsed_time(e) / 20 * 1e3
+            us = s.elapsed_time(e) / REPS * 1e3
             fl = 2.0 * B * H * W * 9 * cin * cout
             res[variant] = (us, out)
             print('B=%d %dx%d cin=%d cout=%d %-14s: %8.1f us  %6.1f TFLOP/s' % (
-                B, H, W, cin, cout, NAMES[variant], us, fl / us / 1e6), flush=True)
+                B, H, W, cin, cout, NAMES.get(variant & 255, str(variant & 255)) + ('+prio' if variant & 256 else ''), us, fl / us / 1e6), flush=True)
         v0 = VARIANTS[0]
         for v in VARIANTS[1:]:
             same = torch.equal(res[v0][1], res[v][1]) if v < 3 or v >= 15 else True
-            print('   %s/%s speedup %.3f, outputs bitwise equal: %s' % (NAMES[v], NAMES[v0], res[v0][0] / res[v][0],
+            print('   %s/%s speedup %.3f, outputs bitwise equal: %s' % (NAMES.get(v & 255, str(v)) + ('+prio' if v & 256 else ''), NAMES.get(v0 & 255, str(v0)), res[v0][0] / res[v][0],
                                                                       same), flush=True)
             assert same
 lib.esr_x3_set_kernel(1)
