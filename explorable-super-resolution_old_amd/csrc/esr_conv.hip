@@ -180,9 +180,14 @@ __global__ __launch_bounds__(NTHREADS, (MT == 1 && NT == 1) ? 2 : 1) void conv_f
                 if (o.lrelu == 1) v = v > 0.f ? v : 0.2f * v;
                 const long long pix = ((long long)b * (o.out_h + 2) + oy + 1) * orow + ox + 1;
                 if (o.r1) v = o.s1 * v + o.r1[pix * o.r1_cp + o.r1_coff + n];
-                if (o.lrelu == 2)
+                if (o.lrelu == 2) {
                     v = o.r2[pix * o.r2_cp + o.r2_coff + n] > 0.f ? v : 0.2f * v;
-                else if (o.r2)
+                } else if (o.lrelu == 3) {  // the saved activation in the split-f16 layout
+                    const _Float16 *g = reinterpret_cast<const _Float16 *>(
+                        reinterpret_cast<const unsigned char *>(o.r2) + pix * o.r2_cp * 4 + ((o.r2_coff + n) >> 3) * 32);
+                    const int e = (o.r2_coff + n) & 7;
+                    v = ((float)g[e] + (float)g[8 + e]) > 0.f ? v : 0.2f * v;
+                } else if (o.r2)
                     v = o.s2 * v + o.r2[pix * o.r2_cp + o.r2_coff + n];
                 if (o.out_planar)
                     o.out[(((long long)b * p.cout + n) * o.out_h + oy) * o.out_w + ox] = v;
@@ -211,7 +216,8 @@ int launch_conv(const float *in, int B, int H, int W, int in_cp, int cin, const 
     if (!in || !w || !bias || !o || !o->out) return ESR_EINVAL;
     if (B <= 0 || H <= 0 || W <= 0 || cin <= 0 || cout <= 0 || cout > 64) return ESR_EINVAL;
     if (cin % 8 || in_cp % 4 || in_cp < cin) return ESR_EINVAL;
-    if (o->lrelu < 0 || o->lrelu > 2 || (o->lrelu == 2 && !o->r2)) return ESR_EINVAL;
+    if (o->lrelu < 0 || o->lrelu > 3 || (o->lrelu >= 2 && !o->r2) || (o->lrelu == 3 && (o->r2_cp % 8 || o->r2_coff % 8)))
+        return ESR_EINVAL;
     if (!o->out_planar && o->out_coff + cout > o->out_cp) return ESR_EINVAL;
     if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(w)) & 15) return ESR_EINVAL;
     ConvParams p;
@@ -267,4 +273,4 @@ extern "C" int esr_conv_set_tile(int32_t rows) {
     return prev;
 }
 
-extern "C" int esr_abi_version(void) { return 7; }
+extern "C" int esr_abi_version(void) { return 8; }

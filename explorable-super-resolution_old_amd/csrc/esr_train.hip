@@ -22,6 +22,13 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int NT = 256;
 inline unsigned nblocks(long long n) { return (unsigned)((n + NT - 1) / NT); }
+
+// value of channel c of a pixel record in the split-f16 layout (include/esr_amd.h: groups of 8 channels, 32 B =
+// 8 × f16 hi then 8 × f16 lo); `rec` points at the pixel's first byte
+__device__ __forceinline__ float split_at(const unsigned char *rec, int c) {
+    const _Float16 *g = reinterpret_cast<const _Float16 *>(rec + (c >> 3) * 32);
+    return (float)g[c & 7] + (float)g[8 + (c & 7)];
+}
 inline int launched() { return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH; }
 
 // ---------------------------------------------------------------------------------------------------------------------
@@ -320,12 +327,14 @@ __device__ __forceinline__ long long pix_index(long long idx, int C, int B, int 
 }
 
 __global__ void lrelu_bwd_kernel(float *d, int d_cp, int d_coff, const float *y, int y_cp, int y_coff, int C, int B,
-                                 int H, int W) {
+                                 int H, int W, int y_split) {
     const long long idx = (long long)blockIdx.x * NT + threadIdx.x;
     if (idx >= (long long)B * H * W * C) return;
     int c;
     const long long pix = pix_index(idx, C, B, H, W, &c);
-    if (!(y[pix * y_cp + y_coff + c] > 0.f)) d[pix * d_cp + d_coff + c] *= 0.2f;
+    const float yv = y_split ? split_at(reinterpret_cast<const unsigned char *>(y) + pix * y_cp * 4, y_coff + c)
+                             : y[pix * y_cp + y_coff + c];
+    if (!(yv > 0.f)) d[pix * d_cp + d_coff + c] *= 0.2f;
 }
 
 __global__ void axpby_kernel(float *out, int o_cp, int o_coff, float a, const float *x1, int x1_cp, int x1_coff,
@@ -519,7 +528,15 @@ extern "C" int esr_lrelu_bwd(float *d, int32_t d_cp, int32_t d_coff, const float
                              int32_t C, int32_t B, int32_t H, int32_t W, esr_stream_t stream) {
     if (!d || !y || C <= 0 || B <= 0 || H <= 0 || W <= 0) return ESR_EINVAL;
     hipLaunchKernelGGL(lrelu_bwd_kernel, dim3(nblocks((long long)B * H * W * C)), dim3(NT), 0, (hipStream_t)stream, d,
-                       d_cp, d_coff, y, y_cp, y_coff, C, B, H, W);
+                       d_cp, d_coff, y, y_cp, y_coff, C, B, H, W, 0);
+    return launched();
+}
+
+extern "C" int esr_lrelu_bwd_split(float *d, int32_t d_cp, int32_t d_coff, const void *y, int32_t y_cp,
+                                   int32_t y_coff, int32_t C, int32_t B, int32_t H, int32_t W, esr_stream_t stream) {
+    if (!d || !y || C <= 0 || B <= 0 || H <= 0 || W <= 0 || y_cp % 8) return ESR_EINVAL;
+    hipLaunchKernelGGL(lrelu_bwd_kernel, dim3(nblocks((long long)B * H * W * C)), dim3(NT), 0, (hipStream_t)stream, d,
+                       d_cp, d_coff, static_cast<const float *>(y), y_cp, y_coff, C, B, H, W, 1);
     return launched();
 }
 

@@ -72,8 +72,9 @@ class TrainWorkspace:
         self.graphs = {}
 
 
-def _train_workspace(net, dev, B, H, W, latent):
-    key = (str(dev), B, H, W, latent, net.nb)
+def _train_workspace(net, dev, B, H, W, latent, precision='f32'):
+    # keyed by precision too: an x3 forward leaves split-f16 records where an fp32 forward expects floats
+    key = (str(dev), B, H, W, latent, net.nb, precision)
     c = net._esr_cache.get('train_ws')
     if c is None or c[0] != key:
         net._esr_cache.pop('train_ws', None)
@@ -215,13 +216,16 @@ def _bwd_packed(net, latent):
 # backward sweep
 # ----------------------------------------------------------------------------------------------------------------------
 class _Runner:
-    def __init__(self, ws, bp, stream, need_params=True, need_input=False):
+    def __init__(self, ws, bp, stream, need_params=True, need_input=False, split=False):
         self.lib = _lib.load()
         self.ws = ws
         self.bp = bp
         self.B = ws.B
         self.stream = stream
         self.need_params, self.need_input = need_params, need_input
+        self.split = split  # forward activations in the split-f16 layout (x3 forward)
+        if split and need_params:
+            raise RuntimeError('esr_amd: weight gradients need the exact-fp32 forward activations')
 
     def dgrad(self, bc, src, src_cp, src_coff, cin_k, h, w, dst, dst_cp, dst_base, accumulate, res=None):
         """dst[:, n0-dst_base ...] (+)= conv(src slice, rot180 W^T) for every output slice; `res` = (buf, cp, coff)
@@ -247,7 +251,7 @@ class _Runner:
         elif res is not None:
             r1, r1_cp, r1_coff = res
         r2, r2_cp, r2_coff = mask if mask is not None else (None, 0, 0)
-        o = E._conv_out(dst, dst_cp, dst_coff, h, w, 2 if mask is not None else 0, r1=r1, r1_cp=r1_cp,
+        o = E._conv_out(dst, dst_cp, dst_coff, h, w, (3 if self.split else 2) if mask is not None else 0, r1=r1, r1_cp=r1_cp,
                         r1_coff=r1_coff, s1=1.0, r2=r2, r2_cp=r2_cp, r2_coff=r2_coff)
         _lib.check(self.lib.esr_conv3x3_fwd(src.data_ptr() + 4 * src_coff, self.B, h, w, src_cp, cin_k, wpk.data_ptr(),
                                             self.bp.zero_bias.data_ptr(), nw, ctypes.byref(o), self.stream),
@@ -280,8 +284,9 @@ class _Runner:
                                              self.bp.dw.data_ptr() + 4 * bc.wg_off, self.stream), 'wgrad_reduce')
 
     def lrelu(self, d, d_cp, d_coff, y, y_cp, y_coff, C, h, w):
-        _lib.check(self.lib.esr_lrelu_bwd(d.data_ptr(), d_cp, d_coff, y.data_ptr(), y_cp, y_coff, C, self.B, h, w,
-                                          self.stream), 'lrelu_bwd')
+        fn = self.lib.esr_lrelu_bwd_split if self.split else self.lib.esr_lrelu_bwd
+        _lib.check(fn(d.data_ptr(), d_cp, d_coff, y.data_ptr(), y_cp, y_coff, C, self.B, h, w, self.stream),
+                   'lrelu_bwd')
 
     def axpby(self, out, o_cp, o_coff, a, x1, x1_cp, x1_coff, b=0.0, x2=None, x2_cp=0, x2_coff=0, C=64, h=0, w=0):
         _lib.check(self.lib.esr_axpby(out.data_ptr(), o_cp, o_coff, a, x1.data_ptr(), x1_cp, x1_coff, b,
@@ -306,13 +311,13 @@ def _rdb_backward(R, P, dcat, convs, fused, zc, cp, H, W, dx):
     R.dgrad_fused(fused['x'], dcat, dcp, zc + 64, 192, H, W, dx[0], dx[1], dx[2], 64, res=(dcat, dcp, d4))
 
 
-def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_input=False):
+def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_input=False, split=False):
     """dL/dparams of RRDBNet (+ CEM in train or eval mode) and/or dL/dinput given dL/dout.
     Returns ({param: grad} or {}, input gradient [B, C_in, h, w] or None)."""
     dev = d_out.device
     stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     bp = _bwd_packed(net, latent)
-    R = _Runner(ws, bp, stream, need_params, need_input)
+    R = _Runner(ws, bp, stream, need_params, need_input, split)
     lib = R.lib
     if need_input:
         ws.dZl.zero_()
@@ -450,12 +455,31 @@ class _GeneratorFn(torch.autograd.Function):
         pre_pad = cem is not None and cem.pre_pad
         m = int(cem.margins_LR) if pre_pad else 0
         Bn, _, h, w = x.shape
-        ws = _train_workspace(net, x.device, Bn, h + 2 * m, w + 2 * m, latent)
+        # Only the input gradient needed (Z optimisation, generator frozen): the forward runs in the x3 precision of
+        # inference and the backward reads its split-f16 activations; weight gradients need the exact-fp32 forward.
+        prec = 'f32'
+        if not any(p.requires_grad for p in params) and \
+                (getattr(net, 'esr_precision', None) or E.DEFAULT_PRECISION) == 'x3':
+            prec = 'x3'
+        ws = _train_workspace(net, x.device, Bn, h + 2 * m, w + 2 * m, latent, prec)
         pk = E._packed(net, latent)  # parameter repack, outside any graph
-        key = ('fwd', tuple(x.shape), _cem_key(cem), id(pk))
-        out, graphed = _run_graphed(ws, key, lambda xs: E._forward(net, xs, cem, 'f32', train_ws=ws)[0],
-                                    x.detach().contiguous())
-        ctx.net, ctx.cem, ctx.ws, ctx.latent, ctx.M = net, cem, ws, latent, E.SF * m
+        if prec == 'x3':  # split-f16 weights built outside any graph (their scales are kernel arguments)
+            for cw in pk.planned + [c for row in pk.up for c in row]:
+                cw.x3()
+
+        def fwd(xs):
+            if prec == 'x3':
+                ws.overflow.zero_()
+            return E._forward(net, xs, cem, prec, train_ws=ws)[0]
+        key = ('fwd', prec, tuple(x.shape), _cem_key(cem), id(pk), getattr(pk, 'version', 0))
+        xd = x.detach().contiguous()
+        out, graphed = _run_graphed(ws, key, fwd, xd)
+        split = prec == 'x3'
+        if split and int(ws.overflow.item()):  # an activation beyond the f16 range: redo in exact fp32
+            E.OVERFLOW_RERUNS += 1
+            ws = _train_workspace(net, x.device, Bn, h + 2 * m, w + 2 * m, latent, 'f32')
+            out, graphed, split = E._forward(net, xd, cem, 'f32', train_ws=ws)[0], False, False
+        ctx.net, ctx.cem, ctx.ws, ctx.latent, ctx.M, ctx.split = net, cem, ws, latent, E.SF * m, split
         ctx.params = params
         return out.clone() if graphed else out
 
@@ -464,10 +488,11 @@ class _GeneratorFn(torch.autograd.Function):
         need_params = any(ctx.needs_input_grad[3:])
         need_input = ctx.needs_input_grad[0]
         bp = _bwd_packed(ctx.net, ctx.latent)  # parameter repack, outside any graph
-        key = ('bwd', tuple(d_out.shape), _cem_key(ctx.cem), ctx.M, need_params, need_input, id(bp))
+        key = ('bwd', tuple(d_out.shape), _cem_key(ctx.cem), ctx.M, need_params, need_input, id(bp), ctx.split)
         (flat, dx), graphed = _run_graphed(
             ctx.ws, key, lambda g: generator_backward(ctx.net, ctx.cem, ctx.ws, g, ctx.latent, ctx.M,
-                                                      need_params=need_params, need_input=need_input),
+                                                      need_params=need_params, need_input=need_input,
+                                                      split=ctx.split),
             d_out.contiguous())
         if graphed:
             flat = flat.clone() if flat is not None else None

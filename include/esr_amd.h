@@ -40,7 +40,8 @@ enum esr_status {
  *   v = acc + bias[n]; if (lrelu == 1) v = v > 0 ? v : 0.2*v   (conv_block CNA + act, block.py:10-23,141-146)
  *   if (r1) v = s1*v + r1[pixel, r1_coff + n]                  (RDB / trunk residuals, block.py:96,235,270)
  *   if (lrelu == 2) v = r2[pixel, r2_coff + n] > 0 ? v : 0.2*v (LeakyReLU backward through the saved activation r2;
- *                                                               exact-fp32 convs only, r2 required)
+ *                                                               exact-fp32 convs only, r2 required; lrelu == 3: r2
+ *                                                               in the split-f16 layout, r2_cp/r2_coff % 8 == 0)
  *   else if (r2) v = s2*v + r2[pixel, r2_coff + n]
  *   out[pixel, out_coff + n] = v   (and out2 likewise when out2 != NULL)
  * Output pixel of input-grid position (y, x) is (out_sy*y + out_oy, out_sx*x + out_ox) in the out grid (out_h × out_w,
@@ -160,6 +161,9 @@ int esr_wgrad_set_kernel(int32_t variant);
 /* LeakyReLU(0.2) backward from the saved output y: d *= (y > 0 ? 1 : 0.2) on a C-channel slice. */
 int esr_lrelu_bwd(float *d, int32_t d_cp, int32_t d_coff, const float *y, int32_t y_cp, int32_t y_coff, int32_t C,
                   int32_t B, int32_t H, int32_t W, esr_stream_t stream);
+/* The same with y in the split-f16 layout (the x3 forward's activations; y_cp % 8 == 0). */
+int esr_lrelu_bwd_split(float *d, int32_t d_cp, int32_t d_coff, const void *y, int32_t y_cp, int32_t y_coff, int32_t C,
+                        int32_t B, int32_t H, int32_t W, esr_stream_t stream);
 /* out = a·x1 + b·x2 (x2 may be NULL) on C-channel slices of padded NHWC buffers (in place allowed, pointwise). */
 int esr_axpby(float *out, int32_t o_cp, int32_t o_coff, float a, const float *x1, int32_t x1_cp, int32_t x1_coff,
               float b, const float *x2, int32_t x2_cp, int32_t x2_coff, int32_t C, int32_t B, int32_t H, int32_t W,
