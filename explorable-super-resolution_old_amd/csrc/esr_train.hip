@@ -20,6 +20,8 @@ namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
 constexpr int NT = 256;
 inline unsigned nblocks(long long n) { return (unsigned)((n + NT - 1) / NT); }
 
@@ -156,8 +158,9 @@ constexpr int W2_NT = 768;
 constexpr int W2_IN_F = WT_HY * WT_HX * WT_IP, W2_D_F = WT_TH * WT_TW * WT_DP;
 constexpr int W2_IN_V4 = WT_HY * WT_HX * 8, W2_D_V4 = WT_TH * WT_TW * 16;
 constexpr int W2_IN_PT = (W2_IN_V4 + W2_NT - 1) / W2_NT, W2_D_PT = (W2_D_V4 + W2_NT - 1) / W2_NT;
+static_assert(W2_IN_PT % 2 == 0 && (W2_IN_V4 / 2 + W2_NT - 1) / W2_NT <= W2_IN_PT / 2, "split staging layout");
 
-template <int NCT>
+template <int NCT, bool SPLIT>
 __global__ __launch_bounds__(W2_NT, 1) void wgrad2_kernel(WgradParams p) {
     constexpr int NQ = 4 / NCT;  // pixel classes
     __shared__ __attribute__((aligned(16))) float smem[W2_IN_F + W2_D_F];
@@ -191,19 +194,45 @@ __global__ __launch_bounds__(W2_NT, 1) void wgrad2_kernel(WgradParams p) {
     auto load_tile = [&](int t) {
         const int tx = t % p.tiles_x, ty = (t / p.tiles_x) % p.tiles_y, b = t / (p.tiles_x * p.tiles_y);
         const int y0 = ty * WT_TH, x0 = tx * WT_TW;
+        if (SPLIT) {
+            // one 8-channel group (32 B: hi[8], lo[8]) per item, 4 groups per pixel, two registers quads per item
 #pragma unroll
-        for (int k = 0; k < W2_IN_PT; ++k) {
-            const int idx = tid + k * W2_NT;
-            const int px = idx >> 3, c4 = idx & 7;
-            const int hy = px / WT_HX, hx = px - hy * WT_HX;
-            const int Y = y0 + hy - 1, X = x0 + hx - 1;
-            f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            if (idx < W2_IN_V4 && Y >= 0 && Y < p.H && X >= 0 && X < p.W && c4 * 4 < kc) {
-                const int sy = p.up2 ? Y / 2 : Y, sx = p.up2 ? X / 2 : X;
-                v = *reinterpret_cast<const f32x4 *>(
-                    p.in + (((long long)b * (Hi + 2) + sy + 1) * (Wi + 2) + sx + 1) * p.in_cp + c0 + c4 * 4);
+            for (int k = 0; k < W2_IN_PT / 2; ++k) {
+                const int idx = tid + k * W2_NT;
+                const int px = idx >> 2, g = idx & 3;
+                const int hy = px / WT_HX, hx = px - hy * WT_HX;
+                const int Y = y0 + hy - 1, X = x0 + hx - 1;
+                f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = {0.f, 0.f, 0.f, 0.f};
+                if (idx < W2_IN_V4 / 2 && Y >= 0 && Y < p.H && X >= 0 && X < p.W && g * 8 < kc) {
+                    const int sy = p.up2 ? Y / 2 : Y, sx = p.up2 ? X / 2 : X;
+                    const f16x8 *src = reinterpret_cast<const f16x8 *>(
+                        reinterpret_cast<const unsigned char *>(p.in) +
+                        ((((long long)b * (Hi + 2) + sy + 1) * (Wi + 2) + sx + 1) * p.in_cp + c0 + g * 8) * 4);
+                    const f16x8 hi = src[0], lo = src[1];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        v0[e] = (float)hi[e] + (float)lo[e];
+                        v1[e] = (float)hi[4 + e] + (float)lo[4 + e];
+                    }
+                }
+                rin[2 * k] = v0;
+                rin[2 * k + 1] = v1;
             }
-            rin[k] = v;
+        } else {
+#pragma unroll
+            for (int k = 0; k < W2_IN_PT; ++k) {
+                const int idx = tid + k * W2_NT;
+                const int px = idx >> 3, c4 = idx & 7;
+                const int hy = px / WT_HX, hx = px - hy * WT_HX;
+                const int Y = y0 + hy - 1, X = x0 + hx - 1;
+                f32x4 v = {0.f, 0.f, 0.f, 0.f};
+                if (idx < W2_IN_V4 && Y >= 0 && Y < p.H && X >= 0 && X < p.W && c4 * 4 < kc) {
+                    const int sy = p.up2 ? Y / 2 : Y, sx = p.up2 ? X / 2 : X;
+                    v = *reinterpret_cast<const f32x4 *>(
+                        p.in + (((long long)b * (Hi + 2) + sy + 1) * (Wi + 2) + sx + 1) * p.in_cp + c0 + c4 * 4);
+                }
+                rin[k] = v;
+            }
         }
 #pragma unroll
         for (int k = 0; k < W2_D_PT; ++k) {
@@ -225,10 +254,22 @@ __global__ __launch_bounds__(W2_NT, 1) void wgrad2_kernel(WgradParams p) {
         }
     };
     auto store_tile = [&]() {
+        if (SPLIT) {
 #pragma unroll
-        for (int k = 0; k < W2_IN_PT; ++k) {
-            const int idx = tid + k * W2_NT;
-            if (idx < W2_IN_V4) *reinterpret_cast<f32x4 *>(s_in + (idx >> 3) * WT_IP + (idx & 7) * 4) = rin[k];
+            for (int k = 0; k < W2_IN_PT / 2; ++k) {
+                const int idx = tid + k * W2_NT;
+                if (idx < W2_IN_V4 / 2) {
+                    float *dst = s_in + (idx >> 2) * WT_IP + (idx & 3) * 8;
+                    *reinterpret_cast<f32x4 *>(dst) = rin[2 * k];
+                    *reinterpret_cast<f32x4 *>(dst + 4) = rin[2 * k + 1];
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < W2_IN_PT; ++k) {
+                const int idx = tid + k * W2_NT;
+                if (idx < W2_IN_V4) *reinterpret_cast<f32x4 *>(s_in + (idx >> 3) * WT_IP + (idx & 7) * 4) = rin[k];
+            }
         }
 #pragma unroll
         for (int k = 0; k < W2_D_PT; ++k) {
@@ -483,11 +524,13 @@ __global__ void input_adjoint_kernel(const float *d_hr, int hr_cp, int hr_coff, 
     out[idx] = v;
 }
 
-extern "C" int esr_conv3x3_wgrad(const float *in, int32_t in_cp, int32_t cin, int32_t up2, const float *dout,
+extern "C" int esr_conv3x3_wgrad(const float *in, int32_t in_cp, int32_t cin, int32_t flags, const float *dout,
                                  int32_t dout_cp, int32_t dout_coff, int32_t cout, int32_t B, int32_t H, int32_t W,
                                  int32_t splits, float *partial, esr_stream_t stream) {
+    const int up2 = flags & 1, split = (flags >> 1) & 1;
     if (!in || !dout || !partial || cin <= 0 || cin % 4 || in_cp % 4 || cout <= 0 || cout > 64 || B <= 0 ||
-        H <= 0 || W <= 0 || splits <= 0 || (up2 && (H % 2 || W % 2)))
+        H <= 0 || W <= 0 || splits <= 0 || (up2 && (H % 2 || W % 2)) || (flags & ~3) ||
+        (split && (cin % 8 || in_cp % 8 || g_wgrad_kernel != 1)))
         return ESR_EINVAL;
     WgradParams p;
     p.in = in; p.in_cp = in_cp; p.cin = cin; p.up2 = up2;
@@ -499,10 +542,17 @@ extern "C" int esr_conv3x3_wgrad(const float *in, int32_t in_cp, int32_t cin, in
     const unsigned total = (unsigned)(p.cin_pad / 32 * splits);
     if (g_wgrad_kernel == 1) {
         const unsigned grid = 8 * ((total + 7) / 8);  // whole XCD rounds; the surplus workgroups exit at once
-        if (p.cout_pad == 64)
-            hipLaunchKernelGGL(wgrad2_kernel<2>, dim3(grid), dim3(W2_NT), 0, (hipStream_t)stream, p);
-        else
-            hipLaunchKernelGGL(wgrad2_kernel<1>, dim3(grid), dim3(W2_NT), 0, (hipStream_t)stream, p);
+        if (split) {
+            if (p.cout_pad == 64)
+                hipLaunchKernelGGL((wgrad2_kernel<2, true>), dim3(grid), dim3(W2_NT), 0, (hipStream_t)stream, p);
+            else
+                hipLaunchKernelGGL((wgrad2_kernel<1, true>), dim3(grid), dim3(W2_NT), 0, (hipStream_t)stream, p);
+        } else {
+            if (p.cout_pad == 64)
+                hipLaunchKernelGGL((wgrad2_kernel<2, false>), dim3(grid), dim3(W2_NT), 0, (hipStream_t)stream, p);
+            else
+                hipLaunchKernelGGL((wgrad2_kernel<1, false>), dim3(grid), dim3(W2_NT), 0, (hipStream_t)stream, p);
+        }
     } else {
         hipLaunchKernelGGL(wgrad_kernel, dim3(total), dim3(256), 0, (hipStream_t)stream, p);
     }

@@ -97,6 +97,15 @@ def pack_x3(packed):
     return out, scale
 
 
+def _pack_x3_scaled(packed, scale):
+    """pack_x3 with a given power-of-two scale (no host sync)."""
+    n32, T, n_pad, _ = packed.shape
+    p16 = packed.view(n32, T, n_pad, 2, 16).permute(0, 3, 1, 2, 4).reshape(2 * n32, T, n_pad, 16)
+    hi, lo = split_f16(p16 * scale)
+    sh = (2 * n32, T, n_pad, 2, 1, 8)
+    return torch.cat([hi.reshape(sh), lo.reshape(sh)], dim=4).contiguous(), scale
+
+
 def to_split(x_nhwc):
     """fp32 [..., C] (C % 8 == 0) -> split-f16 layout with the same byte size, returned as float32 storage."""
     hi, lo = split_f16(x_nhwc)
@@ -213,6 +222,59 @@ class _Packed:
         for cw in self.planned:
             cw.f32 = views[id(cw.f32)]
         self.up = None
+
+    def train_x3(self):
+        """x3 weights for the training / Z-optimisation forward, rebuilt IN PLACE after every parameter change with no
+        host sync: each layer keeps the power-of-two scale pack_x3 chose at the first build (so recorded launches and
+        captured graphs stay valid), and all planned layers are split in one gather over the packed fp32 buffer.
+        Returns a persistent device int32 flag, 1 if any scaled weight left the safe f16 range; the caller then falls
+        back to fp32 for that step and calls reset_train_x3() so the next build picks new scales."""
+        convs = self.planned + [c for row in self.up for c in row]
+        if getattr(self, '_tx3', None) is None:
+            scales = [pack_x3(cw.f32)[1] for cw in convs]  # one host sync per layer, at the first build only
+            self._tx3_epoch = getattr(self, '_tx3_epoch', 0) + 1
+            buf = self.plan.buf
+            idx, sc, views, off = [], [], [], 0
+            outs = []
+            for cw, scl in zip(self.planned, scales):
+                n32, T, n_pad, _ = cw.f32.shape
+                base = cw.f32.storage_offset() - buf.storage_offset()
+                i = torch.arange(base, base + cw.f32.numel(), device=buf.device).view(cw.f32.shape)
+                idx.append(i.view(n32, T, n_pad, 2, 16).permute(0, 3, 1, 2, 4).reshape(-1))
+                sc.append(torch.full((cw.f32.numel(),), scl, device=buf.device))
+                views.append((off, (2 * n32, T, n_pad, 2, 2, 8)))
+                off += 2 * cw.f32.numel()
+            self._tx3_idx, self._tx3_scale = torch.cat(idx), torch.cat(sc)
+            self._tx3 = torch.empty(off, device=buf.device, dtype=torch.float16)
+            for cw, scl, (o, shp) in zip(self.planned, scales, views):
+                n = 1
+                for d in shp:
+                    n *= d
+                outs.append((cw, self._tx3[o:o + n].view(shp), scl, False))
+            for cw, scl in zip([c for row in self.up for c in row], scales[len(self.planned):]):
+                outs.append((cw, torch.empty_like(_pack_x3_scaled(cw.f32, scl)[0]), scl, True))
+            self._tx3_layers = outs
+            self._tx3_bad = torch.zeros(1, device=buf.device, dtype=torch.int32)
+            self._tx3_version = None
+        if self._tx3_version != getattr(self, 'version', 0):
+            g = self.plan.buf[self._tx3_idx] * self._tx3_scale
+            hi = g.half()
+            lo = (g - hi.float()).half()
+            G = g.numel() // 8
+            self._tx3.view(G, 2, 8).copy_(torch.stack([hi.view(G, 8), lo.view(G, 8)], 1))
+            bad = g.abs().amax() >= 61440.0
+            for cw, view, scl, own in self._tx3_layers:
+                if own:  # upsampler phases (sums of taps, not in the gather plan): fixed-scale split of their own
+                    view.copy_(_pack_x3_scaled(cw.f32, scl)[0])
+                    bad = bad | (cw.f32.abs().amax() * scl >= 61440.0)
+            self._tx3_bad.copy_(bad.to(torch.int32).view(1))
+            self._tx3_version = getattr(self, 'version', 0)
+        for cw, view, scl, _ in self._tx3_layers:
+            cw._x3 = (view, scl)
+        return self._tx3_bad
+
+    def reset_train_x3(self):
+        self._tx3 = None
 
     def refresh(self):
         self.plan.refresh()

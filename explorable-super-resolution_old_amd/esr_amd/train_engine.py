@@ -224,8 +224,6 @@ class _Runner:
         self.stream = stream
         self.need_params, self.need_input = need_params, need_input
         self.split = split  # forward activations in the split-f16 layout (x3 forward)
-        if split and need_params:
-            raise RuntimeError('esr_amd: weight gradients need the exact-fp32 forward activations')
 
     def dgrad(self, bc, src, src_cp, src_coff, cin_k, h, w, dst, dst_cp, dst_base, accumulate, res=None):
         """dst[:, n0-dst_base ...] (+)= conv(src slice, rot180 W^T) for every output slice; `res` = (buf, cp, coff)
@@ -277,7 +275,8 @@ class _Runner:
         ntiles = self.B * ((h + 7) // 8) * ((w + 31) // 32)
         splits = max(1, min(WG_SPLITS_MAX, -(-1024 // chunks), ntiles))
         assert splits * bc.wg_n <= self.ws.partial.numel()
-        _lib.check(self.lib.esr_conv3x3_wgrad(inp.data_ptr(), in_cp, cin, up2, dout.data_ptr(), d_cp, d_coff,
+        _lib.check(self.lib.esr_conv3x3_wgrad(inp.data_ptr(), in_cp, cin, up2 | (2 if self.split else 0),
+                                              dout.data_ptr(), d_cp, d_coff,
                                               bc.cout, self.B, h, w, splits, self.ws.partial.data_ptr(), self.stream),
                    'wgrad')
         _lib.check(self.lib.esr_wgrad_reduce(self.ws.partial.data_ptr(), splits, bc.wg_n, scale,
@@ -455,28 +454,30 @@ class _GeneratorFn(torch.autograd.Function):
         pre_pad = cem is not None and cem.pre_pad
         m = int(cem.margins_LR) if pre_pad else 0
         Bn, _, h, w = x.shape
-        # Only the input gradient needed (Z optimisation, generator frozen): the forward runs in the x3 precision of
-        # inference and the backward reads its split-f16 activations; weight gradients need the exact-fp32 forward.
-        prec = 'f32'
-        if not any(p.requires_grad for p in params) and \
-                (getattr(net, 'esr_precision', None) or E.DEFAULT_PRECISION) == 'x3':
-            prec = 'x3'
+        # The forward runs in the model's precision (x3 by default, as inference); the backward reads the split-f16
+        # activations (weight-gradient inputs and LeakyReLU masks) and is exact fp32 itself.  Exception: weight
+        # gradients through the eval-mode CEM pre-pad use the exact-fp32 forward — the replicated margin holds whole
+        # lines of equal pre-activations, and an x3-rounded one near 0 flips its LeakyReLU slope along the line
+        # (measured 7.6e-4 L2 on a weight gradient, tests/test_gpu_train.py X3_GRAD_FLOOR).
+        prec = getattr(net, 'esr_precision', None) or E.DEFAULT_PRECISION
+        if pre_pad and any(p.requires_grad for p in params):
+            prec = 'f32'
         ws = _train_workspace(net, x.device, Bn, h + 2 * m, w + 2 * m, latent, prec)
         pk = E._packed(net, latent)  # parameter repack, outside any graph
-        if prec == 'x3':  # split-f16 weights built outside any graph (their scales are kernel arguments)
-            for cw in pk.planned + [c for row in pk.up for c in row]:
-                cw.x3()
+        bad = pk.train_x3() if prec == 'x3' else None  # x3 weights refreshed in place, fixed per-layer scales
 
         def fwd(xs):
             if prec == 'x3':
-                ws.overflow.zero_()
+                ws.overflow.copy_(bad)  # a weight outside its scale's safe range counts as an overflow
             return E._forward(net, xs, cem, prec, train_ws=ws)[0]
-        key = ('fwd', prec, tuple(x.shape), _cem_key(cem), id(pk), getattr(pk, 'version', 0))
+        key = ('fwd', prec, tuple(x.shape), _cem_key(cem), id(pk), getattr(pk, '_tx3_epoch', 0))
         xd = x.detach().contiguous()
         out, graphed = _run_graphed(ws, key, fwd, xd)
         split = prec == 'x3'
-        if split and int(ws.overflow.item()):  # an activation beyond the f16 range: redo in exact fp32
+        if split and int(ws.overflow.item()):  # an activation (or weight) beyond the f16 range: redo in exact fp32
             E.OVERFLOW_RERUNS += 1
+            if int(bad.item()):
+                pk.reset_train_x3()  # new scales at the next x3 forward
             ws = _train_workspace(net, x.device, Bn, h + 2 * m, w + 2 * m, latent, 'f32')
             out, graphed, split = E._forward(net, xd, cem, 'f32', train_ws=ws)[0], False, False
         ctx.net, ctx.cem, ctx.ws, ctx.latent, ctx.M, ctx.split = net, cem, ws, latent, E.SF * m, split

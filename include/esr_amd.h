@@ -146,10 +146,12 @@ int esr_x3_set_kernel(int32_t variant);
 /* Weight + bias gradient of a 3×3 zero-padded conv on the H×W output grid:
  *   partial[s][tap][ci][co] = Σ_{pixels of split s} in[p + tap][ci] · dout[p][co],   partial[s][9*cin_pad*cout_pad + co]
  *   = Σ dout[p][co] (bias), cin_pad = 32·ceil(cin/32), cout_pad = 32·ceil(cout/32).
- * in: padded NHWC fp32, channels [0, cin) (cin % 4 == 0); with up2 = 1 the conv input is the nearest-×2 upsampling of
- * an (H/2)×(W/2) `in` grid (the upconv of block.py:294-301).  dout: padded NHWC fp32 on the H×W grid, channels
- * [dout_coff, dout_coff + cout), cout <= 64.  Deterministic: reduce the `splits` partials with esr_wgrad_reduce. */
-int esr_conv3x3_wgrad(const float *in, int32_t in_cp, int32_t cin, int32_t up2, const float *dout, int32_t dout_cp,
+ * in: padded NHWC fp32, channels [0, cin) (cin % 4 == 0); flags bit 0 (up2): the conv input is the nearest-×2
+ * upsampling of an (H/2)×(W/2) `in` grid (the upconv of block.py:294-301); flags bit 1: `in` is in the split-f16
+ * layout (the x3 forward's activations; cin, in_cp % 8 == 0; 12-wave kernel only).  dout: padded NHWC fp32 on the
+ * H×W grid, channels [dout_coff, dout_coff + cout), cout <= 64.  Deterministic: reduce the `splits` partials with
+ * esr_wgrad_reduce. */
+int esr_conv3x3_wgrad(const float *in, int32_t in_cp, int32_t cin, int32_t flags, const float *dout, int32_t dout_cp,
                       int32_t dout_coff, int32_t cout, int32_t B, int32_t H, int32_t W, int32_t splits, float *partial,
                       esr_stream_t stream);
 /* out[i] = scale · Σ_s partial[s·n + i], fixed summation order. */

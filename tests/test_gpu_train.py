@@ -1,4 +1,5 @@
-"""GPU parity of the training path: HIP forward with retained activations + hand-written backward (exact fp32)
+"""GPU parity of the training path: HIP forward (x3 by default, or exact fp32) with retained activations + hand-written
+backward (exact fp32)
 against the reference's own training gradients (golden) and the oracle's autograd (all parameters).
 Forward outputs: normwise 1e-5.  Gradients: conftest.grad_parity — relative L2 error against the float64 oracle within
 5× that of the reference's own fp32 evaluation (floor 1e-4, a tenth of the 1e-3 bar; an indexing or layout bug
@@ -43,8 +44,12 @@ def test_training_gradients_vs_reference_golden(gpu_device, name):
         assert ok, (k, msg)
 
 
+@pytest.mark.parametrize('precision', ['x3', 'f32'])
 @pytest.mark.parametrize('latent', [False, True])
-def test_all_parameter_gradients_vs_oracle(gpu_device, latent):
+def test_all_parameter_gradients_vs_oracle(gpu_device, latent, precision):
+    """Every parameter gradient of a training step, with the forward in x3 (default: the backward reads split-f16
+    activations) and in exact fp32."""
+    from esr_amd import engine
     nb = 2
     net = esr_amd.RRDBNet(3, 3, 64, nb, latent_input='all_layers_HR_downscaled' if latent else None,
                           num_latent_channels=3 if latent else 0)
@@ -52,6 +57,7 @@ def test_all_parameter_gradients_vs_oracle(gpu_device, latent):
     sd = model.state_dict()
     params = seeded_params([(k, tuple(v.shape)) for k, v in sd.items()], 51, w_scale=0.7)
     model = _model(nb, latent, params, gpu_device)
+    engine.set_precision(model, precision)
     B, h, w = 2, 10, 14
     lr, z = seeded_inputs(52, (B, 3, h, w), (B, 3, 4 * h, 4 * w) if latent else None, z_mode='pixel')
     x = torch.from_numpy(lr)
@@ -147,14 +153,27 @@ def test_z_gradients_vs_reference_golden(gpu_device, name):
         assert ok, (k, msg)
 
 
+# Gradient floor of conftest.grad_parity for an x3 forward: its activations carry ~2^-21 relative rounding (fp32:
+# 2^-24), so a LeakyReLU pre-activation within that of 0 takes the other slope about 8x as often as in an fp32 forward.
+# In the eval-mode CEM pre-pad margin (a replicated border: whole lines of equal pre-activations) such flips moved
+# weight gradients by up to 7.6e-4 L2, so parameter gradients with pre-pad use the exact-fp32 forward (train_engine);
+# the x3 cases below are held to 5e-4, the fp32 ones to the default 1e-4, all under the 1e-3 parity bar (an indexing
+# bug shows as O(1e-1)).
+X3_GRAD_FLOOR = 5e-4
+
+
+@pytest.mark.parametrize('precision', ['x3', 'f32'])
 @pytest.mark.parametrize('mode', ['eval', 'train'])
-def test_input_and_parameter_gradients_together_vs_oracle(gpu_device, mode):
+def test_input_and_parameter_gradients_together_vs_oracle(gpu_device, mode, precision):
     """Both gradient kinds in one backward (nb=2, latent, pixel Z) against the oracle's autograd."""
+    from esr_amd import engine
     nb = 2
     net = esr_amd.RRDBNet(3, 3, 64, nb, latent_input='all_layers_HR_downscaled', num_latent_channels=3)
     model = C.CEMnet(C.Get_CEM_Config(4)).WrapArchitecture_PyTorch(net)
     params = seeded_params([(k, tuple(v.shape)) for k, v in model.state_dict().items()], 61, w_scale=0.7)
     model = _model(nb, True, params, gpu_device).train(mode == 'train')
+    engine.set_precision(model, precision)
+    floor = X3_GRAD_FLOOR if precision == 'x3' else 1e-4
     B, h, w = 2, 12, 10
     lr, z = seeded_inputs(62, (B, 3, h, w), (B, 3, 4 * h, 4 * w), z_mode='pixel')
     zt = torch.from_numpy(z).to(gpu_device).requires_grad_(True)
@@ -163,12 +182,12 @@ def test_input_and_parameter_gradients_together_vs_oracle(gpu_device, mode):
     (out * R.to(gpu_device)).sum().backward()
     exact, base = (oracle_grads(params, lr, z, R, nb, True, O.cem_design(4), mode == 'eval', dt)
                    for dt in (torch.float64, torch.float32))
-    ok, msg = grad_parity(zt.grad.cpu(), exact['dz'], base['dz'])
+    ok, msg = grad_parity(zt.grad.cpu(), exact['dz'], base['dz'], floor=floor)
     assert ok, msg
     for n, p in model.named_parameters():
         if p.requires_grad:
             k = 'param:' + n[len('generated_image_model.'):]
-            ok, msg = grad_parity(p.grad.cpu(), exact[k], base[k])
+            ok, msg = grad_parity(p.grad.cpu(), exact[k], base[k], floor=floor)
             assert ok, (n, msg)
 
 
