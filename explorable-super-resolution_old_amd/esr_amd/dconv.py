@@ -18,6 +18,7 @@ import ctypes
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from . import _lib
 
@@ -210,6 +211,9 @@ class HipConv2d(nn.Conv2d):
         if k[0] != k[1] or s[0] != s[1] or p[0] != p[1] or self.dilation != (1, 1) or self.groups != 1 or \
                 self.padding_mode != 'zeros' or k[0] * k[1] > MAX_TAPS:
             raise NotImplementedError('HipConv2d: square zero-padded dense convolutions with <= %d taps' % MAX_TAPS)
+        # few input channels (conv0: 3 channels x 9 taps = 27): gather the taps into channels once and run a 1x1 conv,
+        # one 32-wide K step instead of one (mostly zero) K step per tap
+        self._im2col = s[0] == 1 and self.in_channels * k[0] * k[1] <= 32 and self.in_channels < 8
 
     def forward(self, x):
         _check_dev(x)
@@ -217,5 +221,15 @@ class HipConv2d(nn.Conv2d):
             xh = x.permute(0, 2, 3, 1)  # a view: NHWC storage already
         else:
             xh = _ToNHWC.apply(x)
-        y = DConvFn.apply(xh, self.weight, self.bias, self.kernel_size[0], self.stride[0], self.padding[0])
+        k, p = self.kernel_size[0], self.padding[0]
+        if self._im2col:
+            B, H, W, C = xh.shape
+            Ho, Wo = out_size(H, k, 1, p), out_size(W, k, 1, p)
+            xp = F.pad(xh, (0, 0, p, p, p, p))
+            cols = torch.cat([xp[:, ky:ky + Ho, kx:kx + Wo, :] for ky in range(k) for kx in range(k)] +
+                             [xh.new_zeros(B, Ho, Wo, 32 - k * k * C)], dim=3)  # channel (ky*k + kx)*C + c
+            w1 = F.pad(self.weight.permute(0, 2, 3, 1).reshape(self.out_channels, k * k * C), (0, 32 - k * k * C))
+            y = DConvFn.apply(cols, w1.view(self.out_channels, 32, 1, 1), self.bias, 1, 1, 0)
+        else:
+            y = DConvFn.apply(xh, self.weight, self.bias, k, self.stride[0], p)
         return y.permute(0, 3, 1, 2)
