@@ -148,23 +148,32 @@ __global__ __launch_bounds__(256, 1) void wgrad_kernel(WgradParams p) {
 }
 
 // wgrad2: the same GEMM with 12 waves (3 per SIMD) instead of 4, so LDS and MFMA latencies of one wave hide behind
-// the others.  Wave w owns the three taps of tap column tg = w % 3 (dy = 0..2, dx = tg) for one output-channel tile
-// ct and one pixel class q (NCT = 1: four classes; NCT = 2: ct = (w/3) & 1 and two classes), i.e. 3 accumulators;
-// per pixel pair it reads one output-gradient fragment (reused by its 3 taps) and one input fragment per tap.  The
-// next pixel tile's global loads are issued into registers before the current tile is consumed.  The pixel classes
-// are summed through LDS at the end (fixed order).  blockIdx is remapped so that the chunks of one split run on the
-// same XCD and share its L2 for the output-gradient tile.
-constexpr int W2_NT = 768;
-constexpr int W2_IN_F = WT_HY * WT_HX * WT_IP, W2_D_F = WT_TH * WT_TW * WT_DP;
-constexpr int W2_IN_V4 = WT_HY * WT_HX * 8, W2_D_V4 = WT_TH * WT_TW * 16;
-constexpr int W2_IN_PT = (W2_IN_V4 + W2_NT - 1) / W2_NT, W2_D_PT = (W2_D_V4 + W2_NT - 1) / W2_NT;
-static_assert(W2_IN_PT % 2 == 0 && (W2_IN_V4 / 2 + W2_NT - 1) / W2_NT <= W2_IN_PT / 2, "split staging layout");
+// the others.  Wave w owns the three taps of tap column tg = w % 3 (dy = 0..2, dx = tg) for one output-channel tile ct
+// and one pixel class q (N = 32: 4 classes; N = 64: 2 channel tiles x 2 classes), i.e. 3 accumulators; per pixel pair
+// it reads one output-gradient fragment (reused by its 3 taps) and one input fragment per tap.  LDS rows are unpadded
+// (128 B per 32 channels: conflict-free for these lane patterns).  (Measured: 6-wave workgroups for N = 32, two per CU,
+// were 10-15 % slower — the SIMDs hold 2 + 2 + 1 + 1 waves of one workgroup.)  The next pixel tile's global loads are
+// issued into registers before the current tile is consumed.  The pixel classes are summed through LDS at the end
+// (fixed order).  blockIdx is remapped so that the chunks of one split run on the same XCD and share its L2 for the
+// output gradient.
+constexpr int W2_IP = 32;  // LDS pitch of a staged input pixel (32 channels, no padding)
+
+template <int NCT>
+struct W2 {
+    static constexpr int NWV = 12, NT = 64 * NWV, NQ = 4 / NCT;
+    static constexpr int DP = 32 * NCT;  // LDS pitch of a staged output-gradient pixel
+    static constexpr int IN_F = WT_HY * WT_HX * W2_IP, D_F = WT_TH * WT_TW * DP;
+    static constexpr int IN_V4 = WT_HY * WT_HX * 8, D_V4 = WT_TH * WT_TW * 8 * NCT;
+    static constexpr int IN_PT = 2 * ((IN_V4 / 2 + NT - 1) / NT), D_PT = (D_V4 + NT - 1) / NT;
+};
 
 template <int NCT, bool SPLIT>
-__global__ __launch_bounds__(W2_NT, 1) void wgrad2_kernel(WgradParams p) {
-    constexpr int NQ = 4 / NCT;  // pixel classes
-    __shared__ __attribute__((aligned(16))) float smem[W2_IN_F + W2_D_F];
-    float *s_in = smem, *s_d = smem + W2_IN_F;
+__global__ __launch_bounds__(W2<NCT>::NT, 1) void wgrad2_kernel(WgradParams p) {
+    using C = W2<NCT>;
+    constexpr int NT_ = C::NT, NQ = C::NQ, DP = C::DP;
+    static_assert(C::IN_V4 <= C::IN_PT * NT_, "input staging");
+    __shared__ __attribute__((aligned(16))) float smem[C::IN_F + C::D_F];
+    float *s_in = smem, *s_d = smem + C::IN_F;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hl = lane >> 5, ml = lane & 31;
     const int tg = wave % 3, r4 = wave / 3;
     const int ct = NCT == 2 ? (r4 & 1) : 0, q = NCT == 2 ? (r4 >> 1) : r4;
@@ -190,20 +199,20 @@ __global__ __launch_bounds__(W2_NT, 1) void wgrad2_kernel(WgradParams p) {
         for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
     float bsum = 0.f;
 
-    f32x4 rin[W2_IN_PT], rd[W2_D_PT];
+    f32x4 rin[C::IN_PT], rd[C::D_PT];
     auto load_tile = [&](int t) {
         const int tx = t % p.tiles_x, ty = (t / p.tiles_x) % p.tiles_y, b = t / (p.tiles_x * p.tiles_y);
         const int y0 = ty * WT_TH, x0 = tx * WT_TW;
         if (SPLIT) {
-            // one 8-channel group (32 B: hi[8], lo[8]) per item, 4 groups per pixel, two registers quads per item
+            // one 8-channel group (32 B: hi[8], lo[8]) per item, 4 groups per pixel, two register quads per item
 #pragma unroll
-            for (int k = 0; k < W2_IN_PT / 2; ++k) {
-                const int idx = tid + k * W2_NT;
+            for (int k = 0; k < C::IN_PT / 2; ++k) {
+                const int idx = tid + k * NT_;
                 const int px = idx >> 2, g = idx & 3;
                 const int hy = px / WT_HX, hx = px - hy * WT_HX;
                 const int Y = y0 + hy - 1, X = x0 + hx - 1;
                 f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = {0.f, 0.f, 0.f, 0.f};
-                if (idx < W2_IN_V4 / 2 && Y >= 0 && Y < p.H && X >= 0 && X < p.W && g * 8 < kc) {
+                if (idx < C::IN_V4 / 2 && Y >= 0 && Y < p.H && X >= 0 && X < p.W && g * 8 < kc) {
                     const int sy = p.up2 ? Y / 2 : Y, sx = p.up2 ? X / 2 : X;
                     const f16x8 *src = reinterpret_cast<const f16x8 *>(
                         reinterpret_cast<const unsigned char *>(p.in) +
@@ -220,13 +229,13 @@ __global__ __launch_bounds__(W2_NT, 1) void wgrad2_kernel(WgradParams p) {
             }
         } else {
 #pragma unroll
-            for (int k = 0; k < W2_IN_PT; ++k) {
-                const int idx = tid + k * W2_NT;
+            for (int k = 0; k < C::IN_PT; ++k) {
+                const int idx = tid + k * NT_;
                 const int px = idx >> 3, c4 = idx & 7;
                 const int hy = px / WT_HX, hx = px - hy * WT_HX;
                 const int Y = y0 + hy - 1, X = x0 + hx - 1;
                 f32x4 v = {0.f, 0.f, 0.f, 0.f};
-                if (idx < W2_IN_V4 && Y >= 0 && Y < p.H && X >= 0 && X < p.W && c4 * 4 < kc) {
+                if (idx < C::IN_V4 && Y >= 0 && Y < p.H && X >= 0 && X < p.W && c4 * 4 < kc) {
                     const int sy = p.up2 ? Y / 2 : Y, sx = p.up2 ? X / 2 : X;
                     v = *reinterpret_cast<const f32x4 *>(
                         p.in + (((long long)b * (Hi + 2) + sy + 1) * (Wi + 2) + sx + 1) * p.in_cp + c0 + c4 * 4);
@@ -235,12 +244,12 @@ __global__ __launch_bounds__(W2_NT, 1) void wgrad2_kernel(WgradParams p) {
             }
         }
 #pragma unroll
-        for (int k = 0; k < W2_D_PT; ++k) {
-            const int idx = tid + k * W2_NT;
-            const int px = idx >> 4, c4 = idx & 15;
+        for (int k = 0; k < C::D_PT; ++k) {
+            const int idx = tid + k * NT_;
+            const int px = idx / (8 * NCT), c4 = idx % (8 * NCT);
             const int y = y0 + (px >> 5), x = x0 + (px & 31);
             f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            if (idx < W2_D_V4 && c4 < 8 * NCT && y < p.H && x < p.W && c4 * 4 < p.cout) {
+            if (idx < C::D_V4 && y < p.H && x < p.W && c4 * 4 < p.cout) {
                 const float *src = p.dout + (((long long)b * (p.H + 2) + y + 1) * (p.W + 2) + x + 1) * p.dout_cp +
                                    p.dout_coff + c4 * 4;
                 if (vec_d && c4 * 4 + 4 <= p.cout) {
@@ -256,29 +265,30 @@ __global__ __launch_bounds__(W2_NT, 1) void wgrad2_kernel(WgradParams p) {
     auto store_tile = [&]() {
         if (SPLIT) {
 #pragma unroll
-            for (int k = 0; k < W2_IN_PT / 2; ++k) {
-                const int idx = tid + k * W2_NT;
-                if (idx < W2_IN_V4 / 2) {
-                    float *dst = s_in + (idx >> 2) * WT_IP + (idx & 3) * 8;
+            for (int k = 0; k < C::IN_PT / 2; ++k) {
+                const int idx = tid + k * NT_;
+                if (idx < C::IN_V4 / 2) {
+                    float *dst = s_in + (idx >> 2) * W2_IP + (idx & 3) * 8;
                     *reinterpret_cast<f32x4 *>(dst) = rin[2 * k];
                     *reinterpret_cast<f32x4 *>(dst + 4) = rin[2 * k + 1];
                 }
             }
         } else {
 #pragma unroll
-            for (int k = 0; k < W2_IN_PT; ++k) {
-                const int idx = tid + k * W2_NT;
-                if (idx < W2_IN_V4) *reinterpret_cast<f32x4 *>(s_in + (idx >> 3) * WT_IP + (idx & 7) * 4) = rin[k];
+            for (int k = 0; k < C::IN_PT; ++k) {
+                const int idx = tid + k * NT_;
+                if (idx < C::IN_V4) *reinterpret_cast<f32x4 *>(s_in + (idx >> 3) * W2_IP + (idx & 7) * 4) = rin[k];
             }
         }
 #pragma unroll
-        for (int k = 0; k < W2_D_PT; ++k) {
-            const int idx = tid + k * W2_NT;
-            if (idx < W2_D_V4 && (idx & 15) < 8 * NCT)
-                *reinterpret_cast<f32x4 *>(s_d + (idx >> 4) * WT_DP + (idx & 15) * 4) = rd[k];
+        for (int k = 0; k < C::D_PT; ++k) {
+            const int idx = tid + k * NT_;
+            if (idx < C::D_V4) *reinterpret_cast<f32x4 *>(s_d + idx * 4) = rd[k];  // [pixel][DP] is dense
         }
     };
 
+    // bias partial (chunk-0 workgroups): thread (channel tid % DP, pixel phase tid / DP) for tid < 256
+    constexpr int BPH = 256 / DP;
     if (t_begin < t_end) load_tile(t_begin);
     for (int t = t_begin; t < t_end; ++t) {
         __syncthreads();
@@ -286,23 +296,23 @@ __global__ __launch_bounds__(W2_NT, 1) void wgrad2_kernel(WgradParams p) {
         __syncthreads();
         if (t + 1 < t_end) load_tile(t + 1);
         if (chunk == 0 && tid < 256)
-            for (int px = tid >> 6; px < WT_TH * WT_TW; px += 4) bsum += s_d[px * WT_DP + (tid & 63)];
+            for (int px = tid / DP; px < WT_TH * WT_TW; px += BPH) bsum += s_d[px * DP + tid % DP];
         // pixel pairs s = NQ*k + q; lane half hl takes pixel 2s + hl
 #pragma unroll 4
         for (int k = 0; k < WT_TH * WT_TW / (2 * NQ); ++k) {
             const int px = 2 * (NQ * k + q) + hl;
             const int py = px >> 5, pxx = px & 31;
-            const float bb = s_d[px * WT_DP + ct * 32 + ml];
+            const float bb = s_d[px * DP + ct * 32 + ml];
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
-                const float a = s_in[((py + j) * WT_HX + pxx + tg) * WT_IP + ml];
+                const float a = s_in[((py + j) * WT_HX + pxx + tg) * W2_IP + ml];
                 acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bb, acc[j], 0, 0, 0);
             }
         }
     }
     // sum the pixel classes into class 0 (fixed order 1, 2, ...), through LDS
     constexpr int PER_WAVE = 3 * 16 * 64;
-    static_assert(3 * NCT * PER_WAVE <= W2_IN_F + W2_D_F, "class reduction does not fit in LDS");
+    static_assert(3 * NCT * PER_WAVE <= C::IN_F + C::D_F, "class reduction does not fit in LDS");
     const int slot = tg * NCT + ct;
     for (int r = 1; r < NQ; ++r) {
         __syncthreads();
@@ -338,7 +348,7 @@ __global__ __launch_bounds__(W2_NT, 1) void wgrad2_kernel(WgradParams p) {
         __syncthreads();
         if (tid < p.cout_pad) {
             float v = 0.f;
-            if (tid < 64) v = smem[tid] + smem[64 + tid] + smem[128 + tid] + smem[192 + tid];
+            for (int ph = 0; ph < BPH; ++ph) v += smem[ph * DP + tid];
             part[9LL * p.cin_pad * p.cout_pad + tid] = v;
         }
     }
@@ -542,16 +552,17 @@ extern "C" int esr_conv3x3_wgrad(const float *in, int32_t in_cp, int32_t cin, in
     const unsigned total = (unsigned)(p.cin_pad / 32 * splits);
     if (g_wgrad_kernel == 1) {
         const unsigned grid = 8 * ((total + 7) / 8);  // whole XCD rounds; the surplus workgroups exit at once
+        const hipStream_t st = (hipStream_t)stream;
         if (split) {
             if (p.cout_pad == 64)
-                hipLaunchKernelGGL((wgrad2_kernel<2, true>), dim3(grid), dim3(W2_NT), 0, (hipStream_t)stream, p);
+                hipLaunchKernelGGL((wgrad2_kernel<2, true>), dim3(grid), dim3(W2<2>::NT), 0, st, p);
             else
-                hipLaunchKernelGGL((wgrad2_kernel<1, true>), dim3(grid), dim3(W2_NT), 0, (hipStream_t)stream, p);
+                hipLaunchKernelGGL((wgrad2_kernel<1, true>), dim3(grid), dim3(W2<1>::NT), 0, st, p);
         } else {
             if (p.cout_pad == 64)
-                hipLaunchKernelGGL((wgrad2_kernel<2, false>), dim3(grid), dim3(W2_NT), 0, (hipStream_t)stream, p);
+                hipLaunchKernelGGL((wgrad2_kernel<2, false>), dim3(grid), dim3(W2<2>::NT), 0, st, p);
             else
-                hipLaunchKernelGGL((wgrad2_kernel<1, false>), dim3(grid), dim3(W2_NT), 0, (hipStream_t)stream, p);
+                hipLaunchKernelGGL((wgrad2_kernel<1, false>), dim3(grid), dim3(W2<1>::NT), 0, st, p);
         }
     } else {
         hipLaunchKernelGGL(wgrad_kernel, dim3(total), dim3(256), 0, (hipStream_t)stream, p);
