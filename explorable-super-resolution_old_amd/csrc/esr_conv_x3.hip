@@ -201,7 +201,43 @@ __device__ __forceinline__ bool store_tile(const X3Params &p, const float *s_ep,
     return store_px<N, NTHR, TH * TWF>(p, s_ep, 0, r_first, x0, tw, nq, tid);
 }
 
-template <int NT, int TS>
+template <int VM>
+__device__ __forceinline__ void wait_vm_lgkm0() {
+    static_assert(VM >= 0 && VM < 64, "vmcnt");
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(VM) : "memory");
+}
+
+// LDS byte address of a pointer into the kernel's __shared__ array
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+
+// One 16-byte LDS read the compiler does not track: the caller waits for it with lgkm_wait
+__device__ __forceinline__ f16x8 ds_read16(uint32_t a) {
+    f16x8 r;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(a));
+    return r;
+}
+
+template <int OFF>
+__device__ __forceinline__ f16x8 ds_read16o(uint32_t a, int tap) {
+    f16x8 r;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF));
+    (void)tap;
+    return r;
+}
+
+// s_waitcnt lgkmcnt(N) that the K fragments pass through (the empty statements after it are ordered behind it), so
+// no use of them is scheduled before the wait
+template <int N, int K>
+__device__ __forceinline__ void lgkm_wait(f16x8 (&f)[K]) {
+    static_assert(N >= 0 && N < 16, "lgkmcnt");
+    asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(f[0]) : "i"(N));
+#pragma unroll
+    for (int i = 1; i < K; ++i) asm volatile("" : "+v"(f[i]));
+}
+
+template <int NT, int TS, bool ASMRD = (NT == 1)>
 __global__ __launch_bounds__(NTHR, 1) void conv_x3_kernel(X3Params p) {
     constexpr int T = TS * TS;
     constexpr int N = NT * 32;
@@ -303,7 +339,58 @@ __global__ __launch_bounds__(NTHR, 1) void conv_x3_kernel(X3Params p) {
     // Fragments are read X3_PF taps ahead of their MFMAs (X3_PF + 1 register sets): with one tap of lookahead the
     // reads of 8 waves (6-8 ds_read_b128 each) were covered by only ~5 of the wave's own MFMAs, and LDS latency
     // added to the matrix time instead of hiding under it.
+    // Explicit ds_read_b128 fragment reads one tap ahead with counted lgkmcnt waits (see the ring kernel's
+    // compute_asm); MFMAs unpredicated, the order per accumulator unchanged.  N = 32 only (ASMRD default): at N = 64 the
+    // two register sets of 8 fragments next to 64 accumulator registers exceed the 256-VGPR budget and spill.
+    auto compute_asm = [&](const unsigned char *s_in, const unsigned char *s_w) {
+        constexpr int NR = 4 + 2 * NT;  // [ah0, al0, ah1, al1, bh0, bl0, (bh1, bl1)]
+        const uint32_t bi = lds_addr(s_in), bw = lds_addr(s_w);
+        f16x8 f[2][NR];
+        auto ld = [&](int tap, int buf) {
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                f[buf][2 * mt] = ds_read16(bi + aoff[tap][mt][0]);
+                f[buf][2 * mt + 1] = ds_read16(bi + aoff[tap][mt][1]);
+            }
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                f[buf][4 + 2 * nt] = ds_read16(bw + boff0 + (tap * N + nt * 32) * REC);
+                f[buf][5 + 2 * nt] = ds_read16(bw + boff1 + (tap * N + nt * 32) * REC);
+            }
+        };
+        ld(0, 0);
+#pragma unroll
+        for (int tap = 0; tap < T; ++tap) {
+            const int cb = tap & 1;
+            if (tap + 1 < T) {
+                ld(tap + 1, cb ^ 1);
+                lgkm_wait<NR>(f[cb]);
+            } else {
+                lgkm_wait<0>(f[cb]);
+            }
+            f16x8 *q = f[cb];
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(q[2 * mt + 1], q[4 + 2 * nt], acc[mt][nt], 0, 0, 0);
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(q[2 * mt], q[5 + 2 * nt], acc[mt][nt], 0, 0, 0);
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(q[2 * mt], q[4 + 2 * nt], acc[mt][nt], 0, 0, 0);
+        }
+    };
     auto compute = [&](const unsigned char *s_in, const unsigned char *s_w) {
+        if constexpr (ASMRD) {
+            compute_asm(s_in, s_w);
+            return;
+        }
         constexpr int NBUF = X3_PF + 1;
         f16x8 ah[NBUF][2], al[NBUF][2], bh[NBUF][NT], bl[NBUF][NT];
         auto ld = [&](int tap, int buf) {
@@ -343,12 +430,15 @@ __global__ __launch_bounds__(NTHR, 1) void conv_x3_kernel(X3Params p) {
         }
     };
 
+    // the explicit vmcnt(0) before each barrier: compute_asm's reads are invisible to the compiler's LDS-DMA tracking
     dma(0, 0);
     for (int j = 0; j < nchunk; j += 2) {
+        wait_vm_lgkm0<0>();
         __syncthreads();
         if (j + 1 < nchunk) dma(j + 1, 1);
         if (mvalid[0]) compute(lds, lds + 2 * IN_B);
         if (j + 1 >= nchunk) break;
+        wait_vm_lgkm0<0>();
         __syncthreads();
         if (j + 2 < nchunk) dma(j + 2, 0);
         if (mvalid[0]) compute(lds + IN_B, lds + 2 * IN_B + W_B);
@@ -386,11 +476,6 @@ __global__ __launch_bounds__(NTHR, 1) void conv_x3_kernel(X3Params p) {
 // Per accumulator the MFMA sequence is the classic kernel's, so the two kernels agree bit for bit.
 constexpr int IN_PIECES = IN_RECS / 16;  // 1-KB LDS-DMA wave-instructions per input stage (39)
 
-template <int VM>
-__device__ __forceinline__ void wait_vm_lgkm0() {
-    static_assert(VM >= 0 && VM < 64, "vmcnt");
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(VM) : "memory");
-}
 
 __device__ __forceinline__ void raw_barrier() {
     asm volatile("" ::: "memory");
@@ -400,7 +485,9 @@ __device__ __forceinline__ void raw_barrier() {
 
 // DBG bits (diagnostic builds, esr_x3_set_kernel >= 3; outputs are garbage): 1 = no LDS-DMA in the main loop,
 // 2 = no compute, 4 = fragment reads but no MFMAs, 8 = no barriers, 16 = slot 0 always (immediate LDS offsets),
-// 32 = MFMAs not predicated on mvalid, 64 = no epilogue stores (accumulators kept live), 128 = no epilogue at all.
+// 32 = MFMAs not predicated on mvalid, 64 = no epilogue stores (accumulators kept live), 128 = no epilogue at all;
+// 256 (valid outputs) = the compiler-scheduled fragment reads instead of compute_asm's (the pre-asm kernel, for A/B),
+// 512 = compute_asm with lane-constant A addresses (timing probe for the address VALU work).
 template <int NIN, bool STAG, int DBG = 0>
 __global__ __launch_bounds__(NTHR, 1) void conv_x3_ring_kernel(X3Params p) {
     constexpr int T = 9;
@@ -510,7 +597,58 @@ __global__ __launch_bounds__(NTHR, 1) void conv_x3_ring_kernel(X3Params p) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[t][mt][r] = 0.f;
 
+    // Fragment reads as explicit ds_read_b128 with COUNTED lgkmcnt waits: tap t+1's six reads are issued before tap
+    // t's six MFMAs and the wait before those MFMAs leaves them in flight.  (The compiler's own schedule of the plain
+    // loads sinks each read next to its MFMA and drains with lgkmcnt(0), which serialises LDS latency and the matrix
+    // pipe.)  The MFMAs are not predicated on mvalid[1]: an invalid M-tile reads pixel 0's fragments and its
+    // accumulator is never stored, and the wave with both M-tiles valid sets the barrier cadence anyway.
+    auto compute_asm = [&](const unsigned char *s_in, const unsigned char *s_w, f32x16(&ac)[2]) {
+        const uint32_t bi = lds_addr(s_in), bw = lds_addr(s_w);
+        f16x8 f[2][6];  // [buf][ah0, al0, ah1, al1, bh, bl]
+        uint32_t a0[2][2];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+            a0[mt][0] = bi + aoff[0][mt][0];
+            a0[mt][1] = bi + aoff[0][mt][1];
+        }
+        auto ld = [&](int tap, int buf) {
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                if constexpr ((DBG & 512) != 0) {  // timing probe: lane-constant A addresses (wrong outputs)
+                    f[buf][2 * mt] = ds_read16o<0>(a0[mt][0], tap);
+                    f[buf][2 * mt + 1] = ds_read16o<0>(a0[mt][1], tap);
+                } else {
+                    f[buf][2 * mt] = ds_read16(bi + aoff[tap][mt][0]);
+                    f[buf][2 * mt + 1] = ds_read16(bi + aoff[tap][mt][1]);
+                }
+            }
+            f[buf][4] = ds_read16(bw + boff0 + tap * N * REC);
+            f[buf][5] = ds_read16(bw + boff1 + tap * N * REC);
+        };
+        ld(0, 0);
+#pragma unroll
+        for (int tap = 0; tap < T; ++tap) {
+            const int cb = tap & 1;
+            if (tap + 1 < T) {
+                ld(tap + 1, cb ^ 1);
+                lgkm_wait<6>(f[cb]);
+            } else {
+                lgkm_wait<0>(f[cb]);
+            }
+            f16x8 *q = f[cb];
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) ac[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(q[2 * mt + 1], q[4], ac[mt], 0, 0, 0);
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) ac[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(q[2 * mt], q[5], ac[mt], 0, 0, 0);
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) ac[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(q[2 * mt], q[4], ac[mt], 0, 0, 0);
+        }
+    };
     auto compute = [&](const unsigned char *s_in, const unsigned char *s_w, f32x16(&ac)[2]) {
+        if constexpr ((DBG & (4 | 32 | 256)) == 0) {
+            compute_asm(s_in, s_w, ac);
+            return;
+        }
         f16x8 ah[2][2], al[2][2], bh[2], bl[2];
         auto ld = [&](int tap, int buf) {
 #pragma unroll
@@ -867,8 +1005,10 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
     p.overflow = overflow;
     p.o = *o;
     const dim3 block(NTHR);
-    // Ring kernel for N <= 32 when its halved grid still fills the chip: a ring workgroup does two tiles in ~1.8x the
-    // time of a classic one, so compare ceil(pairs/CUs) * 1.8 with ceil(tiles/CUs) (measured at config 2 / 3 shapes).
+    // Ring kernel for N <= 32 when its halved grid still fills the chip: with both kernels on counted-wait fragment
+    // reads a ring workgroup does two tiles in ~2.0x the time of a classic one (tools/x3_ring_ab.py at config 2 / 3
+    // shapes: classic 1-3 % faster at 148², 20 % at 96²), so the ring only pays where the classic grid's last round of
+    // workgroups is nearly empty: compare ceil(pairs/CUs) * 2 with ceil(tiles/CUs).
     const int tiles = p.tiles_x * p.tiles_y, pairs = p.tiles_x * ((p.tiles_y + 1) / 2);
     static int n_cu = 0;
     if (!n_cu) {
@@ -876,14 +1016,14 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
         n_cu = (hipGetDevice(&dev) == hipSuccess &&
                 hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
     }
-    const bool ring_pays = 18 * ((pairs + n_cu - 1) / n_cu) < 10 * ((tiles + n_cu - 1) / n_cu);
+    const bool ring_pays = 20 * ((pairs + n_cu - 1) / n_cu) < 10 * ((tiles + n_cu - 1) / n_cu);
     if (taps_side == 3 && cout <= 32 && (g_x3_kernel == 16 || g_x3_kernel == 17)) {
         const dim3 gridp((unsigned)min(pairs, n_cu));
         if (g_x3_kernel == 16) hipLaunchKernelGGL((conv_x3_pring_kernel<1>), gridp, block, 0, stream, p);
         else hipLaunchKernelGGL((conv_x3_pring_kernel<2>), gridp, block, 0, stream, p);
         return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
     }
-    if (taps_side == 3 && cout <= 32 && (g_x3_kernel >= 2 || (g_x3_kernel == 1 && ring_pays))) {
+    if (taps_side == 3 && cout <= 32 && ((g_x3_kernel >= 2 && g_x3_kernel != 20) || (g_x3_kernel == 1 && ring_pays))) {
         const dim3 grid2((unsigned)pairs);
 #define RING_DBG(v, bits) \
     case v: hipLaunchKernelGGL((conv_x3_ring_kernel<3, true, bits>), grid2, block, 0, stream, p); break;
@@ -901,13 +1041,18 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
         RING_DBG(12, 4 | 1 | 128)
         RING_DBG(13, 64)
         RING_DBG(14, 2 | 128)
+        case 18: hipLaunchKernelGGL((conv_x3_ring_kernel<3, false, 256>), grid2, block, 0, stream, p); break;
+        case 19: hipLaunchKernelGGL((conv_x3_ring_kernel<3, false, 512>), grid2, block, 0, stream, p); break;
         default: hipLaunchKernelGGL((conv_x3_ring_kernel<3, false>), grid2, block, 0, stream, p);
         }
 #undef RING_DBG
         return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
     }
     const dim3 grid((unsigned)(p.tiles_x * p.tiles_y));
-    if (taps_side == 3) {
+    if (taps_side == 3 && g_x3_kernel == 20) {  // A/B: the classic kernel with compiler-scheduled fragment reads
+        if (cout > 32) hipLaunchKernelGGL((conv_x3_kernel<2, 3, false>), grid, block, 0, stream, p);
+        else hipLaunchKernelGGL((conv_x3_kernel<1, 3, false>), grid, block, 0, stream, p);
+    } else if (taps_side == 3) {
         if (cout > 32) hipLaunchKernelGGL((conv_x3_kernel<2, 3>), grid, block, 0, stream, p);
         else hipLaunchKernelGGL((conv_x3_kernel<1, 3>), grid, block, 0, stream, p);
     } else {
@@ -927,7 +1072,7 @@ extern "C" int esr_conv3x3_fwd_x3(const void *in, int32_t B, int32_t H, int32_t 
 }
 
 extern "C" int esr_x3_set_kernel(int32_t variant) {
-    if (variant < 0 || variant > 17) return ESR_EINVAL;
+    if (variant < 0 || variant > 20) return ESR_EINVAL;
     const int prev = g_x3_kernel;
     g_x3_kernel = variant;
     return prev;

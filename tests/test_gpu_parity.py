@@ -294,7 +294,9 @@ def test_x3_ring_kernel_bitwise_equals_classic(gpu_device, cin, cout, B, H, W):
     rs = engine.to_split(_padded(B, H, W, 40, 40, gpu_device, 23))
     outs = []
     try:
-        for variant in (0, 2, 17):  # classic only, ring always, persistent ring always
+        # classic only, ring always, persistent ring always, and ring / classic with the compiler-scheduled fragment
+        # reads (the explicit counted-wait reads must not change a bit)
+        for variant in (0, 2, 17, 18, 20):
             lib.esr_x3_set_kernel(variant)
             out = torch.zeros(B, H + 2, W + 2, 40, device=gpu_device)
             out2 = torch.zeros(B, H + 2, W + 2, 32, device=gpu_device)
@@ -306,7 +308,7 @@ def test_x3_ring_kernel_bitwise_equals_classic(gpu_device, cin, cout, B, H, W):
             outs.append((out, out2))
     finally:
         lib.esr_x3_set_kernel(1)
-    for k in (1, 2):
+    for k in range(1, len(outs)):
         assert torch.equal(outs[0][0], outs[k][0]) and torch.equal(outs[0][1], outs[k][1]), k
     ref = F.leaky_relu(F.conv2d(_nchw(engine.from_split(xs), 0, cin), w.double(), b.cpu().double(), padding=1), 0.2)
     ref = 0.2 * ref + _nchw(engine.from_split(rs), 0, cout)
