@@ -237,7 +237,7 @@ __device__ __forceinline__ void lgkm_wait(f16x8 (&f)[K]) {
     for (int i = 1; i < K; ++i) asm volatile("" : "+v"(f[i]));
 }
 
-template <int NT, int TS, bool ASMRD = (NT == 1)>
+template <int NT, int TS, bool ASMRD = true, int PFD = (NT == 1 ? 2 : 1)>
 __global__ __launch_bounds__(NTHR, 1) void conv_x3_kernel(X3Params p) {
     constexpr int T = TS * TS;
     constexpr int N = NT * 32;
@@ -339,18 +339,25 @@ __global__ __launch_bounds__(NTHR, 1) void conv_x3_kernel(X3Params p) {
     // Fragments are read X3_PF taps ahead of their MFMAs (X3_PF + 1 register sets): with one tap of lookahead the
     // reads of 8 waves (6-8 ds_read_b128 each) were covered by only ~5 of the wave's own MFMAs, and LDS latency
     // added to the matrix time instead of hiding under it.
-    // Explicit ds_read_b128 fragment reads one tap ahead with counted lgkmcnt waits (see the ring kernel's
-    // compute_asm); MFMAs unpredicated, the order per accumulator unchanged.  N = 32 only (ASMRD default): at N = 64 the
-    // two register sets of 8 fragments next to 64 accumulator registers exceed the 256-VGPR budget and spill.
+    // Explicit ds_read_b128 fragment reads PFD taps ahead with counted lgkmcnt waits (see the ring kernel's
+    // compute_asm); MFMAs unpredicated, the order per accumulator unchanged.  PFD = 2 needs 2 x NR < 16 (4-bit
+    // lgkmcnt): N = 32 only.
     auto compute_asm = [&](const unsigned char *s_in, const unsigned char *s_w) {
         constexpr int NR = 4 + 2 * NT;  // [ah0, al0, ah1, al1, bh0, bl0, (bh1, bl1)]
-        const uint32_t bi = lds_addr(s_in), bw = lds_addr(s_w);
-        f16x8 f[2][NR];
+        constexpr int NBUF = PFD + 1;
+        static_assert(PFD * NR < 16, "lgkmcnt is a 4-bit count");
+        // opaque stage bases: otherwise the per-stage fragment addresses are hoisted out of the chunk loop as 2 x 36
+        // loop-invariant VGPRs (the N = 64 kernel then spills)
+        uint32_t bi = lds_addr(s_in), bw = lds_addr(s_w);
+        asm volatile("" : "+s"(bi), "+s"(bw));
+        f16x8 f[NBUF][NR];
         auto ld = [&](int tap, int buf) {
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
-                f[buf][2 * mt] = ds_read16(bi + aoff[tap][mt][0]);
-                f[buf][2 * mt + 1] = ds_read16(bi + aoff[tap][mt][1]);
+                // the lo slot is the hi slot ^ 1 (slot_off), i.e. byte offset ^ 16; stage bases are 1-KB aligned
+                const uint32_t a = bi + aoff[tap][mt][0];
+                f[buf][2 * mt] = ds_read16(a);
+                f[buf][2 * mt + 1] = ds_read16(a ^ 16u);
             }
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) {
@@ -358,16 +365,16 @@ __global__ __launch_bounds__(NTHR, 1) void conv_x3_kernel(X3Params p) {
                 f[buf][5 + 2 * nt] = ds_read16(bw + boff1 + (tap * N + nt * 32) * REC);
             }
         };
-        ld(0, 0);
+#pragma unroll
+        for (int k = 0; k < PFD; ++k) ld(k, k);
 #pragma unroll
         for (int tap = 0; tap < T; ++tap) {
-            const int cb = tap & 1;
-            if (tap + 1 < T) {
-                ld(tap + 1, cb ^ 1);
-                lgkm_wait<NR>(f[cb]);
-            } else {
-                lgkm_wait<0>(f[cb]);
-            }
+            const int cb = tap % NBUF;
+            if (tap + PFD < T) ld(tap + PFD, (tap + PFD) % NBUF);
+            const int ahead = min(PFD, T - 1 - tap);  // read groups still allowed in flight
+            if (ahead >= 2) lgkm_wait<(PFD >= 2 ? 2 * NR : NR)>(f[cb]);
+            else if (ahead == 1) lgkm_wait<NR>(f[cb]);
+            else lgkm_wait<0>(f[cb]);
             f16x8 *q = f[cb];
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt)
@@ -603,7 +610,8 @@ __global__ __launch_bounds__(NTHR, 1) void conv_x3_ring_kernel(X3Params p) {
     // pipe.)  The MFMAs are not predicated on mvalid[1]: an invalid M-tile reads pixel 0's fragments and its
     // accumulator is never stored, and the wave with both M-tiles valid sets the barrier cadence anyway.
     auto compute_asm = [&](const unsigned char *s_in, const unsigned char *s_w, f32x16(&ac)[2]) {
-        const uint32_t bi = lds_addr(s_in), bw = lds_addr(s_w);
+        uint32_t bi = lds_addr(s_in), bw = lds_addr(s_w);
+        asm volatile("" : "+s"(bi), "+s"(bw));  // keep the per-slot addresses from being hoisted (VGPRs)
         f16x8 f[2][6];  // [buf][ah0, al0, ah1, al1, bh, bl]
         uint32_t a0[2][2];
 #pragma unroll
@@ -1023,7 +1031,7 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
         else hipLaunchKernelGGL((conv_x3_pring_kernel<2>), gridp, block, 0, stream, p);
         return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
     }
-    if (taps_side == 3 && cout <= 32 && ((g_x3_kernel >= 2 && g_x3_kernel != 20) || (g_x3_kernel == 1 && ring_pays))) {
+    if (taps_side == 3 && cout <= 32 && ((g_x3_kernel >= 2 && g_x3_kernel < 20) || (g_x3_kernel == 1 && ring_pays))) {
         const dim3 grid2((unsigned)pairs);
 #define RING_DBG(v, bits) \
     case v: hipLaunchKernelGGL((conv_x3_ring_kernel<3, true, bits>), grid2, block, 0, stream, p); break;
@@ -1052,6 +1060,8 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
     if (taps_side == 3 && g_x3_kernel == 20) {  // A/B: the classic kernel with compiler-scheduled fragment reads
         if (cout > 32) hipLaunchKernelGGL((conv_x3_kernel<2, 3, false>), grid, block, 0, stream, p);
         else hipLaunchKernelGGL((conv_x3_kernel<1, 3, false>), grid, block, 0, stream, p);
+    } else if (taps_side == 3 && cout <= 32 && g_x3_kernel == 21) {  // A/B: N = 32 with prefetch distance 1
+        hipLaunchKernelGGL((conv_x3_kernel<1, 3, true, 1>), grid, block, 0, stream, p);
     } else if (taps_side == 3) {
         if (cout > 32) hipLaunchKernelGGL((conv_x3_kernel<2, 3>), grid, block, 0, stream, p);
         else hipLaunchKernelGGL((conv_x3_kernel<1, 3>), grid, block, 0, stream, p);
@@ -1072,7 +1082,7 @@ extern "C" int esr_conv3x3_fwd_x3(const void *in, int32_t B, int32_t H, int32_t 
 }
 
 extern "C" int esr_x3_set_kernel(int32_t variant) {
-    if (variant < 0 || variant > 20) return ESR_EINVAL;
+    if (variant < 0 || variant > 21) return ESR_EINVAL;
     const int prev = g_x3_kernel;
     g_x3_kernel = variant;
     return prev;

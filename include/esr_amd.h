@@ -135,8 +135,9 @@ int esr_upconv2x_phase_fwd_x3(const void *in, int32_t B, int32_t H, int32_t W, i
  * fills the chip, else the classic two-stage kernel; 0 = classic only; 2 = ring always; 15 = ring with staggered DMA
  * issue; 16 / 17 = persistent ring (one workgroup per CU streaming tile pairs), fragment prefetch 1 / 2 taps;
  * 18 / 20 = ring / classic (20 also for cout > 32) with compiler-scheduled fragment reads instead of the explicit
- * counted-wait reads; 3..14 and 19 = diagnostic ablations of the ring kernel (garbage outputs).  0, 1, 2, 15..18 and
- * 20 give bitwise-identical results.  Returns the previous setting, or ESR_EINVAL. */
+ * counted-wait reads; 21 = classic with fragment prefetch distance 1 (default 2); 3..14 and 19 = diagnostic ablations
+ * of the ring kernel (garbage outputs).  0, 1, 2, 15..18, 20 and 21 give bitwise-identical results.  Returns the
+ * previous setting, or ESR_EINVAL. */
 int esr_x3_set_kernel(int32_t variant);
 
 /* ---- training / Z-optimisation backward (esr_train.hip) ------------------------------------------------------------

@@ -296,7 +296,7 @@ def test_x3_ring_kernel_bitwise_equals_classic(gpu_device, cin, cout, B, H, W):
     try:
         # classic only, ring always, persistent ring always, and ring / classic with the compiler-scheduled fragment
         # reads (the explicit counted-wait reads must not change a bit)
-        for variant in (0, 2, 17, 18, 20):
+        for variant in (0, 2, 17, 18, 20, 21):
             lib.esr_x3_set_kernel(variant)
             out = torch.zeros(B, H + 2, W + 2, 40, device=gpu_device)
             out2 = torch.zeros(B, H + 2, W + 2, 32, device=gpu_device)
@@ -313,6 +313,33 @@ def test_x3_ring_kernel_bitwise_equals_classic(gpu_device, cin, cout, B, H, W):
     ref = F.leaky_relu(F.conv2d(_nchw(engine.from_split(xs), 0, cin), w.double(), b.cpu().double(), padding=1), 0.2)
     ref = 0.2 * ref + _nchw(engine.from_split(rs), 0, cout)
     assert normwise_rel(_nchw(engine.from_split(outs[1][0]), 8, 8 + cout), ref) < 1e-5
+
+
+@pytest.mark.parametrize('cin,B,H,W', [(192, 3, 21, 70), (72, 1, 5, 9)])
+def test_x3_n64_explicit_reads_bitwise(gpu_device, cin, B, H, W):
+    """The N = 64 classic kernel with explicit counted-wait fragment reads (default) against the same kernel with the
+    compiler-scheduled reads (esr_x3_set_kernel 20): same MFMA order per accumulator, so bit for bit."""
+    lib = _lib.load()
+    cp = cin + 8
+    xs = engine.to_split(_padded(B, H, W, cp, cin, gpu_device, 31))
+    g = torch.Generator().manual_seed(32)
+    w = torch.randn(64, cin, 3, 3, generator=g) * 0.05
+    b = (torch.rand(64, generator=g) - 0.5).to(gpu_device)
+    wx, scale = engine.pack_x3(engine.pack_conv_weight(w.to(gpu_device), list(range(cin)), 64))
+    outs = []
+    try:
+        for variant in (1, 20):
+            lib.esr_x3_set_kernel(variant)
+            out = torch.zeros(B, H + 2, W + 2, 64, device=gpu_device)
+            o = engine._conv_out(out, 64, 0, H, W, True)
+            _lib.check(lib.esr_conv3x3_fwd_x3(xs.data_ptr(), B, H, W, cp, cin, wx.data_ptr(), b.data_ptr(), scale,
+                                              64, ctypes.byref(o), None, _stream()), 'conv_x3')
+            torch.cuda.synchronize()
+            outs.append(out)
+    finally:
+        lib.esr_x3_set_kernel(1)
+    assert torch.equal(outs[0], outs[1])
+    assert outs[0].abs().sum() > 0
 
 
 def test_conv3x3_x3_planar_output(gpu_device):

@@ -24,6 +24,7 @@ LDS_TAGS_X3 = {153600: 'x3_conv3x3_n64', 116736: 'x3_conv3x3_n32', 139264: 'x3_u
 
 
 def tag(name, lds):
+    name = name.replace('void (anonymous namespace)::', '')
     if name.startswith('conv_x3_ring_kernel'):
         return 'x3_conv3x3_n32'
     if name.startswith('conv_fwd_kernel'):
