@@ -237,8 +237,10 @@ __device__ __forceinline__ void lgkm_wait(f16x8 (&f)[K]) {
     for (int i = 1; i < K; ++i) asm volatile("" : "+v"(f[i]));
 }
 
-template <int NT, int TS, bool ASMRD = true, int PFD = (NT == 1 ? 2 : 1)>
-__global__ __launch_bounds__(NTHR, 1) void conv_x3_kernel(X3Params p) {
+// OS (one stage): a single LDS stage (input + weights, 57 KB at N = 32; the epilogue staging is the larger) and two
+// workgroups per CU (4 waves per SIMD: <= 128 VGPRs; the second launch-bounds argument is waves per SIMD), so one workgroup's DMA waits, prologue and epilogue overlap the other's MFMAs.
+template <int NT, int TS, bool ASMRD = true, int PFD = (NT == 1 ? 2 : 1), bool OS = false>
+__global__ __launch_bounds__(NTHR, OS ? 4 : 1) void conv_x3_kernel(X3Params p) {
     constexpr int T = TS * TS;
     constexpr int N = NT * 32;
     constexpr int W_RECS = T * N;
@@ -246,7 +248,9 @@ __global__ __launch_bounds__(NTHR, 1) void conv_x3_kernel(X3Params p) {
     constexpr int W_B = W_RECS * REC;
     constexpr int EP_P = N + 4;
     constexpr int EP_BYTES = TH * TWF * EP_P * 4;
-    constexpr int LDS_BYTES = 2 * (IN_B + W_B) > EP_BYTES ? 2 * (IN_B + W_B) : EP_BYTES;
+    constexpr int NST = OS ? 1 : 2;  // LDS stages
+    constexpr int LDS_BYTES = NST * (IN_B + W_B) > EP_BYTES ? NST * (IN_B + W_B) : EP_BYTES;
+    static_assert(!OS || 2 * LDS_BYTES <= 163840, "two workgroups per CU");
     constexpr int KIN = (IN_RECS / 16 + NWAVES - 1) / NWAVES;
     constexpr int KW = (W_RECS / 16 + NWAVES - 1) / NWAVES;
     __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
@@ -305,7 +309,7 @@ __global__ __launch_bounds__(NTHR, 1) void conv_x3_kernel(X3Params p) {
             const int r = 16 * k + sub;
             const int s = ps ^ ((r >> 2) & 3);
             __builtin_amdgcn_global_load_lds((glob_void *)(wj + r * REC + (s << 4)),
-                                             (lds_void *)(lds + 2 * IN_B + st * W_B + k * 1024), 16, 0, 0);
+                                             (lds_void *)(lds + NST * IN_B + st * W_B + k * 1024), 16, 0, 0);
         }
     };
 
@@ -438,6 +442,15 @@ __global__ __launch_bounds__(NTHR, 1) void conv_x3_kernel(X3Params p) {
     };
 
     // the explicit vmcnt(0) before each barrier: compute_asm's reads are invisible to the compiler's LDS-DMA tracking
+    if constexpr (OS) {
+        for (int j = 0; j < nchunk; ++j) {
+            if (j) __syncthreads();  // every wave is done reading the stage
+            dma(j, 0);
+            wait_vm_lgkm0<0>();
+            __syncthreads();
+            if (mvalid[0]) compute(lds, lds + IN_B);
+        }
+    } else {
     dma(0, 0);
     for (int j = 0; j < nchunk; j += 2) {
         wait_vm_lgkm0<0>();
@@ -449,6 +462,7 @@ __global__ __launch_bounds__(NTHR, 1) void conv_x3_kernel(X3Params p) {
         __syncthreads();
         if (j + 2 < nchunk) dma(j + 2, 0);
         if (mvalid[0]) compute(lds + IN_B, lds + 2 * IN_B + W_B);
+    }
     }
 
     // ---- epilogue: restage fp32 accumulators as [pixel][channel] ----
@@ -1013,10 +1027,9 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
     p.overflow = overflow;
     p.o = *o;
     const dim3 block(NTHR);
-    // Ring kernel for N <= 32 when its halved grid still fills the chip: with both kernels on counted-wait fragment
-    // reads a ring workgroup does two tiles in ~2.0x the time of a classic one (tools/x3_ring_ab.py at config 2 / 3
-    // shapes: classic 1-3 % faster at 148², 20 % at 96²), so the ring only pays where the classic grid's last round of
-    // workgroups is nearly empty: compare ceil(pairs/CUs) * 2 with ceil(tiles/CUs).
+    // Ring kernel (two tiles per workgroup, esr_x3_set_kernel 2): opt-in only.  With both kernels on counted-wait
+    // fragment reads a ring pair cost ~2.0 two-stage classic tiles, and the one-stage classic kernel at two
+    // workgroups per CU is faster still (tools/x3_ring_ab.py at config 2 / 3 shapes).
     const int tiles = p.tiles_x * p.tiles_y, pairs = p.tiles_x * ((p.tiles_y + 1) / 2);
     static int n_cu = 0;
     if (!n_cu) {
@@ -1024,7 +1037,9 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
         n_cu = (hipGetDevice(&dev) == hipSuccess &&
                 hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
     }
-    const bool ring_pays = 20 * ((pairs + n_cu - 1) / n_cu) < 10 * ((tiles + n_cu - 1) / n_cu);
+    // (no longer chosen automatically: the one-stage classic kernel at two workgroups per CU beats it everywhere)
+    const bool ring_pays = false;
+    (void)tiles;
     if (taps_side == 3 && cout <= 32 && (g_x3_kernel == 16 || g_x3_kernel == 17)) {
         const dim3 gridp((unsigned)min(pairs, n_cu));
         if (g_x3_kernel == 16) hipLaunchKernelGGL((conv_x3_pring_kernel<1>), gridp, block, 0, stream, p);
@@ -1062,9 +1077,14 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
         else hipLaunchKernelGGL((conv_x3_kernel<1, 3, false>), grid, block, 0, stream, p);
     } else if (taps_side == 3 && cout <= 32 && g_x3_kernel == 21) {  // A/B: N = 32 with prefetch distance 1
         hipLaunchKernelGGL((conv_x3_kernel<1, 3, true, 1>), grid, block, 0, stream, p);
+    } else if (taps_side == 3 && cout <= 32 && g_x3_kernel == 22) {  // A/B: two stages, one workgroup per CU
+        hipLaunchKernelGGL((conv_x3_kernel<1, 3>), grid, block, 0, stream, p);
     } else if (taps_side == 3) {
+        // N = 32: one LDS stage and two workgroups per CU (7-14 % faster than two stages and one workgroup at the
+        // config-2/3 shapes, profiles/r1_x3_reads_ab.txt); N = 64 needs 139 KB of epilogue staging and 64
+        // accumulator VGPRs, so it stays at one double-buffered workgroup per CU
         if (cout > 32) hipLaunchKernelGGL((conv_x3_kernel<2, 3>), grid, block, 0, stream, p);
-        else hipLaunchKernelGGL((conv_x3_kernel<1, 3>), grid, block, 0, stream, p);
+        else hipLaunchKernelGGL((conv_x3_kernel<1, 3, true, 1, true>), grid, block, 0, stream, p);
     } else {
         if (cout > 32) hipLaunchKernelGGL((conv_x3_kernel<2, 2>), grid, block, 0, stream, p);
         else hipLaunchKernelGGL((conv_x3_kernel<1, 2>), grid, block, 0, stream, p);
@@ -1082,7 +1102,7 @@ extern "C" int esr_conv3x3_fwd_x3(const void *in, int32_t B, int32_t H, int32_t 
 }
 
 extern "C" int esr_x3_set_kernel(int32_t variant) {
-    if (variant < 0 || variant > 21) return ESR_EINVAL;
+    if (variant < 0 || variant > 22) return ESR_EINVAL;
     const int prev = g_x3_kernel;
     g_x3_kernel = variant;
     return prev;

@@ -131,13 +131,13 @@ int esr_upconv2x_phase_fwd_x3(const void *in, int32_t B, int32_t H, int32_t W, i
                               const void *w_packed, const float *bias, float w_scale, int32_t cout, int32_t py,
                               int32_t px, const esr_conv_out *o, int32_t *overflow, esr_stream_t stream);
 /* Kernel selection for esr_conv3x3_fwd_x3 with cout <= 32 (process-wide; for A/B tests and benchmarks):
- * 1 (default) = ring kernel (two tiles per workgroup, 3-deep LDS-DMA input ring) where its pair-granular grid still
- * fills the chip, else the classic two-stage kernel; 0 = classic only; 2 = ring always; 15 = ring with staggered DMA
- * issue; 16 / 17 = persistent ring (one workgroup per CU streaming tile pairs), fragment prefetch 1 / 2 taps;
- * 18 / 20 = ring / classic (20 also for cout > 32) with compiler-scheduled fragment reads instead of the explicit
- * counted-wait reads; 21 = classic with fragment prefetch distance 1 (default 2); 3..14 and 19 = diagnostic ablations
- * of the ring kernel (garbage outputs).  0, 1, 2, 15..18, 20 and 21 give bitwise-identical results.  Returns the
- * previous setting, or ESR_EINVAL. */
+ * 0 / 1 (default) = classic kernel, one LDS stage, two workgroups per CU; 22 = classic with two LDS stages and one
+ * workgroup per CU; 21 = the same with fragment prefetch distance 1 (default 2); 20 = two-stage classic with
+ * compiler-scheduled fragment reads (also for cout > 32, whose default uses explicit counted-wait reads); 2 = ring
+ * kernel (two tiles per workgroup, 3-deep LDS-DMA input ring); 15 = ring with staggered DMA issue; 18 = ring with
+ * compiler-scheduled reads; 16 / 17 = persistent ring (one workgroup per CU streaming tile pairs), fragment prefetch
+ * 1 / 2 taps; 3..14 and 19 = diagnostic ablations of the ring kernel (garbage outputs).  All others give
+ * bitwise-identical results.  Returns the previous setting, or ESR_EINVAL. */
 int esr_x3_set_kernel(int32_t variant);
 
 /* ---- training / Z-optimisation backward (esr_train.hip) ------------------------------------------------------------

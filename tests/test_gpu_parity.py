@@ -294,9 +294,9 @@ def test_x3_ring_kernel_bitwise_equals_classic(gpu_device, cin, cout, B, H, W):
     rs = engine.to_split(_padded(B, H, W, 40, 40, gpu_device, 23))
     outs = []
     try:
-        # classic only, ring always, persistent ring always, and ring / classic with the compiler-scheduled fragment
-        # reads (the explicit counted-wait reads must not change a bit)
-        for variant in (0, 2, 17, 18, 20, 21):
+        # classic one-stage (default), ring always, persistent ring always, ring / classic with the compiler-scheduled
+        # fragment reads, two-stage classic with prefetch 1 / 2 (none may change a bit)
+        for variant in (0, 2, 17, 18, 20, 21, 22):
             lib.esr_x3_set_kernel(variant)
             out = torch.zeros(B, H + 2, W + 2, 40, device=gpu_device)
             out2 = torch.zeros(B, H + 2, W + 2, 32, device=gpu_device)
