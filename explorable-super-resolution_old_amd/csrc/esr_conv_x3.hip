@@ -238,20 +238,26 @@ __device__ __forceinline__ void lgkm_wait(f16x8 (&f)[K]) {
 }
 
 // OS (one stage): a single LDS stage (input + weights, 57 KB at N = 32; the epilogue staging is the larger) and two
-// workgroups per CU (4 waves per SIMD: <= 128 VGPRs; the second launch-bounds argument is waves per SIMD), so one workgroup's DMA waits, prologue and epilogue overlap the other's MFMAs.
-template <int NT, int TS, bool ASMRD = true, int PFD = (NT == 1 ? 2 : 1), bool OS = false>
-__global__ __launch_bounds__(NTHR, OS ? 4 : 1) void conv_x3_kernel(X3Params p) {
+// workgroups per CU (4 waves per SIMD: <= 128 VGPRs; the second launch-bounds argument is waves per SIMD), so one
+// workgroup's DMA waits, prologue and epilogue overlap the other's MFMAs.  THT: tile height (16: two 32-pixel M-tiles
+// per wave; 8: one, which halves the accumulators and the epilogue staging so N = 64 also fits two per CU).
+template <int NT, int TS, bool ASMRD = true, int PFD = (NT == 1 ? 2 : 1), bool OS = false, int THT = TH,
+          int WPS = (OS ? 4 : 1)>
+__global__ __launch_bounds__(NTHR, WPS) void conv_x3_kernel(X3Params p) {
+    constexpr int MTW = THT / 8;  // M-tiles per wave
+    constexpr int HYT = THT + 2;
+    constexpr int IN_RECS_T = (HYT * HXF + 15) / 16 * 16;
     constexpr int T = TS * TS;
     constexpr int N = NT * 32;
     constexpr int W_RECS = T * N;
-    constexpr int IN_B = IN_RECS * REC;
+    constexpr int IN_B = IN_RECS_T * REC;
     constexpr int W_B = W_RECS * REC;
     constexpr int EP_P = N + 4;
-    constexpr int EP_BYTES = TH * TWF * EP_P * 4;
+    constexpr int EP_BYTES = THT * TWF * EP_P * 4;
     constexpr int NST = OS ? 1 : 2;  // LDS stages
     constexpr int LDS_BYTES = NST * (IN_B + W_B) > EP_BYTES ? NST * (IN_B + W_B) : EP_BYTES;
-    static_assert(!OS || 2 * LDS_BYTES <= 163840, "two workgroups per CU");
-    constexpr int KIN = (IN_RECS / 16 + NWAVES - 1) / NWAVES;
+    static_assert(!OS || (WPS / 2) * LDS_BYTES <= 163840, "WPS / 2 workgroups per CU");
+    constexpr int KIN = (IN_RECS_T / 16 + NWAVES - 1) / NWAVES;
     constexpr int KW = (W_RECS / 16 + NWAVES - 1) / NWAVES;
     __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
 
@@ -266,9 +272,9 @@ __global__ __launch_bounds__(NTHR, OS ? 4 : 1) void conv_x3_kernel(X3Params p) {
     const int x0 = tx * TWF;
     const int tw = min(TWF, p.W - x0);
     const int hx = tw + 2;
-    const int r0 = ty * TH;
+    const int r0 = ty * THT;
     const int rows_tot = p.B * (p.H + 2);
-    const int nq = TH * tw;
+    const int nq = THT * tw;
     const int nmt = (nq + 31) >> 5;
     const long long rowp = (long long)(p.W + 2);
     const long long pixb = 4LL * p.in_cp;
@@ -286,7 +292,7 @@ __global__ __launch_bounds__(NTHR, OS ? 4 : 1) void conv_x3_kernel(X3Params p) {
         const int gy = r0 + hy, gx = x0 + hxi;
         in_hi[i] = -1;
         in_src[i] = 0;
-        if (k < IN_RECS / 16 && r < HY * hx && gy < rows_tot && gx < p.W + 2) {
+        if (k < IN_RECS_T / 16 && r < HYT * hx && gy < rows_tot && gx < p.W + 2) {
             in_src[i] = (gy * rowp + gx) * pixb + (s << 4);
             in_hi[i] = s >> 1;
         }
@@ -296,7 +302,7 @@ __global__ __launch_bounds__(NTHR, OS ? 4 : 1) void conv_x3_kernel(X3Params p) {
 #pragma unroll
         for (int i = 0; i < KIN; ++i) {
             const int k = wave + NWAVES * i;
-            if (k >= IN_RECS / 16) break;
+            if (k >= IN_RECS_T / 16) break;
             const void *src = (in_hi[i] >= 0 && in_hi[i] < groups) ? (const void *)(p.in + in_src[i] + 64LL * j)
                                                                    : (const void *)g_zero_page;
             __builtin_amdgcn_global_load_lds((glob_void *)src, (lds_void *)(lds + st * IN_B + k * 1024), 16, 0, 0);
@@ -313,11 +319,11 @@ __global__ __launch_bounds__(NTHR, OS ? 4 : 1) void conv_x3_kernel(X3Params p) {
         }
     };
 
-    int aoff[T][2][2];
-    bool mvalid[2];
+    int aoff[T][MTW][2];
+    bool mvalid[MTW];
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
-        const int jm = 2 * wave + mt;
+    for (int mt = 0; mt < MTW; ++mt) {
+        const int jm = MTW * wave + mt;
         mvalid[mt] = jm < nmt;
         int q = 32 * jm + ml;
         if (q >= nq) q = 0;
@@ -332,9 +338,9 @@ __global__ __launch_bounds__(NTHR, OS ? 4 : 1) void conv_x3_kernel(X3Params p) {
     const int bsw = (ml >> 2) & 3;
     const int boff0 = ml * REC + (((2 * hl) ^ bsw) << 4), boff1 = ml * REC + (((2 * hl + 1) ^ bsw) << 4);
 
-    f32x16 acc[2][NT];
+    f32x16 acc[MTW][NT];
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < MTW; ++mt)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
@@ -347,7 +353,7 @@ __global__ __launch_bounds__(NTHR, OS ? 4 : 1) void conv_x3_kernel(X3Params p) {
     // compute_asm); MFMAs unpredicated, the order per accumulator unchanged.  PFD = 2 needs 2 x NR < 16 (4-bit
     // lgkmcnt): N = 32 only.
     auto compute_asm = [&](const unsigned char *s_in, const unsigned char *s_w) {
-        constexpr int NR = 4 + 2 * NT;  // [ah0, al0, ah1, al1, bh0, bl0, (bh1, bl1)]
+        constexpr int NR = 2 * MTW + 2 * NT;  // [ah0, al0, (ah1, al1), bh0, bl0, (bh1, bl1)]
         constexpr int NBUF = PFD + 1;
         static_assert(PFD * NR < 16, "lgkmcnt is a 4-bit count");
         // opaque stage bases: otherwise the per-stage fragment addresses are hoisted out of the chunk loop as 2 x 36
@@ -357,7 +363,7 @@ __global__ __launch_bounds__(NTHR, OS ? 4 : 1) void conv_x3_kernel(X3Params p) {
         f16x8 f[NBUF][NR];
         auto ld = [&](int tap, int buf) {
 #pragma unroll
-            for (int mt = 0; mt < 2; ++mt) {
+            for (int mt = 0; mt < MTW; ++mt) {
                 // the lo slot is the hi slot ^ 1 (slot_off), i.e. byte offset ^ 16; stage bases are 1-KB aligned
                 const uint32_t a = bi + aoff[tap][mt][0];
                 f[buf][2 * mt] = ds_read16(a);
@@ -365,8 +371,8 @@ __global__ __launch_bounds__(NTHR, OS ? 4 : 1) void conv_x3_kernel(X3Params p) {
             }
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) {
-                f[buf][4 + 2 * nt] = ds_read16(bw + boff0 + (tap * N + nt * 32) * REC);
-                f[buf][5 + 2 * nt] = ds_read16(bw + boff1 + (tap * N + nt * 32) * REC);
+                f[buf][2 * MTW + 2 * nt] = ds_read16(bw + boff0 + (tap * N + nt * 32) * REC);
+                f[buf][2 * MTW + 1 + 2 * nt] = ds_read16(bw + boff1 + (tap * N + nt * 32) * REC);
             }
         };
 #pragma unroll
@@ -381,20 +387,20 @@ __global__ __launch_bounds__(NTHR, OS ? 4 : 1) void conv_x3_kernel(X3Params p) {
             else lgkm_wait<0>(f[cb]);
             f16x8 *q = f[cb];
 #pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
+            for (int mt = 0; mt < MTW; ++mt)
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt)
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(q[2 * mt + 1], q[4 + 2 * nt], acc[mt][nt], 0, 0, 0);
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(q[2 * mt + 1], q[2 * MTW + 2 * nt], acc[mt][nt], 0, 0, 0);
 #pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt)
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(q[2 * mt], q[5 + 2 * nt], acc[mt][nt], 0, 0, 0);
-#pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
+            for (int mt = 0; mt < MTW; ++mt)
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt)
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(q[2 * mt], q[4 + 2 * nt], acc[mt][nt], 0, 0, 0);
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(q[2 * mt], q[2 * MTW + 1 + 2 * nt], acc[mt][nt], 0, 0, 0);
+#pragma unroll
+            for (int mt = 0; mt < MTW; ++mt)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(q[2 * mt], q[2 * MTW + 2 * nt], acc[mt][nt], 0, 0, 0);
         }
     };
     auto compute = [&](const unsigned char *s_in, const unsigned char *s_w) {
@@ -403,10 +409,10 @@ __global__ __launch_bounds__(NTHR, OS ? 4 : 1) void conv_x3_kernel(X3Params p) {
             return;
         }
         constexpr int NBUF = X3_PF + 1;
-        f16x8 ah[NBUF][2], al[NBUF][2], bh[NBUF][NT], bl[NBUF][NT];
+        f16x8 ah[NBUF][MTW], al[NBUF][MTW], bh[NBUF][NT], bl[NBUF][NT];
         auto ld = [&](int tap, int buf) {
 #pragma unroll
-            for (int mt = 0; mt < 2; ++mt) {
+            for (int mt = 0; mt < MTW; ++mt) {
                 ah[buf][mt] = *reinterpret_cast<const f16x8 *>(s_in + aoff[tap][mt][0]);
                 al[buf][mt] = *reinterpret_cast<const f16x8 *>(s_in + aoff[tap][mt][1]);
             }
@@ -424,17 +430,17 @@ __global__ __launch_bounds__(NTHR, OS ? 4 : 1) void conv_x3_kernel(X3Params p) {
             const int cb = tap % NBUF;
             if (tap + X3_PF < T) ld(tap + X3_PF, (tap + X3_PF) % NBUF);
 #pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
+            for (int mt = 0; mt < MTW; ++mt)
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt)
                     if (mvalid[mt]) acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[cb][mt], bh[cb][nt], acc[mt][nt], 0, 0, 0);
 #pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
+            for (int mt = 0; mt < MTW; ++mt)
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt)
                     if (mvalid[mt]) acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[cb][mt], bl[cb][nt], acc[mt][nt], 0, 0, 0);
 #pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
+            for (int mt = 0; mt < MTW; ++mt)
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt)
                     if (mvalid[mt]) acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[cb][mt], bh[cb][nt], acc[mt][nt], 0, 0, 0);
@@ -469,19 +475,19 @@ __global__ __launch_bounds__(NTHR, OS ? 4 : 1) void conv_x3_kernel(X3Params p) {
     __syncthreads();
     float *s_ep = reinterpret_cast<float *>(lds);
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
+    for (int mt = 0; mt < MTW; ++mt) {
         if (!mvalid[mt]) continue;
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int q = 32 * (2 * wave + mt) + (r & 3) + 8 * (r >> 2) + 4 * hl;
+                const int q = 32 * (MTW * wave + mt) + (r & 3) + 8 * (r >> 2) + 4 * hl;
                 if (q < nq) s_ep[q * EP_P + nt * 32 + ml] = acc[mt][nt][r];
             }
     }
     __syncthreads();
 
-    const bool ok = store_tile<N>(p, s_ep, r0, x0, tw, nq, tid);
+    const bool ok = store_px<N, NTHR, THT * TWF>(p, s_ep, 0, r0, x0, tw, nq, tid);
     if (!ok && p.overflow) atomicOr(p.overflow, 1);
 }
 
@@ -1039,7 +1045,12 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
     }
     // (no longer chosen automatically: the one-stage classic kernel at two workgroups per CU beats it everywhere)
     const bool ring_pays = false;
-    (void)tiles;
+    // N = 32 one-stage kernel, 16-row tiles at 2 workgroups per CU vs 8-row tiles at 3: a round of 8-row workgroups
+    // takes ~3/4 of a round of 16-row ones (measured: at 148², where both grids fill their last round, 16-row is ~1 %
+    // faster over a whole bench step; 8-row is 15-20 % faster at 96², where the 16-row grid's second round is nearly
+    // empty), so compare rounds x 3 with rounds x 4, ties to 16-row
+    const int tiles8 = p.tiles_x * ((B * (H + 2) - 2 + 7) / 8);
+    const bool row8_pays = 3 * ((tiles8 + 3 * n_cu - 1) / (3 * n_cu)) < 4 * ((tiles + 2 * n_cu - 1) / (2 * n_cu));
     if (taps_side == 3 && cout <= 32 && (g_x3_kernel == 16 || g_x3_kernel == 17)) {
         const dim3 gridp((unsigned)min(pairs, n_cu));
         if (g_x3_kernel == 16) hipLaunchKernelGGL((conv_x3_pring_kernel<1>), gridp, block, 0, stream, p);
@@ -1077,12 +1088,24 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
         else hipLaunchKernelGGL((conv_x3_kernel<1, 3, false>), grid, block, 0, stream, p);
     } else if (taps_side == 3 && cout <= 32 && g_x3_kernel == 21) {  // A/B: N = 32 with prefetch distance 1
         hipLaunchKernelGGL((conv_x3_kernel<1, 3, true, 1>), grid, block, 0, stream, p);
-    } else if (taps_side == 3 && cout <= 32 && g_x3_kernel == 22) {  // A/B: two stages, one workgroup per CU
+    } else if (taps_side == 3 && cout > 32 && g_x3_kernel == 23) {
+        // A/B: N = 64 with 8-row tiles, one stage, two workgroups per CU (prefetch 2 would spill at 128 VGPRs)
+        p.tiles_y = (B * (H + 2) - 2 + 7) / 8;
+        const dim3 grid8((unsigned)(p.tiles_x * p.tiles_y));
+        hipLaunchKernelGGL((conv_x3_kernel<2, 3, true, 1, true, 8>), grid8, block, 0, stream, p);
+    } else if (taps_side == 3 && cout <= 32 && g_x3_kernel != 22 && g_x3_kernel != 26 &&
+               (g_x3_kernel == 25 || row8_pays)) {
+        // N = 32 with 8-row tiles (one 32-pixel M-tile per wave), one stage, three workgroups per CU (<= 80 VGPRs)
+        p.tiles_y = (B * (H + 2) - 2 + 7) / 8;
+        const dim3 grid8((unsigned)(p.tiles_x * p.tiles_y));
+        hipLaunchKernelGGL((conv_x3_kernel<1, 3, true, 1, true, 8, 6>), grid8, block, 0, stream, p);
+    } else if (taps_side == 3 && cout <= 32 && g_x3_kernel == 22) {  // A/B: two stages, one workgroup per CU (16 rows)
         hipLaunchKernelGGL((conv_x3_kernel<1, 3>), grid, block, 0, stream, p);
     } else if (taps_side == 3) {
-        // N = 32: one LDS stage and two workgroups per CU (7-14 % faster than two stages and one workgroup at the
-        // config-2/3 shapes, profiles/r1_x3_reads_ab.txt); N = 64 needs 139 KB of epilogue staging and 64
-        // accumulator VGPRs, so it stays at one double-buffered workgroup per CU
+        // N = 32 with 16-row tiles (variant 26, or where row8_pays is false): one LDS stage and two workgroups per CU
+        // (7-14 % faster than two stages and one workgroup at the config-2/3 shapes, profiles/r1_x3_reads_ab.txt);
+        // N = 64 stays at one double-buffered 16-row workgroup per CU (variant 23, 8-row tiles at two per CU: 8 %
+        // faster at 96², 4 % slower at 148²)
         if (cout > 32) hipLaunchKernelGGL((conv_x3_kernel<2, 3>), grid, block, 0, stream, p);
         else hipLaunchKernelGGL((conv_x3_kernel<1, 3, true, 1, true>), grid, block, 0, stream, p);
     } else {
@@ -1102,7 +1125,7 @@ extern "C" int esr_conv3x3_fwd_x3(const void *in, int32_t B, int32_t H, int32_t 
 }
 
 extern "C" int esr_x3_set_kernel(int32_t variant) {
-    if (variant < 0 || variant > 22) return ESR_EINVAL;
+    if (variant < 0 || variant > 26) return ESR_EINVAL;
     const int prev = g_x3_kernel;
     g_x3_kernel = variant;
     return prev;

@@ -131,8 +131,9 @@ int esr_upconv2x_phase_fwd_x3(const void *in, int32_t B, int32_t H, int32_t W, i
                               const void *w_packed, const float *bias, float w_scale, int32_t cout, int32_t py,
                               int32_t px, const esr_conv_out *o, int32_t *overflow, esr_stream_t stream);
 /* Kernel selection for esr_conv3x3_fwd_x3 with cout <= 32 (process-wide; for A/B tests and benchmarks):
- * 0 / 1 (default) = classic kernel, one LDS stage, two workgroups per CU; 22 = classic with two LDS stages and one
- * workgroup per CU; 21 = the same with fragment prefetch distance 1 (default 2); 20 = two-stage classic with
+ * 0 / 1 (default) = classic kernel, one LDS stage, 8-row tiles at three workgroups per CU or 16-row tiles at two
+ * (a wave-quantisation cost model picks; 25 / 26 force one); 22 = classic with two LDS stages and one workgroup per
+ * CU; 23 = cout > 32 with 8-row tiles at two workgroups per CU; 21 = the same with fragment prefetch distance 1 (default 2); 20 = two-stage classic with
  * compiler-scheduled fragment reads (also for cout > 32, whose default uses explicit counted-wait reads); 2 = ring
  * kernel (two tiles per workgroup, 3-deep LDS-DMA input ring); 15 = ring with staggered DMA issue; 18 = ring with
  * compiler-scheduled reads; 16 / 17 = persistent ring (one workgroup per CU streaming tile pairs), fragment prefetch

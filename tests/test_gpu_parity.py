@@ -296,7 +296,7 @@ def test_x3_ring_kernel_bitwise_equals_classic(gpu_device, cin, cout, B, H, W):
     try:
         # classic one-stage (default), ring always, persistent ring always, ring / classic with the compiler-scheduled
         # fragment reads, two-stage classic with prefetch 1 / 2 (none may change a bit)
-        for variant in (0, 2, 17, 18, 20, 21, 22):
+        for variant in (0, 2, 17, 18, 20, 21, 22, 25, 26):
             lib.esr_x3_set_kernel(variant)
             out = torch.zeros(B, H + 2, W + 2, 40, device=gpu_device)
             out2 = torch.zeros(B, H + 2, W + 2, 32, device=gpu_device)
@@ -328,7 +328,7 @@ def test_x3_n64_explicit_reads_bitwise(gpu_device, cin, B, H, W):
     wx, scale = engine.pack_x3(engine.pack_conv_weight(w.to(gpu_device), list(range(cin)), 64))
     outs = []
     try:
-        for variant in (1, 20):
+        for variant in (1, 20, 23):  # default, compiler-scheduled reads, 8-row tiles at two workgroups per CU
             lib.esr_x3_set_kernel(variant)
             out = torch.zeros(B, H + 2, W + 2, 64, device=gpu_device)
             o = engine._conv_out(out, 64, 0, H, W, True)
@@ -338,7 +338,7 @@ def test_x3_n64_explicit_reads_bitwise(gpu_device, cin, B, H, W):
             outs.append(out)
     finally:
         lib.esr_x3_set_kernel(1)
-    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
     assert outs[0].abs().sum() > 0
 
 

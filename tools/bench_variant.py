@@ -1,0 +1,14 @@
+#!/usr/bin/env python3
+"""Run bench.py with an x3 conv kernel variant forced (esr_x3_set_kernel), for same-box A/B of whole steps.
+    python tools/bench_variant.py VARIANT [bench.py args...]"""
+import os
+import runpy
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, 'explorable-super-resolution_old_amd'))
+from esr_amd import _lib  # noqa: E402
+
+_lib.load().esr_x3_set_kernel(int(sys.argv[1]))
+sys.argv = [os.path.join(REPO, 'bench.py')] + sys.argv[2:]
+runpy.run_path(sys.argv[0], run_name='__main__')
