@@ -61,6 +61,7 @@ struct X3Params {
     float w_scale_inv;
     int cout;
     int tap_y0, tap_x0, tiles_x, tiles_y;
+    int xcd_map;  // 1: blockIdx -> tile grouped per XCD (xcd_tile)
     int *overflow;
     esr_conv_out o;
 };
@@ -207,6 +208,17 @@ __device__ __forceinline__ void wait_vm_lgkm0() {
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(VM) : "memory");
 }
 
+// Workgroups are dispatched round-robin over the 8 XCDs (blockIdx b runs on XCD b % 8), each with its own L2.  With
+// tiles numbered row-major, horizontally adjacent tiles then sit in different L2s and every tile's halo rows are
+// fetched from HBM again by the XCD that owns the neighbour.  xcd_tile renumbers so that XCD x gets one contiguous
+// run of tiles (a band of whole tile rows): vertical and horizontal neighbours share an L2, and the workgroups
+// co-resident on an XCD at any moment cover a compact band.  A bijection for any grid size.
+constexpr int N_XCD = 8;
+__device__ __forceinline__ int xcd_tile(int b, int nb) {
+    const int x = b % N_XCD, l = b / N_XCD, q = nb / N_XCD, r = nb % N_XCD;
+    return x < r ? x * (q + 1) + l : r * (q + 1) + (x - r) * q + l;
+}
+
 // LDS byte address of a pointer into the kernel's __shared__ array
 __device__ __forceinline__ uint32_t lds_addr(const void *p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
@@ -267,8 +279,9 @@ __global__ __launch_bounds__(NTHR, WPS) void conv_x3_kernel(X3Params p) {
     const int hl = lane >> 5;
     const int ml = lane & 31;
 
-    const int tx = blockIdx.x % p.tiles_x;
-    const int ty = blockIdx.x / p.tiles_x;
+    const int tile = p.xcd_map ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x;
+    const int tx = tile % p.tiles_x;
+    const int ty = tile / p.tiles_x;
     const int x0 = tx * TWF;
     const int tw = min(TWF, p.W - x0);
     const int hx = tw + 2;
@@ -1009,6 +1022,7 @@ __global__ __launch_bounds__(NTHR, 1) void conv_x3_pring_kernel(X3Params p) {
 }
 
 int g_x3_kernel = 1;  // esr_x3_set_kernel (include/esr_amd.h)
+int g_x3_map = 1;     // esr_x3_set_tile_map (XCD-grouped: ~1 % per step, profiles/r1_x3_xcdmap_ab.txt)
 
 int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const void *w, const float *bias,
               float w_scale, int cout, int taps_side, int ty0, int tx0, const esr_conv_out *o, int *overflow,
@@ -1030,6 +1044,7 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
     p.tap_y0 = ty0; p.tap_x0 = tx0;
     p.tiles_x = (W + TWF - 1) / TWF;
     p.tiles_y = (B * (H + 2) - 2 + TH - 1) / TH;
+    p.xcd_map = g_x3_map;
     p.overflow = overflow;
     p.o = *o;
     const dim3 block(NTHR);
@@ -1128,6 +1143,13 @@ extern "C" int esr_x3_set_kernel(int32_t variant) {
     if (variant < 0 || variant > 26) return ESR_EINVAL;
     const int prev = g_x3_kernel;
     g_x3_kernel = variant;
+    return prev;
+}
+
+extern "C" int esr_x3_set_tile_map(int32_t mode) {
+    if (mode < 0 || mode > 1) return ESR_EINVAL;
+    const int prev = g_x3_map;
+    g_x3_map = mode;
     return prev;
 }
 

@@ -342,6 +342,35 @@ def test_x3_n64_explicit_reads_bitwise(gpu_device, cin, B, H, W):
     assert outs[0].abs().sum() > 0
 
 
+@pytest.mark.parametrize('cout,cin,B,H,W', [(32, 72, 3, 21, 70), (64, 96, 2, 37, 150), (32, 64, 5, 33, 40)])
+def test_x3_xcd_tile_map_bitwise(gpu_device, cout, cin, B, H, W):
+    """XCD-grouped block -> tile order (default, esr_x3_set_tile_map 1) against row-major blockIdx order (0): a
+    renumbering of the same tiles, so bit for bit; grids of 15 / 30 / 45 (16-row) and 8-row tiles are not multiples of
+    the 8 XCDs, which exercises the remainder split of xcd_tile."""
+    lib = _lib.load()
+    cp = cin + 8
+    xs = engine.to_split(_padded(B, H, W, cp, cin, gpu_device, 41))
+    g = torch.Generator().manual_seed(42)
+    w = torch.randn(cout, cin, 3, 3, generator=g) * 0.05
+    b = (torch.rand(cout, generator=g) - 0.5).to(gpu_device)
+    wx, scale = engine.pack_x3(engine.pack_conv_weight(w.to(gpu_device), list(range(cin)), cout))
+    outs = []
+    try:
+        for mode in (1, 0):
+            lib.esr_x3_set_tile_map(mode)
+            out = torch.zeros(B, H + 2, W + 2, cout, device=gpu_device)
+            o = engine._conv_out(out, cout, 0, H, W, True)
+            _lib.check(lib.esr_conv3x3_fwd_x3(xs.data_ptr(), B, H, W, cp, cin, wx.data_ptr(), b.data_ptr(), scale,
+                                              cout, ctypes.byref(o), None, _stream()), 'conv_x3')
+            torch.cuda.synchronize()
+            outs.append(out)
+    finally:
+        lib.esr_x3_set_tile_map(1)
+    assert torch.equal(outs[0], outs[1])
+    ref = F.leaky_relu(F.conv2d(_nchw(engine.from_split(xs), 0, cin), w.double(), b.cpu().double(), padding=1), 0.2)
+    assert normwise_rel(_nchw(engine.from_split(outs[0]), 0, cout), ref) < 1e-5
+
+
 def test_conv3x3_x3_planar_output(gpu_device):
     lib = _lib.load()
     B, H, W, cin = 2, 19, 45, 72

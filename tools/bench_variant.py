@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Run bench.py with an x3 conv kernel variant forced (esr_x3_set_kernel), for same-box A/B of whole steps.
+"""Run bench.py with an x3 conv kernel variant forced (esr_x3_set_kernel / esr_x3_set_tile_map), for same-box A/B of whole steps.
     python tools/bench_variant.py VARIANT [bench.py args...]"""
 import os
 import runpy
@@ -9,6 +9,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, 'explorable-super-resolution_old_amd'))
 from esr_amd import _lib  # noqa: E402
 
-_lib.load().esr_x3_set_kernel(int(sys.argv[1]))
+_v = int(sys.argv[1])  # + 1000: row-major block -> tile order (esr_x3_set_tile_map 0), else XCD-grouped (1)
+_lib.load().esr_x3_set_kernel(_v % 1000)
+_lib.load().esr_x3_set_tile_map(0 if _v >= 1000 else 1)
 sys.argv = [os.path.join(REPO, 'bench.py')] + sys.argv[2:]
 runpy.run_path(sys.argv[0], run_name='__main__')

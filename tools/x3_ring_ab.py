@@ -37,7 +37,8 @@ for H, W in ((h, h) for h in HWS):
         xs = engine.to_split(x)
         res = {}
         for variant in VARIANTS:
-            lib.esr_x3_set_kernel(variant)
+            lib.esr_x3_set_kernel(variant % 1000)
+            lib.esr_x3_set_tile_map(0 if variant >= 1000 else 1)  # variant + 1000: row-major block order
             out = torch.zeros(B, H + 2, W + 2, cp, device=dev)
             o = engine._conv_out(out, cp, cin if cin + cout <= cp else 0, H, W, True)
 
@@ -56,11 +57,12 @@ for H, W in ((h, h) for h in HWS):
             fl = 2.0 * B * H * W * 9 * cin * cout
             res[variant] = (us, out)
             print('B=%d %dx%d cin=%d cout=%d %-14s: %8.1f us  %6.1f TFLOP/s' % (
-                B, H, W, cin, cout, NAMES.get(variant & 255, str(variant & 255)) + ('+prio' if variant & 256 else ''), us, fl / us / 1e6), flush=True)
+                B, H, W, cin, cout, NAMES.get(variant % 1000, str(variant)) + ('+rowmajor' if variant >= 1000 else ''), us, fl / us / 1e6), flush=True)
         v0 = VARIANTS[0]
         for v in VARIANTS[1:]:
-            same = torch.equal(res[v0][1], res[v][1]) if v < 3 or (v >= 15 and v != 19) else True
-            print('   %s/%s speedup %.3f, outputs bitwise equal: %s' % (NAMES.get(v & 255, str(v)) + ('+prio' if v & 256 else ''), NAMES.get(v0 & 255, str(v0)), res[v0][0] / res[v][0],
+            same = torch.equal(res[v0][1], res[v][1]) if v % 1000 < 3 or (v % 1000 >= 15 and v % 1000 != 19) else True
+            print('   %s/%s speedup %.3f, outputs bitwise equal: %s' % (NAMES.get(v % 1000, str(v)) + ('+rowmajor' if v >= 1000 else ''), NAMES.get(v0 % 1000, str(v0)), res[v0][0] / res[v][0],
                                                                       same), flush=True)
             assert same
 lib.esr_x3_set_kernel(1)
+lib.esr_x3_set_tile_map(1)
