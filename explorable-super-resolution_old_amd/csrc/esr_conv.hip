@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include "esr_amd.h"
 
+int esr_g_conv_tile_map = 1;  // set with the x3 kernels' order by esr_x3_set_tile_map (esr_conv_x3.hip)
+
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -35,6 +37,7 @@ struct ConvParams {
     int cout;
     int tap_y0, tap_x0;  // halo-tile offset of tap 0 (0,0 for 3×3; (py,px) for an upconv phase)
     int tiles_x, tiles_y;
+    int xcd_map;  // 1: XCD-grouped tile order
     esr_conv_out o;
 };
 
@@ -57,7 +60,13 @@ __global__ __launch_bounds__(NTHREADS, (MT == 1 && NT == 1) ? 2 : 1) void conv_f
     const int hl = lane >> 5;   // lane half
     const int ml = lane & 31;
 
+    // XCD-grouped tile order (esr_x3_set_tile_map; same renumbering as esr_conv_x3.hip's xcd_tile): workgroup b runs on
+    // XCD b % 8, and each XCD takes one contiguous run of tiles so neighbouring tiles share its L2
     int t = blockIdx.x;
+    if (p.xcd_map) {
+        const int nb = gridDim.x, x = t % 8, l = t / 8, q = nb / 8, r = nb % 8;
+        t = x < r ? x * (q + 1) + l : r * (q + 1) + (x - r) * q + l;
+    }
     const int tx = t % p.tiles_x;
     t /= p.tiles_x;
     const int ty = t % p.tiles_y;
@@ -231,6 +240,7 @@ int launch_conv(const float *in, int B, int H, int W, int in_cp, int cin, const 
     const int tiles8 = p.tiles_x * ((H + 7) / 8) * B;
     const int mt = g_conv_tile == 4 ? 1 : g_conv_tile == 8 ? 2 : ((cout <= 32 || tiles8 < 8 * n_cus()) ? 1 : 2);
     p.tiles_y = (H + 4 * mt - 1) / (4 * mt);
+    p.xcd_map = esr_g_conv_tile_map;
     p.o = *o;
     const dim3 grid((unsigned)(p.tiles_x * p.tiles_y * B)), block(NTHREADS);
 #define ESR_CONV_LAUNCH(NT_, TS_, MT_) hipLaunchKernelGGL((conv_fwd_kernel<NT_, TS_, MT_>), grid, block, 0, stream, p)

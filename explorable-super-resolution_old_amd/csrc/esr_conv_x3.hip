@@ -33,6 +33,8 @@
 #include <hip/hip_runtime.h>
 #include "esr_amd.h"
 
+extern int esr_g_conv_tile_map;  // esr_conv.hip: the exact-fp32 conv kernel's tile order
+
 namespace {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -1150,6 +1152,7 @@ extern "C" int esr_x3_set_tile_map(int32_t mode) {
     if (mode < 0 || mode > 1) return ESR_EINVAL;
     const int prev = g_x3_map;
     g_x3_map = mode;
+    esr_g_conv_tile_map = mode;
     return prev;
 }
 

@@ -141,7 +141,7 @@ int esr_upconv2x_phase_fwd_x3(const void *in, int32_t B, int32_t H, int32_t W, i
  * bitwise-identical results.  Returns the previous setting, or ESR_EINVAL. */
 int esr_x3_set_kernel(int32_t variant);
 
-/* Block -> tile order of the classic x3 conv kernel: 1 (default) = XCD-grouped (workgroups run round-robin over the
+/* Block -> tile order of the classic x3 conv kernel and the exact-fp32 conv kernel: 1 (default) = XCD-grouped (workgroups run round-robin over the
  * 8 XCDs; each XCD gets one contiguous band of tiles so neighbouring tiles' halos are shared in its L2), 0 = row-major
  * over blockIdx.  Results are bitwise identical.  Returns the previous setting, or ESR_EINVAL. */
 int esr_x3_set_tile_map(int32_t mode);

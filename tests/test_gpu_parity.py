@@ -71,6 +71,34 @@ def test_conv3x3_layer(gpu_device, cin, cout, H, W):
     assert torch.all(out[:, 0] == 0) and torch.all(out[:, -1] == 0) and torch.all(out[:, :, 0] == 0)
 
 
+@pytest.mark.parametrize('cin,cout,H,W', [(72, 32, 13, 37), (136, 64, 30, 70)])
+def test_conv3x3_xcd_tile_map_bitwise(gpu_device, cin, cout, H, W):
+    """Exact-fp32 conv: XCD-grouped tile order (default) against row-major blockIdx order, bit for bit."""
+    lib = _lib.load()
+    B = 3
+    cp = cin + 8
+    x = _padded(B, H, W, cp, cin, gpu_device, 5)
+    g = torch.Generator().manual_seed(6)
+    w = torch.randn(cout, cin, 3, 3, generator=g) * 0.1
+    bd = (torch.rand(cout, generator=g) - 0.5).to(gpu_device)
+    wp = engine.pack_conv_weight(w.to(gpu_device), list(range(cin)), 32 if cout <= 32 else 64)
+    outs = []
+    try:
+        for mode in (1, 0):
+            lib.esr_x3_set_tile_map(mode)
+            out = torch.zeros(B, H + 2, W + 2, cout, device=gpu_device)
+            o = engine._conv_out(out, cout, 0, H, W, True)
+            _lib.check(lib.esr_conv3x3_fwd(x.data_ptr(), B, H, W, cp, cin, wp.data_ptr(), bd.data_ptr(), cout,
+                                           ctypes.byref(o), _stream()), 'conv')
+            torch.cuda.synchronize()
+            outs.append(out)
+    finally:
+        lib.esr_x3_set_tile_map(1)
+    assert torch.equal(outs[0], outs[1])
+    ref = F.leaky_relu(F.conv2d(_nchw(x, 0, cin), w.double(), bd.cpu().double(), padding=1), 0.2)
+    assert normwise_rel(_nchw(outs[0], 0, cout), ref) < 1e-5
+
+
 def test_conv3x3_planar_output(gpu_device):
     lib = _lib.load()
     B, H, W, cin = 2, 19, 45, 72
