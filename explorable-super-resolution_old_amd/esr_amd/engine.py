@@ -41,6 +41,28 @@ PRECISIONS = ('x3', 'f32')
 
 # Optional per-launch profiling (bench.py): a list collecting (tag, algorithmic FLOPs, start event, end event).
 _PROFILE = None
+_TIMER_POOL = {}  # op count -> esr timers created ahead of a timed region (reserve_timers)
+
+
+def reserve_timers(n_ops, count):
+    """Create `count` per-op HIP-event timers for op lists of `n_ops` launches now, so that a profiled timed region
+    takes them from the pool instead of creating n_ops + 1 events per forward inside it (hipEventCreate is a host call
+    of several µs; ~360 per forward left the GPU idle ~3 % of a bench step)."""
+    lib = _lib.load()
+    pool = _TIMER_POOL.setdefault(int(n_ops), [])
+    for _ in range(count):
+        t = lib.esr_timer_create(int(n_ops))
+        if not t:
+            raise RuntimeError('esr_amd: esr_timer_create failed')
+        pool.append(t)
+
+
+def release_timers():
+    """Destroy the timers reserve_timers created and no profiled forward used."""
+    lib = _lib.load()
+    for pool in _TIMER_POOL.values():
+        while pool:
+            lib.esr_timer_destroy(pool.pop())
 # Number of forwards recomputed in f32 after an f16-range overflow (observability; tests read it).
 OVERFLOW_RERUNS = 0
 
@@ -453,7 +475,8 @@ class _OpPlan:
                 self.ops[k].p[j] = out.data_ptr()
         timer = None
         if _PROFILE is not None:
-            timer = lib.esr_timer_create(self.n)
+            pool = _TIMER_POOL.get(self.n)
+            timer = pool.pop() if pool else lib.esr_timer_create(self.n)
             if not timer:
                 raise RuntimeError('esr_amd: esr_timer_create failed')
             _PROFILE.append(('ops', self.tags, timer, self.n))
