@@ -106,6 +106,28 @@ __device__ __forceinline__ float split_at(const float *buf, long long pix, int c
     return (float)g[ch & 7] + (float)g[8 + (ch & 7)];
 }
 
+// Output location of tile pixel q (tile rows of width tw from tall padded row r_first + 1, column x0): padded output
+// pixel index, image, output row / column; false if q is past the tile, or on a halo row or past the batch.
+__device__ __forceinline__ bool locate_q(const X3Params &p, int q, int r_first, int x0, int tw, int nq,
+                                         long long &opix, int &b, int &oy, int &ox) {
+    const esr_conv_out &o = p.o;
+    const int HP = p.H + 2;
+    const int b0 = r_first / HP;
+    const int row = (tw == TWF) ? (q >> 5) : q / tw;
+    const int col = q - row * tw;
+    int yy = r_first + 1 + row - b0 * HP;
+    b = b0;
+    while (yy >= HP) {
+        yy -= HP;
+        ++b;
+    }
+    const int y = yy - 1;
+    oy = o.out_sy * y + o.out_oy;
+    ox = o.out_sx * (x0 + col) + o.out_ox;
+    opix = ((long long)b * (o.out_h + 2) + oy + 1) * (long long)(o.out_w + 2) + ox + 1;
+    return q < nq && b < p.B && y >= 0 && y < p.H;
+}
+
 // store_px: NTH_ cooperating threads (thread index t) store NPX consecutive pixels q0 .. q0+NPX-1 of the tile, whose
 // accumulators s_ep holds in rows 0 .. NPX-1 (a whole tile by the workgroup, or one 32-pixel M-tile by its wave).
 template <int N, int NTH_, int NPX>
@@ -116,23 +138,8 @@ __device__ __forceinline__ bool store_px(const X3Params &p, const float *s_ep, i
     constexpr int PPI = NTH_ / GROUPS;         // pixels per iteration
     constexpr int ITERS = NPX / PPI;
     const esr_conv_out &o = p.o;
-    const long long orow = (long long)(o.out_w + 2);
-    const int HP = p.H + 2;
-    const int b0 = r_first / HP;
     auto locate = [&](int q, long long &opix, int &b, int &oy, int &ox) {
-        const int row = (tw == TWF) ? (q >> 5) : q / tw;
-        const int col = q - row * tw;
-        int yy = r_first + 1 + row - b0 * HP;
-        b = b0;
-        while (yy >= HP) {
-            yy -= HP;
-            ++b;
-        }
-        const int y = yy - 1;
-        oy = o.out_sy * y + o.out_oy;
-        ox = o.out_sx * (x0 + col) + o.out_ox;
-        opix = ((long long)b * (o.out_h + 2) + oy + 1) * orow + ox + 1;
-        return q < nq && b < p.B && y >= 0 && y < p.H;
+        return locate_q(p, q, r_first, x0, tw, nq, opix, b, oy, ox);
     };
     if (o.out_planar) {
         for (int it = t; it < NPX * p.cout; it += NTH_) {
@@ -255,9 +262,13 @@ __device__ __forceinline__ void lgkm_wait(f16x8 (&f)[K]) {
 // workgroups per CU (4 waves per SIMD: <= 128 VGPRs; the second launch-bounds argument is waves per SIMD), so one
 // workgroup's DMA waits, prologue and epilogue overlap the other's MFMAs.  THT: tile height (16: two 32-pixel M-tiles
 // per wave; 8: one, which halves the accumulators and the epilogue staging so N = 64 also fits two per CU).
+// DE (direct epilogue, N = 32): the MFMA operands are swapped (weights as A, pixels as B), so each lane ends with
+// channels of ONE pixel; one v_permlane32_swap per register pair gathers 8 consecutive channels (one split group) per
+// lane, and every lane finishes and stores its groups straight from registers: no LDS restage, no barrier.
 template <int NT, int TS, bool ASMRD = true, int PFD = (NT == 1 ? 2 : 1), bool OS = false, int THT = TH,
-          int WPS = (OS ? 4 : 1)>
+          int WPS = (OS ? 4 : 1), bool DE = false>
 __global__ __launch_bounds__(NTHR, WPS) void conv_x3_kernel(X3Params p) {
+    static_assert(!DE || (NT == 1 && ASMRD), "direct epilogue: N = 32, explicit fragment reads");
     constexpr int MTW = THT / 8;  // M-tiles per wave
     constexpr int HYT = THT + 2;
     constexpr int IN_RECS_T = (HYT * HXF + 15) / 16 * 16;
@@ -401,21 +412,23 @@ __global__ __launch_bounds__(NTHR, WPS) void conv_x3_kernel(X3Params p) {
             else if (ahead == 1) lgkm_wait<NR>(f[cb]);
             else lgkm_wait<0>(f[cb]);
             f16x8 *q = f[cb];
+            // (a, b) -> MFMA operands in the kernel's orientation: pixels x channels, or channels x pixels (DE)
+            auto mma = [&](const f16x8 &a, const f16x8 &b, f32x16 &c) {
+                if constexpr (DE) c = __builtin_amdgcn_mfma_f32_32x32x16_f16(b, a, c, 0, 0, 0);
+                else c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+            };
 #pragma unroll
             for (int mt = 0; mt < MTW; ++mt)
 #pragma unroll
-                for (int nt = 0; nt < NT; ++nt)
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(q[2 * mt + 1], q[2 * MTW + 2 * nt], acc[mt][nt], 0, 0, 0);
+                for (int nt = 0; nt < NT; ++nt) mma(q[2 * mt + 1], q[2 * MTW + 2 * nt], acc[mt][nt]);
 #pragma unroll
             for (int mt = 0; mt < MTW; ++mt)
 #pragma unroll
-                for (int nt = 0; nt < NT; ++nt)
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(q[2 * mt], q[2 * MTW + 1 + 2 * nt], acc[mt][nt], 0, 0, 0);
+                for (int nt = 0; nt < NT; ++nt) mma(q[2 * mt], q[2 * MTW + 1 + 2 * nt], acc[mt][nt]);
 #pragma unroll
             for (int mt = 0; mt < MTW; ++mt)
 #pragma unroll
-                for (int nt = 0; nt < NT; ++nt)
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(q[2 * mt], q[2 * MTW + 2 * nt], acc[mt][nt], 0, 0, 0);
+                for (int nt = 0; nt < NT; ++nt) mma(q[2 * mt], q[2 * MTW + 2 * nt], acc[mt][nt]);
         }
     };
     auto compute = [&](const unsigned char *s_in, const unsigned char *s_w) {
@@ -484,6 +497,66 @@ __global__ __launch_bounds__(NTHR, WPS) void conv_x3_kernel(X3Params p) {
         if (j + 2 < nchunk) dma(j + 2, 0);
         if (mvalid[0]) compute(lds + IN_B, lds + 2 * IN_B + W_B);
     }
+    }
+
+    if constexpr (DE) {
+        // acc[mt][0][r] = channel 8 (r >> 2) + 4 hl + (r & 3) of pixel 32 jm + ml.  Swapping registers r = 4..7 of
+        // lanes 0-31 with r = 0..3 of lanes 32-63 (and r = 12..15 with 8..11) leaves every lane with channels
+        // 8 (2 s + hl) + j in registers 8 s + j, j = 0..7: split groups 2 s + hl, s = 0, 1.
+        const esr_conv_out &o = p.o;
+        bool ok = true;
+#pragma unroll
+        for (int mt = 0; mt < MTW; ++mt) {
+            if (!mvalid[mt]) continue;
+            f32x16 &a = acc[mt][0];
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    // v_permlane32_swap: lanes 32-63 of the first operand <-> lanes 0-31 of the second
+                    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a[8 * s + k]),
+                                                                    __float_as_uint(a[8 * s + 4 + k]), false, false);
+                    a[8 * s + k] = __uint_as_float(r[0]);
+                    a[8 * s + 4 + k] = __uint_as_float(r[1]);
+                }
+            long long opix;
+            int b, oy, ox;
+            if (!locate_q(p, 32 * (MTW * wave + mt) + ml, r0, x0, tw, nq, opix, b, oy, ox)) continue;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int c = 8 * (2 * s + hl);
+                if (c >= p.cout) continue;
+                float v[8], r1v[8], r2v[8];
+                if (!o.out_planar) {
+                    if (o.r1) load_group(reinterpret_cast<const unsigned char *>(o.r1) + (opix * o.r1_cp + o.r1_coff + c) * 4, r1v);
+                    if (o.r2) load_group(reinterpret_cast<const unsigned char *>(o.r2) + (opix * o.r2_cp + o.r2_coff + c) * 4, r2v);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        r1v[j] = (o.r1 && c + j < p.cout) ? split_at(o.r1, opix, o.r1_cp, o.r1_coff + c + j) : 0.f;
+                        r2v[j] = (o.r2 && c + j < p.cout) ? split_at(o.r2, opix, o.r2_cp, o.r2_coff + c + j) : 0.f;
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    v[j] = a[8 * s + j] * p.w_scale_inv + ((c + j < p.cout) ? p.bias[c + j] : 0.f);
+                    if (o.lrelu) v[j] = lrelu(v[j]);
+                    if (o.r1) v[j] = o.s1 * v[j] + r1v[j];
+                    if (o.r2) v[j] = o.s2 * v[j] + r2v[j];
+                }
+                if (o.out_planar) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+                        if (c + j < p.cout) o.out[(((long long)b * p.cout + c + j) * o.out_h + oy) * o.out_w + ox] = v[j];
+                } else {
+                    ok &= store_group(reinterpret_cast<unsigned char *>(o.out) + (opix * o.out_cp + o.out_coff + c) * 4, v);
+                    if (o.out2)
+                        store_group(reinterpret_cast<unsigned char *>(o.out2) + (opix * o.out2_cp + o.out2_coff + c) * 4, v);
+                }
+            }
+        }
+        if (!ok && p.overflow) atomicOr(p.overflow, 1);
+        return;
     }
 
     // ---- epilogue: restage fp32 accumulators as [pixel][channel] ----
@@ -1110,6 +1183,15 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
         p.tiles_y = (B * (H + 2) - 2 + 7) / 8;
         const dim3 grid8((unsigned)(p.tiles_x * p.tiles_y));
         hipLaunchKernelGGL((conv_x3_kernel<2, 3, true, 1, true, 8>), grid8, block, 0, stream, p);
+    } else if (taps_side == 3 && cout <= 32 && (g_x3_kernel == 27 || g_x3_kernel == 28)) {
+        // N = 32 with the direct (register) epilogue: 27 = 16-row tiles at two workgroups per CU, 28 = 8-row at three
+        if (g_x3_kernel == 28) {
+            p.tiles_y = (B * (H + 2) - 2 + 7) / 8;
+            const dim3 grid8((unsigned)(p.tiles_x * p.tiles_y));
+            hipLaunchKernelGGL((conv_x3_kernel<1, 3, true, 1, true, 8, 6, true>), grid8, block, 0, stream, p);
+        } else {
+            hipLaunchKernelGGL((conv_x3_kernel<1, 3, true, 1, true, TH, 4, true>), grid, block, 0, stream, p);
+        }
     } else if (taps_side == 3 && cout <= 32 && g_x3_kernel != 22 && g_x3_kernel != 26 &&
                (g_x3_kernel == 25 || row8_pays)) {
         // N = 32 with 8-row tiles (one 32-pixel M-tile per wave), one stage, three workgroups per CU (<= 80 VGPRs)
@@ -1142,7 +1224,7 @@ extern "C" int esr_conv3x3_fwd_x3(const void *in, int32_t B, int32_t H, int32_t 
 }
 
 extern "C" int esr_x3_set_kernel(int32_t variant) {
-    if (variant < 0 || variant > 26) return ESR_EINVAL;
+    if (variant < 0 || variant > 28) return ESR_EINVAL;
     const int prev = g_x3_kernel;
     g_x3_kernel = variant;
     return prev;

@@ -324,7 +324,7 @@ def test_x3_ring_kernel_bitwise_equals_classic(gpu_device, cin, cout, B, H, W):
     try:
         # classic one-stage (default), ring always, persistent ring always, ring / classic with the compiler-scheduled
         # fragment reads, two-stage classic with prefetch 1 / 2 (none may change a bit)
-        for variant in (0, 2, 17, 18, 20, 21, 22, 25, 26):
+        for variant in (0, 2, 17, 18, 20, 21, 22, 25, 26, 27, 28):
             lib.esr_x3_set_kernel(variant)
             out = torch.zeros(B, H + 2, W + 2, 40, device=gpu_device)
             out2 = torch.zeros(B, H + 2, W + 2, 32, device=gpu_device)
@@ -399,7 +399,8 @@ def test_x3_xcd_tile_map_bitwise(gpu_device, cout, cin, B, H, W):
     assert normwise_rel(_nchw(engine.from_split(outs[0]), 0, cout), ref) < 1e-5
 
 
-def test_conv3x3_x3_planar_output(gpu_device):
+@pytest.mark.parametrize('variant', [1, 27, 28])  # default, direct register epilogue 16- / 8-row
+def test_conv3x3_x3_planar_output(gpu_device, variant):
     lib = _lib.load()
     B, H, W, cin = 2, 19, 45, 72
     x = engine.to_split(_padded(B, H, W, cin, cin, gpu_device, 14))
@@ -408,9 +409,14 @@ def test_conv3x3_x3_planar_output(gpu_device):
     wx, scale = engine.pack_x3(engine.pack_conv_weight(w.to(gpu_device), list(range(cin)), 32))
     out = torch.full((B, 3, H, W), 7.0, device=gpu_device)
     o = engine._conv_out(out, 0, 0, H, W, False, planar=1)
-    _lib.check(lib.esr_conv3x3_fwd_x3(x.data_ptr(), B, H, W, cin, cin, wx.data_ptr(), b.to(gpu_device).data_ptr(),
-                                      scale, 3, ctypes.byref(o), None, _stream()), 'conv_x3')
-    torch.cuda.synchronize()
+    try:
+        lib.esr_x3_set_kernel(variant)
+        _lib.check(lib.esr_conv3x3_fwd_x3(x.data_ptr(), B, H, W, cin, cin, wx.data_ptr(),
+                                          b.to(gpu_device).data_ptr(), scale, 3, ctypes.byref(o), None, _stream()),
+                   'conv_x3')
+        torch.cuda.synchronize()
+    finally:
+        lib.esr_x3_set_kernel(1)
     ref = F.conv2d(_nchw(engine.from_split(x), 0, cin), w.double(), b.double(), padding=1)
     assert normwise_rel(out.cpu(), ref) < 1e-5
 
