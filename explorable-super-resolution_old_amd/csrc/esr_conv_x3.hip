@@ -266,8 +266,10 @@ __device__ __forceinline__ void lgkm_wait(f16x8 (&f)[K]) {
 // channels of ONE pixel; one v_permlane32_swap per register pair gathers 8 consecutive channels (one split group) per
 // lane, and every lane finishes and stores its groups straight from registers: no LDS restage, no barrier.
 template <int NT, int TS, bool ASMRD = true, int PFD = (NT == 1 ? 2 : 1), bool OS = false, int THT = TH,
-          int WPS = (OS ? 4 : 1), bool DE = false>
+          int WPS = (OS ? 4 : 1), bool DE = false, int DBGX = 0>
 __global__ __launch_bounds__(NTHR, WPS) void conv_x3_kernel(X3Params p) {
+    // DBGX (diagnostic builds, esr_x3_set_kernel 29 / 30; outputs are garbage): 1 = LDS-DMA of chunk 0 only, 2 = no
+    // fragment reads / MFMAs
     static_assert(!DE || (NT == 1 && ASMRD), "direct epilogue: N = 32, explicit fragment reads");
     constexpr int MTW = THT / 8;  // M-tiles per wave
     constexpr int HYT = THT + 2;
@@ -479,10 +481,10 @@ __global__ __launch_bounds__(NTHR, WPS) void conv_x3_kernel(X3Params p) {
     if constexpr (OS) {
         for (int j = 0; j < nchunk; ++j) {
             if (j) __syncthreads();  // every wave is done reading the stage
-            dma(j, 0);
+            if (!(DBGX & 1) || j == 0) dma(j, 0);
             wait_vm_lgkm0<0>();
             __syncthreads();
-            if (mvalid[0]) compute(lds, lds + IN_B);
+            if (mvalid[0] && !(DBGX & 2)) compute(lds, lds + IN_B);
         }
     } else {
     dma(0, 0);
@@ -1183,6 +1185,10 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
         p.tiles_y = (B * (H + 2) - 2 + 7) / 8;
         const dim3 grid8((unsigned)(p.tiles_x * p.tiles_y));
         hipLaunchKernelGGL((conv_x3_kernel<2, 3, true, 1, true, 8>), grid8, block, 0, stream, p);
+    } else if (taps_side == 3 && cout <= 32 && (g_x3_kernel == 29 || g_x3_kernel == 30)) {
+        // diagnostics of the 16-row one-stage kernel: 29 = no LDS-DMA after chunk 0, 30 = no compute
+        if (g_x3_kernel == 29) hipLaunchKernelGGL((conv_x3_kernel<1, 3, true, 1, true, TH, 4, false, 1>), grid, block, 0, stream, p);
+        else hipLaunchKernelGGL((conv_x3_kernel<1, 3, true, 1, true, TH, 4, false, 2>), grid, block, 0, stream, p);
     } else if (taps_side == 3 && cout <= 32 && (g_x3_kernel == 27 || g_x3_kernel == 28)) {
         // N = 32 with the direct (register) epilogue: 27 = 16-row tiles at two workgroups per CU, 28 = 8-row at three
         if (g_x3_kernel == 28) {
@@ -1224,7 +1230,7 @@ extern "C" int esr_conv3x3_fwd_x3(const void *in, int32_t B, int32_t H, int32_t 
 }
 
 extern "C" int esr_x3_set_kernel(int32_t variant) {
-    if (variant < 0 || variant > 28) return ESR_EINVAL;
+    if (variant < 0 || variant > 30) return ESR_EINVAL;
     const int prev = g_x3_kernel;
     g_x3_kernel = variant;
     return prev;
