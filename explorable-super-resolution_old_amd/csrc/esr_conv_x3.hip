@@ -32,6 +32,7 @@
 // 1/w_scale, bias, LeakyReLU, residuals (split inputs), split + 16-byte stores, or fp32 planar stores for CEM.
 #include <hip/hip_runtime.h>
 #include "esr_amd.h"
+#include "esr_x3c.h"
 
 extern int esr_g_conv_tile_map;  // esr_conv.hip: the exact-fp32 conv kernel's tile order
 
@@ -325,26 +326,28 @@ __global__ __launch_bounds__(NTHR, WPS) void conv_x3_kernel(X3Params p) {
             in_hi[i] = s >> 1;
         }
     }
-    auto dma = [&](int j, int st) {
-        const int groups = min(16, p.cin - 16 * j) >> 3;
-#pragma unroll
-        for (int i = 0; i < KIN; ++i) {
-            const int k = wave + NWAVES * i;
-            if (k >= IN_RECS_T / 16) break;
-            const void *src = (in_hi[i] >= 0 && in_hi[i] < groups) ? (const void *)(p.in + in_src[i] + 64LL * j)
+    // LDS-DMA piece q (0 .. KIN + KW - 1: input pieces, then weight pieces) of chunk j into stage st; pieces past the
+    // tile are skipped (wave-uniform)
+    auto dma_piece = [&](int j, int st, int q) {
+        if (q < KIN) {
+            const int k = wave + NWAVES * q;
+            if (k >= IN_RECS_T / 16) return;
+            const int groups = min(16, p.cin - 16 * j) >> 3;
+            const void *src = (in_hi[q] >= 0 && in_hi[q] < groups) ? (const void *)(p.in + in_src[q] + 64LL * j)
                                                                    : (const void *)g_zero_page;
             __builtin_amdgcn_global_load_lds((glob_void *)src, (lds_void *)(lds + st * IN_B + k * 1024), 16, 0, 0);
-        }
-        const unsigned char *wj = p.w + (long long)j * W_B;
-#pragma unroll
-        for (int i = 0; i < KW; ++i) {
-            const int k = wave + NWAVES * i;
-            if (k >= W_RECS / 16) break;
+        } else {
+            const int k = wave + NWAVES * (q - KIN);
+            if (k >= W_RECS / 16) return;
             const int r = 16 * k + sub;
             const int s = ps ^ ((r >> 2) & 3);
-            __builtin_amdgcn_global_load_lds((glob_void *)(wj + r * REC + (s << 4)),
+            __builtin_amdgcn_global_load_lds((glob_void *)(p.w + (long long)j * W_B + r * REC + (s << 4)),
                                              (lds_void *)(lds + NST * IN_B + st * W_B + k * 1024), 16, 0, 0);
         }
+    };
+    auto dma = [&](int j, int st) {
+#pragma unroll
+        for (int q = 0; q < KIN + KW; ++q) dma_piece(j, st, q);
     };
 
     int aoff[T][MTW][2];
@@ -380,7 +383,7 @@ __global__ __launch_bounds__(NTHR, WPS) void conv_x3_kernel(X3Params p) {
     // Explicit ds_read_b128 fragment reads PFD taps ahead with counted lgkmcnt waits (see the ring kernel's
     // compute_asm); MFMAs unpredicated, the order per accumulator unchanged.  PFD = 2 needs 2 x NR < 16 (4-bit
     // lgkmcnt): N = 32 only.
-    auto compute_asm = [&](const unsigned char *s_in, const unsigned char *s_w) {
+    auto compute_asm = [&](const unsigned char *s_in, const unsigned char *s_w, auto &&hook) {
         constexpr int NR = 2 * MTW + 2 * NT;  // [ah0, al0, (ah1, al1), bh0, bl0, (bh1, bl1)]
         constexpr int NBUF = PFD + 1;
         static_assert(PFD * NR < 16, "lgkmcnt is a 4-bit count");
@@ -419,6 +422,7 @@ __global__ __launch_bounds__(NTHR, WPS) void conv_x3_kernel(X3Params p) {
                 if constexpr (DE) c = __builtin_amdgcn_mfma_f32_32x32x16_f16(b, a, c, 0, 0, 0);
                 else c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
             };
+            if constexpr ((DBGX & 8) != 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
             for (int mt = 0; mt < MTW; ++mt)
 #pragma unroll
@@ -431,11 +435,13 @@ __global__ __launch_bounds__(NTHR, WPS) void conv_x3_kernel(X3Params p) {
             for (int mt = 0; mt < MTW; ++mt)
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt) mma(q[2 * mt], q[2 * MTW + 2 * nt], acc[mt][nt]);
+            if constexpr ((DBGX & 8) != 0) __builtin_amdgcn_s_setprio(0);
+            hook(tap);  // e.g. the next chunk's LDS-DMA pieces, issued behind this tap's MFMAs
         }
     };
-    auto compute = [&](const unsigned char *s_in, const unsigned char *s_w) {
+    auto compute = [&](const unsigned char *s_in, const unsigned char *s_w, auto &&hook) {
         if constexpr (ASMRD) {
-            compute_asm(s_in, s_w);
+            compute_asm(s_in, s_w, hook);
             return;
         }
         constexpr int NBUF = X3_PF + 1;
@@ -474,30 +480,50 @@ __global__ __launch_bounds__(NTHR, WPS) void conv_x3_kernel(X3Params p) {
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt)
                     if (mvalid[mt]) acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[cb][mt], bh[cb][nt], acc[mt][nt], 0, 0, 0);
+            hook(tap);
         }
     };
 
     // the explicit vmcnt(0) before each barrier: compute_asm's reads are invisible to the compiler's LDS-DMA tracking
+    auto none = [](int) {};
     if constexpr (OS) {
         for (int j = 0; j < nchunk; ++j) {
             if (j) __syncthreads();  // every wave is done reading the stage
             if (!(DBGX & 1) || j == 0) dma(j, 0);
             wait_vm_lgkm0<0>();
             __syncthreads();
-            if (mvalid[0] && !(DBGX & 2)) compute(lds, lds + IN_B);
+            if (mvalid[0] && !(DBGX & 2)) compute(lds, lds + IN_B, none);
         }
     } else {
+    // IL (DBGX & 4): the next chunk's LDS-DMA pieces are spread over the first taps of this chunk, two behind each
+    // tap's MFMAs, instead of issued as one burst before them (an LDS-DMA issue stalls the issuing wave ~60-180
+    // cycles; as a burst both waves of a SIMD stall together and the matrix pipe idles)
+    constexpr int NPC = KIN + KW;
+    auto next = [&](int j, int st) {
+        return [&, j, st](int tap) {
+            if constexpr ((DBGX & 4) != 0) {
+                if (j < nchunk && !(DBGX & 1)) {
+                    constexpr int PER = (NPC + 4) / 5;  // pieces per tap over the first five taps
+#pragma unroll
+                    for (int e = 0; e < PER; ++e)
+                        if (PER * tap + e < NPC) dma_piece(j, st, PER * tap + e);
+                }
+            }
+        };
+    };
     dma(0, 0);
     for (int j = 0; j < nchunk; j += 2) {
         wait_vm_lgkm0<0>();
         __syncthreads();
-        if (j + 1 < nchunk) dma(j + 1, 1);
-        if (mvalid[0]) compute(lds, lds + 2 * IN_B);
+        if (!(DBGX & 4) && !(DBGX & 1) && j + 1 < nchunk) dma(j + 1, 1);
+        if (mvalid[0] && !(DBGX & 2)) compute(lds, lds + 2 * IN_B, next(j + 1, 1));
+        else if (DBGX & 4) for (int q = 0; q < NPC; ++q) if (j + 1 < nchunk && !(DBGX & 1)) dma_piece(j + 1, 1, q);
         if (j + 1 >= nchunk) break;
         wait_vm_lgkm0<0>();
         __syncthreads();
-        if (j + 2 < nchunk) dma(j + 2, 0);
-        if (mvalid[0]) compute(lds + IN_B, lds + 2 * IN_B + W_B);
+        if (!(DBGX & 4) && !(DBGX & 1) && j + 2 < nchunk) dma(j + 2, 0);
+        if (mvalid[0] && !(DBGX & 2)) compute(lds + IN_B, lds + 2 * IN_B + W_B, next(j + 2, 0));
+        else if (DBGX & 4) for (int q = 0; q < NPC; ++q) if (j + 2 < nchunk && !(DBGX & 1)) dma_piece(j + 2, 0, q);
     }
     }
 
@@ -577,6 +603,7 @@ __global__ __launch_bounds__(NTHR, WPS) void conv_x3_kernel(X3Params p) {
     }
     __syncthreads();
 
+    if constexpr ((DBGX & 16) != 0) return;  // diagnostic: no epilogue stores
     const bool ok = store_px<N, NTHR, THT * TWF>(p, s_ep, 0, r0, x0, tw, nq, tid);
     if (!ok && p.overflow) atomicOr(p.overflow, 1);
 }
@@ -1151,10 +1178,12 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
     }
     if (taps_side == 3 && cout <= 32 && ((g_x3_kernel >= 2 && g_x3_kernel < 20) || (g_x3_kernel == 1 && ring_pays))) {
         const dim3 grid2((unsigned)pairs);
-#define RING_DBG(v, bits) \
-    case v: hipLaunchKernelGGL((conv_x3_ring_kernel<3, true, bits>), grid2, block, 0, stream, p); break;
         switch (g_x3_kernel) {
         case 15: hipLaunchKernelGGL((conv_x3_ring_kernel<3, true>), grid2, block, 0, stream, p); break;
+        case 18: hipLaunchKernelGGL((conv_x3_ring_kernel<3, false, 256>), grid2, block, 0, stream, p); break;
+#ifdef ESR_X3_EXPERIMENTS  // ablations of the ring kernel (garbage outputs): the experiment library only
+#define RING_DBG(v, bits) \
+    case v: hipLaunchKernelGGL((conv_x3_ring_kernel<3, true, bits>), grid2, block, 0, stream, p); break;
         RING_DBG(3, 1)
         RING_DBG(4, 2)
         RING_DBG(5, 4)
@@ -1167,14 +1196,57 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
         RING_DBG(12, 4 | 1 | 128)
         RING_DBG(13, 64)
         RING_DBG(14, 2 | 128)
-        case 18: hipLaunchKernelGGL((conv_x3_ring_kernel<3, false, 256>), grid2, block, 0, stream, p); break;
         case 19: hipLaunchKernelGGL((conv_x3_ring_kernel<3, false, 512>), grid2, block, 0, stream, p); break;
+#undef RING_DBG
+#endif
         default: hipLaunchKernelGGL((conv_x3_ring_kernel<3, false>), grid2, block, 0, stream, p);
         }
-#undef RING_DBG
         return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
     }
     const dim3 grid((unsigned)(p.tiles_x * p.tiles_y));
+    // Default (variant 1) since round 2: the column-tile kernel (esr_conv_x3c.hip) for 3x3 convs with cout > 32, and
+    // with cout <= 32 where the 16-row classic grid fills its rounds (2-6 % faster per launch at the config-2/3
+    // shapes, bitwise identical; profiles/r2_x3c_ab.txt); where 8-row classic tiles at three workgroups per CU pay
+    // (small grids), the classic kernel stays.  Variant 24 = the round-1 automatic choice (classic only).
+    const bool x3c_pays = taps_side == 3 && (cout > 32 || !row8_pays);
+    if ((g_x3_kernel >= 50 && g_x3_kernel <= 60) || (g_x3_kernel == 1 && x3c_pays)) {  // column-tile kernels
+        X3cParams c;
+        c.in = p.in; c.B = B; c.H = H; c.W = W; c.in_cp = in_cp; c.cin = cin; c.w = p.w; c.bias = bias;
+        c.w_scale_inv = p.w_scale_inv; c.cout = cout; c.tap_y0 = ty0; c.tap_x0 = tx0; c.tiles_x = c.tiles_y = 0;
+        c.xcd_map = g_x3_map; c.overflow = overflow; c.o = *o;
+        if (g_x3_kernel == 60) return x3c_launch(c, taps_side, stream, 16);
+#ifdef ESR_X3_EXPERIMENTS  // 51-54: x3c ablations, 55-59: the warp-specialised persistent form and its ablations
+        static const int dbg[5] = {0, 1, 2, 4, 5};
+        if (g_x3_kernel >= 55) return x3s_launch(c, taps_side, stream, dbg[g_x3_kernel - 55]);
+        return x3c_launch(c, taps_side, stream, dbg[g_x3_kernel - 50]);
+#else
+        return x3c_launch(c, taps_side, stream, 0);
+#endif
+    }
+#ifdef ESR_X3_EXPERIMENTS  // DBGX ablations of the classic kernel (40-46; 29/30 below), garbage outputs
+    if (taps_side == 3 && g_x3_kernel >= 40 && g_x3_kernel < 50) {
+#define XV(NT_, fl) hipLaunchKernelGGL((conv_x3_kernel<NT_, 3, true, (NT_ == 1 ? 2 : 1), false, TH, 1, false, fl>), grid, block, 0, stream, p)
+        const bool n64 = cout > 32;
+        switch (g_x3_kernel) {
+        case 40: if (n64) XV(2, 4); else XV(1, 4); break;
+        case 41: if (n64) XV(2, 4 | 8); else XV(1, 4 | 8); break;
+        case 42: if (n64) XV(2, 1); else XV(1, 1); break;
+        case 43: if (n64) XV(2, 2); else XV(1, 2); break;
+        case 44: if (n64) XV(2, 16); else XV(1, 16); break;
+        case 45: if (n64) XV(2, 8); else XV(1, 8); break;
+        case 46: if (n64) XV(2, 4 | 16); else XV(1, 4 | 16); break;
+        default: if (n64) XV(2, 0); else XV(1, 0);
+        }
+#undef XV
+        return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+    }
+    if (taps_side == 3 && cout <= 32 && (g_x3_kernel == 29 || g_x3_kernel == 30)) {
+        // the 16-row one-stage kernel: 29 = no LDS-DMA after chunk 0, 30 = no compute
+        if (g_x3_kernel == 29) hipLaunchKernelGGL((conv_x3_kernel<1, 3, true, 1, true, TH, 4, false, 1>), grid, block, 0, stream, p);
+        else hipLaunchKernelGGL((conv_x3_kernel<1, 3, true, 1, true, TH, 4, false, 2>), grid, block, 0, stream, p);
+        return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+    }
+#endif
     if (taps_side == 3 && g_x3_kernel == 20) {  // A/B: the classic kernel with compiler-scheduled fragment reads
         if (cout > 32) hipLaunchKernelGGL((conv_x3_kernel<2, 3, false>), grid, block, 0, stream, p);
         else hipLaunchKernelGGL((conv_x3_kernel<1, 3, false>), grid, block, 0, stream, p);
@@ -1185,10 +1257,6 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
         p.tiles_y = (B * (H + 2) - 2 + 7) / 8;
         const dim3 grid8((unsigned)(p.tiles_x * p.tiles_y));
         hipLaunchKernelGGL((conv_x3_kernel<2, 3, true, 1, true, 8>), grid8, block, 0, stream, p);
-    } else if (taps_side == 3 && cout <= 32 && (g_x3_kernel == 29 || g_x3_kernel == 30)) {
-        // diagnostics of the 16-row one-stage kernel: 29 = no LDS-DMA after chunk 0, 30 = no compute
-        if (g_x3_kernel == 29) hipLaunchKernelGGL((conv_x3_kernel<1, 3, true, 1, true, TH, 4, false, 1>), grid, block, 0, stream, p);
-        else hipLaunchKernelGGL((conv_x3_kernel<1, 3, true, 1, true, TH, 4, false, 2>), grid, block, 0, stream, p);
     } else if (taps_side == 3 && cout <= 32 && (g_x3_kernel == 27 || g_x3_kernel == 28)) {
         // N = 32 with the direct (register) epilogue: 27 = 16-row tiles at two workgroups per CU, 28 = 8-row at three
         if (g_x3_kernel == 28) {
@@ -1230,7 +1298,13 @@ extern "C" int esr_conv3x3_fwd_x3(const void *in, int32_t B, int32_t H, int32_t 
 }
 
 extern "C" int esr_x3_set_kernel(int32_t variant) {
-    if (variant < 0 || variant > 30) return ESR_EINVAL;
+    if (variant < 0 || variant > 60) return ESR_EINVAL;
+#ifndef ESR_X3_EXPERIMENTS
+    // the production library carries the bitwise-identical A/B variants only (include/esr_amd.h)
+    const bool ab = variant <= 2 || variant == 15 || (variant >= 16 && variant <= 18) ||
+                    (variant >= 20 && variant <= 28) || variant == 50 || variant == 60;
+    if (!ab) return ESR_EINVAL;
+#endif
     const int prev = g_x3_kernel;
     g_x3_kernel = variant;
     return prev;

@@ -1,0 +1,727 @@
+// esr_conv_x3c.hip — x3 (split-f16) 3×3 convolution / polyphase upconv, column-tile form.
+//
+// Same numerics, layouts and epilogue contract as esr_conv_x3.hip (read that header first): fp32 values carried as f16
+// hi/lo pairs, each product a·b = a_hi·b_hi + a_hi·b_lo + a_lo·b_hi on v_mfma_f32_32x32x16_f16 with fp32 accumulation.
+// What differs is how the work is cut, to spend fewer LDS reads and no VALU per MFMA:
+//
+//  * An M-tile (the 32 MFMA rows) is a COLUMN segment of 32 pixels of the tall batch image (B·(H+2) rows, halo rows
+//    between images are the vertical padding).  The tall dimension is a multiple of 32 at every bench shape, so no
+//    M-tile is partial; the width needs no multiple of 32 either (a tile is 16 columns; waves past the image width skip
+//    their MFMAs).
+//  * A workgroup (256 threads, 4 waves) owns a 32-row × 16-column output tile; wave w owns tile columns 4w..4w+3.
+//    Two workgroups share a CU (one LDS stage each), so one's LDS-DMA, barriers and epilogue overlap the other's MFMAs.
+//  * Column reuse: the A fragment of (halo column hx, tap row dy) is read from LDS once and feeds every output column
+//    c = hx - dx of the wave (up to 3 taps), and each wave keeps the B fragments (weights) of all taps of a 32-channel
+//    N-tile in registers for the whole K chunk.  Per 16-channel chunk a wave issues 36 A reads + 18 B reads per N-tile
+//    for 108 MFMAs (the row-tile kernel: 1 read per MFMA at N = 32).
+//  * LDS images are column-major: input record (hx, hy) at hx·34 + hy, its four 16-B slots XOR-swizzled by (hy>>2)&3
+//    (applied on the DMA source address: the LDS-DMA destination is lane-linear), so a column shift is an immediate
+//    offset and only the three tap rows need per-lane address registers; ds_read_b128 lane groups are conflict-free.
+#include <hip/hip_runtime.h>
+#include <type_traits>
+#include "esr_amd.h"
+#include "esr_x3c.h"
+
+namespace {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) const void glob_void;
+
+constexpr int REC = 64;                          // bytes per staged record: 16 channels, split
+constexpr int CT = 32;                           // tile rows = MFMA M
+constexpr int CW = 4;                            // output columns per wave
+constexpr int NWV = 4;                           // waves per workgroup
+constexpr int NTHR = 64 * NWV;
+constexpr int TWC = CW * NWV;                    // 16 output columns per tile
+constexpr int HYC = CT + 2;                      // 34 halo rows
+constexpr int HXC = TWC + 2;                     // 18 halo columns
+constexpr int IN_RECS = HYC * HXC;               // 612
+constexpr int IN_PIECES = (IN_RECS + 15) / 16;   // 39 one-KB LDS-DMA wave-instructions
+constexpr int IN_B = IN_PIECES * 16 * REC;       // 39936
+constexpr int KIN = (IN_PIECES + NWV - 1) / NWV; // input pieces per wave (10)
+constexpr int N_XCD = 8;
+
+__device__ __attribute__((aligned(16))) unsigned char g_zero64[64];
+
+__device__ __forceinline__ float lrelu(float v) { return v > 0.f ? v : 0.2f * v; }
+
+__device__ __forceinline__ void load_group(const unsigned char *p, float v[8]) {
+    const f16x8 hi = *reinterpret_cast<const f16x8 *>(p);
+    const f16x8 lo = *reinterpret_cast<const f16x8 *>(p + 16);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (float)hi[j] + (float)lo[j];
+}
+
+__device__ __forceinline__ bool store_group(unsigned char *p, const float v[8]) {
+    f16x8 hi, lo;
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        hi[j] = (_Float16)v[j];
+        lo[j] = (_Float16)(v[j] - (float)hi[j]);
+        ok = ok && (fabsf(v[j]) < 65504.f);
+    }
+    *reinterpret_cast<f16x8 *>(p) = hi;
+    *reinterpret_cast<f16x8 *>(p + 16) = lo;
+    return ok;
+}
+
+__device__ __forceinline__ float split_at(const float *buf, long long pix, int cp, int ch) {
+    const _Float16 *g = reinterpret_cast<const _Float16 *>(buf + pix * cp + (ch & ~7));
+    return (float)g[ch & 7] + (float)g[8 + (ch & 7)];
+}
+
+// blockIdx -> tile so that each XCD (blocks b, b+8, ... share one) walks one contiguous run of tiles; a bijection
+__device__ __forceinline__ int xcd_tile(int b, int nb) {
+    const int x = b % N_XCD, l = b / N_XCD, q = nb / N_XCD, r = nb % N_XCD;
+    return x < r ? x * (q + 1) + l : r * (q + 1) + (x - r) * q + l;
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+
+// One 16-byte LDS read the compiler does not track (the caller waits with lgkm_wait); OFF is the immediate offset.
+template <int OFF>
+__device__ __forceinline__ f16x8 ds_read16(uint32_t a) {
+    static_assert(OFF >= 0 && OFF < 65536, "ds_read offset");
+    f16x8 r;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF));
+    return r;
+}
+
+// s_waitcnt lgkmcnt(N) that the listed fragments pass through, so no use of them is scheduled before it
+template <int N>
+__device__ __forceinline__ void lgkm_wait2(f16x8 &a, f16x8 &b) {
+    static_assert(N >= 0 && N < 16, "lgkmcnt");
+    asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(N));
+}
+
+template <int N, int K>
+__device__ __forceinline__ void lgkm_wait_arr(f16x8 (&f)[K]) {
+    static_assert(N >= 0 && N < 16, "lgkmcnt");
+    asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(f[0]) : "i"(N));
+#pragma unroll
+    for (int i = 1; i < K; ++i) asm volatile("" : "+v"(f[i]));
+}
+
+__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// compile-time loop: f(std::integral_constant<int, i>) for i in [I, E)
+template <int I, int E, class F>
+__device__ __forceinline__ void sfor(F &&f) {
+    if constexpr (I < E) {
+        f(std::integral_constant<int, I>{});
+        sfor<I + 1, E>(f);
+    }
+}
+
+// NT: 32-channel N-tiles (cout <= 32 * NT); TS: taps per side (3: 3×3 conv; 2: one polyphase upconv phase).
+// DBG (diagnostic builds only, garbage outputs): 1 = LDS-DMA of chunk 0 only, 2 = no fragment reads / MFMAs,
+// 4 = no epilogue stores.  RB: the B fragments (weights) are loaded from global memory (L1/L2) into registers
+// instead of being staged in LDS: the LDS-DMA moves only the input halo tile (32-48 % fewer staged bytes).
+template <int NT, int TS, int DBG = 0, bool RB = false>
+__global__ __launch_bounds__(NTHR, 2) void conv_x3c_kernel(X3cParams p) {
+    constexpr int T = TS * TS;
+    constexpr int N = 32 * NT;
+    constexpr int W_RECS = T * N;
+    constexpr int W_PIECES = W_RECS / 16;
+    constexpr int KW = (W_PIECES + NWV - 1) / NWV;
+    constexpr int W_B = W_RECS * REC;
+    constexpr int LDS_BYTES = IN_B + (RB ? 0 : W_B);
+    constexpr int EP_P = N + 4;                            // epilogue row pitch (floats)
+    constexpr int NIC = CW + TS - 1;                       // halo columns a wave reads (6 for 3×3)
+    constexpr int NSTEP = NIC * TS;                        // A steps (halo column, tap row) per sweep
+    static_assert(NWV * 32 * EP_P * 4 <= IN_B, "per-wave epilogue areas fit in the input region");
+    static_assert(2 * LDS_BYTES <= 163840, "two workgroups per CU");
+    __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_BYTES];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int hl = lane >> 5;
+    const int ml = lane & 31;
+
+    const int tile = p.xcd_map ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x;
+    const int tx = tile % p.tiles_x;
+    const int ty = tile / p.tiles_x;
+    const int x0 = tx * TWC;             // first halo column = padded column x0; output padded columns x0+1+c
+    const int r0 = ty * CT;              // first halo row (tall padded image); output tall rows r0+1+m
+    const int tw = min(TWC, p.W - x0);   // valid output columns of the tile
+    const int ncw = min(CW, max(0, tw - CW * wave));  // valid output columns of this wave
+    const int rows_tot = p.B * (p.H + 2);
+    const long long rowp = (long long)(p.W + 2);
+    const long long pixb = 4LL * p.in_cp;
+    const int nchunk = (p.cin + 15) >> 4;
+    const unsigned char *tile_in = p.in + ((long long)r0 * rowp + x0) * pixb;
+
+    // ---- LDS-DMA addressing: input piece q of this wave = records 16 (wave + 4 i) .. +15, lane -> (record, slot) ----
+    const int sub = lane >> 2, ps = lane & 3;
+    unsigned in_off[KIN];  // byte offset from tile_in (slot included); bit 0 set = zero page; bit 1 = lo group
+#pragma unroll
+    for (int i = 0; i < KIN; ++i) {
+        const int q = wave + NWV * i;
+        const int r = 16 * q + sub;
+        const int hx = r / HYC, hy = r - (r / HYC) * HYC;
+        const int s = ps ^ ((hy >> 2) & 3);
+        const bool v = q < IN_PIECES && r < IN_RECS && r0 + hy < rows_tot && x0 + hx < p.W + 2;
+        in_off[i] = v ? (unsigned)((hy * rowp + hx) * pixb + (s << 4)) | ((s >> 1) << 1) : 1u;
+    }
+    auto dma = [&](int j) {
+        const int groups = min(16, p.cin - 16 * j) >> 3;  // 8-channel groups present in the chunk (1 or 2)
+#pragma unroll
+        for (int i = 0; i < KIN; ++i) {
+            const int q = wave + NWV * i;
+            if (q >= IN_PIECES) break;
+            const unsigned o = in_off[i];
+            const bool ok = !(o & 1u) && ((o >> 1) & 1u) < (unsigned)groups;
+            const void *src = ok ? (const void *)(tile_in + (o & ~3u) + 64LL * j) : (const void *)g_zero64;
+            __builtin_amdgcn_global_load_lds((glob_void *)src, (lds_void *)(lds + q * 1024), 16, 0, 0);
+        }
+        if constexpr (!RB) {
+            const unsigned char *wj = p.w + (long long)j * W_B;
+#pragma unroll
+            for (int i = 0; i < KW; ++i) {
+                const int q = wave + NWV * i;
+                if (q >= W_PIECES) break;
+                const int r = 16 * q + sub;
+                const int s = ps ^ ((r >> 2) & 3);
+                __builtin_amdgcn_global_load_lds((glob_void *)(wj + r * REC + (s << 4)),
+                                                 (lds_void *)(lds + IN_B + q * 1024), 16, 0, 0);
+            }
+        }
+    };
+
+    // ---- fragment addresses: A (pixels, halo column hx, tap row dy): lane (ml, hl) reads record hx*HYC + ml + dy,
+    // logical slot 2hl (hi) / 2hl+1 (lo); B (weights, tap t, N-tile nt): record t*N + nt*32 + ml ----
+    uint32_t a_hi[TS], a_lo[TS];
+#pragma unroll
+    for (int d = 0; d < TS; ++d) {
+        const int dy = p.tap_y0 + d;
+        const int hy = ml + dy;
+        const uint32_t o = lds_addr(lds) + hy * REC + (((2 * hl) ^ ((hy >> 2) & 3)) << 4) +
+                           (uint32_t)(CW * wave + p.tap_x0) * HYC * REC;
+        a_hi[d] = o;
+        a_lo[d] = o ^ 16u;
+    }
+    const uint32_t b_hi = lds_addr(lds) + IN_B + ml * REC + (((2 * hl) ^ ((ml >> 2) & 3)) << 4);
+    const uint32_t b_lo = b_hi ^ 16u;
+    const f16x8 *w_lane = reinterpret_cast<const f16x8 *>(p.w + ml * REC + 32 * hl);  // RB: this lane's B slice
+
+    f32x16 acc[CW][NT];
+#pragma unroll
+    for (int c = 0; c < CW; ++c)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[c][nt][r] = 0.f;
+
+    // One K chunk from the staged LDS images.  Per N-tile, a sweep over steps s = (tap row d, halo column ic),
+    // d-major: the A pair of step s is read two steps ahead and feeds the output columns c = ic - dx (taps (d, dx));
+    // only the B fragments of tap row d are live (double-buffered: row d+1 is read at the first step of row d).  All
+    // indices are compile-time, so every fragment address is a base register plus an immediate offset.  Issue order:
+    // B(0), A(0), A(1), then per step s (after its wait) B(d+1) if ic == 0, and A(s+2); LDS reads complete in order,
+    // so the wait for A(s) counts the reads issued after it, and B(d) (issued before A(d*NIC - NIC + 2)) is back by
+    // the first step of row d.
+    auto compute = [&](int j) {
+        const f16x8 *wj = w_lane + (long long)j * (W_B / 16);
+        sfor<0, NT>([&](auto NTc) {
+            constexpr int nt = decltype(NTc)::value;
+            f16x8 bh[2][TS], bl[2][TS], ah[3], al[3];
+            auto ldb = [&](auto Dc) {
+                constexpr int d = decltype(Dc)::value;
+                sfor<0, TS>([&](auto Xc) {
+                    constexpr int dx = decltype(Xc)::value, t = d * TS + dx;
+                    if constexpr (RB) {  // global (L1/L2) loads; the compiler waits for them before first use
+                        bh[d & 1][dx] = wj[(t * N + nt * 32) * (REC / 16)];
+                        bl[d & 1][dx] = wj[(t * N + nt * 32) * (REC / 16) + 1];
+                    } else {
+                        bh[d & 1][dx] = ds_read16<(t * N + nt * 32) * REC>(b_hi);
+                        bl[d & 1][dx] = ds_read16<(t * N + nt * 32) * REC>(b_lo);
+                    }
+                });
+            };
+            auto lda = [&](auto Sc) {
+                constexpr int s = decltype(Sc)::value, d = s / NIC, ic = s % NIC, buf = s % 3;
+                ah[buf] = ds_read16<ic * HYC * REC>(a_hi[d]);
+                al[buf] = ds_read16<ic * HYC * REC>(a_lo[d]);
+            };
+            ldb(std::integral_constant<int, 0>{});
+            lda(std::integral_constant<int, 0>{});
+            if constexpr (NSTEP > 1) lda(std::integral_constant<int, 1>{});
+            sfor<0, NSTEP>([&](auto Sc) {
+                constexpr int s = decltype(Sc)::value, d = s / NIC, ic = s % NIC, buf = s % 3;
+                constexpr int pd = (s - 1) / NIC, pic = (s - 1) % NIC;  // the previous step
+                constexpr int after = s == 0 ? (NSTEP > 1 ? 2 : 0)
+                                             : ((!RB && pic == 0 && pd + 1 < TS) ? 2 * TS : 0) + (s + 1 < NSTEP ? 2 : 0);
+                lgkm_wait2<after>(ah[buf], al[buf]);
+                if constexpr (ic == 0 && !RB) {  // B(d) is back too: pass its registers through an (empty) ordering point
+#pragma unroll
+                    for (int x = 0; x < TS; ++x) asm volatile("" : "+v"(bh[d & 1][x]), "+v"(bl[d & 1][x]));
+                }
+                if constexpr (ic == 0 && d + 1 < TS) ldb(std::integral_constant<int, d + 1>{});
+                if constexpr (s + 2 < NSTEP) lda(std::integral_constant<int, s + 2>{});
+                // products lo*hi, hi*lo, hi*hi, each over the output columns c = ic - dx this A pair feeds
+                sfor<0, 3>([&](auto Pc) {
+                    constexpr int pr = decltype(Pc)::value;
+                    sfor<0, TS>([&](auto Xc) {
+                        constexpr int dx = decltype(Xc)::value, c = ic - dx;
+                        if constexpr (c >= 0 && c < CW) {
+                            const f16x8 &a = pr == 0 ? al[buf] : ah[buf];
+                            const f16x8 &b = pr == 1 ? bl[d & 1][dx] : bh[d & 1][dx];
+                            acc[c][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc[c][nt], 0, 0, 0);
+                        }
+                    });
+                });
+            });
+        });
+    };
+
+    for (int j = 0; j < nchunk; ++j) {
+        if (j) __builtin_amdgcn_s_barrier();  // every wave is done reading the stage (its reads were waited for)
+        if (!(DBG & 1) || j == 0) dma(j);
+        wait_vm0();
+        __builtin_amdgcn_s_barrier();
+        if (ncw > 0 && !(DBG & 2)) compute(j);
+    }
+
+    // ---- epilogue: each wave restages one output column at a time through its own LDS area and stores it ----
+    __builtin_amdgcn_s_barrier();  // all waves are done with the input stage it aliases
+    if (ncw <= 0) return;
+    const esr_conv_out &o = p.o;
+    float *s_ep = reinterpret_cast<float *>(lds) + wave * 32 * EP_P;
+    constexpr int G = N / 8;            // 8-channel groups per pixel
+    constexpr int ITEMS = 32 * G / 64;  // (pixel, group) items per lane per column
+    const int HP = p.H + 2;
+    bool ok = true;
+    float bk[ITEMS][8];
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+        const int g = (lane + 64 * k) % G;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bk[k][e] = (8 * g + e < p.cout) ? p.bias[8 * g + e] : 0.f;
+    }
+#pragma unroll
+    for (int c = 0; c < CW; ++c) {
+        if (c >= ncw) break;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = 8 * (r >> 2) + 4 * hl + (r & 3);
+                s_ep[m * EP_P + nt * 32 + ml] = acc[c][nt][r];
+            }
+        const int x = x0 + CW * wave + c;  // interior column of the output pixel
+        if constexpr ((DBG & 4) != 0) continue;  // diagnostic: restage only, no global loads / stores
+        if (o.out_planar) {
+            for (int it = lane; it < 32 * p.cout; it += 64) {
+                const int ch = it / 32, m = it % 32;
+                const int R = r0 + 1 + m;
+                const int b = R / HP, y = R - b * HP - 1;
+                if (R >= rows_tot || y < 0 || y >= p.H) continue;
+                const int oy = o.out_sy * y + o.out_oy, ox = o.out_sx * x + o.out_ox;
+                const long long opix = ((long long)b * (o.out_h + 2) + oy + 1) * (long long)(o.out_w + 2) + ox + 1;
+                float v = s_ep[m * EP_P + ch] * p.w_scale_inv + p.bias[ch];
+                if (o.lrelu) v = lrelu(v);
+                if (o.r1) v = o.s1 * v + split_at(o.r1, opix, o.r1_cp, o.r1_coff + ch);
+                if (o.r2) v = o.s2 * v + split_at(o.r2, opix, o.r2_cp, o.r2_coff + ch);
+                o.out[(((long long)b * p.cout + ch) * o.out_h + oy) * o.out_w + ox] = v;
+            }
+        } else {
+            long long opix[ITEMS];
+            bool val[ITEMS];
+#pragma unroll
+            for (int k = 0; k < ITEMS; ++k) {
+                const int it = lane + 64 * k, m = it / G, g = it % G;
+                const int R = r0 + 1 + m;
+                const int b = R / HP, y = R - b * HP - 1;
+                const int oy = o.out_sy * y + o.out_oy, ox = o.out_sx * x + o.out_ox;
+                opix[k] = ((long long)b * (o.out_h + 2) + oy + 1) * (long long)(o.out_w + 2) + ox + 1;
+                val[k] = R < rows_tot && y >= 0 && y < p.H && 8 * g < p.cout;
+            }
+            float r1v[ITEMS][8], r2v[ITEMS][8];
+            if (o.r1) {
+#pragma unroll
+                for (int k = 0; k < ITEMS; ++k)
+                    if (val[k])
+                        load_group(reinterpret_cast<const unsigned char *>(o.r1) +
+                                       (opix[k] * o.r1_cp + o.r1_coff + 8 * ((lane + 64 * k) % G)) * 4, r1v[k]);
+            }
+            if (o.r2) {
+#pragma unroll
+                for (int k = 0; k < ITEMS; ++k)
+                    if (val[k])
+                        load_group(reinterpret_cast<const unsigned char *>(o.r2) +
+                                       (opix[k] * o.r2_cp + o.r2_coff + 8 * ((lane + 64 * k) % G)) * 4, r2v[k]);
+            }
+#pragma unroll
+            for (int k = 0; k < ITEMS; ++k) {
+                if (!val[k]) continue;
+                const int it = lane + 64 * k, m = it / G, g = it % G;
+                float v[8];
+                const f32x4 v0 = *reinterpret_cast<const f32x4 *>(s_ep + m * EP_P + 8 * g);
+                const f32x4 v1 = *reinterpret_cast<const f32x4 *>(s_ep + m * EP_P + 8 * g + 4);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { v[e] = v0[e]; v[e + 4] = v1[e]; }
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    v[e] = v[e] * p.w_scale_inv + bk[k][e];
+                    if (o.lrelu) v[e] = lrelu(v[e]);
+                    if (o.r1) v[e] = o.s1 * v[e] + r1v[k][e];
+                    if (o.r2) v[e] = o.s2 * v[e] + r2v[k][e];
+                }
+                ok &= store_group(reinterpret_cast<unsigned char *>(o.out) + (opix[k] * o.out_cp + o.out_coff + 8 * g) * 4, v);
+                if (o.out2)
+                    store_group(reinterpret_cast<unsigned char *>(o.out2) + (opix[k] * o.out2_cp + o.out2_coff + 8 * g) * 4, v);
+            }
+        }
+    }
+    if (!ok && p.overflow) atomicOr(p.overflow, 1);
+}
+
+
+#ifdef ESR_X3_EXPERIMENTS  // spills at its register budget and runs 2-5x slower (r2 A/B): experiment library only
+// ---- warp-specialised persistent form --------------------------------------------------------------------------
+//
+// One workgroup per CU walks its tiles (an XCD-local band, x3s_tile) as one stream of units u = (tile, K chunk).
+// Compute waves own 4 output columns and one 32-channel N-tile each (N = 64: 8 compute waves, two per SIMD; N = 32:
+// 4); the last 4 waves only move data: they stage unit u+1 into the other LDS stage by LDS-DMA while unit u is
+// computed, so the matrix pipes never wait for a tile's loads, not even at tile boundaries.  One s_barrier per unit:
+// [loaders: DMA(u+1), vmcnt(0) | compute waves: unit u, their last LDS read waited] -> barrier.  The MFMA operands
+// are swapped (weights as A, pixels as B), so each lane ends with channels of ONE pixel and the epilogue
+// (v_permlane32_swap regroup, bias, LeakyReLU, residuals, split, 16-B stores) runs from registers: no LDS restage,
+// and the loaders keep both stages busy across it.
+constexpr int S_CW = 4;                               // output columns per compute wave
+constexpr int S_NLW = 4;                              // loader waves
+static_assert(S_CW * 4 == TWC, "four compute waves span the tile width");
+constexpr int S_KIN = (IN_PIECES + S_NLW - 1) / S_NLW;
+
+// k-th tile of workgroup b in a grid of g: XCD x = b % 8 owns tiles [x Q, (x+1) Q) (Q = ceil(ntiles / 8)), dealt
+// round-robin to its workgroups, so the tiles in flight on one XCD are neighbours (their halos share its L2).  -1 past
+// the end.
+__device__ __forceinline__ int x3s_tile(int b, int g, int ntiles, int k) {
+    const int x = b % N_XCD, l = b / N_XCD;
+    const int per = (g - x + N_XCD - 1) / N_XCD;  // workgroups on XCD x
+    const int q = (ntiles + N_XCD - 1) / N_XCD;
+    const int t = l + k * per;
+    return (t < q && x * q + t < ntiles) ? x * q + t : -1;
+}
+
+template <int NT> struct X3sShape {
+    static constexpr int NCOMP = 4 * NT;                  // compute waves
+    static constexpr int NTHR = 64 * (NCOMP + S_NLW);
+    static constexpr int WPS = (NCOMP + S_NLW) / 4;       // waves per SIMD (register budget 512 / WPS)
+};
+
+template <int NT, int TS, int DBG = 0>
+__global__ __launch_bounds__(X3sShape<NT>::NTHR, X3sShape<NT>::WPS) void conv_x3s_kernel(X3cParams p) {
+    constexpr int NCOMP = X3sShape<NT>::NCOMP;
+    constexpr int T = TS * TS;
+    constexpr int N = 32 * NT;
+    constexpr int W_RECS = T * N;
+    constexpr int W_PIECES = W_RECS / 16;
+    constexpr int KW = (W_PIECES + S_NLW - 1) / S_NLW;
+    constexpr int W_B = W_RECS * REC;
+    constexpr int STAGE = IN_B + W_B;
+    constexpr int NIC = S_CW + TS - 1;
+    constexpr int NSTEP = NIC * TS;
+    static_assert(2 * STAGE <= 163840, "two LDS stages");
+    __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * STAGE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool is_loader = wave >= NCOMP;
+    const int cw = wave & 3;        // compute wave: column group
+    const int nt = wave >> 2;       // compute wave: N-tile
+    const int hl = lane >> 5;
+    const int ml = lane & 31;
+    const int ntiles = p.tiles_x * p.tiles_y;
+    const int rows_tot = p.B * (p.H + 2);
+    const long long rowp = (long long)(p.W + 2);
+    const long long pixb = 4LL * p.in_cp;
+    const int nchunk = (p.cin + 15) >> 4;
+    int ntile_mine = 0;
+    while (x3s_tile(blockIdx.x, gridDim.x, ntiles, ntile_mine) >= 0) ++ntile_mine;
+    const int nunits = ntile_mine * nchunk;
+
+    // ---- loader side: no state across units (addresses recomputed per unit) ----
+    auto dma = [&](int u) {
+        const int lw = wave - NCOMP;
+        const int sub = lane >> 2, ps = lane & 3;
+        const int k = u / nchunk, j = u - k * nchunk;
+        const int t = x3s_tile(blockIdx.x, gridDim.x, ntiles, k);
+        const int x0 = (t % p.tiles_x) * TWC, r0 = (t / p.tiles_x) * CT;
+        const unsigned char *tile_in = p.in + ((long long)r0 * rowp + x0) * pixb + 64LL * j;
+        unsigned char *st = lds + (u & 1) * STAGE;
+        const int groups = min(16, p.cin - 16 * j) >> 3;
+#pragma unroll
+        for (int i = 0; i < S_KIN; ++i) {
+            const int q = lw + S_NLW * i;
+            if (q >= IN_PIECES) break;
+            const int r = 16 * q + sub;
+            const int hx = r / HYC, hy = r - (r / HYC) * HYC;
+            const int s = ps ^ ((hy >> 2) & 3);
+            const bool ok = r < IN_RECS && r0 + hy < rows_tot && x0 + hx < p.W + 2 && (s >> 1) < groups;
+            const void *src = ok ? (const void *)(tile_in + (hy * rowp + hx) * pixb + (s << 4)) : (const void *)g_zero64;
+            __builtin_amdgcn_global_load_lds((glob_void *)src, (lds_void *)(st + q * 1024), 16, 0, 0);
+        }
+        const unsigned char *wj = p.w + (long long)j * W_B;
+#pragma unroll
+        for (int i = 0; i < KW; ++i) {
+            const int q = lw + S_NLW * i;
+            if (q >= W_PIECES) break;
+            const int r = 16 * q + sub;
+            const int s = ps ^ ((r >> 2) & 3);
+            __builtin_amdgcn_global_load_lds((glob_void *)(wj + r * REC + (s << 4)),
+                                             (lds_void *)(st + IN_B + q * 1024), 16, 0, 0);
+        }
+    };
+
+    // ---- compute side: fragment base addresses in stage 0 (stage 1: + STAGE) ----
+    uint32_t a_hi[TS], a_lo[TS];
+#pragma unroll
+    for (int d = 0; d < TS; ++d) {
+        const int hy = ml + p.tap_y0 + d;
+        const uint32_t o = lds_addr(lds) + hy * REC + (((2 * hl) ^ ((hy >> 2) & 3)) << 4) +
+                           (uint32_t)(S_CW * cw + p.tap_x0) * HYC * REC;
+        a_hi[d] = o;
+        a_lo[d] = o ^ 16u;
+    }
+    const uint32_t b_hi0 = lds_addr(lds) + IN_B + (nt * 32 + ml) * REC + (((2 * hl) ^ ((ml >> 2) & 3)) << 4);
+
+    f32x16 acc[S_CW];
+    auto zero_acc = [&]() {
+#pragma unroll
+        for (int c = 0; c < S_CW; ++c)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[c][r] = 0.f;
+    };
+    zero_acc();
+
+    // one unit from stage sb (0 or STAGE bytes): the d-major sweep of conv_x3c_kernel for this wave's N-tile, with
+    // swapped MFMA operands
+    auto compute = [&](uint32_t sb) {
+        const uint32_t bh_b = b_hi0 + sb, bl_b = (b_hi0 + sb) ^ 16u;
+        f16x8 bh[2][TS], bl[2][TS], ah[3], al[3];
+        auto ldb = [&](auto Dc) {
+            constexpr int d = decltype(Dc)::value;
+            sfor<0, TS>([&](auto Xc) {
+                constexpr int dx = decltype(Xc)::value, t = d * TS + dx;
+                bh[d & 1][dx] = ds_read16<t * N * REC>(bh_b);
+                bl[d & 1][dx] = ds_read16<t * N * REC>(bl_b);
+            });
+        };
+        auto lda = [&](auto Sc) {
+            constexpr int s = decltype(Sc)::value, d = s / NIC, ic = s % NIC, buf = s % 3;
+            ah[buf] = ds_read16<ic * HYC * REC>(a_hi[d] + sb);
+            al[buf] = ds_read16<ic * HYC * REC>(a_lo[d] + sb);
+        };
+        ldb(std::integral_constant<int, 0>{});
+        lda(std::integral_constant<int, 0>{});
+        if constexpr (NSTEP > 1) lda(std::integral_constant<int, 1>{});
+        sfor<0, NSTEP>([&](auto Sc) {
+            constexpr int s = decltype(Sc)::value, d = s / NIC, ic = s % NIC, buf = s % 3;
+            constexpr int pd = (s - 1) / NIC, pic = (s - 1) % NIC;
+            constexpr int after = s == 0 ? (NSTEP > 1 ? 2 : 0)
+                                         : ((pic == 0 && pd + 1 < TS) ? 2 * TS : 0) + (s + 1 < NSTEP ? 2 : 0);
+            lgkm_wait2<after>(ah[buf], al[buf]);
+            if constexpr (ic == 0) {
+#pragma unroll
+                for (int x = 0; x < TS; ++x) asm volatile("" : "+v"(bh[d & 1][x]), "+v"(bl[d & 1][x]));
+            }
+            if constexpr (ic == 0 && d + 1 < TS) ldb(std::integral_constant<int, d + 1>{});
+            if constexpr (s + 2 < NSTEP) lda(std::integral_constant<int, s + 2>{});
+            sfor<0, 3>([&](auto Pc) {
+                constexpr int pr = decltype(Pc)::value;
+                sfor<0, TS>([&](auto Xc) {
+                    constexpr int dx = decltype(Xc)::value, c = ic - dx;
+                    if constexpr (c >= 0 && c < S_CW) {
+                        const f16x8 &a = pr == 0 ? al[buf] : ah[buf];
+                        const f16x8 &b = pr == 1 ? bl[d & 1][dx] : bh[d & 1][dx];
+                        acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b, a, acc[c], 0, 0, 0);
+                    }
+                });
+            });
+        });
+    };
+
+    // epilogue of tile t from registers: lane (ml, hl) holds pixel m = ml of each of its columns; after the
+    // permlane32 regroup, channels 32 nt + 8 (2 s + hl) + e (e < 8) in acc[c][8 s + e]
+    const esr_conv_out &o = p.o;
+    const int HP = p.H + 2;
+    auto epilogue = [&](int t, int ncw) {
+        const int x0 = (t % p.tiles_x) * TWC, r0 = (t / p.tiles_x) * CT;
+        const int R = r0 + 1 + ml;
+        const int b = R / HP, y = R - b * HP - 1;
+        const bool vrow = R < rows_tot && y >= 0 && y < p.H;
+        bool ok = true;
+#pragma unroll 1
+        for (int c = 0; c < ncw; ++c) {  // a runtime loop: one column's registers live at a time
+            f32x16 a;
+            switch (c) {
+            case 0: a = acc[0]; break;
+            case 1: a = acc[1]; break;
+            case 2: a = acc[2]; break;
+            default: a = acc[3]; break;
+            }
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a[8 * s2 + k]),
+                                                                    __float_as_uint(a[8 * s2 + 4 + k]), false, false);
+                    a[8 * s2 + k] = __uint_as_float(r[0]);
+                    a[8 * s2 + 4 + k] = __uint_as_float(r[1]);
+                }
+            const int x = x0 + S_CW * cw + c;
+            const int oy = o.out_sy * y + o.out_oy, ox = o.out_sx * x + o.out_ox;
+            const long long opix = ((long long)b * (o.out_h + 2) + oy + 1) * (long long)(o.out_w + 2) + ox + 1;
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const int ch = 32 * nt + 8 * (2 * s2 + hl);
+                if (!vrow || ch >= p.cout || (DBG & 4)) continue;
+                float v[8], r1v[8], r2v[8];
+                if (o.r1) load_group(reinterpret_cast<const unsigned char *>(o.r1) + (opix * o.r1_cp + o.r1_coff + ch) * 4, r1v);
+                if (o.r2) load_group(reinterpret_cast<const unsigned char *>(o.r2) + (opix * o.r2_cp + o.r2_coff + ch) * 4, r2v);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    v[e] = a[8 * s2 + e] * p.w_scale_inv + p.bias[ch + e];
+                    if (o.lrelu) v[e] = lrelu(v[e]);
+                    if (o.r1) v[e] = o.s1 * v[e] + r1v[e];
+                    if (o.r2) v[e] = o.s2 * v[e] + r2v[e];
+                }
+                ok &= store_group(reinterpret_cast<unsigned char *>(o.out) + (opix * o.out_cp + o.out_coff + ch) * 4, v);
+                if (o.out2)
+                    store_group(reinterpret_cast<unsigned char *>(o.out2) + (opix * o.out2_cp + o.out2_coff + ch) * 4, v);
+            }
+        }
+        if (!ok && p.overflow) atomicOr(p.overflow, 1);
+    };
+
+    if (is_loader) {
+        if (nunits > 0) dma(0);
+        wait_vm0();
+    }
+    __builtin_amdgcn_s_barrier();
+    int cur_tile = x3s_tile(blockIdx.x, gridDim.x, ntiles, 0);
+    int j = 0, k = 0;
+    for (int u = 0; u < nunits; ++u) {
+        if (is_loader) {
+            if (u + 1 < nunits && !(DBG & 1)) dma(u + 1);
+            wait_vm0();
+        } else {
+            const int ncw = min(S_CW, max(0, min(TWC, p.W - (cur_tile % p.tiles_x) * TWC) - S_CW * cw));
+            if (ncw > 0 && !(DBG & 2)) compute((u & 1) * STAGE);
+            if (j == nchunk - 1) {
+#ifdef X3S_KEEP_ONLY
+#pragma unroll
+                for (int c = 0; c < S_CW; ++c) asm volatile("" : "+v"(acc[c]));
+#else
+                if (ncw > 0) epilogue(cur_tile, ncw);
+#endif
+                zero_acc();
+            }
+        }
+        if (++j == nchunk) {
+            j = 0;
+            cur_tile = x3s_tile(blockIdx.x, gridDim.x, ntiles, ++k);
+        }
+        __builtin_amdgcn_s_barrier();
+    }
+}
+
+#endif  // ESR_X3_EXPERIMENTS
+
+}  // namespace
+
+static int n_cus() {
+    static int n = 0;
+    if (!n) {
+        int dev = 0, v = 0;
+        n = (hipGetDevice(&dev) == hipSuccess &&
+             hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
+    }
+    return n;
+}
+
+#ifdef ESR_X3_EXPERIMENTS
+int x3s_launch(const X3cParams &p0, int taps_side, hipStream_t stream, int dbg) {
+    X3cParams p = p0;
+    p.tiles_x = (p.W + TWC - 1) / TWC;
+    p.tiles_y = (p.B * (p.H + 2) - 2 + CT - 1) / CT;
+    const int ntiles = p.tiles_x * p.tiles_y;
+    const dim3 grid((unsigned)min(ntiles, n_cus()));
+    const bool n64 = p.cout > 32;
+#ifdef ESR_X3_EXPERIMENTS
+    if (taps_side == 3 && dbg) {
+#define XD(f) if (n64) hipLaunchKernelGGL((conv_x3s_kernel<2, 3, f>), grid, dim3(X3sShape<2>::NTHR), 0, stream, p); \
+              else hipLaunchKernelGGL((conv_x3s_kernel<1, 3, f>), grid, dim3(X3sShape<1>::NTHR), 0, stream, p)
+        switch (dbg) {
+        case 1: XD(1); break;
+        case 2: XD(2); break;
+        case 4: XD(4); break;
+        default: XD(1 | 4);
+        }
+#undef XD
+        return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+    }
+#else
+    (void)dbg;
+#endif
+    const dim3 b1(X3sShape<1>::NTHR), b2(X3sShape<2>::NTHR);
+    if (taps_side == 3) {
+        if (n64) hipLaunchKernelGGL((conv_x3s_kernel<2, 3>), grid, b2, 0, stream, p);
+        else hipLaunchKernelGGL((conv_x3s_kernel<1, 3>), grid, b1, 0, stream, p);
+    } else {
+        if (n64) hipLaunchKernelGGL((conv_x3s_kernel<2, 2>), grid, b2, 0, stream, p);
+        else hipLaunchKernelGGL((conv_x3s_kernel<1, 2>), grid, b1, 0, stream, p);
+    }
+    return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+}
+#endif
+
+int x3c_launch(const X3cParams &p0, int taps_side, hipStream_t stream, int dbg) {
+    X3cParams p = p0;
+    p.tiles_x = (p.W + TWC - 1) / TWC;
+    p.tiles_y = (p.B * (p.H + 2) - 2 + CT - 1) / CT;
+    const dim3 grid((unsigned)(p.tiles_x * p.tiles_y)), block(NTHR);
+    const bool n64 = p.cout > 32;
+    if (dbg == 16) {  // register-B form
+        if (taps_side == 3) {
+            if (n64) hipLaunchKernelGGL((conv_x3c_kernel<2, 3, 0, true>), grid, block, 0, stream, p);
+            else hipLaunchKernelGGL((conv_x3c_kernel<1, 3, 0, true>), grid, block, 0, stream, p);
+        } else {
+            if (n64) hipLaunchKernelGGL((conv_x3c_kernel<2, 2, 0, true>), grid, block, 0, stream, p);
+            else hipLaunchKernelGGL((conv_x3c_kernel<1, 2, 0, true>), grid, block, 0, stream, p);
+        }
+        return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+    }
+#ifdef ESR_X3_EXPERIMENTS
+    if (taps_side == 3 && dbg) {
+#define XD(f) if (n64) hipLaunchKernelGGL((conv_x3c_kernel<2, 3, f>), grid, block, 0, stream, p); \
+              else hipLaunchKernelGGL((conv_x3c_kernel<1, 3, f>), grid, block, 0, stream, p)
+        switch (dbg) {
+        case 1: XD(1); break;
+        case 2: XD(2); break;
+        case 4: XD(4); break;
+        default: XD(1 | 4);
+        }
+#undef XD
+        return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+    }
+#else
+    (void)dbg;
+#endif
+    if (taps_side == 3) {
+        if (n64) hipLaunchKernelGGL((conv_x3c_kernel<2, 3>), grid, block, 0, stream, p);
+        else hipLaunchKernelGGL((conv_x3c_kernel<1, 3>), grid, block, 0, stream, p);
+    } else {
+        if (n64) hipLaunchKernelGGL((conv_x3c_kernel<2, 2>), grid, block, 0, stream, p);
+        else hipLaunchKernelGGL((conv_x3c_kernel<1, 2>), grid, block, 0, stream, p);
+    }
+    return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+}

@@ -3,8 +3,8 @@
 Keeps the interface the reference's drivers use — `feed_data`, `ConcatLatent`, `GetLatent`, `optimize_parameters`,
 `test`, `get_current_visuals`, attributes `netG`, `netD`, `CEM_net`, `fake_H`, `var_L`, `var_H`, `model_input`,
 `num_latent_channels`, `Z_size_factor`, `log_dict`, `step` — for the configuration the shipped JSONs select:
-CEM_arch, latent `all_layers`/`HR_downscaled` (or no latent), WGAN-GP (non-relativistic), range loss, D_verification
-'past'/None, gradient accumulation.  Options the shipped configs switch off (VGG feature loss — broken in the
+CEM_arch, latent `all_layers`/`HR_downscaled` (or no latent), WGAN-GP (relativistic or not), range loss, D_verification
+'past'/'current'/None, fixed or adaptive D_update_ratio, gradient accumulation.  Options the shipped configs switch off (VGG feature loss — broken in the
 reference, pixel/high-pass/shift-invariant/optimal-Z/latent losses, encoder, decomposed D input) raise
 NotImplementedError instead of silently differing.  Checkpoints and logs keep the reference's formats
 (base_model.py:86-144; SRRaGAN_model.py:695-719, 766-813): `{step}_G.pth` / `{step}_D.pth` dicts with
@@ -82,6 +82,9 @@ def _broadcast_buffers(module):
         dist.broadcast(b, 0)
 
 
+LATENT_WEIGHTS_RELATIVE_STD = 0.  # base_model.py:116
+
+
 class SRRaGANModel:
     def __init__(self, opt, accumulation_steps_per_batch=1, kernel=None, device=None):
         self.opt = opt
@@ -130,10 +133,10 @@ class SRRaGANModel:
                   'shift_invariant_weight'):
             if t.get(k):
                 raise NotImplementedError('%s > 0 is not part of the built training path (shipped configs use 0)' % k)
-        if opt['network_D'].get('decomposed_input') or opt['network_D'].get('relativistic') not in (0, None, False):
-            if opt['network_D'].get('decomposed_input'):
-                raise NotImplementedError('decomposed D input')
-        self.relativistic_D = bool(opt['network_D'].get('relativistic'))
+        if opt['network_D'].get('decomposed_input'):
+            raise NotImplementedError('decomposed D input')
+        rel = opt['network_D'].get('relativistic')
+        self.relativistic_D = rel is None or bool(rel)  # SRRaGAN_model.py:87: unset means relativistic
         self.D_verification = t.get('D_verification')
         assert self.D_verification in ['current', 'past', None]
         self.grad_accumulation_steps_G = t.get('grad_accumulation_steps_G', 1)
@@ -161,7 +164,8 @@ class SRRaGANModel:
             self.netD = networks.define_D(opt, CEM=self.CEM_net).to(self.device)
             self.netD.train()
             self.cri_gan = GANLoss(t['gan_type'], 1.0, 0.0)
-            self.global_D_update_ratio = t.get('D_update_ratio') or 1
+            r = t.get('D_update_ratio')
+            self.global_D_update_ratio = r if r is not None else 1  # <= 0: adaptive ratio (optimize_parameters)
             self.D_init_iters = t.get('D_init_iters') or 0
             if t['gan_type'] == 'wgan-gp':
                 self.cri_gp = GradientPenaltyLoss(device=self.device)
@@ -240,6 +244,23 @@ class SRRaGANModel:
             s[3:] /= _world()
         return float(s[0] / s[2]), float(s[1] / s[2]), float(s[3]), float(s[4])
 
+    def _d_update_ratio(self, t):
+        """SRRaGAN_model.py:314-324: the configured ratio, or (D_update_ratio <= 0) one adapted to the mean logged
+        D_logits_diff of the last D_valid_Steps_4_G_update D steps (> 1: D steps per G step; < 1: G steps per D step)."""
+        if self.global_D_update_ratio > 0:
+            return self.global_D_update_ratio
+        n = t['D_valid_Steps_4_G_update']
+        if len(self.log_dict['D_logits_diff']) < n:
+            return n
+        log_mean = np.log(max(1e-5, np.mean([v[1] for v in self.log_dict['D_logits_diff'][-n:]])))
+        if log_mean < -2:
+            return int(-2 * np.ceil((log_mean + 1) * 2) / 2)
+        return 1 / max(1, int(np.floor((log_mean + 2) * 20)))
+
+    def _interp_points(self, n):
+        """WGAN-GP interpolation points, one per image (SRRaGAN_model.py:388-391, random_pt.uniform_())."""
+        return torch.rand(n, 1, 1, 1, device=self.device)
+
     def optimize_parameters(self):
         """SRRaGAN_model.py:307-575 for the shipped training configuration."""
         t = self.opt['train']
@@ -249,7 +270,7 @@ class SRRaGANModel:
         first_acc_D = self.step % self.grad_accumulation_steps_D == 0
         last_acc_D = self.step % self.grad_accumulation_steps_D == self.grad_accumulation_steps_D - 1
         if first_acc_D:
-            self.cur_D_update_ratio = self.global_D_update_ratio
+            self.cur_D_update_ratio = self._d_update_ratio(t)
         G_grads_retained = first_acc_D or self.generator_step
         for p in self.netG.parameters():
             if not getattr(p, '_esr_frozen', False):
@@ -282,7 +303,7 @@ class SRRaGANModel:
             l_d_total = (l_d_real + l_d_fake) / 2
             l_d_gp = None
             if t['gan_type'] == 'wgan-gp':
-                rp = torch.rand(self.var_ref.size(0), 1, 1, 1, device=self.device)
+                rp = self._interp_points(self.var_ref.size(0))
                 interp = rp * self.fake_H.detach() + (1 - rp) * self.var_ref
                 interp.requires_grad = True
                 l_d_gp = self.l_gp_w * self.cri_gp(interp, self.netD(interp))
@@ -323,6 +344,7 @@ class SRRaGANModel:
                     p.requires_grad = False
             if first_acc_G:
                 self.optimizer_G.zero_grad()
+                self._g_logs = {'l_g_range': [], 'l_g_gan': []}
             l_g_total = 0
             if self.cri_range is not None:
                 l_g_range = self.cri_range(self.fake_H)
@@ -335,8 +357,13 @@ class SRRaGANModel:
                                               self.cri_gan(pred_g_fake - torch.mean(pred_d_real), True)) / 2
                 else:
                     l_g_gan = self.l_gan_w * self.cri_gan(pred_g_fake, True)
-                l_g_total = l_g_total + l_g_gan / self.grad_accumulation_steps_G
+                l_g_gan = l_g_gan / self.grad_accumulation_steps_G  # logged divided, as the reference (:526, 539)
+                l_g_total = l_g_total + l_g_gan
             l_g_total.backward()
+            if self.cri_range is not None:
+                self._g_logs['l_g_range'].append(l_g_range.item())
+            if self.D_exists:
+                self._g_logs['l_g_gan'].append(l_g_gan.item())
             if last_acc_G:
                 _allreduce_grads([p for p in self.netG.parameters() if p.requires_grad])
                 if self.latent_input is not None and self.latent_grads_multiplier != 1:  # :543-546
@@ -345,10 +372,9 @@ class SRRaGANModel:
                             p.grad[:, c, ...] *= self.latent_grads_multiplier
                 self.optimizer_G.step()
                 g = self.gradient_step_num
-                if self.cri_range is not None:
-                    self.log_dict['l_g_range'].append((g, l_g_range.item()))
-                if self.D_exists:
-                    self.log_dict['l_g_gan'].append((g, l_g_gan.item()))
+                for k, v in self._g_logs.items():  # means over the accumulated micro-batches (:566-574)
+                    if v:
+                        self.log_dict[k].append((g, float(np.mean(v))))
         self.step += 1
 
     def update_learning_rate(self):
@@ -426,7 +452,11 @@ class SRRaGANModel:
             if self.latent_input is not None and 'weight' in key and lv.dim() > 1 and \
                     cs[1] in list(ls[1] + self.num_latent_channels * np.array([1, self.opt['scale'] ** 2])):
                 extra = cs[1] - ls[1]
-                out[ck] = torch.cat([torch.zeros((cs[0], extra) + cs[2:], dtype=lv.dtype), lv.cpu()], 1)
+                # the reference's expression (base_model.py:130-134): 0 x (loaded std / current std) x current
+                # weights, so the prepended zeros carry the current weights' signs (and NaN if their std is 0)
+                cur = cv[:, :extra].detach().cpu()
+                out[ck] = torch.cat([LATENT_WEIGHTS_RELATIVE_STD * lv.std() / cur.std() * cur.to(lv.dtype),
+                                     lv.cpu()], 1)
                 if hasattr(self, 'channels_idx_4_grad_amplification'):
                     self.channels_idx_4_grad_amplification[i] = list(range(extra))
             elif self.CEM_arch and any(op in key for op in op_names):

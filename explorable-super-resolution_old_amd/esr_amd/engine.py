@@ -616,6 +616,8 @@ def _forward(net, x, cem, precision, train_ws=None, rec=None):
             ev = _prof_begin(prof, '%sconv3x3_n%d' % (tagp, 32 if cout <= 32 else 64), 2.0 * Bn * h_ * w_ * 9 * cin_ref * cout)
         if x3:
             wx, scale = cw.x3()
+            if rec is not None:  # the op list holds wx's pointer: keep it alive (train_x3 may swap cw._x3 later)
+                rec.keep.append(wx)
             rc = lib.esr_conv3x3_fwd_x3(inp.data_ptr(), Bn, h_, w_, in_cp, cin, wx.data_ptr(), cw.bias.data_ptr(),
                                         scale, cout, ctypes.byref(o), ovf, stream)
         else:
@@ -657,6 +659,8 @@ def _forward(net, x, cem, precision, train_ws=None, rec=None):
                 ev = _prof_begin(prof, tagp + 'upconv2x_phase', 2.0 * Bn * (2 * sh) * (2 * sw) * 9 * 64 * 64 / 4)
             if x3:
                 wx, scale = cw.x3()
+                if rec is not None:
+                    rec.keep.append(wx)
                 rc = lib.esr_upconv2x_phase_fwd_x3(src.data_ptr(), Bn, sh, sw, 64, 64, wx.data_ptr(),
                                                    cw.bias.data_ptr(), scale, 64, py, px, ctypes.byref(o), ovf, stream)
             else:

@@ -16,6 +16,7 @@ and the reduction scales.
 """
 import ctypes
 import os
+import weakref
 
 import torch
 
@@ -72,14 +73,35 @@ class TrainWorkspace:
         self.graphs = {}
 
 
+class _Owner:
+    """Held by the autograd context of one training forward; the workspace keeps a weak reference to it.  While it is
+    alive and its backward has not run, the workspace's saved activations belong to that forward."""
+    __slots__ = ('done', '__weakref__')
+
+    def __init__(self):
+        self.done = False
+
+
+def _busy(ws):
+    o = ws.owner() if getattr(ws, 'owner', None) is not None else None
+    return o is not None and not o.done
+
+
 def _train_workspace(net, dev, B, H, W, latent, precision='f32'):
+    """The cached workspace of this shape, or — when its saved activations still await a backward (a second grad
+    forward before the first one's backward: two generator calls in one loss, retained graphs) — a fresh one, so that
+    no forward overwrites another's activations."""
     # keyed by precision too: an x3 forward leaves split-f16 records where an fp32 forward expects floats
     key = (str(dev), B, H, W, latent, net.nb, precision)
     c = net._esr_cache.get('train_ws')
     if c is None or c[0] != key:
+        if c is not None and _busy(c[1]):
+            return TrainWorkspace(dev, B, H, W, latent, net.nb)  # the cached one is still needed: keep it
         net._esr_cache.pop('train_ws', None)
         c = (key, TrainWorkspace(dev, B, H, W, latent, net.nb))
         net._esr_cache['train_ws'] = c
+    if _busy(c[1]):
+        return TrainWorkspace(dev, B, H, W, latent, net.nb)
     return c[1]
 
 
@@ -482,12 +504,16 @@ class _GeneratorFn(torch.autograd.Function):
             out, graphed, split = E._forward(net, xd, cem, 'f32', train_ws=ws)[0], False, False
         ctx.net, ctx.cem, ctx.ws, ctx.latent, ctx.M, ctx.split = net, cem, ws, latent, E.SF * m, split
         ctx.params = params
+        ctx.owner = _Owner()
+        ws.owner = weakref.ref(ctx.owner)
         return out.clone() if graphed else out
 
     @staticmethod
     def backward(ctx, d_out):
         need_params = any(ctx.needs_input_grad[3:])
         need_input = ctx.needs_input_grad[0]
+        if ctx.ws.owner() is not ctx.owner:  # cannot happen through _train_workspace; guards direct workspace reuse
+            raise RuntimeError('esr_amd: the saved activations of this forward were overwritten by a later forward')
         bp = _bwd_packed(ctx.net, ctx.latent)  # parameter repack, outside any graph
         key = ('bwd', tuple(d_out.shape), _cem_key(ctx.cem), ctx.M, need_params, need_input, id(bp), ctx.split)
         (flat, dx), graphed = _run_graphed(
@@ -499,6 +525,7 @@ class _GeneratorFn(torch.autograd.Function):
             flat = flat.clone() if flat is not None else None
             dx = dx.clone() if dx is not None else None
         grads = _split_grads(bp, flat) if flat is not None else {}
+        ctx.owner.done = True  # the workspace may be reused (a retained graph's second backward would then raise)
         return (dx, None, None) + tuple(grads.get(p) for p in ctx.params)
 
 

@@ -130,15 +130,20 @@ int esr_conv3x3_fwd_x3(const void *in, int32_t B, int32_t H, int32_t W, int32_t 
 int esr_upconv2x_phase_fwd_x3(const void *in, int32_t B, int32_t H, int32_t W, int32_t in_cp, int32_t cin,
                               const void *w_packed, const float *bias, float w_scale, int32_t cout, int32_t py,
                               int32_t px, const esr_conv_out *o, int32_t *overflow, esr_stream_t stream);
-/* Kernel selection for esr_conv3x3_fwd_x3 with cout <= 32 (process-wide; for A/B tests and benchmarks):
- * 0 / 1 (default) = classic kernel, one LDS stage, 8-row tiles at three workgroups per CU or 16-row tiles at two
- * (a wave-quantisation cost model picks; 25 / 26 force one); 22 = classic with two LDS stages and one workgroup per
- * CU; 23 = cout > 32 with 8-row tiles at two workgroups per CU; 21 = the same with fragment prefetch distance 1 (default 2); 20 = two-stage classic with
- * compiler-scheduled fragment reads (also for cout > 32, whose default uses explicit counted-wait reads); 2 = ring
- * kernel (two tiles per workgroup, 3-deep LDS-DMA input ring); 15 = ring with staggered DMA issue; 18 = ring with
- * compiler-scheduled reads; 16 / 17 = persistent ring (one workgroup per CU streaming tile pairs), fragment prefetch
- * 1 / 2 taps; 3..14 and 19 = diagnostic ablations of the ring kernel (garbage outputs).  All others give
- * bitwise-identical results.  Returns the previous setting, or ESR_EINVAL. */
+/* Kernel selection for esr_conv3x3_fwd_x3 (process-wide; for A/B tests and benchmarks).  All variants below give
+ * bitwise-identical results.
+ * 0 / 1 (default) = automatic: the column-tile kernel (32x16 tiles, esr_conv_x3c.hip) for cout > 32 and, for
+ *   cout <= 32, where 16-row classic tiles fill their rounds; otherwise the classic kernel with 8-row tiles at three
+ *   workgroups per CU; 24 = the round-1 automatic choice (classic kernel only: 8-row at three per CU or 16-row at two,
+ *   by a wave-quantisation cost model; 25 / 26 force one); 50 = column-tile kernel; 60 = column-tile kernel with the
+ *   weights read into registers from global memory instead of LDS;
+ * 22 = classic with two LDS stages and one workgroup per CU; 23 = cout > 32 with 8-row tiles at two workgroups per
+ *   CU; 21 = the same with fragment prefetch distance 1 (default 2); 20 = two-stage classic with compiler-scheduled
+ *   fragment reads; 27 / 28 = classic with the register epilogue (16- / 8-row);
+ * 2 = ring kernel (two tiles per workgroup, 3-deep LDS-DMA input ring); 15 = ring with staggered DMA issue; 18 = ring
+ *   with compiler-scheduled reads; 16 / 17 = persistent ring (one workgroup per CU streaming tile pairs).
+ * Diagnostic ablations (garbage outputs) exist only in the experiment build (make exp, -DESR_X3_EXPERIMENTS); the
+ * production library returns ESR_EINVAL for them.  Returns the previous setting, or ESR_EINVAL. */
 int esr_x3_set_kernel(int32_t variant);
 
 /* Block -> tile order of the classic x3 conv kernel and the exact-fp32 conv kernel: 1 (default) = XCD-grouped (workgroups run round-robin over the

@@ -1,0 +1,232 @@
+"""Golden fixtures for the training loop and the checkpoint formats, made by running the REFERENCE's own
+SRRaGANModel (read-only at /root/reference) in this container.  Run once here; only the small outputs are committed.
+
+    python tests/golden/make_golden_train.py
+
+Uses the in-memory shims of make_golden.py plus, for importing models/SRRaGAN_model.py:
+  * stub modules for what its imports pull in but the training step never calls (torchvision.utils, GPUtil,
+    skimage.transform, skimage.color): attribute access returns a function that raises if called;
+  * `networks.define_D` builds Discriminator_VGG_128_(nb=n_layers) — the shipped `discriminator_vgg_128` + n_layers
+    combination passes nb= to a class without it; this is the class DESIGN.md pins the port's D to;
+  * `torch.Tensor.cuda` is the identity while process_loaded_state_dict runs (base_model.py:133-135 moves the
+    latent-widened weights to CUDA; this container has no GPU);
+  * the WGAN-GP interpolation points (SRRaGAN_model.py:391, `self.random_pt.uniform_()`) are drawn from a NumPy PCG64
+    stream instead of torch's CPU generator, so that the GPU test can feed the port the same points.
+Fixtures (tests/golden/):
+  train_*.npz  — per micro-step generator_step flags, every log_dict series, and digests of the G/D parameter updates
+                 (per-key L2 norms of the final parameters and of their change, projections of the change on a seeded
+                 random direction, the full change of the small keys), for the reference run in float32 and float64
+                 (the float64 run is the accuracy yardstick: the port's error is judged against the reference's own
+                 float32 error, as conftest.grad_parity does for gradients).
+  ckpt_remap.npz — base_model.load_network + process_loaded_state_dict of a plain (no latent, no CEM prefix) RRDBNet
+                 state dict into the latent CEM generator: output key order, per-key SHA-256, the gradient-amplified
+                 channel lists.
+  ckpt/7_G.pth — written by base_model.save_network (model_state_dict on the CPU + Adam optimizer_state_dict with
+                 state for three parameters), read back by the test with torch.load(weights_only=True).
+"""
+import hashlib
+import json
+import os
+import sys
+import types
+
+sys.dont_write_bytecode = True
+sys.pycache_prefix = '/tmp/esr_golden_pycache'
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import make_golden as MG  # noqa: E402
+from oracle.recipe import seeded_params  # noqa: E402
+from train_recipe import CKPT_CFG, TRAIN_CFGS, random_points, step_data, train_opt  # noqa: E402
+
+SMALL = 4096  # keys with at most this many elements get their full parameter change stored
+
+
+class _Stub(types.ModuleType):
+    __path__ = []
+
+    def __getattr__(self, k):
+        if k.startswith('__'):
+            raise AttributeError(k)
+
+        def f(*a, **kw):
+            raise RuntimeError('stub %s.%s called' % (self.__name__, k))
+        return f
+
+
+def _stub(name):
+    m = _Stub(name)
+    sys.modules[name] = m
+    parent, _, child = name.rpartition('.')
+    if parent in sys.modules:
+        setattr(sys.modules[parent], child, m)
+
+
+def install_train_shims():
+    MG.install_shims()
+    sys.modules.pop('torchvision', None)
+    for n in ('torchvision', 'torchvision.utils', 'GPUtil', 'skimage', 'skimage.transform', 'skimage.color'):
+        _stub(n)
+
+
+class FixedRP(torch.Tensor):
+    """random_pt whose uniform_() takes the next row of a preset NumPy stream (results of ops are plain tensors)."""
+    __torch_function__ = torch._C._disabled_torch_function_impl
+    stream = None
+
+    def uniform_(self, *a, **k):
+        v = next(FixedRP.stream)
+        with torch.no_grad():
+            self.copy_(torch.from_numpy(v).to(self.dtype).view(self.shape))
+        return self
+
+
+def build_reference(cfg, dtype):
+    import models.networks as networks
+    import models.modules.architecture as arch
+    import models.SRRaGAN_model as R
+
+    def define_D(opt, CEM=None):
+        o = opt['network_D']
+        patch = opt['datasets']['train']['patch_size'] - (2 * CEM.invalidity_margins_HR if CEM is not None else 0)
+        D = arch.Discriminator_VGG_128_(in_nc=o['in_nc'], base_nf=o['nf'], norm_type=o['norm_type'],
+                                        act_type=o['act_type'], mode=o['mode'], input_patch_size=patch,
+                                        nb=o['n_layers'])
+        networks.init_weights(D, init_type='kaiming', scale=1)
+        return D
+    networks.define_D = define_D
+    R.networks.define_D = define_D
+    os.makedirs('/tmp/esr_golden_train_models', exist_ok=True)
+    torch.set_default_dtype(dtype)
+    torch.cuda.FloatTensor = torch.DoubleTensor if dtype == torch.float64 else torch.FloatTensor
+    try:
+        model = R.SRRaGANModel(train_opt(cfg), accumulation_steps_per_batch=cfg['acc'])
+    finally:
+        torch.set_default_dtype(torch.float32)
+    gsd, dsd = model.netG.state_dict(), model.netD.state_dict()
+    gp = seeded_params([(k, tuple(v.shape)) for k, v in gsd.items()], cfg['seed'], w_scale=1.0)
+    dp = seeded_params([(k, tuple(v.shape)) for k, v in dsd.items() if 'running' not in k and 'num_batches' not in k],
+                       cfg['seed'] + 1, w_scale=1.0)
+    model.netG.load_state_dict({k: torch.from_numpy(v) for k, v in gp.items()}, strict=False)
+    model.netD.load_state_dict({k: torch.from_numpy(v) for k, v in dp.items()}, strict=False)
+    if dtype == torch.float64:
+        model.netG.double()
+        model.netD.double()
+    # optimisers were built over the same Parameter objects; the load copied into them in place
+    B = cfg['batch']
+    model.random_pt = torch.zeros(B, 1, 1, 1, dtype=dtype).as_subclass(FixedRP)
+    return model
+
+
+def run_reference(cfg, dtype):
+    model = build_reference(cfg, dtype)
+    g0 = {k: v.detach().clone() for k, v in model.netG.named_parameters()}
+    d0 = {k: v.detach().clone() for k, v in model.netD.named_parameters()}
+    FixedRP.stream = random_points(cfg)
+    flags = []
+    for k in range(cfg['steps']):
+        lr, hr, z = step_data(cfg, k)
+        cast = lambda a: torch.from_numpy(a).to(dtype)  # noqa: E731
+        model.feed_data({'LR': cast(lr), 'HR': cast(hr), 'Z': cast(z)})
+        model.optimize_parameters()
+        flags.append(bool(model.generator_step))
+    return model, g0, d0, flags
+
+
+def digest(prefix, final, init, d, proj_seed):
+    rng = np.random.default_rng(proj_seed)
+    for k in final:
+        f = final[k].detach().double().numpy()
+        delta = f - init[k].double().numpy()
+        p = rng.standard_normal(f.shape)
+        d['%s_norm:%s' % (prefix, k)] = np.float64(np.linalg.norm(f))
+        d['%s_dnorm:%s' % (prefix, k)] = np.float64(np.linalg.norm(delta))
+        d['%s_dproj:%s' % (prefix, k)] = np.float64((p * delta).sum())
+        if f.size <= SMALL:
+            d['%s_delta:%s' % (prefix, k)] = delta.astype(np.float64)
+
+
+def train_fixture(name, cfg):
+    d = {'cfg': np.str_(json.dumps(cfg))}
+    for tag, dtype in (('f32', torch.float32), ('f64', torch.float64)):
+        model, g0, d0, flags = run_reference(cfg, dtype)
+        d['%s_generator_step' % tag] = np.array(flags)
+        for k, v in model.log_dict.items():
+            if v:
+                d['%s_log:%s' % (tag, k)] = np.array(v, dtype=np.float64)
+        digest(tag + '_G', dict(model.netG.named_parameters()), g0, d, cfg['seed'] + 400)
+        digest(tag + '_D', dict(model.netD.named_parameters()), d0, d, cfg['seed'] + 401)
+        for k, v in model.netD.state_dict().items():
+            if 'running' in k:
+                d['%s_Dbuf:%s' % (tag, k)] = v.double().numpy()
+        print('train_%s [%s]: generator_step %s, logs %s' % (
+            name, tag, flags, {k: ['%.4g' % x[1] for x in v] for k, v in model.log_dict.items() if v}))
+    np.savez_compressed(os.path.join(HERE, 'train_%s.npz' % name), **d)
+
+
+def _sha(t):
+    return hashlib.sha256(t.detach().contiguous().cpu().numpy().tobytes()).hexdigest()
+
+
+def checkpoint_fixtures():
+    """base_model.py:86-144 on the reference model: load a plain checkpoint into the latent CEM generator; write a
+    {step}_G.pth."""
+    import models.modules.architecture as arch
+    cfg = dict(CKPT_CFG)
+    model = build_reference(cfg, torch.float32)
+    plain = arch.RRDBNet(in_nc=3, out_nc=3, nf=64, nb=cfg['nb'], gc=32, upscale=4, norm_type=None,
+                         act_type='leakyrelu', mode='CNA', upsample_mode='upconv', latent_input=None,
+                         num_latent_channels=0)
+    psd = seeded_params([(k, tuple(v.shape)) for k, v in plain.state_dict().items()], 900, w_scale=1.0)
+    path = '/tmp/esr_golden_plain_G.pth'
+    torch.save({k: torch.from_numpy(v) for k, v in psd.items()}, path)
+    cuda = torch.Tensor.cuda
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    try:
+        model.load_network(path, model.netG)
+    finally:
+        torch.Tensor.cuda = cuda
+    sd = model.netG.state_dict()
+    d = dict(keys=np.str_(json.dumps(list(sd.keys()))), sha=np.str_(json.dumps({k: _sha(v) for k, v in sd.items()})),
+             amplified=np.str_(json.dumps(model.channels_idx_4_grad_amplification)), plain_seed=np.int64(900),
+             cfg=np.str_(json.dumps(cfg)))
+    np.savez_compressed(os.path.join(HERE, 'ckpt_remap.npz'), **d)
+    print('ckpt_remap: %d keys, %d amplified' % (len(sd), sum(1 for c in model.channels_idx_4_grad_amplification if c)))
+    # save_network after one Adam step on three small parameters (optimizer state for those only)
+    model = build_reference(cfg, torch.float32)
+    names = ['generated_image_model.model.0.bias', 'generated_image_model.model.4.bias',
+             'generated_image_model.model.6.bias']
+    named = dict(model.netG.named_parameters())
+    rng = np.random.default_rng(901)
+    model.optimizer_G.zero_grad()
+    for n in names:
+        named[n].grad = torch.from_numpy(rng.standard_normal(tuple(named[n].shape)).astype(np.float32))
+    model.optimizer_G.step()
+    os.makedirs(os.path.join(HERE, 'ckpt'), exist_ok=True)
+    p = model.save_network(os.path.join(HERE, 'ckpt'), model.netG, 'G', 7, model.optimizer_G)
+    ref = {n: named[n].detach().numpy() for n in names}
+    st = model.optimizer_G.state_dict()
+    np.savez_compressed(os.path.join(HERE, 'ckpt_save.npz'), names=np.str_(json.dumps(names)),
+                        param_seed=np.int64(cfg['seed']), cfg=np.str_(json.dumps(cfg)),
+                        **{'after:' + n: v for n, v in ref.items()},
+                        **{'exp_avg:%d' % i: s['exp_avg'].numpy() for i, s in st['state'].items()},
+                        **{'exp_avg_sq:%d' % i: s['exp_avg_sq'].numpy() for i, s in st['state'].items()})
+    print('ckpt_save: %s (%d bytes), state for params %s' % (p, os.path.getsize(p), sorted(st['state'])))
+
+
+def main():
+    install_train_shims()
+    torch.set_num_threads(8)
+    which = sys.argv[1:] or list(TRAIN_CFGS) + ['ckpt']
+    for name in which:
+        if name == 'ckpt':
+            checkpoint_fixtures()
+        else:
+            train_fixture(name, TRAIN_CFGS[name])
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,66 @@
+"""Configurations and per-step data of the training-loop fixtures (tests/golden/make_golden_train.py runs the
+reference on them; tests/test_gpu_train_loop.py runs esr_amd on them).  Pure NumPy: no reference code.
+
+TEST INFRASTRUCTURE ONLY."""
+import numpy as np
+
+from oracle.recipe import seeded_inputs
+
+
+def train_opt(cfg):
+    """The shipped train_esrgan_CEM.json at fixture size (nb, batch, patch), with the loop knobs of `cfg`."""
+    patch = 4 * cfg['lr_size']
+    return {
+        'model': 'srragan', 'is_train': True, 'scale': 4, 'gpu_ids': None, 'range': [0, 1], 'test': None,
+        'path': {'log': '/tmp/esr_golden_train_log', 'models': '/tmp/esr_golden_train_models',
+                 'pretrain_model_G': None, 'pretrain_model_D': None},
+        'datasets': {'train': {'patch_size': patch, 'batch_size': cfg['batch']}},
+        'network_G': {'which_model_G': 'RRDB_net', 'CEM_arch': 1, 'latent_input': 'all_layers',
+                      'latent_input_domain': 'HR_downscaled', 'latent_channels': 'SVDinNormedOut_structure_tensor',
+                      'norm_type': None, 'mode': 'CNA', 'nf': 64, 'nb': cfg['nb'], 'in_nc': 3, 'out_nc': 3, 'gc': 32,
+                      'group': 1, 'scale': 4},
+        'network_D': {'which_model_D': 'discriminator_vgg_128', 'relativistic': cfg['relativistic'],
+                      'decomposed_input': 0, 'pre_clipping': 0, 'add_quantization_noise': 0, 'norm_type': 'batch',
+                      'act_type': 'leakyrelu', 'mode': 'CNA', 'n_layers': 6, 'nf': 64, 'in_nc': 3},
+        'train': {'resume': 0, 'lr_G': cfg['lr'], 'weight_decay_G': 0, 'beta1_G': 0.9, 'lr_D': cfg['lr'],
+                  'lr_E': 1e-4, 'lr_latent': cfg['lr'], 'weight_decay_D': 0, 'beta1_D': 0.9,
+                  'lr_scheme': 'MultiStepLR', 'lr_steps': [50000], 'lr_gamma': 0.5, 'pixel_domain': 'HR',
+                  'pixel_criterion': 'l1', 'feature_domain': 'HR', 'feature_criterion': 'l1', 'gan_type': 'wgan-gp',
+                  'optimalZ_loss_type': None, 'D_verification': cfg['D_verification'],
+                  'min_D_prob_ratio_4_G': cfg['min_D_prob_ratio_4_G'], 'min_mean_D_correct': cfg['min_mean_D_correct'],
+                  'D_update_ratio': cfg['D_update_ratio'], 'D_valid_Steps_4_G_update': cfg['D_valid_steps'],
+                  'CEM_exp': 1, 'pixel_weight': 0, 'feature_weight': 0, 'gan_weight': 1, 'latent_weight': 0,
+                  'optimalZ_loss_weight': 0, 'range_weight': 5000, 'highpass_weight': 0, 'shift_invariant_weight': 0,
+                  'D_init_iters': 0, 'E_init_iters': 40000, 'gp_weigth': 10,
+                  'grad_accumulation_steps_G': cfg['acc'], 'grad_accumulation_steps_D': cfg['acc']},
+    }
+
+
+def step_data(cfg, k):
+    """Micro-step k's batch: LR ~ U[0,1), HR ~ U[0,1) (patch size), per-image constant Z ~ U[-1,1) at HR size."""
+    B, h = cfg['batch'], cfg['lr_size']
+    lr, z = seeded_inputs(cfg['seed'] + 100 + k, (B, 3, h, h), (B, 3, 4 * h, 4 * h), z_mode='image')
+    hr = np.random.default_rng(cfg['seed'] + 200 + k).random((B, 3, 4 * h, 4 * h)).astype(np.float32)
+    return lr, hr, z
+
+
+def random_points(cfg):
+    rng = np.random.default_rng(cfg['seed'] + 300)
+    while True:
+        yield rng.random((cfg['batch'], 1, 1, 1)).astype(np.float32)
+
+
+# the shipped loop at fixture size: non-relativistic WGAN-GP, fixed D_update_ratio, D_verification 'past', gradient
+# accumulation 2; and the other branches: relativistic D, adaptive ratio (D_update_ratio 0), no verification
+TRAIN_CFGS = {
+    'past_ratio2_acc2': dict(nb=1, batch=2, lr_size=40, lr=1e-4, relativistic=0, D_update_ratio=2,
+                             D_verification='past', D_valid_steps=1, min_D_prob_ratio_4_G=float(np.exp(0.02)),
+                             min_mean_D_correct=-1.0, acc=2, steps=12, seed=500),
+    'adaptive_rel': dict(nb=1, batch=2, lr_size=40, lr=1e-4, relativistic=1, D_update_ratio=0,
+                         D_verification=None, D_valid_steps=2, min_D_prob_ratio_4_G=1.0,
+                         min_mean_D_correct=0.0, acc=1, steps=8, seed=600),
+}
+CKPT_CFG = dict(nb=1, batch=2, lr_size=40, lr=1e-4, relativistic=0, D_update_ratio=1, D_verification=None,
+                D_valid_steps=1, min_D_prob_ratio_4_G=1.0, min_mean_D_correct=0.0, acc=1, steps=0, seed=700)
+
+

@@ -143,3 +143,89 @@ def test_logs_and_lr_npz_roundtrip(tmp_path):
     m.save_lr(40)
     with np.load(tmp_path / 'lr.npz') as f:
         assert float(f['lr_G']) == 3e-5 and float(f['lr_D']) == 7e-5 and int(f['step_num']) == 40
+
+
+# ---- pinned by the reference itself (tests/golden/make_golden_train.py: the reference's base_model.py ran here) ----
+GOLDEN = os.path.join(os.path.dirname(__file__), 'golden')
+
+
+def _sha(t):
+    import hashlib
+    return hashlib.sha256(t.detach().contiguous().cpu().numpy().tobytes()).hexdigest()
+
+
+def _latent_cem_nb1(seed):
+    """The latent CEM generator (nb=1) holding the seeded parameters the reference model held (make_golden_train
+    build_reference: seeded_params over its state_dict keys, w_scale 1)."""
+    import json
+    from oracle.recipe import seeded_params
+    net = esr_amd.RRDBNet(3, 3, 64, 1, latent_input='all_layers_HR_downscaled', num_latent_channels=3)
+    cem = C.CEMnet(C.Get_CEM_Config(4))
+    model = cem.WrapArchitecture_PyTorch(net)
+    sd = model.state_dict()
+    params = seeded_params([(k, tuple(v.shape)) for k, v in sd.items()], seed, w_scale=1.0)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=False)
+    return cem, model, params
+
+
+def test_load_network_matches_reference_remap(tmp_path):
+    """base_model.load_network + process_loaded_state_dict (base_model.py:100-144) of a plain pretrained RRDBNet
+    state dict into the latent CEM generator, as the reference computed it: same key order, bitwise equal tensors
+    (the prepended latent weights are the reference's signed zeros), same gradient-amplified channel lists."""
+    import json
+    from oracle.recipe import seeded_params
+    d = np.load(os.path.join(GOLDEN, 'ckpt_remap.npz'))
+    cfg = json.loads(str(d['cfg']))
+    cem, model, _ = _latent_cem_nb1(cfg['seed'])
+    plain = esr_amd.RRDBNet(3, 3, 64, 1, num_latent_channels=0).state_dict()
+    psd = seeded_params([(k, tuple(v.shape)) for k, v in plain.items()], int(d['plain_seed']), w_scale=1.0)
+    path = str(tmp_path / 'plain_G.pth')
+    torch.save({k: torch.from_numpy(v) for k, v in psd.items()}, path)
+    m = _bare_model(cem, latent=True)
+    m.channels_idx_4_grad_amplification = [[] for _ in model.parameters()]
+    m.load_network(path, model)
+    sd = model.state_dict()
+    assert list(sd) == json.loads(str(d['keys']))
+    ref_sha = json.loads(str(d['sha']))
+    bad = [k for k, v in sd.items() if _sha(v) != ref_sha[k]]
+    assert not bad, bad
+    assert m.channels_idx_4_grad_amplification == json.loads(str(d['amplified']))
+
+
+def test_reference_saved_checkpoint_loads(tmp_path):
+    """A {step}_G.pth written by the reference's save_network (base_model.py:86-97) after one Adam step on three
+    parameters: load_network restores every parameter and the Adam state bit for bit; a checkpoint the port writes has
+    the same structure (keys, dtypes, shapes, optimizer param_groups keys)."""
+    import json
+    d = np.load(os.path.join(GOLDEN, 'ckpt_save.npz'))
+    cfg = json.loads(str(d['cfg']))
+    names = json.loads(str(d['names']))
+    cem, model, params = _latent_cem_nb1(cfg['seed'] + 1)  # different weights: the load must overwrite them all
+    gparams = [p for n, p in model.named_parameters() if 'Filter' not in n]
+    opt = torch.optim.Adam(gparams, lr=cfg['lr'], betas=(0.9, 0.999))
+    m = _bare_model(cem, latent=True)
+    m.channels_idx_4_grad_amplification = [[] for _ in model.parameters()]
+    ref_file = os.path.join(GOLDEN, 'ckpt', '7_G.pth')
+    m.load_network(ref_file, model, optimizer=opt)
+    _, _, expect = _latent_cem_nb1(cfg['seed'])
+    for k, v in model.named_parameters():
+        if 'Filter' in k:
+            continue
+        ref = d['after:' + k] if k in names else expect[k]
+        assert np.array_equal(v.detach().numpy(), ref), k
+    st = opt.state_dict()['state']
+    assert sorted(st) == sorted(int(f.split(':')[1]) for f in d.files if f.startswith('exp_avg:'))
+    for i, s in st.items():
+        assert np.array_equal(s['exp_avg'].numpy(), d['exp_avg:%d' % i])
+        assert np.array_equal(s['exp_avg_sq'].numpy(), d['exp_avg_sq:%d' % i])
+    mine = torch.load(m.save_network(str(tmp_path), model, 'G', 7, opt), weights_only=True)
+    ref = torch.load(ref_file, weights_only=True)
+    assert set(mine) == set(ref) == {'model_state_dict', 'optimizer_state_dict'}
+    assert list(mine['model_state_dict']) == list(ref['model_state_dict'])
+    for k, v in ref['model_state_dict'].items():
+        w = mine['model_state_dict'][k]
+        assert w.dtype == v.dtype and w.shape == v.shape and w.device == v.device, k
+        assert torch.equal(w, v), k
+    assert set(mine['optimizer_state_dict']) == set(ref['optimizer_state_dict'])
+    assert set(mine['optimizer_state_dict']['param_groups'][0]) >= {'lr', 'betas', 'eps', 'weight_decay', 'params'}
+    assert mine['optimizer_state_dict']['param_groups'][0]['params'] == ref['optimizer_state_dict']['param_groups'][0]['params']

@@ -235,6 +235,37 @@ def test_full_size_rrdb23_cem_vs_oracle(gpu_device, latent, precision):
     assert mse < 1e-8
 
 
+@pytest.mark.parametrize('precision', ['x3', 'f32'])
+@pytest.mark.parametrize('latent', [False, True])
+def test_c2_production_grid_vs_oracle_and_batch1(gpu_device, latent, precision):
+    """Config 2 at its real grid: B=32 × 128² LR, RRDB-23 + CEM eval (pre-pad → 148² tall batch image, the production
+    tile count and XCD remainder split of every conv launch).  Two images of the batch (first and last: different
+    tiles of the tall image, the last one touching its bottom edge) against the CPU oracle at the north_star 1e-3 bar,
+    and bitwise equal to the same images run alone (B=1)."""
+    B = 32
+    model, params = _big_model(23, latent, gpu_device, precision, seed=23)
+    model.eval()
+    g = torch.Generator().manual_seed(24)
+    lr = torch.rand(B, 3, 128, 128, generator=g)
+    x = lr
+    if latent:  # per-image constant Z as in training, a different one per image
+        z = (2 * torch.rand(B, 3, 1, 1, generator=g) - 1).expand(B, 3, 512, 512).contiguous()
+        x = torch.cat([z.view(B, 48, 128, 128), lr], 1)
+    xd = x.to(gpu_device)
+    with torch.no_grad():
+        out = model(xd)
+        torch.cuda.synchronize()
+        design = O.cem_design(4)
+        for i in (0, B - 1):
+            alone = model(xd[i:i + 1].contiguous())
+            assert torch.equal(out[i:i + 1], alone), i
+            ref = O.sr_forward(x[i:i + 1], O.strip_prefix(params), 23, latent, design, pre_pad=True)
+            err = normwise_rel(out[i:i + 1].cpu(), ref)
+            print('C2 grid image %d (latent=%s, %s): normwise %.3e' % (i, latent, precision, err))
+            assert err < 1e-3
+    assert tuple(out.shape) == (B, 3, 512, 512)
+
+
 @pytest.mark.parametrize('precision', ['f32', 'x3'])
 def test_cem_consistency_and_batch_invariance(gpu_device, precision):
     """Size-independent properties at a larger batch: (1) CEM consistency — DownscaleOP(SR) reproduces the LR input in
@@ -323,8 +354,9 @@ def test_x3_ring_kernel_bitwise_equals_classic(gpu_device, cin, cout, B, H, W):
     outs = []
     try:
         # classic one-stage (default), ring always, persistent ring always, ring / classic with the compiler-scheduled
-        # fragment reads, two-stage classic with prefetch 1 / 2 (none may change a bit)
-        for variant in (0, 2, 17, 18, 20, 21, 22, 25, 26, 27, 28):
+        # fragment reads, two-stage classic with prefetch 1 / 2, the round-1 automatic choice, the column-tile kernel
+        # (LDS / register weights) (none may change a bit)
+        for variant in (0, 2, 17, 18, 20, 21, 22, 25, 26, 27, 28, 24, 50, 60):
             lib.esr_x3_set_kernel(variant)
             out = torch.zeros(B, H + 2, W + 2, 40, device=gpu_device)
             out2 = torch.zeros(B, H + 2, W + 2, 32, device=gpu_device)
@@ -356,7 +388,9 @@ def test_x3_n64_explicit_reads_bitwise(gpu_device, cin, B, H, W):
     wx, scale = engine.pack_x3(engine.pack_conv_weight(w.to(gpu_device), list(range(cin)), 64))
     outs = []
     try:
-        for variant in (1, 20, 23):  # default, compiler-scheduled reads, 8-row tiles at two workgroups per CU
+        # default (column tiles), compiler-scheduled reads, 8-row tiles at two workgroups per CU, the round-1 default,
+        # column tiles with register weights
+        for variant in (1, 20, 23, 24, 60):
             lib.esr_x3_set_kernel(variant)
             out = torch.zeros(B, H + 2, W + 2, 64, device=gpu_device)
             o = engine._conv_out(out, 64, 0, H, W, True)
@@ -366,7 +400,8 @@ def test_x3_n64_explicit_reads_bitwise(gpu_device, cin, B, H, W):
             outs.append(out)
     finally:
         lib.esr_x3_set_kernel(1)
-    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    for k in range(1, len(outs)):
+        assert torch.equal(outs[0], outs[k]), k
     assert outs[0].abs().sum() > 0
 
 
@@ -399,7 +434,8 @@ def test_x3_xcd_tile_map_bitwise(gpu_device, cout, cin, B, H, W):
     assert normwise_rel(_nchw(engine.from_split(outs[0]), 0, cout), ref) < 1e-5
 
 
-@pytest.mark.parametrize('variant', [1, 27, 28])  # default, direct register epilogue 16- / 8-row
+# default, direct register epilogue 16- / 8-row, classic, column tiles
+@pytest.mark.parametrize('variant', [1, 27, 28, 24, 50])
 def test_conv3x3_x3_planar_output(gpu_device, variant):
     lib = _lib.load()
     B, H, W, cin = 2, 19, 45, 72

@@ -1,0 +1,82 @@
+"""State hazards of the cached executors: recorded inference op lists must survive the training
+path swapping the x3 weight tensors, and a second grad-enabled forward before the first one's backward must not
+overwrite the first forward's saved activations."""
+import pytest
+import torch
+
+from conftest import fixture_input, fixture_params, golden
+
+import esr_amd
+from esr_amd import CEMnet as C
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(params, dev, nb=1):
+    net = esr_amd.RRDBNet(3, 3, 64, nb, num_latent_channels=0)
+    model = C.CEMnet(C.Get_CEM_Config(4)).WrapArchitecture_PyTorch(net)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=False)
+    return model.to(dev)
+
+
+def test_recorded_inference_survives_training_forward(gpu_device):
+    """inference (records the op list) -> grad forward + backward with G unchanged (train_x3 swaps each layer's x3
+    weights for its persistent training views; no optimiser step, so the plan key is unchanged) -> the freed blocks
+    are reallocated and poisoned -> inference replays the recorded list: bitwise equal to the first inference and to a
+    fresh model's eager output."""
+    d = golden('grad_plain_nb1')
+    _, params = fixture_params(d)
+    x = fixture_input(d).to(gpu_device)
+    model = _model(params, gpu_device).eval()
+    with torch.no_grad():
+        first = model(x).clone()
+        again = model(x).clone()
+    assert torch.equal(first, again)
+    model.train()
+    (model(x) * torch.from_numpy(d['R']).to(gpu_device)).sum().backward()
+    model.eval()
+    poison = [torch.full((1 << k,), float('nan'), device=gpu_device, dtype=torch.float16) for k in range(8, 22)
+              for _ in range(4)]
+    with torch.no_grad():
+        replay = model(x).clone()
+    del poison
+    assert torch.equal(replay, first)
+    fresh = _model(params, gpu_device).eval()
+    with torch.no_grad():
+        assert torch.equal(fresh(x), first)
+
+
+def test_second_grad_forward_keeps_first_activations(gpu_device):
+    """Two generator calls inside one loss (y1 from x1, y2 from x2, then one backward through both): each call must
+    back-propagate through its own saved activations; the summed gradients equal the sum of two separate steps."""
+    d = golden('grad_plain_nb1')
+    _, params = fixture_params(d)
+    x1 = fixture_input(d).to(gpu_device)
+    x2 = torch.flip(x1, dims=[3]).contiguous()
+    R = torch.from_numpy(d['R']).to(gpu_device)
+
+    def grads(xs):
+        model = _model(params, gpu_device).train()
+        loss = sum((model(x) * R).sum() for x in xs)
+        loss.backward()
+        return [p.grad.clone() for p in model.parameters() if p.requires_grad]
+
+    both = grads([x1, x2])
+    g1, g2 = grads([x1]), grads([x2])
+    for b, a1, a2 in zip(both, g1, g2):
+        ref = a1 + a2
+        assert float((b - ref).norm() / ref.norm().clamp_min(1e-30)) < 1e-5
+
+
+def test_retained_graph_second_backward_raises_after_reuse(gpu_device):
+    """A forward whose workspace was handed to a later forward after its backward ran: a second backward through the
+    retained graph would read the later forward's activations, so it raises instead of returning wrong gradients."""
+    d = golden('grad_plain_nb1')
+    _, params = fixture_params(d)
+    x = fixture_input(d).to(gpu_device)
+    model = _model(params, gpu_device).train()
+    y = model(x)
+    y.sum().backward(retain_graph=True)
+    model(torch.flip(x, dims=[2]).contiguous()).sum().backward()
+    with pytest.raises(RuntimeError, match='overwritten'):
+        y.sum().backward()

@@ -1,0 +1,114 @@
+"""SRRaGANModel.optimize_parameters against the REFERENCE's own training loop (SRRaGAN_model.py:307-575), run by
+tests/golden/make_golden_train.py on the same seeded weights, batches and WGAN-GP interpolation points:
+  * the generator_step sequence (D_update_ratio fixed 2 / adaptive, D_verification 'past' with a blocking threshold,
+    gradient accumulation 2, relativistic and non-relativistic D) — exactly;
+  * every log_dict series (D/G losses, D statistics, update ratio), the G and D parameter updates after Adam (per-key
+    norms, projections on a seeded direction, full changes of the small keys) and the D BatchNorm running buffers.
+Yardstick: the reference ran in float32 and in float64; the port's distance to the float64 run must be within 5× the
+reference's own float32 distance plus a floor of 1e-4 of the quantity's norm (GAN training amplifies rounding: the
+reference's float32 and float64 runs already differ by up to a few % in late differences of nearly equal losses).
+Both generator precisions (x3 forward, exact fp32 forward; the backward is fp32 in both) are held to it."""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, 'golden'))
+from train_recipe import TRAIN_CFGS, random_points, step_data, train_opt  # noqa: E402
+
+from oracle.recipe import seeded_params  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+FACTOR, FLOOR = 5.0, 1e-4
+
+
+def _close(mine, f32, f64):
+    mine, f32, f64 = (np.asarray(v, dtype=np.float64).ravel() for v in (mine, f32, f64))
+    err, base = np.linalg.norm(mine - f64), np.linalg.norm(f32 - f64)
+    bound = FACTOR * base + FLOOR * max(np.linalg.norm(f64), 1e-12)
+    return err <= bound, 'err %.3e  bound %.3e  (ref f32 err %.3e, |ref| %.3e)' % (err, bound, base,
+                                                                                 np.linalg.norm(f64))
+
+
+def _run_port(cfg, precision, dev):
+    from esr_amd import engine
+    from esr_amd.SRRaGAN_model import SRRaGANModel
+    torch.manual_seed(0)
+    model = SRRaGANModel(train_opt(cfg), accumulation_steps_per_batch=cfg['acc'], device=dev)
+    gsd, dsd = model.netG.state_dict(), model.netD.state_dict()
+    gp = seeded_params([(k, tuple(v.shape)) for k, v in gsd.items()], cfg['seed'], w_scale=1.0)
+    dp = seeded_params([(k, tuple(v.shape)) for k, v in dsd.items() if 'running' not in k and 'num_batches' not in k],
+                       cfg['seed'] + 1, w_scale=1.0)
+    model.netG.load_state_dict({k: torch.from_numpy(v) for k, v in gp.items()}, strict=False)
+    model.netD.load_state_dict({k: torch.from_numpy(v) for k, v in dp.items()}, strict=False)
+    engine.set_precision(model.netG, precision)
+    pts = random_points(cfg)
+    model._interp_points = lambda n: torch.from_numpy(next(pts)).to(dev).view(n, 1, 1, 1)
+    g0 = {k: v.detach().clone() for k, v in model.netG.named_parameters()}
+    d0 = {k: v.detach().clone() for k, v in model.netD.named_parameters()}
+    flags = []
+    for k in range(cfg['steps']):
+        lr, hr, z = step_data(cfg, k)
+        t = lambda a: torch.from_numpy(a).to(dev)  # noqa: E731
+        model.feed_data({'LR': t(lr), 'HR': t(hr), 'Z': t(z)})
+        model.optimize_parameters()
+        flags.append(bool(model.generator_step))
+    return model, g0, d0, flags
+
+
+@pytest.mark.parametrize('precision', ['x3', 'f32'])
+@pytest.mark.parametrize('name', sorted(TRAIN_CFGS))
+def test_optimize_parameters_vs_reference_loop(gpu_device, name, precision):
+    d = np.load(os.path.join(HERE, 'golden', 'train_%s.npz' % name))
+    cfg = json.loads(str(d['cfg']))
+    model, g0, d0, flags = _run_port(cfg, precision, gpu_device)
+    assert flags == list(d['f64_generator_step']) == list(d['f32_generator_step'])
+    fails = []
+    for f in [f for f in d.files if f.startswith('f64_log:')]:
+        key = f[len('f64_log:'):]
+        ref64, ref32 = d[f], d['f32_log:' + key]
+        mine = np.array(model.log_dict[key], dtype=np.float64)
+        assert mine.shape == ref64.shape, (key, mine.shape, ref64.shape)
+        assert np.array_equal(mine[:, 0], ref64[:, 0]), key  # gradient-step numbers
+        ok, msg = _close(mine[:, 1], ref32[:, 1], ref64[:, 1])
+        print('log %-24s %s' % (key, msg))
+        if not ok:
+            fails.append(('log', key, msg))
+    for net, start, tag in ((model.netG, g0, 'G'), (model.netD, d0, 'D')):
+        named = dict(net.named_parameters())
+        rng = np.random.default_rng(cfg['seed'] + (400 if tag == 'G' else 401))
+        dn, dp, small = {'m': [], '32': [], '64': []}, {'m': [], '32': [], '64': []}, {'m': [], '32': [], '64': []}
+        for k in named:
+            f = named[k].detach().double().cpu().numpy()
+            delta = f - start[k].double().cpu().numpy()
+            p = rng.standard_normal(f.shape)
+            dn['m'].append(np.linalg.norm(delta))
+            dp['m'].append((p * delta).sum())
+            for r in ('32', '64'):
+                dn[r].append(float(d['f%s_%s_dnorm:%s' % (r, tag, k)]))
+                dp[r].append(float(d['f%s_%s_dproj:%s' % (r, tag, k)]))
+            if 'f64_%s_delta:%s' % (tag, k) in d.files:
+                small['m'].append(delta.ravel())
+                for r in ('32', '64'):
+                    small[r].append(d['f%s_%s_delta:%s' % (r, tag, k)].ravel())
+        for what, v in (('update norms', dn), ('update projections', dp)):
+            ok, msg = _close(v['m'], v['32'], v['64'])
+            print('%s %-20s %s' % (tag, what, msg))
+            if not ok:
+                fails.append((tag, what, msg))
+        if small['m']:
+            ok, msg = _close(*(np.concatenate(small[r]) for r in ('m', '32', '64')))
+            print('%s %-20s %s' % (tag, 'small-key updates', msg))
+            if not ok:
+                fails.append((tag, 'small-key updates', msg))
+    for k, v in model.netD.state_dict().items():
+        if 'running' in k:
+            ok, msg = _close(v.double().cpu().numpy(), d['f32_Dbuf:' + k], d['f64_Dbuf:' + k])
+            if not ok:
+                fails.append(('D buffer', k, msg))
+    assert not fails, fails
