@@ -13,8 +13,9 @@ logs.npz / lr.npz; checkpoints are read with torch.load(weights_only=True).  Che
 TensorBoard are out of scope.
 
 Multi-GPU: one process per GPU (torch.distributed, RCCL).  The reference's nn.DataParallel computes every loss on the
-gathered global batch; with equal per-rank batches the average of per-rank gradients equals that gradient, so after
-each backward the G / D gradients are all-reduced (average, one flat bucket per network).  BatchNorm statistics stay
+gathered global batch; with equal per-rank batches the average of per-rank gradients equals that gradient, so the G / D
+gradients of the last accumulation micro-step are averaged by bucketed asynchronous all-reduces launched from inside
+the backward as each bucket's gradients become final (GradBuckets).  BatchNorm statistics stay
 per-replica (as DataParallel's) and the running buffers are broadcast from rank 0 (DataParallel keeps replica 0's).
 The per-image D statistics that gate the generator step are all-reduced so that every rank takes the same branch.
 """
@@ -73,6 +74,85 @@ def _allreduce_grads(params):
         n = g.numel()
         g.copy_(flat[o:o + n].view_as(g))
         o += n
+
+
+class GradBuckets:
+    """DDP-style gradient averaging for one network over ranks (the reference's nn.DataParallel, networks.py:99-101,
+    125-126, computes every loss on the gathered global batch; with equal per-rank batches the average of the per-rank
+    gradients is that gradient).
+
+    Parameters are grouped into buckets of at most `cap_bytes` in reverse registration order — the order a backward
+    finalises them (output layers first).  While armed (the last micro-step of a gradient accumulation), a
+    post-accumulate-grad hook marks each parameter whose gradient that backward has finished; when a bucket is
+    complete its flattened gradients go out as one asynchronous all-reduce (RCCL over xGMI), overlapping the rest of the
+    backward.  `finish()` launches any bucket whose parameters got no gradient in this backward (requires_grad toggled
+    off, or not reached), waits for every bucket, averages and writes back.  Buckets are ≥ a few MB so that each ring
+    all-reduce runs near the per-link xGMI bandwidth rather than its latency."""
+
+    def __init__(self, params, cap_bytes=16 << 20):
+        self.params = list(params)
+        self.buckets, cur, size = [], [], 0
+        for p in reversed(self.params):
+            n = p.numel() * p.element_size()
+            if cur and size + n > cap_bytes:
+                self.buckets.append(cur)
+                cur, size = [], 0
+            cur.append(p)
+            size += n
+        if cur:
+            self.buckets.append(cur)
+        self.where = {id(p): b for b, ps in enumerate(self.buckets) for p in ps}
+        self.armed = False
+        self.launched_in_backward = 0
+        self._pending = [set() for _ in self.buckets]
+        self._works = [None] * len(self.buckets)
+        self.hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params] \
+            if _world() > 1 else []
+
+    def arm(self):
+        self.armed = _world() > 1
+        self._pending = [set(id(p) for p in ps) for ps in self.buckets]
+        self._works = [None] * len(self.buckets)
+        self.launched_in_backward = 0
+
+    def _launch(self, b):
+        grads = [p.grad for p in self.buckets[b] if p.grad is not None]
+        if not grads:
+            self._works[b] = ()
+            return
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        self._works[b] = (dist.all_reduce(flat, async_op=True), flat, grads)
+
+    def _on_grad(self, p):
+        if not self.armed:
+            return
+        b = self.where[id(p)]
+        pend = self._pending[b]
+        pend.discard(id(p))
+        if not pend and self._works[b] is None:
+            self._launch(b)
+            self.launched_in_backward += 1
+
+    def finish(self):
+        if not self.armed:
+            return
+        self.armed = False
+        for b in range(len(self.buckets)):
+            if self._works[b] is None:
+                self._launch(b)
+        w = _world()
+        for item in self._works:
+            if not item:
+                continue
+            work, flat, grads = item
+            work.wait()
+            flat /= w
+            o = 0
+            for g in grads:
+                n = g.numel()
+                g.copy_(flat[o:o + n].view_as(g))
+                o += n
+        self._works = [None] * len(self.buckets)
 
 
 def _broadcast_buffers(module):
@@ -177,6 +257,8 @@ class SRRaGANModel:
             self.global_D_update_ratio, self.D_init_iters = 1, 0
         self.schedulers = [torch.optim.lr_scheduler.MultiStepLR(o, t['lr_steps'], t['lr_gamma'])
                            for o in self.optimizers]
+        self._g_buckets = GradBuckets(gparams)
+        self._d_buckets = GradBuckets(list(self.netD.parameters())) if self.D_exists else None
 
     # ------------------------------------------------------------------------------------------------------------------
     def ConcatLatent(self, LR_image, latent_input):
@@ -257,6 +339,24 @@ class SRRaGANModel:
             return int(-2 * np.ceil((log_mean + 1) * 2) / 2)
         return 1 / max(1, int(np.floor((log_mean + 2) * 20)))
 
+    def _gate_generator_step(self, t, first_acc_D, diff, correct):
+        """SRRaGAN_model.py:400-427: whether this micro-step also updates G.  `diff`/`correct` are this micro-step's
+        D statistics over the GLOBAL batch (all-reduced by _d_statistics) and log_dict holds the all-reduced history,
+        so every rank takes the same branch, as DataParallel's single process did."""
+        if first_acc_D:
+            self.generator_step = (self.gradient_step_num % max(1, self.cur_D_update_ratio) == 0 and
+                                   self.gradient_step_num > self.D_init_iters)
+            self.generator_step = self.generator_step and self.step % self.grad_accumulation_steps_D >= \
+                self.grad_accumulation_steps_D - self.grad_accumulation_steps_G
+            if self.generator_step and self.D_verification == 'past' and t.get('D_valid_Steps_4_G_update', 0) > 0:
+                n = t['D_valid_Steps_4_G_update']
+                self.generator_step = len(self.log_dict['D_logits_diff']) >= n and \
+                    all(v[1] > np.log(t['min_D_prob_ratio_4_G']) for v in self.log_dict['D_logits_diff'][-n:]) and \
+                    all(v[1] > t['min_mean_D_correct'] for v in self.log_dict['Correctly_distinguished'][-n:])
+        if self.D_verification == 'current' and self.generator_step:
+            self.generator_step = correct == 1.0 and diff > np.log(t['min_D_prob_ratio_4_G'])
+        return self.generator_step
+
     def _interp_points(self, n):
         """WGAN-GP interpolation points, one per image (SRRaGAN_model.py:388-391, random_pt.uniform_())."""
         return torch.rand(n, 1, 1, 1, device=self.device)
@@ -310,23 +410,14 @@ class SRRaGANModel:
                 l_d_total = l_d_total + l_d_gp
             diff, correct, d_real, d_fake = self._d_statistics(pred_d_real, pred_d_fake)
             self._d_logs.append((l_d_real.item(), l_d_fake.item(), d_real, d_fake, diff, correct))
-            if first_acc_D:
-                self.generator_step = (self.gradient_step_num % max(1, self.cur_D_update_ratio) == 0 and
-                                       self.gradient_step_num > self.D_init_iters)
-                self.generator_step = self.generator_step and self.step % self.grad_accumulation_steps_D >= \
-                    self.grad_accumulation_steps_D - self.grad_accumulation_steps_G
-                if self.generator_step and self.D_verification == 'past' and t.get('D_valid_Steps_4_G_update', 0) > 0:
-                    n = t['D_valid_Steps_4_G_update']
-                    self.generator_step = len(self.log_dict['D_logits_diff']) >= n and \
-                        all(v[1] > np.log(t['min_D_prob_ratio_4_G']) for v in self.log_dict['D_logits_diff'][-n:]) and \
-                        all(v[1] > t['min_mean_D_correct'] for v in self.log_dict['Correctly_distinguished'][-n:])
-            if self.D_verification == 'current' and self.generator_step:
-                self.generator_step = correct == 1.0 and diff > np.log(t['min_D_prob_ratio_4_G'])
+            self._gate_generator_step(t, first_acc_D, diff, correct)
             if G_grads_retained and not self.generator_step:
                 self.fake_H = self.fake_H.detach()
+            if last_acc_D:
+                self._d_buckets.arm()  # bucket all-reduces launch from inside this backward
             (l_d_total / self.grad_accumulation_steps_D).backward(retain_graph=self.generator_step)
             if last_acc_D:
-                _allreduce_grads(list(self.netD.parameters()))
+                self._d_buckets.finish()
                 self.optimizer_D.step()
                 _broadcast_buffers(self.netD)
                 a = np.mean(np.array(self._d_logs), axis=0)
@@ -359,13 +450,15 @@ class SRRaGANModel:
                     l_g_gan = self.l_gan_w * self.cri_gan(pred_g_fake, True)
                 l_g_gan = l_g_gan / self.grad_accumulation_steps_G  # logged divided, as the reference (:526, 539)
                 l_g_total = l_g_total + l_g_gan
+            if last_acc_G:
+                self._g_buckets.arm()
             l_g_total.backward()
             if self.cri_range is not None:
                 self._g_logs['l_g_range'].append(l_g_range.item())
             if self.D_exists:
                 self._g_logs['l_g_gan'].append(l_g_gan.item())
             if last_acc_G:
-                _allreduce_grads([p for p in self.netG.parameters() if p.requires_grad])
+                self._g_buckets.finish()
                 if self.latent_input is not None and self.latent_grads_multiplier != 1:  # :543-546
                     for idx, p in zip(self.channels_idx_4_grad_amplification, self.netG.parameters()):
                         for c in idx:

@@ -4,10 +4,15 @@ tests/golden/make_golden_train.py on the same seeded weights, batches and WGAN-G
     gradient accumulation 2, relativistic and non-relativistic D) — exactly;
   * every log_dict series (D/G losses, D statistics, update ratio), the G and D parameter updates after Adam (per-key
     norms, projections on a seeded direction, full changes of the small keys) and the D BatchNorm running buffers.
-Yardstick: the reference ran in float32 and in float64; the port's distance to the float64 run must be within 5× the
-reference's own float32 distance plus a floor of 1e-4 of the quantity's norm (GAN training amplifies rounding: the
-reference's float32 and float64 runs already differ by up to a few % in late differences of nearly equal losses).
-Both generator precisions (x3 forward, exact fp32 forward; the backward is fp32 in both) are held to it."""
+Yardstick: the reference ran in float32 and in float64; the port's L2 distance to the float64 run must be within 5×
+the reference's own float32 distance plus a floor of 1e-4 of the quantity's scale.  GAN training amplifies rounding
+(the reference's own float32 and float64 runs differ by up to a few % in late differences of nearly equal losses), so
+the scale of a series that is a difference of D outputs (D_logits_diff, l_d_real/l_d_fake/l_d_real_fake — relativistic
+or not) is the norm of the D outputs it is formed from, not of the difference itself.  Projections of the parameter
+updates on a random direction additionally allow 5 % of their norm: near-zero gradient components flip the sign of
+their first Adam updates (±lr each) under any rounding change; the reference's own float32 run is already 1-2 % off
+there, while a wrong learning rate, step count, accumulation or gating moves them by O(1).  Both generator precisions
+(x3 forward, exact fp32 forward; the backward is fp32 in both) are held to it."""
 import json
 import os
 import sys
@@ -27,12 +32,17 @@ pytestmark = pytest.mark.gpu
 FACTOR, FLOOR = 5.0, 1e-4
 
 
-def _close(mine, f32, f64):
+D_DIFFERENCES = ('l_d_real', 'l_d_fake', 'l_d_real_fake', 'D_logits_diff')
+PROJ_REL = 0.05
+
+
+def _close(mine, f32, f64, scale=None, rel=0.0):
     mine, f32, f64 = (np.asarray(v, dtype=np.float64).ravel() for v in (mine, f32, f64))
-    err, base = np.linalg.norm(mine - f64), np.linalg.norm(f32 - f64)
-    bound = FACTOR * base + FLOOR * max(np.linalg.norm(f64), 1e-12)
-    return err <= bound, 'err %.3e  bound %.3e  (ref f32 err %.3e, |ref| %.3e)' % (err, bound, base,
-                                                                                 np.linalg.norm(f64))
+    err, base, norm = np.linalg.norm(mine - f64), np.linalg.norm(f32 - f64), np.linalg.norm(f64)
+    scale = norm if scale is None else scale
+    bound = FACTOR * base + FLOOR * max(scale, 1e-12) + rel * norm
+    return err <= bound, 'err %.3e  bound %.3e  (ref f32 err %.3e, |ref| %.3e, scale %.3e)' % (
+        err, bound, base, norm, scale)
 
 
 def _run_port(cfg, precision, dev):
@@ -75,7 +85,10 @@ def test_optimize_parameters_vs_reference_loop(gpu_device, name, precision):
         mine = np.array(model.log_dict[key], dtype=np.float64)
         assert mine.shape == ref64.shape, (key, mine.shape, ref64.shape)
         assert np.array_equal(mine[:, 0], ref64[:, 0]), key  # gradient-step numbers
-        ok, msg = _close(mine[:, 1], ref32[:, 1], ref64[:, 1])
+        scale = None
+        if key in D_DIFFERENCES:
+            scale = 2 * (np.linalg.norm(d['f64_log:D_real'][:, 1]) + np.linalg.norm(d['f64_log:D_fake'][:, 1]))
+        ok, msg = _close(mine[:, 1], ref32[:, 1], ref64[:, 1], scale)
         print('log %-24s %s' % (key, msg))
         if not ok:
             fails.append(('log', key, msg))
@@ -96,8 +109,8 @@ def test_optimize_parameters_vs_reference_loop(gpu_device, name, precision):
                 small['m'].append(delta.ravel())
                 for r in ('32', '64'):
                     small[r].append(d['f%s_%s_delta:%s' % (r, tag, k)].ravel())
-        for what, v in (('update norms', dn), ('update projections', dp)):
-            ok, msg = _close(v['m'], v['32'], v['64'])
+        for what, v, rel in (('update norms', dn, 0.0), ('update projections', dp, PROJ_REL)):
+            ok, msg = _close(v['m'], v['32'], v['64'], rel=rel)
             print('%s %-20s %s' % (tag, what, msg))
             if not ok:
                 fails.append((tag, what, msg))

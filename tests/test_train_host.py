@@ -1,6 +1,7 @@
 """CPU tests of the training-step host side: discriminator layout + forward/GP/range losses vs the reference's golden
 vector, and the multi-process (gloo, world size 2) gradient / statistics reductions of SRRaGANModel."""
 import json
+import copy
 import os
 
 import numpy as np
@@ -90,7 +91,49 @@ def _dist_worker(rank, world, port, q):
         pred_real = torch.full((2, 1, 3, 3), 1.0 + rank)          # per-image diffs: rank 0: (+1,+1)
         pred_fake = torch.tensor([0.0, 3.0 + rank]).view(2, 1, 1, 1).expand(2, 1, 3, 3)  # rank 1: (+2,-2)
         diff, correct, d_real, d_fake = m._d_statistics(pred_real, pred_fake)
-        q.put((rank, p[0].grad.clone(), p[1].grad.clone(), diff, correct, d_real, d_fake))
+        # bucketed all-reduce launched from inside the backward (several buckets), against a flat average
+        torch.manual_seed(0)
+        net = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 16), torch.nn.ReLU(),
+                                  torch.nn.Linear(16, 4))
+        ref_net = copy.deepcopy(net)
+        x = torch.randn(5, 8, generator=torch.Generator().manual_seed(10 + rank))
+        buckets = M.GradBuckets(list(net.parameters()), cap_bytes=600)
+        buckets.arm()
+        net(x).square().sum().backward()
+        launched = buckets.launched_in_backward
+        buckets.finish()
+        ref_net(x).square().sum().backward()
+        M._allreduce_grads(list(ref_net.parameters()))
+        same = all(torch.allclose(a.grad, b.grad, rtol=1e-6, atol=1e-7) for a, b in zip(net.parameters(),
+                                                                                         ref_net.parameters()))
+        # an unarmed backward (not the last accumulation micro-step) leaves the local gradients alone
+        net.zero_grad()
+        net(x).square().sum().backward()
+        local = [q_.grad.clone() for q_ in net.parameters()]
+        buckets.finish()
+        untouched = all(torch.equal(a, q_.grad) for a, q_ in zip(local, net.parameters()))
+        # BatchNorm running buffers: rank 0's everywhere
+        bn = torch.nn.BatchNorm2d(3)
+        bn.running_mean.fill_(rank + 1.0)
+        bn.num_batches_tracked.fill_(7 * (rank + 1))
+        M._broadcast_buffers(bn)
+        bufs = (float(bn.running_mean[0]), int(bn.num_batches_tracked))
+        # generator_step gating on ranks whose LOCAL D statistics disagree: rank 0's two images are both classified
+        # correctly (a local 'current' check would pass), rank 1 has one wrong; the global batch has 3 of 4 correct
+        g = M.SRRaGANModel.__new__(M.SRRaGANModel)
+        g.gradient_step_num, g.cur_D_update_ratio, g.D_init_iters, g.step = 4, 2, 0, 8
+        g.grad_accumulation_steps_D = g.grad_accumulation_steps_G = 1
+        t = {'min_D_prob_ratio_4_G': 1.01, 'min_mean_D_correct': 0.6, 'D_valid_Steps_4_G_update': 1}
+        pr = torch.full((2, 1, 2, 2), 1.0)
+        pf = torch.tensor([0.0, 0.0 if rank == 0 else 3.0]).view(2, 1, 1, 1).expand(2, 1, 2, 2)
+        gd, gc, _, _ = g._d_statistics(pr, pf)
+        g.D_verification = 'current'
+        cur = g._gate_generator_step(t, True, gd, gc)
+        g.D_verification = 'past'  # history of all-reduced values, identical on every rank
+        g.log_dict = {'D_logits_diff': [(3, 0.5)], 'Correctly_distinguished': [(3, 0.75)]}
+        past = g._gate_generator_step(t, True, gd, gc)
+        q.put((rank, p[0].grad.clone(), p[1].grad.clone(), diff, correct, d_real, d_fake, launched, same, untouched,
+               bufs, gd, gc, cur, past))
     finally:
         dist.destroy_process_group()
 
@@ -114,4 +157,14 @@ def test_ddp_gradient_average_and_consistent_statistics():
     # images: rank0 diffs (1-0, 1-3) = (1,-2); rank1 (2-0, 2-4) = (2,-2) -> mean -0.25, correct 0.5
     for r in res:
         assert abs(r[3] - (-0.25)) < 1e-6 and abs(r[4] - 0.5) < 1e-6
-    assert res[0][3:] == res[1][3:]
+    assert res[0][3:7] == res[1][3:7]
+    for r in res:
+        launched, same, untouched, bufs = r[7:11]
+        assert launched >= 2, launched  # at least two buckets went out before backward() returned
+        assert same and untouched
+        assert bufs == (1.0, 7)
+        gd, gc, cur, past = r[11:]
+        assert abs(gc - 0.75) < 1e-6 and abs(gd - 0.25) < 1e-6  # global batch: diffs (1, 1, 1, -2)
+        assert cur is False  # 3 of 4 correct globally: no G step on either rank (rank 0 alone would say yes)
+        assert past is True  # the shared history passes 'past' on both ranks
+    assert res[0][11:] == res[1][11:]
