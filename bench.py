@@ -12,6 +12,9 @@ One JSON line on rank 0: value = HR Mpixels/s over all ranks; `roofline` = the d
 instantiation that takes the most time) from HIP events around every launch in the timed region (recorded natively by
 the op-list executor esr_run_ops, so the timing adds no host round trips); `cpu_baseline` =
 the CPU oracle restatement (oracle/esr_oracle.py, PyTorch-CPU oneDNN convs) on a bounded sample, rank 0 only.
+Extra keys, each timed separately after the headline (--no-legs skips them): `fp32_c2` (the same step in exact fp32),
+`train_c3` / `train_c4` (one SRRaGANModel.optimize_parameters step, bench_train.py), `zopt_c5` (one Z-optimisation
+iteration, bench_zopt.py).
 """
 import argparse
 import json
@@ -51,6 +54,9 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--precision', choices=['x3', 'f32'], default='x3')
     ap.add_argument('--cpu-images', type=int, default=8, help='images in the bounded CPU-baseline sample')
+    ap.add_argument('--no-legs', action='store_true', help='skip the extra legs (exact-fp32 C2, C3/C4 training step, '
+                    'C5 Z-optimisation iteration)')
+    ap.add_argument('--leg-steps', type=int, default=3)
     return ap.parse_args()
 
 
@@ -124,6 +130,58 @@ def pmc_traffic(kernel_tag):
             return (r['hbm_read_bytes_per_launch'] + (r['hbm_write_bytes_per_launch'] or 0.0),
                     '%s (%s)' % (os.path.relpath(path, REPO), d['source']))
     return None
+
+
+def _timed(fn, steps, dev, world):
+    """Seconds for `steps` calls of fn(), barrier + synchronize bracketed, max over ranks."""
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt
+
+
+def run_legs(args, dev, world, rank):
+    """Extra legs in the same run, each timed on its own after the headline's timed region (HIP work synchronised,
+    barrier, max over ranks): the C2 step in exact fp32, one C3 training step (C4 when N>1: DP over RCCL) and one C5
+    Z-optimisation iteration.  A failing leg records its error instead of a number."""
+    import argparse as ap_
+    import bench_train
+    import bench_zopt
+    legs = {}
+    try:
+        a = ap_.Namespace(**vars(args))
+        a.precision = 'f32'
+        model = build_model(a, dev)
+        x = make_input(a, dev, rank)
+        with torch.no_grad():
+            model(x)
+            dt = _timed(lambda: model(x), args.leg_steps, dev, world)
+        hr = 4 * args.lr_size
+        legs['fp32_c2'] = {'value': round(world * args.batch * hr * hr * args.leg_steps / dt / 1e6, 3),
+                           'unit': 'HR Mpixels/s', 'ms_per_step': round(dt / args.leg_steps * 1e3, 2),
+                           'steps': args.leg_steps, 'dtype': 'f32',
+                           'note': 'the headline workload with every conv in exact fp32 (f32-input MFMA)'}
+        del model, x
+    except Exception as e:  # noqa: BLE001
+        legs['fp32_c2'] = {'error': repr(e)}
+    torch.cuda.empty_cache()
+    for key, mod in (('train_c4' if world > 1 else 'train_c3', bench_train), ('zopt_c5', bench_zopt)):
+        try:
+            legs[key] = mod.run(mod.leg_args(steps=args.leg_steps), dev, world, rank)
+        except Exception as e:  # noqa: BLE001
+            legs[key] = {'error': repr(e)}
+        torch.cuda.empty_cache()
+    return legs
 
 
 def main():
@@ -211,6 +269,8 @@ def main():
         cb, parity = cpu_baseline(args, model, x, out)
         rec['cpu_baseline'] = cb
         rec['parity'] = parity
+    if not args.no_legs:
+        rec.update(run_legs(args, dev, world, rank))
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if world > 1:

@@ -40,23 +40,17 @@ def make_opt(args):
     }
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=5)
-    ap.add_argument('--warmup', type=int, default=2)
-    ap.add_argument('--batch', type=int, default=16)
-    ap.add_argument('--lr-size', type=int, default=96)
-    ap.add_argument('--nb', type=int, default=23)
-    ap.add_argument('--no-latent', dest='latent', action='store_false')
-    args = ap.parse_args()
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    torch.cuda.set_device(local)
-    dev = torch.device('cuda', local)
-    if world > 1:
-        dist.init_process_group('nccl', device_id=dev)
+def leg_args(**kw):
+    """Default arguments of this benchmark (BASELINE config 3 per GPU), for callers such as bench.py."""
+    d = dict(gpus=1, steps=3, warmup=2, batch=16, lr_size=96, nb=23, latent=True)
+    d.update(kw)
+    return argparse.Namespace(**d)
+
+
+def run(args, dev, world, rank):
+    """Build the model, run args.warmup + args.steps optimize_parameters() calls (timed: the steps, bracketed by
+    barrier + synchronize, max over ranks), return the JSON record."""
+    from esr_amd import engine
     from esr_amd.SRRaGAN_model import SRRaGANModel
     torch.manual_seed(1000 + rank)
     model = SRRaGANModel(make_opt(args), device=dev)
@@ -87,16 +81,41 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     value = world * args.batch * hr * hr * args.steps / dt / 1e6
-    rec = {'metric': 'training HR Mpixels/s (RRDB-23 + CEM G fwd+bwd, VGG128_ D + WGAN-GP, Adam)', 'value': round(value, 4),
-           'unit': 'HR Mpixels/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
-           'ms_per_step': round(dt / args.steps * 1e3, 2), 'higher_is_better': True, 'scaling': 'weak',
-           'dtype': 'f32', 'data': 'synthetic', 'generator_steps_in_timed_region': gsteps,
-           'config': {'workload': 'BASELINE config %s: batch %d/GPU of %dx%d LR crops (%dx%d HR, D on %dx%d after CEM '
-                                  'unpad), nb=%d, latent=%s' % ('4' if world > 1 else '3', args.batch, args.lr_size,
-                                                                 args.lr_size, hr, hr, hr - 80, hr - 80, args.nb,
-                                                                 args.latent),
-                      'global_batch': world * args.batch, 'parallelism': 'dp%d (RCCL all-reduce of G/D grads)' % world},
-           'last_losses': {k: v[-1][1] for k, v in model.log_dict.items() if v}}
+    fwd = getattr(model.netG.module if hasattr(model.netG, 'module') else model.netG, 'generated_image_model',
+                  None)
+    fwd = getattr(fwd, 'esr_precision', engine.DEFAULT_PRECISION) if fwd is not None else engine.DEFAULT_PRECISION
+    return {'metric': 'training HR Mpixels/s (RRDB-23 + CEM G fwd+bwd, VGG128_ D + WGAN-GP, Adam)',
+            'value': round(value, 4), 'unit': 'HR Mpixels/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': round(dt / args.steps * 1e3, 2), 'higher_is_better': True,
+            'scaling': 'weak', 'dtype': 'f32', 'fwd_dtype': fwd, 'bwd_dtype': 'f32', 'data': 'synthetic',
+            'generator_steps_in_timed_region': gsteps,
+            'config': {'workload': 'BASELINE config %s: batch %d/GPU of %dx%d LR crops (%dx%d HR, D on %dx%d after '
+                                   'CEM unpad), nb=%d, latent=%s' % ('4' if world > 1 else '3', args.batch,
+                                                                      args.lr_size, args.lr_size, hr, hr, hr - 80,
+                                                                      hr - 80, args.nb, args.latent),
+                       'global_batch': world * args.batch,
+                       'parallelism': 'dp%d (bucketed RCCL all-reduce of G/D grads)' % world},
+            'last_losses': {k: v[-1][1] for k, v in model.log_dict.items() if v}}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--batch', type=int, default=16)
+    ap.add_argument('--lr-size', type=int, default=96)
+    ap.add_argument('--nb', type=int, default=23)
+    ap.add_argument('--no-latent', dest='latent', action='store_false')
+    args = ap.parse_args()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=dev)
+    rec = run(args, dev, world, rank)
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if world > 1:

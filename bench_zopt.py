@@ -31,23 +31,17 @@ def learned_kernel(size=13, sigma=(1.6, 2.6), theta=np.pi / 6):
     return k / k.sum()
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=5)
-    ap.add_argument('--warmup', type=int, default=2)
-    ap.add_argument('--batch', type=int, default=8)
-    ap.add_argument('--lr-size', type=int, default=128)
-    ap.add_argument('--nb', type=int, default=23)
-    ap.add_argument('--objective', default='max_STD')
-    args = ap.parse_args()
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    torch.cuda.set_device(local)
-    dev = torch.device('cuda', local)
-    if world > 1:
-        dist.init_process_group('nccl', device_id=dev)
+def leg_args(**kw):
+    """Default arguments of this benchmark (BASELINE config 5 per GPU), for callers such as bench.py."""
+    d = dict(gpus=1, steps=3, warmup=2, batch=8, lr_size=128, nb=23, objective='max_STD')
+    d.update(kw)
+    return argparse.Namespace(**d)
+
+
+def run(args, dev, world, rank):
+    """Build the latent CEM model with the learned kernel, run args.warmup then args.steps Z iterations (timed,
+    barrier + synchronize bracketed, max over ranks), return the JSON record."""
+    from esr_amd import engine
     from esr_amd.SRRaGAN_model import SRRaGANModel
     from esr_amd.Z_optimization import Z_optimizer
     from esr_amd import networks
@@ -85,17 +79,39 @@ def main():
         dt = float(t.item())
     m = int(cem.margins_LR)
     flop_iter = 2 * 2 * 18316944 * (h + 2 * m) ** 2 * B  # fwd + input dgrad, SURVEY.md §8(d) latent MAC/LR-px
-    rec = {'metric': 'Z-optimisation HR Mpixels/s per iteration (latent RRDB-23 + learned-kernel CEM, fwd + dZ + Adam)',
-           'value': round(world * B * (4 * h) ** 2 * args.steps / dt / 1e6, 4), 'unit': 'HR Mpixels/s',
-           'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
-           'ms_per_step': round(dt / args.steps * 1e3, 2), 'higher_is_better': True, 'scaling': 'weak',
-           'dtype': 'f32', 'data': 'synthetic',
-           'achieved_TFLOPs': round(flop_iter * args.steps / dt / 1e12, 2),
-           'config': {'workload': 'BASELINE config 5: batch %d/GPU of %dx%d LR, learned 13x13 kernel (CEM margins '
-                                  '%d/%d, G at %dx%d), objective %s, nb=%d' % (B, h, h, m, 4 * m, h + 2 * m,
-                                                                               h + 2 * m, args.objective, args.nb),
-                      'global_batch': world * B, 'parallelism': 'images sharded, no collective'},
-           'final_loss': zo.loss_values[-1]}
+    fwd = getattr(cem.generated_image_model, 'esr_precision', engine.DEFAULT_PRECISION)
+    return {'metric': 'Z-optimisation HR Mpixels/s per iteration (latent RRDB-23 + learned-kernel CEM, fwd + dZ + '
+                      'Adam)',
+            'value': round(world * B * (4 * h) ** 2 * args.steps / dt / 1e6, 4), 'unit': 'HR Mpixels/s',
+            'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+            'ms_per_step': round(dt / args.steps * 1e3, 2), 'higher_is_better': True, 'scaling': 'weak',
+            'dtype': 'f32', 'fwd_dtype': fwd, 'bwd_dtype': 'f32', 'data': 'synthetic',
+            'achieved_TFLOPs': round(flop_iter * args.steps / dt / 1e12, 2),
+            'config': {'workload': 'BASELINE config 5: batch %d/GPU of %dx%d LR, learned 13x13 kernel (CEM margins '
+                                   '%d/%d, G at %dx%d), objective %s, nb=%d' % (B, h, h, m, 4 * m, h + 2 * m,
+                                                                                h + 2 * m, args.objective, args.nb),
+                       'global_batch': world * B, 'parallelism': 'images sharded, no collective'},
+            'final_loss': zo.loss_values[-1]}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--batch', type=int, default=8)
+    ap.add_argument('--lr-size', type=int, default=128)
+    ap.add_argument('--nb', type=int, default=23)
+    ap.add_argument('--objective', default='max_STD')
+    args = ap.parse_args()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=dev)
+    rec = run(args, dev, world, rank)
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if world > 1:

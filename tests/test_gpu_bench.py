@@ -15,7 +15,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def test_bench_json_contract():
     cmd = [sys.executable, os.path.join(REPO, 'bench.py'), '--steps', '2', '--warmup', '1', '--batch', '2',
-           '--lr-size', '32', '--nb', '1', '--cpu-images', '1']
+           '--lr-size', '32', '--nb', '1', '--cpu-images', '1', '--no-legs']
     res = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=110)
     assert res.returncode == 0, res.stderr[-2000:]
     lines = [ln for ln in res.stdout.splitlines() if ln.startswith('{')]
