@@ -57,6 +57,8 @@ def parse():
     ap.add_argument('--no-legs', action='store_true', help='skip the extra legs (exact-fp32 C2, C3/C4 training step, '
                     'C5 Z-optimisation iteration)')
     ap.add_argument('--leg-steps', type=int, default=3)
+    ap.add_argument('--no-op-timers', action='store_true', help='time the steps without the per-launch HIP events '
+                    '(no roofline; measures what the events themselves cost)')
     return ap.parse_args()
 
 
@@ -213,7 +215,7 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         prof = []
-        engine._PROFILE = prof
+        engine._PROFILE = None if args.no_op_timers else prof
         t0 = time.perf_counter()
         for _ in range(args.steps):
             out = model(x)
@@ -229,6 +231,14 @@ def main():
     hr = 4 * args.lr_size
     total_px = world * args.batch * hr * hr * args.steps
     value = total_px / dt / 1e6
+    if args.no_op_timers:
+        if rank == 0:
+            print(json.dumps({'metric': METRIC, 'value': round(value, 3), 'unit': 'HR Mpixels/s', 'n_gpus': world,
+                              'steps': args.steps, 'ms_per_step': round(dt / args.steps * 1e3, 3),
+                              'note': 'no per-launch events (timer-overhead check; not the bench line)'}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     # roofline of the dominant kernel from the per-launch events
     per = {}
     for tag, flops, ms in engine.profile_records(prof):

@@ -116,10 +116,24 @@ __global__ __launch_bounds__(256) void cem_down_tiled(const float *__restrict__ 
     const float *g = gen + plane * HH * WW;
     for (int k = threadIdx.x; k < kd * kd; k += 256) sw[k] = wd[k];
     const int Y0 = sf * i0 + ph - pd, X0 = sf * j0 + ph - pd;
-    for (int k = threadIdx.x; k < WH * WH; k += 256) {
-        const int y = k / WH, x = k - y * WH;
-        const float v = g[(long long)clampi(Y0 + y, 0, HH - 1) * WW + clampi(X0 + x, 0, WW - 1)];
-        s[((x % sf) * WH + y) * P + x / sf] = v;
+    // 64 lanes along a window row (coalesced), 4 rows per pass, 8 passes' loads in flight before their LDS stores
+    // (one load at a time made the staging latency-bound); WH <= 128 (kd <= 64), no integer division
+    const int lx = threadIdx.x & 63, ly = threadIdx.x >> 6;
+    for (int yb = ly; yb < WH; yb += 32) {
+        float v[8][2];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float *grow = g + (long long)clampi(Y0 + yb + 4 * e, 0, HH - 1) * WW;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) v[e][h] = grow[clampi(X0 + lx + 64 * h, 0, WW - 1)];
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int y = yb + 4 * e, x = lx + 64 * h;
+                if (y < WH && x < WH) s[((x & (sf - 1)) * WH + y) * P + x / sf] = v[e][h];
+            }
     }
     __syncthreads();
     const int i = i0 + ty, j = j0 + tx;
@@ -170,6 +184,147 @@ __global__ __launch_bounds__(256) void cem_up_add_phase(const float *__restrict_
         }
     }
     out[(plane * OH + Y) * OW + X] = gen[(plane * HH + Yp) * WW + Xp] + acc;
+}
+
+// Inverse filter, tiled: a 64×16 block of outputs of one plane stages its replicate-clamped (16+ki-1)×(64+ki-1) input
+// window in LDS once (the direct kernel re-read every input ki² times through L1/L2, with a clamp per tap); each thread
+// owns 4 consecutive outputs of a row and slides a 4-wide register window along each tap row, so one LDS read feeds
+// 4 FMAs.  Accumulation order per output (u-major, v-minor) is the direct kernel's: results are bitwise equal.
+__global__ __launch_bounds__(256) void cem_inv_tiled(const float *__restrict__ rin, float *__restrict__ q, int H, int W,
+                                                     const float *__restrict__ wi, int ki) {
+    extern __shared__ float smem[];
+    const int WP = 64 + ki - 1, WR = 16 + ki - 1;
+    float *s = smem;                           // [WR][WP]
+    const int j0 = blockIdx.x * 64, i0 = blockIdx.y * 16;
+    const long long plane = blockIdx.z;
+    const float *src = rin + plane * H * W;
+    const int pd = ki / 2;
+    const int lx = threadIdx.x & 63, ly = threadIdx.x >> 6;
+    for (int yb = ly; yb < WR; yb += 32) {  // 8 passes' loads in flight before their stores (WP <= 128)
+        float v[8][2];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float *row = src + (long long)clampi(i0 + yb + 4 * e - pd, 0, H - 1) * W;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) v[e][h] = row[clampi(j0 + lx + 64 * h - pd, 0, W - 1)];
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int y = yb + 4 * e, x = lx + 64 * h;
+                if (y < WR && x < WP) s[y * WP + x] = v[e][h];
+            }
+    }
+    __syncthreads();
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    for (int u = 0; u < ki; ++u) {
+        const float *sr = s + (ty + u) * WP + 4 * tx;
+        const float *wr = wi + u * ki;  // wave-uniform index: scalar loads through the constant cache
+        float r0 = sr[0], r1 = sr[1], r2 = sr[2];
+#pragma unroll 4
+        for (int v = 0; v < ki; ++v) {
+            const float r3 = sr[v + 3], w = wr[v];
+            a0 += w * r0;
+            a1 += w * r1;
+            a2 += w * r2;
+            a3 += w * r3;
+            r0 = r1;
+            r1 = r2;
+            r2 = r3;
+        }
+    }
+    const int i = i0 + ty, j = j0 + 4 * tx;
+    if (i >= H) return;
+    float *qo = q + (plane * H + i) * W;
+    if (j < W) qo[j] = a0;
+    if (j + 1 < W) qo[j + 1] = a1;
+    if (j + 2 < W) qo[j + 2] = a2;
+    if (j + 3 < W) qo[j + 3] = a3;
+}
+
+// Up + back-projection + crop, tiled (interior stride phases, as cem_up_add_phase): a 64×16 block of cropped HR outputs
+// of one plane stages the q window its taps can reach in LDS, zero outside [0,H)×[0,W) — exactly the taps the phase
+// kernel skips (for 0 < ph < sf-1 a tap outside the HR grid, or on a clamped border row, is not a stuffed sample) — so
+// the tap loops have no bounds tests: each output visits the (kd/sf)² taps of its own sub-pixel phase, u0 + sf·a,
+// v0 + sf·b, reading q[r + a][c + b].  Same taps in the same order as cem_up_add_phase: bitwise equal.
+template <int sf, int RPT>
+__global__ __launch_bounds__(256) void cem_up_add_tiled(const float *__restrict__ q, const float *__restrict__ gen,
+                                                        float *__restrict__ out, int H, int W, int ph,
+                                                        const float *__restrict__ wu, int kd, int M) {
+    extern __shared__ float smem[];
+    float *sw = smem;
+    const int QC = (63 + kd - 1) / sf + 3, QR = (16 * RPT - 1 + kd - 1) / sf + 3;
+    float *sq = smem + ((kd * kd + 3) & ~3);  // [QR][QC]
+    const int HH = sf * H, WW = sf * W, OH = HH - 2 * M, OW = WW - 2 * M;
+    const int X0 = blockIdx.x * 64, Y0 = blockIdx.y * 16 * RPT;
+    const long long plane = blockIdx.z;
+    const int pd = kd / 2;
+    // q row of the first tap of the block's first output row, minus one (floor division of a possibly negative value)
+    const int qr0 = (Y0 + M - pd - ph + sf * (kd + sf)) / sf - (kd + sf) - 1;
+    const int qc0 = (X0 + M - pd - ph + sf * (kd + sf)) / sf - (kd + sf) - 1;
+    // thread (tx, ty): the 4 consecutive outputs X0 + 4 tx + e (e < 4) of rows Y0 + ty + 16 k (k < RPT); one 16-B gen
+    // load and one 16-B store per 4 outputs when rows are 16-B aligned (WW, OW, M multiples of 4), else per element.
+    // The gen loads are issued before the q window is staged, so their latency hides behind the staging and taps.
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;  // 16 column groups x 16 rows
+    const int Xb = X0 + 4 * tx;
+    const bool vec = ((WW | OW | M) & 3) == 0 && Xb + 4 <= OW;
+    float4 gv[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        const int Y = Y0 + ty + 16 * k;
+        const float *g = gen + (plane * HH + min(Y, OH - 1) + M) * WW + min(Xb, OW - 1) + M;
+        if (vec) {
+            gv[k] = *reinterpret_cast<const float4 *>(g);
+        } else {
+            gv[k].x = g[0];
+            gv[k].y = Xb + 1 < OW ? g[1] : 0.f;
+            gv[k].z = Xb + 2 < OW ? g[2] : 0.f;
+            gv[k].w = Xb + 3 < OW ? g[3] : 0.f;
+        }
+    }
+    for (int k = threadIdx.x; k < kd * kd; k += 256) sw[k] = wu[k];
+    const float *qp = q + plane * H * W;
+    for (int k = threadIdx.x; k < QR * QC; k += 256) {
+        const int r = k / QC, c = k - r * QC;
+        const int qr = qr0 + r, qc = qc0 + c;
+        sq[k] = (qr >= 0 && qr < H && qc >= 0 && qc < W) ? qp[(long long)qr * W + qc] : 0.f;
+    }
+    __syncthreads();
+    if (Xb >= OW) return;
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        const int Y = Y0 + ty + 16 * k;
+        if (Y >= OH) return;
+        const int Yp = Y + M;
+        const int u0 = (pd + ph - Yp + sf * (Yp + kd)) % sf;
+        const int rb = (Yp + u0 - pd - ph + sf * (kd + sf)) / sf - (kd + sf) - qr0;
+        float acc[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int Xp = Xb + e + M;
+            const int v0 = (pd + ph - Xp + sf * (Xp + kd)) % sf;
+            const int cb = (Xp + v0 - pd - ph + sf * (kd + sf)) / sf - (kd + sf) - qc0;
+            float a_ = 0.f;
+            for (int u = u0, a = 0; u < kd; u += sf, ++a) {
+                const float *qrow = sq + (rb + a) * QC + cb;
+                const float *wrow = sw + u * kd;
+                for (int v = v0, b = 0; v < kd; v += sf, ++b) a_ += wrow[v] * qrow[b];
+            }
+            acc[e] = a_;
+        }
+        float *o = out + (plane * OH + Y) * OW + Xb;
+        if (vec) {
+            *reinterpret_cast<float4 *>(o) = make_float4(gv[k].x + acc[0], gv[k].y + acc[1], gv[k].z + acc[2],
+                                                         gv[k].w + acc[3]);
+        } else {
+            const float gg[4] = {gv[k].x, gv[k].y, gv[k].z, gv[k].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (Xb + e < OW) o[e] = gg[e] + acc[e];
+        }
+    }
 }
 
 // ---- model-input preparation ----
@@ -257,6 +412,7 @@ __global__ __launch_bounds__(NT) void prep_hr_kernel(PrepParams p) {
 }
 
 inline unsigned nblocks(long long n) { return (unsigned)((n + NT - 1) / NT); }
+int g_cem_direct = 0;  // esr_cem_set_direct: 1 = the untiled inverse / up-add kernels
 inline int launched() { return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH; }
 
 }  // namespace
@@ -281,8 +437,14 @@ extern "C" int esr_cem_down(const float *gen, const float *lr, float *r, int32_t
 extern "C" int esr_cem_inv(const float *r, float *q, int32_t B, int32_t H, int32_t W, const float *w_inv, int32_t ki,
                            esr_stream_t stream) {
     if (!r || !q || !w_inv || B <= 0 || H <= 0 || W <= 0 || ki <= 0 || ki > MAXK || !(ki & 1)) return ESR_EINVAL;
-    hipLaunchKernelGGL(cem_inv_kernel, dim3(nblocks((long long)B * 3 * H * W)), dim3(NT), 0, (hipStream_t)stream, r,
-                       q, B, H, W, w_inv, ki);
+    const size_t lds = 4 * (size_t)(16 + ki - 1) * (64 + ki - 1);
+    if (lds <= 64 * 1024 && !g_cem_direct) {
+        hipLaunchKernelGGL(cem_inv_tiled, dim3((W + 63) / 64, (H + 15) / 16, B * 3), dim3(256), lds,
+                           (hipStream_t)stream, r, q, H, W, w_inv, ki);
+    } else {
+        hipLaunchKernelGGL(cem_inv_kernel, dim3(nblocks((long long)B * 3 * H * W)), dim3(NT), 0, (hipStream_t)stream,
+                           r, q, B, H, W, w_inv, ki);
+    }
     return launched();
 }
 
@@ -292,14 +454,29 @@ extern "C" int esr_cem_up_add(const float *q, const float *gen, float *out, int3
         ph < 0 || ph >= sf || M < 0 || 2 * M >= sf * H || 2 * M >= sf * W)
         return ESR_EINVAL;
     if (sf == 4 && ph > 0 && ph < sf - 1) {
-        hipLaunchKernelGGL(cem_up_add_phase<4>, dim3((sf * W - 2 * M + 63) / 64, (sf * H - 2 * M + 3) / 4, B * 3),
-                           dim3(256), 0, (hipStream_t)stream, q, gen, out, H, W, ph, w_up, kd, M);
+        constexpr int RPT = 1;  // rows per thread: 64 x 16 outputs per block (64 x 64 measured slower)
+        const int QC = (63 + kd - 1) / sf + 3, QR = (16 * RPT - 1 + kd - 1) / sf + 3;
+        const size_t lds = 4 * (((kd * kd + 3) & ~3) + (size_t)QR * QC);
+        if (g_cem_direct)
+            hipLaunchKernelGGL(cem_up_add_phase<4>, dim3((sf * W - 2 * M + 63) / 64, (sf * H - 2 * M + 3) / 4, B * 3),
+                               dim3(256), 0, (hipStream_t)stream, q, gen, out, H, W, ph, w_up, kd, M);
+        else
+            hipLaunchKernelGGL((cem_up_add_tiled<4, RPT>), dim3((sf * W - 2 * M + 63) / 64,
+                                                              (sf * H - 2 * M + 16 * RPT - 1) / (16 * RPT), B * 3),
+                               dim3(256), lds, (hipStream_t)stream, q, gen, out, H, W, ph, w_up, kd, M);
     } else {
         const long long n = (long long)B * 3 * (sf * H - 2 * M) * (sf * W - 2 * M);
         hipLaunchKernelGGL(cem_up_add_kernel, dim3(nblocks(n)), dim3(NT), 0, (hipStream_t)stream, q, gen, out, B, H,
                            W, sf, ph, w_up, kd, M);
     }
     return launched();
+}
+
+extern "C" int esr_cem_set_direct(int32_t direct) {
+    if (direct < 0 || direct > 1) return ESR_EINVAL;
+    const int prev = g_cem_direct;
+    g_cem_direct = direct;
+    return prev;
 }
 
 extern "C" int esr_prep_input(const float *x, int32_t B, int32_t nz, int32_t h, int32_t w, int32_t sf, int32_t m,

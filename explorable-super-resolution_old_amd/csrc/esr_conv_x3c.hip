@@ -123,19 +123,26 @@ __device__ __forceinline__ void sfor(F &&f) {
 // DBG (diagnostic builds only, garbage outputs): 1 = LDS-DMA of chunk 0 only, 2 = no fragment reads / MFMAs,
 // 4 = no epilogue stores.  RB: the B fragments (weights) are loaded from global memory (L1/L2) into registers
 // instead of being staged in LDS: the LDS-DMA moves only the input halo tile (32-48 % fewer staged bytes).
-template <int NT, int TS, int DBG = 0, bool RB = false>
-__global__ __launch_bounds__(NTHR, 2) void conv_x3c_kernel(X3cParams p) {
+// WR (NT = 1): at the start of each K chunk every wave copies the B fragments of all taps from LDS into registers,
+// after which the weight stage is free: the next chunk's weights are LDS-DMA'd while this chunk is computed, so only
+// the halo tile's transfer sits between two chunks' MFMAs (the weights are a third of the staged bytes at N = 32).
+template <int NT, int TS, int DBG = 0, bool RB = false, int CWV = CW, bool WR = false>
+__global__ __launch_bounds__(64 * (TWC / CWV), 2) void conv_x3c_kernel(X3cParams p) {
+    static_assert(!WR || (NT == 1 && !RB), "register-resident weights: one N-tile, weights staged in LDS");
+    constexpr int CWk = CWV;                               // output columns per wave
+    constexpr int NW = TWC / CWk;                          // waves per workgroup
+    constexpr int KINk = (IN_PIECES + NW - 1) / NW;        // input pieces per wave
     constexpr int T = TS * TS;
     constexpr int N = 32 * NT;
     constexpr int W_RECS = T * N;
     constexpr int W_PIECES = W_RECS / 16;
-    constexpr int KW = (W_PIECES + NWV - 1) / NWV;
+    constexpr int KW = (W_PIECES + NW - 1) / NW;
     constexpr int W_B = W_RECS * REC;
     constexpr int LDS_BYTES = IN_B + (RB ? 0 : W_B);
     constexpr int EP_P = N + 4;                            // epilogue row pitch (floats)
-    constexpr int NIC = CW + TS - 1;                       // halo columns a wave reads (6 for 3×3)
+    constexpr int NIC = CWk + TS - 1;                       // halo columns a wave reads (6 for 3×3)
     constexpr int NSTEP = NIC * TS;                        // A steps (halo column, tap row) per sweep
-    static_assert(NWV * 32 * EP_P * 4 <= IN_B, "per-wave epilogue areas fit in the input region");
+    static_assert(NW * 32 * EP_P * 4 <= IN_B, "per-wave epilogue areas fit in the input region");
     static_assert(2 * LDS_BYTES <= 163840, "two workgroups per CU");
     __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_BYTES];
 
@@ -151,7 +158,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv_x3c_kernel(X3cParams p) {
     const int x0 = tx * TWC;             // first halo column = padded column x0; output padded columns x0+1+c
     const int r0 = ty * CT;              // first halo row (tall padded image); output tall rows r0+1+m
     const int tw = min(TWC, p.W - x0);   // valid output columns of the tile
-    const int ncw = min(CW, max(0, tw - CW * wave));  // valid output columns of this wave
+    const int ncw = min(CWk, max(0, tw - CWk * wave));  // valid output columns of this wave
     const int rows_tot = p.B * (p.H + 2);
     const long long rowp = (long long)(p.W + 2);
     const long long pixb = 4LL * p.in_cp;
@@ -160,32 +167,34 @@ __global__ __launch_bounds__(NTHR, 2) void conv_x3c_kernel(X3cParams p) {
 
     // ---- LDS-DMA addressing: input piece q of this wave = records 16 (wave + 4 i) .. +15, lane -> (record, slot) ----
     const int sub = lane >> 2, ps = lane & 3;
-    unsigned in_off[KIN];  // byte offset from tile_in (slot included); bit 0 set = zero page; bit 1 = lo group
+    unsigned in_off[KINk];  // byte offset from tile_in (slot included); bit 0 set = zero page; bit 1 = lo group
 #pragma unroll
-    for (int i = 0; i < KIN; ++i) {
-        const int q = wave + NWV * i;
+    for (int i = 0; i < KINk; ++i) {
+        const int q = wave + NW * i;
         const int r = 16 * q + sub;
         const int hx = r / HYC, hy = r - (r / HYC) * HYC;
         const int s = ps ^ ((hy >> 2) & 3);
         const bool v = q < IN_PIECES && r < IN_RECS && r0 + hy < rows_tot && x0 + hx < p.W + 2;
         in_off[i] = v ? (unsigned)((hy * rowp + hx) * pixb + (s << 4)) | ((s >> 1) << 1) : 1u;
     }
-    auto dma = [&](int j) {
+    auto dma_in = [&](int j) {
         const int groups = min(16, p.cin - 16 * j) >> 3;  // 8-channel groups present in the chunk (1 or 2)
 #pragma unroll
-        for (int i = 0; i < KIN; ++i) {
-            const int q = wave + NWV * i;
+        for (int i = 0; i < KINk; ++i) {
+            const int q = wave + NW * i;
             if (q >= IN_PIECES) break;
             const unsigned o = in_off[i];
             const bool ok = !(o & 1u) && ((o >> 1) & 1u) < (unsigned)groups;
             const void *src = ok ? (const void *)(tile_in + (o & ~3u) + 64LL * j) : (const void *)g_zero64;
             __builtin_amdgcn_global_load_lds((glob_void *)src, (lds_void *)(lds + q * 1024), 16, 0, 0);
         }
+    };
+    auto dma_w = [&](int j) {
         if constexpr (!RB) {
             const unsigned char *wj = p.w + (long long)j * W_B;
 #pragma unroll
             for (int i = 0; i < KW; ++i) {
-                const int q = wave + NWV * i;
+                const int q = wave + NW * i;
                 if (q >= W_PIECES) break;
                 const int r = 16 * q + sub;
                 const int s = ps ^ ((r >> 2) & 3);
@@ -193,6 +202,10 @@ __global__ __launch_bounds__(NTHR, 2) void conv_x3c_kernel(X3cParams p) {
                                                  (lds_void *)(lds + IN_B + q * 1024), 16, 0, 0);
             }
         }
+    };
+    auto dma = [&](int j) {
+        dma_in(j);
+        dma_w(j);
     };
 
     // ---- fragment addresses: A (pixels, halo column hx, tap row dy): lane (ml, hl) reads record hx*HYC + ml + dy,
@@ -203,7 +216,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv_x3c_kernel(X3cParams p) {
         const int dy = p.tap_y0 + d;
         const int hy = ml + dy;
         const uint32_t o = lds_addr(lds) + hy * REC + (((2 * hl) ^ ((hy >> 2) & 3)) << 4) +
-                           (uint32_t)(CW * wave + p.tap_x0) * HYC * REC;
+                           (uint32_t)(CWk * wave + p.tap_x0) * HYC * REC;
         a_hi[d] = o;
         a_lo[d] = o ^ 16u;
     }
@@ -211,9 +224,10 @@ __global__ __launch_bounds__(NTHR, 2) void conv_x3c_kernel(X3cParams p) {
     const uint32_t b_lo = b_hi ^ 16u;
     const f16x8 *w_lane = reinterpret_cast<const f16x8 *>(p.w + ml * REC + 32 * hl);  // RB: this lane's B slice
 
-    f32x16 acc[CW][NT];
+    f16x8 bregh[WR ? T : 1], bregl[WR ? T : 1];  // WR: this chunk's B fragments of every tap
+    f32x16 acc[CWk][NT];
 #pragma unroll
-    for (int c = 0; c < CW; ++c)
+    for (int c = 0; c < CWk; ++c)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
@@ -233,6 +247,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv_x3c_kernel(X3cParams p) {
             f16x8 bh[2][TS], bl[2][TS], ah[3], al[3];
             auto ldb = [&](auto Dc) {
                 constexpr int d = decltype(Dc)::value;
+                if constexpr (WR) return;
                 sfor<0, TS>([&](auto Xc) {
                     constexpr int dx = decltype(Xc)::value, t = d * TS + dx;
                     if constexpr (RB) {  // global (L1/L2) loads; the compiler waits for them before first use
@@ -256,9 +271,10 @@ __global__ __launch_bounds__(NTHR, 2) void conv_x3c_kernel(X3cParams p) {
                 constexpr int s = decltype(Sc)::value, d = s / NIC, ic = s % NIC, buf = s % 3;
                 constexpr int pd = (s - 1) / NIC, pic = (s - 1) % NIC;  // the previous step
                 constexpr int after = s == 0 ? (NSTEP > 1 ? 2 : 0)
-                                             : ((!RB && pic == 0 && pd + 1 < TS) ? 2 * TS : 0) + (s + 1 < NSTEP ? 2 : 0);
+                                             : ((!RB && !WR && pic == 0 && pd + 1 < TS) ? 2 * TS : 0) +
+                                               (s + 1 < NSTEP ? 2 : 0);
                 lgkm_wait2<after>(ah[buf], al[buf]);
-                if constexpr (ic == 0 && !RB) {  // B(d) is back too: pass its registers through an (empty) ordering point
+                if constexpr (ic == 0 && !RB && !WR) {  // B(d) is back too: pass its registers through an ordering point
 #pragma unroll
                     for (int x = 0; x < TS; ++x) asm volatile("" : "+v"(bh[d & 1][x]), "+v"(bl[d & 1][x]));
                 }
@@ -269,9 +285,10 @@ __global__ __launch_bounds__(NTHR, 2) void conv_x3c_kernel(X3cParams p) {
                     constexpr int pr = decltype(Pc)::value;
                     sfor<0, TS>([&](auto Xc) {
                         constexpr int dx = decltype(Xc)::value, c = ic - dx;
-                        if constexpr (c >= 0 && c < CW) {
+                        if constexpr (c >= 0 && c < CWk) {
                             const f16x8 &a = pr == 0 ? al[buf] : ah[buf];
-                            const f16x8 &b = pr == 1 ? bl[d & 1][dx] : bh[d & 1][dx];
+                            const f16x8 &b = WR ? (pr == 1 ? bregl[WR ? d * TS + dx : 0] : bregh[WR ? d * TS + dx : 0])
+                                                : (pr == 1 ? bl[d & 1][dx] : bh[d & 1][dx]);
                             acc[c][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc[c][nt], 0, 0, 0);
                         }
                     });
@@ -280,12 +297,35 @@ __global__ __launch_bounds__(NTHR, 2) void conv_x3c_kernel(X3cParams p) {
         });
     };
 
+    if constexpr (WR) {
+        dma(0);
+        for (int j = 0; j < nchunk; ++j) {
+            wait_vm0();
+            __builtin_amdgcn_s_barrier();  // chunk j's halo and weights have landed for every wave
+            sfor<0, T>([&](auto Tc) {
+                constexpr int t = decltype(Tc)::value;
+                bregh[t] = ds_read16<t * N * REC>(b_hi);
+                bregl[t] = ds_read16<t * N * REC>(b_lo);
+            });
+            lgkm_wait_arr<0>(bregh);
+#pragma unroll
+            for (int t = 0; t < T; ++t) asm volatile("" : "+v"(bregl[t]));
+            __builtin_amdgcn_s_barrier();  // every wave holds its B fragments: the weight stage is free
+            if (j + 1 < nchunk) dma_w(j + 1);  // lands while chunk j is computed
+            if (ncw > 0) compute(j);
+            if (j + 1 < nchunk) {
+                __builtin_amdgcn_s_barrier();  // every wave is done reading the halo stage
+                dma_in(j + 1);
+            }
+        }
+    } else {
     for (int j = 0; j < nchunk; ++j) {
         if (j) __builtin_amdgcn_s_barrier();  // every wave is done reading the stage (its reads were waited for)
         if (!(DBG & 1) || j == 0) dma(j);
         wait_vm0();
         __builtin_amdgcn_s_barrier();
         if (ncw > 0 && !(DBG & 2)) compute(j);
+    }
     }
 
     // ---- epilogue: each wave restages one output column at a time through its own LDS area and stores it ----
@@ -305,7 +345,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv_x3c_kernel(X3cParams p) {
         for (int e = 0; e < 8; ++e) bk[k][e] = (8 * g + e < p.cout) ? p.bias[8 * g + e] : 0.f;
     }
 #pragma unroll
-    for (int c = 0; c < CW; ++c) {
+    for (int c = 0; c < CWk; ++c) {
         if (c >= ncw) break;
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
@@ -314,7 +354,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv_x3c_kernel(X3cParams p) {
                 const int m = 8 * (r >> 2) + 4 * hl + (r & 3);
                 s_ep[m * EP_P + nt * 32 + ml] = acc[c][nt][r];
             }
-        const int x = x0 + CW * wave + c;  // interior column of the output pixel
+        const int x = x0 + CWk * wave + c;  // interior column of the output pixel
         if constexpr ((DBG & 4) != 0) continue;  // diagnostic: restage only, no global loads / stores
         if (o.out_planar) {
             for (int it = lane; it < 32 * p.cout; it += 64) {
@@ -690,6 +730,19 @@ int x3c_launch(const X3cParams &p0, int taps_side, hipStream_t stream, int dbg) 
     p.tiles_y = (p.B * (p.H + 2) - 2 + CT - 1) / CT;
     const dim3 grid((unsigned)(p.tiles_x * p.tiles_y)), block(NTHR);
     const bool n64 = p.cout > 32;
+    if (dbg == 32) {  // 8 waves of 2 columns (N = 32 only: the per-wave epilogue areas of N = 64 do not fit)
+        const dim3 block8(64 * (TWC / 2));
+        if (taps_side == 3 && !n64) hipLaunchKernelGGL((conv_x3c_kernel<1, 3, 0, false, 2>), grid, block8, 0, stream, p);
+        else if (!n64) hipLaunchKernelGGL((conv_x3c_kernel<1, 2, 0, false, 2>), grid, block8, 0, stream, p);
+        else return x3c_launch(p0, taps_side, stream, 0);
+        return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+    }
+    if (dbg == 64) {  // N = 32: weights copied to registers per chunk, the next chunk's weights DMA'd under compute
+        if (n64) return x3c_launch(p0, taps_side, stream, 0);
+        if (taps_side == 3) hipLaunchKernelGGL((conv_x3c_kernel<1, 3, 0, false, 4, true>), grid, block, 0, stream, p);
+        else hipLaunchKernelGGL((conv_x3c_kernel<1, 2, 0, false, 4, true>), grid, block, 0, stream, p);
+        return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+    }
     if (dbg == 16) {  // register-B form
         if (taps_side == 3) {
             if (n64) hipLaunchKernelGGL((conv_x3c_kernel<2, 3, 0, true>), grid, block, 0, stream, p);

@@ -8,7 +8,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('ESR_AMD_LIB', os.path.join(_HERE, 'libesr_amd.so'))
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 c_int = ctypes.c_int32
 c_float = ctypes.c_float
@@ -50,6 +50,7 @@ _SIGNATURES = {
                                   c_int, c_int, ctypes.POINTER(ConvOut), c_void_p, c_void_p],
     'esr_x3_set_kernel': [c_int],
     'esr_x3_set_tile_map': [c_int],
+    'esr_cem_set_direct': [c_int],
     'esr_conv_set_tile': [c_int],
     'esr_cem_down': [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int,
                      c_void_p],

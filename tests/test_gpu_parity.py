@@ -356,7 +356,7 @@ def test_x3_ring_kernel_bitwise_equals_classic(gpu_device, cin, cout, B, H, W):
         # classic one-stage (default), ring always, persistent ring always, ring / classic with the compiler-scheduled
         # fragment reads, two-stage classic with prefetch 1 / 2, the round-1 automatic choice, the column-tile kernel
         # (LDS / register weights) (none may change a bit)
-        for variant in (0, 2, 17, 18, 20, 21, 22, 25, 26, 27, 28, 24, 50, 60):
+        for variant in (0, 2, 17, 18, 20, 21, 22, 25, 26, 27, 28, 24, 50, 60, 61, 62):
             lib.esr_x3_set_kernel(variant)
             out = torch.zeros(B, H + 2, W + 2, 40, device=gpu_device)
             out2 = torch.zeros(B, H + 2, W + 2, 32, device=gpu_device)
@@ -477,3 +477,47 @@ def test_upconv2x_phases_x3(gpu_device, H, W):
     ref = F.leaky_relu(F.conv2d(F.interpolate(_nchw(engine.from_split(x), 0, 64), scale_factor=2, mode='nearest'),
                                 w.double(), b.double(), padding=1), 0.2)
     assert normwise_rel(_nchw(engine.from_split(out), 0, 64), ref) < 1e-5
+
+
+@pytest.mark.parametrize('B,H,W,ki,kd,M', [(32, 148, 148, 27, 17, 40), (2, 21, 37, 13, 13, 0), (1, 9, 70, 33, 25, 8)])
+def test_cem_tiled_stencils_bitwise_equal_direct(gpu_device, B, H, W, ki, kd, M):
+    """The LDS-tiled inverse-filter and up-add kernels (default) against the direct kernels (esr_cem_set_direct(1)):
+    same taps in the same order per output, so bit for bit — at the config-2 shape (B=32, 148² LR) and at ragged
+    shapes (tiles past the image edge, windows clamped on every side) — and against float64."""
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(61)
+    r = torch.randn(B, 3, H, W, generator=g).to(gpu_device)
+    wi = (torch.randn(ki, ki, generator=g) * 0.05).to(gpu_device)
+    wu = (torch.randn(kd, kd, generator=g) * 0.1).to(gpu_device)
+    gen = torch.randn(B, 3, 4 * H, 4 * W, generator=g).to(gpu_device)
+    res = {}
+    try:
+        for direct in (1, 0):
+            lib.esr_cem_set_direct(direct)
+            q = torch.empty_like(r)
+            _lib.check(lib.esr_cem_inv(r.data_ptr(), q.data_ptr(), B, H, W, wi.data_ptr(), ki, _stream()), 'inv')
+            outs = []
+            for ph in (1, 2):
+                out = torch.full((B, 3, 4 * H - 2 * M, 4 * W - 2 * M), 7.0, device=gpu_device)
+                _lib.check(lib.esr_cem_up_add(q.data_ptr(), gen.data_ptr(), out.data_ptr(), B, H, W, 4, ph,
+                                              wu.data_ptr(), kd, M, _stream()), 'up_add')
+                outs.append(out)
+            torch.cuda.synchronize()
+            res[direct] = (q, outs)
+    finally:
+        lib.esr_cem_set_direct(0)
+    assert torch.equal(res[0][0], res[1][0])
+    for a, b in zip(res[0][1], res[1][1]):
+        assert torch.equal(a, b)
+    # float64: replicate-padded cross-correlation (inverse filter); zero-stuffed ×4 grid at phase ph, replicate-padded
+    rd = r.double().cpu()
+    ref_q = F.conv2d(F.pad(rd.view(B * 3, 1, H, W), (ki // 2,) * 4, mode='replicate'), wi.double().cpu().view(1, 1, ki, ki))
+    assert normwise_rel(res[0][0].cpu().view(B * 3, 1, H, W), ref_q) < 1e-5
+    qd = res[0][0].double().cpu().view(B * 3, 1, H, W)
+    for ph, got in zip((1, 2), res[0][1]):
+        st = torch.zeros(B * 3, 1, 4 * H, 4 * W, dtype=torch.float64)
+        st[:, :, ph::4, ph::4] = qd
+        up = F.conv2d(F.pad(st, (kd // 2,) * 4, mode='replicate'), wu.double().cpu().view(1, 1, kd, kd))
+        ref = gen.double().cpu().view(B * 3, 1, 4 * H, 4 * W) + up
+        ref = ref[:, :, M:4 * H - M, M:4 * W - M]
+        assert normwise_rel(got.cpu().view_as(ref), ref) < 1e-5
