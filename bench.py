@@ -57,6 +57,7 @@ def parse():
     ap.add_argument('--no-legs', action='store_true', help='skip the extra legs (exact-fp32 C2, C3/C4 training step, '
                     'C5 Z-optimisation iteration)')
     ap.add_argument('--leg-steps', type=int, default=3)
+    ap.add_argument('--x3-kernel', type=int, default=None, help='esr_x3_set_kernel variant (A/B; default automatic)')
     ap.add_argument('--no-op-timers', action='store_true', help='time the steps without the per-launch HIP events '
                     '(no roofline; measures what the events themselves cost)')
     return ap.parse_args()
@@ -196,6 +197,10 @@ def main():
     if world > 1:
         dist.init_process_group('nccl', device_id=dev)
     from esr_amd import engine
+    if args.x3_kernel is not None:
+        from esr_amd import _lib
+        if _lib.load().esr_x3_set_kernel(args.x3_kernel) < 0:
+            raise SystemExit('esr_x3_set_kernel(%d) rejected' % args.x3_kernel)
     model = build_model(args, dev)
     x = make_input(args, dev, rank)
     with torch.no_grad():

@@ -1208,8 +1208,9 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
     // with cout <= 32 where the 16-row classic grid fills its rounds (2-6 % faster per launch at the config-2/3
     // shapes, bitwise identical; profiles/r2_x3c_ab.txt); where 8-row classic tiles at three workgroups per CU pay
     // (small grids), the classic kernel stays.  Variant 24 = the round-1 automatic choice (classic only).
-    const bool x3c_pays = taps_side == 3 && (cout > 32 || !row8_pays);
-    if ((g_x3_kernel >= 50 && g_x3_kernel <= 62) || (g_x3_kernel == 1 && x3c_pays)) {  // column-tile kernels
+    // the polyphase upconv phases (2x2 taps) too: 341 -> 287 us per config-2 launch (whole-step A/B, 2 rounds)
+    const bool x3c_pays = taps_side == 2 || (taps_side == 3 && (cout > 32 || !row8_pays));
+    if ((g_x3_kernel >= 50 && g_x3_kernel <= 62) || ((g_x3_kernel == 1 || g_x3_kernel == 63) && x3c_pays)) {
         X3cParams c;
         c.in = p.in; c.B = B; c.H = H; c.W = W; c.in_cp = in_cp; c.cin = cin; c.w = p.w; c.bias = bias;
         c.w_scale_inv = p.w_scale_inv; c.cout = cout; c.tap_y0 = ty0; c.tap_x0 = tx0; c.tiles_x = c.tiles_y = 0;
@@ -1300,11 +1301,11 @@ extern "C" int esr_conv3x3_fwd_x3(const void *in, int32_t B, int32_t H, int32_t 
 }
 
 extern "C" int esr_x3_set_kernel(int32_t variant) {
-    if (variant < 0 || variant > 62) return ESR_EINVAL;
+    if (variant < 0 || variant > 63) return ESR_EINVAL;
 #ifndef ESR_X3_EXPERIMENTS
     // the production library carries the bitwise-identical A/B variants only (include/esr_amd.h)
     const bool ab = variant <= 2 || variant == 15 || (variant >= 16 && variant <= 18) ||
-                    (variant >= 20 && variant <= 28) || variant == 50 || (variant >= 60 && variant <= 62);
+                    (variant >= 20 && variant <= 28) || variant == 50 || (variant >= 60 && variant <= 63);
     if (!ab) return ESR_EINVAL;
 #endif
     const int prev = g_x3_kernel;

@@ -85,8 +85,9 @@ class GradBuckets:
     finalises them (output layers first).  While armed (the last micro-step of a gradient accumulation), a
     post-accumulate-grad hook marks each parameter whose gradient that backward has finished; when a bucket is
     complete its flattened gradients go out as one asynchronous all-reduce (RCCL over xGMI), overlapping the rest of the
-    backward.  `finish()` launches any bucket whose parameters got no gradient in this backward (requires_grad toggled
-    off, or not reached), waits for every bucket, averages and writes back.  Buckets are ≥ a few MB so that each ring
+    backward; buckets go out strictly in bucket order (the same collective sequence on every rank).  `finish()` launches
+    the buckets still pending (parameters that got no gradient in this backward: requires_grad toggled off, or not
+    reached), waits for every bucket, averages and writes back.  Buckets are ≥ a few MB so that each ring
     all-reduce runs near the per-link xGMI bandwidth rather than its latency."""
 
     def __init__(self, params, cap_bytes=16 << 20):
@@ -104,6 +105,7 @@ class GradBuckets:
         self.where = {id(p): b for b, ps in enumerate(self.buckets) for p in ps}
         self.armed = False
         self.launched_in_backward = 0
+        self._next = 0
         self._pending = [set() for _ in self.buckets]
         self._works = [None] * len(self.buckets)
         self.hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params] \
@@ -113,6 +115,7 @@ class GradBuckets:
         self.armed = _world() > 1
         self._pending = [set(id(p) for p in ps) for ps in self.buckets]
         self._works = [None] * len(self.buckets)
+        self._next = 0
         self.launched_in_backward = 0
 
     def _launch(self, b):
@@ -127,19 +130,20 @@ class GradBuckets:
         if not self.armed:
             return
         b = self.where[id(p)]
-        pend = self._pending[b]
-        pend.discard(id(p))
-        if not pend and self._works[b] is None:
-            self._launch(b)
+        self._pending[b].discard(id(p))
+        # launch complete buckets strictly in bucket order (the same sequence of collectives on every rank, as RCCL
+        # requires, whatever order the backward finalises the parameters in)
+        while self._next < len(self.buckets) and not self._pending[self._next]:
+            self._launch(self._next)
+            self._next += 1
             self.launched_in_backward += 1
 
     def finish(self):
         if not self.armed:
             return
         self.armed = False
-        for b in range(len(self.buckets)):
-            if self._works[b] is None:
-                self._launch(b)
+        for b in range(self._next, len(self.buckets)):  # the rest, still in bucket order
+            self._launch(b)
         w = _world()
         for item in self._works:
             if not item:

@@ -135,10 +135,10 @@ int esr_upconv2x_phase_fwd_x3(const void *in, int32_t B, int32_t H, int32_t W, i
                               int32_t px, const esr_conv_out *o, int32_t *overflow, esr_stream_t stream);
 /* Kernel selection for esr_conv3x3_fwd_x3 (process-wide; for A/B tests and benchmarks).  All variants below give
  * bitwise-identical results.
- * 0 / 1 (default) = automatic: the column-tile kernel (32x16 tiles, esr_conv_x3c.hip) for cout > 32 and, for
+ * 0 / 1 (default) = automatic: the column-tile kernel (32x16 tiles, esr_conv_x3c.hip) for the upconv phases, cout > 32 and, for
  *   cout <= 32, where 16-row classic tiles fill their rounds; otherwise the classic kernel with 8-row tiles at three
  *   workgroups per CU; 24 = the round-1 automatic choice (classic kernel only: 8-row at three per CU or 16-row at two,
- *   by a wave-quantisation cost model; 25 / 26 force one); 50 = column-tile kernel; 60 = column-tile kernel with the
+ *   by a wave-quantisation cost model; 25 / 26 force one); 50 = column-tile kernel; 63 = same as 1; 60 = column-tile kernel with the
  *   weights read into registers from global memory instead of LDS;
  * 22 = classic with two LDS stages and one workgroup per CU; 23 = cout > 32 with 8-row tiles at two workgroups per
  *   CU; 21 = the same with fragment prefetch distance 1 (default 2); 20 = two-stage classic with compiler-scheduled

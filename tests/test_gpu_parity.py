@@ -457,9 +457,11 @@ def test_conv3x3_x3_planar_output(gpu_device, variant):
     assert normwise_rel(out.cpu(), ref) < 1e-5
 
 
-@pytest.mark.parametrize('H,W', [(6, 9), (16, 40)])
-def test_upconv2x_phases_x3(gpu_device, H, W):
+@pytest.mark.parametrize('variant', [1, 24])  # column-tile kernel (default), classic kernel
+@pytest.mark.parametrize('H,W', [(6, 9), (16, 40), (37, 21)])
+def test_upconv2x_phases_x3(gpu_device, H, W, variant):
     lib = _lib.load()
+    lib.esr_x3_set_kernel(variant)
     B = 2
     x = engine.to_split(_padded(B, H, W, 64, 64, gpu_device, 16))
     w = torch.randn(64, 64, 3, 3, generator=torch.Generator().manual_seed(17)) * 0.05
@@ -474,6 +476,7 @@ def test_upconv2x_phases_x3(gpu_device, H, W):
             _lib.check(lib.esr_upconv2x_phase_fwd_x3(x.data_ptr(), B, H, W, 64, 64, wx.data_ptr(), bd.data_ptr(),
                                                      scale, 64, py, px, ctypes.byref(o), None, _stream()), 'up_x3')
     torch.cuda.synchronize()
+    lib.esr_x3_set_kernel(1)
     ref = F.leaky_relu(F.conv2d(F.interpolate(_nchw(engine.from_split(x), 0, 64), scale_factor=2, mode='nearest'),
                                 w.double(), b.double(), padding=1), 0.2)
     assert normwise_rel(_nchw(engine.from_split(out), 0, 64), ref) < 1e-5
