@@ -71,6 +71,16 @@ struct X3Params {
 
 __device__ __forceinline__ float lrelu(float v) { return v > 0.f ? v : 0.2f * v; }
 
+// Epilogue after 1/w_scale and bias (include/esr_amd.h esr_conv_out): LeakyReLU (lrelu 1), residuals; lrelu 3 = the
+// LeakyReLU backward through the saved split activation r2 (data-gradient convs of the x3 backward; r2 not added).
+__device__ __forceinline__ float epi(const esr_conv_out &o, float v, float r1, float r2) {
+    if (o.lrelu == 1) v = lrelu(v);
+    if (o.r1) v = o.s1 * v + r1;
+    if (o.lrelu == 3) v = r2 > 0.f ? v : 0.2f * v;
+    else if (o.r2) v = o.s2 * v + r2;
+    return v;
+}
+
 __device__ __forceinline__ void load_group(const unsigned char *p, float v[8]) {
     const f16x8 hi = *reinterpret_cast<const f16x8 *>(p);
     const f16x8 lo = *reinterpret_cast<const f16x8 *>(p + 16);
@@ -149,9 +159,7 @@ __device__ __forceinline__ bool store_px(const X3Params &p, const float *s_ep, i
             int b, oy, ox;
             if (!locate(q0 + qq, opix, b, oy, ox)) continue;
             float v = s_ep[qq * EP_P + c] * p.w_scale_inv + p.bias[c];
-            if (o.lrelu) v = lrelu(v);
-            if (o.r1) v = o.s1 * v + split_at(o.r1, opix, o.r1_cp, o.r1_coff + c);
-            if (o.r2) v = o.s2 * v + split_at(o.r2, opix, o.r2_cp, o.r2_coff + c);
+            v = epi(o, v, o.r1 ? split_at(o.r1, opix, o.r1_cp, o.r1_coff + c) : 0.f, o.r2 ? split_at(o.r2, opix, o.r2_cp, o.r2_coff + c) : 0.f);
             o.out[(((long long)b * p.cout + c) * o.out_h + oy) * o.out_w + ox] = v;
         }
         return true;
@@ -195,9 +203,7 @@ __device__ __forceinline__ bool store_px(const X3Params &p, const float *s_ep, i
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             v[j] = v[j] * p.w_scale_inv + bk[j];
-            if (o.lrelu) v[j] = lrelu(v[j]);
-            if (o.r1) v[j] = o.s1 * v[j] + r1v[k][j];
-            if (o.r2) v[j] = o.s2 * v[j] + r2v[k][j];
+            v[j] = epi(o, v[j], o.r1 ? r1v[k][j] : 0.f, o.r2 ? r2v[k][j] : 0.f);
         }
         ok &= store_group(reinterpret_cast<unsigned char *>(o.out) + (opix[k] * o.out_cp + o.out_coff + c) * 4, v);
         if (o.out2)
@@ -568,9 +574,7 @@ __global__ __launch_bounds__(NTHR, WPS) void conv_x3_kernel(X3Params p) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     v[j] = a[8 * s + j] * p.w_scale_inv + ((c + j < p.cout) ? p.bias[c + j] : 0.f);
-                    if (o.lrelu) v[j] = lrelu(v[j]);
-                    if (o.r1) v[j] = o.s1 * v[j] + r1v[j];
-                    if (o.r2) v[j] = o.s2 * v[j] + r2v[j];
+                    v[j] = epi(o, v[j], o.r1 ? r1v[j] : 0.f, o.r2 ? r2v[j] : 0.f);
                 }
                 if (o.out_planar) {
 #pragma unroll
@@ -1133,7 +1137,8 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
               hipStream_t stream) {
     if (!in || !w || !bias || !o || !o->out) return ESR_EINVAL;
     if (B <= 0 || H <= 0 || W <= 0 || cin <= 0 || cout <= 0 || cout > 64 || !(w_scale > 0.f)) return ESR_EINVAL;
-    if (cin % 8 || in_cp % 8 || in_cp < cin || o->lrelu < 0 || o->lrelu > 1) return ESR_EINVAL;
+    if (cin % 8 || in_cp % 8 || in_cp < cin || !(o->lrelu == 0 || o->lrelu == 1 || (o->lrelu == 3 && o->r2)))
+        return ESR_EINVAL;
     if (!o->out_planar && (cout % 8 || o->out_cp % 8 || o->out_coff % 8 || o->out_coff + cout > o->out_cp))
         return ESR_EINVAL;
     if ((o->r1 && (o->r1_cp % 8 || o->r1_coff % 8)) || (o->r2 && (o->r2_cp % 8 || o->r2_coff % 8)) ||

@@ -48,6 +48,16 @@ __device__ __attribute__((aligned(16))) unsigned char g_zero64[64];
 
 __device__ __forceinline__ float lrelu(float v) { return v > 0.f ? v : 0.2f * v; }
 
+// Epilogue after 1/w_scale and bias (include/esr_amd.h esr_conv_out): LeakyReLU (lrelu 1), residuals; lrelu 3 = the
+// LeakyReLU backward through the saved split activation r2 (data-gradient convs of the x3 backward; r2 not added).
+__device__ __forceinline__ float epi(const esr_conv_out &o, float v, float r1, float r2) {
+    if (o.lrelu == 1) v = lrelu(v);
+    if (o.r1) v = o.s1 * v + r1;
+    if (o.lrelu == 3) v = r2 > 0.f ? v : 0.2f * v;
+    else if (o.r2) v = o.s2 * v + r2;
+    return v;
+}
+
 __device__ __forceinline__ void load_group(const unsigned char *p, float v[8]) {
     const f16x8 hi = *reinterpret_cast<const f16x8 *>(p);
     const f16x8 lo = *reinterpret_cast<const f16x8 *>(p + 16);
@@ -365,9 +375,7 @@ __global__ __launch_bounds__(64 * (TWC / CWV), 2) void conv_x3c_kernel(X3cParams
                 const int oy = o.out_sy * y + o.out_oy, ox = o.out_sx * x + o.out_ox;
                 const long long opix = ((long long)b * (o.out_h + 2) + oy + 1) * (long long)(o.out_w + 2) + ox + 1;
                 float v = s_ep[m * EP_P + ch] * p.w_scale_inv + p.bias[ch];
-                if (o.lrelu) v = lrelu(v);
-                if (o.r1) v = o.s1 * v + split_at(o.r1, opix, o.r1_cp, o.r1_coff + ch);
-                if (o.r2) v = o.s2 * v + split_at(o.r2, opix, o.r2_cp, o.r2_coff + ch);
+                v = epi(o, v, o.r1 ? split_at(o.r1, opix, o.r1_cp, o.r1_coff + ch) : 0.f, o.r2 ? split_at(o.r2, opix, o.r2_cp, o.r2_coff + ch) : 0.f);
                 o.out[(((long long)b * p.cout + ch) * o.out_h + oy) * o.out_w + ox] = v;
             }
         } else {
@@ -409,9 +417,7 @@ __global__ __launch_bounds__(64 * (TWC / CWV), 2) void conv_x3c_kernel(X3cParams
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
                     v[e] = v[e] * p.w_scale_inv + bk[k][e];
-                    if (o.lrelu) v[e] = lrelu(v[e]);
-                    if (o.r1) v[e] = o.s1 * v[e] + r1v[k][e];
-                    if (o.r2) v[e] = o.s2 * v[e] + r2v[k][e];
+                    v[e] = epi(o, v[e], o.r1 ? r1v[k][e] : 0.f, o.r2 ? r2v[k][e] : 0.f);
                 }
                 ok &= store_group(reinterpret_cast<unsigned char *>(o.out) + (opix[k] * o.out_cp + o.out_coff + 8 * g) * 4, v);
                 if (o.out2)
@@ -630,9 +636,7 @@ __global__ __launch_bounds__(X3sShape<NT>::NTHR, X3sShape<NT>::WPS) void conv_x3
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
                     v[e] = a[8 * s2 + e] * p.w_scale_inv + p.bias[ch + e];
-                    if (o.lrelu) v[e] = lrelu(v[e]);
-                    if (o.r1) v[e] = o.s1 * v[e] + r1v[e];
-                    if (o.r2) v[e] = o.s2 * v[e] + r2v[e];
+                    v[e] = epi(o, v[e], o.r1 ? r1v[e] : 0.f, o.r2 ? r2v[e] : 0.f);
                 }
                 ok &= store_group(reinterpret_cast<unsigned char *>(o.out) + (opix * o.out_cp + o.out_coff + ch) * 4, v);
                 if (o.out2)

@@ -48,6 +48,7 @@ struct WgradParams {
     int dout_cp, dout_coff, cout, cout_pad;
     int B, H, W, tiles_x, tiles_y, splits, cin_pad;
     float *partial;  // [splits][9*cin_pad*cout_pad + cout_pad]
+    int dsplit;      // output gradient in the split-f16 layout (x3 kernel only)
 };
 
 __global__ __launch_bounds__(256, 1) void wgrad_kernel(WgradParams p) {
@@ -354,15 +355,321 @@ __global__ __launch_bounds__(W2<NCT>::NT, 1) void wgrad2_kernel(WgradParams p) {
     }
 }
 
+// wgrad3 (x3): the same GEMM on v_mfma_f32_32x32x16_f16 in the split-f16 scheme of the forward — products
+// a_hi·b_hi + a_hi·b_lo + a_lo·b_hi, fp32 accumulation.  A = the input activations, already split by the x3 forward
+// (f16 hi/lo groups of 8 channels); B = the output gradient, fp32 in memory, split here per pixel tile after scaling
+// by 2^e (e from the tile's max |dout|, so that its largest element lands in [2^13, 2^14) and the lo parts stay far
+// above f16's subnormal range).  The accumulators live in the scale of the current tile: on a scale change they are
+// multiplied by 2^(e_new - e_old) (v_ldexp: exact), and by 2^-e at the end — so the result equals the unscaled sum
+// up to the products' rounding.  The bias gradient is summed from the fp32 values (exact fp32).
+// K = pixels: both operands are read with ds_read_b64_tr_b16 from pixel-major LDS images (128 B per pixel and 32
+// channels: the global split record as it stands), 4 consecutive pixels × 16 channels per 16-lane group, so a tap's
+// pixel shift is only a different row address.  Bank conflicts: pixels p and p+2 share their bank set (128-B rows),
+// so pixel p stores its hi and lo halves swapped when (p >> 1) & 1 — the 4 pixels × 32 channels of one read then
+// cover the 64 banks exactly.  Waves as in wgrad2 (tap column tg, output-channel tile ct, pixel class q; 3 taps per
+// wave), 12 waves, next tile's global loads in registers while the current one is consumed.
+template <int NCT>
+struct W3 {
+    static constexpr int NWV = 12, NT = 64 * NWV, NQ = 4 / NCT;
+    static constexpr int IN_PX = WT_HY * WT_HX;                 // halo pixels
+    static constexpr int IN_B = IN_PX * 128;                    // input image bytes
+    static constexpr int D_B = WT_TH * WT_TW * 128;             // one output-channel tile's image bytes
+    static constexpr int IN_IT = IN_PX * 8;                     // 16-B items of the input tile
+    static constexpr int IN_PT = (IN_IT + NT - 1) / NT;
+    static constexpr int D_V4 = WT_TH * WT_TW * 8 * NCT;        // fp32 quads of the output-gradient tile
+    static constexpr int D_PT = (D_V4 + NT - 1) / NT;
+    static constexpr int RED_B = 2 * NWV * 4;                   // per-wave max |dout|, double-buffered
+    static constexpr int LDS_B = IN_B + NCT * D_B + RED_B;
+};
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ s16x4 tr_read(const unsigned char *lds, int byte_off) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(lds + byte_off));
+}
+__device__ __forceinline__ f16x8 cat8(s16x4 a, s16x4 b) {
+    return __builtin_bit_cast(f16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+template <int NCT>
+__global__ __launch_bounds__(W3<NCT>::NT, 1) void wgrad3_kernel(WgradParams p) {
+    using C = W3<NCT>;
+    constexpr int NT_ = C::NT, NQ = C::NQ;
+    static_assert(NT_ % (8 * NCT) == 0, "a thread's output-gradient channel quad must not change across items");
+    __shared__ __attribute__((aligned(16))) unsigned char smem[C::LDS_B];
+    unsigned char *s_in = smem, *s_d = smem + C::IN_B;
+    float *s_red = reinterpret_cast<float *>(smem + C::IN_B + NCT * C::D_B);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hl = lane >> 5;
+    const int tg = wave % 3, r4 = wave / 3;
+    const int ct = NCT == 2 ? (r4 & 1) : 0, q = NCT == 2 ? (r4 >> 1) : r4;
+    const int nchunks = p.cin_pad / 32;
+    const int total = nchunks * p.splits;
+    const int per_xcd = (total + 7) / 8;
+    const int L = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+    if (L >= total) return;
+    const int chunk = L % nchunks, split = L / nchunks;
+    const int ntiles = p.B * p.tiles_y * p.tiles_x;
+    const int t_begin = (int)((long long)ntiles * split / p.splits);
+    const int t_end = (int)((long long)ntiles * (split + 1) / p.splits);
+    const int c0 = chunk * 32;
+    const int kc = min(32, p.cin - c0);
+    const int Hi = p.up2 ? p.H / 2 : p.H, Wi = p.up2 ? p.W / 2 : p.W;
+    const bool vec_d = ((p.dout_cp | p.dout_coff) & 3) == 0;
+    const int my_c4 = tid % (8 * NCT);  // this thread's output-gradient channel quad (fixed, see static_assert)
+
+    // transposed-read lane roles: group i16 = lane & 15 supplies row (pixel) rq = i16 >> 2, channel block 4·(i16 & 3)
+    // of the 16 channels 16·((lane >> 4) & 1) ...; the half hl takes K rows 8·hl ...
+    const int i16 = lane & 15, rq = i16 >> 2;
+    const int chb = 16 * ((lane >> 4) & 1) + 4 * (i16 & 3);      // first channel of the lane's 4-channel block
+    const int ch_off = (chb >> 3) * 32 + (chb & 4) * 2;           // its byte offset in a 128-B pixel record (hi)
+
+    f32x16 acc[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    f32x4 bacc = {0.f, 0.f, 0.f, 0.f};
+    int e_cur = 0;
+
+    f32x4 rin[C::IN_PT], rd[C::D_PT];
+    auto load_tile = [&](int t) {
+        const int tx = t % p.tiles_x, ty = (t / p.tiles_x) % p.tiles_y, b = t / (p.tiles_x * p.tiles_y);
+        const int y0 = ty * WT_TH, x0 = tx * WT_TW;
+#pragma unroll
+        for (int k = 0; k < C::IN_PT; ++k) {
+            const int idx = tid + k * NT_;
+            const int px = idx >> 3, part = idx & 7;  // part = 2·group + (0 hi | 1 lo)
+            const int hy = px / WT_HX, hx = px - hy * WT_HX;
+            const int Y = y0 + hy - 1, X = x0 + hx - 1;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (idx < C::IN_IT && Y >= 0 && Y < p.H && X >= 0 && X < p.W && (part >> 1) * 8 < kc) {
+                const int sy = p.up2 ? Y / 2 : Y, sx = p.up2 ? X / 2 : X;
+                v = *reinterpret_cast<const f32x4 *>(
+                    reinterpret_cast<const unsigned char *>(p.in) +
+                    ((((long long)b * (Hi + 2) + sy + 1) * (Wi + 2) + sx + 1) * p.in_cp + c0) * 4 + part * 16);
+            }
+            rin[k] = v;
+        }
+#pragma unroll
+        for (int k = 0; k < C::D_PT; ++k) {
+            const int idx = tid + k * NT_;
+            const int px = idx / (8 * NCT), c4 = idx % (8 * NCT);
+            const int y = y0 + (px >> 5), x = x0 + (px & 31);
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (idx < C::D_V4 && y < p.H && x < p.W && c4 * 4 < p.cout) {
+                const long long pix = ((long long)b * (p.H + 2) + y + 1) * (p.W + 2) + x + 1;
+                if (p.dsplit) {  // 4 channels = half an 8-channel group: f16 hi[4] at +0, lo[4] at +16
+                    const unsigned char *g = reinterpret_cast<const unsigned char *>(p.dout) +
+                                             (pix * p.dout_cp + p.dout_coff + (c4 >> 1) * 8) * 4 + (c4 & 1) * 8;
+                    const f16x4 h = *reinterpret_cast<const f16x4 *>(g), l = *reinterpret_cast<const f16x4 *>(g + 16);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = (float)h[e] + (float)l[e];
+                } else {
+                    const float *src = p.dout + pix * p.dout_cp + p.dout_coff + c4 * 4;
+                    if (vec_d && c4 * 4 + 4 <= p.cout) {
+                        v = *reinterpret_cast<const f32x4 *>(src);
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[e] = (c4 * 4 + e < p.cout) ? src[e] : 0.f;
+                    }
+                }
+            }
+            rd[k] = v;
+        }
+    };
+    // max |dout| of the tile in registers: per wave (lane shuffles), then per workgroup through s_red[slot]
+    auto publish_max = [&](int slot) {
+        float m = 0.f;
+#pragma unroll
+        for (int k = 0; k < C::D_PT; ++k)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) m = fmaxf(m, fabsf(rd[k][e]));
+#pragma unroll
+        for (int s = 32; s >= 1; s >>= 1) m = fmaxf(m, __shfl_xor(m, s));
+        if (lane == 0) s_red[slot * C::NWV + wave] = m;
+    };
+    auto store_tile = [&](float scale) {
+#pragma unroll
+        for (int k = 0; k < C::IN_PT; ++k) {
+            const int idx = tid + k * NT_;
+            if (idx < C::IN_IT) {
+                const int px = idx >> 3, part = idx & 7;
+                const int sw = ((px >> 1) & 1);  // hi/lo swap of pixel px
+                *reinterpret_cast<f32x4 *>(s_in + px * 128 + (part >> 1) * 32 + ((part & 1) ^ sw) * 16) = rin[k];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < C::D_PT; ++k) {
+            const int idx = tid + k * NT_;
+            if (idx < C::D_V4) {
+                const int px = idx / (8 * NCT), c4 = idx % (8 * NCT);
+                const int cti = c4 >> 3, cq = c4 & 7;  // channel tile, quad within it
+                f16x4 h, l;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float x = rd[k][e] * scale;
+                    h[e] = (_Float16)x;
+                    l[e] = (_Float16)(x - (float)h[e]);
+                }
+                const int sw = ((px >> 1) & 1);
+                unsigned char *rec = s_d + cti * C::D_B + px * 128 + (cq >> 1) * 32 + (cq & 1) * 8;
+                *reinterpret_cast<f16x4 *>(rec + sw * 16) = h;
+                *reinterpret_cast<f16x4 *>(rec + (sw ^ 1) * 16) = l;
+            }
+        }
+    };
+    // byte offset of the lane's hi (lo = hi_or_lo 1) 4-channel block in pixel record px of an image
+    auto rec_off = [&](int px, int lo) { return px * 128 + ch_off + ((lo ^ ((px >> 1) & 1)) << 4); };
+
+    if (t_begin < t_end) {
+        load_tile(t_begin);
+        publish_max(0);
+    }
+    for (int t = t_begin; t < t_end; ++t) {
+        __syncthreads();
+        float m = 0.f;
+#pragma unroll
+        for (int w = 0; w < C::NWV; ++w) m = fmaxf(m, s_red[((t - t_begin) & 1) * C::NWV + w]);
+        int e_new = e_cur;
+        if (m > 0.f && m <= 3.4e38f) {  // a finite nonzero tile max; NaN / inf propagate unscaled
+            int ex;
+            frexpf(m, &ex);  // m < 2^ex
+            e_new = 14 - ex;
+        }
+        if (e_new != e_cur) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[j][r] = ldexpf(acc[j][r], e_new - e_cur);
+            e_cur = e_new;
+        }
+        if (chunk == 0) {
+#pragma unroll
+            for (int k = 0; k < C::D_PT; ++k)
+                if (tid + k * NT_ < C::D_V4) bacc += rd[k];
+        }
+        store_tile(ldexpf(1.f, e_cur));
+        __syncthreads();
+        if (t + 1 < t_end) load_tile(t + 1);
+        const unsigned char *img_d = s_d + ct * C::D_B;
+#pragma unroll 2
+        for (int kk = 0; kk < 16 / NQ; ++kk) {
+            const int kb = NQ * kk + q;             // K block: 16 pixels of tile row kb >> 1
+            const int py = kb >> 1, px0 = 16 * (kb & 1) + 8 * hl + rq;
+            const int dp = py * WT_TW + px0;        // output-gradient pixel of K rows 8hl + rq (+4)
+            const f16x8 bh = cat8(tr_read(img_d, rec_off(dp, 0)), tr_read(img_d, rec_off(dp + 4, 0)));
+            const f16x8 bl = cat8(tr_read(img_d, rec_off(dp, 1)), tr_read(img_d, rec_off(dp + 4, 1)));
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const int ip = (py + j) * WT_HX + px0 + tg;
+                const f16x8 ah = cat8(tr_read(s_in, rec_off(ip, 0)), tr_read(s_in, rec_off(ip + 4, 0)));
+                const f16x8 al = cat8(tr_read(s_in, rec_off(ip, 1)), tr_read(s_in, rec_off(ip + 4, 1)));
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[j], 0, 0, 0);
+            }
+        }
+        if (t + 1 < t_end) publish_max((t + 1 - t_begin) & 1);
+    }
+    // back to the unscaled domain, then sum the pixel classes into class 0 (fixed order 1, 2, ...) through LDS
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = ldexpf(acc[j][r], -e_cur);
+    constexpr int PER_WAVE = 3 * 16 * 64;
+    static_assert(3 * NCT * PER_WAVE * 4 <= C::LDS_B, "class reduction does not fit in LDS");
+    float *red = reinterpret_cast<float *>(smem);
+    const int slot = tg * NCT + ct;
+    for (int r = 1; r < NQ; ++r) {
+        __syncthreads();
+        if (q == r) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) red[slot * PER_WAVE + (j * 16 + e) * 64 + lane] = acc[j][e];
+        }
+        __syncthreads();
+        if (q == 0) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) acc[j][e] += red[slot * PER_WAVE + (j * 16 + e) * 64 + lane];
+        }
+    }
+    float *part = p.partial + (long long)split * (9LL * p.cin_pad * p.cout_pad + p.cout_pad);
+    if (q == 0) {
+        const int ml = lane & 31;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int tap = 3 * j + tg;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int ci = c0 + (e & 3) + 8 * (e >> 2) + 4 * hl;
+                part[((long long)tap * p.cin_pad + ci) * p.cout_pad + ct * 32 + ml] = acc[j][e];
+            }
+        }
+    }
+    if (chunk == 0) {  // bias: threads with the same channel quad, summed in thread order
+        __syncthreads();
+        reinterpret_cast<f32x4 *>(smem)[tid] = bacc;
+        __syncthreads();
+        if (tid < p.cout_pad) {
+            const float *b4 = reinterpret_cast<const float *>(smem);
+            float v = 0.f;
+            for (int th = tid / 4; th < NT_; th += 8 * NCT) v += b4[th * 4 + (tid & 3)];
+            part[9LL * p.cin_pad * p.cout_pad + tid] = v;
+        }
+    }
+}
+
 int g_wgrad_kernel = 1;  // 0 = wgrad_kernel (4 waves), 1 = wgrad2_kernel (12 waves)
 
-__global__ void wgrad_reduce_kernel(const float *partial, int splits, long long n, float scale, float *out) {
+// Gradient scale of the x3 backward (esr_grad_amax): S = 2^(11 - ex) for max|g| < 2^ex, so the largest scaled
+// element lies in [2^10, 2^11) (headroom 2^5 below the f16 range for growth through a residual block); 1 for an
+// all-zero or non-finite max (a NaN / inf propagates unscaled).
+__device__ __forceinline__ float gscale_of(const unsigned *amax) {
+    if (!amax) return 1.f;
+    const float m = __uint_as_float(*amax);
+    if (!(m > 0.f) || !(m <= 3.4e38f)) return 1.f;
+    int ex;
+    frexpf(m, &ex);
+    return ldexpf(1.f, 11 - ex);
+}
+
+__global__ void wgrad_reduce_kernel(const float *partial, int splits, long long n, float scale, float *out,
+                                    const unsigned *amax) {
     const long long i = (long long)blockIdx.x * NT + threadIdx.x;
     if (i >= n) return;
     float s = 0.f;
     for (int k = 0; k < splits; ++k) s += partial[(long long)k * n + i];
-    out[i] = scale * s;
+    out[i] = amax ? (scale * s) / gscale_of(amax) : scale * s;
 }
+
+// max |x| over a C-channel fp32 slice, OR-ed into *amax as float bits (non-negative floats order as unsigned ints)
+__global__ void grad_amax_kernel(const float *x, int cp, int coff, int C, int B, int H, int W, unsigned *amax) {
+    __shared__ float red[NT / 64];
+    const long long n = (long long)B * H * W * C;
+    float m = 0.f;
+    for (long long idx = (long long)blockIdx.x * NT + threadIdx.x; idx < n; idx += (long long)gridDim.x * NT) {
+        const int c = idx % C;
+        long long q = idx / C;
+        const int xx = q % W;
+        q /= W;
+        const int y = q % H;
+        const int b = q / H;
+        m = fmaxf(m, fabsf(x[(((long long)b * (H + 2) + y + 1) * (W + 2) + xx + 1) * cp + coff + c]));
+    }
+    for (int s = 32; s >= 1; s >>= 1) m = fmaxf(m, __shfl_xor(m, s));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < NT / 64; ++w) m = fmaxf(m, red[w]);
+        atomicMax(amax, __float_as_uint(m));
+    }
+}
+
 
 // ---------------------------------------------------------------------------------------------------------------------
 // elementwise helpers on padded NHWC channel slices
@@ -375,6 +682,61 @@ __device__ __forceinline__ long long pix_index(long long idx, int C, int B, int 
     const int y = q % H;
     const int b = q / H;
     return ((long long)b * (H + 2) + y + 1) * (W + 2) + x + 1;
+}
+
+// out = a·x1 + b·x2 on 8-channel groups; an operand in the split-f16 layout holds values scaled by S (gscale_of):
+// it is read as (hi + lo) / S, and a split output is written as v·S (overflow flagged like the x3 convs)
+__device__ __forceinline__ void ld8(const void *base, long long pix, int cp, int coff, int split, float inv_s,
+                                    float v[8]) {
+    if (split) {
+        const unsigned char *g = static_cast<const unsigned char *>(base) + (pix * cp + coff) * 4;
+        const f16x8 h = *reinterpret_cast<const f16x8 *>(g), l = *reinterpret_cast<const f16x8 *>(g + 16);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = ((float)h[e] + (float)l[e]) * inv_s;
+    } else {
+        const float *f = static_cast<const float *>(base) + pix * cp + coff;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = f[e];
+    }
+}
+
+__global__ void axpby_gs_kernel(void *out, int o_cp, int o_coff, int o_split, float a, const void *x1, int x1_cp,
+                                int x1_coff, int x1_split, float b, const void *x2, int x2_cp, int x2_coff,
+                                int x2_split, int C, int B, int H, int W, const unsigned *amax, int *overflow) {
+    const long long idx = (long long)blockIdx.x * NT + threadIdx.x;
+    const int G = C / 8;
+    if (idx >= (long long)B * H * W * G) return;
+    int g;
+    const long long pix = pix_index(idx, G, B, H, W, &g);
+    const float S = gscale_of(amax), inv_s = 1.f / S;
+    float v[8], w[8];
+    ld8(x1, pix, x1_cp, x1_coff + 8 * g, x1_split, inv_s, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= a;
+    if (x2) {
+        ld8(x2, pix, x2_cp, x2_coff + 8 * g, x2_split, inv_s, w);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += b * w[e];
+    }
+    if (o_split) {
+        f16x8 h, l;
+        bool ok = true;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float x = v[e] * S;
+            h[e] = (_Float16)x;
+            l[e] = (_Float16)(x - (float)h[e]);
+            ok = ok && fabsf(x) < 65504.f;
+        }
+        unsigned char *p = static_cast<unsigned char *>(out) + (pix * o_cp + o_coff + 8 * g) * 4;
+        *reinterpret_cast<f16x8 *>(p) = h;
+        *reinterpret_cast<f16x8 *>(p + 16) = l;
+        if (!ok && overflow) atomicOr(overflow, 1);
+    } else {
+        float *f = static_cast<float *>(out) + pix * o_cp + o_coff + 8 * g;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = v[e];
+    }
 }
 
 __global__ void lrelu_bwd_kernel(float *d, int d_cp, int d_coff, const float *y, int y_cp, int y_coff, int C, int B,
@@ -537,10 +899,11 @@ __global__ void input_adjoint_kernel(const float *d_hr, int hr_cp, int hr_coff, 
 extern "C" int esr_conv3x3_wgrad(const float *in, int32_t in_cp, int32_t cin, int32_t flags, const float *dout,
                                  int32_t dout_cp, int32_t dout_coff, int32_t cout, int32_t B, int32_t H, int32_t W,
                                  int32_t splits, float *partial, esr_stream_t stream) {
-    const int up2 = flags & 1, split = (flags >> 1) & 1;
+    const int up2 = flags & 1, split = (flags >> 1) & 1, x3 = (flags >> 2) & 1, dsplit = (flags >> 3) & 1;
     if (!in || !dout || !partial || cin <= 0 || cin % 4 || in_cp % 4 || cout <= 0 || cout > 64 || B <= 0 ||
-        H <= 0 || W <= 0 || splits <= 0 || (up2 && (H % 2 || W % 2)) || (flags & ~3) ||
-        (split && (cin % 8 || in_cp % 8 || g_wgrad_kernel != 1)))
+        H <= 0 || W <= 0 || splits <= 0 || (up2 && (H % 2 || W % 2)) || (flags & ~15) ||
+        (split && (cin % 8 || in_cp % 8 || (!x3 && g_wgrad_kernel != 1))) || (x3 && !split) ||
+        (dsplit && (!x3 || cout % 8 || dout_cp % 8 || dout_coff % 8)))
         return ESR_EINVAL;
     WgradParams p;
     p.in = in; p.in_cp = in_cp; p.cin = cin; p.up2 = up2;
@@ -549,8 +912,16 @@ extern "C" int esr_conv3x3_wgrad(const float *in, int32_t in_cp, int32_t cin, in
     p.tiles_x = (W + WT_TW - 1) / WT_TW; p.tiles_y = (H + WT_TH - 1) / WT_TH;
     p.splits = splits; p.cin_pad = (cin + 31) / 32 * 32;
     p.partial = partial;
+    p.dsplit = dsplit;
     const unsigned total = (unsigned)(p.cin_pad / 32 * splits);
-    if (g_wgrad_kernel == 1) {
+    if (x3) {
+        const unsigned grid = 8 * ((total + 7) / 8);
+        const hipStream_t st = (hipStream_t)stream;
+        if (p.cout_pad == 64)
+            hipLaunchKernelGGL((wgrad3_kernel<2>), dim3(grid), dim3(W3<2>::NT), 0, st, p);
+        else
+            hipLaunchKernelGGL((wgrad3_kernel<1>), dim3(grid), dim3(W3<1>::NT), 0, st, p);
+    } else if (g_wgrad_kernel == 1) {
         const unsigned grid = 8 * ((total + 7) / 8);  // whole XCD rounds; the surplus workgroups exit at once
         const hipStream_t st = (hipStream_t)stream;
         if (split) {
@@ -581,7 +952,37 @@ extern "C" int esr_wgrad_reduce(const float *partial, int32_t splits, int64_t n,
                                 esr_stream_t stream) {
     if (!partial || !out || splits <= 0 || n <= 0) return ESR_EINVAL;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(nblocks(n)), dim3(NT), 0, (hipStream_t)stream, partial, splits, n,
-                       scale, out);
+                       scale, out, nullptr);
+    return launched();
+}
+
+extern "C" int esr_wgrad_reduce_gs(const float *partial, int32_t splits, int64_t n, float scale, const uint32_t *amax,
+                                   float *out, esr_stream_t stream) {
+    if (!partial || !out || !amax || splits <= 0 || n <= 0) return ESR_EINVAL;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(nblocks(n)), dim3(NT), 0, (hipStream_t)stream, partial, splits, n,
+                       scale, out, amax);
+    return launched();
+}
+
+extern "C" int esr_grad_amax(const float *x, int32_t cp, int32_t coff, int32_t C, int32_t B, int32_t H, int32_t W,
+                             uint32_t *amax, esr_stream_t stream) {
+    if (!x || !amax || C <= 0 || B <= 0 || H <= 0 || W <= 0 || coff + C > cp) return ESR_EINVAL;
+    const long long n = (long long)B * H * W * C;
+    const unsigned grid = (unsigned)((n + NT - 1) / NT < 1024 ? (n + NT - 1) / NT : 1024);
+    hipLaunchKernelGGL(grad_amax_kernel, dim3(grid), dim3(NT), 0, (hipStream_t)stream, x, cp, coff, C, B, H, W, amax);
+    return launched();
+}
+
+extern "C" int esr_axpby_gs(void *out, int32_t o_cp, int32_t o_coff, int32_t o_split, float a, const void *x1,
+                            int32_t x1_cp, int32_t x1_coff, int32_t x1_split, float b, const void *x2, int32_t x2_cp,
+                            int32_t x2_coff, int32_t x2_split, int32_t C, int32_t B, int32_t H, int32_t W,
+                            const uint32_t *amax, int32_t *overflow, esr_stream_t stream) {
+    if (!out || !x1 || !amax || C <= 0 || C % 8 || B <= 0 || H <= 0 || W <= 0 || (o_cp | o_coff) % 8 ||
+        (x1_cp | x1_coff) % 8 || (x2 && (x2_cp | x2_coff) % 8))
+        return ESR_EINVAL;
+    hipLaunchKernelGGL(axpby_gs_kernel, dim3(nblocks((long long)B * H * W * (C / 8))), dim3(NT), 0,
+                       (hipStream_t)stream, out, o_cp, o_coff, o_split, a, x1, x1_cp, x1_coff, x1_split, b, x2, x2_cp,
+                       x2_coff, x2_split, C, B, H, W, amax, overflow);
     return launched();
 }
 

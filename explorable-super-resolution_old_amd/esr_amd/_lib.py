@@ -8,7 +8,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('ESR_AMD_LIB', os.path.join(_HERE, 'libesr_amd.so'))
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 c_int = ctypes.c_int32
 c_float = ctypes.c_float
@@ -60,6 +60,10 @@ _SIGNATURES = {
     'esr_conv3x3_wgrad': [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                           c_void_p, c_void_p],
     'esr_wgrad_reduce': [c_void_p, c_int, ctypes.c_int64, c_float, c_void_p, c_void_p],
+    'esr_wgrad_reduce_gs': [c_void_p, c_int, ctypes.c_int64, c_float, c_void_p, c_void_p, c_void_p],
+    'esr_grad_amax': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    'esr_axpby_gs': [c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_int,
+                     c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     'esr_wgrad_set_kernel': [c_int],
     'esr_lrelu_bwd': [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     'esr_lrelu_bwd_split': [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],

@@ -15,6 +15,7 @@ The reference's residual scales (0.2 in RDB and RRDB, block.py:235, 270) are fol
 and the reduction scales.
 """
 import ctypes
+import math
 import os
 import weakref
 
@@ -28,6 +29,12 @@ WG_SPLITS_MAX = 128
 # run once eagerly, it is captured into a HIP graph and replayed (one launch), with the parameter repack (GatherPlan
 # refresh) kept outside the graph.  ESR_TRAIN_GRAPHS=0 keeps everything eager.
 USE_GRAPHS = os.environ.get('ESR_TRAIN_GRAPHS', '1') != '0'
+# Weight gradients of an x3 forward (split-f16 activations) on the x3 MFMA kernel (esr_conv3x3_wgrad flag 4); 0 keeps
+# the exact-fp32 weight-gradient kernel reading the same split activations.
+WGRAD_X3 = os.environ.get('ESR_WGRAD_X3', '0') != '0'
+# Data gradients inside the residual blocks on the x3 conv (split-f16 gradients scaled per RRDB, include/esr_amd.h
+# "x3 backward") when the forward ran in x3 and only parameter gradients are wanted (training); 0 keeps them fp32.
+DGRAD_X3 = os.environ.get('ESR_DGRAD_X3', '0') != '0'
 
 
 def _z(dev, *s):
@@ -68,6 +75,8 @@ class TrainWorkspace:
         self.dZl = _z(dev, B, H + 2, W + 2, 8)
         self.dFirst = _z(dev, B, H + 2, W + 2, self.first_cp)
         self.dZh = _z(dev, B, 4 * H + 2, 4 * W + 2, 8) if latent else None
+        self.gamax = torch.zeros(nb, device=dev, dtype=torch.int32)  # per-RRDB max |gradient| bits (x3 backward)
+        self.bwd_overflow = torch.zeros(1, device=dev, dtype=torch.int32)
         self.wg_n_max = 9 * 224 * 64 + 64
         self.partial = torch.empty(WG_SPLITS_MAX * self.wg_n_max, device=dev, dtype=torch.float32)
         self.graphs = {}
@@ -192,6 +201,45 @@ class _BwdPacked:
         self.params = plan.params
         assert all(id(p) in by_param for p in self.params), 'generator parameter without a backward rule'
         self.gidx = torch.cat([by_param[id(p)] for p in self.params]).to(dev)
+        self._x3 = None
+
+    def x3_fused(self):
+        """The fused RDB data-gradient weights in the x3 layout (engine.pack_x3: [chunk16][tap][n][2 × (hi 8 | lo 8)]),
+        rebuilt in place with one gather after every refresh of the fp32 packs.  Each weight keeps the power-of-two
+        scale chosen at the first build (one host sync, then none: captured graphs stay valid); returns
+        ([{target: (x3 tensor, scale)}] per RDB, device int32 flag = a weight left its scale's safe range)."""
+        buf = self.plan.buf
+        if self._x3 is None:
+            views = [(i, k, v) for i, f in enumerate(self.rdb_fused) for k, v in f.items()]
+            amax = torch.stack([v.abs().max() for _, _, v in views]).cpu().tolist()  # first build only
+            idx, scl, out, off = [], [], [], 0
+            for (i, k, v), a in zip(views, amax):
+                n32, T, n_pad, _ = v.shape
+                sc = 1.0 if a == 0.0 else 2.0 ** (14 - math.floor(math.log2(a)))
+                pos = torch.arange(v.numel(), device=buf.device) + v.storage_offset()
+                idx.append(pos.view(n32, T, n_pad, 2, 16).permute(0, 3, 1, 2, 4).reshape(-1))
+                scl.append(torch.full((v.numel(),), sc, device=buf.device))
+                out.append((i, k, off, v.numel(), sc))
+                off += 2 * v.numel()
+            self._x3_idx, self._x3_scl = torch.cat(idx), torch.cat(scl)
+            self._x3_buf = torch.empty(off, device=buf.device, dtype=torch.float16)
+            self._x3_w = [dict() for _ in self.rdb_fused]
+            for i, k, o, n, sc in out:
+                self._x3_w[i][k] = (self._x3_buf[o:o + 2 * n], sc)
+            self._x3_bad = torch.zeros(1, device=buf.device, dtype=torch.int32)
+            self._x3 = 'stale'
+        if self._x3 == 'stale':
+            g = buf[self._x3_idx] * self._x3_scl
+            hi = g.half()
+            lo = (g - hi.float()).half()
+            G = g.numel() // 8
+            self._x3_buf.view(G, 2, 8).copy_(torch.stack([hi.view(G, 8), lo.view(G, 8)], 1))
+            self._x3_bad.copy_((g.abs().amax() >= 61440.0).to(torch.int32).view(1))
+            self._x3 = 'fresh'
+        return self._x3_w, self._x3_bad
+
+    def reset_x3(self):
+        self._x3 = None
 
 
 def _fused_rdb_weights(plan, convs, zc):
@@ -230,6 +278,8 @@ def _bwd_packed(net, latent):
     if c[1] != vkey:
         with torch.no_grad():
             c[2].plan.refresh()
+        if c[2]._x3 is not None:
+            c[2]._x3 = 'stale'
         c[1] = vkey
     return c[2]
 
@@ -246,6 +296,7 @@ class _Runner:
         self.stream = stream
         self.need_params, self.need_input = need_params, need_input
         self.split = split  # forward activations in the split-f16 layout (x3 forward)
+        self.x3 = None  # x3 backward: (per-RDB x3 fused weights, gradient-amax buffer, overflow flag)
 
     def dgrad(self, bc, src, src_cp, src_coff, cin_k, h, w, dst, dst_cp, dst_base, accumulate, res=None):
         """dst[:, n0-dst_base ...] (+)= conv(src slice, rot180 W^T) for every output slice; `res` = (buf, cp, coff)
@@ -288,8 +339,9 @@ class _Runner:
                                                 wpk.data_ptr(), self.bp.zero_bias.data_ptr(), nw, ctypes.byref(o),
                                                 self.stream), 'dgrad_in')
 
-    def wgrad(self, bc, inp, in_cp, cin, up2, dout, d_cp, d_coff, h, w, scale=1.0):
-        """Weight + bias gradient of one conv into its region of the flat packed-layout buffer bp.dw."""
+    def wgrad(self, bc, inp, in_cp, cin, up2, dout, d_cp, d_coff, h, w, scale=1.0, amax=None):
+        """Weight + bias gradient of one conv into its region of the flat packed-layout buffer bp.dw.  `amax` (a
+        device pointer): the output gradient is split-f16, scaled by the gradient scale of that amax."""
         if not self.need_params:
             return
         assert cin == bc.cin_buf
@@ -297,12 +349,29 @@ class _Runner:
         ntiles = self.B * ((h + 7) // 8) * ((w + 31) // 32)
         splits = max(1, min(WG_SPLITS_MAX, -(-1024 // chunks), ntiles))
         assert splits * bc.wg_n <= self.ws.partial.numel()
-        _lib.check(self.lib.esr_conv3x3_wgrad(inp.data_ptr(), in_cp, cin, up2 | (2 if self.split else 0),
-                                              dout.data_ptr(), d_cp, d_coff,
+        flags = up2 | ((6 if WGRAD_X3 or amax is not None else 2) if self.split else 0) | (8 if amax is not None else 0)
+        _lib.check(self.lib.esr_conv3x3_wgrad(inp.data_ptr(), in_cp, cin, flags, dout.data_ptr(), d_cp, d_coff,
                                               bc.cout, self.B, h, w, splits, self.ws.partial.data_ptr(), self.stream),
                    'wgrad')
-        _lib.check(self.lib.esr_wgrad_reduce(self.ws.partial.data_ptr(), splits, bc.wg_n, scale,
-                                             self.bp.dw.data_ptr() + 4 * bc.wg_off, self.stream), 'wgrad_reduce')
+        dst = self.bp.dw.data_ptr() + 4 * bc.wg_off
+        if amax is None:
+            _lib.check(self.lib.esr_wgrad_reduce(self.ws.partial.data_ptr(), splits, bc.wg_n, scale, dst, self.stream),
+                       'wgrad_reduce')
+        else:
+            _lib.check(self.lib.esr_wgrad_reduce_gs(self.ws.partial.data_ptr(), splits, bc.wg_n, scale, amax, dst,
+                                                    self.stream), 'wgrad_reduce_gs')
+
+    def dgrad_x3(self, wx, src, src_cp, src_coff, cin_k, h, w, dst, dst_cp, dst_coff, nw, res=None, mask=None):
+        """dgrad_fused on the x3 conv: src / dst / res are split-f16 gradients at one scale (the conv is linear, so
+        the scale passes through); the LeakyReLU backward reads the saved split activation `mask`."""
+        wpk, w_scale = wx
+        r1, r1_cp, r1_coff = res if res is not None else (None, 0, 0)
+        r2, r2_cp, r2_coff = mask if mask is not None else (None, 0, 0)
+        o = E._conv_out(dst, dst_cp, dst_coff, h, w, 3 if mask is not None else 0, r1=r1, r1_cp=r1_cp,
+                        r1_coff=r1_coff, s1=1.0, r2=r2, r2_cp=r2_cp, r2_coff=r2_coff)
+        _lib.check(self.lib.esr_conv3x3_fwd_x3(src.data_ptr() + 4 * src_coff, self.B, h, w, src_cp, cin_k,
+                                               wpk.data_ptr(), self.bp.zero_bias.data_ptr(), w_scale, nw,
+                                               ctypes.byref(o), self.x3[2].data_ptr(), self.stream), 'dgrad_x3')
 
     def lrelu(self, d, d_cp, d_coff, y, y_cp, y_coff, C, h, w):
         fn = self.lib.esr_lrelu_bwd_split if self.split else self.lib.esr_lrelu_bwd
@@ -313,6 +382,19 @@ class _Runner:
         _lib.check(self.lib.esr_axpby(out.data_ptr(), o_cp, o_coff, a, x1.data_ptr(), x1_cp, x1_coff, b,
                                       None if x2 is None else x2.data_ptr(), x2_cp, x2_coff, C, self.B, h, w,
                                       self.stream), 'axpby')
+
+
+def _rdb_backward_x3(R, P, dcat, convs, fx3, zc, cp, H, W, dx, amax):
+    """_rdb_backward with the concat-gradient buffers in the split-f16 layout at gradient scale S(amax): the fused
+    data-gradient convs on the x3 conv, the weight gradients on the x3 kernel reading the split gradients."""
+    dcp = R.ws.dcp
+    d4 = zc + 192
+    R.wgrad(convs[4], P, cp, zc + 192, 0, dcat, dcp, d4, H, W, scale=0.2, amax=amax)
+    for m in (4, 3, 2, 1):
+        s_in, t = zc + 64 + 32 * m, zc + 64 + 32 * (m - 1)
+        R.dgrad_x3(fx3['m%d' % m], dcat, dcp, s_in, zc + 256 - s_in, H, W, dcat, dcp, t, 32, mask=(P, cp, t))
+        R.wgrad(convs[m - 1], P, cp, t, 0, dcat, dcp, t, H, W, amax=amax)
+    R.dgrad_x3(fx3['x'], dcat, dcp, zc + 64, 192, H, W, dx[0], dx[1], dx[2], 64, res=(dcat, dcp, d4))
 
 
 def _rdb_backward(R, P, dcat, convs, fused, zc, cp, H, W, dx):
@@ -332,14 +414,22 @@ def _rdb_backward(R, P, dcat, convs, fused, zc, cp, H, W, dx):
     R.dgrad_fused(fused['x'], dcat, dcp, zc + 64, 192, H, W, dx[0], dx[1], dx[2], 64, res=(dcat, dcp, d4))
 
 
-def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_input=False, split=False):
-    """dL/dparams of RRDBNet (+ CEM in train or eval mode) and/or dL/dinput given dL/dout.
+def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_input=False, split=False, x3=False):
+    """dL/dparams of RRDBNet (+ CEM in train or eval mode) and/or dL/dinput given dL/dout.  x3 (with split, params
+    only): the residual blocks' backward in the split-f16 scheme; ws.bwd_overflow then tells whether a scaled gradient
+    or a weight left its f16 range (the caller reruns without x3).
     Returns ({param: grad} or {}, input gradient [B, C_in, h, w] or None)."""
     dev = d_out.device
     stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     bp = _bwd_packed(net, latent)
     R = _Runner(ws, bp, stream, need_params, need_input, split)
     lib = R.lib
+    if x3:
+        assert split and need_params and not need_input
+        fx3, bad = bp.x3_fused()
+        ws.gamax.zero_()
+        ws.bwd_overflow.copy_(bad)
+        R.x3 = (fx3, ws.gamax, ws.bwd_overflow)
     if need_input:
         ws.dZl.zero_()
         ws.dFirst.zero_()
@@ -403,6 +493,18 @@ def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_in
     D0, D1 = ws.D
     dcp, d4 = ws.dcp, zc + 192
     for k in reversed(range(net.nb)):
+        if x3:  # gradient scale of this RRDB from max |trunk gradient| at its output
+            amax = ws.gamax.data_ptr() + 4 * k
+            ovf = ws.bwd_overflow.data_ptr()
+            _lib.check(lib.esr_grad_amax(ws.GA.data_ptr(), 64, 0, 64, Bn, H, W, amax, stream), 'grad_amax')
+            _lib.check(lib.esr_axpby_gs(D0.data_ptr(), dcp, d4, 1, 0.2, ws.GA.data_ptr(), 64, 0, 0, 0.0, None, 0, 0,
+                                        0, 64, Bn, H, W, amax, ovf, stream), 'axpby_gs')
+            for j, (dc, dn) in zip((2, 1, 0), ((D0, D1), (D1, D0), (D0, D1))):
+                _rdb_backward_x3(R, Q[3 * k + j], dc, bp.rdb[3 * k + j], R.x3[0][3 * k + j], zc, cp, H, W,
+                                 (dn, dcp, d4), amax)
+            _lib.check(lib.esr_axpby_gs(ws.GA.data_ptr(), 64, 0, 0, 1.0, ws.GA.data_ptr(), 64, 0, 0, 1.0,
+                                        D1.data_ptr(), dcp, d4, 1, 64, Bn, H, W, amax, ovf, stream), 'axpby_gs')
+            continue
         R.axpby(D0, dcp, d4, 0.2, ws.GA, 64, 0, C=64, h=H, w=W)
         for j, (dc, dn) in zip((2, 1, 0), ((D0, D1), (D1, D0), (D0, D1))):
             _rdb_backward(R, Q[3 * k + j], dc, bp.rdb[3 * k + j], bp.rdb_fused[3 * k + j], zc, cp, H, W, (dn, dcp, d4))
@@ -515,12 +617,24 @@ class _GeneratorFn(torch.autograd.Function):
         if ctx.ws.owner() is not ctx.owner:  # cannot happen through _train_workspace; guards direct workspace reuse
             raise RuntimeError('esr_amd: the saved activations of this forward were overwritten by a later forward')
         bp = _bwd_packed(ctx.net, ctx.latent)  # parameter repack, outside any graph
-        key = ('bwd', tuple(d_out.shape), _cem_key(ctx.cem), ctx.M, need_params, need_input, id(bp), ctx.split)
-        (flat, dx), graphed = _run_graphed(
-            ctx.ws, key, lambda g: generator_backward(ctx.net, ctx.cem, ctx.ws, g, ctx.latent, ctx.M,
-                                                      need_params=need_params, need_input=need_input,
-                                                      split=ctx.split),
-            d_out.contiguous())
+        x3 = DGRAD_X3 and ctx.split and need_params and not need_input
+        if x3:
+            bp.x3_fused()  # x3 repack of the data-gradient weights, outside any graph
+
+        def run(x3):
+            key = ('bwd', tuple(d_out.shape), _cem_key(ctx.cem), ctx.M, need_params, need_input, id(bp), ctx.split,
+                   x3)
+            return _run_graphed(
+                ctx.ws, key, lambda g: generator_backward(ctx.net, ctx.cem, ctx.ws, g, ctx.latent, ctx.M,
+                                                          need_params=need_params, need_input=need_input,
+                                                          split=ctx.split, x3=x3),
+                d_out.contiguous())
+        (flat, dx), graphed = run(x3)
+        if x3 and int(ctx.ws.bwd_overflow.item()):  # a scaled gradient (or weight) left f16's range: redo in fp32
+            E.OVERFLOW_RERUNS += 1
+            if int(bp._x3_bad.item()):
+                bp.reset_x3()  # new weight scales at the next x3 backward
+            (flat, dx), graphed = run(False)
         if graphed:
             flat = flat.clone() if flat is not None else None
             dx = dx.clone() if dx is not None else None

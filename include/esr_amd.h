@@ -40,8 +40,9 @@ enum esr_status {
  *   v = acc + bias[n]; if (lrelu == 1) v = v > 0 ? v : 0.2*v   (conv_block CNA + act, block.py:10-23,141-146)
  *   if (r1) v = s1*v + r1[pixel, r1_coff + n]                  (RDB / trunk residuals, block.py:96,235,270)
  *   if (lrelu == 2) v = r2[pixel, r2_coff + n] > 0 ? v : 0.2*v (LeakyReLU backward through the saved activation r2;
- *                                                               exact-fp32 convs only, r2 required; lrelu == 3: r2
- *                                                               in the split-f16 layout, r2_cp/r2_coff % 8 == 0)
+ *                                                               r2 required; lrelu == 3: r2 in the split-f16
+ *                                                               layout, r2_cp/r2_coff % 8 == 0; the x3 convs take
+ *                                                               lrelu 0, 1 and 3)
  *   else if (r2) v = s2*v + r2[pixel, r2_coff + n]
  *   out[pixel, out_coff + n] = v   (and out2 likewise when out2 != NULL)
  * Output pixel of input-grid position (y, x) is (out_sy*y + out_oy, out_sx*x + out_ox) in the out grid (out_h × out_w,
@@ -172,6 +173,29 @@ int esr_conv3x3_wgrad(const float *in, int32_t in_cp, int32_t cin, int32_t flags
                       esr_stream_t stream);
 /* out[i] = scale · Σ_s partial[s·n + i], fixed summation order. */
 int esr_wgrad_reduce(const float *partial, int32_t splits, int64_t n, float scale, float *out, esr_stream_t stream);
+
+/* ---- x3 backward (split-f16 gradients) ----------------------------------------------------------------------------
+ * esr_conv3x3_wgrad flags: bit 0 = nearest-×2 input (upconv), bit 1 = input in the split-f16 layout (the x3 forward's
+ * activations), bit 2 = x3 products on f16 MFMA (requires bit 1; the output gradient is split per pixel tile after
+ * a power-of-two scaling chosen from the tile's max, the accumulators rescaled exactly between tiles), bit 3 = the
+ * output gradient itself in the split layout (requires bit 2; cout, dout_cp, dout_coff % 8 == 0).
+ * Inside the residual blocks the x3 backward keeps its data gradients in the split layout, scaled by a power of two
+ * S per RRDB so that they sit inside f16's range: S = 2^(11 - ex) for max|g| < 2^ex, g the fp32 trunk gradient at
+ * the block's output, whose max esr_grad_amax accumulates (as float bits, atomic max) into *amax (zeroed by the
+ * caller).  The data-gradient convs run on esr_conv3x3_fwd_x3 (linear: S passes through) with o->lrelu = 3, the
+ * LeakyReLU backward through the saved split activation r2 (block.py:10-23, 233-235). */
+int esr_grad_amax(const float *x, int32_t cp, int32_t coff, int32_t C, int32_t B, int32_t H, int32_t W,
+                  uint32_t *amax, esr_stream_t stream);
+/* out = a·x1 + b·x2 (x2 may be NULL) on C-channel slices (C % 8 == 0); each of out / x1 / x2 is fp32 or (flag 1)
+ * split-f16 holding values × S(amax): split operands are read as (hi + lo) / S, a split output is written as v·S
+ * (*overflow |= 1 if |v·S| >= 65504).  Channel pitches / offsets % 8 == 0. */
+int esr_axpby_gs(void *out, int32_t o_cp, int32_t o_coff, int32_t o_split, float a, const void *x1, int32_t x1_cp,
+                 int32_t x1_coff, int32_t x1_split, float b, const void *x2, int32_t x2_cp, int32_t x2_coff,
+                 int32_t x2_split, int32_t C, int32_t B, int32_t H, int32_t W, const uint32_t *amax,
+                 int32_t *overflow, esr_stream_t stream);
+/* out[i] = scale / S(amax) · Σ_s partial[s·n + i]: the weight gradient of a conv whose output gradient was scaled. */
+int esr_wgrad_reduce_gs(const float *partial, int32_t splits, int64_t n, float scale, const uint32_t *amax, float *out,
+                        esr_stream_t stream);
 /* Kernel selection for esr_conv3x3_wgrad (process-wide, for A/B tests and benchmarks): 1 (default) = 12-wave
  * kernel (three waves per SIMD, next tile prefetched into registers, XCD-grouped chunks), 0 = the 4-wave kernel.
  * Both are deterministic; they sum the pixels in different orders.  Returns the previous setting, or ESR_EINVAL. */

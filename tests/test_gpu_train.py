@@ -191,7 +191,7 @@ def test_input_and_parameter_gradients_together_vs_oracle(gpu_device, mode, prec
             assert ok, (n, msg)
 
 
-@pytest.mark.parametrize('variant', [0, 1])
+@pytest.mark.parametrize('variant', [0, 1, 'x3'])
 @pytest.mark.parametrize('cin,in_cp,cout,dout_cp,dout_coff,up2,B,H,W,splits', [
     (64, 64, 32, 192, 64, 0, 2, 20, 40, 7),      # RDB growth conv: dout a channel slice of a concat buffer
     (72, 80, 64, 64, 0, 0, 3, 13, 33, 5),        # latent-slot input, cout 64, ragged tiles
@@ -202,7 +202,11 @@ def test_input_and_parameter_gradients_together_vs_oracle(gpu_device, mode, prec
 ])
 def test_weight_gradient_kernels_vs_float64(gpu_device, variant, cin, in_cp, cout, dout_cp, dout_coff, up2, B, H, W,
                                             splits):
-    """esr_conv3x3_wgrad (both kernels) + esr_wgrad_reduce against torch.nn.grad.conv2d_weight in float64."""
+    """esr_conv3x3_wgrad (both fp32 kernels, and the x3 kernel on split-f16 activations) + esr_wgrad_reduce against
+    torch.nn.grad.conv2d_weight in float64.  The x3 kernel splits the output gradient per pixel tile after a
+    power-of-two scaling; here the output gradient is ~2^-30 (a realistic loss-gradient magnitude, far below f16's
+    range) and its magnitude changes by 2^3 steps from one 8-row tile / image to the next, so that tiles take
+    different scales (the accumulator is rescaled between them) and every tile still counts in the norm."""
     import ctypes
     from esr_amd import _lib
     lib = _lib.load()
@@ -213,16 +217,27 @@ def test_weight_gradient_kernels_vs_float64(gpu_device, variant, cin, in_cp, cou
     xin = torch.zeros(B, Hi + 2, Wi + 2, in_cp)
     xin[:, 1:-1, 1:-1, :cin] = x.permute(0, 2, 3, 1)
     dbuf = torch.randn(B, H + 2, W + 2, dout_cp, generator=g)  # junk around the slice must be ignored
+    if variant == 'x3':
+        if cin % 8 or in_cp % 8:
+            pytest.skip('split-f16 activations need 8-channel groups')
+        tile = torch.arange(H).view(1, H) // 8 + torch.arange(B).view(B, 1)
+        dy = dy * torch.exp2(-30.0 + 3.0 * (tile % 5 - 2)).view(B, 1, H, 1)  # 2^-36 .. 2^-24 by tile
     dbuf[:, 1:-1, 1:-1, dout_coff:dout_coff + cout] = dy.permute(0, 2, 3, 1)
+    flags = up2
+    if variant == 'x3':
+        from esr_amd import engine as E
+        xin = E.to_split(xin)
+        x = E.from_split(E.to_split(x.permute(0, 2, 3, 1).contiguous())).permute(0, 3, 1, 2)  # the values it holds
+        flags = up2 | 6
     cin_pad, cout_pad = 32 * ((cin + 31) // 32), 64 if cout > 32 else 32
     n = 9 * cin_pad * cout_pad + cout_pad
     xin, dbuf = xin.to(gpu_device), dbuf.to(gpu_device)
     partial = torch.full((splits * n,), float('nan'), device=gpu_device)
     out = torch.empty(n, device=gpu_device)
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    prev = lib.esr_wgrad_set_kernel(variant)
+    prev = lib.esr_wgrad_set_kernel(variant if variant != 'x3' else 1)
     try:
-        _lib.check(lib.esr_conv3x3_wgrad(xin.data_ptr(), in_cp, cin, up2, dbuf.data_ptr(), dout_cp, dout_coff, cout,
+        _lib.check(lib.esr_conv3x3_wgrad(xin.data_ptr(), in_cp, cin, flags, dbuf.data_ptr(), dout_cp, dout_coff, cout,
                                          B, H, W, splits, partial.data_ptr(), st), 'wgrad')
         _lib.check(lib.esr_wgrad_reduce(partial.data_ptr(), splits, n, 1.0, out.data_ptr(), st), 'reduce')
         torch.cuda.synchronize()
