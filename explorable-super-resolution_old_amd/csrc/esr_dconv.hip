@@ -29,6 +29,8 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int NTH = 256;
 constexpr int MT = 256;                  // pixels per workgroup
@@ -169,6 +171,182 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_kernel(FwdParams p) {
     }
 }
 
+// ---- x3 forward (split-f16 operands, fp32-level accuracy) -------------------------------------------------------------
+// The same gather-GEMM on v_mfma_f32_32x32x16_f16: every staged fp32 operand value v is carried as hi = f16(v·s),
+// lo = f16(v·s - hi) and a product as a_hi·b_hi + a_hi·b_lo + a_lo·b_hi (esr_conv_x3.hip's scheme), with the split
+// done here at staging (the operands are PyTorch-produced fp32 tensors: activations, gradients, or gradients of
+// gradients in the WGAN-GP double backward).  Scales: per K step (one tap × 32 channels) the workgroup takes the max
+// |a| of its 256 × 32 A tile and max |b| of its 64 × 32 B tile; s_a = 2^eA, s_b = 2^eB bring each max into
+// [2^13, 2^14), so tiny gradients (~1e-9) sit in f16's normal range like activations do.  The accumulators hold the
+// sum in the scale 2^(eA + eB) of the current step and are multiplied by 2^(new - old) when it changes (v_ldexp:
+// exact), by 2^-(eA + eB) at the end.  LDS rows: 32 f16 hi then 32 f16 lo (128 B) + 16 B pad: the 16 rows of a
+// ds_read_b128 group land on 16 distinct 4-bank slots.
+constexpr int XP = 144;  // LDS row pitch (bytes) of the x3 kernel
+
+__device__ __forceinline__ int tile_exp(float m, int e_keep) {
+    if (!(m > 0.f) || !(m <= 3.4e38f)) return e_keep;  // all zero, or NaN / inf (propagates unscaled)
+    int ex;
+    frexpf(m, &ex);
+    return 14 - ex;
+}
+
+__global__ __launch_bounds__(NTH, 2) void dconv_fwd_x3_kernel(FwdParams p) {
+    __shared__ __attribute__((aligned(16))) unsigned char lds[(MT + NB) * XP];
+    __shared__ float s_red[2][2][NTH / 64];
+    unsigned char *s_a = lds, *s_b = lds + MT * XP;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hl = lane >> 5, ml = lane & 31;
+    const int per_img = p.MH * p.MW;
+    const long long M = (long long)p.B * per_img;
+    const long long m0 = (long long)blockIdx.x * MT;
+    const int n0 = blockIdx.y * NB;
+    const int cg = tid & 7;
+    const bool vec = p.vec != 0;
+
+    int pb[A_IT], py[A_IT], px[A_IT];
+#pragma unroll
+    for (int k = 0; k < A_IT; ++k) {
+        const long long m = m0 + (tid >> 3) + 32 * k;
+        pb[k] = -1;
+        py[k] = 0;
+        px[k] = 0;
+        if (m < M) {
+            const int b = (int)(m / per_img), r = (int)(m - (long long)b * per_img);
+            pb[k] = b;
+            py[k] = r / p.MW;
+            px[k] = r - py[k] * p.MW;
+        }
+    }
+    f32x4 ra[A_IT], rb[B_IT];
+    const int nsteps = p.T * p.nck;
+    auto load = [&](int step) {
+        const int t = step / p.nck, j = step - t * p.nck;
+        const int c = j * KC + cg * 4;
+        const int oy = p.offy[t], ox = p.offx[t];
+#pragma unroll
+        for (int k = 0; k < A_IT; ++k) {
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            const int sy = p.smy * py[k] + oy, sx = p.smx * px[k] + ox;
+            if (pb[k] >= 0 && c < p.kc && sy >= 0 && sy < p.Hs && sx >= 0 && sx < p.Ws)
+                v = load4(p.src + (((long long)pb[k] * p.Hs + sy) * p.Ws + sx) * p.sp, c, p.kc, vec);
+            ra[k] = v;
+        }
+        const float *wj = p.w + ((long long)(t * p.nck + j) * p.n_pad + n0) * KC;
+#pragma unroll
+        for (int k = 0; k < B_IT; ++k) rb[k] = *reinterpret_cast<const f32x4 *>(wj + (tid + k * NTH) * 4);
+    };
+    auto publish = [&](int slot) {
+        float ma = 0.f, mb = 0.f;
+#pragma unroll
+        for (int k = 0; k < A_IT; ++k)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) ma = fmaxf(ma, fabsf(ra[k][e]));
+#pragma unroll
+        for (int k = 0; k < B_IT; ++k)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) mb = fmaxf(mb, fabsf(rb[k][e]));
+#pragma unroll
+        for (int s = 32; s >= 1; s >>= 1) {
+            ma = fmaxf(ma, __shfl_xor(ma, s));
+            mb = fmaxf(mb, __shfl_xor(mb, s));
+        }
+        if (lane == 0) {
+            s_red[slot][0][wave] = ma;
+            s_red[slot][1][wave] = mb;
+        }
+    };
+    auto put = [&](unsigned char *row, f32x4 v, float s) {  // 4 channels at quad cg of a staged row
+        f16x4 h, l;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float x = v[e] * s;
+            h[e] = (_Float16)x;
+            l[e] = (_Float16)(x - (float)h[e]);
+        }
+        *reinterpret_cast<f16x4 *>(row + cg * 8) = h;
+        *reinterpret_cast<f16x4 *>(row + 64 + cg * 8) = l;
+    };
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.f;
+    int ea = 0, eb = 0;
+
+    load(0);
+    publish(0);
+    for (int step = 0; step < nsteps; ++step) {
+        __syncthreads();
+        float ma = 0.f, mb = 0.f;
+#pragma unroll
+        for (int w = 0; w < NTH / 64; ++w) {
+            ma = fmaxf(ma, s_red[step & 1][0][w]);
+            mb = fmaxf(mb, s_red[step & 1][1][w]);
+        }
+        const int ea2 = tile_exp(ma, ea), eb2 = tile_exp(mb, eb);
+        if (ea2 + eb2 != ea + eb) {
+            const int d = ea2 + eb2 - ea - eb;
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc[mt][nt][r] = ldexpf(acc[mt][nt][r], d);
+        }
+        ea = ea2;
+        eb = eb2;
+        const float sa = ldexpf(1.f, ea), sb = ldexpf(1.f, eb);
+#pragma unroll
+        for (int k = 0; k < A_IT; ++k) put(s_a + ((tid >> 3) + 32 * k) * XP, ra[k], sa);
+#pragma unroll
+        for (int k = 0; k < B_IT; ++k) put(s_b + ((tid + k * NTH) >> 3) * XP, rb[k], sb);
+        __syncthreads();
+        if (step + 1 < nsteps) load(step + 1);
+        const unsigned char *a0 = s_a + (64 * wave + ml) * XP + 16 * hl;
+        const unsigned char *b0 = s_b + ml * XP + 16 * hl;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            f16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                ah[i] = *reinterpret_cast<const f16x8 *>(a0 + i * 32 * XP + 32 * s);
+                al[i] = *reinterpret_cast<const f16x8 *>(a0 + i * 32 * XP + 64 + 32 * s);
+                bh[i] = *reinterpret_cast<const f16x8 *>(b0 + i * 32 * XP + 32 * s);
+                bl[i] = *reinterpret_cast<const f16x8 *>(b0 + i * 32 * XP + 64 + 32 * s);
+            }
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt) {
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[mt], bh[nt], acc[mt][nt], 0, 0, 0);
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mt], bl[nt], acc[mt][nt], 0, 0, 0);
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mt], bh[nt], acc[mt][nt], 0, 0, 0);
+                }
+        }
+        if (step + 1 < nsteps) publish((step + 1) & 1);
+    }
+
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+        const int n = n0 + nt * 32 + ml;
+        if (n >= p.n) continue;
+        const float bn = p.bias ? p.bias[n] : 0.f;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const long long m = m0 + 64 * wave + 32 * mt + (r & 3) + 8 * (r >> 2) + 4 * hl;
+                if (m >= M) continue;
+                const int b = (int)(m / per_img), rr = (int)(m - (long long)b * per_img);
+                const int Y = rr / p.MW, X = rr - (rr / p.MW) * p.MW;
+                const int oy = p.omy * Y + p.oay, ox = p.omx * X + p.oax;
+                p.out[(((long long)b * p.Ho + oy) * p.Wo + ox) * p.op + n] = ldexpf(acc[mt][nt][r], -(ea + eb)) + bn;
+            }
+    }
+}
+
 // ---- weight gradient ------------------------------------------------------------------------------------------------
 constexpr int WKP = 64;   // pixels per K step
 constexpr int WPS = 68;   // LDS row pitch (floats) of the [pixel][64 channels] tiles
@@ -262,6 +440,8 @@ bool aligned16(const void *ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15)
 
 }  // namespace
 
+int g_dconv_x3 = 0;  // esr_dconv_set_x3
+
 extern "C" int esr_dconv_fwd(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t src_pitch, int32_t kc,
                              const float *w_packed, int32_t nck, int32_t n_pad, const float *bias, float *out,
                              int32_t Ho, int32_t Wo, int32_t out_pitch, int32_t n, int32_t MH, int32_t MW, int32_t omy,
@@ -286,8 +466,18 @@ extern "C" int esr_dconv_fwd(const float *src, int32_t B, int32_t Hs, int32_t Ws
     const long long gx = (M + MT - 1) / MT;
     if (gx > 0x7fffffff) return ESR_EINVAL;
     const dim3 grid((unsigned)gx, (unsigned)((n + NB - 1) / NB)), block(NTH);
-    hipLaunchKernelGGL(dconv_fwd_kernel, grid, block, 0, (hipStream_t)stream, p);
+    if (g_dconv_x3)
+        hipLaunchKernelGGL(dconv_fwd_x3_kernel, grid, block, 0, (hipStream_t)stream, p);
+    else
+        hipLaunchKernelGGL(dconv_fwd_kernel, grid, block, 0, (hipStream_t)stream, p);
     return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+}
+
+extern "C" int esr_dconv_set_x3(int32_t on) {
+    if (on < 0 || on > 1) return ESR_EINVAL;
+    const int prev = g_dconv_x3;
+    g_dconv_x3 = on;
+    return prev;
 }
 
 extern "C" int esr_dconv_wgrad(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t src_pitch, int32_t cin,

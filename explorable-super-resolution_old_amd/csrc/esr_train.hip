@@ -638,13 +638,26 @@ __device__ __forceinline__ float gscale_of(const unsigned *amax) {
     return ldexpf(1.f, 11 - ex);
 }
 
+// Each workgroup: 32 consecutive outputs × 8 slices of the splits; a slice is summed in split order, then the 8
+// slice sums in slice order (fixed order: deterministic), so a reduction over ~100 splits runs with 8× the
+// threads of a one-thread-per-output loop.
+constexpr int RED_O = 32, RED_S = NT / RED_O;
 __global__ void wgrad_reduce_kernel(const float *partial, int splits, long long n, float scale, float *out,
                                     const unsigned *amax) {
-    const long long i = (long long)blockIdx.x * NT + threadIdx.x;
-    if (i >= n) return;
+    __shared__ float sl[RED_S][RED_O];
+    const int o = threadIdx.x % RED_O, q = threadIdx.x / RED_O;
+    const long long i = (long long)blockIdx.x * RED_O + o;
+    const int k0 = splits * q / RED_S, k1 = splits * (q + 1) / RED_S;
     float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += partial[(long long)k * n + i];
-    out[i] = amax ? (scale * s) / gscale_of(amax) : scale * s;
+    if (i < n)
+        for (int k = k0; k < k1; ++k) s += partial[(long long)k * n + i];
+    sl[q][o] = s;
+    __syncthreads();
+    if (q == 0 && i < n) {
+        float t = sl[0][o];
+        for (int r = 1; r < RED_S; ++r) t += sl[r][o];
+        out[i] = amax ? (scale * t) / gscale_of(amax) : scale * t;
+    }
 }
 
 // max |x| over a C-channel fp32 slice, OR-ed into *amax as float bits (non-negative floats order as unsigned ints)
@@ -951,16 +964,16 @@ extern "C" int esr_wgrad_set_kernel(int32_t variant) {
 extern "C" int esr_wgrad_reduce(const float *partial, int32_t splits, int64_t n, float scale, float *out,
                                 esr_stream_t stream) {
     if (!partial || !out || splits <= 0 || n <= 0) return ESR_EINVAL;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(nblocks(n)), dim3(NT), 0, (hipStream_t)stream, partial, splits, n,
-                       scale, out, nullptr);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n + RED_O - 1) / RED_O)), dim3(NT), 0,
+                       (hipStream_t)stream, partial, splits, n, scale, out, nullptr);
     return launched();
 }
 
 extern "C" int esr_wgrad_reduce_gs(const float *partial, int32_t splits, int64_t n, float scale, const uint32_t *amax,
                                    float *out, esr_stream_t stream) {
     if (!partial || !out || !amax || splits <= 0 || n <= 0) return ESR_EINVAL;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(nblocks(n)), dim3(NT), 0, (hipStream_t)stream, partial, splits, n,
-                       scale, out, amax);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n + RED_O - 1) / RED_O)), dim3(NT), 0,
+                       (hipStream_t)stream, partial, splits, n, scale, out, amax);
     return launched();
 }
 

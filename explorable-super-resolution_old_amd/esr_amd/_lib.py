@@ -60,6 +60,7 @@ _SIGNATURES = {
     'esr_conv3x3_wgrad': [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                           c_void_p, c_void_p],
     'esr_wgrad_reduce': [c_void_p, c_int, ctypes.c_int64, c_float, c_void_p, c_void_p],
+    'esr_dconv_set_x3': [c_int],
     'esr_wgrad_reduce_gs': [c_void_p, c_int, ctypes.c_int64, c_float, c_void_p, c_void_p, c_void_p],
     'esr_grad_amax': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     'esr_axpby_gs': [c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_int,

@@ -15,6 +15,7 @@ HipConv2d takes/returns NCHW tensors with NHWC storage (torch.channels_last), wh
 There is no CPU path: a CPU tensor raises.
 """
 import ctypes
+import os
 
 import torch
 import torch.nn as nn
@@ -25,6 +26,27 @@ from . import _lib
 MAX_TAPS = 64
 _WG_SPLIT_TARGET = 1024          # workgroups a weight-gradient launch aims for (split-K over pixels)
 _WG_PARTIAL_MAX = 64 << 20       # floats of split-K partials per launch
+# Precision of the gather-GEMM forward / data-gradient launches: 'x3' (default) = split-f16 operands with per-K-step
+# power-of-two scaling on f16 MFMA (fp32-level accuracy, esr_dconv.hip), 'f32' = exact fp32 MFMA.
+PRECISION = os.environ.get('ESR_DCONV_PRECISION', 'x3')
+_applied = [None]
+
+
+def set_precision(p):
+    """Select 'x3' or 'f32' for the discriminator convolutions (process-wide); returns the previous setting."""
+    global PRECISION
+    if p not in ('x3', 'f32'):
+        raise ValueError(p)
+    prev, PRECISION = PRECISION, p
+    return prev
+
+
+def _lib_for_launch():
+    lib = _lib.load()
+    if _applied[0] != PRECISION:
+        lib.esr_dconv_set_x3(1 if PRECISION == 'x3' else 0)
+        _applied[0] = PRECISION
+    return lib
 
 
 def _stream(t):
@@ -61,7 +83,7 @@ def _gather(src, wt, bias, out, MH, MW, omy, oay, omx, oax, smy, smx, offy, offx
     B, Hs, Ws, C = src.shape
     _, Ho, Wo, N = out.shape
     wp, nck, n_pad = _pack(wt, N)
-    lib = _lib.load()
+    lib = _lib_for_launch()
     _lib.check(lib.esr_dconv_fwd(src.data_ptr(), B, Hs, Ws, C, C, wp.data_ptr(), nck, n_pad,
                                  None if bias is None else bias.data_ptr(), out.data_ptr(), Ho, Wo, N, N, MH, MW,
                                  omy, oay, omx, oax, smy, smx, len(offy), _i32(offy), _i32(offx), _stream(src)),

@@ -31,10 +31,10 @@ WG_SPLITS_MAX = 128
 USE_GRAPHS = os.environ.get('ESR_TRAIN_GRAPHS', '1') != '0'
 # Weight gradients of an x3 forward (split-f16 activations) on the x3 MFMA kernel (esr_conv3x3_wgrad flag 4); 0 keeps
 # the exact-fp32 weight-gradient kernel reading the same split activations.
-WGRAD_X3 = os.environ.get('ESR_WGRAD_X3', '0') != '0'
+WGRAD_X3 = os.environ.get('ESR_WGRAD_X3', '1') != '0'
 # Data gradients inside the residual blocks on the x3 conv (split-f16 gradients scaled per RRDB, include/esr_amd.h
 # "x3 backward") when the forward ran in x3 and only parameter gradients are wanted (training); 0 keeps them fp32.
-DGRAD_X3 = os.environ.get('ESR_DGRAD_X3', '0') != '0'
+DGRAD_X3 = os.environ.get('ESR_DGRAD_X3', '1') != '0'
 
 
 def _z(dev, *s):
@@ -347,9 +347,12 @@ class _Runner:
         assert cin == bc.cin_buf
         chunks = bc.cin_pad // 32
         ntiles = self.B * ((h + 7) // 8) * ((w + 31) // 32)
-        splits = max(1, min(WG_SPLITS_MAX, -(-1024 // chunks), ntiles))
+        x3 = self.split and (WGRAD_X3 or amax is not None)
+        # split-K: the fp32 kernel at ~4 workgroups per CU; the x3 kernel (one 12-wave workgroup per CU) at ~1 — more
+        # splits only add partial traffic for the reduction (tools/wgrad_ab.py)
+        splits = max(1, min(WG_SPLITS_MAX, (256 // chunks) if x3 else -(-1024 // chunks), ntiles))
         assert splits * bc.wg_n <= self.ws.partial.numel()
-        flags = up2 | ((6 if WGRAD_X3 or amax is not None else 2) if self.split else 0) | (8 if amax is not None else 0)
+        flags = up2 | ((6 if x3 else 2) if self.split else 0) | (8 if amax is not None else 0)
         _lib.check(self.lib.esr_conv3x3_wgrad(inp.data_ptr(), in_cp, cin, flags, dout.data_ptr(), d_cp, d_coff,
                                               bc.cout, self.B, h, w, splits, self.ws.partial.data_ptr(), self.stream),
                    'wgrad')

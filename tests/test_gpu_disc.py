@@ -32,14 +32,25 @@ pytestmark = pytest.mark.gpu
     (100, 1, 1, 1, 0, 5, 7),       # 1x1 head: 100 channels in, 1 out (unaligned pitches)
     (130, 70, 4, 2, 1, 8, 9),      # partial K chunks and N blocks
 ])
-def test_dconv_ops_vs_float64(gpu_device, ci, co, k, s, p, H, W):
+@pytest.mark.parametrize('precision', ['x3', 'f32'])
+def test_dconv_ops_vs_float64(gpu_device, ci, co, k, s, p, H, W, precision):
+    prev = dconv.set_precision(precision)
+    try:
+        _dconv_ops(gpu_device, ci, co, k, s, p, H, W, scale=1e-9 if precision == 'x3' else 1.0)
+    finally:
+        dconv.set_precision(prev)
+
+
+def _dconv_ops(gpu_device, ci, co, k, s, p, H, W, scale):
+    """scale: the output gradient's magnitude (x3: ~1e-9, a realistic loss gradient far below f16's range, which the
+    per-step scaling must bring back)."""
     g = torch.Generator().manual_seed(ci * 1000 + co)
     B = 3
     x = torch.randn(B, ci, H, W, generator=g)
     w = torch.randn(co, ci, k, k, generator=g) / np.sqrt(ci * k * k)
     b = torch.randn(co, generator=g) * 0.1
     Ho, Wo = dconv.out_size(H, k, s, p), dconv.out_size(W, k, s, p)
-    gy = torch.randn(B, co, Ho, Wo, generator=g)
+    gy = torch.randn(B, co, Ho, Wo, generator=g) * scale
     nhwc = lambda t: t.permute(0, 2, 3, 1).contiguous().to(gpu_device)  # noqa: E731
     back = lambda t: t.permute(0, 3, 1, 2).double().cpu()  # noqa: E731
     wd, bd = w.to(gpu_device), b.to(gpu_device)

@@ -45,12 +45,13 @@ def main():
         chunks = (cin + 31) // 32
         ntiles = B * ((H + 7) // 8) * ((W + 31) // 32)
         splits0 = max(1, min(128, -(-1024 // chunks), ntiles))
+        splits_x3 = max(1, min(128, 256 // chunks, ntiles))
         cin_pad, cout_pad = 32 * chunks, 64 if cout > 32 else 32
         n = 9 * cin_pad * cout_pad + cout_pad
         part = torch.empty(splits0 * n, device=dev)
         flops = 2 * 9 * cin * cout * B * H * W
         variants = [('f32', 2, splits0)] + [('x3_s%d' % max(1, int(splits0 * s)), 6, max(1, int(splits0 * s)))
-                                            for s in scales]
+                                            for s in scales] + [("x3_auto", 6, splits_x3)]
 
         def run(flags, splits, reps, out=None):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
