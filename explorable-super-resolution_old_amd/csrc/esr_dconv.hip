@@ -53,6 +53,7 @@ struct FwdParams {
     int omy, oay, omx, oax, smy, smx;
     int T;
     int offy[MAXT], offx[MAXT];
+    float *partial;  // split-K (x3 kernel, gridDim.z > 1): [z][M][n_pad] raw sums, reduced by dconv_splitk_reduce
 };
 
 __device__ __forceinline__ f32x4 load4(const float *row, int c, int kc, bool vec) {
@@ -190,15 +191,18 @@ __device__ __forceinline__ int tile_exp(float m, int e_keep) {
     return 14 - ex;
 }
 
+// NBX = 64 or 128 output channels per workgroup (128: the A tile, re-gathered per tap, feeds twice the MFMAs)
+template <int NBX>
 __global__ __launch_bounds__(NTH, 2) void dconv_fwd_x3_kernel(FwdParams p) {
-    __shared__ __attribute__((aligned(16))) unsigned char lds[(MT + NB) * XP];
+    constexpr int NTN = NBX / 32, BX_IT = NBX * KC / 4 / NTH;
+    __shared__ __attribute__((aligned(16))) unsigned char lds[(MT + NBX) * XP];
     __shared__ float s_red[2][2][NTH / 64];
     unsigned char *s_a = lds, *s_b = lds + MT * XP;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hl = lane >> 5, ml = lane & 31;
     const int per_img = p.MH * p.MW;
     const long long M = (long long)p.B * per_img;
     const long long m0 = (long long)blockIdx.x * MT;
-    const int n0 = blockIdx.y * NB;
+    const int n0 = blockIdx.y * NBX;
     const int cg = tid & 7;
     const bool vec = p.vec != 0;
 
@@ -216,8 +220,11 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_x3_kernel(FwdParams p) {
             px[k] = r - py[k] * p.MW;
         }
     }
-    f32x4 ra[A_IT], rb[B_IT];
-    const int nsteps = p.T * p.nck;
+    f32x4 ra[A_IT], rb[BX_IT];
+    // split-K: workgroup z of gridDim.z takes K steps [s_begin, s_end)
+    const int nsteps_all = p.T * p.nck;
+    const int s_begin = (int)((long long)nsteps_all * blockIdx.z / gridDim.z);
+    const int s_end = (int)((long long)nsteps_all * (blockIdx.z + 1) / gridDim.z);
     auto load = [&](int step) {
         const int t = step / p.nck, j = step - t * p.nck;
         const int c = j * KC + cg * 4;
@@ -232,7 +239,7 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_x3_kernel(FwdParams p) {
         }
         const float *wj = p.w + ((long long)(t * p.nck + j) * p.n_pad + n0) * KC;
 #pragma unroll
-        for (int k = 0; k < B_IT; ++k) rb[k] = *reinterpret_cast<const f32x4 *>(wj + (tid + k * NTH) * 4);
+        for (int k = 0; k < BX_IT; ++k) rb[k] = *reinterpret_cast<const f32x4 *>(wj + (tid + k * NTH) * 4);
     };
     auto publish = [&](int slot) {
         float ma = 0.f, mb = 0.f;
@@ -241,7 +248,7 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_x3_kernel(FwdParams p) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) ma = fmaxf(ma, fabsf(ra[k][e]));
 #pragma unroll
-        for (int k = 0; k < B_IT; ++k)
+        for (int k = 0; k < BX_IT; ++k)
 #pragma unroll
             for (int e = 0; e < 4; ++e) mb = fmaxf(mb, fabsf(rb[k][e]));
 #pragma unroll
@@ -266,24 +273,26 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_x3_kernel(FwdParams p) {
         *reinterpret_cast<f16x4 *>(row + 64 + cg * 8) = l;
     };
 
-    f32x16 acc[2][2];
+    f32x16 acc[2][NTN];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
+        for (int nt = 0; nt < NTN; ++nt)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.f;
     int ea = 0, eb = 0;
 
-    load(0);
-    publish(0);
-    for (int step = 0; step < nsteps; ++step) {
+    if (s_begin < s_end) {
+        load(s_begin);
+        publish(0);
+    }
+    for (int step = s_begin; step < s_end; ++step) {
         __syncthreads();
         float ma = 0.f, mb = 0.f;
 #pragma unroll
         for (int w = 0; w < NTH / 64; ++w) {
-            ma = fmaxf(ma, s_red[step & 1][0][w]);
-            mb = fmaxf(mb, s_red[step & 1][1][w]);
+            ma = fmaxf(ma, s_red[(step - s_begin) & 1][0][w]);
+            mb = fmaxf(mb, s_red[(step - s_begin) & 1][1][w]);
         }
         const int ea2 = tile_exp(ma, ea), eb2 = tile_exp(mb, eb);
         if (ea2 + eb2 != ea + eb) {
@@ -291,7 +300,7 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_x3_kernel(FwdParams p) {
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-                for (int nt = 0; nt < 2; ++nt)
+                for (int nt = 0; nt < NTN; ++nt)
 #pragma unroll
                     for (int r = 0; r < 16; ++r) acc[mt][nt][r] = ldexpf(acc[mt][nt][r], d);
         }
@@ -301,35 +310,49 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_x3_kernel(FwdParams p) {
 #pragma unroll
         for (int k = 0; k < A_IT; ++k) put(s_a + ((tid >> 3) + 32 * k) * XP, ra[k], sa);
 #pragma unroll
-        for (int k = 0; k < B_IT; ++k) put(s_b + ((tid + k * NTH) >> 3) * XP, rb[k], sb);
+        for (int k = 0; k < BX_IT; ++k) put(s_b + ((tid + k * NTH) >> 3) * XP, rb[k], sb);
         __syncthreads();
-        if (step + 1 < nsteps) load(step + 1);
+        if (step + 1 < s_end) load(step + 1);
         const unsigned char *a0 = s_a + (64 * wave + ml) * XP + 16 * hl;
         const unsigned char *b0 = s_b + ml * XP + 16 * hl;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-            f16x8 ah[2], al[2], bh[2], bl[2];
+            f16x8 ah[2], al[2];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 ah[i] = *reinterpret_cast<const f16x8 *>(a0 + i * 32 * XP + 32 * s);
                 al[i] = *reinterpret_cast<const f16x8 *>(a0 + i * 32 * XP + 64 + 32 * s);
-                bh[i] = *reinterpret_cast<const f16x8 *>(b0 + i * 32 * XP + 32 * s);
-                bl[i] = *reinterpret_cast<const f16x8 *>(b0 + i * 32 * XP + 64 + 32 * s);
             }
+#pragma unroll
+            for (int nt = 0; nt < NTN; ++nt) {
+                const f16x8 bh = *reinterpret_cast<const f16x8 *>(b0 + nt * 32 * XP + 32 * s);
+                const f16x8 bl = *reinterpret_cast<const f16x8 *>(b0 + nt * 32 * XP + 64 + 32 * s);
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt) {
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[mt], bh, acc[mt][nt], 0, 0, 0);
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mt], bl, acc[mt][nt], 0, 0, 0);
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mt], bh, acc[mt][nt], 0, 0, 0);
+                }
+            }
+        }
+        if (step + 1 < s_end) publish((step + 1 - s_begin) & 1);
+    }
+
+    if (gridDim.z > 1) {  // raw partial sums, pixel-linear; bias and the output map are the reduction's
+        float *part = p.partial + (long long)blockIdx.z * M * p.n_pad;
+#pragma unroll
+        for (int nt = 0; nt < NTN; ++nt)
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-                for (int nt = 0; nt < 2; ++nt) {
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[mt], bh[nt], acc[mt][nt], 0, 0, 0);
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mt], bl[nt], acc[mt][nt], 0, 0, 0);
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mt], bh[nt], acc[mt][nt], 0, 0, 0);
+                for (int r = 0; r < 16; ++r) {
+                    const long long m = m0 + 64 * wave + 32 * mt + (r & 3) + 8 * (r >> 2) + 4 * hl;
+                    if (m < M) part[m * p.n_pad + n0 + nt * 32 + ml] = ldexpf(acc[mt][nt][r], -(ea + eb));
                 }
-        }
-        if (step + 1 < nsteps) publish((step + 1) & 1);
+        return;
     }
-
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
+    for (int nt = 0; nt < NTN; ++nt) {
         const int n = n0 + nt * 32 + ml;
         if (n >= p.n) continue;
         const float bn = p.bias ? p.bias[n] : 0.f;
@@ -345,6 +368,22 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_x3_kernel(FwdParams p) {
                 p.out[(((long long)b * p.Ho + oy) * p.Wo + ox) * p.op + n] = ldexpf(acc[mt][nt][r], -(ea + eb)) + bn;
             }
     }
+}
+
+// out[map(m)][n] = bias[n] + Σ_z partial[z][m][n], z in order (deterministic)
+__global__ void dconv_splitk_reduce(FwdParams p, int ksplit) {
+    const long long M = (long long)p.B * p.MH * p.MW;
+    const long long i = (long long)blockIdx.x * NTH + threadIdx.x;
+    if (i >= M * p.n) return;
+    const long long m = i / p.n;
+    const int n = (int)(i - m * p.n);
+    float v = 0.f;
+    for (int z = 0; z < ksplit; ++z) v += p.partial[((long long)z * M + m) * p.n_pad + n];
+    const int per_img = p.MH * p.MW;
+    const int b = (int)(m / per_img), rr = (int)(m - (long long)b * per_img);
+    const int Y = rr / p.MW, X = rr - Y * p.MW;
+    const int oy = p.omy * Y + p.oay, ox = p.omx * X + p.oax;
+    p.out[(((long long)b * p.Ho + oy) * p.Wo + ox) * p.op + n] = v + (p.bias ? p.bias[n] : 0.f);
 }
 
 // ---- weight gradient ------------------------------------------------------------------------------------------------
@@ -440,14 +479,17 @@ bool aligned16(const void *ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15)
 
 }  // namespace
 
-int g_dconv_x3 = 0;  // esr_dconv_set_x3
+int g_dconv_x3 = 0;   // esr_dconv_set_x3
+int g_dconv_nb = 128; // x3: widest N tile allowed (esr_dconv_set_x3(2) = 64 only, for A/B)
 
-extern "C" int esr_dconv_fwd(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t src_pitch, int32_t kc,
-                             const float *w_packed, int32_t nck, int32_t n_pad, const float *bias, float *out,
-                             int32_t Ho, int32_t Wo, int32_t out_pitch, int32_t n, int32_t MH, int32_t MW, int32_t omy,
-                             int32_t oay, int32_t omx, int32_t oax, int32_t smy, int32_t smx, int32_t T,
-                             const int32_t *offy, const int32_t *offx, esr_stream_t stream) {
+extern "C" int esr_dconv_fwd_sk(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t src_pitch, int32_t kc,
+                                const float *w_packed, int32_t nck, int32_t n_pad, const float *bias, float *out,
+                                int32_t Ho, int32_t Wo, int32_t out_pitch, int32_t n, int32_t MH, int32_t MW,
+                                int32_t omy, int32_t oay, int32_t omx, int32_t oax, int32_t smy, int32_t smx, int32_t T,
+                                const int32_t *offy, const int32_t *offx, int32_t ksplit, float *partial,
+                                esr_stream_t stream) {
     if (!src || !w_packed || !out || !offy || !offx) return ESR_EINVAL;
+    if (ksplit < 1 || (ksplit > 1 && (!partial || !g_dconv_x3 || ksplit > T * nck))) return ESR_EINVAL;
     if (B <= 0 || Hs <= 0 || Ws <= 0 || kc <= 0 || src_pitch < kc || n <= 0 || out_pitch < n || MH <= 0 || MW <= 0)
         return ESR_EINVAL;
     if (T <= 0 || T > ESR_DCONV_MAX_TAPS || nck != (kc + KC - 1) / KC || n_pad % NB || n_pad < n) return ESR_EINVAL;
@@ -462,21 +504,41 @@ extern "C" int esr_dconv_fwd(const float *src, int32_t B, int32_t Hs, int32_t Ws
     p.MH = MH; p.MW = MW; p.omy = omy; p.oay = oay; p.omx = omx; p.oax = oax; p.smy = smy; p.smx = smx;
     p.T = T;
     for (int t = 0; t < T; ++t) { p.offy[t] = offy[t]; p.offx[t] = offx[t]; }
+    p.partial = partial;
     const long long M = (long long)B * MH * MW;
     const long long gx = (M + MT - 1) / MT;
     if (gx > 0x7fffffff) return ESR_EINVAL;
     const dim3 grid((unsigned)gx, (unsigned)((n + NB - 1) / NB)), block(NTH);
-    if (g_dconv_x3)
-        hipLaunchKernelGGL(dconv_fwd_x3_kernel, grid, block, 0, (hipStream_t)stream, p);
+    // 128-channel N tiles only where the grid still fills the chip (the A tile then feeds twice the MFMAs)
+    const bool wide = n_pad % 128 == 0 && g_dconv_nb != 64 && gx * (n_pad / 128) * ksplit >= 512;
+    if (g_dconv_x3 && wide)
+        hipLaunchKernelGGL(dconv_fwd_x3_kernel<128>, dim3((unsigned)gx, (unsigned)(n_pad / 128), (unsigned)ksplit),
+                           block, 0, (hipStream_t)stream, p);
+    else if (g_dconv_x3)
+        hipLaunchKernelGGL(dconv_fwd_x3_kernel<64>, dim3((unsigned)gx, (unsigned)(n_pad / 64), (unsigned)ksplit),
+                           block, 0, (hipStream_t)stream, p);
     else
         hipLaunchKernelGGL(dconv_fwd_kernel, grid, block, 0, (hipStream_t)stream, p);
+    if (ksplit > 1)
+        hipLaunchKernelGGL(dconv_splitk_reduce, dim3((unsigned)((M * n + NTH - 1) / NTH)), block, 0,
+                           (hipStream_t)stream, p, ksplit);
     return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
 }
 
+extern "C" int esr_dconv_fwd(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t src_pitch, int32_t kc,
+                             const float *w_packed, int32_t nck, int32_t n_pad, const float *bias, float *out,
+                             int32_t Ho, int32_t Wo, int32_t out_pitch, int32_t n, int32_t MH, int32_t MW, int32_t omy,
+                             int32_t oay, int32_t omx, int32_t oax, int32_t smy, int32_t smx, int32_t T,
+                             const int32_t *offy, const int32_t *offx, esr_stream_t stream) {
+    return esr_dconv_fwd_sk(src, B, Hs, Ws, src_pitch, kc, w_packed, nck, n_pad, bias, out, Ho, Wo, out_pitch, n, MH,
+                            MW, omy, oay, omx, oax, smy, smx, T, offy, offx, 1, nullptr, stream);
+}
+
 extern "C" int esr_dconv_set_x3(int32_t on) {
-    if (on < 0 || on > 1) return ESR_EINVAL;
-    const int prev = g_dconv_x3;
-    g_dconv_x3 = on;
+    if (on < 0 || on > 2) return ESR_EINVAL;
+    const int prev = g_dconv_x3 ? (g_dconv_nb == 64 ? 2 : 1) : 0;
+    g_dconv_x3 = on != 0;
+    g_dconv_nb = on == 2 ? 64 : 128;
     return prev;
 }
 

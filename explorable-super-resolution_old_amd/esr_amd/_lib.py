@@ -79,6 +79,9 @@ _SIGNATURES = {
     'esr_dconv_fwd': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
                       c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                       ctypes.POINTER(c_int), ctypes.POINTER(c_int), c_void_p],
+    'esr_dconv_fwd_sk': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                         c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                         ctypes.POINTER(c_int), ctypes.POINTER(c_int), c_int, c_void_p, c_void_p],
     'esr_dconv_wgrad': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int,
                         c_int, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int), c_int, c_void_p, c_void_p],
     'esr_timer_create': [c_int],

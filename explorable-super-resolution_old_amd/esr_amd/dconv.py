@@ -84,9 +84,18 @@ def _gather(src, wt, bias, out, MH, MW, omy, oay, omx, oax, smy, smx, offy, offx
     _, Ho, Wo, N = out.shape
     wp, nck, n_pad = _pack(wt, N)
     lib = _lib_for_launch()
-    _lib.check(lib.esr_dconv_fwd(src.data_ptr(), B, Hs, Ws, C, C, wp.data_ptr(), nck, n_pad,
-                                 None if bias is None else bias.data_ptr(), out.data_ptr(), Ho, Wo, N, N, MH, MW,
-                                 omy, oay, omx, oax, smy, smx, len(offy), _i32(offy), _i32(offx), _stream(src)),
+    # split-K (x3) where the grid would fill few CUs and K is long (the 8x8 pseudo-FC layer): ~512 workgroups,
+    # at least 8 K steps per slice
+    wgs = -(-B * MH * MW // 256) * (n_pad // 64)
+    nsteps = len(offy) * nck
+    ks = 1
+    if PRECISION == 'x3' and wgs < 512 and nsteps >= 16:
+        ks = max(1, min(-(-512 // wgs), nsteps // 8))
+    part = torch.empty(ks * B * MH * MW * n_pad, device=src.device) if ks > 1 else None
+    _lib.check(lib.esr_dconv_fwd_sk(src.data_ptr(), B, Hs, Ws, C, C, wp.data_ptr(), nck, n_pad,
+                                    None if bias is None else bias.data_ptr(), out.data_ptr(), Ho, Wo, N, N, MH, MW,
+                                    omy, oay, omx, oax, smy, smx, len(offy), _i32(offy), _i32(offx), ks,
+                                    None if part is None else part.data_ptr(), _stream(src)),
                'esr_dconv_fwd')
 
 

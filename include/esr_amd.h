@@ -255,10 +255,20 @@ int esr_dconv_fwd(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t s
                   int32_t Wo, int32_t out_pitch, int32_t n_out, int32_t MH, int32_t MW, int32_t omy, int32_t oay,
                   int32_t omx, int32_t oax, int32_t smy, int32_t smx, int32_t T, const int32_t *offy,
                   const int32_t *offx, esr_stream_t stream);
+/* esr_dconv_fwd with split-K over ksplit workgroup slices of the K steps (x3 precision only; for the small-M,
+ * long-K launches — the 8×8 pseudo-FC layer — that would fill few CUs): partial = caller buffer of
+ * ksplit·MH·MW·B·n_pad floats; a second kernel sums the slices in order (deterministic) and applies bias and the
+ * output map.  ksplit = 1 is esr_dconv_fwd. */
+int esr_dconv_fwd_sk(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t src_pitch, int32_t kc,
+                     const float *w_packed, int32_t nck, int32_t n_pad, const float *bias, float *out, int32_t Ho,
+                     int32_t Wo, int32_t out_pitch, int32_t n, int32_t MH, int32_t MW, int32_t omy, int32_t oay,
+                     int32_t omx, int32_t oax, int32_t smy, int32_t smx, int32_t T, const int32_t *offy,
+                     const int32_t *offx, int32_t ksplit, float *partial, esr_stream_t stream);
 /* Precision of esr_dconv_fwd (process-wide): 0 (the library default) = exact fp32 MFMA; 1 = x3: both operands split
  * into f16 hi/lo at staging after a power-of-two scaling per K step (one tap × 32 channels) chosen from the
  * workgroup's max |a| and max |b|, products hi·hi + hi·lo + lo·hi on f16 MFMA, the fp32 accumulators rescaled exactly
- * when the step's scale changes.  Returns the previous setting, or ESR_EINVAL. */
+ * when the step's scale changes; 128 output channels per workgroup where n_pad % 128 == 0, else 64 (2 = x3 with
+ * 64-channel tiles only, for A/B; identical results).  Returns the previous setting, or ESR_EINVAL. */
 int esr_dconv_set_x3(int32_t on);
 /* esr_dconv_wgrad: weight gradient of the forward conv above (src = its input, dy = dL/dout on the MH x MW grid):
  *   partial[s][t][ci][co] = sum over the pixels of split s of src[b, smy*Y+offy[t], smx*X+offx[t], ci] * dy[b, Y, X, co]

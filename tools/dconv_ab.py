@@ -1,0 +1,65 @@
+"""A/B timing of the discriminator gather-GEMM forward (esr_dconv_fwd) on the config-3 layer shapes (B=16, D input
+304², Discriminator_VGG_128_ nb=6): exact fp32, x3 with 64-channel N tiles, x3 with 128 (default).  Order-balanced
+(two rounds, the second reported); µs per launch, TFLOP/s, and the x3 results' normwise difference from fp32.
+
+    python tools/dconv_ab.py
+"""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', 'explorable-super-resolution_old_amd'))
+from esr_amd import _lib, dconv  # noqa: E402
+
+LAYERS = [  # name, ci, co, k, s, p, H
+    ('conv0_im2col', 32, 64, 1, 1, 0, 304),
+    ('conv0_1', 64, 64, 4, 2, 1, 304),
+    ('conv1_0', 64, 128, 3, 1, 1, 152),
+    ('conv1_1', 128, 128, 4, 2, 1, 152),
+    ('conv2_0', 128, 256, 3, 1, 1, 76),
+    ('conv2_1', 256, 256, 4, 2, 1, 76),
+    ('fc8', 256, 100, 8, 1, 0, 38),
+]
+
+
+def main():
+    lib = _lib.load()
+    dev = torch.device('cuda')
+    B = 16
+    for name, ci, co, k, s, p, H in LAYERS:
+        x = torch.randn(B, H, H, ci, device=dev)
+        w = torch.randn(co, ci, k, k, device=dev) / (ci * k * k) ** 0.5
+        b = torch.randn(co, device=dev) * 0.1
+        Ho = dconv.out_size(H, k, s, p)
+        flops = 2 * B * Ho * Ho * co * ci * k * k
+        row, outs = {}, {}
+        for rnd in range(2):
+            for tag, mode in (('f32', 0), ('x3_n64', 2), ('x3_n128', 1)):
+                dconv.set_precision('f32' if mode == 0 else 'x3')
+                dconv._applied[0] = None
+                dconv._lib_for_launch()
+                lib.esr_dconv_set_x3(mode)
+                for _ in range(2):
+                    dconv.conv_forward(x, w, b, k, s, p)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(10):
+                    y = dconv.conv_forward(x, w, b, k, s, p)
+                e1.record()
+                torch.cuda.synchronize()
+                us = e0.elapsed_time(e1) * 100
+                outs[tag] = y
+                if rnd:
+                    row[tag + '_us'] = round(us, 1)
+                    row[tag + '_tflops'] = round(flops / us / 1e6, 1)
+        for tag in ('x3_n64', 'x3_n128'):
+            row[tag + '_diff'] = float((outs[tag] - outs['f32']).norm() / outs['f32'].norm())
+        print(name, json.dumps(row), flush=True)
+    lib.esr_dconv_set_x3(0)
+    dconv._applied[0] = None
+
+
+if __name__ == '__main__':
+    main()
