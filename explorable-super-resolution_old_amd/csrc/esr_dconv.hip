@@ -32,6 +32,15 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+__device__ __forceinline__ s16x4 tr_read(const unsigned char *lds, int byte_off) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(lds + byte_off));
+}
+__device__ __forceinline__ f16x8 cat8(s16x4 a, s16x4 b) {
+    return __builtin_bit_cast(f16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
 constexpr int NTH = 256;
 constexpr int MT = 256;                  // pixels per workgroup
 constexpr int NB = 64;                   // output channels per workgroup
@@ -475,6 +484,220 @@ __global__ __launch_bounds__(NTH, 2) void dconv_wgrad_kernel(WgradParams p) {
     }
 }
 
+// ---- x3 weight gradient ----------------------------------------------------------------------------------------------
+// dconv_wgrad's GEMM (M = input channels, N = output channels, K = pixels) on v_mfma_f32_32x32x16_f16 in the split
+// scheme, operands split at staging after a per-K-step (64 pixels) power-of-two scaling of each (as
+// dconv_fwd_x3_kernel).  Workgroup tile CIB × COB channels (64 or 128 each), 4 waves in 2 × 2, each wave
+// (CIB/64) × (COB/64) 32×32 accumulators.  LDS: per pixel one row of 32-byte chunks, logical chunks [hi of channels
+// 16j..16j+15]_j then [lo ...]_j, stored at physical chunk (logical ^ 2·(row & 3)); fragments come from
+// ds_read_b64_tr_b16 (4 pixel rows × 16 channels per 16-lane group), and with the XOR the 4 rows × 2 chunks of a
+// half-wave's read cover the 64 banks once.
+template <int CIB, int COB>
+__global__ __launch_bounds__(NTH, 2) void dconv_wgrad_x3_kernel(WgradParams p) {
+    constexpr int AQ = CIB / 16, BQ = COB / 16;            // fp32 quads per thread per K step
+    constexpr int AROW = 4 * CIB, BROW = 4 * COB;           // LDS row bytes (hi + lo)
+    constexpr int MTW = CIB / 64, NTW = COB / 64;           // accumulator tiles per wave
+    __shared__ __attribute__((aligned(16))) unsigned char lds[WKP * (AROW + BROW)];
+    __shared__ float s_red[2][2][NTH / 64];
+    __shared__ long long s_tab[2][2][WKP];  // per K step: source / output-gradient element offset of each pixel row
+    unsigned char *s_a = lds, *s_b = lds + WKP * AROW;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hl = lane >> 5;
+    const int nci = (p.cin + CIB - 1) / CIB, nco = (p.cout + COB - 1) / COB;
+    int bid = blockIdx.x;
+    const int cob = bid % nco;
+    bid /= nco;
+    const int cib = bid % nci;
+    const int t = bid / nci;
+    const int split = blockIdx.y;
+    const int per_img = p.MH * p.MW;
+    const long long P = (long long)p.B * per_img;
+    const long long k0 = (long long)split * p.pix_per_split;
+    const long long k1 = min(P, k0 + p.pix_per_split);
+    const int ci0 = cib * CIB, co0 = cob * COB;
+    const int oy = p.offy[t], ox = p.offx[t];
+    const bool svec = p.svec != 0, dvec = p.dvec != 0;
+    // Pixel table: wave 0's lane r tracks pixel m = kb + r of the current K step as (b, Y, X), advancing by WKP per
+    // step without divisions, and publishes the two element offsets (-1: outside the split / the source image).
+    int tb = 0, tY = 0, tX = 0;
+    if (wave == 0) {
+        const long long m = k0 + lane;
+        tb = (int)(m / per_img);
+        const int r = (int)(m - (long long)tb * per_img);
+        tY = r / p.MW;
+        tX = r - tY * p.MW;
+    }
+    auto table = [&](long long kb, int slot) {  // wave 0 only; pixel of (tb, tY, tX) is kb + lane
+        long long ao = -1, dofs = -1;
+        if (kb + lane < k1) {
+            const int sy = p.smy * tY + oy, sx = p.smx * tX + ox;
+            if (sy >= 0 && sy < p.Hs && sx >= 0 && sx < p.Ws) ao = (((long long)tb * p.Hs + sy) * p.Ws + sx) * p.sp;
+            dofs = (((long long)tb * p.MH + tY) * p.MW + tX) * p.dp;
+        }
+        s_tab[slot][0][lane] = ao;
+        s_tab[slot][1][lane] = dofs;
+        tX += WKP;
+        while (tX >= p.MW) {
+            tX -= p.MW;
+            if (++tY == p.MH) {
+                tY = 0;
+                ++tb;
+            }
+        }
+    };
+    // staging roles: thread -> (pixel row, 4-channel quad); quads per row CIB/4 (A) and COB/4 (B)
+    f32x4 ra[AQ], rb[BQ];
+    auto load = [&](int slot) {
+#pragma unroll
+        for (int k = 0; k < AQ; ++k) {
+            const int idx = tid + k * NTH, row = idx / (CIB / 4), q4 = idx % (CIB / 4);
+            const long long ao = s_tab[slot][0][row];
+            const int ci = ci0 + 4 * q4;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (ao >= 0 && ci < p.cin) v = load4(p.src + ao, ci, p.cin, svec);
+            ra[k] = v;
+        }
+#pragma unroll
+        for (int k = 0; k < BQ; ++k) {
+            const int idx = tid + k * NTH, row = idx / (COB / 4), q4 = idx % (COB / 4);
+            const long long dofs = s_tab[slot][1][row];
+            const int co = co0 + 4 * q4;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (dofs >= 0 && co < p.cout) v = load4(p.dy + dofs, co, p.cout, dvec);
+            rb[k] = v;
+        }
+    };
+    auto publish = [&](int slot) {
+        float ma = 0.f, mb = 0.f;
+#pragma unroll
+        for (int k = 0; k < AQ; ++k)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) ma = fmaxf(ma, fabsf(ra[k][e]));
+#pragma unroll
+        for (int k = 0; k < BQ; ++k)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) mb = fmaxf(mb, fabsf(rb[k][e]));
+#pragma unroll
+        for (int s = 32; s >= 1; s >>= 1) {
+            ma = fmaxf(ma, __shfl_xor(ma, s));
+            mb = fmaxf(mb, __shfl_xor(mb, s));
+        }
+        if (lane == 0) {
+            s_red[slot][0][wave] = ma;
+            s_red[slot][1][wave] = mb;
+        }
+    };
+    // byte offset of (row, channel c (multiple of 4), lo) in an image with NCH channels
+    auto off = [](int row, int c, int lo, int nch) {
+        const int logical = lo * (nch / 16) + (c >> 4);
+        return row * 4 * nch + ((logical ^ (2 * (row & 3))) << 5) + (c & 15) * 2;
+    };
+    auto put = [&](unsigned char *img, int nch, int row, int c, f32x4 v, float s) {
+        f16x4 h, l;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float x = v[e] * s;
+            h[e] = (_Float16)x;
+            l[e] = (_Float16)(x - (float)h[e]);
+        }
+        *reinterpret_cast<f16x4 *>(img + off(row, c, 0, nch)) = h;
+        *reinterpret_cast<f16x4 *>(img + off(row, c, 1, nch)) = l;
+    };
+
+    const int wm = wave >> 1, wn = wave & 1;
+    f32x16 acc[MTW][NTW];
+#pragma unroll
+    for (int i = 0; i < MTW; ++i)
+#pragma unroll
+        for (int j = 0; j < NTW; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    int ea = 0, eb = 0;
+    // transposed-read lane roles (see wgrad3_kernel): row rq of the 4, channel block 4·(lane & 3) of the 16 of group
+    const int i16 = lane & 15, rq = i16 >> 2, grp = (lane >> 4) & 1;
+    const int cblk = 16 * grp + 4 * (i16 & 3);  // channel offset within a 32-channel tile
+
+    if (wave == 0) table(k0, 0);
+    __syncthreads();
+    if (k0 < k1) {
+        load(0);
+        publish(0);
+    }
+    for (long long kb = k0; kb < k1; kb += WKP) {
+        const int it = (int)((kb - k0) / WKP);
+        __syncthreads();
+        if (wave == 0 && kb + WKP < k1) table(kb + WKP, (it + 1) & 1);
+        float ma = 0.f, mb = 0.f;
+#pragma unroll
+        for (int w = 0; w < NTH / 64; ++w) {
+            ma = fmaxf(ma, s_red[it & 1][0][w]);
+            mb = fmaxf(mb, s_red[it & 1][1][w]);
+        }
+        const int ea2 = tile_exp(ma, ea), eb2 = tile_exp(mb, eb);
+        if (ea2 + eb2 != ea + eb) {
+            const int d = ea2 + eb2 - ea - eb;
+#pragma unroll
+            for (int i = 0; i < MTW; ++i)
+#pragma unroll
+                for (int j = 0; j < NTW; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc[i][j][r] = ldexpf(acc[i][j][r], d);
+        }
+        ea = ea2;
+        eb = eb2;
+        const float sa = ldexpf(1.f, ea), sb = ldexpf(1.f, eb);
+#pragma unroll
+        for (int k = 0; k < AQ; ++k) {
+            const int idx = tid + k * NTH;
+            put(s_a, CIB, idx / (CIB / 4), 4 * (idx % (CIB / 4)), ra[k], sa);
+        }
+#pragma unroll
+        for (int k = 0; k < BQ; ++k) {
+            const int idx = tid + k * NTH;
+            put(s_b, COB, idx / (COB / 4), 4 * (idx % (COB / 4)), rb[k], sb);
+        }
+        __syncthreads();
+        if (kb + WKP < k1) load((it + 1) & 1);
+#pragma unroll
+        for (int kq = 0; kq < WKP / 16; ++kq) {
+            const int r0 = 16 * kq + 8 * hl + rq;  // K rows (pixels) r0 and r0 + 4 of this lane's two reads
+            f16x8 bh[NTW], bl[NTW];
+#pragma unroll
+            for (int j = 0; j < NTW; ++j) {
+                const int c = 32 * (NTW * wn + j) + cblk;
+                bh[j] = cat8(tr_read(s_b, off(r0, c, 0, COB)), tr_read(s_b, off(r0 + 4, c, 0, COB)));
+                bl[j] = cat8(tr_read(s_b, off(r0, c, 1, COB)), tr_read(s_b, off(r0 + 4, c, 1, COB)));
+            }
+#pragma unroll
+            for (int i = 0; i < MTW; ++i) {
+                const int c = 32 * (MTW * wm + i) + cblk;
+                const f16x8 ah = cat8(tr_read(s_a, off(r0, c, 0, CIB)), tr_read(s_a, off(r0 + 4, c, 0, CIB)));
+                const f16x8 al = cat8(tr_read(s_a, off(r0, c, 1, CIB)), tr_read(s_a, off(r0 + 4, c, 1, CIB)));
+#pragma unroll
+                for (int j = 0; j < NTW; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[j], acc[i][j], 0, 0, 0);
+                }
+            }
+        }
+        if (kb + WKP < k1) publish((it + 1) & 1);
+    }
+    const int cin_pad = 64 * p.ci_blocks, cout_pad = 64 * p.co_blocks;
+    float *dst = p.partial + ((long long)split * p.T + t) * cin_pad * cout_pad;
+    const int ml = lane & 31;
+#pragma unroll
+    for (int i = 0; i < MTW; ++i)
+#pragma unroll
+        for (int j = 0; j < NTW; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int ci = ci0 + 32 * (MTW * wm + i) + (r & 3) + 8 * (r >> 2) + 4 * hl;
+                const int co = co0 + 32 * (NTW * wn + j) + ml;
+                if (ci < cin_pad && co < cout_pad)
+                    dst[(long long)ci * cout_pad + co] = ldexpf(acc[i][j][r], -(ea + eb));
+            }
+}
+
 bool aligned16(const void *ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; }
 
 }  // namespace
@@ -562,6 +785,17 @@ extern "C" int esr_dconv_wgrad(const float *src, int32_t B, int32_t Hs, int32_t 
     p.pix_per_split = ((P + splits - 1) / splits + WKP - 1) / WKP * WKP;
     p.partial = partial;
     for (int t = 0; t < T; ++t) { p.offy[t] = offy[t]; p.offx[t] = offx[t]; }
+    if (g_dconv_x3) {  // x3: 128-channel blocks where the padded width is a multiple of 128
+        const int cib = (64 * p.ci_blocks) % 128 == 0 ? 128 : 64, cob = (64 * p.co_blocks) % 128 == 0 ? 128 : 64;
+        const long long gx = (long long)T * ((cin + cib - 1) / cib) * ((cout + cob - 1) / cob);
+        const dim3 grid((unsigned)gx, (unsigned)splits), block(NTH);
+        const hipStream_t st = (hipStream_t)stream;
+        if (cib == 128 && cob == 128) hipLaunchKernelGGL((dconv_wgrad_x3_kernel<128, 128>), grid, block, 0, st, p);
+        else if (cib == 128) hipLaunchKernelGGL((dconv_wgrad_x3_kernel<128, 64>), grid, block, 0, st, p);
+        else if (cob == 128) hipLaunchKernelGGL((dconv_wgrad_x3_kernel<64, 128>), grid, block, 0, st, p);
+        else hipLaunchKernelGGL((dconv_wgrad_x3_kernel<64, 64>), grid, block, 0, st, p);
+        return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+    }
     const long long gx = (long long)T * p.ci_blocks * p.co_blocks;
     const dim3 grid((unsigned)gx, (unsigned)splits), block(NTH);
     hipLaunchKernelGGL(dconv_wgrad_kernel, grid, block, 0, (hipStream_t)stream, p);

@@ -149,13 +149,18 @@ def conv_wgrad(x, gy, k, s, p):
     T = k * k
     cin_pad, cout_pad = 64 * ((Ci + 63) // 64), 64 * ((Co + 63) // 64)
     n = T * cin_pad * cout_pad
-    tiles = T * (cin_pad // 64) * (cout_pad // 64)
     P = B * Ho * Wo
-    splits = max(1, min(-(-_WG_SPLIT_TARGET // tiles), -(-P // 256), _WG_PARTIAL_MAX // n))
+    if PRECISION == 'x3':  # x3 kernel: 128-channel blocks where the padded width allows, ~2 workgroups per CU
+        cib, cob = (128 if cin_pad % 128 == 0 else 64), (128 if cout_pad % 128 == 0 else 64)
+        tiles = T * (cin_pad // cib) * (cout_pad // cob)
+        splits = max(1, min(-(-512 // tiles), -(-P // 256), _WG_PARTIAL_MAX // n))
+    else:
+        tiles = T * (cin_pad // 64) * (cout_pad // 64)
+        splits = max(1, min(-(-_WG_SPLIT_TARGET // tiles), -(-P // 256), _WG_PARTIAL_MAX // n))
     partial = torch.empty(splits * n, device=x.device, dtype=torch.float32)
     red = torch.empty(n, device=x.device, dtype=torch.float32)
     taps = [(ky, kx) for ky in range(k) for kx in range(k)]
-    lib = _lib.load()
+    lib = _lib_for_launch()
     st = _stream(x)
     _lib.check(lib.esr_dconv_wgrad(x.data_ptr(), B, H, W, Ci, Ci, gy.data_ptr(), Ho, Wo, Co, Co, s, s, T,
                                    _i32([ky - p for ky, _ in taps]), _i32([kx - p for _, kx in taps]), splits,

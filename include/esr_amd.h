@@ -267,7 +267,8 @@ int esr_dconv_fwd_sk(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_
 /* Precision of esr_dconv_fwd (process-wide): 0 (the library default) = exact fp32 MFMA; 1 = x3: both operands split
  * into f16 hi/lo at staging after a power-of-two scaling per K step (one tap × 32 channels) chosen from the
  * workgroup's max |a| and max |b|, products hi·hi + hi·lo + lo·hi on f16 MFMA, the fp32 accumulators rescaled exactly
- * when the step's scale changes; 128 output channels per workgroup where n_pad % 128 == 0, else 64 (2 = x3 with
+ * when the step's scale changes (esr_dconv_wgrad likewise: per 64-pixel K step, 128-channel blocks where the padded
+ * widths allow); 128 output channels per workgroup where n_pad % 128 == 0, else 64 (2 = x3 with
  * 64-channel tiles only, for A/B; identical results).  Returns the previous setting, or ESR_EINVAL. */
 int esr_dconv_set_x3(int32_t on);
 /* esr_dconv_wgrad: weight gradient of the forward conv above (src = its input, dy = dL/dout on the MH x MW grid):

@@ -35,6 +35,7 @@ def main():
         Ho = dconv.out_size(H, k, s, p)
         flops = 2 * B * Ho * Ho * co * ci * k * k
         row, outs = {}, {}
+        gy = torch.randn(B, Ho, Ho, co, device=dev) * 1e-8
         for rnd in range(2):
             for tag, mode in (('f32', 0), ('x3_n64', 2), ('x3_n128', 1)):
                 dconv.set_precision('f32' if mode == 0 else 'x3')
@@ -50,12 +51,22 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 us = e0.elapsed_time(e1) * 100
+                dconv.conv_wgrad(x, gy, k, s, p)
+                e0.record()
+                for _ in range(10):
+                    gw = dconv.conv_wgrad(x, gy, k, s, p)
+                e1.record()
+                torch.cuda.synchronize()
+                us_w = e0.elapsed_time(e1) * 100
                 outs[tag] = y
+                outs[tag + 'w'] = gw
                 if rnd:
                     row[tag + '_us'] = round(us, 1)
                     row[tag + '_tflops'] = round(flops / us / 1e6, 1)
+                    row[tag + '_wgrad_us'] = round(us_w, 1)
         for tag in ('x3_n64', 'x3_n128'):
             row[tag + '_diff'] = float((outs[tag] - outs['f32']).norm() / outs['f32'].norm())
+            row[tag + '_wgrad_diff'] = float((outs[tag + 'w'] - outs['f32w']).norm() / outs['f32w'].norm())
         print(name, json.dumps(row), flush=True)
     lib.esr_dconv_set_x3(0)
     dconv._applied[0] = None
