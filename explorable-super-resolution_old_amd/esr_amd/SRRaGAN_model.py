@@ -31,6 +31,7 @@ import torch
 import torch.distributed as dist
 
 from . import CEMnet
+from . import engine as E
 from . import networks
 from .loss import CreateRangeLoss, GANLoss, GradientPenaltyLoss
 
@@ -376,8 +377,8 @@ class SRRaGANModel:
         if first_acc_D:
             self.cur_D_update_ratio = self._d_update_ratio(t)
         G_grads_retained = first_acc_D or self.generator_step
-        for p in self.netG.parameters():
-            if not getattr(p, '_esr_frozen', False):
+        for p in E.param_list(self.netG):
+            if not getattr(p, '_esr_frozen', False) and p.requires_grad != G_grads_retained:
                 p.requires_grad = G_grads_retained
         if self.CEM_net is not None:
             self.var_H, self.var_ref = self.CEM_net.HR_unpadder(self.var_H), self.CEM_net.HR_unpadder(self.var_ref)
@@ -464,7 +465,7 @@ class SRRaGANModel:
             if last_acc_G:
                 self._g_buckets.finish()
                 if self.latent_input is not None and self.latent_grads_multiplier != 1:  # :543-546
-                    for idx, p in zip(self.channels_idx_4_grad_amplification, self.netG.parameters()):
+                    for idx, p in zip(self.channels_idx_4_grad_amplification, E.param_list(self.netG)):
                         for c in idx:
                             p.grad[:, c, ...] *= self.latent_grads_multiplier
                 self.optimizer_G.step()

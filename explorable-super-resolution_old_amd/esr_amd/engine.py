@@ -224,7 +224,7 @@ class _Packed:
             return [0, 1, 2] + [-1] * 5 + [3 + c for c in range(n_feat)]
 
         self.net = net
-        plan = self.plan = GatherPlan(net.parameters())
+        plan = self.plan = GatherPlan(param_list(net))
         pk = lambda conv, cmap, n_pad: plan.reg(pack_conv_weight(plan.w(conv.weight), cmap, n_pad))  # noqa: E731
         m = net.model
         first_map = ([0, 1, 2] + [-1] * 5 + [3, 4, 5] + [-1] * 5) if latent else ([0, 1, 2] + [-1] * 5)
@@ -320,12 +320,33 @@ class _Packed:
                     o._x3 = None
 
 
+def param_list(m):
+    """list(m.parameters()), cached on the module: walking RRDB-23's module tree for its 702 parameters costs ~5 ms
+    of host time per call, and a training step needs the list several times.  The cache is revalidated on every
+    call (each cached (module, name) slot must still hold the same Parameter object, ~0.2 ms); adding new submodules
+    after the first call is not detected."""
+    c = m.__dict__.get('_esr_plist')
+    if c is not None:
+        slots, plist = c
+        if all(mod._parameters.get(n) is q for (mod, n), q in zip(slots, plist)):
+            return plist
+    slots, plist, seen = [], [], set()
+    for mod in m.modules():
+        for n, q in mod._parameters.items():
+            if q is not None and id(q) not in seen:
+                seen.add(id(q))
+                slots.append((mod, n))
+                plist.append(q)
+    m.__dict__['_esr_plist'] = (slots, plist)
+    return plist
+
+
 def _param_key(net):
-    return tuple((p.data_ptr(), p._version) for p in net.parameters())
+    return tuple((p.data_ptr(), p._version) for p in param_list(net))
 
 
 def _struct_key(net):
-    return tuple((p.data_ptr(), tuple(p.shape)) for p in net.parameters())
+    return tuple((p.data_ptr(), p.shape) for p in param_list(net))
 
 
 def _packed(net, latent):
@@ -535,7 +556,7 @@ def generator_forward(net, x, cem=None):
     """RRDBNet.forward, optionally wrapped by CEM_PyTorch.forward (cem = the CEM_PyTorch module)."""
     global OVERFLOW_RERUNS
     _require_device(x, 'generator input')
-    if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in net.parameters())):
+    if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in param_list(net))):
         # training step / Z optimisation: retained activations + HIP backward (exact fp32)
         from . import train_engine
         return train_engine.generator_forward_train(net, x.contiguous(), cem)

@@ -166,7 +166,7 @@ class _BwdPacked:
             return list(range(n)) if not latent else [0, 1, 2] + [-1] * 5 + [3 + c for c in range(n)]
         m = net.model
         zc = 8 if latent else 0
-        plan = self.plan = E.GatherPlan(net.parameters(), scales=(1.0, 0.2))
+        plan = self.plan = E.GatherPlan(E.param_list(net), scales=(1.0, 0.2))
         first_map = ([0, 1, 2] + [-1] * 5 + [3, 4, 5] + [-1] * 5) if latent else ([0, 1, 2] + [-1] * 5)
         self.first = _BwdConv(plan, m[0], first_map, dgrad_from=len(first_map), in_width=len(first_map))
         self.rdb, self.rdb_fused = [], []
@@ -647,5 +647,5 @@ class _GeneratorFn(torch.autograd.Function):
 
 
 def generator_forward_train(net, x, cem):
-    params = [p for p in net.parameters()]
+    params = E.param_list(net)
     return _GeneratorFn.apply(x, net, cem, *params)

@@ -11,8 +11,9 @@ the scale of a series that is a difference of D outputs (D_logits_diff, l_d_real
 or not) is the norm of the D outputs it is formed from, not of the difference itself.  Projections of the parameter
 updates on a random direction additionally allow 5 % of their norm: near-zero gradient components flip the sign of
 their first Adam updates (±lr each) under any rounding change; the reference's own float32 run is already 1-2 % off
-there, while a wrong learning rate, step count, accumulation or gating moves them by O(1).  Both generator precisions
-(x3 forward, exact fp32 forward; the backward is fp32 in both) are held to it."""
+there, while a wrong learning rate, step count, accumulation or gating moves them by O(1).  Both step precisions
+are held to it: 'x3' (the default: generator forward and backward and every discriminator convolution in the split-f16
+scheme) and 'f32' (all exact fp32)."""
 import json
 import os
 import sys
@@ -46,7 +47,7 @@ def _close(mine, f32, f64, scale=None, rel=0.0):
 
 
 def _run_port(cfg, precision, dev):
-    from esr_amd import engine
+    from esr_amd import dconv, engine
     from esr_amd.SRRaGAN_model import SRRaGANModel
     torch.manual_seed(0)
     model = SRRaGANModel(train_opt(cfg), accumulation_steps_per_batch=cfg['acc'], device=dev)
@@ -57,6 +58,9 @@ def _run_port(cfg, precision, dev):
     model.netG.load_state_dict({k: torch.from_numpy(v) for k, v in gp.items()}, strict=False)
     model.netD.load_state_dict({k: torch.from_numpy(v) for k, v in dp.items()}, strict=False)
     engine.set_precision(model.netG, precision)
+    # the whole step in one precision: exact fp32 also for the discriminator convolutions and the generator backward
+    # (the x3 backward only runs after an x3 forward)
+    dconv.set_precision(precision)
     pts = random_points(cfg)
     model._interp_points = lambda n: torch.from_numpy(next(pts)).to(dev).view(n, 1, 1, 1)
     g0 = {k: v.detach().clone() for k, v in model.netG.named_parameters()}
@@ -74,9 +78,14 @@ def _run_port(cfg, precision, dev):
 @pytest.mark.parametrize('precision', ['x3', 'f32'])
 @pytest.mark.parametrize('name', sorted(TRAIN_CFGS))
 def test_optimize_parameters_vs_reference_loop(gpu_device, name, precision):
+    from esr_amd import dconv
     d = np.load(os.path.join(HERE, 'golden', 'train_%s.npz' % name))
     cfg = json.loads(str(d['cfg']))
-    model, g0, d0, flags = _run_port(cfg, precision, gpu_device)
+    prev = dconv.PRECISION
+    try:
+        model, g0, d0, flags = _run_port(cfg, precision, gpu_device)
+    finally:
+        dconv.set_precision(prev)
     assert flags == list(d['f64_generator_step']) == list(d['f32_generator_step'])
     fails = []
     for f in [f for f in d.files if f.startswith('f64_log:')]:
