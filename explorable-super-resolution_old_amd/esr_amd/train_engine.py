@@ -75,6 +75,7 @@ class TrainWorkspace:
         self.dZl = _z(dev, B, H + 2, W + 2, 8)
         self.dFirst = _z(dev, B, H + 2, W + 2, self.first_cp)
         self.dZh = _z(dev, B, 4 * H + 2, 4 * W + 2, 8) if latent else None
+        self.dzs = _z(dev, B, H + 2, W + 2, 8) if latent else None  # x3 backward: split latent-slot gradient
         self.gamax = torch.zeros(nb, device=dev, dtype=torch.int32)  # per-RRDB max |gradient| bits (x3 backward)
         self.bwd_overflow = torch.zeros(1, device=dev, dtype=torch.int32)
         self.wg_n_max = 9 * 224 * 64 + 64
@@ -387,9 +388,11 @@ class _Runner:
                                       self.stream), 'axpby')
 
 
-def _rdb_backward_x3(R, P, dcat, convs, fx3, zc, cp, H, W, dx, amax):
+def _rdb_backward_x3(R, P, dcat, convs, fx3, zc, cp, H, W, dx, amax, z_first=False):
     """_rdb_backward with the concat-gradient buffers in the split-f16 layout at gradient scale S(amax): the fused
-    data-gradient convs on the x3 conv, the weight gradients on the x3 kernel reading the split gradients."""
+    data-gradient convs on the x3 conv, the weight gradients on the x3 kernel reading the split gradients.  The latent
+    slot's gradient (Z optimisation) is summed over the RRDB's three blocks in the split scratch ws.dzs (z_first: this
+    block starts the sum)."""
     dcp = R.ws.dcp
     d4 = zc + 192
     R.wgrad(convs[4], P, cp, zc + 192, 0, dcat, dcp, d4, H, W, scale=0.2, amax=amax)
@@ -397,6 +400,9 @@ def _rdb_backward_x3(R, P, dcat, convs, fx3, zc, cp, H, W, dx, amax):
         s_in, t = zc + 64 + 32 * m, zc + 64 + 32 * (m - 1)
         R.dgrad_x3(fx3['m%d' % m], dcat, dcp, s_in, zc + 256 - s_in, H, W, dcat, dcp, t, 32, mask=(P, cp, t))
         R.wgrad(convs[m - 1], P, cp, t, 0, dcat, dcp, t, H, W, amax=amax)
+    if R.need_input and zc:
+        R.dgrad_x3(fx3['z'], dcat, dcp, zc + 64, 192, H, W, R.ws.dzs, 8, 0, zc,
+                   res=None if z_first else (R.ws.dzs, 8, 0))
     R.dgrad_x3(fx3['x'], dcat, dcp, zc + 64, 192, H, W, dx[0], dx[1], dx[2], 64, res=(dcat, dcp, d4))
 
 
@@ -428,7 +434,7 @@ def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_in
     R = _Runner(ws, bp, stream, need_params, need_input, split)
     lib = R.lib
     if x3:
-        assert split and need_params and not need_input
+        assert split and (need_params or need_input)
         fx3, bad = bp.x3_fused()
         ws.gamax.zero_()
         ws.bwd_overflow.copy_(bad)
@@ -504,9 +510,12 @@ def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_in
                                         0, 64, Bn, H, W, amax, ovf, stream), 'axpby_gs')
             for j, (dc, dn) in zip((2, 1, 0), ((D0, D1), (D1, D0), (D0, D1))):
                 _rdb_backward_x3(R, Q[3 * k + j], dc, bp.rdb[3 * k + j], R.x3[0][3 * k + j], zc, cp, H, W,
-                                 (dn, dcp, d4), amax)
+                                 (dn, dcp, d4), amax, z_first=j == 2)
             _lib.check(lib.esr_axpby_gs(ws.GA.data_ptr(), 64, 0, 0, 1.0, ws.GA.data_ptr(), 64, 0, 0, 1.0,
                                         D1.data_ptr(), dcp, d4, 1, 64, Bn, H, W, amax, ovf, stream), 'axpby_gs')
+            if need_input and zc:  # latent-slot gradient of this RRDB's blocks, back to fp32
+                _lib.check(lib.esr_axpby_gs(ws.dZl.data_ptr(), 8, 0, 0, 1.0, ws.dZl.data_ptr(), 8, 0, 0, 1.0,
+                                            ws.dzs.data_ptr(), 8, 0, 1, 8, Bn, H, W, amax, ovf, stream), 'axpby_gs')
             continue
         R.axpby(D0, dcp, d4, 0.2, ws.GA, 64, 0, C=64, h=H, w=W)
         for j, (dc, dn) in zip((2, 1, 0), ((D0, D1), (D1, D0), (D0, D1))):
@@ -620,7 +629,7 @@ class _GeneratorFn(torch.autograd.Function):
         if ctx.ws.owner() is not ctx.owner:  # cannot happen through _train_workspace; guards direct workspace reuse
             raise RuntimeError('esr_amd: the saved activations of this forward were overwritten by a later forward')
         bp = _bwd_packed(ctx.net, ctx.latent)  # parameter repack, outside any graph
-        x3 = DGRAD_X3 and ctx.split and need_params and not need_input
+        x3 = DGRAD_X3 and ctx.split and (need_params or need_input)
         if x3:
             bp.x3_fused()  # x3 repack of the data-gradient weights, outside any graph
 
