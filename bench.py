@@ -54,6 +54,7 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--precision', choices=['x3', 'f32'], default='x3')
     ap.add_argument('--cpu-images', type=int, default=8, help='images in the bounded CPU-baseline sample')
+    ap.add_argument('--no-cpu-variants', action='store_true', help='skip the latent Z=0 / Z~U[-1,1] CPU baselines')
     ap.add_argument('--no-legs', action='store_true', help='skip the extra legs (exact-fp32 C2, C3/C4 training step, '
                     'C5 Z-optimisation iteration)')
     ap.add_argument('--leg-steps', type=int, default=3)
@@ -118,6 +119,41 @@ def cpu_baseline(args, model, x_gpu, out_gpu):
                        '(oneDNN) restatement oracle/esr_oracle.py, %d threads' % (n, threads)},
             {'normwise_rel_err_vs_cpu_ref': err, 'psnr_vs_ref_db': (10 * np.log10(1.0 / mse)) if mse > 0 else None,
              'images_compared': n})
+
+
+def cpu_baseline_variants(args):
+    """BASELINE.md's CPU-baseline protocol for the other config-1 variants: latent RRDB-23 (all_layers,
+    HR_downscaled, 3 channels) + CEM on one 128² LR image with Z = 0 and with Z ~ U[-1, 1] per HR pixel, 1 warm-up then
+    the median of 3 runs, same threads as cpu_baseline.  The oracle with freshly initialised latent weights (the
+    plain variant is cpu_baseline itself)."""
+    import copy
+    from oracle import esr_oracle as O
+    a = copy.copy(args)
+    a.variant = 'latent'
+    model = build_model(a, torch.device('cpu'))
+    sd = {k: v.detach().float() for k, v in model.state_dict().items()}
+    P = O.strip_prefix({k: v for k, v in sd.items() if 'Filter' not in k})
+    design = None if args.no_cem else O.cem_design(4)
+    h = args.lr_size
+    g = torch.Generator().manual_seed(7)
+    lr = torch.rand(1, 3, h, h, generator=g)
+    out = {}
+    for tag, z in (('latent_z0', torch.zeros(1, 3, 4 * h, 4 * h)),
+                   ('latent_zuniform', 2 * torch.rand(1, 3, 4 * h, 4 * h, generator=g) - 1)):
+        x = torch.cat([z.reshape(1, 48, h, h), lr], 1)  # raw HR view, SRRaGAN_model.py:252
+        ts = []
+        with torch.no_grad():
+            for r in range(4):
+                t0 = time.perf_counter()
+                O.sr_forward(x, P, args.nb, True, design, pre_pad=design is not None)
+                if r:
+                    ts.append(time.perf_counter() - t0)
+        t = sorted(ts)[1]
+        out[tag] = {'value': round((4 * h) ** 2 / t / 1e6, 4), 'unit': 'HR Mpixels/s', 's_per_image': round(t, 3)}
+    out['protocol'] = ('config 1: 1 image %dx%d LR -> %dx%d, RRDB-%d latent%s (eval), 1 warm-up + median of 3, '
+                       '%d threads, oracle/esr_oracle.py' % (h, h, 4 * h, 4 * h, args.nb, '' if args.no_cem else ' + CEM',
+                                                             torch.get_num_threads()))
+    return out
 
 
 def pmc_traffic(kernel_tag):
@@ -282,6 +318,8 @@ def main():
         rec['roofline']['traffic_source'] = traffic[1]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb, parity = cpu_baseline(args, model, x, out)
+        if not args.no_cpu_variants:
+            cb['variants'] = cpu_baseline_variants(args)
         rec['cpu_baseline'] = cb
         rec['parity'] = parity
     if not args.no_legs:
