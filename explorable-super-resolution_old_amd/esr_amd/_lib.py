@@ -61,6 +61,14 @@ _SIGNATURES = {
                           c_void_p, c_void_p],
     'esr_wgrad_reduce': [c_void_p, c_int, ctypes.c_int64, c_float, c_void_p, c_void_p],
     'esr_dconv_set_x3': [c_int],
+    'esr_bn_workspace_floats': [ctypes.c_int64, c_int],
+    'esr_bn_lrelu_fwd': [c_void_p, ctypes.c_int64, c_int, c_void_p, c_void_p, c_float, c_float, c_void_p, c_void_p,
+                         c_void_p, c_void_p, c_void_p, c_void_p],
+    'esr_bn_lrelu_bwd': [c_void_p, c_void_p, ctypes.c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
+                         c_void_p, c_void_p, c_void_p, c_void_p],
+    'esr_bn_lrelu_bwd2': [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int64, c_int, c_void_p,
+                          c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                          c_void_p],
     'esr_wgrad_reduce_gs': [c_void_p, c_int, ctypes.c_int64, c_float, c_void_p, c_void_p, c_void_p],
     'esr_grad_amax': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     'esr_axpby_gs': [c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_int,
@@ -91,7 +99,7 @@ _SIGNATURES = {
     'esr_op_size': [],
     'esr_abi_version': [],
 }
-_RESTYPES = {'esr_timer_create': c_void_p, 'esr_timer_destroy': None}
+_RESTYPES = {'esr_timer_create': c_void_p, 'esr_timer_destroy': None, 'esr_bn_workspace_floats': ctypes.c_int64}
 EXPORTED = tuple(_SIGNATURES)
 
 _lib = None

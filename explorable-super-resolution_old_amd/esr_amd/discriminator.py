@@ -9,11 +9,18 @@ same state_dict keys and order as the reference (tests/golden/disc_*.npz).
 Every convolution (3×3 s1, 4×4 s2, the 8×8 "pseudo-FC" and the 1×1 head) is a HipConv2d: forward, data gradient
 and weight gradient on the exact-fp32 MFMA gather-GEMM kernels of csrc/esr_dconv.hip, differentiable to any order, so
 the D step and the WGAN-GP double backward (loss.py:244-263) run every convolution on HIP.  BatchNorm and LeakyReLU
-stay PyTorch elementwise ops on the channels-last activations the convolutions produce.
+run fused on HIP in training mode (esr_amd/bn.py: forward, backward, double backward); in eval mode they are
+PyTorch ops on the channels-last activations the convolutions produce.
 """
+import os
+
 import torch.nn as nn
 
+from .bn import bn_lrelu
 from .dconv import HipConv2d
+
+# BatchNorm + LeakyReLU pairs fused on HIP in training mode (esr_amd/bn.py); ESR_FUSED_BN=0 keeps PyTorch's ops
+FUSED_BN = os.environ.get('ESR_FUSED_BN', '1') != '0'
 
 LRELU = 0.2
 
@@ -56,4 +63,23 @@ class Discriminator_VGG_128_(nn.Module):
                                         nn.Sequential(*_conv_block(min(100, nfeat), 1, 1)))
 
     def forward(self, x):
-        return self.classifier(self.features(x))
+        return _run(self.classifier, _run(self.features, x))
+
+
+def _run(seq, x):
+    """seq(x), with every training-mode BatchNorm2d -> LeakyReLU pair (conv_block's norm + act) run as the fused HIP
+    layer of bn.py (forward, backward and double backward); nested Sequentials are walked the same way."""
+    mods = list(seq.children())
+    i = 0
+    while i < len(mods):
+        m = mods[i]
+        nxt = mods[i + 1] if i + 1 < len(mods) else None
+        if isinstance(m, nn.Sequential):
+            x = _run(m, x)
+        elif FUSED_BN and isinstance(m, nn.BatchNorm2d) and m.training and isinstance(nxt, nn.LeakyReLU) and x.is_cuda:
+            x = bn_lrelu(x, m, nxt.negative_slope)
+            i += 1
+        else:
+            x = m(x)
+        i += 1
+    return x

@@ -319,6 +319,24 @@ void esr_timer_destroy(esr_timer_t timer);
 int esr_run_ops(const esr_op *ops, int32_t n, esr_timer_t timer, esr_stream_t stream);
 int esr_op_size(void);                                  /* sizeof(esr_op), checked by the binding */
 
+/* ---- discriminator BatchNorm2d (training) + LeakyReLU (esr_bn.hip) ------------------------------------------------
+ * conv_block(CNA)'s norm + act (block.py:129-156) fused on channels-last activations x [P][C] (P = B·H·W):
+ *   μ, v = batch mean / biased variance per channel, r = 1/sqrt(v + eps), y = lrelu_slope(γ·(x − μ)·r + β).
+ * esr_bn_lrelu_fwd writes y and the per-channel mu, rs (= r) and var (the caller updates the running buffers).
+ * esr_bn_lrelu_bwd: gx = ∂L/∂x for upstream gy, and sums2 = [Σ gz ; Σ gz·x̂] (= dβ ; dγ), gz = gy·lrelu'.
+ * esr_bn_lrelu_bwd2: the backward of (x, γ, gy) -> (gx, dγ, dβ) (the WGAN-GP double backward, loss.py:244-263) for
+ * upstream u = ∂/∂gx, ggg = ∂/∂dγ, ggb = ∂/∂dβ (each may be NULL = 0): g_x, g_gy and g_gamma (formulas in
+ * esr_bn.hip's header).  ws = scratch of esr_bn_workspace_floats(P, C) floats.  Deterministic (fixed-order sums). */
+int64_t esr_bn_workspace_floats(int64_t P, int32_t C);
+int esr_bn_lrelu_fwd(const float *x, int64_t P, int32_t C, const float *gamma, const float *beta, float eps,
+                     float slope, float *y, float *mu, float *rs, float *var, float *ws, esr_stream_t stream);
+int esr_bn_lrelu_bwd(const float *x, const float *gy, int64_t P, int32_t C, const float *gamma, const float *beta,
+                     const float *mu, const float *rs, float slope, float *gx, float *sums2, float *ws,
+                     esr_stream_t stream);
+int esr_bn_lrelu_bwd2(const float *x, const float *gy, const float *u, const float *ggg, const float *ggb, int64_t P,
+                      int32_t C, const float *gamma, const float *beta, const float *mu, const float *rs, float slope,
+                      const float *sums2, float *g_x, float *g_gy, float *g_gamma, float *ws, esr_stream_t stream);
+
 /* Library / ABI version (bumped on any signature change). */
 int esr_abi_version(void);
 

@@ -158,3 +158,43 @@ def test_discriminator_d_step_vs_float64_oracle(gpu_device):
     worst32 = max(e_32.values())
     bad = {k: (e_hip[k], e_32[k]) for k in e_hip if e_hip[k] > max(1e-4, 10 * e_32[k], 2 * worst32)}
     assert not bad, bad
+
+
+@pytest.mark.parametrize('C,B,H,W', [(64, 2, 9, 11), (100, 3, 5, 4), (1, 4, 6, 6), (300, 2, 3, 5)])
+def test_fused_bn_lrelu_vs_float64(gpu_device, C, B, H, W):
+    """esr_amd/bn.py (csrc/esr_bn.hip) against nn.BatchNorm2d + LeakyReLU(0.2) in float64 on the CPU: output, running
+    buffers, first-order gradients (x, γ, β) and the second-order gradients the WGAN-GP penalty takes (x, γ, and the
+    upstream gradient), for random upstream and second-order weights."""
+    from esr_amd.bn import bn_lrelu
+    g = torch.Generator().manual_seed(C * 31 + B)
+    x = torch.randn(B, C, H, W, generator=g) * 3 + 0.5
+    bn = torch.nn.BatchNorm2d(C)
+    with torch.no_grad():
+        bn.weight.copy_(torch.randn(C, generator=g))
+        bn.bias.copy_(torch.randn(C, generator=g) * 0.5)
+        bn.running_var.uniform_(0.5, 2.0)
+    gy = torch.randn(B, C, H, W, generator=g)
+    r1, r2, r3 = torch.randn(B, C, H, W, generator=g), torch.randn(C, generator=g), torch.randn(C, generator=g)
+    bn64 = torch.nn.BatchNorm2d(C).double()
+    bn64.load_state_dict({k: v.double() if v.is_floating_point() else v for k, v in bn.state_dict().items()})
+    bng = torch.nn.BatchNorm2d(C).to(gpu_device)
+    bng.load_state_dict(bn.state_dict())
+
+    def grads(run, xx, bnm, gyy, rr):
+        xx = xx.clone().requires_grad_(True)
+        gyy = gyy.clone().requires_grad_(True)
+        y = run(xx, bnm)
+        gx, gw, gb = torch.autograd.grad(y, (xx, bnm.weight, bnm.bias), gyy, create_graph=True)
+        s = (gx * rr[0]).sum() + (gw * rr[1]).sum() + (gb * rr[2]).sum()
+        hx, hw, hy = torch.autograd.grad(s, (xx, bnm.weight, gyy))
+        return y.detach(), gx.detach(), gw.detach(), gb.detach(), hx, hw, hy
+
+    ref = grads(lambda t, m: F.leaky_relu(m(t), 0.2), x.double(), bn64, gy.double(), [t.double() for t in (r1, r2, r3)])
+    dev = lambda t: t.to(gpu_device).contiguous(memory_format=torch.channels_last) if t.dim() == 4 else t.to(gpu_device)  # noqa: E731
+    got = grads(lambda t, m: bn_lrelu(t, m, 0.2), dev(x), bng, dev(gy), [dev(t) for t in (r1, r2, r3)])
+    names = ('y', 'dx', 'dgamma', 'dbeta', 'd2x', 'd2gamma', 'd2gy')
+    for n, a, b in zip(names, got, ref):
+        assert normwise_rel(a.double().cpu(), b) < 1e-5, (n, normwise_rel(a.double().cpu(), b))
+    assert normwise_rel(bng.running_mean.double().cpu(), bn64.running_mean) < 1e-6
+    assert normwise_rel(bng.running_var.double().cpu(), bn64.running_var) < 1e-6
+    assert int(bng.num_batches_tracked) == int(bn64.num_batches_tracked) == 1

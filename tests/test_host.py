@@ -113,7 +113,7 @@ def test_upconv_polyphase_fold_equals_nearest_then_conv():
 
 def test_library_exports_every_header_symbol():
     hdr = open(os.path.join(REPO, 'include', 'esr_amd.h')).read()
-    declared = sorted(set(re.findall(r'^(?:int|void|esr_timer_t)\s+(esr_\w+)\s*\(', hdr, flags=re.M)))
+    declared = sorted(set(re.findall(r'^(?:int|int64_t|void|esr_timer_t)\s+(esr_\w+)\s*\(', hdr, flags=re.M)))
     assert declared and set(declared) == set(_lib.EXPORTED)
     lib = ctypes.CDLL(_lib.LIB_PATH)
     for s in declared:
