@@ -84,10 +84,12 @@ def run(args, dev, world, rank):
     fwd = getattr(model.netG.module if hasattr(model.netG, 'module') else model.netG, 'generated_image_model',
                   None)
     fwd = getattr(fwd, 'esr_precision', engine.DEFAULT_PRECISION) if fwd is not None else engine.DEFAULT_PRECISION
+    from esr_amd import dconv, train_engine
+    bwd = 'x3' if fwd == 'x3' and train_engine.DGRAD_X3 and train_engine.WGRAD_X3 else 'f32'
     return {'metric': 'training HR Mpixels/s (RRDB-23 + CEM G fwd+bwd, VGG128_ D + WGAN-GP, Adam)',
             'value': round(value, 4), 'unit': 'HR Mpixels/s', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(dt / args.steps * 1e3, 2), 'higher_is_better': True,
-            'scaling': 'weak', 'dtype': 'f32', 'fwd_dtype': fwd, 'bwd_dtype': 'f32', 'data': 'synthetic',
+            'scaling': 'weak', 'dtype': 'f32', 'fwd_dtype': fwd, 'bwd_dtype': bwd, 'd_dtype': dconv.PRECISION, 'data': 'synthetic',
             'generator_steps_in_timed_region': gsteps,
             'config': {'workload': 'BASELINE config %s: batch %d/GPU of %dx%d LR crops (%dx%d HR, D on %dx%d after '
                                    'CEM unpad), nb=%d, latent=%s' % ('4' if world > 1 else '3', args.batch,

@@ -80,12 +80,14 @@ def run(args, dev, world, rank):
     m = int(cem.margins_LR)
     flop_iter = 2 * 2 * 18316944 * (h + 2 * m) ** 2 * B  # fwd + input dgrad, SURVEY.md §8(d) latent MAC/LR-px
     fwd = getattr(cem.generated_image_model, 'esr_precision', engine.DEFAULT_PRECISION)
+    from esr_amd import train_engine
+    bwd = 'x3' if fwd == 'x3' and train_engine.DGRAD_X3 else 'f32'
     return {'metric': 'Z-optimisation HR Mpixels/s per iteration (latent RRDB-23 + learned-kernel CEM, fwd + dZ + '
                       'Adam)',
             'value': round(world * B * (4 * h) ** 2 * args.steps / dt / 1e6, 4), 'unit': 'HR Mpixels/s',
             'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
             'ms_per_step': round(dt / args.steps * 1e3, 2), 'higher_is_better': True, 'scaling': 'weak',
-            'dtype': 'f32', 'fwd_dtype': fwd, 'bwd_dtype': 'f32', 'data': 'synthetic',
+            'dtype': 'f32', 'fwd_dtype': fwd, 'bwd_dtype': bwd, 'data': 'synthetic',
             'achieved_TFLOPs': round(flop_iter * args.steps / dt / 1e12, 2),
             'config': {'workload': 'BASELINE config 5: batch %d/GPU of %dx%d LR, learned 13x13 kernel (CEM margins '
                                    '%d/%d, G at %dx%d), objective %s, nb=%d' % (B, h, h, m, 4 * m, h + 2 * m,

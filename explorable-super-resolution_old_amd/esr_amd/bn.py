@@ -92,3 +92,42 @@ def bn_lrelu(x, bn, slope):
             bn.running_mean.mul_(1 - m).add_(mu, alpha=m)
             bn.running_var.mul_(1 - m).add_(var, alpha=m * n / max(n - 1, 1))
     return y.view(B, H, W, C).permute(0, 3, 1, 2)
+
+
+class _LReLUFn(torch.autograd.Function):
+    """LeakyReLU on a contiguous channels-last tensor, out of place (y saved; its sign is the mask)."""
+
+    @staticmethod
+    def forward(ctx, x, slope):
+        y = torch.where(x > 0, x, x * slope)
+        ctx.save_for_backward(y)
+        ctx.slope = slope
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (y,) = ctx.saved_tensors
+        return _LReLUBwdFn.apply(g.contiguous(), y, ctx.slope), None
+
+
+class _LReLUBwdFn(torch.autograd.Function):
+    """g -> g·lrelu'(y): linear in g (its own backward applies the same mask); the mask has zero derivative."""
+
+    @staticmethod
+    def forward(ctx, g, y, slope):
+        ctx.save_for_backward(y)
+        ctx.slope = slope
+        return torch.where(y > 0, g, g * slope)
+
+    @staticmethod
+    def backward(ctx, gg):
+        (y,) = ctx.saved_tensors
+        return _LReLUBwdFn.apply(gg.contiguous(), y, ctx.slope), None, None
+
+
+def lrelu_nhwc(x, slope):
+    """nn.LeakyReLU(slope) (in-place or not: same values) on an NCHW tensor with channels-last storage, computed out of
+    place on the contiguous NHWC storage.  The discriminator's in-place LeakyReLU on such a view made autograd clone and
+    re-copy the 64-channel 304² activation of its first conv about 30 times per training step."""
+    y = _LReLUFn.apply(x.permute(0, 2, 3, 1), slope)
+    return y.permute(0, 3, 1, 2)

@@ -16,7 +16,7 @@ import os
 
 import torch.nn as nn
 
-from .bn import bn_lrelu
+from .bn import bn_lrelu, lrelu_nhwc
 from .dconv import HipConv2d
 
 # BatchNorm + LeakyReLU pairs fused on HIP in training mode (esr_amd/bn.py); ESR_FUSED_BN=0 keeps PyTorch's ops
@@ -68,7 +68,8 @@ class Discriminator_VGG_128_(nn.Module):
 
 def _run(seq, x):
     """seq(x), with every training-mode BatchNorm2d -> LeakyReLU pair (conv_block's norm + act) run as the fused HIP
-    layer of bn.py (forward, backward and double backward); nested Sequentials are walked the same way."""
+    layer of bn.py (forward, backward and double backward) and the other LeakyReLUs out of place on the channels-last
+    storage (bn.lrelu_nhwc); nested Sequentials are walked the same way."""
     mods = list(seq.children())
     i = 0
     while i < len(mods):
@@ -79,6 +80,9 @@ def _run(seq, x):
         elif FUSED_BN and isinstance(m, nn.BatchNorm2d) and m.training and isinstance(nxt, nn.LeakyReLU) and x.is_cuda:
             x = bn_lrelu(x, m, nxt.negative_slope)
             i += 1
+        elif FUSED_BN and isinstance(m, nn.LeakyReLU) and x.is_cuda and \
+                x.permute(0, 2, 3, 1).is_contiguous():  # a LeakyReLU without norm in front (conv0, classifier)
+            x = lrelu_nhwc(x, m.negative_slope)
         else:
             x = m(x)
         i += 1

@@ -198,3 +198,24 @@ def test_fused_bn_lrelu_vs_float64(gpu_device, C, B, H, W):
     assert normwise_rel(bng.running_mean.double().cpu(), bn64.running_mean) < 1e-6
     assert normwise_rel(bng.running_var.double().cpu(), bn64.running_var) < 1e-6
     assert int(bng.num_batches_tracked) == int(bn64.num_batches_tracked) == 1
+
+
+def test_lrelu_nhwc_second_order(gpu_device):
+    """bn.lrelu_nhwc (the discriminator's LeakyReLUs without a norm in front) against F.leaky_relu in float64:
+    output, gradient and the gradient's own gradient (w.r.t. the upstream gradient)."""
+    from esr_amd.bn import lrelu_nhwc
+    g = torch.Generator().manual_seed(5)
+    x, gy, r = (torch.randn(2, 16, 7, 9, generator=g) for _ in range(3))
+
+    def run(fn, xx, gyy, rr):
+        xx, gyy = xx.clone().requires_grad_(True), gyy.clone().requires_grad_(True)
+        y = fn(xx)
+        (gx,) = torch.autograd.grad(y, xx, gyy, create_graph=True)
+        (hy,) = torch.autograd.grad((gx * rr).sum(), gyy)
+        return y.detach(), gx.detach(), hy
+
+    ref = run(lambda t: F.leaky_relu(t, 0.2), x.double(), gy.double(), r.double())
+    cl = lambda t: t.to(gpu_device).contiguous(memory_format=torch.channels_last)  # noqa: E731
+    got = run(lambda t: lrelu_nhwc(t, 0.2), cl(x), cl(gy), cl(r))
+    for a, b in zip(got, ref):
+        assert normwise_rel(a.double().cpu(), b) < 1e-7
