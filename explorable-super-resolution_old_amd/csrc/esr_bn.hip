@@ -60,6 +60,7 @@ __global__ __launch_bounds__(NT) void bn_colsum(BnP p, float *partial) {
 #pragma unroll
         for (int k = 0; k < K; ++k) s[k] = 0.f;
         if (act) {
+#pragma unroll 4
             for (long long r = r0 + ph; r < r1; r += rpi) {
                 const long long i = r * C + c;
                 const float x = p.x[i];
@@ -101,14 +102,26 @@ __global__ __launch_bounds__(NT) void bn_colsum(BnP p, float *partial) {
     }
 }
 
-// out[k][c] = Σ_b partial[b][k][c] (blocks in order)
+// out[k][c] = Σ_b partial[b][k][c]: workgroup = 32 consecutive (k, c) outputs × 8 slices of the blocks, each slice
+// summed in block order, then the slices in slice order (fixed order: deterministic)
 __global__ void bn_finish(const float *partial, int nblk, int K, int C, float *out) {
-    const int i = blockIdx.x * NT + threadIdx.x;
-    if (i >= K * C) return;
-    const int k = i / C, c = i - k * C;
+    __shared__ float sl[8][32];
+    const int o = threadIdx.x & 31, q = threadIdx.x >> 5;
+    const int i = blockIdx.x * 32 + o;
+    const int b0 = nblk * q / 8, b1 = nblk * (q + 1) / 8;
     float v = 0.f;
-    for (int b = 0; b < nblk; ++b) v += partial[((long long)b * K + k) * C + c];
-    out[i] = v;
+    if (i < K * C) {
+        const int k = i / C, c = i - k * C;
+#pragma unroll 4
+        for (int b = b0; b < b1; ++b) v += partial[((long long)b * K + k) * C + c];
+    }
+    sl[q][o] = v;
+    __syncthreads();
+    if (q == 0 && i < K * C) {
+        float t = sl[0][o];
+        for (int r = 1; r < 8; ++r) t += sl[r][o];
+        out[i] = t;
+    }
 }
 
 // mean / invstd from the sums: mode 0 -> mu = s/N; mode 1 -> rs = 1/sqrt(s/N + eps) (and var = s/N)
@@ -172,14 +185,14 @@ __global__ void bn_ggamma(const float *sums, const float *rs, int C, long long P
 
 inline int launched() { return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH; }
 inline unsigned grid_of(long long n) { return (unsigned)((n + NT - 1) / NT); }
-inline int nblocks_for(long long P) { return (int)(P / 512 < 1 ? 1 : (P / 512 > MAXB ? MAXB : P / 512)); }
+inline int nblocks_for(long long P) { return (int)(P / 256 < 1 ? 1 : (P / 256 > MAXB ? MAXB : P / 256)); }
 
 template <int MODE>
 int colsum(const BnP &p, float *partial, float *out, hipStream_t st) {
     constexpr int K = MODE == 3 ? 3 : (MODE == 2 ? 2 : 1);
     const int nb = nblocks_for(p.P);
     hipLaunchKernelGGL(bn_colsum<MODE>, dim3(nb), dim3(NT), 0, st, p, partial);
-    hipLaunchKernelGGL(bn_finish, dim3(grid_of((long long)K * p.C)), dim3(NT), 0, st, partial, nb, K, p.C, out);
+    hipLaunchKernelGGL(bn_finish, dim3((unsigned)((K * p.C + 31) / 32)), dim3(NT), 0, st, partial, nb, K, p.C, out);
     return launched();
 }
 
