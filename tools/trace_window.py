@@ -1,6 +1,7 @@
 """Per-kernel time inside the last part of a rocprofv3 kernel trace (the timed steps of a bench run).
 
-    python tools/trace_window.py TRACE.csv START_MS [STEPS]   (START_MS from the trace's first kernel)
+    python tools/trace_window.py TRACE.csv START_MS [STEPS]   (START_MS from the trace's first kernel; a negative
+                                                              value -X takes the trace's last X ms)
 """
 import csv
 import sys
@@ -11,6 +12,9 @@ start = float(sys.argv[2])
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 ev = sorted((int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Kernel_Name'], r['LDS_Block_Size']) for r in rows)
 t0 = ev[0][0]
+if start < 0:
+    t0 = max(e[1] for e in ev) + start * 1e6
+    start = 0.0
 ev = [e for e in ev if (e[0] - t0) / 1e6 >= start]
 span = (max(e[1] for e in ev) - ev[0][0]) / 1e6
 busy, end = 0, 0
