@@ -19,6 +19,9 @@ import bench_train  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--min-numel', type=int, default=4_000_000)
+    ap.add_argument('--host', action='store_true', help='print the ops by self CPU time instead')
+    ap.add_argument('--syncs', action='store_true', help='count the Python call sites of tensor -> host scalar '
+                    'conversions (item / float / int / bool / iteration) in one step')
     a = ap.parse_args()
     from esr_amd.SRRaGAN_model import SRRaGANModel
     args = bench_train.leg_args()
@@ -33,10 +36,35 @@ def main():
         model.feed_data(data)
         model.optimize_parameters()
     torch.cuda.synchronize()
+    if a.syncs:
+        import collections
+        import traceback
+        cnt = collections.Counter()
+
+        def wrap(name):
+            orig = getattr(torch.Tensor, name)
+
+            def f(self, *args, **kw):
+                if self.is_cuda:
+                    cnt[(name, ''.join(traceback.format_stack(limit=5)[:-1]))] += 1
+                return orig(self, *args, **kw)
+            setattr(torch.Tensor, name, f)
+        for name in ('item', '__float__', '__int__', '__bool__', '__iter__', 'tolist', '__index__'):
+            wrap(name)
+        model.feed_data(data)
+        model.optimize_parameters()
+        torch.cuda.synchronize()
+        for (name, st), n in cnt.most_common(12):
+            print('%5d x %s\n%s' % (n, name, st), flush=True)
+        return
     with profile(activities=[ProfilerActivity.CPU], record_shapes=True, with_stack=True) as prof:
         model.feed_data(data)
         model.optimize_parameters()
         torch.cuda.synchronize()
+    if a.host:
+        print(prof.key_averages().table(sort_by='self_cpu_time_total', row_limit=40), flush=True)
+        print(prof.key_averages(group_by_stack_n=3).table(sort_by='self_cpu_time_total', row_limit=25), flush=True)
+        return
     for ev in prof.events():
         if ev.name not in ('aten::copy_', 'aten::leaky_relu_backward', 'aten::add', 'aten::add_', 'aten::contiguous',
                            'aten::clone', 'aten::leaky_relu', 'aten::mul', 'aten::sub'):
