@@ -153,6 +153,92 @@ __global__ __launch_bounds__(256) void cem_down_tiled(const float *__restrict__ 
     r[idx] = negate ? -out : out;
 }
 
+// Down, register-window form (sf = 4): a 32×16 block of LR outputs of one plane stages its replicate-clamped HR window
+// (77 × 141 values for kd = 17) in LDS de-interleaved by column phase x mod 4, rows padded to P ≡ 8 (mod 16) words.
+// Thread (tx, ty) owns the 4 consecutive outputs j0 + 4 tx + e of row i0 + ty: for every tap row u it reads the 8
+// values [4 tx, 4 tx + 8) of each phase row with two ds_read_b128 (conflict-free: 8 lanes cover 128 B of one row, the
+// next row group starts 32 banks later), i.e. 8 LDS reads per tap row for 4·kd FMAs, and the weights are wave-uniform
+// scalar loads.  Per output the taps are summed u-major, v ascending — the order of cem_down_tiled: bitwise equal.
+constexpr int DW_TX = 8, DW_TY = 16;  // 32 × 16 LR outputs, 128 threads
+// The window is staged from the 16-B-aligned column Xa = X0 & ~3 (O = X0 - Xa, a template parameter) with 16-B loads
+// (per-element clamped loads only where a 16-B group crosses the image border), all of a thread's loads in flight
+// before its LDS stores.
+template <int KD, int O>
+__global__ __launch_bounds__(128) void cem_down_win4(const float *__restrict__ gen, const float *__restrict__ lr,
+                                                     float *__restrict__ r, int H, int W, int ph,
+                                                     const float *__restrict__ wd, int negate) {
+    constexpr int sf = 4, kd = KD;
+    static_assert(KD + O <= 20, "8-value windows cover taps v + O < 20");
+    constexpr int WR = (DW_TY - 1) * sf + kd;             // window rows
+    constexpr int WC4 = ((4 * DW_TX - 1) * sf + kd + O + 3) / 4;  // 16-B column groups from Xa
+    constexpr int P = ((WC4 + 7) & ~15) + 8;              // >= WC4, ≡ 8 (mod 16) words
+    constexpr int NL = (WR * WC4 + 127) / 128;            // 16-B loads per thread
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int j0 = blockIdx.x * 4 * DW_TX, i0 = blockIdx.y * DW_TY;
+    const long long plane = blockIdx.z;
+    const int HH = sf * H, WW = sf * W, pd = kd / 2;
+    const float *g = gen + plane * HH * WW;
+    const int Y0 = sf * i0 + ph - pd, Xa = sf * j0 + ph - pd - O;
+    float4 v[NL];
+#pragma unroll
+    for (int n = 0; n < NL; ++n) {
+        const int k = threadIdx.x + 128 * n, y = k / WC4, c = k - y * WC4;
+        if (y < WR) {
+            const float *grow = g + (long long)clampi(Y0 + y, 0, HH - 1) * WW;
+            const int x = Xa + 4 * c;
+            if (x >= 0 && x + 3 < WW) {
+                v[n] = *reinterpret_cast<const float4 *>(grow + x);
+            } else {
+                v[n].x = grow[clampi(x, 0, WW - 1)];
+                v[n].y = grow[clampi(x + 1, 0, WW - 1)];
+                v[n].z = grow[clampi(x + 2, 0, WW - 1)];
+                v[n].w = grow[clampi(x + 3, 0, WW - 1)];
+            }
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < NL; ++n) {
+        const int k = threadIdx.x + 128 * n, y = k / WC4, c = k - y * WC4;
+        if (y < WR) {
+            smem[(0 * WR + y) * P + c] = v[n].x;
+            smem[(1 * WR + y) * P + c] = v[n].y;
+            smem[(2 * WR + y) * P + c] = v[n].z;
+            smem[(3 * WR + y) * P + c] = v[n].w;
+        }
+    }
+    __syncthreads();
+    const int tx = threadIdx.x % DW_TX, ty = threadIdx.x / DW_TX;
+    const int i = i0 + ty, j = j0 + 4 * tx;
+    if (i >= H || j >= W) return;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < kd; ++u) {
+        float win[4][8];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float4 *src = reinterpret_cast<const float4 *>(smem + (q * WR + sf * ty + u) * P + 4 * tx);
+            const float4 a = src[0], b = src[1];
+            win[q][0] = a.x; win[q][1] = a.y; win[q][2] = a.z; win[q][3] = a.w;
+            win[q][4] = b.x; win[q][5] = b.y; win[q][6] = b.z; win[q][7] = b.w;
+        }
+        const float *wr = wd + u * kd;  // wave-uniform: scalar loads
+#pragma unroll
+        for (int vv = 0; vv < kd; ++vv) {
+            const float w = wr[vv];
+            constexpr int dummy = 0;
+            (void)dummy;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[e] += w * win[(vv + O) & 3][e + ((vv + O) >> 2)];
+        }
+    }
+    const long long idx = (plane * H + i) * W + j;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        if (j + e >= W) break;
+        const float out = (lr ? lr[idx + e] : 0.f) - acc[e];
+        r[idx + e] = negate ? -out : out;
+    }
+}
+
 // Up + back-projection + crop, for stride phases whose clamped border rows/columns are not stuffed rows
 // (0 < ph < sf-1: replicate padding of the zero-stuffed grid then reads zeros): only the ≈(kd/sf)² taps that land on
 // stuffed samples are visited, with no modulo in the tap loops.
@@ -412,7 +498,7 @@ __global__ __launch_bounds__(NT) void prep_hr_kernel(PrepParams p) {
 }
 
 inline unsigned nblocks(long long n) { return (unsigned)((n + NT - 1) / NT); }
-int g_cem_direct = 0;  // esr_cem_set_direct: 1 = the untiled inverse / up-add kernels
+int g_cem_direct = 0;  // esr_cem_set_direct: 1 = the untiled inverse / up-add kernels and the LDS-tiled down kernel
 inline int launched() { return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH; }
 
 }  // namespace
@@ -424,7 +510,21 @@ extern "C" int esr_cem_down(const float *gen, const float *lr, float *r, int32_t
         return ESR_EINVAL;
     const int WH = 15 * sf + kd, P = (WH + sf - 1) / sf + 1;
     const size_t lds = 4 * (((kd * kd + 3) & ~3) + (size_t)sf * WH * P);
-    if (sf == 4 && lds <= 64 * 1024) {
+    if (sf == 4 && kd == 17 && !g_cem_direct) {
+        constexpr int WR = (DW_TY - 1) * 4 + 17;
+        const dim3 grid((W + 4 * DW_TX - 1) / (4 * DW_TX), (H + DW_TY - 1) / DW_TY, B * 3);
+        const int o = ((ph - kd / 2) % 4 + 4) % 4;  // X0 mod 4 (X0 = 4 j0 + ph - kd/2)
+#define DW(O_) { constexpr int WC4 = ((4 * DW_TX - 1) * 4 + 17 + O_ + 3) / 4, PW = ((WC4 + 7) & ~15) + 8; \
+            hipLaunchKernelGGL((cem_down_win4<17, O_>), grid, dim3(128), (size_t)4 * 4 * WR * PW, (hipStream_t)stream, \
+                               gen, lr, r, H, W, ph, w_down, negate); }
+        switch (o) {
+        case 0: DW(0) break;
+        case 1: DW(1) break;
+        case 2: DW(2) break;
+        default: DW(3)
+        }
+#undef DW
+    } else if (sf == 4 && lds <= 64 * 1024) {
         hipLaunchKernelGGL(cem_down_tiled<4>, dim3((W + 15) / 16, (H + 15) / 16, B * 3), dim3(256), lds,
                            (hipStream_t)stream, gen, lr, r, H, W, ph, w_down, kd, negate);
     } else {

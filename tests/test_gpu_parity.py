@@ -486,17 +486,25 @@ def test_upconv2x_phases_x3(gpu_device, H, W, variant):
 def test_cem_tiled_stencils_bitwise_equal_direct(gpu_device, B, H, W, ki, kd, M):
     """The LDS-tiled inverse-filter and up-add kernels (default) against the direct kernels (esr_cem_set_direct(1)):
     same taps in the same order per output, so bit for bit — at the config-2 shape (B=32, 148² LR) and at ragged
-    shapes (tiles past the image edge, windows clamped on every side) — and against float64."""
+    shapes (tiles past the image edge, windows clamped on every side) — and against float64.  The register-window down
+    kernel (default at sf 4, kd 17) against the LDS-tiled one (direct mode) within rounding, and against float64."""
     lib = _lib.load()
     g = torch.Generator().manual_seed(61)
     r = torch.randn(B, 3, H, W, generator=g).to(gpu_device)
     wi = (torch.randn(ki, ki, generator=g) * 0.05).to(gpu_device)
     wu = (torch.randn(kd, kd, generator=g) * 0.1).to(gpu_device)
     gen = torch.randn(B, 3, 4 * H, 4 * W, generator=g).to(gpu_device)
-    res = {}
+    lr = torch.randn(B, 3, H, W, generator=g).to(gpu_device)
+    res, downs = {}, {}
     try:
         for direct in (1, 0):
             lib.esr_cem_set_direct(direct)
+            downs[direct] = []
+            for ph in (1, 2):
+                d = torch.full((B, 3, H, W), 7.0, device=gpu_device)
+                _lib.check(lib.esr_cem_down(gen.data_ptr(), lr.data_ptr(), d.data_ptr(), B, H, W, 4, ph, wu.data_ptr(),
+                                            kd, 0, _stream()), 'down')
+                downs[direct].append(d)
             q = torch.empty_like(r)
             _lib.check(lib.esr_cem_inv(r.data_ptr(), q.data_ptr(), B, H, W, wi.data_ptr(), ki, _stream()), 'inv')
             outs = []
@@ -512,6 +520,13 @@ def test_cem_tiled_stencils_bitwise_equal_direct(gpu_device, B, H, W, ki, kd, M)
     assert torch.equal(res[0][0], res[1][0])
     for a, b in zip(res[0][1], res[1][1]):
         assert torch.equal(a, b)
+    for a, b in zip(downs[0], downs[1]):  # FMA contraction differs between the two down kernels: rounding-level
+        assert normwise_rel(a.cpu().double(), b.cpu().double()) < 1e-6
+    gd = F.conv2d(F.pad(gen.double().cpu().view(B * 3, 1, 4 * H, 4 * W), (kd // 2,) * 4, mode='replicate'),
+                  wu.double().cpu().view(1, 1, kd, kd))
+    for ph, got in zip((1, 2), downs[0]):
+        ref = lr.double().cpu().view(B * 3, 1, H, W) - gd[:, :, ph::4, ph::4]
+        assert normwise_rel(got.cpu().view_as(ref), ref) < 1e-5
     # float64: replicate-padded cross-correlation (inverse filter); zero-stuffed ×4 grid at phase ph, replicate-padded
     rd = r.double().cpu()
     ref_q = F.conv2d(F.pad(rd.view(B * 3, 1, H, W), (ki // 2,) * 4, mode='replicate'), wi.double().cpu().view(1, 1, ki, ki))
