@@ -224,8 +224,6 @@ __global__ __launch_bounds__(128) void cem_down_win4(const float *__restrict__ g
 #pragma unroll
         for (int vv = 0; vv < kd; ++vv) {
             const float w = wr[vv];
-            constexpr int dummy = 0;
-            (void)dummy;
 #pragma unroll
             for (int e = 0; e < 4; ++e) acc[e] += w * win[(vv + O) & 3][e + ((vv + O) >> 2)];
         }
@@ -413,6 +411,60 @@ __global__ __launch_bounds__(256) void cem_up_add_tiled(const float *__restrict_
     }
 }
 
+// Up + back-projection + crop, register-window form (sf 4, 16-B-aligned rows: WW, OW, M multiples of 4; interior
+// stride phases as cem_up_add_tiled).  A block covers 4 output rows × 256 columns; wave w owns row Y0 + w, so the tap
+// rows u0 + 4a of its sub-pixel row phase — and the weights they use — are wave-uniform (scalar loads).  Lane l owns
+// the 4 consecutive outputs Xb = X0 + 4 l + e: their column phases are e, so output e visits taps v = v0_e + 4 b with
+// v0_e = (C0 - e) & 3 (C0 = (kd/2 + ph) & 3, a template parameter) and reads q columns cb_0 + [e > C0] + b.  Per tap row
+// a lane reads 5 q values (consecutive lanes, consecutive words) for the ≈kd FMAs of its 4 outputs.  Taps per output
+// in the order of cem_up_add_tiled (u ascending, then v).
+template <int KD, int C0>
+__global__ __launch_bounds__(256) void cem_up_add_win4(const float *__restrict__ q, const float *__restrict__ gen,
+                                                       float *__restrict__ out, int H, int W, int ph,
+                                                       const float *__restrict__ wu, int M) {
+    constexpr int sf = 4, kd = KD, pd = KD / 2;
+    constexpr int QC = (255 + kd - 1) / sf + 3, QR = (3 + kd - 1) / sf + 3;
+    __shared__ float sq[QR * QC];
+    const int HH = sf * H, WW = sf * W, OH = HH - 2 * M, OW = WW - 2 * M;
+    const int X0 = blockIdx.x * 256, Y0 = blockIdx.y * 4;
+    const long long plane = blockIdx.z;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int qr0 = (Y0 + M - pd - ph + sf * (kd + sf)) / sf - (kd + sf) - 1;
+    const int qc0 = (X0 + M - pd - ph + sf * (kd + sf)) / sf - (kd + sf) - 1;
+    const int Y = Y0 + wave, Xb = X0 + 4 * lane;
+    float4 gv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (Y < OH && Xb < OW) gv = *reinterpret_cast<const float4 *>(gen + (plane * HH + Y + M) * WW + Xb + M);
+    const float *qp = q + plane * H * W;
+    for (int k = threadIdx.x; k < QR * QC; k += 256) {
+        const int r = k / QC, c = k - r * QC;
+        const int qr = qr0 + r, qc = qc0 + c;
+        sq[k] = (qr >= 0 && qr < H && qc >= 0 && qc < W) ? qp[(long long)qr * W + qc] : 0.f;
+    }
+    __syncthreads();
+    if (Y >= OH || Xb >= OW) return;
+    const int Yp = Y + M, Xp = Xb + M;
+    const int u0 = (pd + ph - Yp + sf * (Yp + kd)) % sf;  // wave-uniform
+    const int rb = (Yp + u0 - pd - ph + sf * (kd + sf)) / sf - (kd + sf) - qr0;
+    const int cb = (Xp + C0 - pd - ph + sf * (kd + sf)) / sf - (kd + sf) - qc0;  // output 0: v0 = C0
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int u = u0, a = 0; u < kd; u += sf, ++a) {
+        const float *qrow = sq + (rb + a) * QC + cb;
+        float qv[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) qv[k] = qrow[k];
+        const float *wr = wu + u * kd;  // wave-uniform row
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int v0 = (C0 - e) & 3, off = e > C0 ? 1 : 0;
+#pragma unroll
+            for (int b = 0; b < 5; ++b)
+                if (v0 + sf * b < kd) acc[e] += wr[v0 + sf * b] * qv[off + b];
+        }
+    }
+    *reinterpret_cast<float4 *>(out + (plane * OH + Y) * OW + Xb) =
+        make_float4(gv.x + acc[0], gv.y + acc[1], gv.z + acc[2], gv.w + acc[3]);
+}
+
 // ---- model-input preparation ----
 
 struct PrepParams {
@@ -557,7 +609,19 @@ extern "C" int esr_cem_up_add(const float *q, const float *gen, float *out, int3
         constexpr int RPT = 1;  // rows per thread: 64 x 16 outputs per block (64 x 64 measured slower)
         const int QC = (63 + kd - 1) / sf + 3, QR = (16 * RPT - 1 + kd - 1) / sf + 3;
         const size_t lds = 4 * (((kd * kd + 3) & ~3) + (size_t)QR * QC);
-        if (g_cem_direct)
+        const int c0 = (kd / 2 + ph) & 3;
+        if (!g_cem_direct && kd == 17 && (((sf * W) | (sf * W - 2 * M) | M) & 3) == 0) {
+            const dim3 grid((sf * W - 2 * M + 255) / 256, (sf * H - 2 * M + 3) / 4, B * 3);
+#define UW(C) hipLaunchKernelGGL((cem_up_add_win4<17, C>), grid, dim3(256), 0, (hipStream_t)stream, q, gen, out, H, W, \
+                                 ph, w_up, M)
+            switch (c0) {
+            case 0: UW(0); break;
+            case 1: UW(1); break;
+            case 2: UW(2); break;
+            default: UW(3);
+            }
+#undef UW
+        } else if (g_cem_direct)
             hipLaunchKernelGGL(cem_up_add_phase<4>, dim3((sf * W - 2 * M + 63) / 64, (sf * H - 2 * M + 3) / 4, B * 3),
                                dim3(256), 0, (hipStream_t)stream, q, gen, out, H, W, ph, w_up, kd, M);
         else

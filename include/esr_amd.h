@@ -116,9 +116,10 @@ int esr_cem_inv(const float *r, float *q, int32_t B, int32_t H, int32_t W, const
  * out: NCHW [B][3][sf*H-2M][sf*W-2M]; w_up = sf²·ds_kernel. */
 int esr_cem_up_add(const float *q, const float *gen, float *out, int32_t B, int32_t H, int32_t W, int32_t sf,
                    int32_t ph, const float *w_up, int32_t kd, int32_t M, esr_stream_t stream);
-/* A/B of the CEM stencil kernels (process-wide): 0 (default) = LDS-tiled inverse filter and up-add, register-window
- * down stencil (sf 4, kd 17); 1 = the direct (untiled) inverse / up-add kernels (bitwise equal) and the LDS-tiled down
- * kernel (equal to rounding: FMA contraction differs).  Returns the previous setting, or ESR_EINVAL. */
+/* A/B of the CEM stencil kernels (process-wide): 0 (default) = LDS-tiled inverse filter, register-window up-add and
+ * down stencils (sf 4, kd 17; LDS-tiled otherwise); 1 = the direct (untiled) inverse / up-add kernels (bitwise equal)
+ * and the LDS-tiled down kernel (equal to rounding: FMA contraction differs).  Returns the previous setting, or
+ * ESR_EINVAL. */
 int esr_cem_set_direct(int32_t direct);
 
 /* ---- split-precision ("x3") path --------------------------------------------------------------------------------
