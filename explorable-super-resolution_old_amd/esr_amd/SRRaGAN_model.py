@@ -33,6 +33,7 @@ import torch.distributed as dist
 from . import CEMnet
 from . import engine as E
 from . import networks
+from .flat_optim import FlatAdam
 from .loss import CreateRangeLoss, GANLoss, GradientPenaltyLoss
 
 
@@ -242,8 +243,13 @@ class SRRaGANModel:
         if self.latent_input is not None:  # SRRaGAN_model.py:79-80
             self.latent_grads_multiplier = t['lr_latent'] / t['lr_G'] if t.get('lr_latent') else 1
             self.channels_idx_4_grad_amplification = [[] for _ in self.netG.parameters()]
-        self.optimizer_G = torch.optim.Adam(gparams, lr=lr_G, weight_decay=t.get('weight_decay_G') or 0,
-                                            betas=(t['beta1_G'], 0.999))
+        # one flat buffer for all generator parameters (flat_optim.py: the reference's per-element update)
+        self.optimizer_G = FlatAdam(gparams, lr=lr_G, weight_decay=t.get('weight_decay_G') or 0,
+                                    betas=(t['beta1_G'], 0.999))
+        g = self.netG.module if isinstance(self.netG, torch.nn.DataParallel) else self.netG
+        rrdb = g.generated_image_model if self.CEM_net is not None else g
+        # the backward adds its flat gradient buffer straight into the optimiser's (single process: no bucket hooks)
+        rrdb._esr_flat_grad = self.optimizer_G if _world() == 1 else None
         self.optimizers.append(self.optimizer_G)
         if self.D_exists:
             self.netD = networks.define_D(opt, CEM=self.CEM_net).to(self.device)

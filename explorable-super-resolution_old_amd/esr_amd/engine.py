@@ -207,8 +207,22 @@ class GatherPlan:
         self._parts = None
         return views
 
+    def _flat_source(self):
+        """The FlatAdam buffer (flat_optim.py) if the parameters are exactly its consecutive views, else None."""
+        fl = getattr(self.params[0], '_esr_flat', None)
+        if fl is None or fl.numel() != self.N:
+            return None
+        base, o = fl.data_ptr(), 0
+        for p in self.params:
+            if getattr(p, '_esr_flat', None) is not fl or p.data_ptr() != base + 4 * o or not p.is_contiguous():
+                return None
+            o += p.numel()
+        return fl.detach()
+
     def refresh(self):
-        flat = torch.cat([p.detach().reshape(-1) for p in self.params])
+        flat = self._flat_source()
+        if flat is None:
+            flat = torch.cat([p.detach().reshape(-1) for p in self.params])
         ext = torch.cat([flat.new_zeros(1)] + [flat * s if s != 1.0 else flat for s in self.scales])
         torch.index_select(ext, 0, self.idx, out=self.buf)
 
@@ -342,7 +356,12 @@ def param_list(m):
 
 
 def _param_key(net):
-    return tuple((p.data_ptr(), p._version) for p in param_list(net))
+    ps = param_list(net)
+    key = tuple((p.data_ptr(), p._version) for p in ps)
+    # parameters bound to a FlatAdam buffer (flat_optim.py) change when the buffer is updated in place, which bumps
+    # the buffer's version counter, not theirs
+    fl = getattr(ps[0], '_esr_flat', None) if ps else None
+    return key + ((id(fl), fl._version),) if fl is not None else key
 
 
 def _struct_key(net):

@@ -650,7 +650,15 @@ class _GeneratorFn(torch.autograd.Function):
         if graphed:
             flat = flat.clone() if flat is not None else None
             dx = dx.clone() if dx is not None else None
-        grads = _split_grads(bp, flat) if flat is not None else {}
+        fg = getattr(ctx.net, '_esr_flat_grad', None)  # the generator's FlatAdam, when no per-parameter hooks wait
+        if flat is not None and fg is not None and all(ctx.needs_input_grad[3:]) and fg.accepts_flat_grad(bp.params):
+            # flat is laid out as the optimiser's buffer: one add instead of 702 per-parameter accumulations (the
+            # parameters' .grad are views of fg.flat.grad, so every reader sees the sum)
+            fg._sync_views()
+            fg.flat.grad.add_(flat)
+            grads = {}
+        else:
+            grads = _split_grads(bp, flat) if flat is not None else {}
         ctx.owner.done = True  # the workspace may be reused (a retained graph's second backward would then raise)
         return (dx, None, None) + tuple(grads.get(p) for p in ctx.params)
 
