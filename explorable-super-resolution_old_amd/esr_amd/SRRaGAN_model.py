@@ -327,15 +327,51 @@ class SRRaGANModel:
             self.var_ref = (data['ref'] if 'ref' in data else data['HR']).to(self.device)
 
     # ------------------------------------------------------------------------------------------------------------------
-    def _d_statistics(self, pred_real, pred_fake):
-        """Per-image D logit differences, summed over ranks (global-batch semantics of DataParallel)."""
+    def _d_statistics_t(self, pred_real, pred_fake):
+        """Per-image D logit differences, summed over ranks (global-batch semantics of DataParallel), as a device
+        tensor [mean diff, fraction correctly distinguished, mean D(real), mean D(fake)] (no host sync)."""
         diff = torch.mean(pred_real.detach() - pred_fake.detach(), dim=list(range(1, pred_real.dim())))
         s = torch.stack([diff.sum(), (diff > 0).float().sum(), torch.tensor(float(diff.numel()), device=diff.device),
                          pred_real.detach().mean(), pred_fake.detach().mean()])
         if _world() > 1:
             dist.all_reduce(s)
             s[3:] /= _world()
-        return float(s[0] / s[2]), float(s[1] / s[2]), float(s[3]), float(s[4])
+        return torch.stack([s[0] / s[2], s[1] / s[2], s[3], s[4]])
+
+    def _d_statistics(self, pred_real, pred_fake):
+        return tuple(float(v) for v in self._d_statistics_t(pred_real, pred_fake).tolist())
+
+    # ---- logged scalars: device values are read back in one copy when someone needs them ----------------------------
+    # The reference calls .item() on every logged loss right away (SRRaGAN_model.py:401-574); each call drains the GPU.
+    # Here they queue (in step order) and are copied to the host together when log_dict is read (the training loop's
+    # logging, the 'past' gate or the adaptive D_update_ratio) — same values, same order, no mid-step sync.
+    @property
+    def log_dict(self):
+        self._flush_logs()
+        return self._log_dict
+
+    @log_dict.setter
+    def log_dict(self, d):
+        self._flush_logs()
+        self._log_dict = d
+
+    def _defer(self, tensor, fn):
+        self.__dict__.setdefault('_pending_logs', []).append((tensor, fn))
+
+    def _flush_logs(self):
+        pend = self.__dict__.get('_pending_logs')
+        if not pend:
+            return
+        self._pending_logs = []
+        ts = [t.reshape(-1) for t, _ in pend if t is not None]
+        vals = torch.cat(ts).tolist() if ts else []
+        i = 0
+        for t, fn in pend:
+            if t is None:
+                fn(None)
+            else:
+                fn(vals[i:i + t.numel()])
+                i += t.numel()
 
     def _d_update_ratio(self, t):
         """SRRaGAN_model.py:314-324: the configured ratio, or (D_update_ratio <= 0) one adapted to the mean logged
@@ -419,8 +455,16 @@ class SRRaGANModel:
                 interp.requires_grad = True
                 l_d_gp = self.l_gp_w * self.cri_gp(interp, self.netD(interp))
                 l_d_total = l_d_total + l_d_gp
-            diff, correct, d_real, d_fake = self._d_statistics(pred_d_real, pred_d_fake)
-            self._d_logs.append((l_d_real.item(), l_d_fake.item(), d_real, d_fake, diff, correct))
+            # [l_d_real, l_d_fake, D_real, D_fake, D_logits_diff, Correctly_distinguished] of this micro-step
+            st = self._d_statistics_t(pred_d_real, pred_d_fake)
+            vals = torch.stack([l_d_real.detach().reshape(()), l_d_fake.detach().reshape(()), st[2], st[3], st[0], st[1]])
+            if self.D_verification == 'current':  # the gate needs this micro-step's statistics now
+                v = vals.tolist()
+                self._d_logs.append(v)
+                diff, correct = v[4], v[5]
+            else:
+                self._defer(vals, self._d_logs.append)
+                diff = correct = None
             self._gate_generator_step(t, first_acc_D, diff, correct)
             if G_grads_retained and not self.generator_step:
                 self.fake_H = self.fake_H.detach()
@@ -431,14 +475,17 @@ class SRRaGANModel:
                 self._d_buckets.finish()
                 self.optimizer_D.step()
                 _broadcast_buffers(self.netD)
-                a = np.mean(np.array(self._d_logs), axis=0)
-                g = self.gradient_step_num
-                for k, v in (('l_d_real', a[0]), ('l_d_fake', a[1]), ('l_d_real_fake', a[0] + a[1]), ('D_real', a[2]),
-                             ('D_fake', a[3]), ('D_logits_diff', a[4]), ('Correctly_distinguished', a[5]),
-                             ('D_update_ratio', self.cur_D_update_ratio)):
-                    self.log_dict[k].append((g, float(v)))
+
+                def log_d(_, rows=self._d_logs, g=self.gradient_step_num, ratio=self.cur_D_update_ratio):
+                    a = np.mean(np.array(rows), axis=0)
+                    for k, v in (('l_d_real', a[0]), ('l_d_fake', a[1]), ('l_d_real_fake', a[0] + a[1]),
+                                 ('D_real', a[2]), ('D_fake', a[3]), ('D_logits_diff', a[4]),
+                                 ('Correctly_distinguished', a[5]), ('D_update_ratio', ratio)):
+                        self._log_dict[k].append((g, float(v)))
+                self._defer(None, log_d)
                 if l_d_gp is not None:
-                    self.log_dict['l_d_gp'].append((g, l_d_gp.item()))
+                    self._defer(l_d_gp.detach().reshape(1),
+                                lambda v, g=self.gradient_step_num: self._log_dict['l_d_gp'].append((g, v[0])))
         # ---- G step ----
         if self.generator_step:
             if self.D_exists:
@@ -465,9 +512,9 @@ class SRRaGANModel:
                 self._g_buckets.arm()
             l_g_total.backward()
             if self.cri_range is not None:
-                self._g_logs['l_g_range'].append(l_g_range.item())
+                self._defer(l_g_range.detach().reshape(1), lambda v, rows=self._g_logs['l_g_range']: rows.append(v[0]))
             if self.D_exists:
-                self._g_logs['l_g_gan'].append(l_g_gan.item())
+                self._defer(l_g_gan.detach().reshape(1), lambda v, rows=self._g_logs['l_g_gan']: rows.append(v[0]))
             if last_acc_G:
                 self._g_buckets.finish()
                 if self.latent_input is not None and self.latent_grads_multiplier != 1:  # :543-546
@@ -475,10 +522,12 @@ class SRRaGANModel:
                         for c in idx:
                             p.grad[:, c, ...] *= self.latent_grads_multiplier
                 self.optimizer_G.step()
-                g = self.gradient_step_num
-                for k, v in self._g_logs.items():  # means over the accumulated micro-batches (:566-574)
-                    if v:
-                        self.log_dict[k].append((g, float(np.mean(v))))
+
+                def log_g(_, logs=self._g_logs, g=self.gradient_step_num):
+                    for k, v in logs.items():  # means over the accumulated micro-batches (:566-574)
+                        if v:
+                            self._log_dict[k].append((g, float(np.mean(v))))
+                self._defer(None, log_g)
         self.step += 1
 
     def update_learning_rate(self):
