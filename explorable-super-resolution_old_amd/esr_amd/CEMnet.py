@@ -172,8 +172,9 @@ class CEMnet:
 class Filter_Layer(nn.Module):
     """CEMnet.py:130-140: frozen depthwise conv.  Forward runs the matching libesr_amd stencil."""
 
-    def __init__(self, filt, kind):
+    def __init__(self, filt, kind, sf=4):
         super().__init__()
+        self.sf = int(sf)  # the CEM's scale factor (stride of 'down', zero-stuffing of 'up')
         k = np.asarray(filt)
         self.Filter_OP = nn.Conv2d(in_channels=3, out_channels=3, kernel_size=k.shape, bias=False, groups=3)
         self.Filter_OP.weight = nn.Parameter(
@@ -202,9 +203,10 @@ class CEM_PyTorch(nn.Module):
         self.pre_pad = False
 
     def _set_filters(self, CEMnet):
-        self.Conv_LR_with_Inv_hTh_OP = Filter_Layer(CEMnet.inv_hTh, 'inv')
-        self.Upscale_OP = Filter_Layer(CEMnet.ds_kernel * CEMnet.ds_factor ** 2, 'up')
-        self.DownscaleOP = Filter_Layer(np.rot90(CEMnet.ds_kernel, 2), 'down')
+        sf = int(CEMnet.ds_factor)
+        self.Conv_LR_with_Inv_hTh_OP = Filter_Layer(CEMnet.inv_hTh, 'inv', sf)
+        self.Upscale_OP = Filter_Layer(CEMnet.ds_kernel * CEMnet.ds_factor ** 2, 'up', sf)
+        self.DownscaleOP = Filter_Layer(np.rot90(CEMnet.ds_kernel, 2), 'down', sf)
         self.margins_LR = int(CEMnet.invalidity_margins_LR)
         self.margins_HR = int(CEMnet.invalidity_margins_HR)
 

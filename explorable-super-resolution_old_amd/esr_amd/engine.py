@@ -36,6 +36,20 @@ from . import _lib
 SF = 4
 CEM_PHASE = SF - SF // 2 - 1  # calc_strides(None, 4) pre_stride (imresize_CEM.py:83-85)
 _FOLD = (((1., 0., 0.), (0., 1., 1.)), ((1., 1., 0.), (0., 0., 1.)))  # nearest-×2 polyphase tap folding, phase 0/1
+# nearest-×f upconv: output phase p of an upsampled axis is a 2-tap conv on the LR grid at offsets (t0 - 1, t0); its
+# taps are the 3 conv taps k summed by the LR pixel floor((f·y + p + k - 1) / f) they read.  (fold rows, t0) per phase
+_FOLDS = {2: ((_FOLD[0], 0), (_FOLD[1], 1))}
+
+
+def cem_phase(sf):
+    """calc_strides(None, sf) pre_stride (imresize_CEM.py:83-85): the sub-pixel phase of the CEM's strided filters."""
+    return sf - sf // 2 - 1
+
+
+def up_stages(net):
+    """The upsampler stages of RRDBNet: [(module index, factor)] — two ×2 for ×4, one for ×2."""
+    n, f = getattr(net, 'n_up', 2), getattr(net, 'up_factor', 2)
+    return [(2 + i, f) for i in range(n)]
 DEFAULT_PRECISION = os.environ.get('ESR_PRECISION', 'x3')
 PRECISIONS = ('x3', 'f32')
 
@@ -144,11 +158,12 @@ def from_split(buf):
     return (h[..., 0, :] + h[..., 1, :]).reshape(buf.shape)
 
 
-def fold_upconv_phase(w, py, px):
-    """Nearest-×2 upsample then 3×3 conv == per output phase (py,px) a 2×2 conv on the LR grid whose taps are sums of
+def fold_upconv_phase(w, py, px, f=2):
+    """Nearest-×f upsample then 3×3 conv == per output phase (py,px) a 2×2 conv on the LR grid whose taps are sums of
     the 3×3 taps landing on the same source pixel (block.py:294-301)."""
-    F = torch.tensor(_FOLD, dtype=w.dtype, device=w.device)
-    return torch.einsum('ay,bx,oiyx->oiab', F[py], F[px], w.detach())
+    Fy = torch.tensor(_FOLDS[f][py][0], dtype=w.dtype, device=w.device)
+    Fx = torch.tensor(_FOLDS[f][px][0], dtype=w.dtype, device=w.device)
+    return torch.einsum('ay,bx,oiyx->oiab', Fy, Fx, w.detach())
 
 
 class _ConvW:
@@ -251,8 +266,9 @@ class _Packed:
                                         rdb.convs[i][0].bias) for i in range(5)])
         lrc = m[1].sub[net.nb]
         self.lr_conv = _ConvW(pk(lrc, lr_map(64), 64), lrc.bias)
-        self.hr0 = _ConvW(pk(m[4], lr_map(64), 64), m[4].bias)
-        self.hr1 = _ConvW(pk(m[6], lr_map(64), 32), m[6].bias)
+        i0 = 2 + getattr(net, 'n_up', 2)  # HR_conv0, then its LeakyReLU, then HR_conv1
+        self.hr0 = _ConvW(pk(m[i0], lr_map(64), 64), m[i0].bias)
+        self.hr1 = _ConvW(pk(m[i0 + 2], lr_map(64), 32), m[i0 + 2].bias)
         views = plan.finalize(net.model[0].weight.device)
         self.planned = [self.first, self.lr_conv, self.hr0, self.hr1] + [cw for r in self.rdb for cw in r]
         for cw in self.planned:
@@ -321,10 +337,10 @@ class _Packed:
         # after the first build so that recorded op lists and captured HIP graphs keep valid pointers
         m = self.net.model
         up = []
-        for j in (2, 3):
+        for j, f in up_stages(self.net):
             c = m[j][1]
-            up.append([_ConvW(pack_conv_weight(fold_upconv_phase(c.weight, py, px), list(range(64)), 64), c.bias)
-                       for py in (0, 1) for px in (0, 1)])
+            up.append([_ConvW(pack_conv_weight(fold_upconv_phase(c.weight, py, px, f), list(range(64)), 64), c.bias)
+                       for py in range(f) for px in range(f)])
         if self.up is None:
             self.up = up
         else:
@@ -384,7 +400,7 @@ def _packed(net, latent):
 
 
 class _Workspace:
-    def __init__(self, dev, B, H, W, latent):
+    def __init__(self, dev, B, H, W, latent, sf=4):
         zc = 8 if latent else 0
         z = lambda *s: torch.zeros(*s, device=dev, dtype=torch.float32)  # noqa: E731
         self.B, self.H, self.W, self.zc = B, H, W, zc
@@ -396,19 +412,20 @@ class _Workspace:
         self.fea = z(B, H + 2, W + 2, 64)
         self.P = [z(B, H + 2, W + 2, self.cp) for _ in range(3)]
         self.U0 = z(B, H + 2, W + 2, 64)
-        self.U1 = z(B, 2 * H + 2, 2 * W + 2, 64)
-        self.HR = [z(B, 4 * H + 2, 4 * W + 2, self.hr_cp) for _ in range(2)]
+        self.U1 = z(B, 2 * H + 2, 2 * W + 2, 64) if sf == 4 else None  # between the two ×2 upconvs of ×4
+        self.HR = [z(B, sf * H + 2, sf * W + 2, self.hr_cp) for _ in range(2)]
         self.lr = z(B, 3, H, W)
         self.overflow = torch.zeros(1, device=dev, dtype=torch.int32)
 
 
 def _workspace(net, dev, B, H, W, latent, precision):
     # keyed by precision too: the zero padding channels of an fp32 workspace are not zero when read as split-f16 pairs
-    key = (str(dev), B, H, W, latent, precision)
+    sf = getattr(net, 'upscale', SF)
+    key = (str(dev), B, H, W, latent, precision, sf)
     c = net._esr_cache.get('ws')
     if c is None or c[0] != key:
         net._esr_cache.pop('ws', None)  # free the previous shape's buffers first
-        c = (key, _Workspace(dev, B, H, W, latent))
+        c = (key, _Workspace(dev, B, H, W, latent, sf))
         net._esr_cache['ws'] = c
     return c[1]
 
@@ -577,6 +594,10 @@ def generator_forward(net, x, cem=None):
     _require_device(x, 'generator input')
     if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in param_list(net))):
         # training step / Z optimisation: retained activations + HIP backward (exact fp32)
+        if getattr(net, 'upscale', SF) != SF:
+            raise NotImplementedError('esr_amd: the HIP backward (training, Z optimisation) implements the ×4 '
+                                      'generator; ×%d runs inference only (torch.no_grad / frozen parameters)'
+                                      % net.upscale)
         from . import train_engine
         return train_engine.generator_forward_train(net, x.contiguous(), cem)
     precision = getattr(net, 'esr_precision', None) or DEFAULT_PRECISION
@@ -603,10 +624,13 @@ def _forward(net, x, cem, precision, train_ws=None, rec=None):
     x3 = precision == 'x3'
     latent = net.latent_input is not None
     nz = net.nl if latent else 0
+    sf = getattr(net, 'upscale', SF)
+    if sf != SF and train_ws is not None:
+        raise NotImplementedError('esr_amd: the training / Z-optimisation backward implements the ×4 generator')
     Bn, C, h, w = x.shape
-    if C != 3 + nz * SF * SF:
+    if C != 3 + nz * sf * sf:
         raise RuntimeError('esr_amd: expected %d input channels (3 LR + %d rearranged HR latent), got %d'
-                           % (3 + nz * SF * SF, nz * SF * SF, C))
+                           % (3 + nz * sf * sf, nz * sf * sf, C))
     if latent and nz != 3:
         raise NotImplementedError('esr_amd latent path is built for 3 latent channels')
     pre_pad = cem is not None and cem.pre_pad
@@ -641,7 +665,7 @@ def _forward(net, x, cem, precision, train_ws=None, rec=None):
         zlr = (ctypes.c_void_p * 4)(*([t.data_ptr() for t in grp] + [None] * (4 - len(grp))))
         zlr_cp = (ctypes.c_int32 * 4)(*([cp] * 4))
         first = gi == 0
-        _lib.check(lib.esr_prep_input(x.data_ptr(), Bn, nz, h, w, SF, m, ws.lr.data_ptr() if first else None,
+        _lib.check(lib.esr_prep_input(x.data_ptr(), Bn, nz, h, w, sf, m, ws.lr.data_ptr() if first else None,
                                       ws.first.data_ptr() if first else None, ws.first_cp, ws.first_lr_off, zlr,
                                       zlr_cp, len(grp), zhr, zhr_cp, 2 if (nz and first) else 0, int(x3), stream),
                    'esr_prep_input')
@@ -686,30 +710,33 @@ def _forward(net, x, cem, precision, train_ws=None, rec=None):
     trunk = rrdb_bufs(net.nb - 1)[3] if net.nb > 0 else rrdb_bufs(0)[0]
     conv(trunk, H, W, cp, zc + 64, pk.lr_conv, 64, _conv_out(ws.U0, 64, 0, H, W, False, r1=ws.fea, r1_cp=64, s1=1.0),
          nl + 64)
-    # two nearest-×2 upconvs, four phases each
-    for (src, sh, sw, dst, dcp, dcoff), phw in zip(
-            ((ws.U0, H, W, ws.U1, 64, 0), (ws.U1, 2 * H, 2 * W, HR0, hcp, zc)), pk.up):
+    # the nearest-×2 upconvs (two for ×4, one for ×2), one launch per output phase
+    stages = [(ws.U0, H, W, ws.U1, 64, 0), (ws.U1, 2 * H, 2 * W, HR0, hcp, zc)] if sf == 4 else \
+        [(ws.U0, H, W, HR0, hcp, zc)]
+    for (src, sh, sw, dst, dcp, dcoff), phw, (_, f) in zip(stages, pk.up, up_stages(net)):
         for ph, cw in enumerate(phw):
-            py, px = ph // 2, ph % 2
-            o = _conv_out(dst, dcp, dcoff, 2 * sh, 2 * sw, True, sy=2, sx=2, oy=py, ox=px)
-            ev = None  # reference FLOPs: a 3×3 conv at 2× resolution, a quarter of it per phase
+            py, px = ph // f, ph % f
+            ty, tx = _FOLDS[f][py][1], _FOLDS[f][px][1]  # tap origins of the phase's 2×2 LR conv
+            o = _conv_out(dst, dcp, dcoff, f * sh, f * sw, True, sy=f, sx=f, oy=py, ox=px)
+            ev = None  # reference FLOPs: a 3×3 conv at f× resolution, 1/f² of it per phase
+            fl = 2.0 * Bn * (f * sh) * (f * sw) * 9 * 64 * 64 / (f * f)
             if rec is not None:
-                rec.tag(tagp + 'upconv2x_phase', 2.0 * Bn * (2 * sh) * (2 * sw) * 9 * 64 * 64 / 4)
+                rec.tag(tagp + 'upconv2x_phase', fl)
             elif prof is not None:
-                ev = _prof_begin(prof, tagp + 'upconv2x_phase', 2.0 * Bn * (2 * sh) * (2 * sw) * 9 * 64 * 64 / 4)
+                ev = _prof_begin(prof, tagp + 'upconv2x_phase', fl)
             if x3:
                 wx, scale = cw.x3()
                 if rec is not None:
                     rec.keep.append(wx)
                 rc = lib.esr_upconv2x_phase_fwd_x3(src.data_ptr(), Bn, sh, sw, 64, 64, wx.data_ptr(),
-                                                   cw.bias.data_ptr(), scale, 64, py, px, ctypes.byref(o), ovf, stream)
+                                                   cw.bias.data_ptr(), scale, 64, ty, tx, ctypes.byref(o), ovf, stream)
             else:
                 rc = lib.esr_upconv2x_phase_fwd(src.data_ptr(), Bn, sh, sw, 64, 64, cw.f32.data_ptr(),
-                                                cw.bias.data_ptr(), 64, py, px, ctypes.byref(o), stream)
+                                                cw.bias.data_ptr(), 64, ty, tx, ctypes.byref(o), stream)
             _lib.check(rc, 'esr_upconv2x_phase_fwd')
             if ev is not None:
                 ev.record()
-    HH, WW = SF * H, SF * W
+    HH, WW = sf * H, sf * W
     conv(HR0, HH, WW, hcp, hcp, pk.hr0, 64, _conv_out(HR1, hcp, zc, HH, WW, True), nl + 64)
     gen = torch.empty(Bn, 3, HH, WW, device=dev, dtype=torch.float32)
     if rec is not None:
@@ -717,12 +744,13 @@ def _forward(net, x, cem, precision, train_ws=None, rec=None):
     conv(HR1, HH, WW, hcp, hcp, pk.hr1, 3, _conv_out(gen, 0, 0, HH, WW, False, planar=1), nl + 64)
     if cem is None:
         return gen, ws
-    return cem_apply(lib, cem, gen, ws.lr, Bn, H, W, SF * m if pre_pad else 0, stream), ws
+    return cem_apply(lib, cem, gen, ws.lr, Bn, H, W, sf * m if pre_pad else 0, stream, sf), ws
 
 
-def cem_apply(lib, cem, gen, lr, Bn, H, W, M, stream):
+def cem_apply(lib, cem, gen, lr, Bn, H, W, M, stream, sf=SF):
     """out = crop_M(gen + Up(Inv(lr - Down(gen))))  ==  CEMnet.py:186-190."""
     dev = gen.device
+    ph = cem_phase(sf)
     wd = cem.DownscaleOP.Filter_OP.weight
     wi = cem.Conv_LR_with_Inv_hTh_OP.Filter_OP.weight
     wu = cem.Upscale_OP.Filter_OP.weight
@@ -733,12 +761,12 @@ def cem_apply(lib, cem, gen, lr, Bn, H, W, M, stream):
     q = torch.empty_like(r)
     if hasattr(lib, 'keep'):  # recording an op list: the intermediates must outlive this call
         lib.keep += [r, q]
-    out = torch.empty(Bn, 3, SF * H - 2 * M, SF * W - 2 * M, device=dev, dtype=torch.float32)
-    _lib.check(lib.esr_cem_down(gen.data_ptr(), lr.data_ptr(), r.data_ptr(), Bn, H, W, SF, CEM_PHASE,
+    out = torch.empty(Bn, 3, sf * H - 2 * M, sf * W - 2 * M, device=dev, dtype=torch.float32)
+    _lib.check(lib.esr_cem_down(gen.data_ptr(), lr.data_ptr(), r.data_ptr(), Bn, H, W, sf, ph,
                                 wd[0, 0].contiguous().data_ptr(), kd, 0, stream), 'esr_cem_down')
     _lib.check(lib.esr_cem_inv(r.data_ptr(), q.data_ptr(), Bn, H, W, wi[0, 0].contiguous().data_ptr(), ki, stream),
                'esr_cem_inv')
-    _lib.check(lib.esr_cem_up_add(q.data_ptr(), gen.data_ptr(), out.data_ptr(), Bn, H, W, SF, CEM_PHASE,
+    _lib.check(lib.esr_cem_up_add(q.data_ptr(), gen.data_ptr(), out.data_ptr(), Bn, H, W, sf, ph,
                                   wu[0, 0].contiguous().data_ptr(), kd, M, stream), 'esr_cem_up_add')
     return out
 
@@ -758,19 +786,21 @@ def cem_filter_op(layer, x):
     wk = w[0, 0].contiguous()
     stream = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
     Bn, _, Hx, Wx = x.shape
+    sf = getattr(layer, 'sf', SF)
+    ph = cem_phase(sf)
     if layer.kind == 'down':
-        if Hx % SF or Wx % SF:
-            raise RuntimeError('esr_amd: DownscaleOP input size must be divisible by %d' % SF)
-        out = torch.empty(Bn, 3, Hx // SF, Wx // SF, device=x.device, dtype=torch.float32)
-        _lib.check(lib.esr_cem_down(x.data_ptr(), None, out.data_ptr(), Bn, Hx // SF, Wx // SF, SF, CEM_PHASE,
+        if Hx % sf or Wx % sf:
+            raise RuntimeError('esr_amd: DownscaleOP input size must be divisible by %d' % sf)
+        out = torch.empty(Bn, 3, Hx // sf, Wx // sf, device=x.device, dtype=torch.float32)
+        _lib.check(lib.esr_cem_down(x.data_ptr(), None, out.data_ptr(), Bn, Hx // sf, Wx // sf, sf, ph,
                                     wk.data_ptr(), k, 1, stream), 'esr_cem_down')
     elif layer.kind == 'inv':
         out = torch.empty_like(x)
         _lib.check(lib.esr_cem_inv(x.data_ptr(), out.data_ptr(), Bn, Hx, Wx, wk.data_ptr(), k, stream), 'esr_cem_inv')
     elif layer.kind == 'up':
-        zero = torch.zeros(Bn, 3, SF * Hx, SF * Wx, device=x.device, dtype=torch.float32)
+        zero = torch.zeros(Bn, 3, sf * Hx, sf * Wx, device=x.device, dtype=torch.float32)
         out = torch.empty_like(zero)
-        _lib.check(lib.esr_cem_up_add(x.data_ptr(), zero.data_ptr(), out.data_ptr(), Bn, Hx, Wx, SF, CEM_PHASE,
+        _lib.check(lib.esr_cem_up_add(x.data_ptr(), zero.data_ptr(), out.data_ptr(), Bn, Hx, Wx, sf, ph,
                                       wk.data_ptr(), k, 0, stream), 'esr_cem_up_add')
     else:
         raise ValueError(layer.kind)

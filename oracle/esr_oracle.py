@@ -295,14 +295,16 @@ def bilinear_down4(z_hr):
 
 
 def rrdbnet_forward(x, P, nb, latent, sf=4):
-    """RRDBNet.forward.  x: [B, 3, h, w] (plain) or [B, 48+3, h, w] (latent, HR Z as a raw view, SRRaGAN_model.py:252).
-    P: dict of reference-named parameters without the 'generated_image_model.' prefix."""
+    """RRDBNet.forward.  x: [B, 3, h, w] (plain) or [B, 3·sf²+3, h, w] (latent, HR Z as a raw view,
+    SRRaGAN_model.py:252).  P: dict of reference-named parameters without the 'generated_image_model.' prefix.
+    sf 4: two nearest-×2 upconvs; 2 / 3: one nearest-×2 / ×3 upconv (architecture.py:113-136)."""
     z_lr = z_hr = None
     if latent:
         zr, x = x[:, :-3], x[:, -3:]
         B, _, h, w = x.shape
         z_hr = zr.reshape(B, -1, sf * h, sf * w)
-        z_lr = bilinear_down4(z_hr)
+        z_lr = bilinear_down4(z_hr) if sf == 4 else \
+            F.interpolate(z_hr, scale_factor=1 / sf, mode='bilinear', align_corners=False)
         x = torch.cat([z_lr, x], 1)
     fea = _conv(x, P, 'model.0', act=False)
     out = torch.cat([z_lr, fea], 1) if latent else fea
@@ -313,14 +315,15 @@ def rrdbnet_forward(x, P, nb, latent, sf=4):
     if latent:
         out = torch.cat([z_lr, out], 1)
     out = fea + _conv(out, P, 'model.1.sub.%d' % nb, act=False)
-    for key in ('model.2.1', 'model.3.1'):  # upconv_blcok: nearest ×2, conv, LReLU (block.py:294-301)
-        out = _conv(F.interpolate(out, scale_factor=2, mode='nearest'), P, key, act=True)
+    ups = [2, 2] if sf == 4 else [sf]
+    for i, f in enumerate(ups):  # upconv_blcok: nearest ×f, conv, LReLU (block.py:294-301)
+        out = _conv(F.interpolate(out, scale_factor=f, mode='nearest'), P, 'model.%d.1' % (2 + i), act=True)
     if latent:
         out = torch.cat([z_hr, out], 1)
-    out = _conv(out, P, 'model.4', act=True)
+    out = _conv(out, P, 'model.%d' % (2 + len(ups)), act=True)
     if latent:
         out = torch.cat([z_hr, out], 1)
-    return _conv(out, P, 'model.6', act=False)
+    return _conv(out, P, 'model.%d' % (4 + len(ups)), act=False)
 
 
 def sr_forward(x, P, nb, latent, design=None, pre_pad=False, sf=4):

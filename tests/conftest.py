@@ -33,13 +33,19 @@ def fixture_params(d):
     return keys, seeded_params(keys, int(d['seed']), float(d['w_scale']))
 
 
+def fixture_upscale(d):
+    """The generator's scale factor of an rrdb_* fixture (×4 unless the fixture records another)."""
+    return int(d['upscale']) if 'upscale' in d else 4
+
+
 def fixture_input(d):
-    """Model input exactly as SRRaGANModel.ConcatLatent builds it (raw view of the HR Z into 48 LR channels)."""
+    """Model input exactly as SRRaGANModel.ConcatLatent builds it (raw view of the HR Z into 3·sf² LR channels)."""
     import torch
     lr = torch.from_numpy(d['lr'])
     if int(d['latent']):
         B, _, h, w = lr.shape
-        return torch.cat([torch.from_numpy(d['z']).reshape(B, 48, h, w), lr], 1)
+        sf = fixture_upscale(d)
+        return torch.cat([torch.from_numpy(d['z']).reshape(B, 3 * sf * sf, h, w), lr], 1)
     return lr
 
 

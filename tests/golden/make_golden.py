@@ -135,26 +135,27 @@ def cem_fixture(CEMnet, name, kernel):
     return cem
 
 
-def rrdb_fixture(arch, CEMnet, name, nb, latent, lr_shape, seed, w_scale, cem_mode=None, z_mode='pixel', kernel=None):
+def rrdb_fixture(arch, CEMnet, name, nb, latent, lr_shape, seed, w_scale, cem_mode=None, z_mode='pixel', kernel=None,
+                 sf=4):
     nl = 3 if latent else 0
-    net = arch.RRDBNet(in_nc=3, out_nc=3, nf=64, nb=nb, gc=32, upscale=4, norm_type=None, act_type='leakyrelu',
+    net = arch.RRDBNet(in_nc=3, out_nc=3, nf=64, nb=nb, gc=32, upscale=sf, norm_type=None, act_type='leakyrelu',
                        mode='CNA', upsample_mode='upconv',
                        latent_input='all_layers_HR_downscaled' if latent else None, num_latent_channels=nl)
     model = net
     cem = None
     if cem_mode is not None:
-        cem = CEMnet.CEMnet(CEMnet.Get_CEM_Config(4), upscale_kernel=kernel)
+        cem = CEMnet.CEMnet(CEMnet.Get_CEM_Config(sf), upscale_kernel=kernel)
         model = cem.WrapArchitecture_PyTorch(net)
     sd = model.state_dict()
     named_shapes = [(k, tuple(v.shape)) for k, v in sd.items()]
     params = seeded_params(named_shapes, seed, w_scale=w_scale)
     model.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=False)
     B, _, h, w = lr_shape
-    lr, z = seeded_inputs(seed + 1, lr_shape, (B, 3, 4 * h, 4 * w) if latent else None, z_mode=z_mode)
+    lr, z = seeded_inputs(seed + 1, lr_shape, (B, 3, sf * h, sf * w) if latent else None, z_mode=z_mode)
     x = torch.from_numpy(lr)
-    if latent:  # SRRaGANModel.ConcatLatent (SRRaGAN_model.py:249-255): raw view of HR Z into 48 LR-sized channels
+    if latent:  # SRRaGANModel.ConcatLatent (SRRaGAN_model.py:249-255): raw view of HR Z into 3·sf² LR-sized channels
         zt = torch.from_numpy(z)
-        x = torch.cat([zt.contiguous().view(B, 3 * 16, h, w), x], 1)
+        x = torch.cat([zt.contiguous().view(B, 3 * sf * sf, h, w), x], 1)
     if cem is not None:
         model.train(cem_mode == 'train')
     else:
@@ -163,6 +164,8 @@ def rrdb_fixture(arch, CEMnet, name, nb, latent, lr_shape, seed, w_scale, cem_mo
         out = model(x).numpy()
     d = dict(lr=lr, out=out, nb=np.int64(nb), latent=np.int64(latent), seed=np.int64(seed), w_scale=np.float64(w_scale),
              cem_mode=np.str_(cem_mode or 'none'), keys=np.str_(json.dumps(named_shapes)))
+    if sf != 4:
+        d['upscale'] = np.int64(sf)
     if z is not None:
         d['z'] = z
     if isinstance(kernel, np.ndarray):
@@ -324,6 +327,15 @@ def main():
         return
     import models.modules.architecture as arch
     torch.set_num_threads(8)
+    if sys.argv[1:] == ['scale2']:  # ×2 generators (architecture.py:113-136) in their own process: imresize's bicubic
+        sf = 2                     # kernel is process-global and sticky.  (×3 cannot be built by the reference:
+        #                            architecture.py:144 concatenates a list and the ×3 nn.Sequential -> TypeError)
+        rrdb_fixture(arch, CEMnet, 'x%d_plain_nb1' % sf, 1, False, (2, 3, 12, 16), 40 + sf, 0.5, sf=sf)
+        rrdb_fixture(arch, CEMnet, 'x%d_plain_nb2_cem_eval' % sf, 2, False, (1, 3, 12, 14), 50 + sf, 0.5,
+                     cem_mode='eval', sf=sf)
+        rrdb_fixture(arch, CEMnet, 'x%d_latent_nb1_cem_eval' % sf, 1, True, (1, 3, 12, 12), 60 + sf, 0.5,
+                     cem_mode='eval', sf=sf)
+        return
     # --- CEM filter design + CEM forward, bicubic default then a learned (non-bicubic) kernel ---
     cem_fixture(CEMnet, 'bicubic', None)
     # --- RRDBNet plain / latent, bare and CEM-wrapped (bicubic kernel) ---

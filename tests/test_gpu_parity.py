@@ -11,7 +11,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from conftest import fixture_input, fixture_params, golden, golden_names, normwise_rel
+from conftest import fixture_input, fixture_upscale, fixture_params, golden, golden_names, normwise_rel
 
 import esr_amd
 from esr_amd import CEMnet as C
@@ -173,12 +173,14 @@ def test_cem_step_vs_golden(gpu_device, name, mode):
 def _product_model(d, dev, precision):
     keys, params = fixture_params(d)
     latent = bool(int(d['latent']))
-    net = esr_amd.RRDBNet(3, 3, 64, int(d['nb']), latent_input='all_layers_HR_downscaled' if latent else None,
+    sf = fixture_upscale(d)
+    net = esr_amd.RRDBNet(3, 3, 64, int(d['nb']), upscale=sf,
+                          latent_input='all_layers_HR_downscaled' if latent else None,
                           num_latent_channels=3 if latent else 0)
     mode = str(d['cem_mode'])
     model = net
     if mode != 'none':
-        cem = C.CEMnet(C.Get_CEM_Config(4), upscale_kernel=d['kernel'] if 'kernel' in d else None)
+        cem = C.CEMnet(C.Get_CEM_Config(sf), upscale_kernel=d['kernel'] if 'kernel' in d else None)
         model = cem.WrapArchitecture_PyTorch(net)
     missing, unexpected = model.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=False)
     assert not unexpected and all('Filter' in k for k in missing)

@@ -11,7 +11,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from conftest import REPO, golden, golden_names
+from conftest import fixture_upscale, REPO, golden, golden_names
 
 import esr_amd
 from esr_amd import CEMnet as C
@@ -43,12 +43,12 @@ def test_blurry_cubic_kernel_is_honoured():
     assert abs(b.ds_kernel.sum() - 1) < 1e-6
 
 
-def _build(nb, latent, cem_mode):
-    net = esr_amd.RRDBNet(3, 3, 64, nb, latent_input='all_layers_HR_downscaled' if latent else None,
+def _build(nb, latent, cem_mode, sf=4):
+    net = esr_amd.RRDBNet(3, 3, 64, nb, upscale=sf, latent_input='all_layers_HR_downscaled' if latent else None,
                           num_latent_channels=3 if latent else 0)
     if cem_mode == 'none':
         return net
-    return C.CEMnet(C.Get_CEM_Config(4)).WrapArchitecture_PyTorch(net)
+    return C.CEMnet(C.Get_CEM_Config(sf)).WrapArchitecture_PyTorch(net)
 
 
 @pytest.mark.parametrize('name', golden_names('rrdb_'))
@@ -57,9 +57,16 @@ def test_state_dict_layout_matches_reference(name):
     if 'kernel' in d:
         pytest.skip('layout identical to the bicubic case; filter sizes covered by the design test')
     ref = json.loads(str(d['keys']))
-    m = _build(int(d['nb']), bool(int(d['latent'])), str(d['cem_mode']))
+    m = _build(int(d['nb']), bool(int(d['latent'])), str(d['cem_mode']), fixture_upscale(d))
     ours = [(k, list(v.shape)) for k, v in m.state_dict().items()]
     assert ours == [(k, list(s)) for k, s in ref]
+
+
+def test_rrdbnet_x3_raises_like_the_reference():
+    """architecture.py:132-144: the reference's ×3 upsampler is an nn.Sequential concatenated to a list (TypeError);
+    there is no ×3 model to match."""
+    with pytest.raises(NotImplementedError):
+        esr_amd.RRDBNet(3, 3, 64, 1, upscale=3, num_latent_channels=0)
 
 
 def test_define_G_from_shipped_config():

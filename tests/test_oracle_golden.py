@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import fixture_input, fixture_params, golden, golden_names, normwise_rel
+from conftest import fixture_upscale, fixture_input, fixture_params, golden, golden_names, normwise_rel
 from oracle import esr_oracle as O
 
 
@@ -51,9 +51,11 @@ def test_rrdbnet_forward(name):
     _, params = fixture_params(d)
     P = O.strip_prefix(params)
     mode = str(d['cem_mode'])
-    design = None if mode == 'none' else O.cem_design(4, d['kernel'] if 'kernel' in d else None)
+    sf = fixture_upscale(d)
+    design = None if mode == 'none' else O.cem_design(sf, d['kernel'] if 'kernel' in d else None)
     with torch.no_grad():
-        out = O.sr_forward(fixture_input(d), P, int(d['nb']), bool(int(d['latent'])), design, pre_pad=mode == 'eval')
+        out = O.sr_forward(fixture_input(d), P, int(d['nb']), bool(int(d['latent'])), design, pre_pad=mode == 'eval',
+                           sf=sf)
     assert out.shape == d['out'].shape
     assert normwise_rel(out.numpy(), d['out']) < 1e-5
 
