@@ -1215,7 +1215,7 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
     // (small grids), the classic kernel stays.  Variant 24 = the round-1 automatic choice (classic only).
     // the polyphase upconv phases (2x2 taps) too: 341 -> 287 us per config-2 launch (whole-step A/B, 2 rounds)
     const bool x3c_pays = taps_side == 2 || (taps_side == 3 && (cout > 32 || !row8_pays));
-    if ((g_x3_kernel >= 50 && g_x3_kernel <= 62) || ((g_x3_kernel == 1 || g_x3_kernel == 63) && x3c_pays)) {
+    if ((g_x3_kernel >= 50 && g_x3_kernel <= 62) || g_x3_kernel == 64 || ((g_x3_kernel == 1 || g_x3_kernel == 63) && x3c_pays)) {
         X3cParams c;
         c.in = p.in; c.B = B; c.H = H; c.W = W; c.in_cp = in_cp; c.cin = cin; c.w = p.w; c.bias = bias;
         c.w_scale_inv = p.w_scale_inv; c.cout = cout; c.tap_y0 = ty0; c.tap_x0 = tx0; c.tiles_x = c.tiles_y = 0;
@@ -1223,6 +1223,10 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
         if (g_x3_kernel == 60) return x3c_launch(c, taps_side, stream, 16);
         if (g_x3_kernel == 61) return x3c_launch(c, taps_side, stream, 32);
         if (g_x3_kernel == 62) return x3c_launch(c, taps_side, stream, 64);
+        // N = 32 3×3 convs (the RDB growth convs): 12-column tiles of four 3-column waves at three workgroups per CU
+        // (variant 64; 0.9 % per config-2 step over the 16-column tiles of variant 50, bitwise equal)
+        if (g_x3_kernel == 64 || ((g_x3_kernel == 1 || g_x3_kernel == 63) && taps_side == 3 && cout <= 32))
+            return x3c_launch(c, taps_side, stream, 128);
 #ifdef ESR_X3_EXPERIMENTS  // 51-54: x3c ablations, 55-59: the warp-specialised persistent form and its ablations
         static const int dbg[5] = {0, 1, 2, 4, 5};
         if (g_x3_kernel >= 55) return x3s_launch(c, taps_side, stream, dbg[g_x3_kernel - 55]);
@@ -1306,11 +1310,11 @@ extern "C" int esr_conv3x3_fwd_x3(const void *in, int32_t B, int32_t H, int32_t 
 }
 
 extern "C" int esr_x3_set_kernel(int32_t variant) {
-    if (variant < 0 || variant > 63) return ESR_EINVAL;
+    if (variant < 0 || variant > 64) return ESR_EINVAL;
 #ifndef ESR_X3_EXPERIMENTS
     // the production library carries the bitwise-identical A/B variants only (include/esr_amd.h)
     const bool ab = variant <= 2 || variant == 15 || (variant >= 16 && variant <= 18) ||
-                    (variant >= 20 && variant <= 28) || variant == 50 || (variant >= 60 && variant <= 63);
+                    (variant >= 20 && variant <= 28) || variant == 50 || (variant >= 60 && variant <= 64);
     if (!ab) return ESR_EINVAL;
 #endif
     const int prev = g_x3_kernel;

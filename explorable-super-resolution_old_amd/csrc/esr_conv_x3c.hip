@@ -136,24 +136,28 @@ __device__ __forceinline__ void sfor(F &&f) {
 // WR (NT = 1): at the start of each K chunk every wave copies the B fragments of all taps from LDS into registers,
 // after which the weight stage is free: the next chunk's weights are LDS-DMA'd while this chunk is computed, so only
 // the halo tile's transfer sits between two chunks' MFMAs (the weights are a third of the staged bytes at N = 32).
-template <int NT, int TS, int DBG = 0, bool RB = false, int CWV = CW, bool WR = false>
-__global__ __launch_bounds__(64 * (TWC / CWV), 2) void conv_x3c_kernel(X3cParams p) {
+// TW: output columns per tile (16 by default); OCC: workgroups per CU the register budget is sized for (A/B: 12-column
+// tiles of 3-column waves at three workgroups per CU, 48 KB of LDS each).
+template <int NT, int TS, int DBG = 0, bool RB = false, int CWV = CW, bool WR = false, int TW = TWC, int OCC = 2>
+__global__ __launch_bounds__(64 * (TW / CWV), (TW / CWV) * OCC / 4) void conv_x3c_kernel(X3cParams p) {
+    constexpr int TWk = TW, HXk = TWk + 2, IN_RECSk = HYC * HXk, IN_PIECESk = (IN_RECSk + 15) / 16;
+    constexpr int IN_Bk = IN_PIECESk * 16 * REC;
     static_assert(!WR || (NT == 1 && !RB), "register-resident weights: one N-tile, weights staged in LDS");
     constexpr int CWk = CWV;                               // output columns per wave
-    constexpr int NW = TWC / CWk;                          // waves per workgroup
-    constexpr int KINk = (IN_PIECES + NW - 1) / NW;        // input pieces per wave
+    constexpr int NW = TWk / CWk;                          // waves per workgroup
+    constexpr int KINk = (IN_PIECESk + NW - 1) / NW;        // input pieces per wave
     constexpr int T = TS * TS;
     constexpr int N = 32 * NT;
     constexpr int W_RECS = T * N;
     constexpr int W_PIECES = W_RECS / 16;
     constexpr int KW = (W_PIECES + NW - 1) / NW;
     constexpr int W_B = W_RECS * REC;
-    constexpr int LDS_BYTES = IN_B + (RB ? 0 : W_B);
+    constexpr int LDS_BYTES = IN_Bk + (RB ? 0 : W_B);
     constexpr int EP_P = N + 4;                            // epilogue row pitch (floats)
     constexpr int NIC = CWk + TS - 1;                       // halo columns a wave reads (6 for 3×3)
     constexpr int NSTEP = NIC * TS;                        // A steps (halo column, tap row) per sweep
-    static_assert(NW * 32 * EP_P * 4 <= IN_B, "per-wave epilogue areas fit in the input region");
-    static_assert(2 * LDS_BYTES <= 163840, "two workgroups per CU");
+    static_assert(NW * 32 * EP_P * 4 <= IN_Bk, "per-wave epilogue areas fit in the input region");
+    static_assert(OCC * LDS_BYTES <= 163840, "OCC workgroups per CU");
     __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_BYTES];
 
     const int tid = threadIdx.x;
@@ -165,9 +169,9 @@ __global__ __launch_bounds__(64 * (TWC / CWV), 2) void conv_x3c_kernel(X3cParams
     const int tile = p.xcd_map ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x;
     const int tx = tile % p.tiles_x;
     const int ty = tile / p.tiles_x;
-    const int x0 = tx * TWC;             // first halo column = padded column x0; output padded columns x0+1+c
+    const int x0 = tx * TWk;             // first halo column = padded column x0; output padded columns x0+1+c
     const int r0 = ty * CT;              // first halo row (tall padded image); output tall rows r0+1+m
-    const int tw = min(TWC, p.W - x0);   // valid output columns of the tile
+    const int tw = min(TWk, p.W - x0);   // valid output columns of the tile
     const int ncw = min(CWk, max(0, tw - CWk * wave));  // valid output columns of this wave
     const int rows_tot = p.B * (p.H + 2);
     const long long rowp = (long long)(p.W + 2);
@@ -184,7 +188,7 @@ __global__ __launch_bounds__(64 * (TWC / CWV), 2) void conv_x3c_kernel(X3cParams
         const int r = 16 * q + sub;
         const int hx = r / HYC, hy = r - (r / HYC) * HYC;
         const int s = ps ^ ((hy >> 2) & 3);
-        const bool v = q < IN_PIECES && r < IN_RECS && r0 + hy < rows_tot && x0 + hx < p.W + 2;
+        const bool v = q < IN_PIECESk && r < IN_RECSk && r0 + hy < rows_tot && x0 + hx < p.W + 2;
         in_off[i] = v ? (unsigned)((hy * rowp + hx) * pixb + (s << 4)) | ((s >> 1) << 1) : 1u;
     }
     auto dma_in = [&](int j) {
@@ -192,7 +196,7 @@ __global__ __launch_bounds__(64 * (TWC / CWV), 2) void conv_x3c_kernel(X3cParams
 #pragma unroll
         for (int i = 0; i < KINk; ++i) {
             const int q = wave + NW * i;
-            if (q >= IN_PIECES) break;
+            if (q >= IN_PIECESk) break;
             const unsigned o = in_off[i];
             const bool ok = !(o & 1u) && ((o >> 1) & 1u) < (unsigned)groups;
             const void *src = ok ? (const void *)(tile_in + (o & ~3u) + 64LL * j) : (const void *)g_zero64;
@@ -209,7 +213,7 @@ __global__ __launch_bounds__(64 * (TWC / CWV), 2) void conv_x3c_kernel(X3cParams
                 const int r = 16 * q + sub;
                 const int s = ps ^ ((r >> 2) & 3);
                 __builtin_amdgcn_global_load_lds((glob_void *)(wj + r * REC + (s << 4)),
-                                                 (lds_void *)(lds + IN_B + q * 1024), 16, 0, 0);
+                                                 (lds_void *)(lds + IN_Bk + q * 1024), 16, 0, 0);
             }
         }
     };
@@ -230,7 +234,7 @@ __global__ __launch_bounds__(64 * (TWC / CWV), 2) void conv_x3c_kernel(X3cParams
         a_hi[d] = o;
         a_lo[d] = o ^ 16u;
     }
-    const uint32_t b_hi = lds_addr(lds) + IN_B + ml * REC + (((2 * hl) ^ ((ml >> 2) & 3)) << 4);
+    const uint32_t b_hi = lds_addr(lds) + IN_Bk + ml * REC + (((2 * hl) ^ ((ml >> 2) & 3)) << 4);
     const uint32_t b_lo = b_hi ^ 16u;
     const f16x8 *w_lane = reinterpret_cast<const f16x8 *>(p.w + ml * REC + 32 * hl);  // RB: this lane's B slice
 
@@ -745,6 +749,14 @@ int x3c_launch(const X3cParams &p0, int taps_side, hipStream_t stream, int dbg) 
         if (n64) return x3c_launch(p0, taps_side, stream, 0);
         if (taps_side == 3) hipLaunchKernelGGL((conv_x3c_kernel<1, 3, 0, false, 4, true>), grid, block, 0, stream, p);
         else hipLaunchKernelGGL((conv_x3c_kernel<1, 2, 0, false, 4, true>), grid, block, 0, stream, p);
+        return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+    }
+    if (dbg == 128) {  // N = 32: 12-column tiles of four 3-column waves, three workgroups per CU (48 KB LDS, <= 168 VGPRs)
+        if (n64) return x3c_launch(p0, taps_side, stream, 0);
+        p.tiles_x = (p.W + 11) / 12;
+        const dim3 grid12((unsigned)(p.tiles_x * p.tiles_y));
+        if (taps_side == 3) hipLaunchKernelGGL((conv_x3c_kernel<1, 3, 0, false, 3, false, 12, 3>), grid12, block, 0, stream, p);
+        else hipLaunchKernelGGL((conv_x3c_kernel<1, 2, 0, false, 3, false, 12, 3>), grid12, block, 0, stream, p);
         return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
     }
     if (dbg == 16) {  // register-B form

@@ -387,8 +387,9 @@ def test_x3_ring_kernel_bitwise_equals_classic(gpu_device, cin, cout, B, H, W):
     try:
         # classic one-stage (default), ring always, persistent ring always, ring / classic with the compiler-scheduled
         # fragment reads, two-stage classic with prefetch 1 / 2, the round-1 automatic choice, the column-tile kernel
-        # (LDS / register weights) (none may change a bit)
-        for variant in (0, 2, 17, 18, 20, 21, 22, 25, 26, 27, 28, 24, 50, 60, 61, 62):
+        # (16-column tiles, LDS / register weights; 12-column tiles at three workgroups per CU, the default where column
+        # tiles pay) (none may change a bit)
+        for variant in (0, 2, 17, 18, 20, 21, 22, 25, 26, 27, 28, 24, 50, 60, 61, 62, 64):
             lib.esr_x3_set_kernel(variant)
             out = torch.zeros(B, H + 2, W + 2, 40, device=gpu_device)
             out2 = torch.zeros(B, H + 2, W + 2, 32, device=gpu_device)
@@ -467,7 +468,7 @@ def test_x3_xcd_tile_map_bitwise(gpu_device, cout, cin, B, H, W):
 
 
 # default, direct register epilogue 16- / 8-row, classic, column tiles
-@pytest.mark.parametrize('variant', [1, 27, 28, 24, 50])
+@pytest.mark.parametrize('variant', [1, 27, 28, 24, 50, 64])
 def test_conv3x3_x3_planar_output(gpu_device, variant):
     lib = _lib.load()
     B, H, W, cin = 2, 19, 45, 72
