@@ -1214,7 +1214,10 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
     // shapes, bitwise identical; profiles/r2_x3c_ab.txt); where 8-row classic tiles at three workgroups per CU pay
     // (small grids), the classic kernel stays.  Variant 24 = the round-1 automatic choice (classic only).
     // the polyphase upconv phases (2x2 taps) too: 341 -> 287 us per config-2 launch (whole-step A/B, 2 rounds)
-    const bool x3c_pays = taps_side == 2 || (taps_side == 3 && (cout > 32 || !row8_pays));
+    // N = 32 12-column tiles (three workgroups per CU) also where the grid is large enough for the classic 8-row
+    // tiles to look better by rounds (≥ 3 full rounds): HR_conv1 at 592² (1115 -> 1060 us per config-2 launch)
+    const int tiles12 = ((W + 11) / 12) * ((B * (H + 2) - 2 + 31) / 32);
+    const bool x3c_pays = taps_side == 2 || (taps_side == 3 && (cout > 32 || !row8_pays || tiles12 >= 9 * n_cu));
     if ((g_x3_kernel >= 50 && g_x3_kernel <= 62) || g_x3_kernel == 64 || ((g_x3_kernel == 1 || g_x3_kernel == 63) && x3c_pays)) {
         X3cParams c;
         c.in = p.in; c.B = B; c.H = H; c.W = W; c.in_cp = in_cp; c.cin = cin; c.w = p.w; c.bias = bias;
