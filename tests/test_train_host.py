@@ -15,6 +15,7 @@ from conftest import golden, normwise_rel
 from esr_amd.discriminator import Discriminator_VGG_128_
 from esr_amd import loss as L
 from esr_amd import SRRaGAN_model as M
+from esr_amd.flat_optim import FlatAdam
 from oracle.recipe import seeded_params
 
 
@@ -135,8 +136,30 @@ def _dist_worker(rank, world, port, q):
         g.D_verification = 'past'  # history of all-reduced values, identical on every rank
         g.log_dict = {'D_logits_diff': [(3, 0.5)], 'Correctly_distinguished': [(3, 0.75)]}
         past = g._gate_generator_step(t, True, gd, gc)
-        q.put((rank, p[0].grad.clone(), p[1].grad.clone(), diff, correct, d_real, d_fake, launched, same, untouched,
-               bufs, gd, gc, cur, past))
+        # the generator's FlatAdam under the bucketed all-reduce: p.grad are views of its flat buffer, the buckets
+        # average into them in place, and two steps equal per-tensor Adam on flat-averaged gradients, bit for bit
+        torch.manual_seed(1)
+        fnet = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 4))
+        rnet = copy.deepcopy(fnet)
+        fopt = FlatAdam(list(fnet.parameters()), lr=1e-2, foreach=False)
+        ropt = torch.optim.Adam(list(rnet.parameters()), lr=1e-2, foreach=False)
+        fb = M.GradBuckets(list(fnet.parameters()), cap_bytes=300)
+        for _ in range(2):
+            fopt.zero_grad()
+            ropt.zero_grad()
+            fb.arm()
+            fnet(x).square().sum().backward()
+            fb.finish()
+            rnet(x).square().sum().backward()
+            M._allreduce_grads(list(rnet.parameters()))
+            fopt.step()
+            ropt.step()
+        flat = (all(torch.equal(a, b) for a, b in zip(fnet.parameters(), rnet.parameters())),
+                float(sum(float(a.double().sum()) for a in fnet.parameters())))
+        # tensors travel as NumPy copies: a tensor in a multiprocessing queue is handed over through a file descriptor
+        # of the sending process, which may already have exited
+        q.put((rank, p[0].grad.numpy().copy(), p[1].grad.numpy().copy(), diff, correct, d_real, d_fake, launched, same,
+               untouched, bufs, gd, gc, cur, past, flat))
     finally:
         dist.destroy_process_group()
 
@@ -155,8 +178,8 @@ def test_ddp_gradient_average_and_consistent_statistics():
         pr.join(60)
         assert pr.exitcode == 0
     for r in res:
-        assert torch.equal(r[1], torch.full((3, 4), 1.5))
-        assert torch.allclose(r[2], torch.arange(5, dtype=torch.float32) * 1.5)
+        assert torch.equal(torch.from_numpy(r[1]), torch.full((3, 4), 1.5))
+        assert torch.allclose(torch.from_numpy(r[2]), torch.arange(5, dtype=torch.float32) * 1.5)
     # images: rank0 diffs (1-0, 1-3) = (1,-2); rank1 (2-0, 2-4) = (2,-2) -> mean -0.25, correct 0.5
     for r in res:
         assert abs(r[3] - (-0.25)) < 1e-6 and abs(r[4] - 0.5) < 1e-6
@@ -166,8 +189,10 @@ def test_ddp_gradient_average_and_consistent_statistics():
         assert launched >= 2, launched  # at least two buckets went out before backward() returned
         assert same and untouched
         assert bufs == (1.0, 7)
-        gd, gc, cur, past = r[11:]
+        gd, gc, cur, past = r[11:15]
         assert abs(gc - 0.75) < 1e-6 and abs(gd - 0.25) < 1e-6  # global batch: diffs (1, 1, 1, -2)
         assert cur is False  # 3 of 4 correct globally: no G step on either rank (rank 0 alone would say yes)
         assert past is True  # the shared history passes 'past' on both ranks
-    assert res[0][11:] == res[1][11:]
+    assert res[0][11:15] == res[1][11:15]
+    assert res[0][15][0] and res[1][15][0]  # FlatAdam + buckets == per-tensor Adam + flat average
+    assert res[0][15][1] == res[1][15][1]   # and the ranks hold the same parameters
