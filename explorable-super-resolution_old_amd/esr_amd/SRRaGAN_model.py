@@ -331,7 +331,8 @@ class SRRaGANModel:
         """Per-image D logit differences, summed over ranks (global-batch semantics of DataParallel), as a device
         tensor [mean diff, fraction correctly distinguished, mean D(real), mean D(fake)] (no host sync)."""
         diff = torch.mean(pred_real.detach() - pred_fake.detach(), dim=list(range(1, pred_real.dim())))
-        s = torch.stack([diff.sum(), (diff > 0).float().sum(), torch.tensor(float(diff.numel()), device=diff.device),
+        # (the image count as a device fill, not torch.tensor(): a pageable host-to-device copy waits for the stream)
+        s = torch.stack([diff.sum(), (diff > 0).float().sum(), diff.new_full((), float(diff.numel())),
                          pred_real.detach().mean(), pred_fake.detach().mean()])
         if _world() > 1:
             dist.all_reduce(s)

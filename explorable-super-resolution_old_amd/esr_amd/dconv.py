@@ -78,11 +78,32 @@ def _pack(wt, n_out):
     return buf.view(T, nck, 32, n_pad).permute(0, 1, 3, 2).contiguous(), nck, n_pad
 
 
-def _gather(src, wt, bias, out, MH, MW, omy, oay, omx, oax, smy, smx, offy, offx):
-    """One esr_dconv_fwd launch: src [B][Hs][Ws][C] and out [B][Ho][Wo][N] contiguous NHWC, wt [T][C][N]."""
+def _packed(w, key, make):
+    """make() -> packed weights of `w` (_pack's result), memoised on w while w is a discriminator parameter
+    (HipConv2d marks its weight) that is unchanged: same storage and version counter, i.e. until the optimiser step,
+    load_state_dict or a .data swap (the generator's packing is keyed the same way, engine._param_key).  The
+    discriminator runs ~4 forwards and their (double) backwards per training step on the same weights; without the
+    memo every launch repacks them (3 PyTorch ops each)."""
+    if not getattr(w, '_esr_dconv_param', False):
+        return make()
+    memo = getattr(w, '_esr_packs', None)
+    if memo is None:
+        memo = w._esr_packs = {}
+    ver = (w.data_ptr(), w._version)
+    hit = memo.get(key)
+    if hit is not None and hit[0] == ver:
+        return hit[1]
+    val = make()
+    memo[key] = (ver, val)
+    return val
+
+
+def _gather(src, packed, bias, out, MH, MW, omy, oay, omx, oax, smy, smx, offy, offx):
+    """One esr_dconv_fwd launch: src [B][Hs][Ws][C] and out [B][Ho][Wo][N] contiguous NHWC, `packed` = _pack(wt [T][C][N],
+    N)."""
     B, Hs, Ws, C = src.shape
     _, Ho, Wo, N = out.shape
-    wp, nck, n_pad = _pack(wt, N)
+    wp, nck, n_pad = packed
     lib = _lib_for_launch()
     # split-K (x3) where the grid would fill few CUs and K is long (the 8x8 pseudo-FC layer): ~512 workgroups,
     # at least 8 K steps per slice
@@ -106,9 +127,9 @@ def conv_forward(x, w, b, k, s, p):
     Co = w.shape[0]
     Ho, Wo = out_size(H, k, s, p), out_size(W, k, s, p)
     y = torch.empty(B, Ho, Wo, Co, device=x.device, dtype=torch.float32)
-    wt = w.detach().permute(2, 3, 1, 0).reshape(k * k, Ci, Co)
+    wp = _packed(w, ('fwd',), lambda: _pack(w.detach().permute(2, 3, 1, 0).reshape(k * k, Ci, Co), Co))
     taps = [(ky, kx) for ky in range(k) for kx in range(k)]
-    _gather(x, wt, None if b is None else b.detach().contiguous(), y, Ho, Wo, 1, 0, 1, 0, s, s,
+    _gather(x, wp, None if b is None else b.detach().contiguous(), y, Ho, Wo, 1, 0, 1, 0, s, s,
             [ky - p for ky, _ in taps], [kx - p for _, kx in taps])
     return y
 
@@ -135,8 +156,9 @@ def conv_dgrad(gy, w, k, s, p, H, W):
             classes.append((cy, cx, MH, MW, [(ky, kx) for ky in tys for kx in txs]))
     gx = (torch.empty if full else torch.zeros)(B, H, W, Ci, device=gy.device, dtype=torch.float32)
     for cy, cx, MH, MW, taps in classes:
-        wt = torch.stack([wd[:, :, ky, kx] for ky, kx in taps])  # [T][Co][Ci]
-        _gather(gy, wt, None, gx, MH, MW, s, cy, s, cx, 1, 1,
+        wp = _packed(w, ('dgrad', s, p, cy, cx),
+                     lambda taps=taps: _pack(torch.stack([wd[:, :, ky, kx] for ky, kx in taps]), Ci))  # [T][Co][Ci]
+        _gather(gy, wp, None, gx, MH, MW, s, cy, s, cx, 1, 1,
                 [(cy + p - ky) // s for ky, _ in taps], [(cx + p - kx) // s for _, kx in taps])
     return gx
 
@@ -258,6 +280,7 @@ class HipConv2d(nn.Conv2d):
         else:
             xh = _ToNHWC.apply(x)
         k, p = self.kernel_size[0], self.padding[0]
+        self.weight._esr_dconv_param = True  # packed-weight memo (_packed); set per call: .to()/_apply may replace it
         if self._im2col:
             B, H, W, C = xh.shape
             Ho, Wo = out_size(H, k, 1, p), out_size(W, k, 1, p)

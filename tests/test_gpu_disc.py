@@ -64,6 +64,38 @@ def _dconv_ops(gpu_device, ci, co, k, s, p, H, W, scale):
     assert normwise_rel(gw.double().cpu(), torch.nn.grad.conv2d_weight(xd, wdd.shape, gyd, stride=s, padding=p)) < 1e-5
 
 
+def test_dconv_packed_weight_memo_follows_updates(gpu_device):
+    """HipConv2d's packed weights are reused while the weight is unchanged (dconv._packed) and rebuilt after an
+    in-place update (optimiser step), a load_state_dict and a .data swap: forward and input gradient stay those of
+    the current weight."""
+    torch.manual_seed(3)
+    conv = dconv.HipConv2d(16, 24, 4, 2, 1).to(gpu_device)
+    x = torch.randn(2, 16, 14, 13, device=gpu_device, requires_grad=True)
+    opt = torch.optim.Adam(conv.parameters(), lr=0.05)
+
+    def check():
+        y = conv(x)
+        gx, = torch.autograd.grad(y.square().sum(), x)
+        w, b = conv.weight.detach().double().cpu(), conv.bias.detach().double().cpu()
+        xd = x.detach().double().cpu()
+        yr = F.conv2d(xd, w, b, stride=2, padding=1)
+        assert normwise_rel(y.detach().double().cpu(), yr) < 1e-5
+        assert normwise_rel(gx.double().cpu(), torch.nn.grad.conv2d_input(xd.shape, w, 2 * yr, stride=2, padding=1)) < 1e-5
+        return y
+
+    check()
+    assert conv.weight._esr_packs  # memo populated (forward + dgrad classes)
+    check()  # memo hit
+    conv(x).square().sum().backward()
+    opt.step()  # in place (version bump)
+    check()
+    sd = {k: v.clone() * 0.5 for k, v in conv.state_dict().items()}
+    conv.load_state_dict(sd)
+    check()
+    conv.weight.data = torch.randn_like(conv.weight)  # new storage, same version
+    check()
+
+
 def _grad_errors(named_grads, ref):
     """Per-parameter max|g - ref| / max(max|ref|, 1e-3 * the largest reference gradient of the model).  The floor only
     matters for the conv biases in front of a BatchNorm (training mode): their exact gradient is 0, and both sides
