@@ -80,8 +80,9 @@ def _pack(wt, n_out):
 
 def _packed(w, key, make):
     """make() -> packed weights of `w` (_pack's result), memoised on w while w is a discriminator parameter
-    (HipConv2d marks its weight) that is unchanged: same storage and version counter, i.e. until the optimiser step,
-    load_state_dict or a .data swap (the generator's packing is keyed the same way, engine._param_key).  The
+    (HipConv2d marks its weight) that is unchanged: same storage and version counter (and FlatAdam buffer version),
+    i.e. until the optimiser step, load_state_dict or a .data swap (the generator's packing is keyed the same way,
+    engine._param_key).  The
     discriminator runs ~4 forwards and their (double) backwards per training step on the same weights; without the
     memo every launch repacks them (3 PyTorch ops each)."""
     if not getattr(w, '_esr_dconv_param', False):
@@ -89,7 +90,8 @@ def _packed(w, key, make):
     memo = getattr(w, '_esr_packs', None)
     if memo is None:
         memo = w._esr_packs = {}
-    ver = (w.data_ptr(), w._version)
+    fl = getattr(w, '_esr_flat', None)  # a FlatAdam view: its in-place update bumps the buffer's version, not w's
+    ver = (w.data_ptr(), w._version, None if fl is None else fl._version)
     hit = memo.get(key)
     if hit is not None and hit[0] == ver:
         return hit[1]
