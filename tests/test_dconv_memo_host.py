@@ -1,0 +1,63 @@
+"""Host logic of the discriminator's packed-weight memo (esr_amd/dconv.py _packed): a hit while the parameter is
+unchanged, a rebuild after every kind of change a training run makes (optimiser step, FlatAdam step on the shared
+buffer, load_state_dict, a .data swap), and no memo for tensors that are not marked discriminator parameters."""
+import torch
+
+from esr_amd import dconv
+from esr_amd.flat_optim import FlatAdam
+
+
+def _counting():
+    calls = []
+
+    def make(w):
+        def f():
+            calls.append(1)
+            return (w.detach().clone(), 1, 64)
+        return f
+    return calls, make
+
+
+def test_memo_hits_until_the_parameter_changes():
+    calls, make = _counting()
+    conv = torch.nn.Conv2d(4, 8, 3)
+    w = conv.weight
+    w._esr_dconv_param = True
+    a = dconv._packed(w, ('fwd',), make(w))
+    b = dconv._packed(w, ('fwd',), make(w))
+    assert len(calls) == 1 and a is b
+    dconv._packed(w, ('dgrad', 1, 1, 0, 0), make(w))  # another key: its own entry
+    assert len(calls) == 2
+    w.grad = torch.ones_like(w)
+    torch.optim.Adam([w], lr=0.1).step()  # in place: version bump
+    c = dconv._packed(w, ('fwd',), make(w))
+    assert len(calls) == 3 and torch.equal(c[0], w.detach())
+    conv.load_state_dict({'weight': torch.zeros_like(w), 'bias': conv.bias.detach()})
+    d = dconv._packed(w, ('fwd',), make(w))
+    assert len(calls) == 4 and not d[0].any()
+    w.data = torch.randn_like(w)  # new storage, same version counter
+    e = dconv._packed(w, ('fwd',), make(w))
+    assert len(calls) == 5 and torch.equal(e[0], w.detach())
+
+
+def test_memo_follows_a_flat_adam_step():
+    calls, make = _counting()
+    conv = torch.nn.Conv2d(4, 8, 3)
+    conv.weight._esr_dconv_param = True
+    opt = FlatAdam(list(conv.parameters()), lr=0.1)
+    w = conv.weight
+    dconv._packed(w, ('fwd',), make(w))
+    v = w._version
+    conv(torch.randn(1, 4, 5, 5)).sum().backward()
+    opt.step()  # updates the shared buffer: w's own version counter does not move
+    assert w._version == v
+    p = dconv._packed(w, ('fwd',), make(w))
+    assert len(calls) == 2 and torch.equal(p[0], w.detach())
+
+
+def test_unmarked_tensors_are_not_memoised():
+    calls, make = _counting()
+    g = torch.randn(8, 4, 3, 3)  # e.g. a weight-gradient tensor used as weights in the double backward
+    dconv._packed(g, ('fwd',), make(g))
+    dconv._packed(g, ('fwd',), make(g))
+    assert len(calls) == 2 and not hasattr(g, '_esr_packs')
