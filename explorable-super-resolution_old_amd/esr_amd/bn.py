@@ -99,7 +99,7 @@ class _LReLUFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, slope):
-        y = torch.where(x > 0, x, x * slope)
+        y = torch.nn.functional.leaky_relu(x, slope)  # one pass (x > 0 ? x : x·slope); where() took three
         ctx.save_for_backward(y)
         ctx.slope = slope
         return y
@@ -117,7 +117,7 @@ class _LReLUBwdFn(torch.autograd.Function):
     def forward(ctx, g, y, slope):
         ctx.save_for_backward(y)
         ctx.slope = slope
-        return torch.where(y > 0, g, g * slope)
+        return torch.ops.aten.leaky_relu_backward(g, y, slope, True)  # y > 0 ? g : g·slope, one pass
 
     @staticmethod
     def backward(ctx, gg):
