@@ -259,6 +259,51 @@ class _ToNHWC(torch.autograd.Function):
         return g.permute(0, 3, 1, 2).contiguous()
 
 
+def _im2col(xh, k, p):
+    """[B][H][W][C] -> [B][Ho][Wo][32] (stride 1): channel (ky*k + kx)*C + c = x[y + ky - p][x + kx - p][c] (zero
+    outside), zero-filled to 32 channels."""
+    B, H, W, C = xh.shape
+    Ho, Wo = out_size(H, k, 1, p), out_size(W, k, 1, p)
+    xp = F.pad(xh, (0, 0, p, p, p, p))
+    return torch.cat([xp[:, ky:ky + Ho, kx:kx + Wo, :] for ky in range(k) for kx in range(k)] +
+                     [xh.new_zeros(B, Ho, Wo, 32 - k * k * C)], dim=3)
+
+
+def _col2im(gc, k, p, H, W, C):
+    """The adjoint of _im2col: every tap's channel group added back at its shift (zeros + k² in-place adds + one
+    copy; autograd through cat / slice / pad made a padded temporary and an add per tap)."""
+    B, Ho, Wo, _ = gc.shape
+    gp = gc.new_zeros(B, H + 2 * p, W + 2 * p, C)
+    for t in range(k * k):
+        ky, kx = divmod(t, k)
+        gp[:, ky:ky + Ho, kx:kx + Wo, :] += gc[..., t * C:(t + 1) * C]
+    return gp[:, p:p + H, p:p + W, :].contiguous()
+
+
+class _Im2ColFn(torch.autograd.Function):
+    """_im2col with _col2im as its gradient (and _im2col as the gradient of that: the WGAN-GP double backward)."""
+
+    @staticmethod
+    def forward(ctx, xh, k, p):
+        ctx.geom = (k, p) + tuple(xh.shape[1:])
+        return _im2col(xh, k, p)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _Col2ImFn.apply(g.contiguous(), *ctx.geom), None, None
+
+
+class _Col2ImFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gc, k, p, H, W, C):
+        ctx.geom = (k, p)
+        return _col2im(gc, k, p, H, W, C)
+
+    @staticmethod
+    def backward(ctx, gg):
+        return _Im2ColFn.apply(gg.contiguous(), *ctx.geom), None, None, None, None, None
+
+
 class HipConv2d(nn.Conv2d):
     """nn.Conv2d of the discriminator (same parameters, state_dict and init) whose forward runs esr_dconv.
 
@@ -284,11 +329,8 @@ class HipConv2d(nn.Conv2d):
         k, p = self.kernel_size[0], self.padding[0]
         self.weight._esr_dconv_param = True  # packed-weight memo (_packed); set per call: .to()/_apply may replace it
         if self._im2col:
-            B, H, W, C = xh.shape
-            Ho, Wo = out_size(H, k, 1, p), out_size(W, k, 1, p)
-            xp = F.pad(xh, (0, 0, p, p, p, p))
-            cols = torch.cat([xp[:, ky:ky + Ho, kx:kx + Wo, :] for ky in range(k) for kx in range(k)] +
-                             [xh.new_zeros(B, Ho, Wo, 32 - k * k * C)], dim=3)  # channel (ky*k + kx)*C + c
+            C = xh.shape[3]
+            cols = _Im2ColFn.apply(xh, k, p)  # channel (ky*k + kx)*C + c
             w1 = F.pad(self.weight.permute(0, 2, 3, 1).reshape(self.out_channels, k * k * C), (0, 32 - k * k * C))
             y = DConvFn.apply(cols, w1.view(self.out_channels, 32, 1, 1), self.bias, 1, 1, 0)
         else:
