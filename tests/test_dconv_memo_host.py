@@ -1,6 +1,7 @@
-"""Host logic of the discriminator's conv0 im2col adjoint and of its packed-weight memo (esr_amd/dconv.py _packed): a hit while the parameter is
-unchanged, a rebuild after every kind of change a training run makes (optimiser step, FlatAdam step on the shared
-buffer, load_state_dict, a .data swap), and no memo for tensors that are not marked discriminator parameters."""
+"""Host logic of the discriminator's conv0 im2col adjoint and of its packed-weight memo (esr_amd/dconv.py _packed):
+a memo hit while the parameter is unchanged, a rebuild after every kind of change a training run makes (optimiser
+step, FlatAdam step on the shared buffer, load_state_dict, a .data swap), and no memo for tensors that are not marked
+discriminator parameters."""
 import torch
 
 from esr_amd import dconv
