@@ -1,0 +1,54 @@
+"""GPU parity of esr_cem_adjoint (csrc/esr_train.hip), the exact adjoint of the CEM stencils with replicate padding
+(CEMnet.py:149-162), against float64 autograd (vjp) of the same stencil on the CPU, for the three calls the generator
+backward makes (train_engine.generator_backward: Upscale_OP, the inverse filter, DownscaleOP with alpha -1 accumulated)
+and for odd sizes where the clamped border rows and columns are a large share.  Bar: 1e-6 normwise (fp32)."""
+import ctypes
+
+import pytest
+import torch
+
+from conftest import normwise_rel
+
+from esr_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+
+def _stencil(x, w, s, c, Oy, Ox):
+    """out[o] = sum_u w[u] x[clamp(s*o + c + u - K//2)] per plane (2-D, replicate clamp), x [P][Ly][Lx]."""
+    K = w.shape[0]
+    Ly, Lx = x.shape[1:]
+    iy = (s * torch.arange(Oy)[:, None] + c + torch.arange(K)[None, :] - K // 2).clamp(0, Ly - 1)  # [Oy][K]
+    ix = (s * torch.arange(Ox)[:, None] + c + torch.arange(K)[None, :] - K // 2).clamp(0, Lx - 1)  # [Ox][K]
+    g = x[:, iy[:, None, :, None], ix[None, :, None, :]]  # [P][Oy][Ox][K][K]
+    return (g * w).sum((-2, -1))
+
+
+@pytest.mark.parametrize('P,Ly,Lx,K,s,c,os_,oc,alpha,acc', [
+    (6, 64, 72, 17, 1, 0, 4, 1, 1.0, 0),     # Upscale_OP adjoint (HR -> LR phase samples), sf 4
+    (6, 16, 18, 13, 1, 0, 1, 0, 1.0, 0),     # inverse filter adjoint (LR -> LR)
+    (6, 64, 72, 17, 4, 1, 1, 0, -1.0, 1),    # DownscaleOP adjoint (LR -> HR), accumulated with alpha -1
+    (3, 13, 11, 17, 4, 1, 1, 0, 1.0, 0),     # tiny HR grid: most outputs on or near the clamped border
+    (3, 22, 26, 9, 2, 0, 2, 0, 1.0, 0),      # sf 2 (phase 0)
+])
+def test_cem_adjoint_vs_float64_vjp(gpu_device, P, Ly, Lx, K, s, c, os_, oc, alpha, acc):
+    gen = torch.Generator().manual_seed(K * 100 + Ly)
+    w = torch.randn(K, K, generator=gen, dtype=torch.float64) / K
+    Oy, Ox = -(-Ly // s), -(-Lx // s)  # forward output size: the strided grid over the input
+    if s == 1:
+        Oy, Ox = Ly, Lx
+    g = torch.randn(P, Oy, Ox, generator=gen, dtype=torch.float64)
+    x = torch.zeros(P, Ly, Lx, dtype=torch.float64, requires_grad=True)
+    ref, = torch.autograd.grad(_stencil(x, w, s, c, Oy, Ox), x, g)  # F^T g on the full input grid
+    ref = alpha * ref[:, oc::os_, oc::os_]
+    base = torch.randn(ref.shape, generator=gen, dtype=torch.float64)
+    if acc:
+        ref = ref + base
+    lib = _lib.load()
+    gd, wd = g.float().to(gpu_device), w.float().to(gpu_device)
+    out = base.float().to(gpu_device) if acc else torch.empty(ref.shape, device=gpu_device)
+    st = ctypes.c_void_p(torch.cuda.current_stream(gpu_device).cuda_stream)
+    _lib.check(lib.esr_cem_adjoint(gd.data_ptr(), P, Oy, Ox, wd.data_ptr(), K, s, c, Ly, Lx, os_, oc, alpha, acc,
+                                   out.data_ptr(), st), 'esr_cem_adjoint')
+    torch.cuda.synchronize()
+    assert normwise_rel(out.double().cpu(), ref) < 1e-6
