@@ -858,25 +858,6 @@ __global__ __launch_bounds__(NT) void cem_adjoint_kernel(AdjParams p) {
     const float *g = p.g + plane * p.Oy * p.Ox;
     const int pd = p.K / 2;
     float acc = 0.f;
-    if (ky > 0 && ky < p.Ly - 1 && kx > 0 && kx < p.Lx - 1) {
-        // interior (no replicate clamp lands here): only the taps with s | (k - c - u + pd) contribute, one o each —
-        // the generic loop below visits the same taps in the same order (acc += w·g), without its per-tap range search
-        const int ty = ky - p.c + pd, tx = kx - p.c + pd;
-        const int ry = ((ty % p.s) + p.s) % p.s, rx = ((tx % p.s) + p.s) % p.s;
-        for (int uy = ry; uy < p.K; uy += p.s) {
-            const int oy = (ty - uy) / p.s;
-            if (oy < 0 || oy >= p.Oy) continue;
-            const float *gr = g + (long long)oy * p.Ox;
-            for (int ux = rx; ux < p.K; ux += p.s) {
-                const int ox = (tx - ux) / p.s;
-                if (ox < 0 || ox >= p.Ox) continue;
-                acc += sw[uy * p.K + ux] * gr[ox];
-            }
-        }
-        float *o = p.out + plane * p.Ny * p.Nx + (long long)i * p.Nx + j;
-        *o = p.accumulate ? *o + p.alpha * acc : p.alpha * acc;
-        return;
-    }
     for (int uy = 0; uy < p.K; ++uy) {
         int ylo, yhi;
         if (!o_range(ky, uy, p.s, p.c, pd, p.Ly, p.Oy, &ylo, &yhi)) continue;
