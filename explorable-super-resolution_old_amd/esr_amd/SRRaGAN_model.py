@@ -1,7 +1,8 @@
 """SRRaGANModel — counterpart of reference codes/models/SRRaGAN_model.py (the north_star's "SRGAN_model").
 
 Keeps the interface the reference's drivers use — `feed_data`, `ConcatLatent`, `GetLatent`, `optimize_parameters`,
-`test`, `get_current_visuals`, attributes `netG`, `netD`, `CEM_net`, `fake_H`, `var_L`, `var_H`, `model_input`,
+`test`, `get_current_visuals`, `update_learning_rate(cur_step)`, `get_current_log`, `get_current_learning_rate`,
+`perform_validation`, `save`/`load`/`save_log`, attributes `netG`, `netD`, `CEM_net`, `fake_H`, `var_L`, `var_H`, `model_input`,
 `num_latent_channels`, `Z_size_factor`, `log_dict`, `step` — for the configuration the shipped JSONs select:
 CEM_arch, latent `all_layers`/`HR_downscaled` (or no latent), WGAN-GP (relativistic or not), range loss, D_verification
 'past'/'current'/None, fixed or adaptive D_update_ratio, gradient accumulation.  Options the shipped configs switch off (VGG feature loss — broken in the
@@ -9,8 +10,8 @@ reference, pixel/high-pass/shift-invariant/optimal-Z/latent losses, encoder, dec
 NotImplementedError instead of silently differing.  Checkpoints and logs keep the reference's formats
 (base_model.py:86-144; SRRaGAN_model.py:695-719, 766-813): `{step}_G.pth` / `{step}_D.pth` dicts with
 model_state_dict + optimizer_state_dict, the positional key-remapping loader with the latent-channel zero-prepend, and
-logs.npz / lr.npz; checkpoints are read with torch.load(weights_only=True).  Checkpoint rotation, plotting and
-TensorBoard are out of scope.
+logs.npz / lr.npz; checkpoints are read with torch.load(weights_only=True).  Plotting (display_log_figure) and
+TensorBoard are out of scope: display_log_figure is a no-op, so codes/train.py runs unchanged.
 
 Multi-GPU: one process per GPU (torch.distributed, RCCL).  The reference's nn.DataParallel computes every loss on the
 gathered global batch; with equal per-rank batches the average of per-rank gradients equals that gradient, so the G / D
@@ -23,7 +24,9 @@ import collections
 import math
 import os
 import re
+import struct
 import warnings
+import zlib
 from collections import OrderedDict
 
 import numpy as np
@@ -206,11 +209,17 @@ class SRRaGANModel:
                 self.CEM_net.WrapArchitecture_PyTorch(only_padders=True)
         self.netG = networks.define_G(opt, CEM=self.CEM_net, num_latent_channels=self.num_latent_channels)
         self.netG.to(self.device)
-        keys = ['l_g_range', 'l_g_gan', 'l_d_real', 'l_d_fake', 'l_d_real_fake', 'D_real', 'D_fake', 'D_logits_diff',
-                'D_update_ratio', 'Correctly_distinguished', 'l_d_gp']
+        # the reference's log keys in its order (SRRaGAN_model.py:72-75): get_current_log reports them in this order
+        keys = ['l_g_pix', 'l_g_fea', 'l_g_range', 'l_g_gan', 'l_d_real', 'l_d_fake', 'D_loss_STD', 'l_d_real_fake',
+                'l_g_highpass', 'l_g_shift_invariant', 'D_real', 'D_fake', 'D_logits_diff', 'psnr_val',
+                'D_update_ratio', 'LR_decrease', 'Correctly_distinguished', 'l_d_gp', 'l_e', 'l_g_optimalZ'] + \
+            ['l_g_latent_%d' % i for i in range(self.num_latent_channels)]
         self.log_dict = OrderedDict((k, []) for k in keys)
+        self.max_accumulation_steps = accumulation_steps_per_batch
         if self.is_train:
             self._init_training(opt, accumulation_steps_per_batch)
+            self.generator_changed = True  # :243, so that train.py validates the initial state
+        self.load()  # :244: resume / pretrained weights / the test model, as the options say
 
     # ------------------------------------------------------------------------------------------------------------------
     def _init_training(self, opt, accumulation_steps_per_batch):
@@ -247,9 +256,9 @@ class SRRaGANModel:
         self.optimizer_G = FlatAdam(gparams, lr=lr_G, weight_decay=t.get('weight_decay_G') or 0,
                                     betas=(t['beta1_G'], 0.999))
         g = self.netG.module if isinstance(self.netG, torch.nn.DataParallel) else self.netG
-        rrdb = g.generated_image_model if self.CEM_net is not None else g
-        # the backward adds its flat gradient buffer straight into the optimiser's (single process: no bucket hooks)
-        rrdb._esr_flat_grad = self.optimizer_G if _world() == 1 else None
+        # the RRDBNet whose backward may add its flat gradient buffer straight into the optimiser's; armed only around
+        # the generator loss's .backward() in optimize_parameters (single process: no bucket hooks wait)
+        self._rrdb = g.generated_image_model if self.CEM_net is not None else g
         self.optimizers.append(self.optimizer_G)
         if self.D_exists:
             self.netD = networks.define_D(opt, CEM=self.CEM_net).to(self.device)
@@ -512,7 +521,13 @@ class SRRaGANModel:
                 l_g_total = l_g_total + l_g_gan
             if last_acc_G:
                 self._g_buckets.arm()
-            l_g_total.backward()
+            # the flat-gradient fast path (train_engine._GeneratorFn.backward) only for this backward: a full
+            # .backward() into every generator parameter, with no per-parameter hooks when single-process
+            self._rrdb._esr_flat_grad = self.optimizer_G if _world() == 1 else None
+            try:
+                l_g_total.backward()
+            finally:
+                self._rrdb._esr_flat_grad = None
             if self.cri_range is not None:
                 self._defer(l_g_range.detach().reshape(1), lambda v, rows=self._g_logs['l_g_range']: rows.append(v[0]))
             if self.D_exists:
@@ -524,6 +539,7 @@ class SRRaGANModel:
                         for c in idx:
                             p.grad[:, c, ...] *= self.latent_grads_multiplier
                 self.optimizer_G.step()
+                self.generator_changed = True  # :548
 
                 def log_g(_, logs=self._g_logs, g=self.gradient_step_num):
                     for k, v in logs.items():  # means over the accumulated micro-batches (:566-574)
@@ -532,9 +548,99 @@ class SRRaGANModel:
                 self._defer(None, log_g)
         self.step += 1
 
-    def update_learning_rate(self):
-        for s in self.schedulers:
-            s.step()
+    def update_learning_rate(self, cur_step=None):
+        """SRRaGAN_model.py:637-683 (the LOSS_BASED branch the reference runs; returns lr_too_low).  Once
+        D_logits_diff holds steps_4_loss_std entries, logs D_loss_STD = the std of (l_d_real + l_d_fake) / 2 over the
+        entries logged at steps >= cur_step - steps_4_loss_std.  Nothing more happens until the log holds
+        2 * steps_4_loss_std entries and its first entry is at least steps_4_loss_std steps old; then, if that std
+        exceeds std_4_lr_drop, training rolls back to the newest checkpoint at or before cur_step - steps_4_loss_std
+        (weights, optimiser states, step counter and logs), every learning rate becomes lr_gamma × its value before the
+        rollback, lr.npz is written and the drop is logged in LR_decrease; True as soon as a learning rate falls below
+        1e-8.  The MultiStepLR schedulers (self.schedulers, :236-239) are never stepped here: the reference's
+        override replaces base_model's scheduler stepping (train.py steps them itself only without a D)."""
+        t = self.opt['train']
+        n = t['steps_4_loss_std']
+        log = self.log_dict
+        reduce_lr = False
+        if len(log['D_logits_diff']) >= n:
+            vals = [(v[1] + log['l_d_fake'][i][1]) / 2 for i, v in enumerate(log['l_d_real']) if v[0] >= cur_step - n]
+            log['D_loss_STD'].append([self.gradient_step_num, np.std(vals)])
+            reduce_lr = t.get('std_4_lr_drop') is not None and log['D_loss_STD'][-1][1] > t['std_4_lr_drop']
+        if len(log['D_logits_diff']) < 2 * n or log['D_logits_diff'][0][0] > cur_step - n:
+            return False
+        if reduce_lr:
+            cur_lr = [o.param_groups[0]['lr'] for o in self.optimizers]
+            self.load(max_step=cur_step - n, resume_train=True)
+            for lr, o in zip(cur_lr, self.optimizers):
+                for group in o.param_groups:
+                    group['lr'] = lr * t['lr_gamma']
+                    if group['lr'] < 1e-8:
+                        return True
+            lr_G, lr_D = self.optimizer_G.param_groups[0]['lr'], self.optimizer_D.param_groups[0]['lr']
+            print('LR(D) reduced to %.2e, LR(G) reduced to %.2e.' % (lr_D, lr_G))
+            self.save_lr(cur_step)
+            self.log_dict['LR_decrease'].append([self.step // self.max_accumulation_steps,
+                                                 {'lr_G': lr_G, 'lr_D': lr_D}])
+        return False
+
+    def get_current_log(self):
+        """SRRaGAN_model.py:685-693: the latest value of every non-empty log series."""
+        out = OrderedDict()
+        for k, v in self.log_dict.items():
+            if len(v) > 0:
+                out[k] = v[-1][1] if isinstance(v[-1], tuple) or len(v[-1]) > 1 else v[-1]
+        return out
+
+    def get_current_learning_rate(self):
+        """base_model.py:44-45."""
+        return self.optimizers[0].param_groups[0]['lr']
+
+    def display_log_figure(self):
+        """base_model.py:160-215 plots the logs with matplotlib: out of scope here (no-op)."""
+
+    def perform_validation(self, data_loader, cur_Z, print_rlt, save_GT_HR, save_images):
+        """SRRaGAN_model.py:586-635: batch-1 `test()` of every validation image with latent value cur_Z, PSNR of
+        the 0-255 float images (utils/util.py:80-104 tensor2img, :168-175 calculate_psnr) averaged into
+        print_rlt['psnr']; with save_images, the centre crops (the smallest HR size - 2) of the SR (and, with
+        save_GT_HR, the HR) images as a collage PNG under path.val_images.  Returns the SR images (HWC BGR float32
+        0-255)."""
+        psnrs, sr_images, collage, gt_collage = [], [], [], []
+        if save_images:
+            n_img = len(data_loader.dataset)
+            rows = int(np.floor(np.sqrt(n_img)))
+            while rows > 1 and np.round(n_img / rows) != n_img / rows:
+                rows -= 1
+            patch = min([min(im['HR'].shape[1:]) for im in data_loader.dataset]) - 2
+        for idx, val_data in enumerate(data_loader):
+            if save_images and idx % rows == 0:
+                collage.append([])
+                gt_collage.append([])
+            val_data['Z'] = cur_Z
+            self.feed_data(val_data)
+            self.test()
+            visuals = self.get_current_visuals()
+            sr_img = 255 * _tensor2img(visuals['SR'])
+            gt_img = 255 * _tensor2img(visuals['HR'])
+            sr_images.append(sr_img)
+            psnrs.append(_psnr(sr_img, gt_img))
+            if save_images:
+                m = ((np.array(sr_img.shape[:2]) - patch) / 2).astype(np.int32)
+                crop = lambda im: np.clip(im[m[0]:-m[0], m[1]:-m[1], ...], 0, 255).astype(np.uint8)  # noqa: E731
+                collage[-1].append(crop(sr_img))
+                if save_GT_HR:
+                    gt_collage[-1].append(crop(gt_img))
+        avg_psnr = float(np.mean(psnrs))
+        if save_images:
+            out_dir = self.opt['path']['val_images']
+            latent = self.opt['network_G'].get('latent_input')
+            _save_png(np.concatenate([np.concatenate(c, 0) for c in collage], 1), os.path.join(
+                out_dir, '{:d}_{}PSNR{:.3f}.png'.format(self.gradient_step_num, ('Z' + str(cur_Z)) if latent else '',
+                                                        avg_psnr)))
+            if save_GT_HR:
+                _save_png(np.concatenate([np.concatenate(c, 0) for c in gt_collage], 1),
+                          os.path.join(out_dir, 'GT_HR.png'))
+        print_rlt['psnr'] += avg_psnr
+        return sr_images
 
     # ------------------------------------------------------------------------------------------------------------------
     def test(self, prevent_grads_calc=True):
@@ -632,6 +738,9 @@ class SRRaGANModel:
         resume = resume_train if resume_train is not None else (self.is_train and self.opt['train'].get('resume'))
         paths = self.opt.get('path') or {}
         if max_step is not None or resume or not self.is_train:
+            if not self.is_train and not (self.save_dir and os.path.isdir(self.save_dir) and
+                                          any('_G.pth' in n for n in os.listdir(self.save_dir))):
+                return  # built programmatically (GUI / Z_optimizer / tests) with no checkpoint directory to load
             names = sorted([n for n in os.listdir(self.save_dir) if '_G.pth' in n], key=self._step_of)
             if max_step is not None:
                 names = [n for n in names if self._step_of(n) <= max_step]
@@ -664,9 +773,15 @@ class SRRaGANModel:
         return path
 
     def save_log(self):
-        """SRRaGAN_model.py:695-698: logs.npz, one array of (step, value) rows per log key."""
-        np.savez(os.path.join(self.log_path, 'logs.npz'), **{k: np.asarray(v, dtype=np.float64).reshape(-1, 2)
-                                                                 for k, v in self.log_dict.items()})
+        """SRRaGAN_model.py:695-698: logs.npz, one array of (step, value) rows per log key (LR_decrease's
+        [step, {lr_G, lr_D}] rows as the object array the reference writes; load_log skips it: it needs unpickling)."""
+        arrays = {}
+        for k, v in self.log_dict.items():
+            if any(isinstance(r[1], dict) for r in v):
+                arrays[k] = np.array([[r[0], r[1]] for r in v], dtype=object)
+            else:
+                arrays[k] = np.asarray(v, dtype=np.float64).reshape(-1, 2)
+        np.savez(os.path.join(self.log_path, 'logs.npz'), **arrays)
 
     def save_lr(self, step_num):
         """The lr.npz the reference writes when it decays the learning rates (SRRaGAN_model.py:676-681), read back by
@@ -684,8 +799,38 @@ class SRRaGANModel:
                     arr = f[key]
                 except ValueError:
                     warnings.warn('logs.npz: skipping %r (object array)' % key)
+                    self.log_dict[key] = []
                     continue
                 rows = [tuple(r) for r in np.asarray(arr).reshape(len(arr), -1).tolist()] if len(arr) else []
                 if max_step is not None:
                     rows = [r for r in rows if r[0] <= max_step]
                 self.log_dict[key] = rows
+
+
+def _tensor2img(t):
+    """utils/util.py:80-104 for a CHW tensor, out_type float32: clamp to [0, 1], HWC, BGR."""
+    a = t.squeeze().float().cpu().clamp_(0, 1).numpy()
+    if a.ndim == 3:
+        a = np.transpose(a[[2, 1, 0], :, :], (1, 2, 0))
+    return a.astype(np.float32)
+
+
+def _psnr(img1, img2):
+    """utils/util.py:168-175 (images in [0, 255])."""
+    mse = np.mean((img1.astype(np.float64) - img2.astype(np.float64)) ** 2)
+    return float('inf') if mse == 0 else 20 * math.log10(255.0 / math.sqrt(mse))
+
+
+def _save_png(img, path):
+    """cv2.imwrite of an HWC BGR (or HW gray) uint8 image (utils/util.py:107-108), as an 8-bit RGB/gray PNG written
+    with zlib (OpenCV is not a dependency here)."""
+    img = np.ascontiguousarray(img[..., ::-1] if img.ndim == 3 else img, dtype=np.uint8)
+    h, w = img.shape[:2]
+    color = 2 if img.ndim == 3 else 0
+    raw = b''.join(b'\x00' + img[r].tobytes() for r in range(h))
+
+    def chunk(tag, data):
+        return struct.pack('>I', len(data)) + tag + data + struct.pack('>I', zlib.crc32(tag + data) & 0xffffffff)
+    with open(path, 'wb') as f:
+        f.write(b'\x89PNG\r\n\x1a\n' + chunk(b'IHDR', struct.pack('>IIBBBBB', w, h, 8, color, 0, 0, 0)) +
+                chunk(b'IDAT', zlib.compress(raw, 6)) + chunk(b'IEND', b''))

@@ -9,8 +9,10 @@ computes the bias corrections on the device in fp32, which is not the reference'
 
 The parameters become views of `flat` and their `.grad` views of `flat.grad`, so everything that reads or writes
 them per tensor (autograd accumulation, the latent-channel gradient amplification, checkpoints, load_state_dict)
-keeps working.  `zero_grad()` zeroes the flat gradient (a parameter that gets no gradient in a step is therefore
-updated with a zero gradient, where the reference skips it; in RRDBNet every parameter is in every backward).
+keeps working.  `zero_grad()` zeroes the flat gradient.  torch's Adam skips a parameter whose .grad is None (and
+keeps a step count per parameter); here every .grad is a view, so step() raises if a parameter does not require grad
+(how a parameter is left out of a backward) instead of updating it with a zero gradient.  In the training step every
+generator / discriminator parameter is in every backward.
 `state_dict()` / `load_state_dict()` use the per-parameter format of torch.optim.Adam, i.e. the reference's
 checkpoint layout (base_model.py:86-111)."""
 import torch
@@ -80,6 +82,11 @@ class FlatAdam(torch.optim.Adam):
     @torch.no_grad()
     def step(self, closure=None):
         self._sync_views()
+        frozen = [i for i, p in enumerate(self.flat_params) if not p.requires_grad]
+        if frozen:
+            # torch's Adam would skip these (grad None) and keep a per-parameter step count; one flat update cannot
+            raise RuntimeError('FlatAdam.step: parameters %s do not require grad (they would be skipped by '
+                               'torch.optim.Adam); unfreeze them or use a per-tensor optimiser' % frozen[:8])
         return super().step(closure)
 
     def state_dict(self):

@@ -650,7 +650,9 @@ class _GeneratorFn(torch.autograd.Function):
         if graphed:
             flat = flat.clone() if flat is not None else None
             dx = dx.clone() if dx is not None else None
-        fg = getattr(ctx.net, '_esr_flat_grad', None)  # the generator's FlatAdam, when no per-parameter hooks wait
+        # the generator's FlatAdam, set by SRRaGANModel.optimize_parameters only around its generator loss's
+        # .backward() (every parameter's AccumulateGrad runs, no per-parameter hooks wait); None everywhere else
+        fg = getattr(ctx.net, '_esr_flat_grad', None)
         if flat is not None and fg is not None and all(ctx.needs_input_grad[3:]) and fg.accepts_flat_grad(bp.params):
             # flat is laid out as the optimiser's buffer: one add instead of 702 per-parameter accumulations (the
             # parameters' .grad are views of fg.flat.grad, so every reader sees the sum)

@@ -21,6 +21,10 @@ Fixtures (tests/golden/):
   ckpt_remap.npz — base_model.load_network + process_loaded_state_dict of a plain (no latent, no CEM prefix) RRDBNet
                  state dict into the latent CEM generator: output key order, per-key SHA-256, the gradient-amplified
                  channel lists.
+  lr_schedule.npz — SRRaGAN_model.update_learning_rate driven per gradient step as train.py:187-189 does
+                 (train_recipe.drive_lr_schedule): the D_loss_STD log, the std_4_lr_drop test, the rollback through
+                 load(max_step=cur_step-steps_4_loss_std, resume_train=True), the LR x lr_gamma, lr.npz, LR_decrease and
+                 the lr_too_low return.
   ckpt/7_G.pth — written by base_model.save_network (model_state_dict on the CPU + Adam optimizer_state_dict with
                  state for three parameters), read back by the test with torch.load(weights_only=True).
 """
@@ -40,7 +44,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 import make_golden as MG  # noqa: E402
 from oracle.recipe import seeded_params  # noqa: E402
-from train_recipe import CKPT_CFG, TRAIN_CFGS, random_points, step_data, train_opt  # noqa: E402
+from train_recipe import CKPT_CFG, LR_CFG, TRAIN_CFGS, drive_lr_schedule, random_points, step_data, train_opt  # noqa: E402,E501
 
 SMALL = 4096  # keys with at most this many elements get their full parameter change stored
 
@@ -217,13 +221,31 @@ def checkpoint_fixtures():
     print('ckpt_save: %s (%d bytes), state for params %s' % (p, os.path.getsize(p), sorted(st['state'])))
 
 
+def lr_schedule_fixture():
+    import shutil
+    cfg = dict(LR_CFG)
+    for d in ('/tmp/esr_golden_train_models', '/tmp/esr_golden_train_log'):
+        shutil.rmtree(d, ignore_errors=True)
+        os.makedirs(d)
+    model = build_reference(cfg, torch.float32)
+    records, dec = drive_lr_schedule(model, cfg)
+    with np.load('/tmp/esr_golden_train_log/lr.npz') as f:
+        lr_file = np.array([f['step_num'], f['lr_G'], f['lr_D']], dtype=np.float64)
+    np.savez_compressed(os.path.join(HERE, 'lr_schedule.npz'), cfg=np.str_(json.dumps(cfg)), records=records,
+                        lr_decrease=dec, lr_file=lr_file)
+    print('lr_schedule: %d calls, returns %s, LR_decrease %s, lr.npz %s' % (
+        len(records), records[:, 1].tolist(), dec.tolist(), lr_file.tolist()))
+
+
 def main():
     install_train_shims()
     torch.set_num_threads(8)
-    which = sys.argv[1:] or list(TRAIN_CFGS) + ['ckpt']
+    which = sys.argv[1:] or list(TRAIN_CFGS) + ['ckpt', 'lr']
     for name in which:
         if name == 'ckpt':
             checkpoint_fixtures()
+        elif name == 'lr':
+            lr_schedule_fixture()
         else:
             train_fixture(name, TRAIN_CFGS[name])
 

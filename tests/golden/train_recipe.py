@@ -24,7 +24,9 @@ def train_opt(cfg):
                       'act_type': 'leakyrelu', 'mode': 'CNA', 'n_layers': 6, 'nf': 64, 'in_nc': 3},
         'train': {'resume': 0, 'lr_G': cfg['lr'], 'weight_decay_G': 0, 'beta1_G': 0.9, 'lr_D': cfg['lr'],
                   'lr_E': 1e-4, 'lr_latent': cfg['lr'], 'weight_decay_D': 0, 'beta1_D': 0.9,
-                  'lr_scheme': 'MultiStepLR', 'lr_steps': [50000], 'lr_gamma': 0.5, 'pixel_domain': 'HR',
+                  'lr_scheme': 'MultiStepLR', 'lr_steps': [50000], 'lr_gamma': cfg.get('lr_gamma', 0.5),
+                  'steps_4_loss_std': cfg.get('steps_4_loss_std'), 'std_4_lr_drop': cfg.get('std_4_lr_drop'),
+                  'pixel_domain': 'HR',
                   'pixel_criterion': 'l1', 'feature_domain': 'HR', 'feature_criterion': 'l1', 'gan_type': 'wgan-gp',
                   'optimalZ_loss_type': None, 'D_verification': cfg['D_verification'],
                   'min_D_prob_ratio_4_G': cfg['min_D_prob_ratio_4_G'], 'min_mean_D_correct': cfg['min_mean_D_correct'],
@@ -64,3 +66,49 @@ CKPT_CFG = dict(nb=1, batch=2, lr_size=40, lr=1e-4, relativistic=0, D_update_rat
                 D_valid_steps=1, min_D_prob_ratio_4_G=1.0, min_mean_D_correct=0.0, acc=1, steps=0, seed=700)
 
 
+
+# update_learning_rate (SRRaGAN_model.py:637-683) as train.py:187-189 drives it: one call per gradient step, D losses
+# whose spread jumps at step 10 (std over a 4-step window: ~0.01 before, ~0.5 after, threshold 0.05), checkpoints at
+# gradient steps 2 and 5 (saved only before the first LR drop), lr_gamma 0.05 so that the fourth drop takes the LR
+# below 1e-8 (the `lr_too_low` return)
+LR_CFG = dict(CKPT_CFG, seed=710, steps_4_loss_std=4, std_4_lr_drop=0.05, lr_gamma=0.05, ckpt_steps=[2, 5],
+              n_calls=60, probe='generated_image_model.model.0.bias')
+
+
+def lr_log_rows(cfg, g):
+    """(l_d_real, l_d_fake, D_logits_diff) logged at gradient step g."""
+    amp = 0.01 if g < 10 else 0.5
+    return 1.0 + amp * np.random.default_rng(cfg['seed'] * 1000 + g).standard_normal(3)
+
+
+def drive_lr_schedule(model, cfg):
+    """train.py's per-step sequence around update_learning_rate, with the D logs and a parameter change ("training")
+    made up: returns one record per call: [cur_step, returned lr_too_low, lr_G, lr_D, model.step after the call,
+    len(D_loss_STD), last D_loss_STD (nan if none), len(LR_decrease), summed change of the probe parameter] and the
+    LR_decrease entries as [step, lr_G, lr_D].  Works on the reference's model and on esr_amd's (same methods)."""
+    import torch
+    acc = cfg['acc']
+    probe = dict(model.netG.named_parameters())[cfg['probe']]
+    start = probe.detach().double().clone()
+    records = []
+    for _ in range(cfg['n_calls']):
+        g = model.step // acc
+        model.gradient_step_num = g  # optimize_parameters' first statement (SRRaGAN_model.py:308)
+        for k, v in zip(('l_d_real', 'l_d_fake', 'D_logits_diff'), lr_log_rows(cfg, g)):
+            model.log_dict[k].append((g, float(v)))
+        with torch.no_grad():
+            probe.add_(1e-3 * (g + 1))
+        model.step += acc
+        if g in cfg['ckpt_steps'] and not model.log_dict['LR_decrease']:
+            model.save(g)
+            model.save_log()
+        ret = model.update_learning_rate(g)
+        std = model.log_dict['D_loss_STD']
+        records.append([g, float(bool(ret)), model.optimizer_G.param_groups[0]['lr'],
+                        model.optimizer_D.param_groups[0]['lr'], model.step, len(std),
+                        float(std[-1][1]) if std else float('nan'), len(model.log_dict['LR_decrease']),
+                        float((probe.detach().double() - start).sum())])
+        if ret:
+            break
+    dec = [[e[0], e[1]['lr_G'], e[1]['lr_D']] for e in model.log_dict['LR_decrease']]
+    return np.array(records, dtype=np.float64), np.array(dec, dtype=np.float64).reshape(-1, 3)

@@ -84,3 +84,16 @@ def test_flat_adam_reattaches_replaced_tensors():
     for pa, pb in zip(a, b):
         assert torch.equal(pa.detach(), pb.detach())
     assert b[2].data_ptr() == ob.flat.data_ptr() + 4 * sum(p.numel() for p in b[:2])
+
+
+def test_flat_adam_refuses_a_frozen_parameter():
+    """torch.optim.Adam skips a parameter that got no gradient; FlatAdam cannot, so it raises instead of moving it."""
+    import pytest
+    ps = _params(3)
+    opt = FlatAdam(ps, lr=1e-3)
+    opt.zero_grad()
+    ps[1].requires_grad_(False)
+    with pytest.raises(RuntimeError, match='do not require grad'):
+        opt.step()
+    ps[1].requires_grad_(True)
+    opt.step()

@@ -38,15 +38,16 @@ PROJ_REL = 0.05
 
 
 def _close(mine, f32, f64, scale=None, rel=0.0):
+    """(ok, message, err / bound)."""
     mine, f32, f64 = (np.asarray(v, dtype=np.float64).ravel() for v in (mine, f32, f64))
     err, base, norm = np.linalg.norm(mine - f64), np.linalg.norm(f32 - f64), np.linalg.norm(f64)
     scale = norm if scale is None else scale
     bound = FACTOR * base + FLOOR * max(scale, 1e-12) + rel * norm
-    return err <= bound, 'err %.3e  bound %.3e  (ref f32 err %.3e, |ref| %.3e, scale %.3e)' % (
-        err, bound, base, norm, scale)
+    return err <= bound, 'err %.3e  bound %.3e  (%5.1f %% of bound; ref f32 err %.3e, |ref| %.3e, scale %.3e)' % (
+        err, bound, 100 * err / bound, base, norm, scale), err / bound
 
 
-def _run_port(cfg, precision, dev):
+def _run_port(cfg, precision, dev, d_precision=None):
     from esr_amd import dconv, engine
     from esr_amd.SRRaGAN_model import SRRaGANModel
     torch.manual_seed(0)
@@ -58,9 +59,9 @@ def _run_port(cfg, precision, dev):
     model.netG.load_state_dict({k: torch.from_numpy(v) for k, v in gp.items()}, strict=False)
     model.netD.load_state_dict({k: torch.from_numpy(v) for k, v in dp.items()}, strict=False)
     engine.set_precision(model.netG, precision)
-    # the whole step in one precision: exact fp32 also for the discriminator convolutions and the generator backward
-    # (the x3 backward only runs after an x3 forward)
-    dconv.set_precision(precision)
+    # by default the whole step in one precision: exact fp32 also for the discriminator convolutions and the generator
+    # backward (the x3 backward only runs after an x3 forward); d_precision splits them (tools/loop_margin.py)
+    dconv.set_precision(precision if d_precision is None else d_precision)
     pts = random_points(cfg)
     model._interp_points = lambda n: torch.from_numpy(next(pts)).to(dev).view(n, 1, 1, 1)
     g0 = {k: v.detach().clone() for k, v in model.netG.named_parameters()}
@@ -75,19 +76,18 @@ def _run_port(cfg, precision, dev):
     return model, g0, d0, flags
 
 
-@pytest.mark.parametrize('precision', ['x3', 'f32'])
-@pytest.mark.parametrize('name', sorted(TRAIN_CFGS))
-def test_optimize_parameters_vs_reference_loop(gpu_device, name, precision):
+def loop_margins(name, precision, dev, d_precision=None):
+    """Run the port on fixture `name`; return (generator_step flags ok, [(kind, key, ok, message, err/bound)])."""
     from esr_amd import dconv
     d = np.load(os.path.join(HERE, 'golden', 'train_%s.npz' % name))
     cfg = json.loads(str(d['cfg']))
     prev = dconv.PRECISION
     try:
-        model, g0, d0, flags = _run_port(cfg, precision, gpu_device)
+        model, g0, d0, flags = _run_port(cfg, precision, dev, d_precision)
     finally:
         dconv.set_precision(prev)
-    assert flags == list(d['f64_generator_step']) == list(d['f32_generator_step'])
-    fails = []
+    flags_ok = flags == list(d['f64_generator_step']) == list(d['f32_generator_step'])
+    rows = []
     for f in [f for f in d.files if f.startswith('f64_log:')]:
         key = f[len('f64_log:'):]
         ref64, ref32 = d[f], d['f32_log:' + key]
@@ -97,10 +97,7 @@ def test_optimize_parameters_vs_reference_loop(gpu_device, name, precision):
         scale = None
         if key in D_DIFFERENCES:
             scale = 2 * (np.linalg.norm(d['f64_log:D_real'][:, 1]) + np.linalg.norm(d['f64_log:D_fake'][:, 1]))
-        ok, msg = _close(mine[:, 1], ref32[:, 1], ref64[:, 1], scale)
-        print('log %-24s %s' % (key, msg))
-        if not ok:
-            fails.append(('log', key, msg))
+        rows.append(('log', key) + _close(mine[:, 1], ref32[:, 1], ref64[:, 1], scale))
     for net, start, tag in ((model.netG, g0, 'G'), (model.netD, d0, 'D')):
         named = dict(net.named_parameters())
         rng = np.random.default_rng(cfg['seed'] + (400 if tag == 'G' else 401))
@@ -119,18 +116,22 @@ def test_optimize_parameters_vs_reference_loop(gpu_device, name, precision):
                 for r in ('32', '64'):
                     small[r].append(d['f%s_%s_delta:%s' % (r, tag, k)].ravel())
         for what, v, rel in (('update norms', dn, 0.0), ('update projections', dp, PROJ_REL)):
-            ok, msg = _close(v['m'], v['32'], v['64'], rel=rel)
-            print('%s %-20s %s' % (tag, what, msg))
-            if not ok:
-                fails.append((tag, what, msg))
+            rows.append((tag, what) + _close(v['m'], v['32'], v['64'], rel=rel))
         if small['m']:
-            ok, msg = _close(*(np.concatenate(small[r]) for r in ('m', '32', '64')))
-            print('%s %-20s %s' % (tag, 'small-key updates', msg))
-            if not ok:
-                fails.append((tag, 'small-key updates', msg))
+            rows.append((tag, 'small-key updates') + _close(*(np.concatenate(small[r]) for r in ('m', '32', '64'))))
     for k, v in model.netD.state_dict().items():
         if 'running' in k:
-            ok, msg = _close(v.double().cpu().numpy(), d['f32_Dbuf:' + k], d['f64_Dbuf:' + k])
-            if not ok:
-                fails.append(('D buffer', k, msg))
+            rows.append(('D buffer', k) + _close(v.double().cpu().numpy(), d['f32_Dbuf:' + k], d['f64_Dbuf:' + k]))
+    return flags_ok, rows
+
+
+@pytest.mark.parametrize('precision', ['x3', 'f32'])
+@pytest.mark.parametrize('name', sorted(TRAIN_CFGS))
+def test_optimize_parameters_vs_reference_loop(gpu_device, name, precision):
+    flags_ok, rows = loop_margins(name, precision, gpu_device)
+    assert flags_ok
+    for kind, key, ok, msg, _ in rows:
+        print('%-8s %-24s %s' % (kind, key, msg))
+    fails = [(kind, key, msg) for kind, key, ok, msg, _ in rows if not ok]
+    print('worst quantity at %.1f %% of its bound' % (100 * max(r[4] for r in rows)))
     assert not fails, fails
