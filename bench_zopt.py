@@ -21,14 +21,12 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 
-def learned_kernel(size=13, sigma=(1.6, 2.6), theta=np.pi / 6):
-    """Synthetic anisotropic Gaussian standing in for a KernelGAN estimate (no dataset / network here)."""
-    r = np.arange(size) - (size - 1) / 2
-    X, Y = np.meshgrid(r, r)
-    c, s = np.cos(theta), np.sin(theta)
-    u, v = c * X + s * Y, -s * X + c * Y
-    k = np.exp(-0.5 * ((u / sigma[0]) ** 2 + (v / sigma[1]) ** 2))
-    return k / k.sum()
+def learned_kernel():
+    """The learned (non-bicubic) 13×13 kernel of the reference-made CEM fixture (tests/golden/cem_learned13.npz,
+    `input_kernel`: the kernel tests/golden/make_golden.py fed the reference's CEM filter design; no KernelGAN run
+    or dataset here).  With it CEM's margins are 13 LR / 52 HR pixels, so the generator runs at 154² per image."""
+    with np.load(os.path.join(REPO, 'tests', 'golden', 'cem_learned13.npz')) as f:
+        return np.asarray(f['input_kernel'], dtype=np.float64)
 
 
 def leg_args(**kw):

@@ -181,6 +181,156 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_kernel(FwdParams p) {
     }
 }
 
+// ---- halo-tile forward (exact fp32, the default) -----------------------------------------------------------------------
+// The same gather-GEMM, but a workgroup owns a 2-D output tile (TY rows × 32 columns of the MH × MW grid of one image)
+// instead of 256 pixel-linear outputs, so the source pixels of ALL taps of a 32-channel chunk are one halo window that
+// is staged in LDS once per chunk: IY = smy·(TY-1) + span_y + 1 rows × (smx·31 + span_x + 1) columns (span = max - min
+// tap offset).  The gather kernel re-stages the 256 source rows of every (tap, chunk) step: 9 / 16 / 64 × the rows for
+// the 3×3 / 4×4 / 8×8 convolutions, which made it L2→LDS-staging-bound at ≈half the f32 MFMA rate.
+// Stride-2 sources (the 4×4 s2 forward) are stored de-interleaved by column parity (parity-major, then half-column), so
+// the 32 lanes of a fragment read consecutive LDS pixels for every tap: pixel pitch 36 floats → the 16 lanes of a
+// ds_read_b128 group hit 16 distinct 4-bank slots.  The weights of one (tap, chunk) step (64 output channels × 32)
+// are prefetched into registers during the previous step and staged through a small LDS slab, as the gather kernel.
+// Wave w of 4 owns WM M-tiles (output rows) × WN N-tiles (32 channels) of v_mfma_f32_32x32x2_f32; TY = 2·WM·WN.
+// Split-K (gridDim.z > 1) divides the chunks; the raw sums go to `partial` for dconv_splitk_reduce.
+struct HaloParams {
+    int TY, tiles_x, tiles_y;  // tile rows; tiles per image row / column
+    int IY, IXp, npar, IXt;    // halo rows; columns per parity; parities (= smx); IXt = npar·IXp
+    int oymin, oxmin;          // smallest tap offsets
+    int b_off;                 // byte offset of the weight slab in LDS
+};
+
+template <int WM, int WN>
+__global__ __launch_bounds__(NTH, 2) void dconv_fwd_halo_kernel(FwdParams p, HaloParams h) {
+    constexpr int TY = 2 * WM * WN, MW_ = TY / WM;  // waves along M
+    extern __shared__ __attribute__((aligned(16))) float dlds[];
+    float *s_a = dlds, *s_b = dlds + h.b_off / 4;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hl = lane >> 5, ml = lane & 31;
+    int id = blockIdx.x;
+    const int txi = id % h.tiles_x;
+    id /= h.tiles_x;
+    const int tyi = id % h.tiles_y, b = id / h.tiles_y;
+    const int Y0 = tyi * TY, X0 = txi * 32;
+    const int n0 = blockIdx.y * NB;
+    const int wm = wave % MW_, wn = wave / MW_;
+    const bool vec = p.vec != 0;
+    const int sy0 = p.smy * Y0 + h.oymin, sx0 = p.smx * X0 + h.oxmin;
+    const int c_begin = (int)((long long)p.nck * blockIdx.z / gridDim.z);
+    const int c_end = (int)((long long)p.nck * (blockIdx.z + 1) / gridDim.z);
+    const int nsteps = (c_end - c_begin) * p.T;
+
+    f32x4 rb[B_IT];
+    auto load_b = [&](int step) {
+        const int j = c_begin + step / p.T, t = step - (step / p.T) * p.T;
+        const float *wj = p.w + ((long long)(t * p.nck + j) * p.n_pad + n0) * KC;
+#pragma unroll
+        for (int k = 0; k < B_IT; ++k) rb[k] = *reinterpret_cast<const f32x4 *>(wj + (tid + k * NTH) * 4);
+    };
+    // the halo window of chunk j: every thread stages (pixel, 4-channel quad) items, 8 loads in flight at a time
+    auto stage_a = [&](int j) {
+        const int total = h.IY * h.IXt * 8;
+        const float *img = p.src + (long long)b * p.Hs * p.Ws * p.sp;
+        for (int base = 0; base < total; base += 8 * NTH) {
+            f32x4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int idx = base + u * NTH + tid;
+                v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+                if (idx < total) {
+                    const int pix = idx >> 3, q = idx & 7;
+                    const int r = pix / h.IXt, cc = pix - r * h.IXt;
+                    const int par = cc / h.IXp, hc = cc - par * h.IXp;
+                    const int sy = sy0 + r, sx = sx0 + hc * h.npar + par, c = j * KC + 4 * q;
+                    if (sy >= 0 && sy < p.Hs && sx >= 0 && sx < p.Ws && c < p.kc)
+                        v[u] = load4(img + ((long long)sy * p.Ws + sx) * p.sp, c, p.kc, vec);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int idx = base + u * NTH + tid;
+                if (idx < total) *reinterpret_cast<f32x4 *>(s_a + (idx >> 3) * PS + 4 * (idx & 7)) = v[u];
+            }
+        }
+    };
+
+    f32x16 acc[WM][WN];
+#pragma unroll
+    for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int k = 0; k < WN; ++k)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][k][r] = 0.f;
+
+    if (nsteps > 0) load_b(0);
+    for (int step = 0; step < nsteps; ++step) {
+        const int t = step % p.T;
+        __syncthreads();
+        if (t == 0) stage_a(c_begin + step / p.T);
+#pragma unroll
+        for (int k = 0; k < B_IT; ++k) {
+            const int idx = tid + k * NTH;
+            *reinterpret_cast<f32x4 *>(s_b + (idx >> 3) * PS + (idx & 7) * 4) = rb[k];
+        }
+        __syncthreads();
+        if (step + 1 < nsteps) load_b(step + 1);
+        const int dy = p.offy[t] - h.oymin, dx = p.offx[t] - h.oxmin;
+        const int col = (h.npar == 1) ? ml + dx : (dx & 1) * h.IXp + ml + (dx >> 1);
+        const float *a_base[WM];
+#pragma unroll
+        for (int i = 0; i < WM; ++i) {
+            const int ty = wm * WM + i;
+            a_base[i] = s_a + ((p.smy * ty + dy) * h.IXt + col) * PS + 16 * hl;
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            f32x4 av[WM], bv[WN];
+#pragma unroll
+            for (int i = 0; i < WM; ++i) av[i] = *reinterpret_cast<const f32x4 *>(a_base[i] + 4 * g);
+#pragma unroll
+            for (int k = 0; k < WN; ++k)
+                bv[k] = *reinterpret_cast<const f32x4 *>(s_b + ((wn * WN + k) * 32 + ml) * PS + 16 * hl + 4 * g);
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int i = 0; i < WM; ++i)
+#pragma unroll
+                    for (int k = 0; k < WN; ++k)
+                        acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i][s], bv[k][s], acc[i][k], 0, 0, 0);
+        }
+    }
+
+    // D layout (32x32 f32 MFMA): lane holds column n = lane & 31, rows m = (r&3) + 8(r>>2) + 4(lane>>5) = X - X0
+    const long long per_img = (long long)p.MH * p.MW;
+#pragma unroll
+    for (int i = 0; i < WM; ++i) {
+        const int Y = Y0 + wm * WM + i;
+        if (Y >= p.MH) continue;
+#pragma unroll
+        for (int k = 0; k < WN; ++k) {
+            const int nl = (wn * WN + k) * 32 + ml, n = n0 + nl;
+            if (gridDim.z > 1) {  // raw partial sums, pixel-linear; bias and the output map are the reduction's
+                float *part = p.partial + (long long)blockIdx.z * p.B * per_img * p.n_pad;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int X = X0 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+                    if (X < p.MW) part[(b * per_img + (long long)Y * p.MW + X) * p.n_pad + n] = acc[i][k][r];
+                }
+                continue;
+            }
+            if (n >= p.n) continue;
+            const float bn = p.bias ? p.bias[n] : 0.f;
+            const int oy = p.omy * Y + p.oay;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int X = X0 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+                if (X >= p.MW) continue;
+                const int ox = p.omx * X + p.oax;
+                p.out[(((long long)b * p.Ho + oy) * p.Wo + ox) * p.op + n] = acc[i][k][r] + bn;
+            }
+        }
+    }
+}
+
 // ---- x3 forward (split-f16 operands, fp32-level accuracy) -------------------------------------------------------------
 // The same gather-GEMM on v_mfma_f32_32x32x16_f16: every staged fp32 operand value v is carried as hi = f16(v·s),
 // lo = f16(v·s - hi) and a product as a_hi·b_hi + a_hi·b_lo + a_lo·b_hi (esr_conv_x3.hip's scheme), with the split
@@ -700,9 +850,56 @@ __global__ __launch_bounds__(NTH, 2) void dconv_wgrad_x3_kernel(WgradParams p) {
 
 bool aligned16(const void *ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; }
 
+constexpr int HALO_LDS_2PER_CU = 80 * 1024;  // two workgroups per CU
+constexpr int HALO_LDS_MAX = 160 * 1024;
+
+// Halo tiling of an exact-fp32 esr_dconv_fwd launch: false if the gather kernel has to run it (stride > 2, or a halo
+// that does not fit in LDS even at 2-row tiles).
+bool halo_plan(int MH, int MW, int smy, int smx, int T, const int32_t *offy, const int32_t *offx, HaloParams &h,
+               int &lds) {
+    if (smy < 1 || smy > 2 || smx < 1 || smx > 2) return false;
+    int ymin = offy[0], ymax = offy[0], xmin = offx[0], xmax = offx[0];
+    for (int t = 1; t < T; ++t) {
+        ymin = min(ymin, (int)offy[t]); ymax = max(ymax, (int)offy[t]);
+        xmin = min(xmin, (int)offx[t]); xmax = max(xmax, (int)offx[t]);
+    }
+    h.oymin = ymin;
+    h.oxmin = xmin;
+    h.npar = smx;
+    h.IXp = smx == 1 ? 32 + (xmax - xmin) : 32 + ((xmax - xmin) >> 1);
+    h.IXt = h.npar * h.IXp;
+    const int b_bytes = NB * PS * 4;
+    for (int pass = 0; pass < 2; ++pass) {
+        const int budget = pass == 0 ? HALO_LDS_2PER_CU : HALO_LDS_MAX;
+        for (int ty = 8; ty >= 2; ty >>= 1) {
+            if (ty > 2 && MH <= ty / 2) continue;  // a shorter tile wastes fewer rows
+            const int iy = smy * (ty - 1) + (ymax - ymin) + 1;
+            const int a_bytes = iy * h.IXt * PS * 4;
+            if (a_bytes + b_bytes <= budget) {
+                h.TY = ty;
+                h.IY = iy;
+                h.b_off = a_bytes;
+                h.tiles_x = (MW + 31) / 32;
+                h.tiles_y = (MH + ty - 1) / ty;
+                lds = a_bytes + b_bytes;
+                return true;
+            }
+        }
+    }
+    return false;
+}
+
+// split-K slices for a halo launch: enough workgroups to fill the chip twice, at least one chunk per slice
+int halo_splits(const HaloParams &h, int B, int n_pad, int nck) {
+    const long long wgs = (long long)B * h.tiles_x * h.tiles_y * (n_pad / NB);
+    if (wgs >= 512 || nck < 2) return 1;
+    return (int)min((long long)nck, (512 + wgs - 1) / wgs);
+}
+
 }  // namespace
 
 int g_dconv_x3 = 0;   // esr_dconv_set_x3
+int g_dconv_halo = 1; // esr_dconv_set_halo: exact-fp32 forward on the halo-tile kernel where it applies
 int g_dconv_nb = 128; // x3: widest N tile allowed (esr_dconv_set_x3(2) = 64 only, for A/B)
 
 extern "C" int esr_dconv_fwd_sk(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t src_pitch, int32_t kc,
@@ -712,7 +909,7 @@ extern "C" int esr_dconv_fwd_sk(const float *src, int32_t B, int32_t Hs, int32_t
                                 const int32_t *offy, const int32_t *offx, int32_t ksplit, float *partial,
                                 esr_stream_t stream) {
     if (!src || !w_packed || !out || !offy || !offx) return ESR_EINVAL;
-    if (ksplit < 1 || (ksplit > 1 && (!partial || !g_dconv_x3 || ksplit > T * nck))) return ESR_EINVAL;
+    if (ksplit < 1 || (ksplit > 1 && (!partial || ksplit > T * nck))) return ESR_EINVAL;
     if (B <= 0 || Hs <= 0 || Ws <= 0 || kc <= 0 || src_pitch < kc || n <= 0 || out_pitch < n || MH <= 0 || MW <= 0)
         return ESR_EINVAL;
     if (T <= 0 || T > ESR_DCONV_MAX_TAPS || nck != (kc + KC - 1) / KC || n_pad % NB || n_pad < n) return ESR_EINVAL;
@@ -731,6 +928,22 @@ extern "C" int esr_dconv_fwd_sk(const float *src, int32_t B, int32_t Hs, int32_t
     const long long M = (long long)B * MH * MW;
     const long long gx = (M + MT - 1) / MT;
     if (gx > 0x7fffffff) return ESR_EINVAL;
+    HaloParams h;
+    int lds = 0;
+    if (!g_dconv_x3 && g_dconv_halo && halo_plan(MH, MW, smy, smx, T, offy, offx, h, lds)) {
+        if (ksplit > nck) return ESR_EINVAL;  // the halo kernel splits the channel chunks
+        const long long hx = (long long)B * h.tiles_x * h.tiles_y;
+        if (hx > 0x7fffffff) return ESR_EINVAL;
+        const dim3 hgrid((unsigned)hx, (unsigned)(n_pad / NB), (unsigned)ksplit), block(NTH);
+        const hipStream_t st = (hipStream_t)stream;
+        if (h.TY == 8) hipLaunchKernelGGL((dconv_fwd_halo_kernel<2, 2>), hgrid, block, lds, st, p, h);
+        else if (h.TY == 4) hipLaunchKernelGGL((dconv_fwd_halo_kernel<1, 2>), hgrid, block, lds, st, p, h);
+        else hipLaunchKernelGGL((dconv_fwd_halo_kernel<1, 1>), hgrid, block, lds, st, p, h);
+        if (ksplit > 1)
+            hipLaunchKernelGGL(dconv_splitk_reduce, dim3((unsigned)((M * n + NTH - 1) / NTH)), block, 0, st, p,
+                               ksplit);
+        return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+    }
     const dim3 grid((unsigned)gx, (unsigned)((n + NB - 1) / NB)), block(NTH);
     // 128-channel N tiles only where the grid still fills the chip (the A tile then feeds twice the MFMAs)
     const bool wide = n_pad % 128 == 0 && g_dconv_nb != 64 && gx * (n_pad / 128) * ksplit >= 512;
@@ -755,6 +968,30 @@ extern "C" int esr_dconv_fwd(const float *src, int32_t B, int32_t Hs, int32_t Ws
                              const int32_t *offy, const int32_t *offx, esr_stream_t stream) {
     return esr_dconv_fwd_sk(src, B, Hs, Ws, src_pitch, kc, w_packed, nck, n_pad, bias, out, Ho, Wo, out_pitch, n, MH,
                             MW, omy, oay, omx, oax, smy, smx, T, offy, offx, 1, nullptr, stream);
+}
+
+extern "C" int esr_dconv_fwd_splits(int32_t B, int32_t MH, int32_t MW, int32_t n, int32_t kc, int32_t smy,
+                                    int32_t smx, int32_t T, const int32_t *offy, const int32_t *offx) {
+    if (B <= 0 || MH <= 0 || MW <= 0 || n <= 0 || kc <= 0 || T <= 0 || T > ESR_DCONV_MAX_TAPS || !offy || !offx)
+        return ESR_EINVAL;
+    const int nck = (kc + KC - 1) / KC, n_pad = NB * ((n + NB - 1) / NB);
+    HaloParams h;
+    int lds = 0;
+    if (!g_dconv_x3 && g_dconv_halo && halo_plan(MH, MW, smy, smx, T, offy, offx, h, lds))
+        return halo_splits(h, B, n_pad, nck);
+    if (!g_dconv_x3) return 1;
+    // x3 gather kernel: ~512 workgroups, at least 8 K steps per slice, for launches that would fill few CUs
+    const long long wgs = ((long long)B * MH * MW + MT - 1) / MT * (n_pad / NB);
+    const int nsteps = T * nck;
+    if (wgs >= 512 || nsteps < 16) return 1;
+    return (int)max(1LL, min((512 + wgs - 1) / wgs, (long long)(nsteps / 8)));
+}
+
+extern "C" int esr_dconv_set_halo(int32_t on) {
+    if (on < 0 || on > 1) return ESR_EINVAL;
+    const int prev = g_dconv_halo;
+    g_dconv_halo = on;
+    return prev;
 }
 
 extern "C" int esr_dconv_set_x3(int32_t on) {

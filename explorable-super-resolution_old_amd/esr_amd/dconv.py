@@ -29,6 +29,8 @@ _WG_PARTIAL_MAX = 64 << 20       # floats of split-K partials per launch
 # Precision of the gather-GEMM forward / data-gradient launches: 'x3' (default) = split-f16 operands with per-K-step
 # power-of-two scaling on f16 MFMA (fp32-level accuracy, esr_dconv.hip), 'f32' = exact fp32 MFMA.
 PRECISION = os.environ.get('ESR_DCONV_PRECISION', 'x3')
+# exact-fp32 forward / data-gradient kernel: the halo-tile implicit GEMM (default) or the per-tap gather ('0', A/B)
+HALO = os.environ.get('ESR_DCONV_HALO', '1') != '0'
 _applied = [None]
 
 
@@ -45,6 +47,7 @@ def _lib_for_launch():
     lib = _lib.load()
     if _applied[0] != PRECISION:
         lib.esr_dconv_set_x3(1 if PRECISION == 'x3' else 0)
+        lib.esr_dconv_set_halo(1 if HALO else 0)
         _applied[0] = PRECISION
     return lib
 
@@ -107,17 +110,15 @@ def _gather(src, packed, bias, out, MH, MW, omy, oay, omx, oax, smy, smx, offy, 
     _, Ho, Wo, N = out.shape
     wp, nck, n_pad = packed
     lib = _lib_for_launch()
-    # split-K (x3) where the grid would fill few CUs and K is long (the 8x8 pseudo-FC layer): ~512 workgroups,
-    # at least 8 K steps per slice
-    wgs = -(-B * MH * MW // 256) * (n_pad // 64)
-    nsteps = len(offy) * nck
-    ks = 1
-    if PRECISION == 'x3' and wgs < 512 and nsteps >= 16:
-        ks = max(1, min(-(-512 // wgs), nsteps // 8))
+    oy, ox = _i32(offy), _i32(offx)
+    # split-K where the grid would fill few CUs and K is long (the 8x8 pseudo-FC layer); the library says how many
+    ks = lib.esr_dconv_fwd_splits(B, MH, MW, N, C, smy, smx, len(offy), oy, ox)
+    if ks < 1:
+        raise RuntimeError('esr_dconv_fwd_splits failed with esr_status %d' % ks)
     part = torch.empty(ks * B * MH * MW * n_pad, device=src.device) if ks > 1 else None
     _lib.check(lib.esr_dconv_fwd_sk(src.data_ptr(), B, Hs, Ws, C, C, wp.data_ptr(), nck, n_pad,
                                     None if bias is None else bias.data_ptr(), out.data_ptr(), Ho, Wo, N, N, MH, MW,
-                                    omy, oay, omx, oax, smy, smx, len(offy), _i32(offy), _i32(offx), ks,
+                                    omy, oay, omx, oax, smy, smx, len(offy), oy, ox, ks,
                                     None if part is None else part.data_ptr(), _stream(src)),
                'esr_dconv_fwd')
 

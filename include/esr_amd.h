@@ -257,7 +257,8 @@ int esr_dconv_fwd(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t s
                   int32_t Wo, int32_t out_pitch, int32_t n_out, int32_t MH, int32_t MW, int32_t omy, int32_t oay,
                   int32_t omx, int32_t oax, int32_t smy, int32_t smx, int32_t T, const int32_t *offy,
                   const int32_t *offx, esr_stream_t stream);
-/* esr_dconv_fwd with split-K over ksplit workgroup slices of the K steps (x3 precision only; for the small-M,
+/* esr_dconv_fwd with split-K over ksplit workgroup slices of the K steps (x3) or of the 32-channel chunks (fp32
+ * halo kernel) — for the small-M,
  * long-K launches — the 8×8 pseudo-FC layer — that would fill few CUs): partial = caller buffer of
  * ksplit·MH·MW·B·n_pad floats; a second kernel sums the slices in order (deterministic) and applies bias and the
  * output map.  ksplit = 1 is esr_dconv_fwd. */
@@ -266,6 +267,16 @@ int esr_dconv_fwd_sk(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_
                      int32_t Wo, int32_t out_pitch, int32_t n, int32_t MH, int32_t MW, int32_t omy, int32_t oay,
                      int32_t omx, int32_t oax, int32_t smy, int32_t smx, int32_t T, const int32_t *offy,
                      const int32_t *offx, int32_t ksplit, float *partial, esr_stream_t stream);
+/* The ksplit esr_dconv_fwd_sk should get for this launch geometry under the current precision setting (1 = no
+ * split); the caller allocates `partial` accordingly.  Exact fp32: the halo-tile kernel splits the 32-channel chunks
+ * where its grid has < 512 workgroups (the 8×8 pseudo-FC layer); x3: ~512 workgroups, >= 8 K steps per slice. */
+int esr_dconv_fwd_splits(int32_t B, int32_t MH, int32_t MW, int32_t n_out, int32_t kc, int32_t smy, int32_t smx,
+                         int32_t T, const int32_t *offy, const int32_t *offx);
+/* Exact-fp32 esr_dconv_fwd kernel: 1 (default) = halo-tile implicit GEMM (each source pixel of a 32-channel chunk
+ * staged in LDS once for all taps; strides 1 and 2) where the halo fits in LDS, the gather kernel otherwise; 0 = the
+ * gather kernel always (A/B).  Bitwise-different summation order only through the split-K slices.  Returns the
+ * previous setting. */
+int esr_dconv_set_halo(int32_t on);
 /* Precision of esr_dconv_fwd (process-wide): 0 (the library default) = exact fp32 MFMA; 1 = x3: both operands split
  * into f16 hi/lo at staging after a power-of-two scaling per K step (one tap × 32 channels) chosen from the
  * workgroup's max |a| and max |b|, products hi·hi + hi·lo + lo·hi on f16 MFMA, the fp32 accumulators rescaled exactly

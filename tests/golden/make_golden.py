@@ -242,6 +242,60 @@ def zgrad_fixture(arch, CEMnet, name, cem_mode, lr_shape, seed, w_scale, kernel=
     print('zgrad_%s: |dz| %.3e |dlr| %.3e' % (name, np.abs(d['dz']).mean(), np.abs(d['dlr']).mean()))
 
 
+# config 5 at its production grid: the latent RRDB-23 + CEM (eval, pre-pad) with the learned
+# 13×13 kernel, B=8 × 128² LR; the reference computes images 0 and 7 of the batch (eval mode: images independent).
+Z_GRID = dict(B=8, h=128, nb=23, seed=820, w_scale=0.1, images=[0, 7], proj=16)
+
+
+def _digest(v, seed, idx, k):
+    g = np.asarray(v, dtype=np.float64).ravel()
+    return np.random.default_rng([seed, idx]).standard_normal((k, g.size)) @ g
+
+
+def zgrid_fixture(arch, CEMnet):
+    """Z-optimisation input gradients (Z_optimization.py:545-630, generator frozen, loss = Σ out·R) at config 5's grid,
+    float64 and float32: K seeded random projections + norms of dL/dZ, dL/dLR and of the output per image (the full
+    float64 gradients are 6 MB per image).  RRDB.forward (block.py:262-270) runs under torch.utils.checkpoint so that
+    the float64 activations fit this container: the same ops on the same values, recomputed in the backward."""
+    import torch.utils.checkpoint as ckpt
+    import models.modules.block as blk
+    fwd = blk.RRDB.forward
+    blk.RRDB.forward = lambda self, x: ckpt.checkpoint(fwd, self, x, use_reentrant=False)
+    cfg = dict(Z_GRID)
+    k = synthetic_learned_kernel()
+    B, h, idx = cfg['B'], cfg['h'], cfg['images']
+    lr, z = seeded_inputs(cfg['seed'] + 1, (B, 3, h, h), (B, 3, 4 * h, 4 * h), z_mode='pixel')
+    R = np.random.default_rng(cfg['seed'] + 2).standard_normal((B, 3, 4 * h, 4 * h)).astype(np.float32)
+    d = {'cfg': np.str_(json.dumps(cfg)), 'kernel': k}
+    for tag, dtype in (('f64', torch.float64), ('f32', torch.float32)):
+        net = arch.RRDBNet(in_nc=3, out_nc=3, nf=64, nb=cfg['nb'], gc=32, upscale=4, norm_type=None,
+                           act_type='leakyrelu', mode='CNA', upsample_mode='upconv',
+                           latent_input='all_layers_HR_downscaled', num_latent_channels=3)
+        model = CEMnet.CEMnet(CEMnet.Get_CEM_Config(4), upscale_kernel=k).WrapArchitecture_PyTorch(net)
+        sd = model.state_dict()
+        named_shapes = [(n, tuple(v.shape)) for n, v in sd.items()]
+        params = seeded_params(named_shapes, cfg['seed'], w_scale=cfg['w_scale'])
+        model.load_state_dict({n: torch.from_numpy(v) for n, v in params.items()}, strict=False)
+        model = model.to(dtype)
+        model.eval()  # (CEM_PyTorch.train returns None)
+        for q in model.parameters():
+            q.requires_grad = False
+        zt = torch.from_numpy(z[idx]).to(dtype).requires_grad_(True)
+        lt = torch.from_numpy(lr[idx]).to(dtype).requires_grad_(True)
+        out = model(torch.cat([zt.view(len(idx), 48, h, h), lt], 1))
+        (out * torch.from_numpy(R[idx]).to(dtype)).sum().backward()
+        for j, i in enumerate(idx):
+            for name, v in (('dz', zt.grad[j]), ('dlr', lt.grad[j]), ('out', out.detach()[j])):
+                v = v.double().numpy()
+                d['%s_%s_proj:%d' % (tag, name, i)] = _digest(v, cfg['seed'] + {'dz': 10, 'dlr': 11, 'out': 12}[name],
+                                                              i, cfg['proj'])
+                d['%s_%s_norm:%d' % (tag, name, i)] = np.float64(np.linalg.norm(v))
+        print('zgrid [%s]: |dz| %s' % (tag, [float(zt.grad[j].norm()) for j in range(len(idx))]), flush=True)
+        del model, out, zt, lt
+    blk.RRDB.forward = fwd
+    np.savez_compressed(os.path.join(HERE, 'grid_c5_zgrad.npz'), **d)
+
+
 def disc_fixture(arch, loss_mod, name, seed):
     """Discriminator_VGG_128_ (architecture.py:222-284) with nb = n_layers = 6 as the shipped train config builds it
     once define_D's TypeError is resolved, plus one WGAN-GP discriminator loss + gradients exactly as
@@ -327,6 +381,9 @@ def main():
         return
     import models.modules.architecture as arch
     torch.set_num_threads(8)
+    if sys.argv[1:] == ['c5grid']:  # config 5's grid, learned kernel: its own process (imresize's sticky kernel)
+        zgrid_fixture(arch, CEMnet)
+        return
     if sys.argv[1:] == ['scale2']:  # ×2 generators (architecture.py:113-136) in their own process: imresize's bicubic
         sf = 2                     # kernel is process-global and sticky.  (×3 cannot be built by the reference:
         #                            architecture.py:144 concatenates a list and the ×3 nn.Sequential -> TypeError)

@@ -44,7 +44,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 import make_golden as MG  # noqa: E402
 from oracle.recipe import seeded_params  # noqa: E402
-from train_recipe import CKPT_CFG, LR_CFG, TRAIN_CFGS, drive_lr_schedule, random_points, step_data, train_opt  # noqa: E402,E501
+from train_recipe import (C3_GRID_CFG, CKPT_CFG, LR_CFG, TRAIN_CFGS, drive_lr_schedule, grad_projections,  # noqa: E402
+                          random_points, step_data, train_opt)
 
 SMALL = 4096  # keys with at most this many elements get their full parameter change stored
 
@@ -111,7 +112,7 @@ def build_reference(cfg, dtype):
     finally:
         torch.set_default_dtype(torch.float32)
     gsd, dsd = model.netG.state_dict(), model.netD.state_dict()
-    gp = seeded_params([(k, tuple(v.shape)) for k, v in gsd.items()], cfg['seed'], w_scale=1.0)
+    gp = seeded_params([(k, tuple(v.shape)) for k, v in gsd.items()], cfg['seed'], w_scale=cfg.get('w_scale_G', 1.0))
     dp = seeded_params([(k, tuple(v.shape)) for k, v in dsd.items() if 'running' not in k and 'num_batches' not in k],
                        cfg['seed'] + 1, w_scale=1.0)
     model.netG.load_state_dict({k: torch.from_numpy(v) for k, v in gp.items()}, strict=False)
@@ -169,6 +170,44 @@ def train_fixture(name, cfg):
         print('train_%s [%s]: generator_step %s, logs %s' % (
             name, tag, flags, {k: ['%.4g' % x[1] for x in v] for k, v in model.log_dict.items() if v}))
     np.savez_compressed(os.path.join(HERE, 'train_%s.npz' % name), **d)
+
+
+def c3_grid_fixture():
+    """Config 3 at its production grid (train_recipe.C3_GRID_CFG), float64 then float32, one model at a time.  The
+    reference's RRDB.forward (block.py:262-270) runs under torch.utils.checkpoint so that the float64 generator's
+    activations fit this container's memory (~75 GB without): the same ops on the same values, recomputed in the
+    backward — a memory-only wrapper, the results are the reference's own."""
+    import gc
+    import torch.utils.checkpoint as ckpt
+    import models.modules.block as blk
+    if not getattr(blk.RRDB, '_esr_ckpt', False):
+        fwd = blk.RRDB.forward
+        blk.RRDB.forward = lambda self, x: ckpt.checkpoint(fwd, self, x, use_reentrant=False)
+        blk.RRDB._esr_ckpt = True
+    cfg = dict(C3_GRID_CFG)
+    d = {'cfg': np.str_(json.dumps(cfg))}
+    for tag, dtype in (('f64', torch.float64), ('f32', torch.float32)):
+        model, g0, d0, flags = run_reference(cfg, dtype)
+        d['%s_generator_step' % tag] = np.array(flags)
+        for k, v in model.log_dict.items():
+            if v:
+                d['%s_log:%s' % (tag, k)] = np.array(v, dtype=np.float64)
+        for net, t in ((model.netG, 'G'), (model.netD, 'D')):
+            for i, (k, p) in enumerate(net.named_parameters()):
+                if p.grad is None:
+                    continue
+                g = p.grad.detach().double().numpy()
+                d['%s_%s_gproj:%s' % (tag, t, k)] = grad_projections(g, cfg['seed'] + (10 if t == 'G' else 11), i,
+                                                                     cfg['proj'])
+                d['%s_%s_gnorm:%s' % (tag, t, k)] = np.float64(np.linalg.norm(g))
+        for k, v in model.netD.state_dict().items():
+            if 'running' in k:
+                d['%s_Dbuf:%s' % (tag, k)] = v.double().numpy()
+        print('c3_grid [%s]: generator_step %s, logs %s' % (
+            tag, flags, {k: ['%.6g' % x[1] for x in v] for k, v in model.log_dict.items() if v}), flush=True)
+        del model, g0, d0
+        gc.collect()
+    np.savez_compressed(os.path.join(HERE, 'grid_c3_train.npz'), **d)
 
 
 def _sha(t):
@@ -246,6 +285,8 @@ def main():
             checkpoint_fixtures()
         elif name == 'lr':
             lr_schedule_fixture()
+        elif name == 'c3':
+            c3_grid_fixture()
         else:
             train_fixture(name, TRAIN_CFGS[name])
 

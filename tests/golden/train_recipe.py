@@ -112,3 +112,20 @@ def drive_lr_schedule(model, cfg):
             break
     dec = [[e[0], e[1]['lr_G'], e[1]['lr_D']] for e in model.log_dict['LR_decrease']]
     return np.array(records, dtype=np.float64), np.array(dec, dtype=np.float64).reshape(-1, 3)
+
+
+# config 3 at its production grid: B=16 × 96² LR crops, RRDB-23, latent, CEM train mode (the D sees
+# the unpadded 304² HR), WGAN-GP non-relativistic as shipped; 2 micro-steps: step 0 = D step only (generator_step needs
+# gradient_step_num > D_init_iters), step 1 = D step + G step.  define_G's training-time init scale (kaiming × 0.1)
+# for the generator.  The fixture holds digests of the step-1 gradients of every G and D parameter (K seeded random
+# projections + the norm), the logs and the D BatchNorm buffers, from the reference in float32 and float64.
+C3_GRID_CFG = dict(nb=23, batch=16, lr_size=96, lr=1e-4, relativistic=0, D_update_ratio=1, D_verification=None,
+                   D_valid_steps=1, min_D_prob_ratio_4_G=1.0, min_mean_D_correct=0.0, acc=1, steps=2, seed=800,
+                   w_scale_G=0.1, proj=8)
+
+
+def grad_projections(grad, seed, index, k):
+    """k projections of a gradient (any shape, float64 numpy) on seeded standard-normal directions."""
+    g = np.asarray(grad, dtype=np.float64).ravel()
+    P = np.random.default_rng([seed, index]).standard_normal((k, g.size))
+    return P @ g

@@ -15,7 +15,7 @@ import torch.nn.functional as F
 
 from conftest import golden, normwise_rel
 
-from esr_amd import dconv
+from esr_amd import _lib, dconv
 from esr_amd import loss as L
 from esr_amd.discriminator import Discriminator_VGG_128_
 from oracle.esr_oracle import reference_discriminator
@@ -31,17 +31,25 @@ pytestmark = pytest.mark.gpu
     (256, 100, 8, 1, 0, 12, 10),   # pseudo-FC 8x8 valid, 100 outputs (two N blocks, partial)
     (100, 1, 1, 1, 0, 5, 7),       # 1x1 head: 100 channels in, 1 out (unaligned pitches)
     (130, 70, 4, 2, 1, 8, 9),      # partial K chunks and N blocks
+    (64, 64, 3, 1, 1, 37, 70),     # several halo tiles per image, ragged in both directions
+    (32, 64, 4, 2, 1, 41, 75),     # stride-2 halo (column-parity de-interleave), ragged
+    (256, 100, 8, 1, 0, 38, 38),   # the config-3 pseudo-FC geometry: split-K over the channel chunks
 ])
-@pytest.mark.parametrize('precision', ['x3', 'f32'])
+@pytest.mark.parametrize('precision', ['x3', 'f32', 'f32_gather'])
 def test_dconv_ops_vs_float64(gpu_device, ci, co, k, s, p, H, W, precision):
-    prev = dconv.set_precision(precision)
+    """f32 = the halo-tile forward kernel (default), f32_gather = the per-tap gather kernel it replaced."""
+    prev = dconv.set_precision('f32' if precision.startswith('f32') else precision)
+    lib = _lib.load()
+    prev_halo = lib.esr_dconv_set_halo(0 if precision == 'f32_gather' else 1)
     try:
-        _dconv_ops(gpu_device, ci, co, k, s, p, H, W, scale=1e-9 if precision == 'x3' else 1.0)
+        _dconv_ops(gpu_device, ci, co, k, s, p, H, W, scale=1e-9 if precision == 'x3' else 1.0,
+                   tol=1e-5)
     finally:
         dconv.set_precision(prev)
+        lib.esr_dconv_set_halo(prev_halo)
 
 
-def _dconv_ops(gpu_device, ci, co, k, s, p, H, W, scale):
+def _dconv_ops(gpu_device, ci, co, k, s, p, H, W, scale, tol=1e-5):
     """scale: the output gradient's magnitude (x3: ~1e-9, a realistic loss gradient far below f16's range, which the
     per-step scaling must bring back)."""
     g = torch.Generator().manual_seed(ci * 1000 + co)
@@ -59,9 +67,9 @@ def _dconv_ops(gpu_device, ci, co, k, s, p, H, W, scale):
     gw = dconv.conv_wgrad(nhwc(x), nhwc(gy), k, s, p)
     torch.cuda.synchronize()
     xd, wdd, gyd = x.double(), w.double(), gy.double()
-    assert normwise_rel(back(y), F.conv2d(xd, wdd, b.double(), stride=s, padding=p)) < 1e-5
-    assert normwise_rel(back(gx), torch.nn.grad.conv2d_input(xd.shape, wdd, gyd, stride=s, padding=p)) < 1e-5
-    assert normwise_rel(gw.double().cpu(), torch.nn.grad.conv2d_weight(xd, wdd.shape, gyd, stride=s, padding=p)) < 1e-5
+    assert normwise_rel(back(y), F.conv2d(xd, wdd, b.double(), stride=s, padding=p)) < tol
+    assert normwise_rel(back(gx), torch.nn.grad.conv2d_input(xd.shape, wdd, gyd, stride=s, padding=p)) < tol
+    assert normwise_rel(gw.double().cpu(), torch.nn.grad.conv2d_weight(xd, wdd.shape, gyd, stride=s, padding=p)) < tol
 
 
 def test_dconv_packed_weight_memo_follows_updates(gpu_device):

@@ -53,7 +53,7 @@ def _run_port(cfg, precision, dev, d_precision=None):
     torch.manual_seed(0)
     model = SRRaGANModel(train_opt(cfg), accumulation_steps_per_batch=cfg['acc'], device=dev)
     gsd, dsd = model.netG.state_dict(), model.netD.state_dict()
-    gp = seeded_params([(k, tuple(v.shape)) for k, v in gsd.items()], cfg['seed'], w_scale=1.0)
+    gp = seeded_params([(k, tuple(v.shape)) for k, v in gsd.items()], cfg['seed'], w_scale=cfg.get('w_scale_G', 1.0))
     dp = seeded_params([(k, tuple(v.shape)) for k, v in dsd.items() if 'running' not in k and 'num_batches' not in k],
                        cfg['seed'] + 1, w_scale=1.0)
     model.netG.load_state_dict({k: torch.from_numpy(v) for k, v in gp.items()}, strict=False)

@@ -1,6 +1,8 @@
 """A/B timing of the discriminator gather-GEMM forward (esr_dconv_fwd) on the config-3 layer shapes (B=16, D input
 304², Discriminator_VGG_128_ nb=6): exact fp32, x3 with 64-channel N tiles, x3 with 128 (default).  Order-balanced
-(two rounds, the second reported); µs per launch, TFLOP/s, and the x3 results' normwise difference from fp32.
+(two rounds, the second reported); µs per launch, TFLOP/s, and the results' normwise difference from the fp32 gather
+kernel.  Variants: f32_gather (the per-tap gather kernel), f32_halo (halo-tile kernel, the fp32 default), x3 with 64-
+and 128-channel N tiles.  Also the data gradient (all phase classes) per variant.
 
     python tools/dconv_ab.py
 """
@@ -37,11 +39,12 @@ def main():
         row, outs = {}, {}
         gy = torch.randn(B, Ho, Ho, co, device=dev) * 1e-8
         for rnd in range(2):
-            for tag, mode in (('f32', 0), ('x3_n64', 2), ('x3_n128', 1)):
+            for tag, mode, halo in (('f32', 0, 0), ('f32_halo', 0, 1), ('x3_n64', 2, 0), ('x3_n128', 1, 0)):
                 dconv.set_precision('f32' if mode == 0 else 'x3')
                 dconv._applied[0] = None
                 dconv._lib_for_launch()
                 lib.esr_dconv_set_x3(mode)
+                lib.esr_dconv_set_halo(halo)
                 for _ in range(2):
                     dconv.conv_forward(x, w, b, k, s, p)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -51,6 +54,13 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 us = e0.elapsed_time(e1) * 100
+                dconv.conv_dgrad(gy, w, k, s, p, H, H)
+                e0.record()
+                for _ in range(10):
+                    gx = dconv.conv_dgrad(gy, w, k, s, p, H, H)
+                e1.record()
+                torch.cuda.synchronize()
+                us_d = e0.elapsed_time(e1) * 100
                 dconv.conv_wgrad(x, gy, k, s, p)
                 e0.record()
                 for _ in range(10):
@@ -60,15 +70,19 @@ def main():
                 us_w = e0.elapsed_time(e1) * 100
                 outs[tag] = y
                 outs[tag + 'w'] = gw
+                outs[tag + 'd'] = gx
                 if rnd:
                     row[tag + '_us'] = round(us, 1)
                     row[tag + '_tflops'] = round(flops / us / 1e6, 1)
                     row[tag + '_wgrad_us'] = round(us_w, 1)
-        for tag in ('x3_n64', 'x3_n128'):
+                    row[tag + '_dgrad_us'] = round(us_d, 1)
+        for tag in ('f32_halo', 'x3_n64', 'x3_n128'):
             row[tag + '_diff'] = float((outs[tag] - outs['f32']).norm() / outs['f32'].norm())
+            row[tag + '_dgrad_diff'] = float((outs[tag + 'd'] - outs['f32d']).norm() / outs['f32d'].norm())
             row[tag + '_wgrad_diff'] = float((outs[tag + 'w'] - outs['f32w']).norm() / outs['f32w'].norm())
         print(name, json.dumps(row), flush=True)
     lib.esr_dconv_set_x3(0)
+    lib.esr_dconv_set_halo(1)
     dconv._applied[0] = None
 
 
