@@ -342,6 +342,12 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_halo_kernel(FwdParams p, Hal
 // exact), by 2^-(eA + eB) at the end.  LDS rows: 32 f16 hi then 32 f16 lo (128 B) + 16 B pad: the 16 rows of a
 // ds_read_b128 group land on 16 distinct 4-bank slots.
 constexpr int XP = 144;  // LDS row pitch (bytes) of the x3 kernel
+// x6 (NP = 3 pieces): a third f16 piece lo2 = f16(v·s - hi - lo) and the products hi·hi + hi·lo + lo·hi + lo·lo +
+// hi·lo2 + lo2·hi — each operand carried to ~33 bits, every dropped term below 2^-33 of the step's scale, so the
+// result is an fp32 FMA chain's up to the fp32 accumulation itself (x3 drops lo·lo and carries 22 bits: ~2^-22 per
+// product).  Rows: 32 hi, 32 lo, 32 lo2 (f16) + 16 B pad = 208 B = 52 dwords, so the 16 rows of a ds_read_b128
+// group still land on 16 distinct 4-bank slots.
+template <int NP> struct XPitch { static constexpr int v = NP == 2 ? 144 : 208; };
 
 __device__ __forceinline__ int tile_exp(float m, int e_keep) {
     if (!(m > 0.f) || !(m <= 3.4e38f)) return e_keep;  // all zero, or NaN / inf (propagates unscaled)
@@ -351,9 +357,9 @@ __device__ __forceinline__ int tile_exp(float m, int e_keep) {
 }
 
 // NBX = 64 or 128 output channels per workgroup (128: the A tile, re-gathered per tap, feeds twice the MFMAs)
-template <int NBX>
+template <int NBX, int NP>
 __global__ __launch_bounds__(NTH, 2) void dconv_fwd_x3_kernel(FwdParams p) {
-    constexpr int NTN = NBX / 32, BX_IT = NBX * KC / 4 / NTH;
+    constexpr int NTN = NBX / 32, BX_IT = NBX * KC / 4 / NTH, XP = XPitch<NP>::v;
     __shared__ __attribute__((aligned(16))) unsigned char lds[(MT + NBX) * XP];
     __shared__ float s_red[2][2][NTH / 64];
     unsigned char *s_a = lds, *s_b = lds + MT * XP;
@@ -421,15 +427,18 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_x3_kernel(FwdParams p) {
         }
     };
     auto put = [&](unsigned char *row, f32x4 v, float s) {  // 4 channels at quad cg of a staged row
-        f16x4 h, l;
+        f16x4 h, l, l2;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const float x = v[e] * s;
             h[e] = (_Float16)x;
-            l[e] = (_Float16)(x - (float)h[e]);
+            const float r = x - (float)h[e];
+            l[e] = (_Float16)r;
+            if (NP == 3) l2[e] = (_Float16)(r - (float)l[e]);
         }
         *reinterpret_cast<f16x4 *>(row + cg * 8) = h;
         *reinterpret_cast<f16x4 *>(row + 64 + cg * 8) = l;
+        if (NP == 3) *reinterpret_cast<f16x4 *>(row + 128 + cg * 8) = l2;
     };
 
     f32x16 acc[2][NTN];
@@ -476,18 +485,26 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_x3_kernel(FwdParams p) {
         const unsigned char *b0 = s_b + ml * XP + 16 * hl;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-            f16x8 ah[2], al[2];
+            f16x8 ah[2], al[2], al2[2];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 ah[i] = *reinterpret_cast<const f16x8 *>(a0 + i * 32 * XP + 32 * s);
                 al[i] = *reinterpret_cast<const f16x8 *>(a0 + i * 32 * XP + 64 + 32 * s);
+                if (NP == 3) al2[i] = *reinterpret_cast<const f16x8 *>(a0 + i * 32 * XP + 128 + 32 * s);
             }
 #pragma unroll
             for (int nt = 0; nt < NTN; ++nt) {
                 const f16x8 bh = *reinterpret_cast<const f16x8 *>(b0 + nt * 32 * XP + 32 * s);
                 const f16x8 bl = *reinterpret_cast<const f16x8 *>(b0 + nt * 32 * XP + 64 + 32 * s);
+                f16x8 bl2;
+                if (NP == 3) bl2 = *reinterpret_cast<const f16x8 *>(b0 + nt * 32 * XP + 128 + 32 * s);
 #pragma unroll
                 for (int mt = 0; mt < 2; ++mt) {
+                    if (NP == 3) {  // smallest terms first
+                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al2[mt], bh, acc[mt][nt], 0, 0, 0);
+                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mt], bl2, acc[mt][nt], 0, 0, 0);
+                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[mt], bl, acc[mt][nt], 0, 0, 0);
+                    }
                     acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[mt], bh, acc[mt][nt], 0, 0, 0);
                     acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mt], bl, acc[mt][nt], 0, 0, 0);
                     acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mt], bh, acc[mt][nt], 0, 0, 0);
@@ -642,10 +659,13 @@ __global__ __launch_bounds__(NTH, 2) void dconv_wgrad_kernel(WgradParams p) {
 // 16j..16j+15]_j then [lo ...]_j, stored at physical chunk (logical ^ 2·(row & 3)); fragments come from
 // ds_read_b64_tr_b16 (4 pixel rows × 16 channels per 16-lane group), and with the XOR the 4 rows × 2 chunks of a
 // half-wave's read cover the 64 banks once.
-template <int CIB, int COB>
+// NP = 3 (x6): a third piece lo2 and the products lo·lo, hi·lo2, lo2·hi too (see dconv_fwd_x3_kernel).  Rows are
+// then 6·nch bytes; for nch = 64 (384 B ≡ 128 mod 256) the XOR swizzle is 2·((row >> 1) & 1) instead of 2·(row & 3)
+// so that the 4 rows × 64 B of a half-wave's transposed read still cover the 64 banks once.
+template <int CIB, int COB, int NP>
 __global__ __launch_bounds__(NTH, 2) void dconv_wgrad_x3_kernel(WgradParams p) {
     constexpr int AQ = CIB / 16, BQ = COB / 16;            // fp32 quads per thread per K step
-    constexpr int AROW = 4 * CIB, BROW = 4 * COB;           // LDS row bytes (hi + lo)
+    constexpr int AROW = 2 * NP * CIB, BROW = 2 * NP * COB; // LDS row bytes (hi + lo [+ lo2])
     constexpr int MTW = CIB / 64, NTW = COB / 64;           // accumulator tiles per wave
     __shared__ __attribute__((aligned(16))) unsigned char lds[WKP * (AROW + BROW)];
     __shared__ float s_red[2][2][NTH / 64];
@@ -736,21 +756,25 @@ __global__ __launch_bounds__(NTH, 2) void dconv_wgrad_x3_kernel(WgradParams p) {
             s_red[slot][1][wave] = mb;
         }
     };
-    // byte offset of (row, channel c (multiple of 4), lo) in an image with NCH channels
-    auto off = [](int row, int c, int lo, int nch) {
-        const int logical = lo * (nch / 16) + (c >> 4);
-        return row * 4 * nch + ((logical ^ (2 * (row & 3))) << 5) + (c & 15) * 2;
+    // byte offset of (row, channel c (multiple of 4), piece) in an image with NCH channels
+    auto off = [](int row, int c, int piece, int nch) {
+        const int logical = piece * (nch / 16) + (c >> 4);
+        const int sw = (NP == 3 && nch == 64) ? 2 * ((row >> 1) & 1) : 2 * (row & 3);
+        return row * 2 * NP * nch + ((logical ^ sw) << 5) + (c & 15) * 2;
     };
     auto put = [&](unsigned char *img, int nch, int row, int c, f32x4 v, float s) {
-        f16x4 h, l;
+        f16x4 h, l, l2;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const float x = v[e] * s;
             h[e] = (_Float16)x;
-            l[e] = (_Float16)(x - (float)h[e]);
+            const float r = x - (float)h[e];
+            l[e] = (_Float16)r;
+            if (NP == 3) l2[e] = (_Float16)(r - (float)l[e]);
         }
         *reinterpret_cast<f16x4 *>(img + off(row, c, 0, nch)) = h;
         *reinterpret_cast<f16x4 *>(img + off(row, c, 1, nch)) = l;
+        if (NP == 3) *reinterpret_cast<f16x4 *>(img + off(row, c, 2, nch)) = l2;
     };
 
     const int wm = wave >> 1, wn = wave & 1;
@@ -810,20 +834,29 @@ __global__ __launch_bounds__(NTH, 2) void dconv_wgrad_x3_kernel(WgradParams p) {
 #pragma unroll
         for (int kq = 0; kq < WKP / 16; ++kq) {
             const int r0 = 16 * kq + 8 * hl + rq;  // K rows (pixels) r0 and r0 + 4 of this lane's two reads
-            f16x8 bh[NTW], bl[NTW];
+            f16x8 bh[NTW], bl[NTW], bl2[NTW];
 #pragma unroll
             for (int j = 0; j < NTW; ++j) {
                 const int c = 32 * (NTW * wn + j) + cblk;
                 bh[j] = cat8(tr_read(s_b, off(r0, c, 0, COB)), tr_read(s_b, off(r0 + 4, c, 0, COB)));
                 bl[j] = cat8(tr_read(s_b, off(r0, c, 1, COB)), tr_read(s_b, off(r0 + 4, c, 1, COB)));
+                if (NP == 3)
+                    bl2[j] = cat8(tr_read(s_b, off(r0, c, 2, COB)), tr_read(s_b, off(r0 + 4, c, 2, COB)));
             }
 #pragma unroll
             for (int i = 0; i < MTW; ++i) {
                 const int c = 32 * (MTW * wm + i) + cblk;
                 const f16x8 ah = cat8(tr_read(s_a, off(r0, c, 0, CIB)), tr_read(s_a, off(r0 + 4, c, 0, CIB)));
                 const f16x8 al = cat8(tr_read(s_a, off(r0, c, 1, CIB)), tr_read(s_a, off(r0 + 4, c, 1, CIB)));
+                f16x8 al2;
+                if (NP == 3) al2 = cat8(tr_read(s_a, off(r0, c, 2, CIB)), tr_read(s_a, off(r0 + 4, c, 2, CIB)));
 #pragma unroll
                 for (int j = 0; j < NTW; ++j) {
+                    if (NP == 3) {
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al2, bh[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl2[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bl[j], acc[i][j], 0, 0, 0);
+                    }
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[j], acc[i][j], 0, 0, 0);
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[j], acc[i][j], 0, 0, 0);
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[j], acc[i][j], 0, 0, 0);
@@ -900,6 +933,7 @@ int halo_splits(const HaloParams &h, int B, int n_pad, int nck) {
 
 int g_dconv_x3 = 0;   // esr_dconv_set_x3
 int g_dconv_halo = 1; // esr_dconv_set_halo: exact-fp32 forward on the halo-tile kernel where it applies
+int g_dconv_np = 2;   // split pieces of the x3 kernels: 2 = x3, 3 = x6 (esr_dconv_set_x3(3))
 int g_dconv_nb = 128; // x3: widest N tile allowed (esr_dconv_set_x3(2) = 64 only, for A/B)
 
 extern "C" int esr_dconv_fwd_sk(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t src_pitch, int32_t kc,
@@ -947,12 +981,17 @@ extern "C" int esr_dconv_fwd_sk(const float *src, int32_t B, int32_t Hs, int32_t
     const dim3 grid((unsigned)gx, (unsigned)((n + NB - 1) / NB)), block(NTH);
     // 128-channel N tiles only where the grid still fills the chip (the A tile then feeds twice the MFMAs)
     const bool wide = n_pad % 128 == 0 && g_dconv_nb != 64 && gx * (n_pad / 128) * ksplit >= 512;
-    if (g_dconv_x3 && wide)
-        hipLaunchKernelGGL(dconv_fwd_x3_kernel<128>, dim3((unsigned)gx, (unsigned)(n_pad / 128), (unsigned)ksplit),
-                           block, 0, (hipStream_t)stream, p);
+    const dim3 g128((unsigned)gx, (unsigned)(n_pad / 128), (unsigned)ksplit);
+    const dim3 g64((unsigned)gx, (unsigned)(n_pad / 64), (unsigned)ksplit);
+    const hipStream_t hst = (hipStream_t)stream;
+    if (g_dconv_x3 && g_dconv_np == 3 && wide)
+        hipLaunchKernelGGL((dconv_fwd_x3_kernel<128, 3>), g128, block, 0, hst, p);
+    else if (g_dconv_x3 && g_dconv_np == 3)
+        hipLaunchKernelGGL((dconv_fwd_x3_kernel<64, 3>), g64, block, 0, hst, p);
+    else if (g_dconv_x3 && wide)
+        hipLaunchKernelGGL((dconv_fwd_x3_kernel<128, 2>), g128, block, 0, hst, p);
     else if (g_dconv_x3)
-        hipLaunchKernelGGL(dconv_fwd_x3_kernel<64>, dim3((unsigned)gx, (unsigned)(n_pad / 64), (unsigned)ksplit),
-                           block, 0, (hipStream_t)stream, p);
+        hipLaunchKernelGGL((dconv_fwd_x3_kernel<64, 2>), g64, block, 0, hst, p);
     else
         hipLaunchKernelGGL(dconv_fwd_kernel, grid, block, 0, (hipStream_t)stream, p);
     if (ksplit > 1)
@@ -995,10 +1034,11 @@ extern "C" int esr_dconv_set_halo(int32_t on) {
 }
 
 extern "C" int esr_dconv_set_x3(int32_t on) {
-    if (on < 0 || on > 2) return ESR_EINVAL;
-    const int prev = g_dconv_x3 ? (g_dconv_nb == 64 ? 2 : 1) : 0;
+    if (on < 0 || on > 3) return ESR_EINVAL;
+    const int prev = g_dconv_x3 ? (g_dconv_np == 3 ? 3 : g_dconv_nb == 64 ? 2 : 1) : 0;
     g_dconv_x3 = on != 0;
     g_dconv_nb = on == 2 ? 64 : 128;
+    g_dconv_np = on == 3 ? 3 : 2;
     return prev;
 }
 
@@ -1027,10 +1067,15 @@ extern "C" int esr_dconv_wgrad(const float *src, int32_t B, int32_t Hs, int32_t 
         const long long gx = (long long)T * ((cin + cib - 1) / cib) * ((cout + cob - 1) / cob);
         const dim3 grid((unsigned)gx, (unsigned)splits), block(NTH);
         const hipStream_t st = (hipStream_t)stream;
-        if (cib == 128 && cob == 128) hipLaunchKernelGGL((dconv_wgrad_x3_kernel<128, 128>), grid, block, 0, st, p);
-        else if (cib == 128) hipLaunchKernelGGL((dconv_wgrad_x3_kernel<128, 64>), grid, block, 0, st, p);
-        else if (cob == 128) hipLaunchKernelGGL((dconv_wgrad_x3_kernel<64, 128>), grid, block, 0, st, p);
-        else hipLaunchKernelGGL((dconv_wgrad_x3_kernel<64, 64>), grid, block, 0, st, p);
+        if (g_dconv_np == 3) {
+            if (cib == 128 && cob == 128) hipLaunchKernelGGL((dconv_wgrad_x3_kernel<128, 128, 3>), grid, block, 0, st, p);
+            else if (cib == 128) hipLaunchKernelGGL((dconv_wgrad_x3_kernel<128, 64, 3>), grid, block, 0, st, p);
+            else if (cob == 128) hipLaunchKernelGGL((dconv_wgrad_x3_kernel<64, 128, 3>), grid, block, 0, st, p);
+            else hipLaunchKernelGGL((dconv_wgrad_x3_kernel<64, 64, 3>), grid, block, 0, st, p);
+        } else if (cib == 128 && cob == 128) hipLaunchKernelGGL((dconv_wgrad_x3_kernel<128, 128, 2>), grid, block, 0, st, p);
+        else if (cib == 128) hipLaunchKernelGGL((dconv_wgrad_x3_kernel<128, 64, 2>), grid, block, 0, st, p);
+        else if (cob == 128) hipLaunchKernelGGL((dconv_wgrad_x3_kernel<64, 128, 2>), grid, block, 0, st, p);
+        else hipLaunchKernelGGL((dconv_wgrad_x3_kernel<64, 64, 2>), grid, block, 0, st, p);
         return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
     }
     const long long gx = (long long)T * p.ci_blocks * p.co_blocks;

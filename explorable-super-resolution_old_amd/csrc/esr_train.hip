@@ -844,7 +844,10 @@ struct AdjParams {
     int K, s, c, Ly, Lx, Oy, Ox, os, oc, Ny, Nx, planes;
     float alpha;      // out = alpha * F^T(g) (+ beta * out when accumulate)
     int accumulate;
+    int fast;         // interior fast path (esr_cem_adjoint_set_generic(0), the default)
 };
+
+int g_adjoint_generic = 0;  // esr_cem_adjoint_set_generic
 
 __global__ __launch_bounds__(NT) void cem_adjoint_kernel(AdjParams p) {
     __shared__ float sw[64 * 64];
@@ -858,6 +861,27 @@ __global__ __launch_bounds__(NT) void cem_adjoint_kernel(AdjParams p) {
     const float *g = p.g + plane * p.Oy * p.Ox;
     const int pd = p.K / 2;
     float acc = 0.f;
+    if (p.fast && ky > 0 && ky < p.Ly - 1 && kx > 0 && kx < p.Lx - 1) {
+        // interior (no replicate clamp lands here): only the taps with s | (k - c - u + pd) contribute, one o each.
+        // The generic loop below visits the same taps in the same order and adds the same products (its sg is the
+        // one g value), so the two are bitwise equal (tests/test_gpu_cem_adjoint.py) — without its per-tap range
+        // search over all K² taps.
+        const int ty = ky - p.c + pd, tx = kx - p.c + pd;
+        const int ry = ((ty % p.s) + p.s) % p.s, rx = ((tx % p.s) + p.s) % p.s;
+        for (int uy = ry; uy < p.K; uy += p.s) {
+            const int oy = (ty - uy) / p.s;
+            if (oy < 0 || oy >= p.Oy) continue;
+            const float *gr = g + (long long)oy * p.Ox;
+            for (int ux = rx; ux < p.K; ux += p.s) {
+                const int ox = (tx - ux) / p.s;
+                if (ox < 0 || ox >= p.Ox) continue;
+                acc += sw[uy * p.K + ux] * gr[ox];
+            }
+        }
+        float *o = p.out + plane * p.Ny * p.Nx + (long long)i * p.Nx + j;
+        *o = p.accumulate ? *o + p.alpha * acc : p.alpha * acc;
+        return;
+    }
     for (int uy = 0; uy < p.K; ++uy) {
         int ylo, yhi;
         if (!o_range(ky, uy, p.s, p.c, pd, p.Ly, p.Oy, &ylo, &yhi)) continue;
@@ -1049,10 +1073,17 @@ extern "C" int esr_cem_adjoint(const float *g, int32_t planes, int32_t Oy, int32
     AdjParams p;
     p.g = g; p.out = out; p.w = w; p.K = K; p.s = s; p.c = c; p.Ly = Ly; p.Lx = Lx; p.Oy = Oy; p.Ox = Ox;
     p.os = os; p.oc = oc; p.Ny = (Ly - oc + os - 1) / os; p.Nx = (Lx - oc + os - 1) / os; p.planes = planes;
-    p.alpha = alpha; p.accumulate = accumulate;
+    p.alpha = alpha; p.accumulate = accumulate; p.fast = !g_adjoint_generic;
     hipLaunchKernelGGL(cem_adjoint_kernel, dim3(nblocks((long long)planes * p.Ny * p.Nx)), dim3(NT), 0,
                        (hipStream_t)stream, p);
     return launched();
+}
+
+extern "C" int esr_cem_adjoint_set_generic(int32_t on) {
+    if (on < 0 || on > 1) return ESR_EINVAL;
+    const int prev = g_adjoint_generic;
+    g_adjoint_generic = on;
+    return prev;
 }
 
 extern "C" int esr_input_adjoint(const float *d_hr, int32_t hr_cp, int32_t hr_coff, const float *d_lr, int32_t lr_cp,

@@ -93,6 +93,7 @@ _SIGNATURES = {
     'esr_dconv_fwd_splits': [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_int),
                              ctypes.POINTER(c_int)],
     'esr_dconv_set_halo': [c_int],
+    'esr_cem_adjoint_set_generic': [c_int],
     'esr_dconv_wgrad': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int,
                         c_int, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int), c_int, c_void_p, c_void_p],
     'esr_timer_create': [c_int],

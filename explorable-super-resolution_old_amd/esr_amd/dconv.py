@@ -26,18 +26,20 @@ from . import _lib
 MAX_TAPS = 64
 _WG_SPLIT_TARGET = 1024          # workgroups a weight-gradient launch aims for (split-K over pixels)
 _WG_PARTIAL_MAX = 64 << 20       # floats of split-K partials per launch
-# Precision of the gather-GEMM forward / data-gradient launches: 'x3' (default) = split-f16 operands with per-K-step
-# power-of-two scaling on f16 MFMA (fp32-level accuracy, esr_dconv.hip), 'f32' = exact fp32 MFMA.
+# Precision of the discriminator convolutions (forward, data and weight gradients): 'x3' = split-f16 operands (hi, lo)
+# with per-K-step power-of-two scaling on f16 MFMA (3 products, ~2^-22 per product), 'x6' = three f16 pieces and six
+# products (each operand to ~33 bits: an fp32 FMA chain's accuracy, esr_dconv.hip), 'f32' = exact fp32 MFMA.
 PRECISION = os.environ.get('ESR_DCONV_PRECISION', 'x3')
+_LIB_MODE = {'f32': 0, 'x3': 1, 'x6': 3}
 # exact-fp32 forward / data-gradient kernel: the halo-tile implicit GEMM (default) or the per-tap gather ('0', A/B)
 HALO = os.environ.get('ESR_DCONV_HALO', '1') != '0'
 _applied = [None]
 
 
 def set_precision(p):
-    """Select 'x3' or 'f32' for the discriminator convolutions (process-wide); returns the previous setting."""
+    """Select 'x3', 'x6' or 'f32' for the discriminator convolutions (process-wide); returns the previous setting."""
     global PRECISION
-    if p not in ('x3', 'f32'):
+    if p not in _LIB_MODE:
         raise ValueError(p)
     prev, PRECISION = PRECISION, p
     return prev
@@ -46,7 +48,7 @@ def set_precision(p):
 def _lib_for_launch():
     lib = _lib.load()
     if _applied[0] != PRECISION:
-        lib.esr_dconv_set_x3(1 if PRECISION == 'x3' else 0)
+        lib.esr_dconv_set_x3(_LIB_MODE[PRECISION])
         lib.esr_dconv_set_halo(1 if HALO else 0)
         _applied[0] = PRECISION
     return lib
@@ -175,7 +177,7 @@ def conv_wgrad(x, gy, k, s, p):
     cin_pad, cout_pad = 64 * ((Ci + 63) // 64), 64 * ((Co + 63) // 64)
     n = T * cin_pad * cout_pad
     P = B * Ho * Wo
-    if PRECISION == 'x3':  # x3 kernel: 128-channel blocks where the padded width allows, ~2 workgroups per CU
+    if PRECISION != 'f32':  # split kernels: 128-channel blocks where the padded width allows, ~2 workgroups per CU
         cib, cob = (128 if cin_pad % 128 == 0 else 64), (128 if cout_pad % 128 == 0 else 64)
         tiles = T * (cin_pad // cib) * (cout_pad // cob)
         splits = max(1, min(-(-512 // tiles), -(-P // 256), _WG_PARTIAL_MAX // n))

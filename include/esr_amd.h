@@ -226,6 +226,10 @@ int esr_nchw_to_padded(const float *src, int32_t C, int32_t B, int32_t H, int32_
 int esr_cem_adjoint(const float *g, int32_t planes, int32_t Oy, int32_t Ox, const float *w, int32_t K, int32_t s,
                     int32_t c, int32_t Ly, int32_t Lx, int32_t os, int32_t oc, float alpha, int32_t accumulate,
                     float *out, esr_stream_t stream);
+/* esr_cem_adjoint's interior fast path (outputs whose taps see no replicate clamp visit only the contributing taps,
+ * in the generic loop's order: bitwise equal) is the default; 1 = the generic per-tap range search everywhere (A/B,
+ * tests).  Returns the previous setting. */
+int esr_cem_adjoint_set_generic(int32_t on);
 
 /* Input gradient of the generator (Z optimisation, Z_optimization.py:574-630): out [B][C][Hp-2M][Wp-2M] (NCHW) =
  *   RepPad_M^T( d_hr  +  d_pl  +  Bilinear↓sf^T(d_lr) )
@@ -282,7 +286,9 @@ int esr_dconv_set_halo(int32_t on);
  * workgroup's max |a| and max |b|, products hi·hi + hi·lo + lo·hi on f16 MFMA, the fp32 accumulators rescaled exactly
  * when the step's scale changes (esr_dconv_wgrad likewise: per 64-pixel K step, 128-channel blocks where the padded
  * widths allow); 128 output channels per workgroup where n_pad % 128 == 0, else 64 (2 = x3 with
- * 64-channel tiles only, for A/B; identical results).  Returns the previous setting, or ESR_EINVAL. */
+ * 64-channel tiles only, for A/B; identical results; 3 = x6: three f16 pieces hi, lo, lo2 per operand value and the
+ * six products hi·hi, hi·lo, lo·hi, lo·lo, hi·lo2, lo2·hi — every dropped term below 2^-33 of the step's scale, i.e. an
+ * fp32 FMA chain's accuracy).  Returns the previous setting, or ESR_EINVAL. */
 int esr_dconv_set_x3(int32_t on);
 /* esr_dconv_wgrad: weight gradient of the forward conv above (src = its input, dy = dL/dout on the MH x MW grid):
  *   partial[s][t][ci][co] = sum over the pixels of split s of src[b, smy*Y+offy[t], smx*X+offx[t], ci] * dy[b, Y, X, co]

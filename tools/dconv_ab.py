@@ -39,8 +39,9 @@ def main():
         row, outs = {}, {}
         gy = torch.randn(B, Ho, Ho, co, device=dev) * 1e-8
         for rnd in range(2):
-            for tag, mode, halo in (('f32', 0, 0), ('f32_halo', 0, 1), ('x3_n64', 2, 0), ('x3_n128', 1, 0)):
-                dconv.set_precision('f32' if mode == 0 else 'x3')
+            for tag, mode, halo in (('f32', 0, 0), ('f32_halo', 0, 1), ('x3_n64', 2, 0), ('x3_n128', 1, 0),
+                                    ('x6', 3, 0)):
+                dconv.set_precision({0: 'f32', 3: 'x6'}.get(mode, 'x3'))
                 dconv._applied[0] = None
                 dconv._lib_for_launch()
                 lib.esr_dconv_set_x3(mode)
@@ -76,7 +77,7 @@ def main():
                     row[tag + '_tflops'] = round(flops / us / 1e6, 1)
                     row[tag + '_wgrad_us'] = round(us_w, 1)
                     row[tag + '_dgrad_us'] = round(us_d, 1)
-        for tag in ('f32_halo', 'x3_n64', 'x3_n128'):
+        for tag in ('f32_halo', 'x3_n64', 'x3_n128', 'x6'):
             row[tag + '_diff'] = float((outs[tag] - outs['f32']).norm() / outs['f32'].norm())
             row[tag + '_dgrad_diff'] = float((outs[tag + 'd'] - outs['f32d']).norm() / outs['f32d'].norm())
             row[tag + '_wgrad_diff'] = float((outs[tag + 'w'] - outs['f32w']).norm() / outs['f32w'].norm())
