@@ -156,6 +156,26 @@ def cpu_baseline_variants(args):
     return out
 
 
+def reference_parity(dev):
+    """Production-grid parity of the C3 training step and the C5 Z-gradients against the reference-made fixtures
+    (tests/grid_parity.py: the reference's own optimize_parameters at B=16 × 96², its autograd dZ at B=8 × 128² with
+    the learned kernel) — a checker like cpu_baseline, run on rank 0 at N=1 after every timed region."""
+    tests = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'tests')
+    if tests not in sys.path:
+        sys.path.insert(0, tests)
+    import grid_parity as GP
+    out = {}
+    for key, fn in (('train_c3', GP.c3_training_step), ('zopt_c5', GP.c5_z_gradients)):
+        try:
+            r = fn(dev)
+            out[key] = {'vs': 'reference float64 run (5x its float32 error + 1e-4 floor)', 'ok': r['ok'],
+                        'worst_frac_of_bound': r['worst_frac_of_bound'], 'n_fails': len(r['fails'])}
+        except Exception as e:  # noqa: BLE001
+            out[key] = {'error': repr(e)}
+        torch.cuda.empty_cache()
+    return out
+
+
 def pmc_traffic(kernel_tag):
     """HBM bytes per launch of `kernel_tag` from the committed rocprofv3 PMC passes (profiles/pmc_latest.json, made
     by tools/prof_summary.py from separate --pmc FETCH_SIZE / WRITE_SIZE runs of this same default bench command,
@@ -324,6 +344,10 @@ def main():
         rec['parity'] = parity
     if not args.no_legs:
         rec.update(run_legs(args, dev, world, rank))
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            for key, par in reference_parity(dev).items():
+                if isinstance(rec.get(key), dict):
+                    rec[key]['parity'] = par
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if world > 1:

@@ -341,7 +341,6 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_halo_kernel(FwdParams p, Hal
 // sum in the scale 2^(eA + eB) of the current step and are multiplied by 2^(new - old) when it changes (v_ldexp:
 // exact), by 2^-(eA + eB) at the end.  LDS rows: 32 f16 hi then 32 f16 lo (128 B) + 16 B pad: the 16 rows of a
 // ds_read_b128 group land on 16 distinct 4-bank slots.
-constexpr int XP = 144;  // LDS row pitch (bytes) of the x3 kernel
 // x6 (NP = 3 pieces): a third f16 piece lo2 = f16(v·s - hi - lo) and the products hi·hi + hi·lo + lo·hi + lo·lo +
 // hi·lo2 + lo2·hi — each operand carried to ~33 bits, every dropped term below 2^-33 of the step's scale, so the
 // result is an fp32 FMA chain's up to the fp32 accumulation itself (x3 drops lo·lo and carries 22 bits: ~2^-22 per
@@ -543,6 +542,232 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_x3_kernel(FwdParams p) {
                 const int oy = p.omy * Y + p.oay, ox = p.omx * X + p.oax;
                 p.out[(((long long)b * p.Ho + oy) * p.Wo + ox) * p.op + n] = ldexpf(acc[mt][nt][r], -(ea + eb)) + bn;
             }
+    }
+}
+
+
+// ---- halo-tile forward, split precision (x3 / x6) ---------------------------------------------------------------------
+// dconv_fwd_halo_kernel's tiling (the source window of all taps of a 32-channel chunk staged once) with the operands in
+// NP f16 pieces (x3: hi, lo; x6: hi, lo, lo2) as dconv_fwd_x3_kernel.  Scales: per chunk the workgroup's max |a| over
+// the halo window (a first pass over the window's global loads, values discarded; the second pass scales, splits and
+// stores), per (tap, chunk) step the max |b| of the weight slab; the accumulators are rescaled exactly whenever the
+// sum of the two exponents changes.
+template <int WM, int WN, int NP>
+__global__ __launch_bounds__(NTH, 2) void dconv_fwd_halo_x_kernel(FwdParams p, HaloParams h) {
+    constexpr int TY = 2 * WM * WN, MWV = TY / WM, XPn = XPitch<NP>::v;
+    extern __shared__ __attribute__((aligned(16))) unsigned char xlds[];
+    __shared__ float s_reda[NTH / 64], s_redb[2][NTH / 64];  // per-wave max of the halo / of the weight slab
+    unsigned char *s_a = xlds, *s_b = xlds + h.b_off;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hl = lane >> 5, ml = lane & 31;
+    int id = blockIdx.x;
+    const int txi = id % h.tiles_x;
+    id /= h.tiles_x;
+    const int tyi = id % h.tiles_y, b = id / h.tiles_y;
+    const int Y0 = tyi * TY, X0 = txi * 32;
+    const int n0 = blockIdx.y * NB;
+    const int wm = wave % MWV, wn = wave / MWV;
+    const bool vec = p.vec != 0;
+    const int sy0 = p.smy * Y0 + h.oymin, sx0 = p.smx * X0 + h.oxmin;
+    const int c_begin = (int)((long long)p.nck * blockIdx.z / gridDim.z);
+    const int c_end = (int)((long long)p.nck * (blockIdx.z + 1) / gridDim.z);
+    const int nsteps = (c_end - c_begin) * p.T;
+    const float *img = p.src + (long long)b * p.Hs * p.Ws * p.sp;
+
+    auto split_put = [&](unsigned char *row, int q, f32x4 v, float sc) {  // 4 channels at quad q of a staged row
+        f16x4 hi, lo, lo2;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float x = v[e] * sc;
+            hi[e] = (_Float16)x;
+            const float r = x - (float)hi[e];
+            lo[e] = (_Float16)r;
+            if (NP == 3) lo2[e] = (_Float16)(r - (float)lo[e]);
+        }
+        *reinterpret_cast<f16x4 *>(row + q * 8) = hi;
+        *reinterpret_cast<f16x4 *>(row + 64 + q * 8) = lo;
+        if (NP == 3) *reinterpret_cast<f16x4 *>(row + 128 + q * 8) = lo2;
+    };
+    auto halo_item = [&](int idx, int j) -> f32x4 {
+        const int pix = idx >> 3, q = idx & 7;
+        const int r = pix / h.IXt, cc = pix - r * h.IXt;
+        const int par = cc / h.IXp, hc = cc - par * h.IXp;
+        const int sy = sy0 + r, sx = sx0 + hc * h.npar + par, c = j * KC + 4 * q;
+        if (sy >= 0 && sy < p.Hs && sx >= 0 && sx < p.Ws && c < p.kc)
+            return load4(img + ((long long)sy * p.Ws + sx) * p.sp, c, p.kc, vec);
+        return f32x4{0.f, 0.f, 0.f, 0.f};
+    };
+    auto wave_max = [&](float m) {
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+        return m;
+    };
+    // stage chunk j's halo window: pass 1 = max |a| (returns the exponent), pass 2 = scaled split into LDS
+    auto stage_a = [&](int j, int e_keep) {
+        const int total = h.IY * h.IXt * 8;
+        float m = 0.f;
+        for (int base = 0; base < total; base += 8 * NTH) {
+            f32x4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int idx = base + u * NTH + tid;
+                v[u] = idx < total ? halo_item(idx, j) : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) m = fmaxf(m, fabsf(v[u][e]));
+        }
+        m = wave_max(m);
+        if (lane == 0) s_reda[wave] = m;
+        __syncthreads();
+        float mm = 0.f;
+#pragma unroll
+        for (int w = 0; w < NTH / 64; ++w) mm = fmaxf(mm, s_reda[w]);
+        const int ea = tile_exp(mm, e_keep);
+        const float sc = ldexpf(1.f, ea);
+        for (int base = 0; base < total; base += 8 * NTH) {
+            f32x4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int idx = base + u * NTH + tid;
+                v[u] = idx < total ? halo_item(idx, j) : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int idx = base + u * NTH + tid;
+                if (idx < total) split_put(s_a + (idx >> 3) * XPn, idx & 7, v[u], sc);
+            }
+        }
+        return ea;
+    };
+
+    f32x4 rb[B_IT];
+    auto load_b = [&](int step) {
+        const int j = c_begin + step / p.T, t = step - (step / p.T) * p.T;
+        const float *wj = p.w + ((long long)(t * p.nck + j) * p.n_pad + n0) * KC;
+#pragma unroll
+        for (int k = 0; k < B_IT; ++k) rb[k] = *reinterpret_cast<const f32x4 *>(wj + (tid + k * NTH) * 4);
+    };
+    auto publish_b = [&](int slot) {
+        float mb = 0.f;
+#pragma unroll
+        for (int k = 0; k < B_IT; ++k)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) mb = fmaxf(mb, fabsf(rb[k][e]));
+        mb = wave_max(mb);
+        if (lane == 0) s_redb[slot][wave] = mb;
+    };
+
+    f32x16 acc[WM][WN];
+#pragma unroll
+    for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int k = 0; k < WN; ++k)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][k][r] = 0.f;
+    int ea = 0, eb = 0;
+
+    if (nsteps > 0) {
+        load_b(0);
+        publish_b(0);
+    }
+    for (int step = 0; step < nsteps; ++step) {
+        const int t = step % p.T;
+        __syncthreads();  // the previous step's fragment reads are done; this step's weight max is published
+        int ea2 = ea;
+        if (t == 0) ea2 = stage_a(c_begin + step / p.T, ea);  // (contains a barrier)
+        float mmb = 0.f;
+#pragma unroll
+        for (int w = 0; w < NTH / 64; ++w) mmb = fmaxf(mmb, s_redb[step & 1][w]);
+        const int eb2 = tile_exp(mmb, eb);
+        if (ea2 + eb2 != ea + eb) {
+            const int d = ea2 + eb2 - ea - eb;
+#pragma unroll
+            for (int i = 0; i < WM; ++i)
+#pragma unroll
+                for (int k = 0; k < WN; ++k)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc[i][k][r] = ldexpf(acc[i][k][r], d);
+        }
+        ea = ea2;
+        eb = eb2;
+        const float sb = ldexpf(1.f, eb);
+#pragma unroll
+        for (int k = 0; k < B_IT; ++k) {
+            const int idx = tid + k * NTH;
+            split_put(s_b + (idx >> 3) * XPn, idx & 7, rb[k], sb);
+        }
+        __syncthreads();
+        if (step + 1 < nsteps) load_b(step + 1);
+        const int dy = p.offy[t] - h.oymin, dx = p.offx[t] - h.oxmin;
+        const int col = (h.npar == 1) ? ml + dx : (dx & 1) * h.IXp + ml + (dx >> 1);
+        const unsigned char *a_base[WM];
+#pragma unroll
+        for (int i = 0; i < WM; ++i) {
+            const int ty = wm * WM + i;
+            a_base[i] = s_a + ((p.smy * ty + dy) * h.IXt + col) * XPn + 16 * hl;
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            f16x8 ah[WM], al[WM], al2[WM];
+#pragma unroll
+            for (int i = 0; i < WM; ++i) {
+                ah[i] = *reinterpret_cast<const f16x8 *>(a_base[i] + 32 * s2);
+                al[i] = *reinterpret_cast<const f16x8 *>(a_base[i] + 64 + 32 * s2);
+                if (NP == 3) al2[i] = *reinterpret_cast<const f16x8 *>(a_base[i] + 128 + 32 * s2);
+            }
+#pragma unroll
+            for (int k = 0; k < WN; ++k) {
+                const unsigned char *b0 = s_b + ((wn * WN + k) * 32 + ml) * XPn + 16 * hl + 32 * s2;
+                const f16x8 bh = *reinterpret_cast<const f16x8 *>(b0);
+                const f16x8 bl = *reinterpret_cast<const f16x8 *>(b0 + 64);
+                f16x8 bl2;
+                if (NP == 3) bl2 = *reinterpret_cast<const f16x8 *>(b0 + 128);
+#pragma unroll
+                for (int i = 0; i < WM; ++i) {
+                    if (NP == 3) {
+                        acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al2[i], bh, acc[i][k], 0, 0, 0);
+                        acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl2, acc[i][k], 0, 0, 0);
+                        acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bl, acc[i][k], 0, 0, 0);
+                    }
+                    acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh, acc[i][k], 0, 0, 0);
+                    acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl, acc[i][k], 0, 0, 0);
+                    acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh, acc[i][k], 0, 0, 0);
+                }
+            }
+        }
+        if (step + 1 < nsteps) publish_b((step + 1) & 1);
+    }
+
+    const long long per_img = (long long)p.MH * p.MW;
+    const int ue = -(ea + eb);
+#pragma unroll
+    for (int i = 0; i < WM; ++i) {
+        const int Y = Y0 + wm * WM + i;
+        if (Y >= p.MH) continue;
+#pragma unroll
+        for (int k = 0; k < WN; ++k) {
+            const int n = n0 + (wn * WN + k) * 32 + ml;
+            if (gridDim.z > 1) {
+                float *part = p.partial + (long long)blockIdx.z * p.B * per_img * p.n_pad;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int X = X0 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+                    if (X < p.MW) part[(b * per_img + (long long)Y * p.MW + X) * p.n_pad + n] = ldexpf(acc[i][k][r], ue);
+                }
+                continue;
+            }
+            if (n >= p.n) continue;
+            const float bn = p.bias ? p.bias[n] : 0.f;
+            const int oy = p.omy * Y + p.oay;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int X = X0 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+                if (X >= p.MW) continue;
+                const int ox = p.omx * X + p.oax;
+                p.out[(((long long)b * p.Ho + oy) * p.Wo + ox) * p.op + n] = ldexpf(acc[i][k][r], ue) + bn;
+            }
+        }
     }
 }
 
@@ -881,15 +1106,262 @@ __global__ __launch_bounds__(NTH, 2) void dconv_wgrad_x3_kernel(WgradParams p) {
             }
 }
 
+// ---- tap-row weight gradient (split x3 / x6) ----------------------------------------------------------------------------
+// dconv_wgrad_x3_kernel re-gathers the 64 source pixels of a K step for every tap (one tap per workgroup) and reloads
+// the output gradient for every tap.  Here a workgroup owns one ROW of the kernel (the KT taps (ky, 0..KT-1), which
+// share a source row) and a K step is a 64-pixel segment of one output row: the output-gradient segment [64 px][COB]
+// and the source row segment covering all KT taps (64 + KT - 1 pixels at stride 1; two column-parity halves of
+// 64 + (KT - 1)/2 at stride 2) are staged once per step, and every tap reads its A fragments at its column offset —
+// KT× less output-gradient staging and ~KT× less source staging.  Operands in NP f16 pieces with a per-step power-of-
+// two scale per operand (dconv_wgrad_x3_kernel's scheme); LDS images and transposed fragment reads as there (any 4
+// consecutive rows are conflict-free under the XOR swizzle, so a tap's shifted rows keep that).
+struct WrowParams {
+    const float *src;
+    int B, Hs, Ws, sp, cin, svec;
+    const float *dy;
+    int MH, MW, dp, cout, dvec;
+    int smy, smx, T, KT;  // taps; taps per group = the kernel width (group g = taps g·KT .. g·KT + KT - 1)
+    int nseg;             // 64-pixel segments per output row
+    long long segs_per_split;
+    int HP;               // staged source columns per parity
+    int ci_blocks, co_blocks;  // 64-channel units of the partial layout
+    float *partial;            // [split][T][64·ci_blocks][64·co_blocks]
+    int offy[MAXT], offx[MAXT];
+};
+
+constexpr int WSEG = 64;  // output pixels per K step
+
+template <int CIB, int COB, int NP, int KT, int SMX>
+__global__ __launch_bounds__(NTH, 1) void dconv_wgrad_rows_kernel(WrowParams p) {
+    constexpr int HPM = SMX == 1 ? WSEG + KT - 1 : WSEG + (KT - 1) / 2;  // columns per parity (max)
+    constexpr int AROWS = SMX * HPM;
+    constexpr int AQ = (AROWS * CIB / 4 + NTH - 1) / NTH, BQ = WSEG * COB / 4 / NTH;
+    constexpr int AROW = 2 * NP * CIB;
+    constexpr int MTW = CIB / 64, NTW = COB / 64;
+    extern __shared__ __attribute__((aligned(16))) unsigned char rlds[];
+    unsigned char *s_a = rlds, *s_b = rlds + AROWS * AROW;
+    __shared__ float s_red[2][2][NTH / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hl = lane >> 5;
+    const int nci = (p.cin + CIB - 1) / CIB, nco = (p.cout + COB - 1) / COB;
+    int bid = blockIdx.x;
+    const int cob = bid % nco;
+    bid /= nco;
+    const int cib = bid % nci;
+    const int g = bid / nci;  // kernel row
+    const int t0 = g * KT;
+    const int ci0 = cib * CIB, co0 = cob * COB;
+    const int oy = p.offy[t0], oxmin = p.offx[t0];
+    const long long nsegs = (long long)p.B * p.MH * p.nseg;
+    const long long q0 = (long long)blockIdx.y * p.segs_per_split;
+    const long long q1 = min(nsegs, q0 + p.segs_per_split);
+    const bool svec = p.svec != 0, dvec = p.dvec != 0;
+
+    f32x4 ra[AQ], rb[BQ];
+    auto load = [&](long long q) {
+        const int b = (int)(q / ((long long)p.MH * p.nseg));
+        const int r = (int)(q - (long long)b * p.MH * p.nseg);
+        const int Y = r / p.nseg, X0 = (r - Y * p.nseg) * WSEG;
+        const int sy = p.smy * Y + oy, sx0 = p.smx * X0 + oxmin;
+        const bool row_ok = sy >= 0 && sy < p.Hs;
+        const float *srow = p.src + ((long long)b * p.Hs + (row_ok ? sy : 0)) * p.Ws * p.sp;
+#pragma unroll
+        for (int k = 0; k < AQ; ++k) {
+            const int idx = tid + k * NTH, row = idx / (CIB / 4), q4 = idx % (CIB / 4);
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (row < AROWS && row_ok) {
+                const int par = row / HPM, h = row - par * HPM;
+                const int sx = sx0 + h * SMX + par, ci = ci0 + 4 * q4;
+                if (h < p.HP && sx >= 0 && sx < p.Ws && ci < p.cin) v = load4(srow + (long long)sx * p.sp, ci, p.cin, svec);
+            }
+            ra[k] = v;
+        }
+        const float *drow = p.dy + (((long long)b * p.MH + Y) * p.MW) * p.dp;
+#pragma unroll
+        for (int k = 0; k < BQ; ++k) {
+            const int idx = tid + k * NTH, row = idx / (COB / 4), q4 = idx % (COB / 4);
+            const int X = X0 + row, co = co0 + 4 * q4;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (X < p.MW && co < p.cout) v = load4(drow + (long long)X * p.dp, co, p.cout, dvec);
+            rb[k] = v;
+        }
+    };
+    auto publish = [&](int slot) {
+        float ma = 0.f, mb = 0.f;
+#pragma unroll
+        for (int k = 0; k < AQ; ++k)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) ma = fmaxf(ma, fabsf(ra[k][e]));
+#pragma unroll
+        for (int k = 0; k < BQ; ++k)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) mb = fmaxf(mb, fabsf(rb[k][e]));
+#pragma unroll
+        for (int s = 32; s >= 1; s >>= 1) {
+            ma = fmaxf(ma, __shfl_xor(ma, s));
+            mb = fmaxf(mb, __shfl_xor(mb, s));
+        }
+        if (lane == 0) {
+            s_red[slot][0][wave] = ma;
+            s_red[slot][1][wave] = mb;
+        }
+    };
+    auto off = [](int row, int c, int piece, int nch) {
+        const int logical = piece * (nch / 16) + (c >> 4);
+        const int sw = (NP == 3 && nch == 64) ? 2 * ((row >> 1) & 1) : 2 * (row & 3);
+        return row * 2 * NP * nch + ((logical ^ sw) << 5) + (c & 15) * 2;
+    };
+    auto put = [&](unsigned char *img, int nch, int row, int c, f32x4 v, float sc) {
+        f16x4 h, l, l2;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float x = v[e] * sc;
+            h[e] = (_Float16)x;
+            const float r = x - (float)h[e];
+            l[e] = (_Float16)r;
+            if (NP == 3) l2[e] = (_Float16)(r - (float)l[e]);
+        }
+        *reinterpret_cast<f16x4 *>(img + off(row, c, 0, nch)) = h;
+        *reinterpret_cast<f16x4 *>(img + off(row, c, 1, nch)) = l;
+        if (NP == 3) *reinterpret_cast<f16x4 *>(img + off(row, c, 2, nch)) = l2;
+    };
+
+    const int wm = wave >> 1, wn = wave & 1;
+    f32x16 acc[KT][MTW][NTW];
+#pragma unroll
+    for (int x = 0; x < KT; ++x)
+#pragma unroll
+        for (int i = 0; i < MTW; ++i)
+#pragma unroll
+            for (int j = 0; j < NTW; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[x][i][j][r] = 0.f;
+    int ea = 0, eb = 0;
+    const int i16 = lane & 15, rq = i16 >> 2, grp = (lane >> 4) & 1;
+    const int cblk = 16 * grp + 4 * (i16 & 3);
+    int rowoff[KT];  // staged source row of output pixel 0 for each tap
+#pragma unroll
+    for (int x = 0; x < KT; ++x) {
+        const int d = p.offx[t0 + x] - oxmin;
+        rowoff[x] = SMX == 1 ? d : (d & 1) * HPM + (d >> 1);
+    }
+
+    if (q0 < q1) {
+        load(q0);
+        publish(0);
+    }
+    for (long long q = q0; q < q1; ++q) {
+        const int it = (int)(q - q0);
+        __syncthreads();
+        float ma = 0.f, mb = 0.f;
+#pragma unroll
+        for (int w = 0; w < NTH / 64; ++w) {
+            ma = fmaxf(ma, s_red[it & 1][0][w]);
+            mb = fmaxf(mb, s_red[it & 1][1][w]);
+        }
+        const int ea2 = tile_exp(ma, ea), eb2 = tile_exp(mb, eb);
+        if (ea2 + eb2 != ea + eb) {
+            const int d = ea2 + eb2 - ea - eb;
+#pragma unroll
+            for (int x = 0; x < KT; ++x)
+#pragma unroll
+                for (int i = 0; i < MTW; ++i)
+#pragma unroll
+                    for (int j = 0; j < NTW; ++j)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) acc[x][i][j][r] = ldexpf(acc[x][i][j][r], d);
+        }
+        ea = ea2;
+        eb = eb2;
+        const float sa = ldexpf(1.f, ea), sb = ldexpf(1.f, eb);
+#pragma unroll
+        for (int k = 0; k < AQ; ++k) {
+            const int idx = tid + k * NTH, row = idx / (CIB / 4);
+            if (row < AROWS) put(s_a, CIB, row, 4 * (idx % (CIB / 4)), ra[k], sa);
+        }
+#pragma unroll
+        for (int k = 0; k < BQ; ++k) {
+            const int idx = tid + k * NTH;
+            put(s_b, COB, idx / (COB / 4), 4 * (idx % (COB / 4)), rb[k], sb);
+        }
+        __syncthreads();
+        if (q + 1 < q1) load(q + 1);
+#pragma unroll
+        for (int kq = 0; kq < WSEG / 16; ++kq) {
+            const int r0 = 16 * kq + 8 * hl + rq;  // K rows (output pixels) r0 and r0 + 4 of this lane's two reads
+            f16x8 bh[NTW], bl[NTW], bl2[NTW];
+#pragma unroll
+            for (int j = 0; j < NTW; ++j) {
+                const int c = 32 * (NTW * wn + j) + cblk;
+                bh[j] = cat8(tr_read(s_b, off(r0, c, 0, COB)), tr_read(s_b, off(r0 + 4, c, 0, COB)));
+                bl[j] = cat8(tr_read(s_b, off(r0, c, 1, COB)), tr_read(s_b, off(r0 + 4, c, 1, COB)));
+                if (NP == 3)
+                    bl2[j] = cat8(tr_read(s_b, off(r0, c, 2, COB)), tr_read(s_b, off(r0 + 4, c, 2, COB)));
+            }
+#pragma unroll
+            for (int x = 0; x < KT; ++x) {
+                const int ra0 = rowoff[x] + r0;
+#pragma unroll
+                for (int i = 0; i < MTW; ++i) {
+                    const int c = 32 * (MTW * wm + i) + cblk;
+                    const f16x8 ah = cat8(tr_read(s_a, off(ra0, c, 0, CIB)), tr_read(s_a, off(ra0 + 4, c, 0, CIB)));
+                    const f16x8 al = cat8(tr_read(s_a, off(ra0, c, 1, CIB)), tr_read(s_a, off(ra0 + 4, c, 1, CIB)));
+                    f16x8 al2;
+                    if (NP == 3)
+                        al2 = cat8(tr_read(s_a, off(ra0, c, 2, CIB)), tr_read(s_a, off(ra0 + 4, c, 2, CIB)));
+#pragma unroll
+                    for (int j = 0; j < NTW; ++j) {
+                        if (NP == 3) {
+                            acc[x][i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al2, bh[j], acc[x][i][j], 0, 0, 0);
+                            acc[x][i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl2[j], acc[x][i][j], 0, 0, 0);
+                            acc[x][i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bl[j], acc[x][i][j], 0, 0, 0);
+                        }
+                        acc[x][i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[j], acc[x][i][j], 0, 0, 0);
+                        acc[x][i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[j], acc[x][i][j], 0, 0, 0);
+                        acc[x][i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[j], acc[x][i][j], 0, 0, 0);
+                    }
+                }
+            }
+        }
+        if (q + 1 < q1) publish((it + 1) & 1);
+    }
+    const int cin_pad = 64 * p.ci_blocks, cout_pad = 64 * p.co_blocks;
+    const int ml = lane & 31;
+#pragma unroll
+    for (int x = 0; x < KT; ++x) {
+        float *dst = p.partial + ((long long)blockIdx.y * p.T + t0 + x) * cin_pad * cout_pad;
+#pragma unroll
+        for (int i = 0; i < MTW; ++i)
+#pragma unroll
+            for (int j = 0; j < NTW; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int ci = ci0 + 32 * (MTW * wm + i) + (r & 3) + 8 * (r >> 2) + 4 * hl;
+                    const int co = co0 + 32 * (NTW * wn + j) + ml;
+                    if (ci < cin_pad && co < cout_pad)
+                        dst[(long long)ci * cout_pad + co] = ldexpf(acc[x][i][j][r], -(ea + eb));
+                }
+    }
+}
+
 bool aligned16(const void *ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; }
 
 constexpr int HALO_LDS_2PER_CU = 80 * 1024;  // two workgroups per CU
 constexpr int HALO_LDS_MAX = 160 * 1024;
 
-// Halo tiling of an exact-fp32 esr_dconv_fwd launch: false if the gather kernel has to run it (stride > 2, or a halo
-// that does not fit in LDS even at 2-row tiles).
+// Which launches take the halo kernels: stride-1 gathers with one tap (the im2col'd first conv, the 1×1 head) or
+// with >= 9 taps (3×3, 8×8) on grids whose width the 32-column tiles cover with <= 30 % waste.  Measured at config 3
+// (tools/dconv_ab.py, profiles/r3_dconv_ab.txt): the 4×4 stride-2 forward and the 2×2-tap phase classes of its data
+// gradient ran slower than the gather kernel (their source window is 4-6× the outputs), and so did the 8×8 layer's
+// data gradient on its 38-wide grid (two tiles for 38 columns).
+bool halo_wanted(int smy, int smx, int T, int MW) {
+    const int covered = 32 * ((MW + 31) / 32);
+    return smy == 1 && smx == 1 && (T == 1 || T >= 9) && 10 * (covered - MW) <= 3 * MW;
+}
+
+// Halo tiling of an esr_dconv_fwd launch with `pitch` LDS bytes per staged pixel row (144: fp32 / x3, 208: x6):
+// false if the gather kernel has to run it (stride > 2, or a halo that does not fit in LDS even at 2-row tiles).
 bool halo_plan(int MH, int MW, int smy, int smx, int T, const int32_t *offy, const int32_t *offx, HaloParams &h,
-               int &lds) {
+               int &lds, int pitch = PS * 4) {
     if (smy < 1 || smy > 2 || smx < 1 || smx > 2) return false;
     int ymin = offy[0], ymax = offy[0], xmin = offx[0], xmax = offx[0];
     for (int t = 1; t < T; ++t) {
@@ -901,13 +1373,13 @@ bool halo_plan(int MH, int MW, int smy, int smx, int T, const int32_t *offy, con
     h.npar = smx;
     h.IXp = smx == 1 ? 32 + (xmax - xmin) : 32 + ((xmax - xmin) >> 1);
     h.IXt = h.npar * h.IXp;
-    const int b_bytes = NB * PS * 4;
+    const int b_bytes = NB * pitch;
     for (int pass = 0; pass < 2; ++pass) {
         const int budget = pass == 0 ? HALO_LDS_2PER_CU : HALO_LDS_MAX;
         for (int ty = 8; ty >= 2; ty >>= 1) {
             if (ty > 2 && MH <= ty / 2) continue;  // a shorter tile wastes fewer rows
             const int iy = smy * (ty - 1) + (ymax - ymin) + 1;
-            const int a_bytes = iy * h.IXt * PS * 4;
+            const int a_bytes = iy * h.IXt * pitch;
             if (a_bytes + b_bytes <= budget) {
                 h.TY = ty;
                 h.IY = iy;
@@ -929,10 +1401,88 @@ int halo_splits(const HaloParams &h, int B, int n_pad, int nck) {
     return (int)min((long long)nck, (512 + wgs - 1) / wgs);
 }
 
+// The tap-row weight-gradient kernel's shape for a launch: kernel width KT (the taps must be (ky, kx) ky-major with
+// kx consecutive, as the discriminator's convs list them), channel blocks, LDS bytes; false = the per-tap kernel.
+struct RowsPlan {
+    int KT, CIB, COB, HP, lds;
+};
+bool rows_plan(int smx, int T, const int32_t *offy, const int32_t *offx, int np, RowsPlan &r) {
+    if (smx < 1 || smx > 2) return false;
+    int kt = 1;
+    while (kt < T && offy[kt] == offy[0]) ++kt;
+    if (T % kt) return false;
+    for (int t = 0; t < T; ++t)
+        if (offy[t] != offy[t - t % kt] || offx[t] != offx[t - t % kt] + t % kt) return false;
+    if (kt != 1 && kt != 3 && kt != 4 && kt != 8) return false;
+    if (smx == 2 && kt != 4) return false;
+    r.KT = kt;
+    // accumulators per lane = KT · (CIB/64) · (COB/64) · 16 and staging registers must fit one wave per SIMD
+    r.CIB = kt <= 3 ? 128 : 64;
+    r.COB = kt == 1 ? 128 : 64;
+    r.HP = smx == 1 ? WSEG + kt - 1 : WSEG + (kt - 1) / 2;
+    r.lds = smx * r.HP * 2 * np * r.CIB + WSEG * 2 * np * r.COB;
+    return r.lds <= HALO_LDS_MAX - 2048;
+}
+
+int rows_splits(const RowsPlan &r, int B, int MH, int MW, int cin, int cout, int T) {
+    const long long gx = (long long)(T / r.KT) * ((cin + r.CIB - 1) / r.CIB) * ((cout + r.COB - 1) / r.COB);
+    const long long nsegs = (long long)B * MH * ((MW + WSEG - 1) / WSEG);
+    const long long n = (long long)T * 64 * ((cin + 63) / 64) * 64 * ((cout + 63) / 64);
+    long long sp = (512 + gx - 1) / gx;  // ~2 waves of workgroups over 256 CUs (one resident per CU)
+    sp = min(sp, nsegs);
+    sp = min(sp, max(1LL, (64LL << 20) / n));  // partial buffer <= 64 M floats
+    return (int)max(1LL, sp);
+}
+
+// allow a kernel the whole LDS as dynamic shared memory (once per instantiation)
+template <typename K>
+void allow_full_lds(K kernel, bool &done) {
+    if (!done) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  HALO_LDS_MAX - 2048);
+        done = true;
+    }
+}
+
+template <int CIB, int COB, int NP, int KT, int SMX>
+void launch_rows(const WrowParams &p, dim3 grid, int lds, hipStream_t st) {
+    static bool attr = false;
+    allow_full_lds(dconv_wgrad_rows_kernel<CIB, COB, NP, KT, SMX>, attr);
+    hipLaunchKernelGGL((dconv_wgrad_rows_kernel<CIB, COB, NP, KT, SMX>), grid, dim3(NTH), lds, st, p);
+}
+
+template <int NP>
+bool launch_rows_np(const WrowParams &p, const RowsPlan &r, dim3 grid, hipStream_t st) {
+    if (r.KT == 1) launch_rows<128, 128, NP, 1, 1>(p, grid, r.lds, st);
+    else if (r.KT == 3 && p.smx == 1) launch_rows<128, 64, NP, 3, 1>(p, grid, r.lds, st);
+    else if (r.KT == 4 && p.smx == 2) launch_rows<64, 64, NP, 4, 2>(p, grid, r.lds, st);
+    else if (r.KT == 4 && p.smx == 1) launch_rows<64, 64, NP, 4, 1>(p, grid, r.lds, st);
+    else if (r.KT == 8 && p.smx == 1) launch_rows<64, 64, NP, 8, 1>(p, grid, r.lds, st);
+    else return false;
+    return true;
+}
+
+template <int WM, int WN>
+void launch_halo_f32(const FwdParams &p, const HaloParams &h, dim3 grid, int lds, hipStream_t st) {
+    static bool attr = false;
+    allow_full_lds(dconv_fwd_halo_kernel<WM, WN>, attr);
+    hipLaunchKernelGGL((dconv_fwd_halo_kernel<WM, WN>), grid, dim3(NTH), lds, st, p, h);
+}
+
+template <int WM, int WN, int NP>
+void launch_halo_x(const FwdParams &p, const HaloParams &h, dim3 grid, int lds, hipStream_t st) {
+    static bool attr = false;
+    allow_full_lds(dconv_fwd_halo_x_kernel<WM, WN, NP>, attr);
+    hipLaunchKernelGGL((dconv_fwd_halo_x_kernel<WM, WN, NP>), grid, dim3(NTH), lds, st, p, h);
+}
+
 }  // namespace
 
+int g_dconv_rows = 0; // esr_dconv_set_rows: the tap-row weight-gradient kernel (opt-in: slower than the per-tap
+                      // kernel at config 3 with one resident workgroup per CU, profiles/r3_dconv_ab.txt)
+
 int g_dconv_x3 = 0;   // esr_dconv_set_x3
-int g_dconv_halo = 1; // esr_dconv_set_halo: exact-fp32 forward on the halo-tile kernel where it applies
+int g_dconv_halo = 1; // esr_dconv_set_halo: the halo-tile kernels where they apply (halo_wanted), every precision
 int g_dconv_np = 2;   // split pieces of the x3 kernels: 2 = x3, 3 = x6 (esr_dconv_set_x3(3))
 int g_dconv_nb = 128; // x3: widest N tile allowed (esr_dconv_set_x3(2) = 64 only, for A/B)
 
@@ -964,15 +1514,27 @@ extern "C" int esr_dconv_fwd_sk(const float *src, int32_t B, int32_t Hs, int32_t
     if (gx > 0x7fffffff) return ESR_EINVAL;
     HaloParams h;
     int lds = 0;
-    if (!g_dconv_x3 && g_dconv_halo && halo_plan(MH, MW, smy, smx, T, offy, offx, h, lds)) {
-        if (ksplit > nck) return ESR_EINVAL;  // the halo kernel splits the channel chunks
+    const int np = g_dconv_x3 ? g_dconv_np : 0;
+    if (g_dconv_halo && halo_wanted(smy, smx, T, MW) &&
+        halo_plan(MH, MW, smy, smx, T, offy, offx, h, lds, np == 3 ? XPitch<3>::v : PS * 4)) {
+        if (ksplit > nck) return ESR_EINVAL;  // the halo kernels split the channel chunks
         const long long hx = (long long)B * h.tiles_x * h.tiles_y;
         if (hx > 0x7fffffff) return ESR_EINVAL;
         const dim3 hgrid((unsigned)hx, (unsigned)(n_pad / NB), (unsigned)ksplit), block(NTH);
         const hipStream_t st = (hipStream_t)stream;
-        if (h.TY == 8) hipLaunchKernelGGL((dconv_fwd_halo_kernel<2, 2>), hgrid, block, lds, st, p, h);
-        else if (h.TY == 4) hipLaunchKernelGGL((dconv_fwd_halo_kernel<1, 2>), hgrid, block, lds, st, p, h);
-        else hipLaunchKernelGGL((dconv_fwd_halo_kernel<1, 1>), hgrid, block, lds, st, p, h);
+        if (np == 0) {
+            if (h.TY == 8) launch_halo_f32<2, 2>(p, h, hgrid, lds, st);
+            else if (h.TY == 4) launch_halo_f32<1, 2>(p, h, hgrid, lds, st);
+            else launch_halo_f32<1, 1>(p, h, hgrid, lds, st);
+        } else if (np == 2) {
+            if (h.TY == 8) launch_halo_x<2, 2, 2>(p, h, hgrid, lds, st);
+            else if (h.TY == 4) launch_halo_x<1, 2, 2>(p, h, hgrid, lds, st);
+            else launch_halo_x<1, 1, 2>(p, h, hgrid, lds, st);
+        } else {
+            if (h.TY == 8) launch_halo_x<2, 2, 3>(p, h, hgrid, lds, st);
+            else if (h.TY == 4) launch_halo_x<1, 2, 3>(p, h, hgrid, lds, st);
+            else launch_halo_x<1, 1, 3>(p, h, hgrid, lds, st);
+        }
         if (ksplit > 1)
             hipLaunchKernelGGL(dconv_splitk_reduce, dim3((unsigned)((M * n + NTH - 1) / NTH)), block, 0, st, p,
                                ksplit);
@@ -1016,7 +1578,9 @@ extern "C" int esr_dconv_fwd_splits(int32_t B, int32_t MH, int32_t MW, int32_t n
     const int nck = (kc + KC - 1) / KC, n_pad = NB * ((n + NB - 1) / NB);
     HaloParams h;
     int lds = 0;
-    if (!g_dconv_x3 && g_dconv_halo && halo_plan(MH, MW, smy, smx, T, offy, offx, h, lds))
+    const int np = g_dconv_x3 ? g_dconv_np : 0;
+    if (g_dconv_halo && halo_wanted(smy, smx, T, MW) &&
+        halo_plan(MH, MW, smy, smx, T, offy, offx, h, lds, np == 3 ? XPitch<3>::v : PS * 4))
         return halo_splits(h, B, n_pad, nck);
     if (!g_dconv_x3) return 1;
     // x3 gather kernel: ~512 workgroups, at least 8 K steps per slice, for launches that would fill few CUs
@@ -1024,6 +1588,33 @@ extern "C" int esr_dconv_fwd_splits(int32_t B, int32_t MH, int32_t MW, int32_t n
     const int nsteps = T * nck;
     if (wgs >= 512 || nsteps < 16) return 1;
     return (int)max(1LL, min((512 + wgs - 1) / wgs, (long long)(nsteps / 8)));
+}
+
+extern "C" int esr_dconv_wgrad_splits(int32_t B, int32_t MH, int32_t MW, int32_t cin, int32_t cout, int32_t smy,
+                                     int32_t smx, int32_t T, const int32_t *offy, const int32_t *offx) {
+    if (B <= 0 || MH <= 0 || MW <= 0 || cin <= 0 || cout <= 0 || T <= 0 || T > ESR_DCONV_MAX_TAPS || !offy || !offx)
+        return ESR_EINVAL;
+    (void)smy;
+    const int cin_pad = 64 * ((cin + 63) / 64), cout_pad = 64 * ((cout + 63) / 64);
+    const long long n = (long long)T * cin_pad * cout_pad, P = (long long)B * MH * MW;
+    const long long pmax = max(1LL, (64LL << 20) / n);
+    RowsPlan rp;
+    if (g_dconv_x3 && g_dconv_rows && rows_plan(smx, T, offy, offx, g_dconv_np, rp))
+        return rows_splits(rp, B, MH, MW, cin, cout, T);
+    if (g_dconv_x3) {  // per-tap split kernel: 128-channel blocks where the padded widths allow, ~2 workgroups per CU
+        const int cib = cin_pad % 128 == 0 ? 128 : 64, cob = cout_pad % 128 == 0 ? 128 : 64;
+        const long long tiles = (long long)T * (cin_pad / cib) * (cout_pad / cob);
+        return (int)max(1LL, min(min((512 + tiles - 1) / tiles, (P + 255) / 256), pmax));
+    }
+    const long long tiles = (long long)T * (cin_pad / 64) * (cout_pad / 64);  // fp32: ~4 workgroups per CU
+    return (int)max(1LL, min(min((1024 + tiles - 1) / tiles, (P + 255) / 256), pmax));
+}
+
+extern "C" int esr_dconv_set_rows(int32_t on) {
+    if (on < 0 || on > 1) return ESR_EINVAL;
+    const int prev = g_dconv_rows;
+    g_dconv_rows = on;
+    return prev;
 }
 
 extern "C" int esr_dconv_set_halo(int32_t on) {
@@ -1062,6 +1653,26 @@ extern "C" int esr_dconv_wgrad(const float *src, int32_t B, int32_t Hs, int32_t 
     p.pix_per_split = ((P + splits - 1) / splits + WKP - 1) / WKP * WKP;
     p.partial = partial;
     for (int t = 0; t < T; ++t) { p.offy[t] = offy[t]; p.offx[t] = offx[t]; }
+    RowsPlan rp;
+    if (g_dconv_x3 && g_dconv_rows && rows_plan(smx, T, offy, offx, g_dconv_np, rp)) {
+        WrowParams q;
+        q.src = src; q.B = B; q.Hs = Hs; q.Ws = Ws; q.sp = src_pitch; q.cin = cin; q.svec = p.svec;
+        q.dy = dy; q.MH = MH; q.MW = MW; q.dp = dy_pitch; q.cout = cout; q.dvec = p.dvec;
+        q.smy = smy; q.smx = smx; q.T = T; q.KT = rp.KT;
+        q.nseg = (MW + WSEG - 1) / WSEG;
+        const long long nsegs = (long long)B * MH * q.nseg;
+        q.segs_per_split = (nsegs + splits - 1) / splits;
+        q.HP = rp.HP;
+        q.ci_blocks = p.ci_blocks; q.co_blocks = p.co_blocks;
+        q.partial = partial;
+        for (int t = 0; t < T; ++t) { q.offy[t] = offy[t]; q.offx[t] = offx[t]; }
+        const long long gx = (long long)(T / rp.KT) * ((cin + rp.CIB - 1) / rp.CIB) * ((cout + rp.COB - 1) / rp.COB);
+        const dim3 grid((unsigned)gx, (unsigned)splits);
+        const bool ok = g_dconv_np == 3 ? launch_rows_np<3>(q, rp, grid, (hipStream_t)stream)
+                                        : launch_rows_np<2>(q, rp, grid, (hipStream_t)stream);
+        if (!ok) return ESR_EINVAL;
+        return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+    }
     if (g_dconv_x3) {  // x3: 128-channel blocks where the padded width is a multiple of 128
         const int cib = (64 * p.ci_blocks) % 128 == 0 ? 128 : 64, cob = (64 * p.co_blocks) % 128 == 0 ? 128 : 64;
         const long long gx = (long long)T * ((cin + cib - 1) / cib) * ((cout + cob - 1) / cob);

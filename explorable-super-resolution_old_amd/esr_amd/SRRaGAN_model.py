@@ -36,6 +36,7 @@ import torch.distributed as dist
 from . import CEMnet
 from . import engine as E
 from . import networks
+from . import train_engine as TE
 from .flat_optim import FlatAdam
 from .loss import CreateRangeLoss, GANLoss, GradientPenaltyLoss
 
@@ -172,6 +173,8 @@ def _broadcast_buffers(module):
 
 
 LATENT_WEIGHTS_RELATIVE_STD = 0.  # base_model.py:116
+# x3 overflow checks of the training step read once per micro-step (optimize_parameters); 0 = after every pass
+DEFER_OVERFLOW = os.environ.get('ESR_DEFER_OVERFLOW', '1') != '0'
 
 
 class SRRaGANModel:
@@ -420,7 +423,82 @@ class SRRaGANModel:
         return torch.rand(n, 1, 1, 1, device=self.device)
 
     def optimize_parameters(self):
-        """SRRaGAN_model.py:307-575 for the shipped training configuration."""
+        """SRRaGAN_model.py:307-575 for the shipped training configuration.
+
+        The x3 overflow checks of the generator's forward and backward (an activation or scaled gradient beyond the
+        f16 range, or a weight outside its scale) are not read mid-step, where each read drained the stream and left
+        the GPU idle while the host enqueued the discriminator's kernels: the flags are collected on the device
+        (train_engine.deferred_overflow_checks) and read once after the whole micro-step is enqueued.  If one was set,
+        the micro-step is undone from a device snapshot taken before it (both networks' flat parameters, gradients
+        and Adam moments, the discriminator's BatchNorm buffers, the host-side counters, inputs and logs) and redone
+        with the generator in exact fp32 — what the eager per-pass check did.  ESR_DEFER_OVERFLOW=0 keeps the eager
+        checks."""
+        if not DEFER_OVERFLOW or not self.D_exists:
+            return self._optimize_step()
+        self._flush_logs()  # (free: the previous step's check already synchronised)
+        snap = self._snapshot()
+        with TE.deferred_overflow_checks() as chk:
+            self._optimize_step()
+        if chk.overflowed():
+            E.OVERFLOW_RERUNS += 1
+            self._restore(snap)
+            prev = getattr(self._rrdb, 'esr_precision', None)
+            self._rrdb.esr_precision = 'f32'
+            try:
+                with TE.deferred_overflow_checks(on=False):
+                    self._optimize_step()
+            finally:
+                self._rrdb.esr_precision = prev
+
+    _SNAP_ATTRS = ('step', 'gradient_step_num', 'generator_step', 'generator_changed', 'cur_D_update_ratio', 'var_L',
+                   'var_H', 'var_ref', 'model_input', 'fake_H', '_d_logs', '_g_logs')
+
+    def _snapshot(self):
+        """Everything one micro-step changes (see optimize_parameters): device copies are enqueued, not waited for."""
+        host = {k: self.__dict__[k] for k in self._SNAP_ATTRS if k in self.__dict__}
+        host['_d_logs_n'] = len(self.__dict__.get('_d_logs') or [])
+        host['_g_logs_n'] = {k: len(v) for k, v in (self.__dict__.get('_g_logs') or {}).items()}
+        host['_log_n'] = {k: len(v) for k, v in self._log_dict.items()}
+        dev = []
+        for o in self.optimizers:
+            st = o.state.get(o.flat, {})
+            dev.append((o, o.flat.data.clone(), o.flat.grad.clone(),
+                        {k: (v.clone() if torch.is_tensor(v) else v) for k, v in st.items()}))
+        bufs = [(b, b.clone()) for n, b in self.netD.named_buffers()]
+        return host, dev, bufs
+
+    def _restore(self, snap):
+        host, dev, bufs = snap
+        for k in self._SNAP_ATTRS:
+            if k in host:
+                self.__dict__[k] = host[k]
+            else:
+                self.__dict__.pop(k, None)
+        if host.get('_d_logs') is not None:
+            del host['_d_logs'][host['_d_logs_n']:]
+        for k, n in host['_g_logs_n'].items():
+            del self._g_logs[k][n:]
+        self._pending_logs = []  # this micro-step's deferred log values (flushed before the snapshot)
+        for k, v in self._log_dict.items():
+            del v[host['_log_n'].get(k, 0):]
+        with torch.no_grad():
+            for o, data, grad, st in dev:
+                o.flat.data.copy_(data)
+                o.flat.grad.copy_(grad)
+                o._sync_views()
+                if st:
+                    cur = o.state[o.flat]
+                    for k, v in st.items():
+                        if torch.is_tensor(v):
+                            cur[k].copy_(v)
+                        else:
+                            cur[k] = v
+                else:
+                    o.state.pop(o.flat, None)
+            for b, v in bufs:
+                b.copy_(v)
+
+    def _optimize_step(self):
         t = self.opt['train']
         self.gradient_step_num = self.step // self.max_accumulation_steps
         first_acc_G = self.step % self.grad_accumulation_steps_G == 0

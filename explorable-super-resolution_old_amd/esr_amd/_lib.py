@@ -93,6 +93,9 @@ _SIGNATURES = {
     'esr_dconv_fwd_splits': [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_int),
                              ctypes.POINTER(c_int)],
     'esr_dconv_set_halo': [c_int],
+    'esr_dconv_wgrad_splits': [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_int),
+                               ctypes.POINTER(c_int)],
+    'esr_dconv_set_rows': [c_int],
     'esr_cem_adjoint_set_generic': [c_int],
     'esr_dconv_wgrad': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int,
                         c_int, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int), c_int, c_void_p, c_void_p],

@@ -24,8 +24,6 @@ import torch.nn.functional as F
 from . import _lib
 
 MAX_TAPS = 64
-_WG_SPLIT_TARGET = 1024          # workgroups a weight-gradient launch aims for (split-K over pixels)
-_WG_PARTIAL_MAX = 64 << 20       # floats of split-K partials per launch
 # Precision of the discriminator convolutions (forward, data and weight gradients): 'x3' = split-f16 operands (hi, lo)
 # with per-K-step power-of-two scaling on f16 MFMA (3 products, ~2^-22 per product), 'x6' = three f16 pieces and six
 # products (each operand to ~33 bits: an fp32 FMA chain's accuracy, esr_dconv.hip), 'f32' = exact fp32 MFMA.
@@ -176,22 +174,17 @@ def conv_wgrad(x, gy, k, s, p):
     T = k * k
     cin_pad, cout_pad = 64 * ((Ci + 63) // 64), 64 * ((Co + 63) // 64)
     n = T * cin_pad * cout_pad
-    P = B * Ho * Wo
-    if PRECISION != 'f32':  # split kernels: 128-channel blocks where the padded width allows, ~2 workgroups per CU
-        cib, cob = (128 if cin_pad % 128 == 0 else 64), (128 if cout_pad % 128 == 0 else 64)
-        tiles = T * (cin_pad // cib) * (cout_pad // cob)
-        splits = max(1, min(-(-512 // tiles), -(-P // 256), _WG_PARTIAL_MAX // n))
-    else:
-        tiles = T * (cin_pad // 64) * (cout_pad // 64)
-        splits = max(1, min(-(-_WG_SPLIT_TARGET // tiles), -(-P // 256), _WG_PARTIAL_MAX // n))
-    partial = torch.empty(splits * n, device=x.device, dtype=torch.float32)
-    red = torch.empty(n, device=x.device, dtype=torch.float32)
     taps = [(ky, kx) for ky in range(k) for kx in range(k)]
+    oy, ox = _i32([ky - p for ky, _ in taps]), _i32([kx - p for _, kx in taps])
     lib = _lib_for_launch()
     st = _stream(x)
-    _lib.check(lib.esr_dconv_wgrad(x.data_ptr(), B, H, W, Ci, Ci, gy.data_ptr(), Ho, Wo, Co, Co, s, s, T,
-                                   _i32([ky - p for ky, _ in taps]), _i32([kx - p for _, kx in taps]), splits,
-                                   partial.data_ptr(), st), 'esr_dconv_wgrad')
+    splits = lib.esr_dconv_wgrad_splits(B, Ho, Wo, Ci, Co, s, s, T, oy, ox)  # split-K over pixels, library's choice
+    if splits < 1:
+        raise RuntimeError('esr_dconv_wgrad_splits failed with esr_status %d' % splits)
+    partial = torch.empty(splits * n, device=x.device, dtype=torch.float32)
+    red = torch.empty(n, device=x.device, dtype=torch.float32)
+    _lib.check(lib.esr_dconv_wgrad(x.data_ptr(), B, H, W, Ci, Ci, gy.data_ptr(), Ho, Wo, Co, Co, s, s, T, oy, ox,
+                                   splits, partial.data_ptr(), st), 'esr_dconv_wgrad')
     _lib.check(lib.esr_wgrad_reduce(partial.data_ptr(), splits, n, 1.0, red.data_ptr(), st), 'esr_wgrad_reduce')
     return red.view(k, k, cin_pad, cout_pad)[:, :, :Ci, :Co].permute(3, 2, 0, 1).contiguous()
 

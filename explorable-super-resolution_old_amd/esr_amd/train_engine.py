@@ -14,6 +14,7 @@ CEM is one torch.autograd.Function whose backward runs libesr_amd kernels (exact
 The reference's residual scales (0.2 in RDB and RRDB, block.py:235, 270) are folded into the packed backward weights
 and the reduction scales.
 """
+import contextlib
 import ctypes
 import math
 import os
@@ -39,6 +40,52 @@ DGRAD_X3 = os.environ.get('ESR_DGRAD_X3', '1') != '0'
 
 def _z(dev, *s):
     return torch.zeros(*s, device=dev, dtype=torch.float32)
+
+
+class DeferredOverflow:
+    """The x3 overflow flags of the training forwards / backwards run inside `deferred_overflow_checks()`: instead of
+    a blocking 4-byte read right after each forward and backward (which drains the stream and leaves the GPU idle while
+    the host enqueues the discriminator's many small kernels), the flags are copied aside on the device and read once,
+    by the caller, after the whole training step is enqueued (SRRaGANModel.optimize_parameters, which then redoes the
+    step in exact fp32 from a snapshot when one was set)."""
+
+    def __init__(self):
+        self.flags = []   # device int32 scalars (activation / gradient overflow, weight out of its scale)
+        self.resets = []  # (weight-flag tensor, callback resetting the x3 weight scales)
+
+    def add(self, overflow, bad, reset):
+        self.flags.append(overflow.clone())
+        self.resets.append((bad.clone(), reset))
+
+    def overflowed(self):
+        """True if any deferred forward or backward overflowed (one device-to-host read; all-reduced over ranks)."""
+        if not self.flags:
+            return False
+        t = torch.stack([f.reshape(()).float() for f in self.flags] +
+                        [b.reshape(()).float() for b, _ in self.resets])
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)  # every rank redoes the step together
+        vals = t.tolist()
+        n = len(self.flags)
+        for (_, reset), bad in zip(self.resets, vals[n:]):
+            if bad:
+                reset()  # new x3 weight scales at the next x3 forward / backward
+        return any(v != 0 for v in vals)
+
+
+_DEFERRED = [None]
+
+
+@contextlib.contextmanager
+def deferred_overflow_checks(on=True):
+    """Collect (on=True) or check eagerly (on=False) the x3 overflow flags of the training passes in this block."""
+    prev = _DEFERRED[0]
+    _DEFERRED[0] = DeferredOverflow() if on else None
+    try:
+        yield _DEFERRED[0]
+    finally:
+        _DEFERRED[0] = prev
 
 
 class TrainWorkspace:
@@ -610,7 +657,9 @@ class _GeneratorFn(torch.autograd.Function):
         xd = x.detach().contiguous()
         out, graphed = _run_graphed(ws, key, fwd, xd)
         split = prec == 'x3'
-        if split and int(ws.overflow.item()):  # an activation (or weight) beyond the f16 range: redo in exact fp32
+        if split and _DEFERRED[0] is not None:  # checked once after the whole training step (DeferredOverflow)
+            _DEFERRED[0].add(ws.overflow, bad, pk.reset_train_x3)
+        elif split and int(ws.overflow.item()):  # an activation (or weight) beyond the f16 range: redo in exact fp32
             E.OVERFLOW_RERUNS += 1
             if int(bad.item()):
                 pk.reset_train_x3()  # new scales at the next x3 forward
@@ -642,7 +691,9 @@ class _GeneratorFn(torch.autograd.Function):
                                                           split=ctx.split, x3=x3),
                 d_out.contiguous())
         (flat, dx), graphed = run(x3)
-        if x3 and int(ctx.ws.bwd_overflow.item()):  # a scaled gradient (or weight) left f16's range: redo in fp32
+        if x3 and _DEFERRED[0] is not None:  # checked once after the whole training step (DeferredOverflow)
+            _DEFERRED[0].add(ctx.ws.bwd_overflow, bp._x3_bad, bp.reset_x3)
+        elif x3 and int(ctx.ws.bwd_overflow.item()):  # a scaled gradient (or weight) left f16's range: redo in fp32
             E.OVERFLOW_RERUNS += 1
             if int(bp._x3_bad.item()):
                 bp.reset_x3()  # new weight scales at the next x3 backward

@@ -276,10 +276,10 @@ int esr_dconv_fwd_sk(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_
  * where its grid has < 512 workgroups (the 8×8 pseudo-FC layer); x3: ~512 workgroups, >= 8 K steps per slice. */
 int esr_dconv_fwd_splits(int32_t B, int32_t MH, int32_t MW, int32_t n_out, int32_t kc, int32_t smy, int32_t smx,
                          int32_t T, const int32_t *offy, const int32_t *offx);
-/* Exact-fp32 esr_dconv_fwd kernel: 1 (default) = halo-tile implicit GEMM (each source pixel of a 32-channel chunk
- * staged in LDS once for all taps; strides 1 and 2) where the halo fits in LDS, the gather kernel otherwise; 0 = the
- * gather kernel always (A/B).  Bitwise-different summation order only through the split-K slices.  Returns the
- * previous setting. */
+/* esr_dconv_fwd kernels: 1 (default) = the halo-tile implicit GEMMs (each source pixel of a 32-channel chunk staged
+ * in LDS once for all taps; exact fp32, or split x3 / x6 with a per-chunk source scale and a per-step weight scale)
+ * for stride-1 launches with one tap or >= 9 taps where the halo fits in LDS, the gather kernels otherwise; 0 = the
+ * gather kernels always (A/B).  Returns the previous setting. */
 int esr_dconv_set_halo(int32_t on);
 /* Precision of esr_dconv_fwd (process-wide): 0 (the library default) = exact fp32 MFMA; 1 = x3: both operands split
  * into f16 hi/lo at staging after a power-of-two scaling per K step (one tap × 32 channels) chosen from the
@@ -294,6 +294,16 @@ int esr_dconv_set_x3(int32_t on);
  *   partial[s][t][ci][co] = sum over the pixels of split s of src[b, smy*Y+offy[t], smx*X+offx[t], ci] * dy[b, Y, X, co]
  * partial: [splits][T][cin_pad][cout_pad], cin_pad = 64*ceil(cin/64), cout_pad = 64*ceil(cout/64); reduce the splits
  * with esr_wgrad_reduce (fixed order, deterministic). */
+/* The `splits` esr_dconv_wgrad should get for this geometry under the current precision / kernel settings (the
+ * caller sizes `partial` with it).  Returns ESR_EINVAL on bad arguments. */
+int esr_dconv_wgrad_splits(int32_t B, int32_t MH, int32_t MW, int32_t cin, int32_t cout, int32_t smy, int32_t smx,
+                           int32_t T, const int32_t *offy, const int32_t *offx);
+/* Split-precision (x3 / x6) weight gradient kernel: 1 = the tap-row kernel (a workgroup owns one kernel row of taps,
+ * a K step is a 64-pixel output-row segment whose output gradient and source row are staged once for all the row's
+ * taps) where the taps are (ky, kx) ky-major with kx consecutive and the kernel width is 1, 3, 4 (stride 1 or 2) or
+ * 8; 0 (default: the tap-row kernel measured 1.7× slower at config 3) = the per-tap kernel.  Returns the previous
+ * setting. */
+int esr_dconv_set_rows(int32_t on);
 int esr_dconv_wgrad(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t src_pitch, int32_t cin,
                     const float *dy, int32_t MH, int32_t MW, int32_t dy_pitch, int32_t cout, int32_t smy, int32_t smx,
                     int32_t T, const int32_t *offy, const int32_t *offx, int32_t splits, float *partial,

@@ -126,8 +126,15 @@ def build_reference(cfg, dtype):
     return model
 
 
-def run_reference(cfg, dtype):
+def run_reference(cfg, dtype, perturb=None):
+    """perturb = seed: every G and D parameter multiplied by (1 + 2^-24·N(0,1)) before the run — a rounding-level
+    kick, to sample how far the reference's own float32 trajectory moves under perturbations of that size."""
     model = build_reference(cfg, dtype)
+    if perturb is not None:
+        gen = torch.Generator().manual_seed(perturb)
+        with torch.no_grad():
+            for p in list(model.netG.parameters()) + list(model.netD.parameters()):
+                p.mul_(1 + 2.0 ** -24 * torch.randn(p.shape, generator=gen, dtype=p.dtype))
     g0 = {k: v.detach().clone() for k, v in model.netG.named_parameters()}
     d0 = {k: v.detach().clone() for k, v in model.netD.named_parameters()}
     FixedRP.stream = random_points(cfg)
@@ -154,10 +161,15 @@ def digest(prefix, final, init, d, proj_seed):
             d['%s_delta:%s' % (prefix, k)] = delta.astype(np.float64)
 
 
+N_PERTURBED = 6  # float32 reference runs from rounding-level perturbed weights (f32p0 .. f32p5)
+
+
 def train_fixture(name, cfg):
     d = {'cfg': np.str_(json.dumps(cfg))}
-    for tag, dtype in (('f32', torch.float32), ('f64', torch.float64)):
-        model, g0, d0, flags = run_reference(cfg, dtype)
+    runs = [('f32', torch.float32, None), ('f64', torch.float64, None)] + \
+        [('f32p%d' % i, torch.float32, 7000 + i) for i in range(N_PERTURBED)]
+    for tag, dtype, perturb in runs:
+        model, g0, d0, flags = run_reference(cfg, dtype, perturb)
         d['%s_generator_step' % tag] = np.array(flags)
         for k, v in model.log_dict.items():
             if v:

@@ -1,0 +1,133 @@
+"""Production-grid parity checks shared by tests/test_gpu_grid.py and bench.py's reference-check leg (TEST
+INFRASTRUCTURE: reference-made fixtures tests/golden/grid_c3_train.npz and grid_c5_zgrad.npz; the seeded weights and
+inputs come from oracle/recipe.py's NumPy recipe).
+
+Each check returns {'ok': bool, 'worst_frac_of_bound': float, 'fails': [...], 'lines': [...]} where a quantity's
+bound is the reference's own float32 distance to its float64 run × 5 plus a floor of 1e-4 of the quantity's scale
+(conftest.grad_parity's yardstick), evaluated through K seeded random projections where the fixture cannot hold the
+full float64 tensors."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+for _p in (HERE, os.path.join(HERE, 'golden'), os.path.dirname(HERE)):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+FACTOR, FLOOR = 5.0, 1e-4
+
+
+def _proj(v, seed, idx, k):
+    g = np.asarray(v, dtype=np.float64).ravel()
+    return np.random.default_rng([seed, idx]).standard_normal((k, g.size)) @ g
+
+
+def _result(fails, worst, lines):
+    return {'ok': not fails, 'worst_frac_of_bound': round(float(worst), 4), 'fails': fails, 'lines': lines}
+
+
+def c3_training_step(dev, precision='x3', d_precision=None):
+    """Config 3 (B=16 × 96² LR, RRDB-23, latent, CEM train mode, WGAN-GP): two optimize_parameters micro-steps against
+    the reference's own run (tests/golden/make_golden_train.py c3); the step-1 gradient of every G and D parameter,
+    the logs and the D BatchNorm buffers."""
+    from test_gpu_train_loop import D_DIFFERENCES, _close, _run_port
+    from train_recipe import grad_projections
+    from esr_amd import dconv
+    d = np.load(os.path.join(HERE, 'golden', 'grid_c3_train.npz'))
+    cfg = json.loads(str(d['cfg']))
+    prev = dconv.PRECISION
+    try:
+        model, _, _, flags = _run_port(cfg, precision, dev, d_precision)
+    finally:
+        dconv.set_precision(prev)
+    fails, worst, lines = [], 0.0, []
+    if not flags == list(d['f64_generator_step']) == list(d['f32_generator_step']):
+        fails.append(('generator_step', flags))
+    for net, tag in ((model.netG, 'G'), (model.netD, 'D')):
+        errs = []
+        for i, (k, p) in enumerate(net.named_parameters()):
+            key = '%s_gproj:%s' % (tag, k)
+            if 'f64_' + key not in d.files:
+                continue
+            if p.grad is None:
+                fails.append((tag, k, 'no gradient'))
+                continue
+            mine = grad_projections(p.grad.detach().double().cpu().numpy(), cfg['seed'] + (10 if tag == 'G' else 11),
+                                    i, cfg['proj'])
+            p64, p32 = d['f64_' + key], d['f32_' + key]
+            err, base, norm = np.linalg.norm(mine - p64), np.linalg.norm(p32 - p64), np.linalg.norm(p64)
+            bound = FACTOR * base + FLOOR * max(norm, 1e-30)
+            errs.append(err / bound)
+            if err > bound:
+                fails.append((tag, k, 'err %.3e bound %.3e (ref f32 %.3e, |proj| %.3e)' % (err, bound, base, norm)))
+        lines.append('%s: %d parameter gradients, worst at %.1f %% of its bound, median %.1f %%' % (
+            tag, len(errs), 100 * max(errs), 100 * float(np.median(errs))))
+        worst = max(worst, max(errs))
+    for f in [f for f in d.files if f.startswith('f64_log:')]:
+        key = f[len('f64_log:'):]
+        mine = np.array(model.log_dict[key], dtype=np.float64)
+        ref64, ref32 = d[f], d['f32_log:' + key]
+        if mine.shape != ref64.shape:
+            fails.append(('log', key, 'shape %s vs %s' % (mine.shape, ref64.shape)))
+            continue
+        scale = None
+        if key in D_DIFFERENCES:
+            scale = 2 * (np.linalg.norm(d['f64_log:D_real'][:, 1]) + np.linalg.norm(d['f64_log:D_fake'][:, 1]))
+        ok, msg, r = _close(mine[:, 1], ref32[:, 1], ref64[:, 1], scale)
+        lines.append('log %-24s %s' % (key, msg))
+        worst = max(worst, r)
+        if not ok:
+            fails.append(('log', key, msg))
+    for k, v in model.netD.state_dict().items():
+        if 'running' in k:
+            ok, msg, r = _close(v.double().cpu().numpy(), d['f32_Dbuf:' + k], d['f64_Dbuf:' + k])
+            worst = max(worst, r)
+            if not ok:
+                fails.append(('D buffer', k, msg))
+    return _result(fails, worst, lines)
+
+
+def c5_z_gradients(dev, precision='x3'):
+    """Config 5 (latent RRDB-23 + CEM eval with the reference-made learned 13×13 kernel, generator frozen, B=8 × 128²):
+    dL/dZ, dL/dLR and the output of images 0 and 7 against the reference's autograd (make_golden.py c5grid)."""
+    import esr_amd
+    from esr_amd import CEMnet as C
+    from esr_amd import engine
+    from oracle.recipe import seeded_inputs, seeded_params
+    d = np.load(os.path.join(HERE, 'golden', 'grid_c5_zgrad.npz'))
+    cfg = json.loads(str(d['cfg']))
+    B, h, K = cfg['B'], cfg['h'], cfg['proj']
+    net = esr_amd.RRDBNet(3, 3, 64, cfg['nb'], latent_input='all_layers_HR_downscaled', num_latent_channels=3)
+    model = C.CEMnet(C.Get_CEM_Config(4), upscale_kernel=d['kernel']).WrapArchitecture_PyTorch(net)
+    sd = model.state_dict()
+    params = seeded_params([(n, tuple(v.shape)) for n, v in sd.items()], cfg['seed'], w_scale=cfg['w_scale'])
+    model.load_state_dict({n: torch.from_numpy(v) for n, v in params.items()}, strict=False)
+    model = model.to(dev)
+    model.eval()
+    engine.set_precision(model, precision)
+    for q in model.parameters():
+        q.requires_grad = False
+    lr, z = seeded_inputs(cfg['seed'] + 1, (B, 3, h, h), (B, 3, 4 * h, 4 * h), z_mode='pixel')
+    R = np.random.default_rng(cfg['seed'] + 2).standard_normal((B, 3, 4 * h, 4 * h)).astype(np.float32)
+    zt = torch.from_numpy(z).to(dev).requires_grad_(True)
+    lt = torch.from_numpy(lr).to(dev).requires_grad_(True)
+    out = model(torch.cat([zt.view(B, 48, h, h), lt], 1))
+    (out * torch.from_numpy(R).to(dev)).sum().backward()
+    fails, worst, lines = [], 0.0, []
+    for i in cfg['images']:
+        for name, v in (('dz', zt.grad[i]), ('dlr', lt.grad[i]), ('out', out.detach()[i])):
+            mine = _proj(v.double().cpu().numpy(), cfg['seed'] + {'dz': 10, 'dlr': 11, 'out': 12}[name], i, K)
+            p64, p32 = d['f64_%s_proj:%d' % (name, i)], d['f32_%s_proj:%d' % (name, i)]
+            err, base, norm = np.linalg.norm(mine - p64), np.linalg.norm(p32 - p64), np.linalg.norm(p64)
+            # the output against the north_star bar's tenth (1e-4 relative on the projections); gradients as above
+            bound = 1e-4 * norm if name == 'out' else FACTOR * base + FLOOR * norm
+            worst = max(worst, err / bound)
+            lines.append('image %d %-4s err %.3e  bound %.3e  (%.1f %%; ref f32 %.3e, |proj| %.3e)' % (
+                i, name, err, bound, 100 * err / bound, base, norm))
+            if err > bound:
+                fails.append((i, name, err, bound))
+    return _result(fails, worst, lines)

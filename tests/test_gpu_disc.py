@@ -35,18 +35,21 @@ pytestmark = pytest.mark.gpu
     (32, 64, 4, 2, 1, 41, 75),     # stride-2 halo (column-parity de-interleave), ragged
     (256, 100, 8, 1, 0, 38, 38),   # the config-3 pseudo-FC geometry: split-K over the channel chunks
 ])
-@pytest.mark.parametrize('precision', ['x3', 'x6', 'f32', 'f32_gather'])
+@pytest.mark.parametrize('precision', ['x3', 'x6', 'f32', 'x3_gather', 'x6_gather', 'f32_gather'])
 def test_dconv_ops_vs_float64(gpu_device, ci, co, k, s, p, H, W, precision):
-    """f32 = the halo-tile forward kernel (default), f32_gather = the per-tap gather kernel it replaced."""
-    prev = dconv.set_precision('f32' if precision.startswith('f32') else precision)
+    """x3 / x6 / f32 with the halo-tile forward and tap-row weight-gradient kernels where they apply (default),
+    *_gather = the per-tap kernels everywhere."""
+    prev = dconv.set_precision(precision.split('_')[0])
     lib = _lib.load()
-    prev_halo = lib.esr_dconv_set_halo(0 if precision == 'f32_gather' else 1)
+    prev_halo = lib.esr_dconv_set_halo(0 if precision.endswith('_gather') else 1)
+    prev_rows = lib.esr_dconv_set_rows(0 if precision.endswith('_gather') else 1)
     try:
-        _dconv_ops(gpu_device, ci, co, k, s, p, H, W, scale=1e-9 if precision in ('x3', 'x6') else 1.0,
+        _dconv_ops(gpu_device, ci, co, k, s, p, H, W, scale=1.0 if precision.startswith('f32') else 1e-9,
                    tol=1e-5)
     finally:
         dconv.set_precision(prev)
         lib.esr_dconv_set_halo(prev_halo)
+        lib.esr_dconv_set_rows(prev_rows)
 
 
 def _dconv_ops(gpu_device, ci, co, k, s, p, H, W, scale, tol=1e-5):

@@ -37,7 +37,7 @@ def step(variant):
         it = (rp * fake + (1 - rp) * real).requires_grad_(True)
         loss = loss + 10 * gp(it, D(it))
     loss.backward()
-    return {k: p.grad.clone() for k, p in D.named_parameters()}
+    return {k: p.grad.clone() for k, p in D.named_parameters() if p.grad is not None}
 
 
 for variant in ('real', 'nogp', 'gp', 'all'):

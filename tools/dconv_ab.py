@@ -39,13 +39,14 @@ def main():
         row, outs = {}, {}
         gy = torch.randn(B, Ho, Ho, co, device=dev) * 1e-8
         for rnd in range(2):
-            for tag, mode, halo in (('f32', 0, 0), ('f32_halo', 0, 1), ('x3_n64', 2, 0), ('x3_n128', 1, 0),
-                                    ('x6', 3, 0)):
+            for tag, mode, halo in (('f32', 0, 0), ('f32_halo', 0, 1), ('x3_n128', 1, 0), ('x3_halo', 1, 1),
+                                    ('x6', 3, 0), ('x6_halo', 3, 1)):
                 dconv.set_precision({0: 'f32', 3: 'x6'}.get(mode, 'x3'))
                 dconv._applied[0] = None
                 dconv._lib_for_launch()
                 lib.esr_dconv_set_x3(mode)
                 lib.esr_dconv_set_halo(halo)
+                lib.esr_dconv_set_rows(halo)  # *_halo: the halo forward and the tap-row weight gradient
                 for _ in range(2):
                     dconv.conv_forward(x, w, b, k, s, p)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -77,13 +78,14 @@ def main():
                     row[tag + '_tflops'] = round(flops / us / 1e6, 1)
                     row[tag + '_wgrad_us'] = round(us_w, 1)
                     row[tag + '_dgrad_us'] = round(us_d, 1)
-        for tag in ('f32_halo', 'x3_n64', 'x3_n128', 'x6'):
+        for tag in ('f32_halo', 'x3_n128', 'x3_halo', 'x6', 'x6_halo'):
             row[tag + '_diff'] = float((outs[tag] - outs['f32']).norm() / outs['f32'].norm())
             row[tag + '_dgrad_diff'] = float((outs[tag + 'd'] - outs['f32d']).norm() / outs['f32d'].norm())
             row[tag + '_wgrad_diff'] = float((outs[tag + 'w'] - outs['f32w']).norm() / outs['f32w'].norm())
         print(name, json.dumps(row), flush=True)
     lib.esr_dconv_set_x3(0)
     lib.esr_dconv_set_halo(1)
+    lib.esr_dconv_set_rows(1)
     dconv._applied[0] = None
 
 

@@ -64,7 +64,9 @@ def run():
 
 a, la = run()
 b, lb = run()
-print('G=%s D=%s %s: %d micro-steps' % (g, d, name, len(a)))
+c, lc = run()
+print('G=%s D=%s %s: %d micro-steps; run 2 == run 3: %s' % (
+    g, d, name, len(a), all(x[1] == y[1] for x, y in zip(b, c)) and lb == lc))
 for (k, da, ga), (_, db, gb) in zip(a, b):
     diff = [n for n in da if da[n] != db[n]]
     gd = [(n, float((ga[n] - gb[n]).abs().max() / ga[n].abs().max().clamp_min(1e-30))) for n in ga
