@@ -161,7 +161,13 @@ def digest(prefix, final, init, d, proj_seed):
             d['%s_delta:%s' % (prefix, k)] = delta.astype(np.float64)
 
 
-N_PERTURBED = 6  # float32 reference runs from rounding-level perturbed weights (f32p0 .. f32p5)
+# Optional float32 reference runs from rounding-level perturbed weights (f32p0 ..), a sensitivity study: the loop test
+# takes the largest of their distances to the float64 run as its yardstick when present.  Off for the committed
+# fixtures: regenerated on this container (round 3) the reference's own float64 AND float32 trajectories left the
+# committed ones (made by the same script on round 2's container) after the second micro-step — a different
+# generator_step sequence in adaptive_rel — while the perturbed runs all followed the new trajectory: the reference's
+# loop is platform-sensitive beyond what a rounding-level kick shows.  The committed fixtures stay.
+N_PERTURBED = int(os.environ.get('ESR_GOLDEN_PERTURBED', '0'))
 
 
 def train_fixture(name, cfg):
