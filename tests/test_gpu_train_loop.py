@@ -4,8 +4,12 @@ tests/golden/make_golden_train.py on the same seeded weights, batches and WGAN-G
     gradient accumulation 2, relativistic and non-relativistic D) — exactly;
   * every log_dict series (D/G losses, D statistics, update ratio), the G and D parameter updates after Adam (per-key
     norms, projections on a seeded direction, full changes of the small keys) and the D BatchNorm running buffers.
-Yardstick: the reference ran in float32 and in float64; the port's L2 distance to the float64 run must be within 5×
-the reference's own float32 distance plus a floor of 1e-4 of the quantity's scale.  GAN training amplifies rounding
+Yardstick: the reference ran in float64 and in float32 — the plain float32 run and 6 more from weights multiplied by
+(1 + 2^-24·N(0,1)) (tests/golden/make_golden_train.py, ESR_GOLDEN_PERTURBED=6): the port's L2 distance to the float64
+run must be within 5× the largest of those 7 float32 distances plus a floor of 1e-4 of the quantity's scale.  A
+single float32 run is one sample of a spread: under rounding-level kicks the reference's own float32 error of a D
+statistic moves by up to 3-5× (e.g. adaptive_rel D_real 3.2e-5 .. 9.3e-5, classifier BN running mean 4.6e-5 ..
+3.8e-4), so bounding by the one sample made the test flip on reordering alone.  GAN training amplifies rounding
 (the reference's own float32 and float64 runs differ by up to a few % in late differences of nearly equal losses), so
 the scale of a series that is a difference of D outputs (D_logits_diff, l_d_real/l_d_fake/l_d_real_fake — relativistic
 or not) is the norm of the D outputs it is formed from, not of the difference itself.  Projections of the parameter
@@ -94,7 +98,7 @@ def _run_port(cfg, precision, dev, d_precision=None):
 def loop_margins(name, precision, dev, d_precision=None):
     """Run the port on fixture `name`; return (generator_step flags ok, [(kind, key, ok, message, err/bound)])."""
     from esr_amd import dconv
-    d = np.load(os.path.join(HERE, 'golden', 'train_%s.npz' % name))
+    d = np.load(os.path.join(os.environ.get('ESR_LOOP_FIXTURES', os.path.join(HERE, 'golden')), 'train_%s.npz' % name))
     cfg = json.loads(str(d['cfg']))
     prev = dconv.PRECISION
     try:

@@ -64,3 +64,29 @@ def test_z_optimizer_loop_matches_oracle(gpu_device, objective):
     assert ok, msg
     assert [p.requires_grad for p in model.netG.parameters()] == status  # generator unfrozen again
     assert len(zo.loss_values) == iters
+
+
+def test_z_optimizer_overflow_redo_equals_fp32_loop(gpu_device):
+    """Z_optimizer.optimize reads the generator's x3 overflow flags once per iteration: with inputs whose activations
+    leave the f16 range, every iteration is redone from its snapshot in exact fp32, so the loop ends bitwise where the
+    same loop with an exact-fp32 generator does."""
+    from esr_amd import engine
+    nb, B, h, w, iters = 1, 2, 12, 12, 3
+    lr, z0 = seeded_inputs(72, (B, 3, h, w), (B, 3, 4 * h, 4 * w), z_mode='pixel')
+    outs = []
+    before = engine.OVERFLOW_RERUNS
+    for prec in ('x3', 'f32'):
+        torch.manual_seed(0)
+        model = SRRaGANModel(_opt(nb), device=gpu_device)
+        sd = model.netG.module.state_dict()
+        params = seeded_params([(k, tuple(v.shape)) for k, v in sd.items()], 71, w_scale=0.5)
+        model.netG.module.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=False)
+        engine.set_precision(model.netG, prec)
+        data = {'LR': torch.from_numpy(lr * 3e4).to(gpu_device), 'Z': torch.from_numpy(0.9 * z0).to(gpu_device)}
+        model.feed_data(data, need_HR=False)
+        model.test()
+        model.netG.eval()
+        zo = Z_optimizer('max_STD', [4 * h, 4 * w], model, 1.0, iters, data=data, initial_LR=0.05, batch_size=B)
+        outs.append((zo.optimize().cpu(), list(zo.loss_values)))
+    assert engine.OVERFLOW_RERUNS >= before + iters
+    assert torch.equal(outs[0][0], outs[1][0]) and outs[0][1] == outs[1][1]

@@ -17,7 +17,11 @@ pairs = [a.split(':') for a in sys.argv[1:]] or [['x3', 'x3'], ['x3', 'f32'], ['
 dev = torch.device('cuda:0')
 for name in sorted(TRAIN_CFGS):
     for g, d in pairs:
-        ok, rows = loop_margins(name, g, dev, d)
+        try:
+            ok, rows = loop_margins(name, g, dev, d)
+        except AssertionError as e:
+            print('== %s  G=%s D=%s  trajectory left the fixture: %s' % (name, g, d, e))
+            continue
         rows.sort(key=lambda r: -r[4])
         print('== %s  G=%s D=%s  flags %s  worst %.1f %%' % (name, g, d, 'ok' if ok else 'DIFFER', 100 * rows[0][4]))
         for kind, key, _, msg, _ in rows[:6]:
