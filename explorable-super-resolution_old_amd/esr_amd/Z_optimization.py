@@ -15,6 +15,8 @@ desired_SVD, Mag, VGG) are image-editing losses of the GUI, outside this hot pat
 import numpy as np
 import torch
 
+from . import engine as E
+from . import train_engine as TE
 from .loss import GANLoss
 
 _UNSUPPORTED = ('scribble', 'hist', 'dict', 'periodicity', 'local', 'desired_SVD', 'Mag', 'VGG')
@@ -218,25 +220,25 @@ class Z_optimizer:
                 first, last = float(self.loss_values[self.max_iters]), float(self.loss_values[-1])
                 if (first - last) / np.abs(first) < 1e-2 * self.LR:
                     break
-            self.optimizer.zero_grad()
-            self.data['Z'] = self.Z_model()
-            self.model.feed_data(self.data, need_HR=False)
-            self.model.fake_H = self.model.netG(self.model.model_input)
-            if self.model_training:
-                self.model.fake_H = self.HR_unpadder(self.model.fake_H)
-            Z_loss = self._loss(z_iter)
-            if self.loggers is not None:
-                for n, logger in enumerate(self.loggers):
-                    v = Z_loss[n].item() if Z_loss.dim() > 0 else Z_loss.item()
-                    logger.print_format_results('val', {'epoch': 0, 'iters': z_iter, 'time': 0, 'model': '',
-                                                        'lr': self.optimizer.param_groups[0]['lr'], 'Z_loss': v},
-                                                dont_print=True)
-            if not self.model_training:
-                self.latest_Z_loss_values = Z_loss.detach().reshape(-1)  # kept on device (no per-iter sync)
-            Z_loss = Z_loss.mean()
-            Z_loss.backward()
-            self.loss_values.append(Z_loss.detach())
-            self.optimizer.step()
+            # one Z iteration with the generator's x3 overflow checks read once at its end (not after the forward
+            # and again after the backward, each a stream drain): from a snapshot of Z and its Adam state the
+            # iteration is redone with the generator in exact fp32 if a flag was set
+            snap = self._snapshot()
+            with TE.deferred_overflow_checks() as chk:
+                Z_loss = self._iteration(z_iter)
+            if chk.overflowed():
+                E.OVERFLOW_RERUNS += 1
+                self._restore(snap)
+                g = self.model.netG.module.generated_image_model if hasattr(self.model.netG, 'module') else None
+                prev = getattr(g, 'esr_precision', None)
+                if g is not None:
+                    g.esr_precision = 'f32'
+                try:
+                    Z_loss = self._iteration(z_iter)
+                finally:
+                    if g is not None:
+                        g.esr_precision = prev
+            self.loss_values.append(Z_loss)
             z_iter += 1
         self.loss_values = [float(v) for v in self.loss_values]
         if not self.model_training:
@@ -253,3 +255,48 @@ class Z_optimizer:
             self.model.feed_data(self.data, need_HR=False)
             self.model.fake_H = self.model.netG(self.model.model_input)
         return Z_2_return
+
+    def _snapshot(self):
+        params = [p.detach().clone() for p in self.Z_model.parameters()]
+        state = {id(p): {k: (v.clone() if torch.is_tensor(v) else v) for k, v in self.optimizer.state[p].items()}
+                 for p in self.Z_model.parameters() if p in self.optimizer.state}
+        return params, state, self.__dict__.get('latest_Z_loss_values')
+
+    def _restore(self, snap):
+        params, state, latest = snap
+        with torch.no_grad():
+            for p, v in zip(self.Z_model.parameters(), params):
+                p.copy_(v)
+                if id(p) in state:
+                    for k, v2 in state[id(p)].items():
+                        if torch.is_tensor(v2):
+                            self.optimizer.state[p][k].copy_(v2)
+                        else:
+                            self.optimizer.state[p][k] = v2
+                else:
+                    self.optimizer.state.pop(p, None)
+        if latest is not None:
+            self.latest_Z_loss_values = latest
+
+    def _iteration(self, z_iter):
+        """Z_optimization.py:574-630: forward with the current Z, the objective, its backward to Z, one Adam step.
+        Returns the (device) mean loss."""
+        self.optimizer.zero_grad()
+        self.data['Z'] = self.Z_model()
+        self.model.feed_data(self.data, need_HR=False)
+        self.model.fake_H = self.model.netG(self.model.model_input)
+        if self.model_training:
+            self.model.fake_H = self.HR_unpadder(self.model.fake_H)
+        Z_loss = self._loss(z_iter)
+        if self.loggers is not None:
+            for n, logger in enumerate(self.loggers):
+                v = Z_loss[n].item() if Z_loss.dim() > 0 else Z_loss.item()
+                logger.print_format_results('val', {'epoch': 0, 'iters': z_iter, 'time': 0, 'model': '',
+                                                    'lr': self.optimizer.param_groups[0]['lr'], 'Z_loss': v},
+                                            dont_print=True)
+        if not self.model_training:
+            self.latest_Z_loss_values = Z_loss.detach().reshape(-1)  # kept on device (no per-iter sync)
+        Z_loss = Z_loss.mean()
+        Z_loss.backward()
+        self.optimizer.step()
+        return Z_loss.detach()
