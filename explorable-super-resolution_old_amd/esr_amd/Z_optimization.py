@@ -5,22 +5,276 @@ back to the model input (train_engine.generator_backward with need_params=False)
 gradient → the Z slots of all LR/HR convs → bilinear ↓4 adjoint → replicate pre-pad adjoint (esr_input_adjoint).  The
 generator is frozen exactly as the reference freezes it (Manage_Model_Grad_Requirements, Z_optimization.py:545-553),
 so no weight gradients are computed.  Z is parametrised as Z_range·tanh(Z_pre) and stepped with Adam
-(Z_optimization.py:292-300, 451).
+(Z_optimization.py:292-300, 512).
 
-Objectives carried over (Z_optimization.py:574-640): 'l1' (to data['HR']), 'max_STD' / 'min_STD' /
-'STD_increase' / 'STD_decrease' (global masked STD), 'TV' (STD-preserving TV), 'Adversarial' (WGAN generator loss on
-netD) and 'random_l1' (batch diversity).  The GUI-editing objectives (scribble, hist / dict, periodicity, local STD,
-desired_SVD, Mag, VGG) are image-editing losses of the GUI, outside this hot path; they raise NotImplementedError.
+Objectives: every image-editing loss the GUI drives (GUI.py:1505-1600 builds the strings from its buttons and shipped
+switches), evaluated on the device on the generator output, with the reference's keyword grammar and precedence
+(Z_optimization.py:361-523 construction, 578-623 evaluation):
+  'l1' (to data['HR']), 'scribble' (masked L1 to the scribbled image with HSV brightening / darkening regions and
+  per-region 8-neighbour TV), '[local_](max|min)_STD', '[local_]STD_(increase|decrease)' (global masked STD, or the
+  STD of every 7×7 patch inside the opened selection), '[local_STD_]TV', 'hist' / 'dict' and their 'patch' forms
+  (SoftHistogramLoss: KL divergence of soft histograms / kernel density over 6×6 patches, or the KDE "dictionary"
+  distance; 'noDC', 'no_localSTD', '…localSTD' STD preservation), '[local_STD_][nonInt_]periodicity[Plus][_1D]'
+  (integer or bilinearly interpolated translations), 'local_Mag_(increase|decrease)', 'Adversarial' (WGAN generator
+  loss on netD) and 'random_l1[_limited]' (batch diversity).
+  'desired_SVD' raises: the reference's FilterLoss reads data['Z'] / data['HR'] that the Z optimiser never passes
+  (loss.py:79,134: KeyError).  'VGG' raises: its feature extractor is unbuildable in the reference (NameError,
+  architecture.py:294-300) and torchvision is absent.  Plain 'l1' with an image mask raises as the reference does
+  (its masked-L1 closure reads a mask defined only for 'scribble', Z_optimization.py:386-397: NameError).
+  auto_set_hist_temperature raises: its temperature search differentiates the histogram loss's input gradient through
+  the generator a second time (Z_optimization.py:479-499, create_graph=True).
 """
 import numpy as np
 import torch
+import torch.nn.functional as F
 
 from . import engine as E
 from . import train_engine as TE
 from .loss import GANLoss
 
-_UNSUPPORTED = ('scribble', 'hist', 'dict', 'periodicity', 'local', 'desired_SVD', 'Mag', 'VGG')
+_UNSUPPORTED = ('desired_SVD', 'VGG')
 
+
+# ----------------------------------------------------------------------------------------------------------------
+# Patch sets over a mask (Z_optimization.py:230-270)
+# ----------------------------------------------------------------------------------------------------------------
+
+def _patch_sets(mask, patch_size, patches_overlap=1.0):
+    """(patches [N, p²] pixel indices, non-covered pixel indices or None) of `mask` (H×W, nonzero = inside).
+
+    Patches are the p×p windows (row-major over their top-left corners, row-major inside) that lie wholly inside the
+    mask after a binary opening by a p×p square.  With patches_overlap < 1 they are thinned greedily in that order:
+    a window is dropped when the fraction of its pixels already claimed exceeds the overlap (any, for overlap 0).  The
+    claim map has one slot per index in [min, max) addressed as index − min − 1 with NumPy's wrap-around, so the
+    smallest and the largest index share the last slot — the reference's bookkeeping, kept so the same windows
+    survive.  Non-covered pixels: the mask's patch pixels no kept window claims (sorted)."""
+    from scipy.ndimage import binary_opening
+    p = int(patch_size)
+    m = binary_opening(np.asarray(mask), np.ones((p, p), dtype=bool))
+    labels = m * (1 + np.arange(m.size).reshape(m.shape))
+    win = np.lib.stride_tricks.sliding_window_view(labels, (p, p)).reshape(-1, p * p)
+    win = win[np.all(win > 0, axis=1)] - 1
+    if not patches_overlap < 1:
+        return win, None
+    if len(win) == 0:
+        raise ValueError('no %dx%d patch fits inside the mask' % (p, p))
+    uniq = np.unique(win)
+    lo = int(uniq[0])
+    taken = np.zeros(int(uniq[-1]) - lo, dtype=bool)
+    keep = np.ones(len(win), dtype=bool)
+    for j in range(len(win)):
+        slots = win[j] - lo - 1
+        seen = taken[slots]
+        if (patches_overlap == 0 and seen.any()) or seen.mean() > patches_overlap:
+            keep[j] = False
+            continue
+        taken[slots] = True
+    print('%.3f of desired pixels are covered by assigned patches' % taken[uniq - lo - 1].mean())
+    return win[keep], uniq[~taken[uniq - lo - 1]]
+
+
+def _selection_matrix(cols, n_cols, device):
+    """Sparse 0/1 matrix whose row r picks pixel cols[r] (the reference's Patch_Indexes_2_Sparse_Mat layout)."""
+    cols = torch.as_tensor(np.asarray(cols).reshape(-1), dtype=torch.long)
+    rows = torch.arange(cols.numel(), dtype=torch.long)
+    return torch.sparse_coo_tensor(torch.stack([rows, cols]), torch.ones(cols.numel()), (cols.numel(), n_cols),
+                                   device=device)
+
+
+def ReturnPatchExtractionMat(mask, patch_size, device, patches_overlap=1, return_non_covered=False):
+    """Z_optimization.py:230-264: sparse [p²·N, H·W] patch extraction matrix (row d·N + j = pixel d of patch j), and
+    with return_non_covered the [n, H·W] selection of the pixels no patch covers (None when patches_overlap >= 1)."""
+    mask = np.asarray(mask)
+    win, non_cov = _patch_sets(mask, patch_size, patches_overlap)
+    mat = _selection_matrix(win.T, mask.size, device)
+    if return_non_covered:
+        return mat, (None if non_cov is None else _selection_matrix(non_cov, mask.size, device))
+    return mat
+
+
+class _Gather:
+    """Device-side form of a patch set: image plane (flattened) -> [p², N] values (a gather instead of sparse mm)."""
+
+    def __init__(self, win, device):
+        self.idx = torch.as_tensor(np.ascontiguousarray(win.T), dtype=torch.long, device=device)
+
+    def __call__(self, plane):
+        return plane.reshape(-1)[self.idx]
+
+    def size(self, dim):  # the GUI prints patch_extraction_mat.size(1) (GUI.py:1623)
+        return self.idx.shape[1] if dim == 1 else self.idx.shape[0]
+
+
+# ----------------------------------------------------------------------------------------------------------------
+# Soft histogram / kernel density (Z_optimization.py:21-228)
+# ----------------------------------------------------------------------------------------------------------------
+
+_KDE_CHUNK = 1 << 24  # elements of one [dims, samples, bins] block
+
+
+def _kde_block(x, bins, period, temperature, sqrt_eps, exp_power):
+    """log-kernel of every (sample, bin) pair: −mean_d (wrapped |x − b| + ε)^power / T.  x [D, n], bins [D, M]."""
+    d = (x.unsqueeze(-1) - bins.unsqueeze(1)).abs()
+    d = torch.minimum(d, (d - period).abs())  # = min(|x − b|, |x − b − max|, |x − b + max|): circular distance
+    return (-((d + sqrt_eps) ** exp_power) / temperature).mean(0)
+
+
+class SoftHistogramLoss(torch.nn.Module):
+    """Z_optimization.py:21-228 with the same constructor: soft (Gaussian-kernel) histograms of gray pixels, or kernel
+    densities over p×p patches (patch_size > 1) or colour pixels, compared by KL divergence to the desired image's, or
+    (dictionary_not_histogram) the mean −log of each sample's mean kernel value over the desired samples.
+
+    Computed in float64 like the reference (its histograms are cast to float32 before the KL divergence), over blocks
+    of at most 2^24 (sample, bin, dim) triples, each recomputed in the backward (torch.utils.checkpoint), so a large
+    selection never materialises the full pairwise tensor."""
+
+    SQRT_EPSILON = 1e-7
+    EXP_POWER = 2
+
+    def __init__(self, bins, min, max, desired_hist_image_mask=None, desired_hist_image=None, gray_scale=True,
+                 input_im_HR_mask=None, patch_size=1, automatic_temperature=False, image_Z=None, temperature=0.05,
+                 dictionary_not_histogram=False, no_patch_DC=False, no_patch_STD=False):
+        super().__init__()
+        if automatic_temperature:
+            raise NotImplementedError('SoftHistogramLoss(automatic_temperature=True): the temperature search '
+                                      'differentiates through the generator twice (not built)')
+        assert no_patch_DC or not no_patch_STD, 'Not supporting removing of only patch STD without DC'
+        dev = input_im_HR_mask.device if torch.is_tensor(input_im_HR_mask) else \
+            torch.device('cuda', torch.cuda.current_device())
+        self.device = dev
+        self.bin_width = (max - min) / (bins - 1)
+        self.max = max
+        self.temperature = torch.tensor(temperature, dtype=torch.float64, device=dev)
+        self.gray_scale = gray_scale
+        self.patch_size = patch_size
+        self.no_patch_DC, self.no_patch_STD = no_patch_DC, no_patch_STD
+        self.dictionary_not_histogram = dictionary_not_histogram
+        self.num_dims = (1 if gray_scale else 3) if patch_size == 1 else patch_size ** 2
+        self.KDE = not gray_scale or patch_size > 1
+        self.bins = torch.linspace(min, max, bins, device=dev, dtype=torch.float64).view(1, -1) if gray_scale else None
+        self.mean_patches_STD = None
+        desired = None
+        if desired_hist_image is not None:
+            if gray_scale:
+                desired_hist_image = [im.to(dev).mean(1, keepdim=True) for im in desired_hist_image]
+            if patch_size > 1:
+                assert gray_scale, 'Not supporting color images or patch histograms for model training loss for now'
+                overlap = (self.num_dims - patch_size) / self.num_dims  # one row / column apart
+                sets = [_Gather(_patch_sets(m, patch_size, overlap)[0], dev) for m in desired_hist_image_mask]
+                desired = torch.cat([g(im.reshape(-1)) for g, im in zip(sets, desired_hist_image)], 1)  # [D, N]
+                desired = self._normalise_patches(desired, from_desired=True)
+            else:
+                if len(desired_hist_image) > 1:
+                    print('Not supproting multiple hist image versions for non-patch histogram/dictionary. '
+                          'Removing extra image versions.')
+                # (the desired mask is not applied to a pixel histogram's desired image: Z_optimization.py:72-74,92)
+                desired = desired_hist_image[0].reshape(self.num_dims, -1)
+                if self.KDE and desired_hist_image_mask is not None:
+                    keep = torch.as_tensor(np.asarray(desired_hist_image_mask[0]).reshape(-1) != 0, device=dev)
+                    desired = desired[:, keep]
+            if self.KDE:  # (pruned in the desired image's precision, then float64, as :116-129)
+                self.bins = self._prune_bins(desired).double()
+        elif self.KDE:
+            raise ValueError('SoftHistogramLoss: a patch / colour density needs the desired image')
+        if patch_size > 1:
+            self.patch_extraction_mat = _Gather(_patch_sets(np.asarray(
+                input_im_HR_mask.detach().cpu().numpy() if torch.is_tensor(input_im_HR_mask) else input_im_HR_mask),
+                patch_size, 0.5)[0], dev)
+            self.image_mask = None
+        else:
+            self.image_mask = None if input_im_HR_mask is None else \
+                (input_im_HR_mask.reshape(-1) != 0) if torch.is_tensor(input_im_HR_mask) else \
+                torch.as_tensor(np.asarray(input_im_HR_mask).reshape(-1) != 0, device=dev)
+        self.normalizer = None
+        if not dictionary_not_histogram and desired is not None:
+            with torch.no_grad():
+                self.desired_hists_list = [self._histogram(desired.double(), log=False, set_normalizer=True)]
+
+    def _normalise_patches(self, patches, from_desired=False):
+        """Patch DC (and STD) removal, Z_optimization.py:61-67 (desired) and 177-180 (current)."""
+        if not self.no_patch_DC:
+            return patches
+        patches = patches - patches.mean(0, keepdim=True)
+        if self.no_patch_STD:
+            floor = torch.tensor(1 / 255, device=patches.device, dtype=patches.dtype)
+            std = torch.maximum(patches.std(0, keepdim=True), floor)
+            if from_desired:
+                self.mean_patches_STD = float(std.mean())
+            patches = patches / std * self.mean_patches_STD
+        return patches
+
+    def _prune_bins(self, samples):
+        """Desired samples -> KDE bins, dropping every sample that a LATER sample matches within half a bin width in
+        all dims (Z_optimization.py:106-130, at num_sub_images = 1).  [D, n] -> [D, M] float64."""
+        D, n = samples.shape
+        keep = torch.ones(n, dtype=torch.bool, device=samples.device)
+        rows = max(1, _KDE_CHUNK // max(1, D * n))
+        for i0 in range(0, n, rows):
+            i1 = min(n, i0 + rows)
+            close = ((samples[:, i0:i1, None] - samples[:, None, :]).abs() < self.bin_width / 2).all(0)  # [r, n]
+            later = torch.arange(n, device=samples.device)[None, :] > torch.arange(i0, i1, device=samples.device)[:, None]
+            keep[i0:i1] = ~(close & later).any(1)
+        return samples[:, keep]
+
+    def _log_kernels(self, x, temperature):
+        """[n, M] log-kernel matrix of samples x [D, n] against the bins, in blocks recomputed in the backward."""
+        M = self.bins.shape[1]
+        cols = max(1, _KDE_CHUNK // max(1, x.shape[0] * M))
+        args = (self.bins, float(self.max), temperature, self.SQRT_EPSILON, self.EXP_POWER)
+        if x.shape[1] <= cols or not torch.is_grad_enabled():
+            return torch.cat([_kde_block(x[:, j:j + cols], *args) for j in range(0, x.shape[1], cols)], 0)
+        from torch.utils.checkpoint import checkpoint
+        return torch.cat([checkpoint(_kde_block, x[:, j:j + cols], *args, use_reentrant=False)
+                          for j in range(0, x.shape[1], cols)], 0)
+
+    def _histogram(self, x, log, set_normalizer, temperature=None):
+        """ComputeSoftHistogram (Z_optimization.py:168-207) of samples x [D, n] float64: [1, bins (+1)] float32, or the
+        dictionary distances [1, n] float64."""
+        t = self.temperature if temperature is None else temperature
+        h = self._log_kernels(x, t)
+        if self.dictionary_not_histogram:
+            return (-torch.log(torch.exp(h).mean(1))).view(1, -1)
+        hist = torch.exp(h).mean(0)
+        if set_normalizer or not self.KDE:
+            self.normalizer = hist.sum() / x.shape[1]
+        hist = (hist / self.normalizer / x.shape[1]).float()
+        if self.KDE:  # one more bin for all the mass the desired bins do not cover
+            hist = torch.cat([hist, (1 - torch.clamp(hist.sum(), max=1.0)).view(1)])
+        if log:
+            return torch.log(hist + torch.finfo(hist.dtype).eps).view(1, -1)
+        return hist.view(1, -1)
+
+    def _samples(self, image):
+        """One image [C, H, W] -> samples [D, n] float64 (gray or colour pixels inside the mask, or patches)."""
+        if self.gray_scale:
+            image = image.mean(0, keepdim=True)
+        if self.patch_size > 1:
+            return self._normalise_patches(self.patch_extraction_mat(image)).double()
+        x = image.reshape(self.num_dims, -1)
+        if self.image_mask is not None:
+            x = x[:, self.image_mask]
+        return x.double()
+
+    def Feed_Desired_Hist_Im(self, desired_hist_image):
+        """Z_optimization.py:97-104: new desired images (whole images: no mask is applied here)."""
+        self.desired_hists_list = []
+        for im in desired_hist_image:
+            x = im.mean(0, keepdim=True).reshape(1, -1) if self.gray_scale else im.reshape(self.num_dims, -1)
+            with torch.no_grad():
+                self.desired_hists_list.append(self._histogram(x.double(), log=False, set_normalizer=True))
+
+    def forward(self, cur_images):
+        per_image = torch.cat([self._histogram(self._samples(im), log=True, set_normalizer=False)
+                               for im in cur_images], 0)
+        if self.dictionary_not_histogram:
+            return per_image.mean(1).float()
+        target = torch.cat(self.desired_hists_list, 0)
+        return F.kl_div(per_image, target, reduction='mean').float()
+
+
+# ----------------------------------------------------------------------------------------------------------------
+# Z parametrisation (Z_optimization.py:272-324)
+# ----------------------------------------------------------------------------------------------------------------
 
 class Optimizable_Z(torch.nn.Module):
     """Z_optimization.py:271-308: Z = Z_range·tanh(Z_pre) (identity without Z_range), optional Z mask that keeps the
@@ -31,8 +285,9 @@ class Optimizable_Z(torch.nn.Module):
         super().__init__()
         device = device if device is not None else torch.device('cuda', torch.cuda.current_device())
         self.Z = torch.nn.Parameter(torch.zeros(Z_shape, dtype=torch.float32, device=device))
-        if Z_mask is not None and not np.all(Z_mask):
-            self.mask = torch.as_tensor(np.asarray(Z_mask), dtype=torch.float32, device=device)
+        if Z_mask is not None and not np.all(np.asarray(Z_mask.cpu() if torch.is_tensor(Z_mask) else Z_mask)):
+            self.mask = torch.as_tensor(np.asarray(Z_mask.cpu() if torch.is_tensor(Z_mask) else Z_mask),
+                                        dtype=torch.float32, device=device)
             self.initial_pre_tanh_Z = 1 * initial_pre_tanh_Z.float().to(device)
         else:
             self.mask = None
@@ -40,7 +295,7 @@ class Optimizable_Z(torch.nn.Module):
             assert tuple(initial_pre_tanh_Z.shape[1:]) == tuple(self.Z.shape[1:]) and \
                 initial_pre_tanh_Z.size(0) in (1, self.Z.size(0)), 'Initilizer size does not match desired Z size'
             init = initial_pre_tanh_Z.float().to(device)
-            if random_perturbations:
+            if random_perturbations:  # (the mask's fill value above keeps the unperturbed initializer, as :279,285)
                 init = init + 0.001 * torch.randn_like(init)
             self.Z.data[:init.size(0)] = init
         self.Z_range = Z_range
@@ -81,22 +336,78 @@ def TV_Loss(image):
         (image[:, :, :-1, :] - image[:, :, 1:, :]).abs().mean(dim=(1, 2, 3))
 
 
+def IndexingHelper(index, negative=False):
+    """Slice bound of a shift: positive shifts start at `index`, negative ones end there (Z_optimization.py:684)."""
+    if negative:
+        return index if index < 0 else None
+    return index if index > 0 else None
+
+
+def _shifted(image, shift):
+    """image[..., y0:y1, x0:x1] for an integer (dy, dx) shift (Return_Translated_SubImage)."""
+    dy, dx = shift
+    return image[:, :, IndexingHelper(dy):IndexingHelper(dy, True), IndexingHelper(dx):IndexingHelper(dx, True)]
+
+
+def _rgb2hsv(rgb):
+    """scikit-image's rgb2hsv (HWC float; V = max, S = (max − min) / max, H from the sector of the max channel)."""
+    arr = np.asarray(rgb, dtype=np.float64)
+    v = arr.max(-1)
+    delta = v - arr.min(-1)
+    h = np.zeros_like(v)
+    with np.errstate(invalid='ignore', divide='ignore'):
+        s = np.where(delta == 0, 0.0, delta / v)
+        for c, a, b, off in ((0, 1, 2, 0.0), (1, 2, 0, 2.0), (2, 0, 1, 4.0)):  # later channels win ties, as there
+            sel = arr[..., c] == v
+            h[sel] = off + (arr[..., a][sel] - arr[..., b][sel]) / delta[sel]
+        h = (h / 6.0) % 1.0
+    h[delta == 0] = 0.0
+    return np.stack([h, s, v], -1)
+
+
+def _hsv2rgb(hsv):
+    """scikit-image's hsv2rgb (the six hue sectors)."""
+    arr = np.asarray(hsv, dtype=np.float64)
+    h6 = arr[..., 0] * 6
+    sector = np.floor(h6)
+    f = h6 - sector
+    s, v = arr[..., 1], arr[..., 2]
+    p, q, t = v * (1 - s), v * (1 - f * s), v * (1 - (1 - f) * s)
+    table = np.stack([np.stack(c, -1) for c in ((v, t, p), (q, v, p), (p, v, t), (p, q, v), (t, p, v), (v, p, q))])
+    k = np.repeat((sector.astype(np.uint8) % 6)[..., None], 3, -1)
+    return np.take_along_axis(table, k[None], 0)[0]
+
+
+# ----------------------------------------------------------------------------------------------------------------
+# The optimiser (Z_optimization.py:326-682)
+# ----------------------------------------------------------------------------------------------------------------
+
 class Z_optimizer:
-    """Z_optimization.py:326-660 (same constructor arguments; see the module docstring for the objectives)."""
+    """Z_optimization.py:326-682 (same constructor arguments and attributes; objectives in the module docstring)."""
     MIN_LR = 1e-5
+    PATCH_SIZE_4_STD = 7
+    PLUS_MEANS_STD_INCREASE = True
 
     def __init__(self, objective, Z_size, model, Z_range, max_iters, data=None, loggers=None, image_mask=None,
                  Z_mask=None, initial_Z=None, initial_LR=None, existing_optimizer=None, batch_size=1,
                  HR_unpadder=None, auto_set_hist_temperature=False, random_Z_inits=False):
         bad = [t for t in _UNSUPPORTED if t in objective]
-        if bad or (image_mask is not None and 'l1' in objective):
-            raise NotImplementedError('Z objective %r uses GUI image-editing losses (%s) outside the built path'
-                                      % (objective, ', '.join(bad) or 'masked l1 = scribble loss'))
+        if bad:
+            raise NotImplementedError('Z objective %r: %s is broken in the reference (see esr_amd.Z_optimization)'
+                                      % (objective, bad[0]))
+        masked_l1 = image_mask is not None and 'l1' in objective and 'random' not in objective and \
+            'scribble' not in objective
+        if masked_l1:
+            raise NotImplementedError('Z objective %r with an image mask: the reference\'s masked L1 reads a mask it '
+                                      'only defines for "scribble" (NameError)' % objective)
+        if auto_set_hist_temperature and ('hist' in objective or 'dict' in objective):
+            raise NotImplementedError('auto_set_hist_temperature: not built (second-order through the generator)')
         self.device = model.device
-        if initial_Z is not None or hasattr(model, 'model_input'):
+        dev = self.device
+        if initial_Z is not None or 'cur_Z' in model.__dict__ or hasattr(model, 'model_input'):
             if initial_Z is None:
                 initial_Z = 1 * model.GetLatent()
-            pre = initial_Z / Z_range
+            pre = initial_Z.to(dev) / Z_range
             eps = torch.finfo(pre.dtype).eps
             initial_pre_tanh_Z = ArcTanH(torch.clamp(pre, min=-1 + eps, max=1. - eps))
         else:
@@ -104,48 +415,38 @@ class Z_optimizer:
         self.Z_model = Optimizable_Z([batch_size, model.num_latent_channels] + list(Z_size), Z_range=Z_range,
                                      initial_pre_tanh_Z=initial_pre_tanh_Z, Z_mask=Z_mask,
                                      random_perturbations=(random_Z_inits and 'random' not in objective) or
-                                     ('random' in objective and 'limited' in objective), device=self.device)
+                                     ('random' in objective and 'limited' in objective), device=dev)
         assert initial_LR is not None or existing_optimizer is not None, \
             'Should either supply optimizer from previous iterations or initial LR for new optimizer'
-        self.objective = objective
+        self.objective = o = objective
         self.data = data
         self.model = model
         self.model_training = HR_unpadder is not None
+        fake = getattr(model, 'fake_H', None)
         if image_mask is None:
-            self.image_mask = torch.ones(list(model.fake_H.shape[2:]), device=self.device) \
-                if getattr(model, 'fake_H', None) is not None else None
+            self.image_mask = torch.ones(list(fake.shape[2:]), device=dev, dtype=fake.dtype) \
+                if fake is not None else None
             self.Z_mask = None
         else:
-            self.image_mask = torch.as_tensor(np.asarray(image_mask), dtype=torch.float32, device=self.device)
-            self.Z_mask = torch.as_tensor(np.asarray(Z_mask), dtype=torch.float32, device=self.device)
-        if not self.model_training and self.image_mask is not None:
+            assert Z_mask is not None, 'Should either supply both masks or niether'
+            self.image_mask = torch.as_tensor(np.asarray(image_mask), device=dev).to(fake.dtype)
+            self.Z_mask = torch.as_tensor(np.asarray(Z_mask), device=dev).to(fake.dtype)
+            self.initial_Z = 1. * model.GetLatent()
+        self._local_sets = None
+        if 'local' in o:  # patch sets for the local STD / magnitude (Z_optimization.py:361-364)
+            win, non_cov = _patch_sets(np.asarray(image_mask), self.PATCH_SIZE_4_STD, 1 if 'STD' in o else 0.5)
+            self._local_sets = (_Gather(win, dev), None if non_cov is None else
+                                torch.as_tensor(non_cov, dtype=torch.long, device=dev))
+        if not self.model_training:
             self.initial_STD = self.Masked_STD(first_image_only=True)
+            print('Initial STD: %.3e' % self.initial_STD.mean().item())
         if existing_optimizer is None:
-            if 'l1' in objective and 'random' not in objective:
-                if data is not None and 'HR' in data:
-                    self.GT_HR = data['HR']
-                self.loss = torch.nn.L1Loss()
-            elif 'STD' in objective and 'TV' not in objective:
-                assert objective in ['max_STD', 'min_STD', 'STD_increase', 'STD_decrease']
-                if 'increase' in objective or 'decrease' in objective:
-                    inc = data.get('STD_increment') if data is not None else None
-                    self.desired_STD = self.initial_STD
-                    if inc is None:
-                        self.desired_STD = self.desired_STD * (1.05 if 'increase' in objective else 1 / 1.05)
-                    else:
-                        self.desired_STD = self.desired_STD + (inc if 'increase' in objective else -inc)
-            elif 'TV' in objective:
-                self.STD_PRESERVING_WEIGHT = 100
-            elif 'Adversarial' in objective:
-                self.netD = model.netD
-                self.loss = GANLoss('wgan-gp', 1.0, 0.0)
-            elif 'limited' in objective:
-                self.initial_image = 1 * model.fake_H.detach()
-                self.rmse_weight = data['rmse_weight']
+            self._build_objective(data, auto_set_hist_temperature)
             self.optimizer = torch.optim.Adam(self.Z_model.parameters(), lr=initial_LR)
         else:
             self.optimizer = existing_optimizer
         self.LR = initial_LR
+        self.scheduler = None
         self.loggers = loggers
         self.cur_iter = 0
         self.max_iters = max_iters
@@ -153,26 +454,178 @@ class Z_optimizer:
             'allButFirst' if (initial_pre_tanh_Z is not None and initial_pre_tanh_Z.size(0) < batch_size) else False
         self.HR_unpadder = HR_unpadder
 
+    # -- construction of each objective's state, in the reference's precedence (Z_optimization.py:370-511) ------------
+    def _build_objective(self, data, auto_temperature):
+        o, dev = self.objective, self.device
+        if any(w in o for w in ('l1', 'scribble')) and 'random' not in o:
+            if data is not None and 'HR' in data:
+                self.GT_HR = data['HR']
+            if self.image_mask is None:
+                self.loss = torch.nn.L1Loss()
+            else:
+                self._build_scribble(data)
+        elif 'Mag' in o:
+            # the 7×7 patches of the current (gray) image with their STD moved by ±STD_increment (:419-422)
+            patches = self._local_sets[0](self.model.fake_H.mean(dim=1))
+            mean = patches.mean(0, keepdim=True)
+            std = torch.maximum(patches.std(0, keepdim=True), torch.tensor(1 / 255, device=dev))
+            step = data['STD_increment'] * (1 if 'increase' in o else -1)
+            self.desired_patches = (patches - mean) / std * (std + step) + mean
+        elif 'STD' in o and not any(w in o for w in ('periodicity', 'TV', 'dict', 'hist')):
+            assert o.replace('local_', '') in ['max_STD', 'min_STD', 'STD_increase', 'STD_decrease']
+            if 'increase' in o or 'decrease' in o:
+                inc = data['STD_increment']
+                if inc is None:  # multiplicative
+                    self.desired_STD = self.initial_STD * (1.05 if 'increase' in o else 1 / 1.05)
+                else:
+                    self.desired_STD = self.initial_STD + (inc if 'increase' in o else -inc)
+        elif 'periodicity' in o:
+            self.STD_PRESERVING_WEIGHT = 20
+            if 'nonInt' in o:
+                if 'Plus' in o and self.PLUS_MEANS_STD_INCREASE:
+                    self.desired_STD = self.initial_STD + data['STD_increment']
+                self.periodicity_points, self.half_period_points = self._sampling_grids(data['periodicity_points'])
+            else:
+                self.periodicity_points = [np.array(p) for p in data['periodicity_points']]
+        elif 'TV' in o:
+            self.STD_PRESERVING_WEIGHT = 100
+        elif 'hist' in o or 'dict' in o:
+            self.automatic_temperature = auto_temperature
+            self.STD_PRESERVING_WEIGHT = 1e4
+            self.loss = SoftHistogramLoss(
+                bins=256, min=0, max=1, desired_hist_image=data['HR'] if data is not None else None,
+                desired_hist_image_mask=data['Desired_Im_Mask'] if data is not None else None,
+                input_im_HR_mask=self.image_mask, gray_scale=True, patch_size=6 if 'patch' in o else 1,
+                temperature=5e-4 if 'hist' in o else 1e-3, dictionary_not_histogram='dict' in o,
+                no_patch_DC='noDC' in o, no_patch_STD='no_localSTD' in o)
+        elif 'Adversarial' in o:
+            self.netD = self.model.netD
+            self.loss = GANLoss('wgan-gp', 1.0, 0.0)
+        elif 'limited' in o:
+            self.initial_image = 1 * self.model.fake_H.detach()
+            self.rmse_weight = data['rmse_weight']
+
+    def _build_scribble(self, data):
+        """Masked L1 to the scribbled image + per-region TV (Z_optimization.py:376-416).  Scribble ids: 1 = match,
+        2 / 3 = match a brightened / darkened copy of the current image (HSV value × (1 ± brightness_factor), box-
+        smoothed by one pixel), > 3 = one 8-neighbour TV region per id."""
+        from scipy.signal import convolve2d
+        dev, mask = self.device, self.image_mask
+        if 'scribble' not in self.objective:
+            raise NotImplementedError('masked L1 without a scribble mask')
+        sm_np = np.asarray(data['scribble_mask'])
+        sm = torch.as_tensor(sm_np, device=dev).to(mask.dtype)
+        mult = np.ones(sm_np.shape, dtype=np.float32)
+        mult += data['brightness_factor'] * (sm_np == 2) - data['brightness_factor'] * (sm_np == 3)  # (float32)
+        mult = convolve2d(np.pad(mult, 1, mode='edge'), np.ones((3, 3)) / 9, mode='valid')
+        self._l1_mask = mask * ((sm > 0) & (sm < 4)).to(mask.dtype)
+        self._tv_masks = [(mask * (sm == v).to(mask.dtype))[None, None] for v in torch.unique(sm * mask) if v > 3]
+        cur = self.model.fake_H[0].detach().cpu().numpy().transpose(1, 2, 0)
+        hsv = _rgb2hsv(np.clip(255 * cur, 0, 255))
+        hsv[:, :, 2] = hsv[:, :, 2] * mult
+        desired = torch.as_tensor(_hsv2rgb(hsv).transpose(2, 0, 1)[None] / 255, device=dev).to(mask.dtype)
+        region = ((sm == 2) | (sm == 3)).to(mask.dtype)
+        self.GT_HR = self.GT_HR.to(dev) * (1 - region) + region * desired
+        self.loss = self._scribble_loss
+
+    def _scribble_loss(self, produced, target):
+        m = self._l1_mask
+        per = []
+        for i in range(produced.size(0)):
+            v = F.l1_loss(produced[i:i + 1] * m, target * m)
+            if self._tv_masks:
+                v = v + self._region_tv(produced[i:i + 1])
+            per.append(v)
+        return torch.stack(per, 0)
+
+    def _region_tv(self, im):
+        loss = 0
+        for tvm in self._tv_masks:
+            for shift in ((-1, -1), (-1, 0), (0, -1), (1, -1)):  # 4 of the 8 neighbours: each difference once
+                neg = (-shift[0], -shift[1])
+                pair = _shifted(tvm, shift) * _shifted(tvm, neg)
+                loss = loss + (pair * (_shifted(im, shift) - _shifted(im, neg)).abs()).mean(dim=(1, 2, 3))
+        return loss
+
+    def _sampling_grids(self, points):
+        """grid_sample grids of the ±point translations (Z_optimization.py:440-468).  The first grid axis pairs the x
+        range with the image's first size (H) and vice versa, as in the reference (identical for square images)."""
+        size = list(self.model.fake_H.shape[2:])
+        fake = self.model.fake_H
+        full, half = [], []
+        rounds = 1 + int('Plus' in self.objective and not self.PLUS_MEANS_STD_INCREASE)
+        for point in points:
+            point = np.array(point)
+            full.append([])
+            half.append([])
+            for half_round in range(rounds):
+                for minus in range(2):
+                    cur = point * (0.5 if half_round else 1.0) * (-1 if minus else 1)
+                    ranges = []
+                    for axis, comp in enumerate((cur[1], cur[0])):
+                        start = IndexingHelper(comp)
+                        stop = IndexingHelper(comp, negative=True)
+                        lo_hi = [start if start is not None else 0,
+                                 size[axis] + stop if stop is not None else size[axis]]
+                        n = size[axis] - np.ceil(np.abs(np.array([0, size[axis]]) - lo_hi)).astype(np.int16).max()
+                        ranges.append(np.linspace(lo_hi[0], lo_hi[1], num=n) / size[axis] * 2 - 1)
+                    grid = np.meshgrid(*ranges)
+                    g = torch.from_numpy(np.stack(grid, -1)).view([1] + list(grid[0].shape) + [2]).to(
+                        device=fake.device, dtype=fake.dtype)
+                    (half if half_round else full)[-1].append(g)
+        return full, half
+
+    # -- evaluation -----------------------------------------------------------------------------------------------
     def Masked_STD(self, first_image_only=False):
         fake = self.model.fake_H[:1] if first_image_only else self.model.fake_H
-        return torch.std(fake * self.image_mask, dim=(1, 2, 3)).view(1, -1)
+        if self._local_sets is None:
+            return torch.std(fake * self.image_mask, dim=(1, 2, 3)).view(1, -1)
+        gather, non_cov = self._local_sets
+        cols = []
+        for im in fake:
+            g = im.mean(dim=0).reshape(-1)
+            v = gather(g).std(dim=0)
+            if non_cov is not None:
+                v = torch.cat([v, g[non_cov].std(dim=0).view(1)], 0)
+            cols.append(v)
+        return torch.stack(cols, 1)
 
-    def feed_data(self, data):
-        self.data = data
-        self.cur_iter = 0
-        if 'l1' in self.objective:
-            self.GT_HR = data['HR'].to(self.device)
+    def _std_term(self, weight, target):
+        return (weight * (self.Masked_STD(first_image_only=False) - target) ** 2)
 
-    def Manage_Model_Grad_Requirements(self, disable):
-        if disable:
-            self.original_requires_grad_status = [p.requires_grad for p in self.model.netG.parameters()]
-            for p in self.model.netG.parameters():
-                p.requires_grad = False
-        else:
-            for p, s in zip(self.model.netG.parameters(), self.original_requires_grad_status):
-                p.requires_grad = s
+    def PeriodicityLoss(self):
+        plus = 'Plus' in self.objective and self.PLUS_MEANS_STD_INCREASE
+        loss = 0 if plus else self._std_term(self.STD_PRESERVING_WEIGHT, self.initial_STD).mean()
+        image = self.model.fake_H
+        mask = self.image_mask[None, None]
+        for k, point in enumerate(self.periodicity_points):
+            if 'nonInt' in self.objective:
+                a, b = point[0], point[1]
+                pair = self._resample(mask, a) * self._resample(mask, b)
+                loss = loss + (pair * (self._resample(image, a) - self._resample(image, b)).abs()).mean(dim=(1, 2, 3))
+                if 'Plus' in self.objective and not self.PLUS_MEANS_STD_INCREASE:
+                    ha, hb = self.half_period_points[k]
+                    pair = self._resample(mask, ha) * self._resample(mask, hb)
+                    loss = loss - (pair * (self._resample(image, ha) - self._resample(image, hb)).abs()).mean(
+                        dim=(1, 2, 3))
+            else:
+                neg = -point
+                pair = _shifted(mask, point) * _shifted(mask, neg)
+                loss = loss + (pair * (_shifted(image, point) - _shifted(image, neg)).abs()).mean(dim=(1, 2, 3))
+        return loss
+
+    @staticmethod
+    def _resample(image, grid):
+        return F.grid_sample(image, grid.repeat([image.size(0), 1, 1, 1]), align_corners=False)
+
+    def Return_Translated_SubImage(self, image, translation):
+        return _shifted(image, translation)
+
+    def Return_Interpolated_SubImage(self, image, grid):
+        return self._resample(image, grid)
 
     def _loss(self, z_iter):
+        """The objective of the current fake_H, per image where the reference's is (Z_optimization.py:578-623)."""
         fake = self.model.fake_H
         o = self.objective
         if 'random' in o:
@@ -183,23 +636,52 @@ class Z_optimizer:
             if self.Z_mask is not None:
                 Z_loss = Z_loss * self.Z_mask
             Z_loss = -1 * Z_loss.mean(dim=(1, 2, 3))
-        elif 'l1' in o:
-            Z_loss = self.loss(fake, self.GT_HR.to(self.device))
+        elif 'l1' in o or 'scribble' in o:
+            Z_loss = self.loss(fake, self.GT_HR.to(fake.device))
+        elif 'hist' in o or 'dict' in o:
+            Z_loss = self.loss(fake)
+            if 'localSTD' in o:  # (also for 'no_localSTD', as in the reference)
+                Z_loss = Z_loss + self._std_term(self.STD_PRESERVING_WEIGHT, self.initial_STD).mean(0)
         elif 'Adversarial' in o:
             Z_loss = self.loss(self.netD(self.model.CEM_net.HR_unpadder(fake)), True)
-        elif 'STD' in o and 'TV' not in o:
+        elif 'STD' in o and not any(w in o for w in ('periodicity', 'TV')):
             Z_loss = self.Masked_STD(first_image_only=False)
             if 'increase' in o or 'decrease' in o:
                 Z_loss = (Z_loss - self.desired_STD) ** 2
             Z_loss = Z_loss.mean(0)
+        elif 'Mag' in o:
+            gather = self._local_sets[0]
+            Z_loss = torch.stack([((gather(im.mean(dim=0)) - self.desired_patches) ** 2).mean() for im in fake], 0)
+        elif 'periodicity' in o:
+            Z_loss = self.PeriodicityLoss()
+            if 'Plus' in o and self.PLUS_MEANS_STD_INCREASE:
+                Z_loss = Z_loss + (self.STD_PRESERVING_WEIGHT * (self.Masked_STD(first_image_only=False) -
+                                                                 self.desired_STD) ** 2).mean()
         elif 'TV' in o:
-            Z_loss = (self.STD_PRESERVING_WEIGHT * (self.Masked_STD(first_image_only=False) - self.initial_STD) ** 2
-                      ).mean(0) + TV_Loss(fake * self.image_mask)
+            Z_loss = self._std_term(self.STD_PRESERVING_WEIGHT, self.initial_STD).mean(0) + \
+                TV_Loss(fake * self.image_mask)
         else:
             raise NotImplementedError(o)
         if 'max' in o:
             Z_loss = -1 * Z_loss
         return Z_loss
+
+    def feed_data(self, data):
+        self.data = data
+        self.cur_iter = 0
+        if 'l1' in self.objective:
+            self.GT_HR = data['HR'].to(self.device)
+        elif 'hist' in self.objective:
+            self.loss.Feed_Desired_Hist_Im(data['HR'].to(self.device))
+
+    def Manage_Model_Grad_Requirements(self, disable):
+        if disable:
+            self.original_requires_grad_status = [p.requires_grad for p in self.model.netG.parameters()]
+            for p in self.model.netG.parameters():
+                p.requires_grad = False
+        else:
+            for p, s in zip(self.model.netG.parameters(), self.original_requires_grad_status):
+                p.requires_grad = s
 
     def optimize(self):
         """Z_optimization.py:555-655."""
@@ -247,6 +729,8 @@ class Z_optimizer:
             self.model.netG.train(False)
         if 'random' in self.objective and 'limited' in self.objective and len(self.loss_values) > 1:
             self.loss_values[0] = self.loss_values[1]
+        if not self.model_training:
+            print('Final STDs: ', ['%.3e' % v for v in self.Masked_STD(first_image_only=False).mean(0).tolist()])
         self.cur_iter = z_iter + 1
         Z_2_return = self.Z_model.Return_Detached_Z()
         self.Manage_Model_Grad_Requirements(disable=False)
@@ -279,7 +763,7 @@ class Z_optimizer:
             self.latest_Z_loss_values = latest
 
     def _iteration(self, z_iter):
-        """Z_optimization.py:574-630: forward with the current Z, the objective, its backward to Z, one Adam step.
+        """Z_optimization.py:572-635: forward with the current Z, the objective, its backward to Z, one Adam step.
         Returns the (device) mean loss."""
         self.optimizer.zero_grad()
         self.data['Z'] = self.Z_model()
@@ -295,8 +779,12 @@ class Z_optimizer:
                                                     'lr': self.optimizer.param_groups[0]['lr'], 'Z_loss': v},
                                             dont_print=True)
         if not self.model_training:
-            self.latest_Z_loss_values = Z_loss.detach().reshape(-1)  # kept on device (no per-iter sync)
+            # kept on device (no per-iteration sync); a whole-batch scalar (the KL histogram loss) as one value
+            self.latest_Z_loss_values = Z_loss.detach().reshape(-1)
         Z_loss = Z_loss.mean()
         Z_loss.backward()
         self.optimizer.step()
         return Z_loss.detach()
+
+    def ReturnStatus(self):
+        return self.Z_model.PreTanhZ(), self.optimizer

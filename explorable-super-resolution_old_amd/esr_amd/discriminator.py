@@ -7,8 +7,10 @@ this one — `define_D` here builds it (SURVEY.md §7 "training path is broken a
 same state_dict keys and order as the reference (tests/golden/disc_*.npz).
 
 Every convolution (3×3 s1, 4×4 s2, the 8×8 "pseudo-FC" and the 1×1 head) is a HipConv2d: forward, data gradient
-and weight gradient on the exact-fp32 MFMA gather-GEMM kernels of csrc/esr_dconv.hip, differentiable to any order, so
-the D step and the WGAN-GP double backward (loss.py:244-263) run every convolution on HIP.  BatchNorm and LeakyReLU
+and weight gradient on the MFMA kernels of csrc/esr_dconv.hip, differentiable to any order, so the D step and the
+WGAN-GP double backward (loss.py:244-263) run every convolution on HIP.  Their precision is the process-wide
+esr_amd.dconv.PRECISION (default 'x3': split-f16 operands with per-K-step power-of-two scaling on f16 MFMA; 'x6' and
+exact 'f32' via dconv.set_precision or ESR_DCONV_PRECISION).  BatchNorm and LeakyReLU
 run fused on HIP in training mode (esr_amd/bn.py: forward, backward, double backward); in eval mode they are
 PyTorch ops on the channels-last activations the convolutions produce.
 """

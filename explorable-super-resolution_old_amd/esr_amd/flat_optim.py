@@ -81,6 +81,12 @@ class FlatAdam(torch.optim.Adam):
 
     @torch.no_grad()
     def step(self, closure=None):
+        # a .grad set to None from outside (module.zero_grad(set_to_none=True)) and not refilled by a backward: torch's
+        # Adam would skip that parameter, a flat update would move it by its moments with a zero gradient
+        missing = [i for i, p in enumerate(self.flat_params) if p.grad is None]
+        if missing:
+            raise RuntimeError('FlatAdam.step: parameters %s have no gradient (torch.optim.Adam would skip them); '
+                               'run their backward or use a per-tensor optimiser' % missing[:8])
         self._sync_views()
         frozen = [i for i, p in enumerate(self.flat_params) if not p.requires_grad]
         if frozen:

@@ -97,3 +97,17 @@ def test_flat_adam_refuses_a_frozen_parameter():
         opt.step()
     ps[1].requires_grad_(True)
     opt.step()
+
+
+def test_flat_adam_refuses_a_missing_gradient():
+    """A gradient set to None (module.zero_grad(set_to_none=True)) and not refilled: torch's Adam would skip the
+    parameter, so FlatAdam raises instead of moving it with a zero gradient; after a backward it steps again."""
+    import pytest
+    ps = _params(3)
+    opt = FlatAdam(ps, lr=1e-3)
+    opt.zero_grad()
+    ps[2].grad = None
+    with pytest.raises(RuntimeError, match='no gradient'):
+        opt.step()
+    sum((p * p).sum() for p in ps).backward()
+    opt.step()

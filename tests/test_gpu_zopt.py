@@ -82,7 +82,7 @@ def test_z_optimizer_overflow_redo_equals_fp32_loop(gpu_device):
         params = seeded_params([(k, tuple(v.shape)) for k, v in sd.items()], 71, w_scale=0.5)
         model.netG.module.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=False)
         engine.set_precision(model.netG, prec)
-        data = {'LR': torch.from_numpy(lr * 3e4).to(gpu_device), 'Z': torch.from_numpy(0.9 * z0).to(gpu_device)}
+        data = {'LR': torch.from_numpy(lr * 3e5).to(gpu_device), 'Z': torch.from_numpy(0.9 * z0).to(gpu_device)}
         model.feed_data(data, need_HR=False)
         model.test()
         model.netG.eval()
