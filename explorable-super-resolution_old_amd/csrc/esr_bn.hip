@@ -15,7 +15,9 @@
 //   g_x  = r·(G_x̂ − mean(G_x̂) − x̂·mean(G_x̂·x̂)) − G_r·r²·x̂/N,  with
 //          mean(G_x̂) = −(γr/N)(s2·U + A·s1)/N + gg_γ·s1/N,  mean(G_x̂·x̂) = −2(γr/N)·s2·A/N + gg_γ·s2/N.
 // Every pass is either a per-channel column reduction (block partials summed in a fixed order: deterministic) or one
-// elementwise pass; z and the mask are recomputed from (x, μ, r, γ, β) by the same expression everywhere.
+// elementwise pass; z and the mask are recomputed from (x, μ, r, γ, β) by the same expression everywhere.  The column
+// sums accumulate in float64 (per-thread, block and final), as PyTorch's own BatchNorm does on the CPU (acc_type<float>
+// = double): the mean-removal terms then cancel to float64 rounding, not to that of float32 running sums.
 #include <hip/hip_runtime.h>
 #include "esr_amd.h"
 
@@ -41,11 +43,11 @@ __device__ __forceinline__ float mask_of(const BnP &p, float xh, int c) {
     return z > 0.f ? 1.f : p.slope;
 }
 
-// Column reduction: mode 0: Σx; 1: Σ(x − μ)²; 2: Σgz, Σgz·x̂; 3: Σu, Σu·x̂, Σu·gz.  partial[block][k][C].
+// Column reduction: mode 0: Σx; 1: Σ(x − μ)²; 2: Σgz, Σgz·x̂; 3: Σu, Σu·x̂, Σu·gz.  partial[block][k][C] (float64).
 template <int MODE>
-__global__ __launch_bounds__(NT) void bn_colsum(BnP p, float *partial) {
+__global__ __launch_bounds__(NT) void bn_colsum(BnP p, double *partial) {
     constexpr int K = MODE == 3 ? 3 : (MODE == 2 ? 2 : 1);
-    __shared__ float red[K][NT];
+    __shared__ double red[K][NT];
     const int C = p.C, tid = threadIdx.x;
     // thread -> (channel c, row phase) for C <= NT; channel loop otherwise
     const int rpi = C <= NT ? NT / C : 1;  // rows per iteration
@@ -56,9 +58,9 @@ __global__ __launch_bounds__(NT) void bn_colsum(BnP p, float *partial) {
         const int c = C <= NT ? tid % C : cb + tid;
         const int ph = C <= NT ? tid / C : 0;
         const bool act = (C <= NT ? tid < rpi * C : c < C);
-        float s[K];
+        double s[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) s[k] = 0.f;
+        for (int k = 0; k < K; ++k) s[k] = 0.0;
         if (act) {
 #pragma unroll 4
             for (long long r = r0 + ph; r < r1; r += rpi) {
@@ -67,19 +69,19 @@ __global__ __launch_bounds__(NT) void bn_colsum(BnP p, float *partial) {
                 if (MODE == 0) {
                     s[0] += x;
                 } else if (MODE == 1) {
-                    const float d = x - p.mu[c];
+                    const double d = (double)x - (double)p.mu[c];
                     s[0] += d * d;
                 } else {
                     const float xh = xhat_of(p, x, c);
                     const float gz = p.gy[i] * mask_of(p, xh, c);
                     if (MODE == 2) {
                         s[0] += gz;
-                        s[1] += gz * xh;
+                        s[1] += (double)gz * xh;
                     } else {
                         const float u = p.u[i];
                         s[0] += u;
-                        s[1] += u * xh;
-                        s[2] += u * gz;
+                        s[1] += (double)u * xh;
+                        s[2] += (double)u * gz;
                     }
                 }
             }
@@ -90,7 +92,7 @@ __global__ __launch_bounds__(NT) void bn_colsum(BnP p, float *partial) {
         if (C <= NT) {
             if (tid < C)
                 for (int k = 0; k < K; ++k) {
-                    float v = 0.f;
+                    double v = 0.0;
                     for (int q = 0; q < rpi; ++q) v += red[k][q * C + tid];
                     partial[((long long)blockIdx.x * K + k) * C + tid] = v;
                 }
@@ -104,12 +106,12 @@ __global__ __launch_bounds__(NT) void bn_colsum(BnP p, float *partial) {
 
 // out[k][c] = Σ_b partial[b][k][c]: workgroup = 32 consecutive (k, c) outputs × 8 slices of the blocks, each slice
 // summed in block order, then the slices in slice order (fixed order: deterministic)
-__global__ void bn_finish(const float *partial, int nblk, int K, int C, float *out) {
-    __shared__ float sl[8][32];
+__global__ void bn_finish(const double *partial, int nblk, int K, int C, float *out) {
+    __shared__ double sl[8][32];
     const int o = threadIdx.x & 31, q = threadIdx.x >> 5;
     const int i = blockIdx.x * 32 + o;
     const int b0 = nblk * q / 8, b1 = nblk * (q + 1) / 8;
-    float v = 0.f;
+    double v = 0.0;
     if (i < K * C) {
         const int k = i / C, c = i - k * C;
 #pragma unroll 4
@@ -118,9 +120,9 @@ __global__ void bn_finish(const float *partial, int nblk, int K, int C, float *o
     sl[q][o] = v;
     __syncthreads();
     if (q == 0 && i < K * C) {
-        float t = sl[0][o];
+        double t = sl[0][o];
         for (int r = 1; r < 8; ++r) t += sl[r][o];
-        out[i] = t;
+        out[i] = (float)t;
     }
 }
 
@@ -188,7 +190,8 @@ inline unsigned grid_of(long long n) { return (unsigned)((n + NT - 1) / NT); }
 inline int nblocks_for(long long P) { return (int)(P / 256 < 1 ? 1 : (P / 256 > MAXB ? MAXB : P / 256)); }
 
 template <int MODE>
-int colsum(const BnP &p, float *partial, float *out, hipStream_t st) {
+int colsum(const BnP &p, float *ws, float *out, hipStream_t st) {
+    double *partial = reinterpret_cast<double *>(ws);
     constexpr int K = MODE == 3 ? 3 : (MODE == 2 ? 2 : 1);
     const int nb = nblocks_for(p.P);
     hipLaunchKernelGGL(bn_colsum<MODE>, dim3(nb), dim3(NT), 0, st, p, partial);
@@ -199,7 +202,7 @@ int colsum(const BnP &p, float *partial, float *out, hipStream_t st) {
 }  // namespace
 
 extern "C" int64_t esr_bn_workspace_floats(int64_t P, int32_t C) {
-    return (int64_t)MAXB * 3 * C + 8LL * C;
+    return (int64_t)MAXB * 3 * C * 2 + 8LL * C;  // float64 partials, then [5][C] sums
 }
 
 extern "C" int esr_bn_lrelu_fwd(const float *x, int64_t P, int32_t C, const float *gamma, const float *beta, float eps,
@@ -209,7 +212,7 @@ extern "C" int esr_bn_lrelu_fwd(const float *x, int64_t P, int32_t C, const floa
     const hipStream_t st = (hipStream_t)stream;
     BnP p = {};
     p.x = x; p.gamma = gamma; p.beta = beta; p.mu = mu; p.rs = rs; p.P = P; p.C = C; p.slope = slope;
-    float *partial = ws, *sums = ws + (long long)MAXB * 3 * C;
+    float *partial = ws, *sums = ws + (long long)MAXB * 3 * C * 2;
     if (colsum<0>(p, partial, sums, st)) return ESR_ELAUNCH;
     hipLaunchKernelGGL(bn_stats_finish, dim3(grid_of(C)), dim3(NT), 0, st, sums, C, P, eps, 0, mu, rs, var);
     if (colsum<1>(p, partial, sums, st)) return ESR_ELAUNCH;
@@ -241,7 +244,7 @@ extern "C" int esr_bn_lrelu_bwd2(const float *x, const float *gy, const float *u
     BnP p = {};
     p.x = x; p.gy = gy; p.u = u; p.gamma = gamma; p.beta = beta; p.mu = mu; p.rs = rs; p.P = P; p.C = C;
     p.slope = slope; p.ggg = ggg; p.ggb = ggb;
-    float *partial = ws, *sums5 = ws + (long long)MAXB * 3 * C;  // [Σgz, Σgz·x̂, U, A, Q]
+    float *partial = ws, *sums5 = ws + (long long)MAXB * 3 * C * 2;  // [Σgz, Σgz·x̂, U, A, Q]
     (void)hipMemcpyAsync(sums5, sums2, 2 * C * sizeof(float), hipMemcpyDeviceToDevice, st);
     if (u) {
         if (colsum<3>(p, partial, sums5 + 2 * C, st)) return ESR_ELAUNCH;

@@ -1129,6 +1129,116 @@ __global__ __launch_bounds__(NTHR, 1) void conv_x3_pring_kernel(X3Params p) {
     }
 }
 
+// Narrow-N 3×3 conv (cout <= 3, planar fp32 output: HR_conv1 -> CEM, architecture.py:140-141).  An N = 32 MFMA tile
+// would spend 29 of its 32 output columns on padding (10.7× the MFMA work), so the taps go into M instead: for every
+// INPUT pixel p, Y[t·3 + o][p] = Σ_c W[o][c][t] · x[c][p] for the 9 taps t and 3 outputs o (27 of the 32 rows of one
+// v_mfma_f32_32x32x16_f16 tile, K = 16 channels, N = 32 pixels of one padded row), then out[o][y][x] = Σ_t Y[t·3 + o]
+// at the tap's neighbour — the tap shift moves from the K loop into a 9-term sum over an LDS image of Y.  Every input
+// pixel is fetched once per tile straight into the B fragments (no LDS staging: each is used once), the 27×cin
+// weights stay in registers as A fragments for the whole tile.  Tile = NR output rows × 30 columns of the tall padded
+// batch image (input rows NR + 2 × 32 padded columns), 4 waves, input rows round-robin over the waves with the next
+// row's fragments loaded under the current row's MFMAs.  HBM-bound: 4 B per input channel per pixel in, 12 B out.
+constexpr int NR_ROWS = 16;             // output rows per tile
+constexpr int NR_IN = NR_ROWS + 2;      // input rows per tile
+constexpr int NR_COLS = 30;             // output columns per tile (input: 32 padded columns)
+constexpr int NR_M = 27;                // 9 taps × 3 outputs
+constexpr int NR_THR = 256;
+constexpr int NR_LDS = NR_IN * NR_M * 32 * 4;  // Y image [row][m][32 columns] fp32: 62,208 B (two workgroups per CU)
+
+template <int NCH>
+__global__ __launch_bounds__(NR_THR, 2) void conv_x3_narrow_kernel(X3Params p) {
+    __shared__ __attribute__((aligned(16))) float ys[NR_LDS / 4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int hl = lane >> 5, ml = lane & 31;
+    const int tile = p.xcd_map ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x;
+    const int tx = tile % p.tiles_x, ty = tile / p.tiles_x;
+    const int x0 = tx * NR_COLS;                  // first output column = first input padded column
+    const int r0 = 1 + ty * NR_ROWS;              // first output tall padded row
+    const int rows_tot = p.B * (p.H + 2);
+    const long long rowp = (long long)(p.W + 2), pixb = 4LL * p.in_cp;
+
+    // A fragments: row m = ml (tap m / 3, output m % 3), channels 8 hl .. +8 of chunk j (zero past cout / cin)
+    f16x8 ah[NCH], al[NCH];
+    {
+        const int t = ml / 3, o = ml - 3 * (ml / 3);
+        constexpr int N = 32, W_B = 9 * N * REC;
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) {
+            ah[j] = f16x8{};
+            al[j] = f16x8{};
+            if (ml < NR_M && o < p.cout && 16 * j + 8 * hl < p.cin) {
+                const unsigned char *w = p.w + (long long)j * W_B + (t * N + o) * REC + 32 * hl;
+                ah[j] = *reinterpret_cast<const f16x8 *>(w);
+                al[j] = *reinterpret_cast<const f16x8 *>(w + 16);
+            }
+        }
+    }
+    // B fragments of input row i (tall padded row r0 - 1 + i): pixel column x0 + ml, channels 16 j + 8 hl .. +8
+    const int gx = x0 + ml;
+    auto load_row = [&](int i, f16x8 (&bh)[NCH], f16x8 (&bl)[NCH]) {
+        const int gy = r0 - 1 + i;
+        const bool ok = gy < rows_tot && gx < p.W + 2;
+        const unsigned char *src = p.in + (gy * rowp + gx) * pixb + 32 * hl;
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) {
+            if (ok && 16 * j + 8 * hl < p.cin) {
+                bh[j] = *reinterpret_cast<const f16x8 *>(src + 64 * j);
+                bl[j] = *reinterpret_cast<const f16x8 *>(src + 64 * j + 16);
+            } else {
+                bh[j] = f16x8{};
+                bl[j] = f16x8{};
+            }
+        }
+    };
+    auto compute_row = [&](int i, const f16x8 (&bh)[NCH], const f16x8 (&bl)[NCH]) {
+        f32x16 c = {};
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) {
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[j], bh[j], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[j], bl[j], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[j], bh[j], c, 0, 0, 0);
+        }
+        // c[r] = Y[m = (r & 3) + 8 (r >> 2) + 4 hl][pixel ml]
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = (r & 3) + 8 * (r >> 2) + 4 * hl;
+            if (m < NR_M) ys[(i * NR_M + m) * 32 + ml] = c[r];
+        }
+    };
+    f16x8 bh0[NCH], bl0[NCH], bh1[NCH], bl1[NCH];
+    int i = wave;
+    load_row(i, bh0, bl0);
+    while (i < NR_IN) {  // rows wave, wave + 4, ... (wave-uniform bounds); two rows per trip, next row loaded early
+        const int i1 = i + 4;
+        if (i1 < NR_IN) load_row(i1, bh1, bl1);
+        compute_row(i, bh0, bl0);
+        if (i1 >= NR_IN) break;
+        const int i2 = i1 + 4;
+        if (i2 < NR_IN) load_row(i2, bh0, bl0);
+        compute_row(i1, bh1, bl1);
+        i = i2;
+    }
+    __syncthreads();
+    // out[o][y][x] = (Σ_{ky, kx} Y[3 (3 ky + kx) + o] at input row + ky, column + kx) / w_scale + bias
+    const esr_conv_out &o = p.o;
+    const int HP = p.H + 2;
+    for (int idx = tid; idx < 3 * NR_ROWS * 32; idx += NR_THR) {
+        const int col = idx & 31, row = (idx >> 5) % NR_ROWS, oc = idx / (32 * NR_ROWS);
+        const int tr = r0 + row;
+        if (oc >= p.cout || col >= NR_COLS || x0 + col >= p.W || tr >= rows_tot - 1) continue;
+        const int b = tr / HP, y = tr - b * HP - 1;
+        if (y < 0 || y >= p.H) continue;
+        float s = 0.f;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) s += ys[((row + t / 3) * NR_M + 3 * t + oc) * 32 + col + t % 3];
+        const float v = s * p.w_scale_inv + p.bias[oc];
+        const int oy = o.out_sy * y + o.out_oy, ox = o.out_sx * (x0 + col) + o.out_ox;
+        o.out[(((long long)b * p.cout + oc) * o.out_h + oy) * o.out_w + ox] = v;
+    }
+}
+
+int g_x3_narrow = 1;  // esr_x3_set_narrow: the narrow-N kernel for cout <= 3 planar outputs (0: the N = 32 tiles)
+
 int g_x3_kernel = 1;  // esr_x3_set_kernel (include/esr_amd.h)
 int g_x3_map = 1;     // esr_x3_set_tile_map (XCD-grouped: ~1 % per step, profiles/r1_x3_xcdmap_ab.txt)
 
@@ -1157,6 +1267,16 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
     p.overflow = overflow;
     p.o = *o;
     const dim3 block(NTHR);
+    if (g_x3_narrow && taps_side == 3 && cout <= 3 && o->out_planar && o->lrelu == 0 && !o->r1 && !o->r2 &&
+        !o->out2 && cin <= 80 && (g_x3_kernel == 1 || g_x3_kernel == 63)) {
+        X3Params q = p;
+        q.tiles_x = (W + NR_COLS - 1) / NR_COLS;
+        q.tiles_y = (B * (H + 2) - 2 + NR_ROWS - 1) / NR_ROWS;
+        const dim3 gridn((unsigned)(q.tiles_x * q.tiles_y)), blockn(NR_THR);
+        if (cin <= 64) hipLaunchKernelGGL((conv_x3_narrow_kernel<4>), gridn, blockn, 0, stream, q);
+        else hipLaunchKernelGGL((conv_x3_narrow_kernel<5>), gridn, blockn, 0, stream, q);
+        return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+    }
     // Ring kernel (two tiles per workgroup, esr_x3_set_kernel 2): opt-in only.  With both kernels on counted-wait
     // fragment reads a ring pair cost ~2.0 two-stage classic tiles, and the one-stage classic kernel at two
     // workgroups per CU is faster still (tools/x3_ring_ab.py at config 2 / 3 shapes).
@@ -1322,6 +1442,13 @@ extern "C" int esr_x3_set_kernel(int32_t variant) {
 #endif
     const int prev = g_x3_kernel;
     g_x3_kernel = variant;
+    return prev;
+}
+
+extern "C" int esr_x3_set_narrow(int32_t on) {
+    if (on < 0 || on > 1) return ESR_EINVAL;
+    const int prev = g_x3_narrow;
+    g_x3_narrow = on;
     return prev;
 }
 

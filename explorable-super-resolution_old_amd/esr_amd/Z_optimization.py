@@ -460,7 +460,8 @@ class Z_optimizer:
         if any(w in o for w in ('l1', 'scribble')) and 'random' not in o:
             if data is not None and 'HR' in data:
                 self.GT_HR = data['HR']
-            if self.image_mask is None:
+            if self.Z_mask is None:  # no image / Z mask passed (the reference tests self.image_mask, which is the
+                # all-ones mask whenever the model holds a fake_H, and then fails in its masked closure: plain L1 here)
                 self.loss = torch.nn.L1Loss()
             else:
                 self._build_scribble(data)

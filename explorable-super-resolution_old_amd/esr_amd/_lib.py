@@ -50,6 +50,7 @@ _SIGNATURES = {
                                   c_int, c_int, ctypes.POINTER(ConvOut), c_void_p, c_void_p],
     'esr_x3_set_kernel': [c_int],
     'esr_x3_set_tile_map': [c_int],
+    'esr_x3_set_narrow': [c_int],
     'esr_cem_set_direct': [c_int],
     'esr_conv_set_tile': [c_int],
     'esr_cem_down': [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int,

@@ -36,6 +36,9 @@ WGRAD_X3 = os.environ.get('ESR_WGRAD_X3', '1') != '0'
 # Data gradients inside the residual blocks on the x3 conv (split-f16 gradients scaled per RRDB, include/esr_amd.h
 # "x3 backward") when the forward ran in x3 and only parameter gradients are wanted (training); 0 keeps them fp32.
 DGRAD_X3 = os.environ.get('ESR_DGRAD_X3', '1') != '0'
+# with the x3 backward, also the trunk-level data gradients at 2x / 4x resolution (HR_conv0, the two upconvs) on the x3
+# conv, each at its own gradient scale (Runner.dgrad_trunk_x3); '0' keeps them exact fp32
+TRUNK_X3 = os.environ.get('ESR_TRUNK_X3', '1') != '0'
 
 
 def _z(dev, *s):
@@ -123,7 +126,8 @@ class TrainWorkspace:
         self.dFirst = _z(dev, B, H + 2, W + 2, self.first_cp)
         self.dZh = _z(dev, B, 4 * H + 2, 4 * W + 2, 8) if latent else None
         self.dzs = _z(dev, B, H + 2, W + 2, 8) if latent else None  # x3 backward: split latent-slot gradient
-        self.gamax = torch.zeros(nb, device=dev, dtype=torch.int32)  # per-RRDB max |gradient| bits (x3 backward)
+        # per-RRDB max |gradient| bits (x3 backward), then one slot per x3 trunk-level data gradient (_trunk_dgrad_x3)
+        self.gamax = torch.zeros(nb + 4, device=dev, dtype=torch.int32)
         self.bwd_overflow = torch.zeros(1, device=dev, dtype=torch.int32)
         self.wg_n_max = 9 * 224 * 64 + 64
         self.partial = torch.empty(WG_SPLITS_MAX * self.wg_n_max, device=dev, dtype=torch.float32)
@@ -259,6 +263,11 @@ class _BwdPacked:
         buf = self.plan.buf
         if self._x3 is None:
             views = [(i, k, v) for i, f in enumerate(self.rdb_fused) for k, v in f.items()]
+            # the trunk-level data gradients at 2x / 4x resolution (HR_conv0, both upconvs): slices and, for
+            # HR_conv0, the latent-slot (input) slice; keyed (conv, kind, slice index) in self._x3_trunk
+            trunk = [(name, kind, j, v) for name, c in (('hr0', self.hr0), ('up1', self.up[1]), ('up0', self.up[0]))
+                     for kind, sl in (('s', c.slices), ('in', c.in_slices)) for j, (_, _, v) in enumerate(sl)]
+            views += [(None, (name, kind, j), v) for name, kind, j, v in trunk]
             amax = torch.stack([v.abs().max() for _, _, v in views]).cpu().tolist()  # first build only
             idx, scl, out, off = [], [], [], 0
             for (i, k, v), a in zip(views, amax):
@@ -272,8 +281,9 @@ class _BwdPacked:
             self._x3_idx, self._x3_scl = torch.cat(idx), torch.cat(scl)
             self._x3_buf = torch.empty(off, device=buf.device, dtype=torch.float16)
             self._x3_w = [dict() for _ in self.rdb_fused]
+            self._x3_trunk = {}
             for i, k, o, n, sc in out:
-                self._x3_w[i][k] = (self._x3_buf[o:o + 2 * n], sc)
+                (self._x3_trunk if i is None else self._x3_w[i])[k] = (self._x3_buf[o:o + 2 * n], sc)
             self._x3_bad = torch.zeros(1, device=buf.device, dtype=torch.int32)
             self._x3 = 'stale'
         if self._x3 == 'stale':
@@ -424,6 +434,31 @@ class _Runner:
                                                wpk.data_ptr(), self.bp.zero_bias.data_ptr(), w_scale, nw,
                                                ctypes.byref(o), self.x3[2].data_ptr(), self.stream), 'dgrad_x3')
 
+    def dgrad_trunk_x3(self, name, bc, src, h, w, dst, dst_base, s_in, s_out, slot, dz=None):
+        """dst[:, 0:64] (fp32) = the data gradient of trunk conv `name` from its fp32 64-channel output gradient
+        `src`, on the x3 conv: src -> split × S(max |src|) into s_in, the conv into s_out (split, the same scale: the
+        conv is linear), back to fp32 into dst.  s_in / s_out: padded 64-channel buffers of this grid that are free
+        here (zero halos; s_in may be dst, s_out may be src).  dz = (fp32 buffer, pitch, 8-channel split scratch):
+        also the input-slice (latent slot) gradient, accumulated into the buffer.  Gradient-scale slot `slot` of
+        ws.gamax; an f16-range overflow sets ws.bwd_overflow (the backward is then redone in fp32)."""
+        lib, ws, B = self.lib, self.ws, self.B
+        amax = ws.gamax.data_ptr() + 4 * slot
+        ovf = ws.bwd_overflow.data_ptr()
+        _lib.check(lib.esr_grad_amax(src.data_ptr(), 64, 0, 64, B, h, w, amax, self.stream), 'grad_amax')
+        _lib.check(lib.esr_axpby_gs(s_in.data_ptr(), 64, 0, 1, 1.0, src.data_ptr(), 64, 0, 0, 0.0, None, 0, 0, 0, 64,
+                                    B, h, w, amax, ovf, self.stream), 'axpby_gs')
+        tw = self.bp._x3_trunk
+        if dz is not None and self.need_input:
+            zbuf, z_cp, zscr = dz
+            for j, (n0, nw, _) in enumerate(bc.in_slices):
+                self.dgrad_x3(tw[(name, 'in', j)], s_in, 64, 0, 64, h, w, zscr, 8, n0, nw)
+            _lib.check(lib.esr_axpby_gs(zbuf.data_ptr(), z_cp, 0, 0, 1.0, zbuf.data_ptr(), z_cp, 0, 0, 1.0,
+                                        zscr.data_ptr(), 8, 0, 1, 8, B, h, w, amax, ovf, self.stream), 'axpby_gs')
+        for j, (n0, nw, _) in enumerate(bc.slices):
+            self.dgrad_x3(tw[(name, 's', j)], s_in, 64, 0, 64, h, w, s_out, 64, n0 - dst_base, nw)
+        _lib.check(lib.esr_axpby_gs(dst.data_ptr(), 64, 0, 0, 1.0, s_out.data_ptr(), 64, 0, 1, 0.0, None, 0, 0, 0, 64,
+                                    B, h, w, amax, ovf, self.stream), 'axpby_gs')
+
     def lrelu(self, d, d_cp, d_coff, y, y_cp, y_coff, C, h, w):
         fn = self.lib.esr_lrelu_bwd_split if self.split else self.lib.esr_lrelu_bwd
         _lib.check(fn(d.data_ptr(), d_cp, d_coff, y.data_ptr(), y_cp, y_coff, C, self.B, h, w, self.stream),
@@ -527,17 +562,28 @@ def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_in
     # HR_conv0 + LReLU: output HR1.x
     R.lrelu(dA, 64, 0, HR1, hcp, zc, 64, HH, WW)
     R.wgrad(bp.hr0, HR0, hcp, hcp, 0, dA, 64, 0, HH, WW)
-    R.dgrad_in(bp.hr0, dA, 64, 0, 64, HH, WW, ws.dZh, 8)
-    R.dgrad(bp.hr0, dA, 64, 0, 64, HH, WW, dB, 64, zc, accumulate=False)
+    # the trunk-level data gradients at 2x / 4x on the x3 conv when the backward is x3 (TRUNK_X3), else exact fp32
+    tx3 = x3 and TRUNK_X3
+    if tx3:
+        R.dgrad_trunk_x3('hr0', bp.hr0, dA, HH, WW, dB, zc, dB, dA, net.nb, dz=(ws.dZh, 8, ws.dgen_p) if zc else None)
+    else:
+        R.dgrad_in(bp.hr0, dA, 64, 0, 64, HH, WW, ws.dZh, 8)
+        R.dgrad(bp.hr0, dA, 64, 0, 64, HH, WW, dB, 64, zc, accumulate=False)
     # upconv 2: HR0.x = lrelu(conv(nearest2(U1)))
     R.lrelu(dB, 64, 0, HR0, hcp, zc, 64, HH, WW)
     R.wgrad(bp.up[1], ws.U1, 64, 64, 1, dB, 64, 0, HH, WW)
-    R.dgrad(bp.up[1], dB, 64, 0, 64, HH, WW, dA, 64, 0, accumulate=False)
+    if tx3:
+        R.dgrad_trunk_x3('up1', bp.up[1], dB, HH, WW, dA, 0, dA, dB, net.nb + 1)
+    else:
+        R.dgrad(bp.up[1], dB, 64, 0, 64, HH, WW, dA, 64, 0, accumulate=False)
     _lib.check(lib.esr_sum2x2(ws.dU1.data_ptr(), 64, 0, dA.data_ptr(), 64, 0, 64, Bn, 2 * H, 2 * W, stream), 'sum2x2')
     # upconv 1: U1 = lrelu(conv(nearest2(U0)))
     R.lrelu(ws.dU1, 64, 0, ws.U1, 64, 0, 64, 2 * H, 2 * W)
     R.wgrad(bp.up[0], ws.U0, 64, 64, 1, ws.dU1, 64, 0, 2 * H, 2 * W)
-    R.dgrad(bp.up[0], ws.dU1, 64, 0, 64, 2 * H, 2 * W, ws.dUp1, 64, 0, accumulate=False)
+    if tx3:
+        R.dgrad_trunk_x3('up0', bp.up[0], ws.dU1, 2 * H, 2 * W, ws.dUp1, 0, ws.dUp1, ws.dU1, net.nb + 2)
+    else:
+        R.dgrad(bp.up[0], ws.dU1, 64, 0, 64, 2 * H, 2 * W, ws.dUp1, 64, 0, accumulate=False)
     _lib.check(lib.esr_sum2x2(ws.dU0.data_ptr(), 64, 0, ws.dUp1.data_ptr(), 64, 0, 64, Bn, H, W, stream), 'sum2x2')
     # LR_conv: U0 = conv(trunk[Z | x]) + fea
     Q = ws.Q

@@ -157,6 +157,13 @@ int esr_x3_set_kernel(int32_t variant);
  * over blockIdx.  Results are bitwise identical.  Returns the previous setting, or ESR_EINVAL. */
 int esr_x3_set_tile_map(int32_t mode);
 
+/* Narrow-N path of esr_conv3x3_fwd_x3 (process-wide): 1 (default) = a 3×3 conv with cout <= 3, cin <= 80 and a planar
+ * fp32 output without residuals (HR_conv1 -> CEM, architecture.py:140-141) puts the 9 taps × 3 outputs into the MFMA M
+ * dimension (27 of 32 rows) and sums the taps' shifted partial products from LDS, instead of an N = 32 tile of which 29
+ * columns are padding; 0 = the N = 32 tiles.  Results agree to the x3 rounding (not bitwise: the tap sum order
+ * differs).  Returns the previous setting, or ESR_EINVAL. */
+int esr_x3_set_narrow(int32_t on);
+
 /* ---- training / Z-optimisation backward (esr_train.hip) ------------------------------------------------------------
  * The data gradient of every conv is esr_conv3x3_fwd run with rot180, in/out-swapped packed weights (host-side
  * repacking), i.e. the backward of conv_block (block.py:129-156) for loss.backward() in

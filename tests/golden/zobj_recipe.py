@@ -99,6 +99,10 @@ def case_data(name, seed):
             spec.get('lr', 0.05))
 
 
+# stiff=True: a 1e4-weighted STD-preservation term ('localSTD', also inside 'no_localSTD') makes every Adam step
+# overshoot, so after the first iteration the trajectory amplifies rounding differences (the loss jumps by 100x from
+# one iteration to the next in the reference itself); tests compare those cases' later iterations only where the
+# arithmetic order matches the reference's (the CPU) and their first iteration everywhere.
 # The GUI's objective strings with its shipped switches (GUI.py:37-49, 1505-1517: LOCAL_STD_4_OPT, NO_DC_IN_PATCH_
 # HISTOGRAM, DICTIONARY_REPLACES_HISTOGRAM, AUTO_CYCLE_LENGTH_4_PERIODICITY; 'special behaviour' -> Mag, Plus,
 # no_localSTD), plus the plain forms
@@ -111,9 +115,9 @@ CASES = {
     'TV_masked': dict(objective='TV'),
     'dict_noDC': dict(objective='dict_noDC', hist=True),
     'patchdict_noDC': dict(objective='patchdict_noDC', hist=True),
-    'patchdict_noDC_no_localSTD': dict(objective='patchdict_noDC_no_localSTD', hist=True),
-    'hist_localSTD': dict(objective='hist_localSTD', hist=True),
-    'patchhist_noDC_localSTD': dict(objective='patchhist_noDC_localSTD', hist=True),
+    'patchdict_noDC_no_localSTD': dict(objective='patchdict_noDC_no_localSTD', hist=True, stiff=True),
+    'hist_localSTD': dict(objective='hist_localSTD', hist=True, stiff=True),
+    'patchhist_noDC_localSTD': dict(objective='patchhist_noDC_localSTD', hist=True, stiff=True),
     'local_STD_nonInt_periodicity': dict(objective='local_STD_nonInt_periodicity',
                                          points=[[3.3, 1.2], [-0.8, 4.1]]),
     'local_STD_nonInt_periodicity_1D': dict(objective='local_STD_nonInt_periodicity_1D', points=[[2.6, 2.6]]),
@@ -126,3 +130,9 @@ CASES = {
     'random_l1': dict(objective='random_l1', batch=3, lr=0.1),
     'random_l1_limited': dict(objective='random_l1_limited', batch=2, rmse_weight=0.5, lr=0.1),
 }
+
+
+def FIRST_ITERS(name):
+    """Iterations of a case's short run (the first iteration; two for 'random…limited', whose reference loop reads
+    loss_values[1], Z_optimization.py:644)."""
+    return 2 if 'limited' in CASES[name]['objective'] else 1

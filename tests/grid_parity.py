@@ -54,6 +54,9 @@ def c3_training_step(dev, precision='x3', d_precision=None):
             if 'f64_' + key not in d.files:
                 continue
             if p.grad is None:
+                if 'Filter_OP' in k:  # the CEM filters: requires_grad=False at construction (CEMnet.py:134), so the
+                    continue          # reference's optimizer_G leaves them out (SRRaGAN_model.py:207-211); their .grad
+                    #                   there is a by-product of optimize_parameters re-enabling requires_grad (:468)
                 fails.append((tag, k, 'no gradient'))
                 continue
             mine = grad_projections(p.grad.detach().double().cpu().numpy(), cfg['seed'] + (10 if tag == 'G' else 11),

@@ -572,3 +572,35 @@ def test_cem_tiled_stencils_bitwise_equal_direct(gpu_device, B, H, W, ki, kd, M)
         ref = gen.double().cpu().view(B * 3, 1, 4 * H, 4 * W) + up
         ref = ref[:, :, M:4 * H - M, M:4 * W - M]
         assert normwise_rel(got.cpu().view_as(ref), ref) < 1e-5
+
+
+@pytest.mark.parametrize('cin,B,H,W', [(64, 2, 19, 45), (72, 3, 17, 61), (64, 1, 1, 1), (72, 2, 40, 30),
+                                       (64, 4, 33, 92)])
+def test_conv3x3_x3_narrow_planar(gpu_device, cin, B, H, W):
+    """The narrow-N x3 path (cout 3, planar fp32 output: HR_conv1 -> CEM; taps in the MFMA M dimension, shifted
+    partial products summed from LDS) against float64, and against the N = 32 tile path it replaces (same x3 products,
+    another tap summation order), over odd sizes, partial 30-column tiles, the latent 72-channel input (a half-filled
+    last K chunk whose channels past cin are never read) and tiles straddling images of the tall batch image."""
+    lib = _lib.load()
+    cp = cin
+    xs = engine.to_split(_padded(B, H, W, cp, cin, gpu_device, 31))
+    g = torch.Generator().manual_seed(32)
+    w = torch.randn(3, cin, 3, 3, generator=g) * 0.05
+    b = (torch.rand(3, generator=g) - 0.5).to(gpu_device)
+    wx, scale = engine.pack_x3(engine.pack_conv_weight(w.to(gpu_device), list(range(cin)), 32))
+    outs = []
+    try:
+        for narrow in (1, 0):
+            lib.esr_x3_set_narrow(narrow)
+            out = torch.full((B, 3, H, W), 7.0, device=gpu_device)
+            o = engine._conv_out(out, 0, 0, H, W, False, planar=1)
+            _lib.check(lib.esr_conv3x3_fwd_x3(xs.data_ptr(), B, H, W, cp, cin, wx.data_ptr(), b.data_ptr(), scale, 3,
+                                              ctypes.byref(o), None, _stream()), 'conv_x3')
+            torch.cuda.synchronize()
+            outs.append(out.cpu())
+    finally:
+        lib.esr_x3_set_narrow(1)
+    ref = F.conv2d(_nchw(engine.from_split(xs), 0, cin), w.double(), b.cpu().double(), padding=1)
+    for out in outs:
+        assert normwise_rel(out, ref) < 2e-6, normwise_rel(out, ref)
+    assert float((outs[0].double() - outs[1].double()).abs().max() / ref.abs().max()) < 2e-6

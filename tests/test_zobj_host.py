@@ -13,17 +13,18 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, 'golden'))
-from zobj_recipe import CASES, StandInModel, case_data  # noqa: E402
+from zobj_recipe import CASES, FIRST_ITERS, StandInModel, case_data  # noqa: E402
 
 FIX = np.load(os.path.join(HERE, 'golden', 'zobj_cases.npz'))
 LOSS_RTOL, LOSS_ATOL = 2e-4, 1e-7
 Z_RTOL = 2e-3  # relative L2 of the returned Z's change from its initial value
 
 
-def run_port(name, device):
+def run_port(name, device, iters=None):
     from esr_amd.Z_optimization import Z_optimizer
     seed = int(FIX['%s:seed' % name])
-    objective, B, data, img_mask, z_mask, z_range, lr, z, iters, lr0 = case_data(name, seed)
+    objective, B, data, img_mask, z_mask, z_range, lr, z, iters0, lr0 = case_data(name, seed)
+    iters = iters or iters0
     torch.manual_seed(0)
     noise = np.random.default_rng(seed + 7)  # the fixture's torch.normal stream ('random…limited' perturbation)
     orig = torch.randn_like
@@ -47,14 +48,17 @@ def run_port(name, device):
     return zo, z_out.detach().cpu().numpy(), z
 
 
-def check_case(name, device):
-    zo, z_out, z0 = run_port(name, device)
-    ref_loss = FIX['%s:loss_values' % name]
+def check_case(name, device, first=False):
+    """first: the case's short run (the first iteration; FIRST_ITERS) against the reference's short run."""
+    sfx = '1' if first else ''
+    zo, z_out, z0 = run_port(name, device, FIRST_ITERS(name) if first else None)
+    ref_loss = FIX['%s:loss_values%s' % (name, sfx)]
     got = np.array(zo.loss_values)
     assert got.shape == ref_loss.shape
     assert np.allclose(got, ref_loss, rtol=LOSS_RTOL, atol=LOSS_ATOL), (name, got, ref_loss)
-    assert np.allclose(np.array(zo.latest_Z_loss_values), FIX['%s:latest' % name], rtol=LOSS_RTOL, atol=LOSS_ATOL)
-    ref_z = FIX['%s:z_out' % name]
+    assert np.allclose(np.array(zo.latest_Z_loss_values), FIX['%s:latest%s' % (name, sfx)], rtol=LOSS_RTOL,
+                       atol=LOSS_ATOL)
+    ref_z = FIX['%s:z_out%s' % (name, sfx)]
     step = np.linalg.norm(ref_z - z0)
     err = np.linalg.norm(z_out - ref_z)
     if abs(ref_loss[-1] - ref_loss[0]) <= 1e-5 * abs(ref_loss[0]):
@@ -73,6 +77,7 @@ def test_fixture_covers_every_case():
 @pytest.mark.parametrize('name', sorted(CASES))
 def test_objective_matches_reference_cpu(name):
     check_case(name, 'cpu')
+    check_case(name, 'cpu', first=True)
 
 
 def test_patch_extraction_matrix_layout():
