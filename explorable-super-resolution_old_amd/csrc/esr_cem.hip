@@ -470,6 +470,7 @@ __global__ __launch_bounds__(256) void cem_up_add_win4(const float *__restrict__
 struct PrepParams {
     const float *x;
     int B, nz, h, w, sf, m, split;
+    float ascale;  // split outputs hold v × ascale (a power of two: the x3 forward's activation scale)
     float *lr_nchw;
     float *first;
     int first_cp, first_lr_off;
@@ -489,12 +490,13 @@ __device__ __forceinline__ float zhr_at(const PrepParams &p, int b, int c, int Y
     return p.x[b * bstride + (long long)c * Hs * Ws + (long long)yy * Ws + xx];
 }
 
-// Store channel c of a padded-NHWC pixel record, fp32 or split f16 (hi/lo groups of 8, esr_conv_x3.hip).
-__device__ __forceinline__ void put_ch(float *buf, long long pix, int cp, int c, float v, int split) {
+// Store channel c of a padded-NHWC pixel record, fp32 or split f16 (hi/lo groups of 8, esr_conv_x3.hip) of v × ascale.
+__device__ __forceinline__ void put_ch(float *buf, long long pix, int cp, int c, float v, int split, float ascale) {
     if (!split) {
         buf[pix * cp + c] = v;
         return;
     }
+    v *= ascale;
     _Float16 *q = reinterpret_cast<_Float16 *>(reinterpret_cast<unsigned char *>(buf) + (pix * cp + (c & ~7)) * 4);
     const _Float16 hi = (_Float16)v;
     q[c & 7] = hi;
@@ -516,7 +518,7 @@ __global__ __launch_bounds__(NT) void prep_lr_kernel(PrepParams p) {
     for (int c = 0; c < 3; ++c) {
         const float v = lr[(long long)c * p.h * p.w + (long long)sy * p.w + sx];
         if (p.lr_nchw) p.lr_nchw[(((long long)b * 3 + c) * H + y) * W + x] = v;
-        if (p.first) put_ch(p.first, pix, p.first_cp, p.first_lr_off + c, v, p.split);
+        if (p.first) put_ch(p.first, pix, p.first_cp, p.first_lr_off + c, v, p.split, p.ascale);
     }
     if (p.nz == 0) return;
     // F.interpolate(scale 1/sf, bilinear, align_corners=False): src = (d+0.5)*sf-0.5
@@ -529,8 +531,8 @@ __global__ __launch_bounds__(NT) void prep_lr_kernel(PrepParams p) {
     for (int c = 0; c < p.nz; ++c) {
         const float v = hy0 * (hx0 * zhr_at(p, b, c, y0, x0) + lx * zhr_at(p, b, c, y0, x1)) +
                         ly * (hx0 * zhr_at(p, b, c, y1, x0) + lx * zhr_at(p, b, c, y1, x1));
-        if (p.first) put_ch(p.first, pix, p.first_cp, c, v, p.split);
-        for (int k = 0; k < p.n_zlr; ++k) put_ch(p.zlr[k], pix, p.zlr_cp[k], c, v, p.split);
+        if (p.first) put_ch(p.first, pix, p.first_cp, c, v, p.split, p.ascale);
+        for (int k = 0; k < p.n_zlr; ++k) put_ch(p.zlr[k], pix, p.zlr_cp[k], c, v, p.split, p.ascale);
     }
 }
 
@@ -545,7 +547,7 @@ __global__ __launch_bounds__(NT) void prep_hr_kernel(PrepParams p) {
     const long long pix = ((long long)b * (Hs + 2) + Y + 1) * (Ws + 2) + X + 1;
     for (int c = 0; c < p.nz; ++c) {
         const float v = zhr_at(p, b, c, Y, X);
-        for (int k = 0; k < p.n_zhr; ++k) put_ch(p.zhr[k], pix, p.zhr_cp[k], c, v, p.split);
+        for (int k = 0; k < p.n_zhr; ++k) put_ch(p.zhr[k], pix, p.zhr_cp[k], c, v, p.split, p.ascale);
     }
 }
 
@@ -643,15 +645,16 @@ extern "C" int esr_cem_set_direct(int32_t direct) {
     return prev;
 }
 
-extern "C" int esr_prep_input(const float *x, int32_t B, int32_t nz, int32_t h, int32_t w, int32_t sf, int32_t m,
-                              float *lr_nchw, float *first, int32_t first_cp, int32_t first_lr_off,
-                              float *const *zlr_dst, const int32_t *zlr_cp, int32_t n_zlr, float *const *zhr_dst,
-                              const int32_t *zhr_cp, int32_t n_zhr, int32_t split, esr_stream_t stream) {
+extern "C" int esr_prep_input_s(const float *x, int32_t B, int32_t nz, int32_t h, int32_t w, int32_t sf, int32_t m,
+                                float *lr_nchw, float *first, int32_t first_cp, int32_t first_lr_off,
+                                float *const *zlr_dst, const int32_t *zlr_cp, int32_t n_zlr, float *const *zhr_dst,
+                                const int32_t *zhr_cp, int32_t n_zhr, int32_t split, float act_scale,
+                                esr_stream_t stream) {
     if (!x || B <= 0 || h <= 0 || w <= 0 || sf <= 0 || m < 0 || nz < 0 || n_zlr < 0 || n_zlr > 4 || n_zhr < 0 ||
-        n_zhr > 4)
+        n_zhr > 4 || !(act_scale > 0.f))
         return ESR_EINVAL;
     PrepParams p = {};
-    p.x = x; p.B = B; p.nz = nz; p.h = h; p.w = w; p.sf = sf; p.m = m; p.split = split;
+    p.x = x; p.B = B; p.nz = nz; p.h = h; p.w = w; p.sf = sf; p.m = m; p.split = split; p.ascale = act_scale;
     p.lr_nchw = lr_nchw; p.first = first; p.first_cp = first_cp; p.first_lr_off = first_lr_off;
     p.n_zlr = nz ? n_zlr : 0;
     p.n_zhr = nz ? n_zhr : 0;
@@ -664,4 +667,12 @@ extern "C" int esr_prep_input(const float *x, int32_t B, int32_t nz, int32_t h, 
     hipLaunchKernelGGL(prep_hr_kernel, dim3(nblocks((long long)B * sf * H * sf * W)), dim3(NT), 0,
                        (hipStream_t)stream, p);
     return launched();
+}
+
+extern "C" int esr_prep_input(const float *x, int32_t B, int32_t nz, int32_t h, int32_t w, int32_t sf, int32_t m,
+                              float *lr_nchw, float *first, int32_t first_cp, int32_t first_lr_off,
+                              float *const *zlr_dst, const int32_t *zlr_cp, int32_t n_zlr, float *const *zhr_dst,
+                              const int32_t *zhr_cp, int32_t n_zhr, int32_t split, esr_stream_t stream) {
+    return esr_prep_input_s(x, B, nz, h, w, sf, m, lr_nchw, first, first_cp, first_lr_off, zlr_dst, zlr_cp, n_zlr,
+                            zhr_dst, zhr_cp, n_zhr, split, 1.f, stream);
 }

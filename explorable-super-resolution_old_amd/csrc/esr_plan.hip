@@ -34,8 +34,9 @@ int dispatch(const esr_op &op, hipStream_t s) {
         float *zhr[2] = {(float *)p[7], (float *)p[8]};
         const int32_t zlr_cp[4] = {i[8], i[9], i[10], i[11]};
         const int32_t zhr_cp[2] = {i[13], i[14]};
-        return esr_prep_input((const float *)p[0], i[0], i[1], i[2], i[3], i[4], i[5], (float *)p[1], (float *)p[2],
-                              i[6], i[7], zlr, zlr_cp, i[12], zhr, zhr_cp, i[15], i[16], st);
+        return esr_prep_input_s((const float *)p[0], i[0], i[1], i[2], i[3], i[4], i[5], (float *)p[1],
+                                (float *)p[2], i[6], i[7], zlr, zlr_cp, i[12], zhr, zhr_cp, i[15], i[16],
+                                op.f[0] > 0.f ? op.f[0] : 1.f, st);
     }
     case ESR_OP_CEM_DOWN:
         return esr_cem_down((const float *)p[0], (const float *)p[1], (float *)p[2], i[0], i[1], i[2], i[3], i[4],

@@ -643,7 +643,7 @@ __device__ __forceinline__ float gscale_of(const unsigned *amax) {
 // threads of a one-thread-per-output loop.
 constexpr int RED_O = 32, RED_S = NT / RED_O;
 __global__ void wgrad_reduce_kernel(const float *partial, int splits, long long n, float scale, float *out,
-                                    const unsigned *amax) {
+                                    const unsigned *amax, long long n_w = -1, float scale_b = 0.f) {
     __shared__ float sl[RED_S][RED_O];
     const int o = threadIdx.x % RED_O, q = threadIdx.x / RED_O;
     const long long i = (long long)blockIdx.x * RED_O + o;
@@ -656,7 +656,8 @@ __global__ void wgrad_reduce_kernel(const float *partial, int splits, long long 
     if (q == 0 && i < n) {
         float t = sl[0][o];
         for (int r = 1; r < RED_S; ++r) t += sl[r][o];
-        out[i] = amax ? (scale * t) / gscale_of(amax) : scale * t;
+        const float sc = (n_w >= 0 && i >= n_w) ? scale_b : scale;  // entries past n_w: the bias gradients
+        out[i] = amax ? (sc * t) / gscale_of(amax) : sc * t;
     }
 }
 
@@ -998,6 +999,14 @@ extern "C" int esr_wgrad_reduce_gs(const float *partial, int32_t splits, int64_t
     if (!partial || !out || !amax || splits <= 0 || n <= 0) return ESR_EINVAL;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n + RED_O - 1) / RED_O)), dim3(NT), 0,
                        (hipStream_t)stream, partial, splits, n, scale, out, amax);
+    return launched();
+}
+
+extern "C" int esr_wgrad_reduce2(const float *partial, int32_t splits, int64_t n, int64_t n_w, float scale_w,
+                                 float scale_b, const uint32_t *amax, float *out, esr_stream_t stream) {
+    if (!partial || !out || splits <= 0 || n <= 0 || n_w < 0 || n_w > n) return ESR_EINVAL;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n + RED_O - 1) / RED_O)), dim3(NT), 0,
+                       (hipStream_t)stream, partial, splits, n, scale_w, out, amax, (long long)n_w, scale_b);
     return launched();
 }
 

@@ -8,7 +8,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('ESR_AMD_LIB', os.path.join(_HERE, 'libesr_amd.so'))
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 c_int = ctypes.c_int32
 c_float = ctypes.c_float
@@ -71,6 +71,11 @@ _SIGNATURES = {
                           c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                           c_void_p],
     'esr_wgrad_reduce_gs': [c_void_p, c_int, ctypes.c_int64, c_float, c_void_p, c_void_p, c_void_p],
+    'esr_wgrad_reduce2': [c_void_p, c_int, ctypes.c_int64, ctypes.c_int64, c_float, c_float, c_void_p, c_void_p,
+                          c_void_p],
+    'esr_prep_input_s': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int,
+                         ctypes.POINTER(c_void_p), ctypes.POINTER(c_int), c_int,
+                         ctypes.POINTER(c_void_p), ctypes.POINTER(c_int), c_int, c_int, c_float, c_void_p],
     'esr_grad_amax': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     'esr_axpby_gs': [c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_int,
                      c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],

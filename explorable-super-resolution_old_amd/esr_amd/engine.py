@@ -79,6 +79,20 @@ def release_timers():
             lib.esr_timer_destroy(pool.pop())
 # Number of forwards recomputed in f32 after an f16-range overflow (observability; tests read it).
 OVERFLOW_RERUNS = 0
+# Activation scale of the x3 forward (a power of two A): every split activation holds A·v (the prep kernel scales the
+# inputs, every x3 conv adds its bias × A, LeakyReLU and the residual adds are homogeneous, the planar HR_conv1 output is
+# divided by A), so that small activations keep their f16 lo parts in the normal range: a value v is carried to ~2^-22
+# relative only while |A·v| >= 2^-3 (below, the lo part is an f16 subnormal with 2^-24 absolute steps).  A forward whose
+# scaled activation leaves f16's range is redone in exact fp32 and the model's A is lowered 16× (lower_act_scale).
+ACT_SCALE = float(os.environ.get('ESR_ACT_SCALE', '256'))
+
+
+def act_scale(net):
+    return getattr(net, '_esr_act_scale', ACT_SCALE)
+
+
+def lower_act_scale(net):
+    net._esr_act_scale = max(1.0, act_scale(net) / 16)
 
 
 def _prof_begin(prof, tag, flops):
@@ -167,11 +181,12 @@ def fold_upconv_phase(w, py, px, f=2):
 
 
 class _ConvW:
-    """One conv's packed weights in both precisions (x3 built lazily) + its bias parameter."""
-    __slots__ = ('f32', 'bias', '_x3')
+    """One conv's packed weights in both precisions (x3 built lazily) + its bias parameter (and, for the x3 forward,
+    the bias × the activation scale: _Packed.act_bias)."""
+    __slots__ = ('f32', 'bias', '_x3', 'bias_s')
 
     def __init__(self, f32, bias):
-        self.f32, self.bias, self._x3 = f32, bias, None
+        self.f32, self.bias, self._x3, self.bias_s = f32, bias, None, None
 
     def x3(self):
         if self._x3 is None:
@@ -328,6 +343,38 @@ class _Packed:
     def reset_train_x3(self):
         self._tx3 = None
 
+    def act_bias(self, A):
+        """The x3 forward's biases × A (the activation scale, act_scale): one persistent buffer, refreshed by one gather
+        from the parameters when they or A change (pointers stay fixed for recorded op lists and captured graphs); sets
+        every conv's bias_s.  HR_conv1 keeps its own bias: its planar output is divided by A instead."""
+        convs = [cw for cw in self.planned if cw is not self.hr1] + [c for row in self.up for c in row]
+        if getattr(self, '_bs', None) is None:
+            offs, o = {}, 0
+            for p in self.plan.params:
+                offs[id(p)] = o
+                o += p.numel()
+            idx, spans, o = [], [], 0
+            for cw in convs:
+                n = cw.bias.numel()
+                idx.append(torch.arange(offs[id(cw.bias)], offs[id(cw.bias)] + n))
+                spans.append((o, n))
+                o += n
+            dev = self.plan.buf.device
+            self._bs_idx = torch.cat(idx).to(dev)
+            self._bs = torch.empty(o, device=dev, dtype=torch.float32)
+            for cw, (a, n) in zip(convs, spans):
+                cw.bias_s = self._bs[a:a + n]
+            self._bs_key = None
+        key = (getattr(self, 'version', 0), A)
+        if self._bs_key != key:
+            flat = self.plan._flat_source()
+            if flat is None:
+                flat = torch.cat([p.detach().reshape(-1) for p in self.plan.params])
+            torch.index_select(flat, 0, self._bs_idx, out=self._bs)
+            self._bs.mul_(A)
+            self._bs_key = key
+        self.hr1.bias_s = self.hr1.bias
+
     def refresh(self):
         self.plan.refresh()
         self.version = getattr(self, 'version', 0) + 1  # invalidates recorded op lists (new x3 weight tensors)
@@ -480,11 +527,11 @@ class _Recorder:
     def esr_upconv2x_phase_fwd_x3(self, inp, B, H, W, in_cp, cin, w, bias, w_scale, cout, py, px, o, ovf, stream):
         return self._add(_lib.OP_UPCONV_X3, [inp, w, bias, ovf], [B, H, W, in_cp, cin, cout, py, px], [w_scale], o=o)
 
-    def esr_prep_input(self, x, B, nz, h, w, sf, m, lr, first, first_cp, first_lr_off, zlr, zlr_cp, n_zlr, zhr,
-                       zhr_cp, n_zhr, split, stream):
+    def esr_prep_input_s(self, x, B, nz, h, w, sf, m, lr, first, first_cp, first_lr_off, zlr, zlr_cp, n_zlr, zhr,
+                         zhr_cp, n_zhr, split, act_scale, stream):
         return self._add(_lib.OP_PREP, [x, lr, first] + [zlr[k] for k in range(4)] + [zhr[k] for k in range(2)],
                          [B, nz, h, w, sf, m, first_cp, first_lr_off] + [zlr_cp[k] for k in range(4)] + [n_zlr] +
-                         [zhr_cp[k] for k in range(2)] + [n_zhr, split])
+                         [zhr_cp[k] for k in range(2)] + [n_zhr, split], [act_scale])
 
     def esr_cem_down(self, gen, lr, r, B, H, W, sf, ph, w, kd, negate, stream):
         return self._add(_lib.OP_CEM_DOWN, [gen, lr, r, w], [B, H, W, sf, ph, kd, negate])
@@ -564,18 +611,21 @@ USE_OP_LISTS = os.environ.get('ESR_OP_LISTS', '1') != '0'
 
 
 def _plan_key(net, x, cem, precision, pk):
+    a = act_scale(net) if precision == 'x3' else 1.0
     pre_pad = cem is not None and cem.pre_pad
     cem_key = None
     if cem is not None:
         cem_key = (id(cem), pre_pad, int(cem.margins_LR),
                    cem.DownscaleOP.Filter_OP.weight.data_ptr(), cem.Conv_LR_with_Inv_hTh_OP.Filter_OP.weight.data_ptr(),
                    cem.Upscale_OP.Filter_OP.weight.data_ptr())
-    return (id(pk), getattr(pk, 'version', 0), precision, tuple(x.shape), str(x.device), cem_key)
+    return (id(pk), getattr(pk, 'version', 0), precision, tuple(x.shape), str(x.device), cem_key, a)
 
 
 def _planned_forward(net, x, cem, precision):
     pk = _packed(net, net.latent_input is not None)
     key = _plan_key(net, x, cem, precision, pk)
+    if precision == 'x3':
+        pk.act_bias(act_scale(net))  # (no-op unless the parameters or the scale changed)
     plans = net._esr_cache.setdefault('plans', {})
     plan = plans.get(precision)
     if plan is None or plan.key != key:
@@ -612,6 +662,7 @@ def generator_forward(net, x, cem=None):
         if int(ws.overflow.item()):  # one 4-byte D2H per forward
             OVERFLOW_RERUNS += 1
             ws.overflow.zero_()
+            lower_act_scale(net)  # an activation (× the activation scale) left f16's range: smaller scale next time
             out, _ = _forward(net, x, cem, 'f32')
     return out
 
@@ -640,6 +691,10 @@ def _forward(net, x, cem, precision, train_ws=None, rec=None):
     ws = train_ws if train_ws is not None else _workspace(net, dev, Bn, H, W, latent, precision)
     pk = _packed(net, latent)
     _require_device(pk.first.bias, 'generator parameters')
+    A = act_scale(net) if x3 else 1.0
+    if x3:
+        pk.act_bias(A)
+    ws.act_scale = A
     stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     zc, cp, hcp = ws.zc, ws.cp, ws.hr_cp
     HR0, HR1 = ws.HR
@@ -665,9 +720,9 @@ def _forward(net, x, cem, precision, train_ws=None, rec=None):
         zlr = (ctypes.c_void_p * 4)(*([t.data_ptr() for t in grp] + [None] * (4 - len(grp))))
         zlr_cp = (ctypes.c_int32 * 4)(*([cp] * 4))
         first = gi == 0
-        _lib.check(lib.esr_prep_input(x.data_ptr(), Bn, nz, h, w, sf, m, ws.lr.data_ptr() if first else None,
-                                      ws.first.data_ptr() if first else None, ws.first_cp, ws.first_lr_off, zlr,
-                                      zlr_cp, len(grp), zhr, zhr_cp, 2 if (nz and first) else 0, int(x3), stream),
+        _lib.check(lib.esr_prep_input_s(x.data_ptr(), Bn, nz, h, w, sf, m, ws.lr.data_ptr() if first else None,
+                                        ws.first.data_ptr() if first else None, ws.first_cp, ws.first_lr_off, zlr,
+                                        zlr_cp, len(grp), zhr, zhr_cp, 2 if (nz and first) else 0, int(x3), A, stream),
                    'esr_prep_input')
     prof = _PROFILE
     tagp = 'x3_' if x3 else ''
@@ -682,8 +737,10 @@ def _forward(net, x, cem, precision, train_ws=None, rec=None):
             wx, scale = cw.x3()
             if rec is not None:  # the op list holds wx's pointer: keep it alive (train_x3 may swap cw._x3 later)
                 rec.keep.append(wx)
-            rc = lib.esr_conv3x3_fwd_x3(inp.data_ptr(), Bn, h_, w_, in_cp, cin, wx.data_ptr(), cw.bias.data_ptr(),
-                                        scale, cout, ctypes.byref(o), ovf, stream)
+            # activations carry × A: biases × A (bias_s); the planar HR_conv1 output is divided by A instead
+            wsc = scale * A if cw is pk.hr1 else scale
+            rc = lib.esr_conv3x3_fwd_x3(inp.data_ptr(), Bn, h_, w_, in_cp, cin, wx.data_ptr(), cw.bias_s.data_ptr(),
+                                        wsc, cout, ctypes.byref(o), ovf, stream)
         else:
             rc = lib.esr_conv3x3_fwd(inp.data_ptr(), Bn, h_, w_, in_cp, cin, cw.f32.data_ptr(), cw.bias.data_ptr(),
                                      cout, ctypes.byref(o), stream)
@@ -729,7 +786,8 @@ def _forward(net, x, cem, precision, train_ws=None, rec=None):
                 if rec is not None:
                     rec.keep.append(wx)
                 rc = lib.esr_upconv2x_phase_fwd_x3(src.data_ptr(), Bn, sh, sw, 64, 64, wx.data_ptr(),
-                                                   cw.bias.data_ptr(), scale, 64, ty, tx, ctypes.byref(o), ovf, stream)
+                                                   cw.bias_s.data_ptr(), scale, 64, ty, tx, ctypes.byref(o), ovf,
+                                                   stream)
             else:
                 rc = lib.esr_upconv2x_phase_fwd(src.data_ptr(), Bn, sh, sw, 64, 64, cw.f32.data_ptr(),
                                                 cw.bias.data_ptr(), 64, ty, tx, ctypes.byref(o), stream)

@@ -55,10 +55,12 @@ class DeferredOverflow:
     def __init__(self):
         self.flags = []   # device int32 scalars (activation / gradient overflow, weight out of its scale)
         self.resets = []  # (weight-flag tensor, callback resetting the x3 weight scales)
+        self.on_flag = []  # per flag: callback when it is set with no weight flag (forward: lower the activation scale)
 
-    def add(self, overflow, bad, reset):
+    def add(self, overflow, bad, reset, on_overflow=None):
         self.flags.append(overflow.clone())
         self.resets.append((bad.clone(), reset))
+        self.on_flag.append(on_overflow)
 
     def overflowed(self):
         """True if any deferred forward or backward overflowed (one device-to-host read; all-reduced over ranks)."""
@@ -74,6 +76,9 @@ class DeferredOverflow:
         for (_, reset), bad in zip(self.resets, vals[n:]):
             if bad:
                 reset()  # new x3 weight scales at the next x3 forward / backward
+        for cb, flag, bad in zip(self.on_flag, vals[:n], vals[n:]):
+            if cb is not None and flag and not bad:
+                cb()
         return any(v != 0 for v in vals)
 
 
@@ -355,6 +360,7 @@ class _Runner:
         self.need_params, self.need_input = need_params, need_input
         self.split = split  # forward activations in the split-f16 layout (x3 forward)
         self.x3 = None  # x3 backward: (per-RDB x3 fused weights, gradient-amax buffer, overflow flag)
+        self.act_scale = 1.0
 
     def dgrad(self, bc, src, src_cp, src_coff, cin_k, h, w, dst, dst_cp, dst_base, accumulate, res=None):
         """dst[:, n0-dst_base ...] (+)= conv(src slice, rot180 W^T) for every output slice; `res` = (buf, cp, coff)
@@ -415,7 +421,11 @@ class _Runner:
                                               bc.cout, self.B, h, w, splits, self.ws.partial.data_ptr(), self.stream),
                    'wgrad')
         dst = self.bp.dw.data_ptr() + 4 * bc.wg_off
-        if amax is None:
+        A = self.act_scale if self.split else 1.0
+        if A != 1.0:  # weights part x 1/A (the split activations hold A·v); the bias gradients do not read them
+            _lib.check(self.lib.esr_wgrad_reduce2(self.ws.partial.data_ptr(), splits, bc.wg_n, bc.wg_n - bc.cout_pad,
+                                                  scale / A, scale, amax, dst, self.stream), 'wgrad_reduce2')
+        elif amax is None:
             _lib.check(self.lib.esr_wgrad_reduce(self.ws.partial.data_ptr(), splits, bc.wg_n, scale, dst, self.stream),
                        'wgrad_reduce')
         else:
@@ -505,7 +515,8 @@ def _rdb_backward(R, P, dcat, convs, fused, zc, cp, H, W, dx):
     R.dgrad_fused(fused['x'], dcat, dcp, zc + 64, 192, H, W, dx[0], dx[1], dx[2], 64, res=(dcat, dcp, d4))
 
 
-def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_input=False, split=False, x3=False):
+def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_input=False, split=False, x3=False,
+                       act_scale=1.0):
     """dL/dparams of RRDBNet (+ CEM in train or eval mode) and/or dL/dinput given dL/dout.  x3 (with split, params
     only): the residual blocks' backward in the split-f16 scheme; ws.bwd_overflow then tells whether a scaled gradient
     or a weight left its f16 range (the caller reruns without x3).
@@ -514,6 +525,7 @@ def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_in
     stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     bp = _bwd_packed(net, latent)
     R = _Runner(ws, bp, stream, need_params, need_input, split)
+    R.act_scale = act_scale  # the forward's split activations hold A·v: weight gradients read them (x 1/A)
     lib = R.lib
     if x3:
         assert split and (need_params or need_input)
@@ -694,24 +706,30 @@ class _GeneratorFn(torch.autograd.Function):
         ws = _train_workspace(net, x.device, Bn, h + 2 * m, w + 2 * m, latent, prec)
         pk = E._packed(net, latent)  # parameter repack, outside any graph
         bad = pk.train_x3() if prec == 'x3' else None  # x3 weights refreshed in place, fixed per-layer scales
+        A = E.act_scale(net) if prec == 'x3' else 1.0  # activation scale of the x3 forward (engine.ACT_SCALE)
+        if prec == 'x3':
+            pk.act_bias(A)  # biases × A, outside any graph
 
         def fwd(xs):
             if prec == 'x3':
                 ws.overflow.copy_(bad)  # a weight outside its scale's safe range counts as an overflow
             return E._forward(net, xs, cem, prec, train_ws=ws)[0]
-        key = ('fwd', prec, tuple(x.shape), _cem_key(cem), id(pk), getattr(pk, '_tx3_epoch', 0))
+        key = ('fwd', prec, tuple(x.shape), _cem_key(cem), id(pk), getattr(pk, '_tx3_epoch', 0), A)
         xd = x.detach().contiguous()
         out, graphed = _run_graphed(ws, key, fwd, xd)
         split = prec == 'x3'
         if split and _DEFERRED[0] is not None:  # checked once after the whole training step (DeferredOverflow)
-            _DEFERRED[0].add(ws.overflow, bad, pk.reset_train_x3)
+            _DEFERRED[0].add(ws.overflow, bad, pk.reset_train_x3, lambda: E.lower_act_scale(net))
         elif split and int(ws.overflow.item()):  # an activation (or weight) beyond the f16 range: redo in exact fp32
             E.OVERFLOW_RERUNS += 1
             if int(bad.item()):
                 pk.reset_train_x3()  # new scales at the next x3 forward
+            else:
+                E.lower_act_scale(net)  # a scaled activation left f16's range: smaller activation scale next time
             ws = _train_workspace(net, x.device, Bn, h + 2 * m, w + 2 * m, latent, 'f32')
             out, graphed, split = E._forward(net, xd, cem, 'f32', train_ws=ws)[0], False, False
         ctx.net, ctx.cem, ctx.ws, ctx.latent, ctx.M, ctx.split = net, cem, ws, latent, E.SF * m, split
+        ctx.act_scale = A if split else 1.0  # (after an fp32 rerun the activations are unscaled)
         ctx.params = params
         ctx.owner = _Owner()
         ws.owner = weakref.ref(ctx.owner)
@@ -730,11 +748,11 @@ class _GeneratorFn(torch.autograd.Function):
 
         def run(x3):
             key = ('bwd', tuple(d_out.shape), _cem_key(ctx.cem), ctx.M, need_params, need_input, id(bp), ctx.split,
-                   x3)
+                   x3, ctx.act_scale)
             return _run_graphed(
                 ctx.ws, key, lambda g: generator_backward(ctx.net, ctx.cem, ctx.ws, g, ctx.latent, ctx.M,
                                                           need_params=need_params, need_input=need_input,
-                                                          split=ctx.split, x3=x3),
+                                                          split=ctx.split, x3=x3, act_scale=ctx.act_scale),
                 d_out.contiguous())
         (flat, dx), graphed = run(x3)
         if x3 and _DEFERRED[0] is not None:  # checked once after the whole training step (DeferredOverflow)

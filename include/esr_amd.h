@@ -96,6 +96,14 @@ int esr_prep_input(const float *x, int32_t B, int32_t nz, int32_t h, int32_t w, 
                    float *lr_nchw, float *first, int32_t first_cp, int32_t first_lr_off,
                    float *const *zlr_dst, const int32_t *zlr_cp, int32_t n_zlr,
                    float *const *zhr_dst, const int32_t *zhr_cp, int32_t n_zhr, int32_t split, esr_stream_t stream);
+/* esr_prep_input with the split outputs (split = 1) written as v × act_scale, a power of two (the x3 forward's
+ * activation scale: every split activation of an x3 forward holds A·v, so that small activations keep their f16 lo
+ * parts in the normal range; the x3 convs carry it through with their biases scaled by A and the planar HR_conv1 output
+ * divided by it).  The fp32 LR copy for CEM (lr_nchw) is never scaled. */
+int esr_prep_input_s(const float *x, int32_t B, int32_t nz, int32_t h, int32_t w, int32_t sf, int32_t m,
+                     float *lr_nchw, float *first, int32_t first_cp, int32_t first_lr_off, float *const *zlr_dst,
+                     const int32_t *zlr_cp, int32_t n_zlr, float *const *zhr_dst, const int32_t *zhr_cp,
+                     int32_t n_zhr, int32_t split, float act_scale, esr_stream_t stream);
 
 /* CEM step 1, fused DownscaleOP + LR residual (CEMnet.py:152,157-162,186-189):
  *   r[b,c,i,j] = (lr ? lr[b,c,i,j] : 0) - Σ_{u,v<kd} w_down[u][v] · gen[b,c, clamp(sf*i+ph+u-kd/2), clamp(sf*j+ph+v-kd/2)]
@@ -202,6 +210,11 @@ int esr_axpby_gs(void *out, int32_t o_cp, int32_t o_coff, int32_t o_split, float
                  int32_t x1_coff, int32_t x1_split, float b, const void *x2, int32_t x2_cp, int32_t x2_coff,
                  int32_t x2_split, int32_t C, int32_t B, int32_t H, int32_t W, const uint32_t *amax,
                  int32_t *overflow, esr_stream_t stream);
+/* esr_wgrad_reduce / _gs with two scales: out[i] = (i < n_w ? scale_w : scale_b) [/ S(amax) if amax] · Σ_s
+ * partial[s·n + i] — a conv's weights (first n_w entries) read activations of the x3 forward stored × its activation
+ * scale A (scale_w carries 1/A), its bias gradient (the rest) does not. */
+int esr_wgrad_reduce2(const float *partial, int32_t splits, int64_t n, int64_t n_w, float scale_w, float scale_b,
+                      const uint32_t *amax, float *out, esr_stream_t stream);
 /* out[i] = scale / S(amax) · Σ_s partial[s·n + i]: the weight gradient of a conv whose output gradient was scaled. */
 int esr_wgrad_reduce_gs(const float *partial, int32_t splits, int64_t n, float scale, const uint32_t *amax, float *out,
                         esr_stream_t stream);
