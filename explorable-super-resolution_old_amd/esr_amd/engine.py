@@ -729,10 +729,12 @@ def _forward(net, x, cem, precision, train_ws=None, rec=None):
 
     def conv(inp, h_, w_, in_cp, cin, cw, cout, o, cin_ref):
         ev = None
+        # timing tags: the N = 32 / 64 tile classes, and HR_conv1 (cout 3: the narrow-N kernel in x3) on its own
+        ntag = '%sconv3x3_n%d' % (tagp, 3 if cout <= 3 else (32 if cout <= 32 else 64))
         if rec is not None:
-            rec.tag('%sconv3x3_n%d' % (tagp, 32 if cout <= 32 else 64), 2.0 * Bn * h_ * w_ * 9 * cin_ref * cout)
+            rec.tag(ntag, 2.0 * Bn * h_ * w_ * 9 * cin_ref * cout)
         elif prof is not None:
-            ev = _prof_begin(prof, '%sconv3x3_n%d' % (tagp, 32 if cout <= 32 else 64), 2.0 * Bn * h_ * w_ * 9 * cin_ref * cout)
+            ev = _prof_begin(prof, ntag, 2.0 * Bn * h_ * w_ * 9 * cin_ref * cout)
         if x3:
             wx, scale = cw.x3()
             if rec is not None:  # the op list holds wx's pointer: keep it alive (train_x3 may swap cw._x3 later)

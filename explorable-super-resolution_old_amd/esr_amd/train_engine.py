@@ -39,6 +39,18 @@ DGRAD_X3 = os.environ.get('ESR_DGRAD_X3', '1') != '0'
 # with the x3 backward, also the trunk-level data gradients at 2x / 4x resolution (HR_conv0, the two upconvs) on the x3
 # conv, each at its own gradient scale (Runner.dgrad_trunk_x3); '0' keeps them exact fp32
 TRUNK_X3 = os.environ.get('ESR_TRUNK_X3', '1') != '0'
+# weight gradients on a second stream, overlapping the data-gradient chain they do not feed (each wgrad forks from the
+# main stream when its output gradient is ready; the main stream joins before it overwrites a buffer a pending wgrad
+# reads); '0' keeps one stream
+WGRAD_STREAM = os.environ.get('ESR_WGRAD_STREAM', '1') != '0'
+_SIDE = {}
+
+
+def _side_stream(dev):
+    st = _SIDE.get(dev)
+    if st is None:
+        st = _SIDE[dev] = torch.cuda.Stream(device=dev)
+    return st
 
 
 def _z(dev, *s):
@@ -361,6 +373,17 @@ class _Runner:
         self.split = split  # forward activations in the split-f16 layout (x3 forward)
         self.x3 = None  # x3 backward: (per-RDB x3 fused weights, gradient-amax buffer, overflow flag)
         self.act_scale = 1.0
+        self.side = None  # WGRAD_STREAM: (main torch stream, side torch stream, side stream handle)
+
+    def use_side_stream(self, dev):
+        main = torch.cuda.current_stream(dev)
+        side = _side_stream(dev)
+        self.side = (main, side, ctypes.c_void_p(side.cuda_stream))
+
+    def join(self):
+        """The main stream waits for every weight gradient issued so far (before it overwrites what they read)."""
+        if self.side is not None:
+            self.side[0].wait_stream(self.side[1])
 
     def dgrad(self, bc, src, src_cp, src_coff, cin_k, h, w, dst, dst_cp, dst_base, accumulate, res=None):
         """dst[:, n0-dst_base ...] (+)= conv(src slice, rot180 W^T) for every output slice; `res` = (buf, cp, coff)
@@ -417,20 +440,24 @@ class _Runner:
         splits = max(1, min(WG_SPLITS_MAX, (256 // chunks) if x3 else -(-1024 // chunks), ntiles))
         assert splits * bc.wg_n <= self.ws.partial.numel()
         flags = up2 | ((6 if x3 else 2) if self.split else 0) | (8 if amax is not None else 0)
+        st = self.stream
+        if self.side is not None:  # fork: the side stream sees everything issued on the main stream so far
+            self.side[1].wait_stream(self.side[0])
+            st = self.side[2]
         _lib.check(self.lib.esr_conv3x3_wgrad(inp.data_ptr(), in_cp, cin, flags, dout.data_ptr(), d_cp, d_coff,
-                                              bc.cout, self.B, h, w, splits, self.ws.partial.data_ptr(), self.stream),
+                                              bc.cout, self.B, h, w, splits, self.ws.partial.data_ptr(), st),
                    'wgrad')
         dst = self.bp.dw.data_ptr() + 4 * bc.wg_off
         A = self.act_scale if self.split else 1.0
         if A != 1.0:  # weights part x 1/A (the split activations hold A·v); the bias gradients do not read them
             _lib.check(self.lib.esr_wgrad_reduce2(self.ws.partial.data_ptr(), splits, bc.wg_n, bc.wg_n - bc.cout_pad,
-                                                  scale / A, scale, amax, dst, self.stream), 'wgrad_reduce2')
+                                                  scale / A, scale, amax, dst, st), 'wgrad_reduce2')
         elif amax is None:
-            _lib.check(self.lib.esr_wgrad_reduce(self.ws.partial.data_ptr(), splits, bc.wg_n, scale, dst, self.stream),
+            _lib.check(self.lib.esr_wgrad_reduce(self.ws.partial.data_ptr(), splits, bc.wg_n, scale, dst, st),
                        'wgrad_reduce')
         else:
             _lib.check(self.lib.esr_wgrad_reduce_gs(self.ws.partial.data_ptr(), splits, bc.wg_n, scale, amax, dst,
-                                                    self.stream), 'wgrad_reduce_gs')
+                                                    st), 'wgrad_reduce_gs')
 
     def dgrad_x3(self, wx, src, src_cp, src_coff, cin_k, h, w, dst, dst_cp, dst_coff, nw, res=None, mask=None):
         """dgrad_fused on the x3 conv: src / dst / res are split-f16 gradients at one scale (the conv is linear, so
@@ -495,6 +522,7 @@ def _rdb_backward_x3(R, P, dcat, convs, fx3, zc, cp, H, W, dx, amax, z_first=Fal
     if R.need_input and zc:
         R.dgrad_x3(fx3['z'], dcat, dcp, zc + 64, 192, H, W, R.ws.dzs, 8, 0, zc,
                    res=None if z_first else (R.ws.dzs, 8, 0))
+    R.join()  # dx's buffer is the previous block's concat gradient, which its pending weight gradients read
     R.dgrad_x3(fx3['x'], dcat, dcp, zc + 64, 192, H, W, dx[0], dx[1], dx[2], 64, res=(dcat, dcp, d4))
 
 
@@ -512,6 +540,7 @@ def _rdb_backward(R, P, dcat, convs, fused, zc, cp, H, W, dx):
         R.wgrad(convs[m - 1], P, cp, t, 0, dcat, dcp, t, H, W)
     if R.need_input and zc:
         R.dgrad_fused(fused['z'], dcat, dcp, zc + 64, 192, H, W, R.ws.dZl, 8, 0, zc, res='acc')
+    R.join()  # dx's buffer is the previous block's concat gradient, which its pending weight gradients read
     R.dgrad_fused(fused['x'], dcat, dcp, zc + 64, 192, H, W, dx[0], dx[1], dx[2], 64, res=(dcat, dcp, d4))
 
 
@@ -526,6 +555,8 @@ def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_in
     bp = _bwd_packed(net, latent)
     R = _Runner(ws, bp, stream, need_params, need_input, split)
     R.act_scale = act_scale  # the forward's split activations hold A·v: weight gradients read them (x 1/A)
+    if WGRAD_STREAM and need_params:
+        R.use_side_stream(dev)
     lib = R.lib
     if x3:
         assert split and (need_params or need_input)
@@ -576,6 +607,7 @@ def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_in
     R.wgrad(bp.hr0, HR0, hcp, hcp, 0, dA, 64, 0, HH, WW)
     # the trunk-level data gradients at 2x / 4x on the x3 conv when the backward is x3 (TRUNK_X3), else exact fp32
     tx3 = x3 and TRUNK_X3
+    R.join()  # (each trunk data gradient below overwrites buffers that the weight gradient before it reads)
     if tx3:
         R.dgrad_trunk_x3('hr0', bp.hr0, dA, HH, WW, dB, zc, dB, dA, net.nb, dz=(ws.dZh, 8, ws.dgen_p) if zc else None)
     else:
@@ -584,6 +616,7 @@ def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_in
     # upconv 2: HR0.x = lrelu(conv(nearest2(U1)))
     R.lrelu(dB, 64, 0, HR0, hcp, zc, 64, HH, WW)
     R.wgrad(bp.up[1], ws.U1, 64, 64, 1, dB, 64, 0, HH, WW)
+    R.join()
     if tx3:
         R.dgrad_trunk_x3('up1', bp.up[1], dB, HH, WW, dA, 0, dA, dB, net.nb + 1)
     else:
@@ -592,6 +625,7 @@ def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_in
     # upconv 1: U1 = lrelu(conv(nearest2(U0)))
     R.lrelu(ws.dU1, 64, 0, ws.U1, 64, 0, 64, 2 * H, 2 * W)
     R.wgrad(bp.up[0], ws.U0, 64, 64, 1, ws.dU1, 64, 0, 2 * H, 2 * W)
+    R.join()
     if tx3:
         R.dgrad_trunk_x3('up0', bp.up[0], ws.dU1, 2 * H, 2 * W, ws.dUp1, 0, ws.dUp1, ws.dU1, net.nb + 2)
     else:
@@ -607,6 +641,7 @@ def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_in
     D0, D1 = ws.D
     dcp, d4 = ws.dcp, zc + 192
     for k in reversed(range(net.nb)):
+        R.join()  # D0 / D1 are about to be rewritten: the previous RRDB's weight gradients read them
         if x3:  # gradient scale of this RRDB from max |trunk gradient| at its output
             amax = ws.gamax.data_ptr() + 4 * k
             ovf = ws.bwd_overflow.data_ptr()
@@ -629,6 +664,7 @@ def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_in
     # conv_first: dL/dfea = trunk gradient + LR_conv skip
     R.axpby(ws.GA, 64, 0, 1.0, ws.GA, 64, 0, 1.0, ws.dU0, 64, 0, C=64, h=H, w=W)
     R.wgrad(bp.first, ws.first, ws.first_cp, ws.first_cp, 0, ws.GA, 64, 0, H, W)
+    R.join()
     flat = bp.dw.index_select(0, bp.gidx) if need_params else None  # all parameter gradients, reference layout
     dx = None
     if need_input:

@@ -93,6 +93,47 @@ def test_training_step_is_deterministic(gpu_device):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize('nb,latent', [(1, False), (2, True)])
+def test_side_stream_weight_gradients_bitwise(gpu_device, nb, latent):
+    """Weight gradients on the second stream (train_engine.WGRAD_STREAM, overlapping the data-gradient chain) give
+    the same parameter gradients, bit for bit, as the one-stream backward, eagerly and through the captured HIP graphs
+    (calls 2 and 3), in x3 and in exact fp32."""
+    from esr_amd import engine, train_engine as TE
+    from oracle.recipe import seeded_inputs, seeded_params
+    B, h, w = 2, 12, 16
+    net = esr_amd.RRDBNet(3, 3, 64, nb, latent_input='all_layers_HR_downscaled' if latent else None,
+                          num_latent_channels=3 if latent else 0)
+    sd = net.state_dict()
+    params = seeded_params([(k, tuple(v.shape)) for k, v in sd.items()], 91, w_scale=0.5)
+    lr, z = seeded_inputs(92, (B, 3, h, w), (B, 3, 4 * h, 4 * w), z_mode='pixel')
+    x = torch.from_numpy(lr)
+    if latent:
+        x = torch.cat([torch.from_numpy(z).view(B, 48, h, w), x], 1)
+    R = torch.from_numpy(np.random.default_rng(93).standard_normal((B, 3, 4 * h, 4 * w)).astype(np.float32))
+    prev = TE.WGRAD_STREAM
+    try:
+        for prec in ('x3', 'f32'):
+            runs = []
+            for side in (True, False):
+                TE.WGRAD_STREAM = side
+                m = esr_amd.RRDBNet(3, 3, 64, nb, latent_input='all_layers_HR_downscaled' if latent else None,
+                                    num_latent_channels=3 if latent else 0)
+                m.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=False)
+                m = m.to(gpu_device)
+                engine.set_precision(m, prec)
+                calls = []
+                for _ in range(3):  # eager, capture, replay
+                    m.zero_grad()
+                    (m(x.to(gpu_device)) * R.to(gpu_device)).sum().backward()
+                    calls.append([q.grad.clone() for q in m.parameters()])
+                runs.append(calls)
+            for c in range(3):
+                for a, b in zip(runs[0][c], runs[1][c]):
+                    assert torch.equal(a, b), (prec, c)
+    finally:
+        TE.WGRAD_STREAM = prev
+
+
 def test_optimize_parameters_training_step(gpu_device):
     """SRRaGANModel.optimize_parameters on the HIP generator: D step (WGAN-GP) every step, G step from step 1 on;
     both networks move, losses are finite, the generator output keeps the reference shape contract."""

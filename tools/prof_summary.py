@@ -29,6 +29,8 @@ def tag(name, lds):
     name = name.replace('void (anonymous namespace)::', '')
     if name.startswith('conv_x3_ring_kernel'):
         return 'x3_conv3x3_n32'
+    if name.startswith('conv_x3_narrow_kernel'):  # HR_conv1 (cout 3, planar): its own tag, as bench.py's
+        return 'x3_conv3x3_n3'
     if name.startswith('conv_fwd_kernel'):
         return LDS_TAGS.get(int(lds), 'conv_fwd_kernel[lds=%s]' % lds)
     if name.startswith('conv_x3_kernel'):
