@@ -41,8 +41,9 @@ DGRAD_X3 = os.environ.get('ESR_DGRAD_X3', '1') != '0'
 TRUNK_X3 = os.environ.get('ESR_TRUNK_X3', '1') != '0'
 # weight gradients on a second stream, overlapping the data-gradient chain they do not feed (each wgrad forks from the
 # main stream when its output gradient is ready; the main stream joins before it overwrites a buffer a pending wgrad
-# reads); '0' keeps one stream
-WGRAD_STREAM = os.environ.get('ESR_WGRAD_STREAM', '1') != '0'
+# reads).  Opt-in ('1'): on one box, order-balanced, the config-3 step took 159.8 ms with it and 156.3 ms without
+# (profiles/r3_ab_stream.txt) — the concurrent kernels share the CUs and each runs longer than the overlap saves.
+WGRAD_STREAM = os.environ.get('ESR_WGRAD_STREAM', '0') == '1'
 _SIDE = {}
 
 
