@@ -283,4 +283,4 @@ extern "C" int esr_conv_set_tile(int32_t rows) {
     return prev;
 }
 
-extern "C" int esr_abi_version(void) { return 13; }
+extern "C" int esr_abi_version(void) { return 14; }

@@ -1175,19 +1175,18 @@ __global__ __launch_bounds__(NR_THR, 2) void conv_x3_narrow_kernel(X3Params p) {
     }
     // B fragments of input row i (tall padded row r0 - 1 + i): pixel column x0 + ml, channels 16 j + 8 hl .. +8
     const int gx = x0 + ml;
+    // Branch-free, so that the compiler counts the loads in flight (s_waitcnt vmcnt(N)) instead of draining them all at
+    // the first MFMA: a lane past the image reads the clamped last row / column (its Y column is never summed into an
+    // output), a channel group past cin reads group 0 of the same pixel (finite; its A rows are zero)
+    const int gxc = min(gx, p.W + 1);
     auto load_row = [&](int i, f16x8 (&bh)[NCH], f16x8 (&bl)[NCH]) {
-        const int gy = r0 - 1 + i;
-        const bool ok = gy < rows_tot && gx < p.W + 2;
-        const unsigned char *src = p.in + (gy * rowp + gx) * pixb + 32 * hl;
+        const int gy = min(r0 - 1 + i, rows_tot - 1);
+        const unsigned char *src = p.in + ((long long)gy * rowp + gxc) * pixb + 32 * hl;
 #pragma unroll
         for (int j = 0; j < NCH; ++j) {
-            if (ok && 16 * j + 8 * hl < p.cin) {
-                bh[j] = *reinterpret_cast<const f16x8 *>(src + 64 * j);
-                bl[j] = *reinterpret_cast<const f16x8 *>(src + 64 * j + 16);
-            } else {
-                bh[j] = f16x8{};
-                bl[j] = f16x8{};
-            }
+            const unsigned char *s = src + (16 * j + 8 * hl < p.cin ? 64 * j : 0);
+            bh[j] = *reinterpret_cast<const f16x8 *>(s);
+            bl[j] = *reinterpret_cast<const f16x8 *>(s + 16);
         }
     };
     auto compute_row = [&](int i, const f16x8 (&bh)[NCH], const f16x8 (&bl)[NCH]) {
@@ -1205,18 +1204,18 @@ __global__ __launch_bounds__(NR_THR, 2) void conv_x3_narrow_kernel(X3Params p) {
             if (m < NR_M) ys[(i * NR_M + m) * 32 + ml] = c[r];
         }
     };
-    f16x8 bh0[NCH], bl0[NCH], bh1[NCH], bl1[NCH];
-    int i = wave;
-    load_row(i, bh0, bl0);
-    while (i < NR_IN) {  // rows wave, wave + 4, ... (wave-uniform bounds); two rows per trip, next row loaded early
-        const int i1 = i + 4;
-        if (i1 < NR_IN) load_row(i1, bh1, bl1);
-        compute_row(i, bh0, bl0);
-        if (i1 >= NR_IN) break;
-        const int i2 = i1 + 4;
-        if (i2 < NR_IN) load_row(i2, bh0, bl0);
-        compute_row(i1, bh1, bl1);
-        i = i2;
+    // rows wave, wave + 4, ... (wave-uniform bounds), PF of them in flight: with one row ahead a CU held ~32 KB of
+    // loads in flight, about half what HBM's latency-bandwidth product asks for
+    constexpr int RPW = (NR_IN + 3) / 4, PF = NCH <= 4 ? RPW : 3;
+    // (loads unconditional — a wave's row past NR_IN reads a clamped row and is not computed — so that no branch
+    // makes the waitcnt pass assume the worst)
+    f16x8 bh[PF][NCH], bl[PF][NCH];
+#pragma unroll
+    for (int k = 0; k < PF; ++k) load_row(wave + 4 * k, bh[k], bl[k]);
+#pragma unroll
+    for (int k = 0; k < RPW; ++k) {
+        if (wave + 4 * k < NR_IN) compute_row(wave + 4 * k, bh[k % PF], bl[k % PF]);
+        if (k + PF < RPW) load_row(wave + 4 * (k + PF), bh[k % PF], bl[k % PF]);
     }
     __syncthreads();
     // out[o][y][x] = (Σ_{ky, kx} Y[3 (3 ky + kx) + o] at input row + ky, column + kx) / w_scale + bias
@@ -1352,8 +1351,8 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
             return x3c_launch(c, taps_side, stream, 128);
 #ifdef ESR_X3_EXPERIMENTS  // 51-54: x3c ablations, 55-59: the warp-specialised persistent form and its ablations
         static const int dbg[5] = {0, 1, 2, 4, 5};
-        if (g_x3_kernel >= 55) return x3s_launch(c, taps_side, stream, dbg[g_x3_kernel - 55]);
-        return x3c_launch(c, taps_side, stream, dbg[g_x3_kernel - 50]);
+        if (g_x3_kernel >= 55 && g_x3_kernel <= 59) return x3s_launch(c, taps_side, stream, dbg[g_x3_kernel - 55]);
+        return x3c_launch(c, taps_side, stream, g_x3_kernel >= 50 && g_x3_kernel <= 54 ? dbg[g_x3_kernel - 50] : 0);
 #else
         return x3c_launch(c, taps_side, stream, 0);
 #endif

@@ -63,6 +63,8 @@ struct FwdParams {
     int T;
     int offy[MAXT], offx[MAXT];
     float *partial;  // split-K (x3 kernel, gridDim.z > 1): [z][M][n_pad] raw sums, reduced by dconv_splitk_reduce
+    int s2c, s2pad;  // > 0: space-to-depth source (src_quad); 0: plain
+    int d2c, d2pad;  // > 0: depth-to-space output (put_out); 0: plain
 };
 
 __device__ __forceinline__ f32x4 load4(const float *row, int c, int kc, bool vec) {
@@ -72,6 +74,40 @@ __device__ __forceinline__ f32x4 load4(const float *row, int c, int kc, bool vec
     for (int e = 0; e < 4; ++e)
         if (c + e < kc) v[e] = row[c + e];
     return v;
+}
+
+// The 4-channel quad from channel c of gather point (sy, sx) of image b; zero outside the image (the conv's padding).
+// s2c > 0: the source is the space-to-depth view of a stride-2 conv's input (esr_dconv_fwd_sd): virtual channel
+// c = (2·py + px)·s2c + c' of virtual pixel (sy, sx) is channel c' of real pixel (2·sy + py - s2pad, 2·sx + px - s2pad)
+// of the [B][Hs][Ws][sp] source (s2c % 4 == 0, so a quad never straddles two phases).
+__device__ __forceinline__ f32x4 src_quad(const FwdParams &p, int b, int sy, int sx, int c, bool vec) {
+    int kc = p.kc;
+    if (p.s2c) {
+        const int ph = c / p.s2c;
+        c -= ph * p.s2c;
+        sy = 2 * sy + (ph >> 1) - p.s2pad;
+        sx = 2 * sx + (ph & 1) - p.s2pad;
+        kc = ph < 4 ? p.s2c : 0;
+    }
+    if (c < kc && sy >= 0 && sy < p.Hs && sx >= 0 && sx < p.Ws)
+        return load4(p.src + (((long long)b * p.Hs + sy) * p.Ws + sx) * p.sp, c, kc, vec);
+    return f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+// out at output grid point (Y, X), channel n.  d2c > 0: depth-to-space (the data gradient of a stride-2 conv in its
+// space-to-depth form): channel n = (2·py + px)·d2c + c' of grid point (Y, X) is channel c' of real pixel
+// (2·(omy·Y + oay) + py - d2pad, 2·(omx·X + oax) + px - d2pad); pixels outside [0, Ho) × [0, Wo) (the padding
+// border) are dropped.
+__device__ __forceinline__ void put_out(const FwdParams &p, int b, int Y, int X, int n, float v) {
+    int oy = p.omy * Y + p.oay, ox = p.omx * X + p.oax;
+    if (p.d2c) {
+        const int ph = n / p.d2c;
+        n -= ph * p.d2c;
+        oy = 2 * oy + (ph >> 1) - p.d2pad;
+        ox = 2 * ox + (ph & 1) - p.d2pad;
+        if (oy < 0 || oy >= p.Ho || ox < 0 || ox >= p.Wo) return;
+    }
+    p.out[(((long long)b * p.Ho + oy) * p.Wo + ox) * p.op + n] = v;
 }
 
 __global__ __launch_bounds__(NTH, 2) void dconv_fwd_kernel(FwdParams p) {
@@ -108,9 +144,7 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_kernel(FwdParams p) {
 #pragma unroll
         for (int k = 0; k < A_IT; ++k) {
             f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            const int sy = p.smy * py[k] + oy, sx = p.smx * px[k] + ox;
-            if (pb[k] >= 0 && c < p.kc && sy >= 0 && sy < p.Hs && sx >= 0 && sx < p.Ws)
-                v = load4(p.src + (((long long)pb[k] * p.Hs + sy) * p.Ws + sx) * p.sp, c, p.kc, vec);
+            if (pb[k] >= 0) v = src_quad(p, pb[k], p.smy * py[k] + oy, p.smx * px[k] + ox, c, vec);
             ra[k] = v;
         }
         const float *wj = p.w + ((long long)(t * p.nck + j) * p.n_pad + n0) * KC;
@@ -175,8 +209,7 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_kernel(FwdParams p) {
                 if (m >= M) continue;
                 const int b = (int)(m / per_img), rr = (int)(m - (long long)b * per_img);
                 const int Y = rr / p.MW, X = rr - (rr / p.MW) * p.MW;
-                const int oy = p.omy * Y + p.oay, ox = p.omx * X + p.oax;
-                p.out[(((long long)b * p.Ho + oy) * p.Wo + ox) * p.op + n] = acc[mt][nt][r] + bn;
+                put_out(p, b, Y, X, n, acc[mt][nt][r] + bn);
             }
     }
 }
@@ -229,7 +262,6 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_halo_kernel(FwdParams p, Hal
     // the halo window of chunk j: every thread stages (pixel, 4-channel quad) items, 8 loads in flight at a time
     auto stage_a = [&](int j) {
         const int total = h.IY * h.IXt * 8;
-        const float *img = p.src + (long long)b * p.Hs * p.Ws * p.sp;
         for (int base = 0; base < total; base += 8 * NTH) {
             f32x4 v[8];
 #pragma unroll
@@ -240,9 +272,7 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_halo_kernel(FwdParams p, Hal
                     const int pix = idx >> 3, q = idx & 7;
                     const int r = pix / h.IXt, cc = pix - r * h.IXt;
                     const int par = cc / h.IXp, hc = cc - par * h.IXp;
-                    const int sy = sy0 + r, sx = sx0 + hc * h.npar + par, c = j * KC + 4 * q;
-                    if (sy >= 0 && sy < p.Hs && sx >= 0 && sx < p.Ws && c < p.kc)
-                        v[u] = load4(img + ((long long)sy * p.Ws + sx) * p.sp, c, p.kc, vec);
+                    v[u] = src_quad(p, b, sy0 + r, sx0 + hc * h.npar + par, j * KC + 4 * q, vec);
                 }
             }
 #pragma unroll
@@ -319,13 +349,10 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_halo_kernel(FwdParams p, Hal
             }
             if (n >= p.n) continue;
             const float bn = p.bias ? p.bias[n] : 0.f;
-            const int oy = p.omy * Y + p.oay;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int X = X0 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-                if (X >= p.MW) continue;
-                const int ox = p.omx * X + p.oax;
-                p.out[(((long long)b * p.Ho + oy) * p.Wo + ox) * p.op + n] = acc[i][k][r] + bn;
+                if (X < p.MW) put_out(p, b, Y, X, n, acc[i][k][r] + bn);
             }
         }
     }
@@ -396,9 +423,7 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_x3_kernel(FwdParams p) {
 #pragma unroll
         for (int k = 0; k < A_IT; ++k) {
             f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            const int sy = p.smy * py[k] + oy, sx = p.smx * px[k] + ox;
-            if (pb[k] >= 0 && c < p.kc && sy >= 0 && sy < p.Hs && sx >= 0 && sx < p.Ws)
-                v = load4(p.src + (((long long)pb[k] * p.Hs + sy) * p.Ws + sx) * p.sp, c, p.kc, vec);
+            if (pb[k] >= 0) v = src_quad(p, pb[k], p.smy * py[k] + oy, p.smx * px[k] + ox, c, vec);
             ra[k] = v;
         }
         const float *wj = p.w + ((long long)(t * p.nck + j) * p.n_pad + n0) * KC;
@@ -539,8 +564,7 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_x3_kernel(FwdParams p) {
                 if (m >= M) continue;
                 const int b = (int)(m / per_img), rr = (int)(m - (long long)b * per_img);
                 const int Y = rr / p.MW, X = rr - (rr / p.MW) * p.MW;
-                const int oy = p.omy * Y + p.oay, ox = p.omx * X + p.oax;
-                p.out[(((long long)b * p.Ho + oy) * p.Wo + ox) * p.op + n] = ldexpf(acc[mt][nt][r], -(ea + eb)) + bn;
+                put_out(p, b, Y, X, n, ldexpf(acc[mt][nt][r], -(ea + eb)) + bn);
             }
     }
 }
@@ -571,7 +595,6 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_halo_x_kernel(FwdParams p, H
     const int c_begin = (int)((long long)p.nck * blockIdx.z / gridDim.z);
     const int c_end = (int)((long long)p.nck * (blockIdx.z + 1) / gridDim.z);
     const int nsteps = (c_end - c_begin) * p.T;
-    const float *img = p.src + (long long)b * p.Hs * p.Ws * p.sp;
 
     auto split_put = [&](unsigned char *row, int q, f32x4 v, float sc) {  // 4 channels at quad q of a staged row
         f16x4 hi, lo, lo2;
@@ -591,10 +614,7 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_halo_x_kernel(FwdParams p, H
         const int pix = idx >> 3, q = idx & 7;
         const int r = pix / h.IXt, cc = pix - r * h.IXt;
         const int par = cc / h.IXp, hc = cc - par * h.IXp;
-        const int sy = sy0 + r, sx = sx0 + hc * h.npar + par, c = j * KC + 4 * q;
-        if (sy >= 0 && sy < p.Hs && sx >= 0 && sx < p.Ws && c < p.kc)
-            return load4(img + ((long long)sy * p.Ws + sx) * p.sp, c, p.kc, vec);
-        return f32x4{0.f, 0.f, 0.f, 0.f};
+        return src_quad(p, b, sy0 + r, sx0 + hc * h.npar + par, j * KC + 4 * q, vec);
     };
     auto wave_max = [&](float m) {
 #pragma unroll
@@ -759,13 +779,10 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_halo_x_kernel(FwdParams p, H
             }
             if (n >= p.n) continue;
             const float bn = p.bias ? p.bias[n] : 0.f;
-            const int oy = p.omy * Y + p.oay;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int X = X0 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-                if (X >= p.MW) continue;
-                const int ox = p.omx * X + p.oax;
-                p.out[(((long long)b * p.Ho + oy) * p.Wo + ox) * p.op + n] = ldexpf(acc[i][k][r], ue) + bn;
+                if (X < p.MW) put_out(p, b, Y, X, n, ldexpf(acc[i][k][r], ue) + bn);
             }
         }
     }
@@ -783,8 +800,7 @@ __global__ void dconv_splitk_reduce(FwdParams p, int ksplit) {
     const int per_img = p.MH * p.MW;
     const int b = (int)(m / per_img), rr = (int)(m - (long long)b * per_img);
     const int Y = rr / p.MW, X = rr - Y * p.MW;
-    const int oy = p.omy * Y + p.oay, ox = p.omx * X + p.oax;
-    p.out[(((long long)b * p.Ho + oy) * p.Wo + ox) * p.op + n] = v + (p.bias ? p.bias[n] : 0.f);
+    put_out(p, b, Y, X, n, v + (p.bias ? p.bias[n] : 0.f));
 }
 
 // ---- weight gradient ------------------------------------------------------------------------------------------------
@@ -1353,9 +1369,15 @@ constexpr int HALO_LDS_MAX = 160 * 1024;
 // (tools/dconv_ab.py, profiles/r3_dconv_ab.txt): the 4×4 stride-2 forward and the 2×2-tap phase classes of its data
 // gradient ran slower than the gather kernel (their source window is 4-6× the outputs), and so did the 8×8 layer's
 // data gradient on its 38-wide grid (two tiles for 38 columns).
-bool halo_wanted(int smy, int smx, int T, int MW) {
+// The 2×2-tap stride-1 form of a 4×4 stride-2 conv over its space-to-depth source / into its depth-to-space output
+// (sd: esr_dconv_fwd_sd) stages each source pixel once per 32 virtual channels — 8 real channels × 4 phases — so its
+// window fits 8-row tiles at two workgroups per CU; it takes the halo kernel under the same width rule.
+int g_dconv_halo = 1; // esr_dconv_set_halo: the halo-tile kernels where they apply (halo_wanted), every precision;
+                      // 2 = also the space-to-depth forms at any width (A/B)
+bool halo_wanted(int smy, int smx, int T, int MW, bool sd = false) {
     const int covered = 32 * ((MW + 31) / 32);
-    return smy == 1 && smx == 1 && (T == 1 || T >= 9) && 10 * (covered - MW) <= 3 * MW;
+    if (g_dconv_halo == 2 && sd && smy == 1 && smx == 1) return true;
+    return smy == 1 && smx == 1 && (T == 1 || T >= 9 || sd) && 10 * (covered - MW) <= 3 * MW;
 }
 
 // Halo tiling of an esr_dconv_fwd launch with `pitch` LDS bytes per staged pixel row (144: fp32 / x3, 208: x6):
@@ -1482,25 +1504,34 @@ int g_dconv_rows = 0; // esr_dconv_set_rows: the tap-row weight-gradient kernel 
                       // kernel at config 3 with one resident workgroup per CU, profiles/r3_dconv_ab.txt)
 
 int g_dconv_x3 = 0;   // esr_dconv_set_x3
-int g_dconv_halo = 1; // esr_dconv_set_halo: the halo-tile kernels where they apply (halo_wanted), every precision
 int g_dconv_np = 2;   // split pieces of the x3 kernels: 2 = x3, 3 = x6 (esr_dconv_set_x3(3))
 int g_dconv_nb = 128; // x3: widest N tile allowed (esr_dconv_set_x3(2) = 64 only, for A/B)
 
-extern "C" int esr_dconv_fwd_sk(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t src_pitch, int32_t kc,
+extern "C" int esr_dconv_fwd_sd(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t src_pitch, int32_t kc,
                                 const float *w_packed, int32_t nck, int32_t n_pad, const float *bias, float *out,
                                 int32_t Ho, int32_t Wo, int32_t out_pitch, int32_t n, int32_t MH, int32_t MW,
                                 int32_t omy, int32_t oay, int32_t omx, int32_t oax, int32_t smy, int32_t smx, int32_t T,
-                                const int32_t *offy, const int32_t *offx, int32_t ksplit, float *partial,
-                                esr_stream_t stream) {
+                                const int32_t *offy, const int32_t *offx, int32_t ksplit, float *partial, int32_t s2d_c,
+                                int32_t s2d_pad, int32_t d2s_c, int32_t d2s_pad, esr_stream_t stream) {
     if (!src || !w_packed || !out || !offy || !offx) return ESR_EINVAL;
     if (ksplit < 1 || (ksplit > 1 && (!partial || ksplit > T * nck))) return ESR_EINVAL;
-    if (B <= 0 || Hs <= 0 || Ws <= 0 || kc <= 0 || src_pitch < kc || n <= 0 || out_pitch < n || MH <= 0 || MW <= 0)
+    if (s2d_c < 0 || d2s_c < 0 || s2d_pad < 0 || d2s_pad < 0) return ESR_EINVAL;
+    const int src_c = s2d_c ? s2d_c : kc, out_c = d2s_c ? d2s_c : n;  // real channels per source / output pixel
+    if (B <= 0 || Hs <= 0 || Ws <= 0 || kc <= 0 || src_pitch < src_c || n <= 0 || out_pitch < out_c || MH <= 0 ||
+        MW <= 0)
         return ESR_EINVAL;
     if (T <= 0 || T > ESR_DCONV_MAX_TAPS || nck != (kc + KC - 1) / KC || n_pad % NB || n_pad < n) return ESR_EINVAL;
     if (!aligned16(w_packed)) return ESR_EINVAL;
-    // every output pixel the grid writes must lie inside the output tensor
-    if (oay < 0 || oax < 0 || omy * (MH - 1) + oay >= Ho || omx * (MW - 1) + oax >= Wo) return ESR_EINVAL;
+    if (s2d_c && (s2d_c % 4 || kc != 4 * s2d_c)) return ESR_EINVAL;
+    if (d2s_c) {  // every grid point maps to at least one real pixel; the bias would be per virtual channel
+        if (n != 4 * d2s_c || bias || omy != 1 || omx != 1 || oay || oax) return ESR_EINVAL;
+        if (2 * (MH - 1) - d2s_pad >= Ho || 2 * (MW - 1) - d2s_pad >= Wo) return ESR_EINVAL;
+    } else if (oay < 0 || oax < 0 || omy * (MH - 1) + oay >= Ho || omx * (MW - 1) + oax >= Wo) {
+        return ESR_EINVAL;  // every output pixel the grid writes must lie inside the output tensor
+    }
+    const bool sd = s2d_c || d2s_c;
     FwdParams p;
+    p.s2c = s2d_c; p.s2pad = s2d_pad; p.d2c = d2s_c; p.d2pad = d2s_pad;
     p.src = src; p.B = B; p.Hs = Hs; p.Ws = Ws; p.sp = src_pitch; p.kc = kc;
     p.vec = (src_pitch % 4 == 0 && aligned16(src)) ? 1 : 0;
     p.w = w_packed; p.nck = nck; p.n_pad = n_pad; p.bias = bias;
@@ -1515,7 +1546,7 @@ extern "C" int esr_dconv_fwd_sk(const float *src, int32_t B, int32_t Hs, int32_t
     HaloParams h;
     int lds = 0;
     const int np = g_dconv_x3 ? g_dconv_np : 0;
-    if (g_dconv_halo && halo_wanted(smy, smx, T, MW) &&
+    if (g_dconv_halo && halo_wanted(smy, smx, T, MW, sd) &&
         halo_plan(MH, MW, smy, smx, T, offy, offx, h, lds, np == 3 ? XPitch<3>::v : PS * 4)) {
         if (ksplit > nck) return ESR_EINVAL;  // the halo kernels split the channel chunks
         const long long hx = (long long)B * h.tiles_x * h.tiles_y;
@@ -1562,6 +1593,16 @@ extern "C" int esr_dconv_fwd_sk(const float *src, int32_t B, int32_t Hs, int32_t
     return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
 }
 
+extern "C" int esr_dconv_fwd_sk(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t src_pitch, int32_t kc,
+                                const float *w_packed, int32_t nck, int32_t n_pad, const float *bias, float *out,
+                                int32_t Ho, int32_t Wo, int32_t out_pitch, int32_t n, int32_t MH, int32_t MW,
+                                int32_t omy, int32_t oay, int32_t omx, int32_t oax, int32_t smy, int32_t smx, int32_t T,
+                                const int32_t *offy, const int32_t *offx, int32_t ksplit, float *partial,
+                                esr_stream_t stream) {
+    return esr_dconv_fwd_sd(src, B, Hs, Ws, src_pitch, kc, w_packed, nck, n_pad, bias, out, Ho, Wo, out_pitch, n, MH,
+                            MW, omy, oay, omx, oax, smy, smx, T, offy, offx, ksplit, partial, 0, 0, 0, 0, stream);
+}
+
 extern "C" int esr_dconv_fwd(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t src_pitch, int32_t kc,
                              const float *w_packed, int32_t nck, int32_t n_pad, const float *bias, float *out,
                              int32_t Ho, int32_t Wo, int32_t out_pitch, int32_t n, int32_t MH, int32_t MW, int32_t omy,
@@ -1571,15 +1612,15 @@ extern "C" int esr_dconv_fwd(const float *src, int32_t B, int32_t Hs, int32_t Ws
                             MW, omy, oay, omx, oax, smy, smx, T, offy, offx, 1, nullptr, stream);
 }
 
-extern "C" int esr_dconv_fwd_splits(int32_t B, int32_t MH, int32_t MW, int32_t n, int32_t kc, int32_t smy,
-                                    int32_t smx, int32_t T, const int32_t *offy, const int32_t *offx) {
+extern "C" int esr_dconv_fwd_splits_sd(int32_t B, int32_t MH, int32_t MW, int32_t n, int32_t kc, int32_t smy,
+                                       int32_t smx, int32_t T, const int32_t *offy, const int32_t *offx, int32_t sd) {
     if (B <= 0 || MH <= 0 || MW <= 0 || n <= 0 || kc <= 0 || T <= 0 || T > ESR_DCONV_MAX_TAPS || !offy || !offx)
         return ESR_EINVAL;
     const int nck = (kc + KC - 1) / KC, n_pad = NB * ((n + NB - 1) / NB);
     HaloParams h;
     int lds = 0;
     const int np = g_dconv_x3 ? g_dconv_np : 0;
-    if (g_dconv_halo && halo_wanted(smy, smx, T, MW) &&
+    if (g_dconv_halo && halo_wanted(smy, smx, T, MW, sd != 0) &&
         halo_plan(MH, MW, smy, smx, T, offy, offx, h, lds, np == 3 ? XPitch<3>::v : PS * 4))
         return halo_splits(h, B, n_pad, nck);
     if (!g_dconv_x3) return 1;
@@ -1588,6 +1629,16 @@ extern "C" int esr_dconv_fwd_splits(int32_t B, int32_t MH, int32_t MW, int32_t n
     const int nsteps = T * nck;
     if (wgs >= 512 || nsteps < 16) return 1;
     return (int)max(1LL, min((512 + wgs - 1) / wgs, (long long)(nsteps / 8)));
+}
+
+extern "C" int esr_dconv_uses_halo(int32_t smy, int32_t smx, int32_t T, int32_t MW, int32_t sd) {
+    if (T <= 0 || T > ESR_DCONV_MAX_TAPS || MW <= 0) return ESR_EINVAL;
+    return g_dconv_halo && halo_wanted(smy, smx, T, MW, sd != 0) ? 1 : 0;
+}
+
+extern "C" int esr_dconv_fwd_splits(int32_t B, int32_t MH, int32_t MW, int32_t n, int32_t kc, int32_t smy,
+                                    int32_t smx, int32_t T, const int32_t *offy, const int32_t *offx) {
+    return esr_dconv_fwd_splits_sd(B, MH, MW, n, kc, smy, smx, T, offy, offx, 0);
 }
 
 extern "C" int esr_dconv_wgrad_splits(int32_t B, int32_t MH, int32_t MW, int32_t cin, int32_t cout, int32_t smy,
@@ -1618,7 +1669,7 @@ extern "C" int esr_dconv_set_rows(int32_t on) {
 }
 
 extern "C" int esr_dconv_set_halo(int32_t on) {
-    if (on < 0 || on > 1) return ESR_EINVAL;
+    if (on < 0 || on > 2) return ESR_EINVAL;
     const int prev = g_dconv_halo;
     g_dconv_halo = on;
     return prev;

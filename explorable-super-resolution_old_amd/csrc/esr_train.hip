@@ -624,6 +624,189 @@ __global__ __launch_bounds__(W3<NCT>::NT, 1) void wgrad3_kernel(WgradParams p) {
     }
 }
 
+// wgrad3d: wgrad3 for an output gradient that is already split-f16 (dsplit: the x3 backward's residual-block
+// gradients, values S·g at one scale S per pass, esr_grad_amax).  Both operands are then bit copies of global
+// records, so both tiles go HBM/L2 -> LDS by LDS-DMA (global_load_lds_dwordx4: no VGPR staging, no per-tile max or
+// rescale, no VALU split) into two LDS stages — tile t+1 is in flight while tile t is consumed, one barrier per tile.
+// LDS images, swizzle (applied on the DMA source address: the destination of a DMA is lane-linear) and wave roles are
+// wgrad3's, and so are the products (three f16 MFMAs per product on the stored f16 pieces; their scale is S, not a
+// per-tile 2^e — both powers of two).  N = 64 (two channel tiles) takes 4-row pixel tiles so that two stages fit.
+// The bias gradient is summed from the LDS image (hi + lo) by the chunk-0 workgroups.
+template <int NCT, int TH>
+struct W3D {
+    static constexpr int NWV = 12, NT = 64 * NWV, NQ = 4 / NCT;
+    static constexpr int HY = TH + 2, HX = WT_TW + 2, IN_PX = HY * HX, D_PX = TH * WT_TW;
+    static constexpr int IN_PC = (IN_PX + 7) / 8, D_PC = D_PX / 8;  // 1-KB pieces (8 records of 128 B)
+    static constexpr int IN_B = IN_PC * 1024, D_B = D_PC * 1024;
+    static constexpr int STAGE = IN_B + NCT * D_B;
+    static constexpr int PIECES = IN_PC + NCT * D_PC;
+    static constexpr int KP = (PIECES + NWV - 1) / NWV;  // DMA wave-instructions per wave and tile
+    static constexpr int LDS_B = 2 * STAGE;
+};
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) const void glob_void;
+__device__ __attribute__((aligned(16))) unsigned char g_wzero[64];  // zero page: the DMA source of absent records
+
+template <int NCT, int TH>
+__global__ __launch_bounds__((W3D<NCT, TH>::NT), 1) void wgrad3d_kernel(WgradParams p) {
+    using C = W3D<NCT, TH>;
+    constexpr int NT_ = C::NT, NQ = C::NQ;
+    static_assert(C::LDS_B <= 160 * 1024, "two stages per CU");
+    static_assert(3 * NCT * 3 * 16 * 64 * 4 <= C::LDS_B && NT_ * 4 <= C::LDS_B, "reductions fit in LDS");
+    __shared__ __attribute__((aligned(1024))) unsigned char smem[C::LDS_B];
+    const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int tg = wave % 3, r4 = wave / 3;
+    const int ct = NCT == 2 ? (r4 & 1) : 0, q = NCT == 2 ? (r4 >> 1) : r4;
+    const int nchunks = p.cin_pad / 32;
+    const int total = nchunks * p.splits;
+    const int per_xcd = (total + 7) / 8;
+    const int L = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+    if (L >= total) return;
+    const int chunk = L % nchunks, split = L / nchunks;
+    const int ntiles = p.B * p.tiles_y * p.tiles_x;
+    const int t_begin = (int)((long long)ntiles * split / p.splits);
+    const int t_end = (int)((long long)ntiles * (split + 1) / p.splits);
+    const int c0 = chunk * 32;
+    const int kg = (min(32, p.cin - c0) + 7) >> 3;  // 8-channel groups present in this chunk
+    const int Hi = p.up2 ? p.H / 2 : p.H, Wi = p.up2 ? p.W / 2 : p.W;
+    const unsigned char *gin = reinterpret_cast<const unsigned char *>(p.in);
+    const unsigned char *gd = reinterpret_cast<const unsigned char *>(p.dout);
+    const int drec = lane >> 3, slot = lane & 7, grp = slot >> 1;  // lane -> record of a piece, 16-B slot, group
+
+    // DMA of tile t into stage stg: piece pc = wave + 12 i; LDS byte pc·1024 + 16·lane = record 8 pc + drec, slot;
+    // the slot's logical half is (slot & 1) ^ swap(record), so the source half is chosen accordingly
+    auto dma_tile = [&](int t, int stg) {
+        const int tx = t % p.tiles_x, ty = (t / p.tiles_x) % p.tiles_y, b = t / (p.tiles_x * p.tiles_y);
+        const int y0 = ty * TH, x0 = tx * WT_TW;
+        unsigned char *base = smem + stg * C::STAGE;
+#pragma unroll
+        for (int i = 0; i < C::KP; ++i) {
+            const int pc = wave + C::NWV * i;
+            if (pc >= C::PIECES) break;
+            const void *src = g_wzero;
+            if (pc < C::IN_PC) {
+                const int r = 8 * pc + drec;
+                const int hy = r / C::HX, hx = r - hy * C::HX;
+                const int Y = y0 + hy - 1, X = x0 + hx - 1;
+                const int half = (slot & 1) ^ ((r >> 1) & 1);
+                if (r < C::IN_PX && Y >= 0 && Y < p.H && X >= 0 && X < p.W && grp < kg) {
+                    const int sy = p.up2 ? Y / 2 : Y, sx = p.up2 ? X / 2 : X;
+                    src = gin + ((((long long)b * (Hi + 2) + sy + 1) * (Wi + 2) + sx + 1) * p.in_cp + c0) * 4 +
+                          grp * 32 + half * 16;
+                }
+            } else {
+                const int pd = pc - C::IN_PC, cti = pd / C::D_PC, r = 8 * (pd - cti * C::D_PC) + drec;
+                const int y = y0 + (r >> 5), x = x0 + (r & 31);
+                const int half = (slot & 1) ^ ((r >> 1) & 1);
+                if (y < p.H && x < p.W && cti * 32 + grp * 8 < p.cout) {
+                    const long long pix = ((long long)b * (p.H + 2) + y + 1) * (p.W + 2) + x + 1;
+                    src = gd + (pix * p.dout_cp + p.dout_coff + cti * 32 + grp * 8) * 4 + half * 16;
+                }
+            }
+            __builtin_amdgcn_global_load_lds((glob_void *)src, (lds_void *)(base + pc * 1024), 16, 0, 0);
+        }
+    };
+
+    // transposed-read lane roles as wgrad3
+    const int i16 = lane & 15, rq = i16 >> 2;
+    const int chb = 16 * ((lane >> 4) & 1) + 4 * (i16 & 3);
+    const int ch_off = (chb >> 3) * 32 + (chb & 4) * 2;
+    auto rec_off = [&](int px, int lo) { return px * 128 + ch_off + ((lo ^ ((px >> 1) & 1)) << 4); };
+    // bias (chunk 0): thread -> channel bc of the 32·NCT, pixels bp0, bp0 + BST, ... of the tile
+    constexpr int BST = NT_ / (32 * NCT);
+    const int bc = tid % (32 * NCT), bp0 = tid / (32 * NCT);
+    const int b_off = (bc >> 5) * C::D_B + ((bc & 31) >> 3) * 32 + (bc & 7) * 2;
+    float bsum = 0.f;
+
+    f32x16 acc[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+
+    if (t_begin < t_end) dma_tile(t_begin, 0);
+    for (int t = t_begin; t < t_end; ++t) {
+        const int stg = (t - t_begin) & 1;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of tile t are in LDS
+        __syncthreads();  // ... every wave's; and every wave is done reading stage stg ^ 1 (tile t - 1)
+        if (t + 1 < t_end) dma_tile(t + 1, stg ^ 1);
+        const unsigned char *s_in = smem + stg * C::STAGE, *s_d = s_in + C::IN_B;
+        if (chunk == 0) {
+            for (int px = bp0; px < C::D_PX; px += BST) {
+                const unsigned char *rc = s_d + b_off + px * 128;
+                const int sw = (px >> 1) & 1;
+                bsum += (float)*reinterpret_cast<const _Float16 *>(rc + (sw << 4)) +
+                        (float)*reinterpret_cast<const _Float16 *>(rc + ((sw ^ 1) << 4));
+            }
+        }
+        const unsigned char *img_d = s_d + ct * C::D_B;
+#pragma unroll 2
+        for (int kk = 0; kk < 2 * TH / NQ; ++kk) {
+            const int kb = NQ * kk + q;             // K block: 16 pixels of tile row kb >> 1
+            const int py = kb >> 1, px0 = 16 * (kb & 1) + 8 * hl + rq;
+            const int dp = py * WT_TW + px0;
+            const f16x8 bh = cat8(tr_read(img_d, rec_off(dp, 0)), tr_read(img_d, rec_off(dp + 4, 0)));
+            const f16x8 bl = cat8(tr_read(img_d, rec_off(dp, 1)), tr_read(img_d, rec_off(dp + 4, 1)));
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const int ip = (py + j) * C::HX + px0 + tg;
+                const f16x8 ah = cat8(tr_read(s_in, rec_off(ip, 0)), tr_read(s_in, rec_off(ip + 4, 0)));
+                const f16x8 al = cat8(tr_read(s_in, rec_off(ip, 1)), tr_read(s_in, rec_off(ip + 4, 1)));
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[j], 0, 0, 0);
+            }
+        }
+    }
+    // sum the pixel classes into class 0 (fixed order 1, 2, ...) through LDS, as wgrad3
+    constexpr int PER_WAVE = 3 * 16 * 64;
+    float *red = reinterpret_cast<float *>(smem);
+    const int rslot = tg * NCT + ct;
+    for (int r = 1; r < NQ; ++r) {
+        __syncthreads();
+        if (q == r) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) red[rslot * PER_WAVE + (j * 16 + e) * 64 + lane] = acc[j][e];
+        }
+        __syncthreads();
+        if (q == 0) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) acc[j][e] += red[rslot * PER_WAVE + (j * 16 + e) * 64 + lane];
+        }
+    }
+    float *part = p.partial + (long long)split * (9LL * p.cin_pad * p.cout_pad + p.cout_pad);
+    if (q == 0) {
+        const int ml = lane & 31;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int tap = 3 * j + tg;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int ci = c0 + (e & 3) + 8 * (e >> 2) + 4 * hl;
+                part[((long long)tap * p.cin_pad + ci) * p.cout_pad + ct * 32 + ml] = acc[j][e];
+            }
+        }
+    }
+    if (chunk == 0) {  // bias: the threads of one channel, summed in thread order
+        __syncthreads();
+        red[tid] = bsum;
+        __syncthreads();
+        if (tid < p.cout_pad) {
+            float v = 0.f;
+            for (int th = tid; th < NT_; th += 32 * NCT) v += red[th];
+            part[9LL * p.cin_pad * p.cout_pad + tid] = v;
+        }
+    }
+}
+
+int g_wgrad3_dma = 1;  // esr_wgrad3_set_dma: wgrad3d for split-f16 output gradients (0: wgrad3, A/B)
+
 int g_wgrad_kernel = 1;  // 0 = wgrad_kernel (4 waves), 1 = wgrad2_kernel (12 waves)
 
 // Gradient scale of the x3 backward (esr_grad_amax): S = 2^(11 - ex) for max|g| < 2^ex, so the largest scaled
@@ -952,7 +1135,16 @@ extern "C" int esr_conv3x3_wgrad(const float *in, int32_t in_cp, int32_t cin, in
     p.partial = partial;
     p.dsplit = dsplit;
     const unsigned total = (unsigned)(p.cin_pad / 32 * splits);
-    if (x3) {
+    if (x3 && dsplit && g_wgrad3_dma) {
+        const unsigned grid = 8 * ((total + 7) / 8);
+        const hipStream_t st = (hipStream_t)stream;
+        if (p.cout_pad == 64) {
+            p.tiles_y = (H + 3) / 4;
+            hipLaunchKernelGGL((wgrad3d_kernel<2, 4>), dim3(grid), dim3(W3D<2, 4>::NT), 0, st, p);
+        } else {
+            hipLaunchKernelGGL((wgrad3d_kernel<1, 8>), dim3(grid), dim3(W3D<1, 8>::NT), 0, st, p);
+        }
+    } else if (x3) {
         const unsigned grid = 8 * ((total + 7) / 8);
         const hipStream_t st = (hipStream_t)stream;
         if (p.cout_pad == 64)
@@ -977,6 +1169,13 @@ extern "C" int esr_conv3x3_wgrad(const float *in, int32_t in_cp, int32_t cin, in
         hipLaunchKernelGGL(wgrad_kernel, dim3(total), dim3(256), 0, (hipStream_t)stream, p);
     }
     return launched();
+}
+
+extern "C" int esr_wgrad3_set_dma(int32_t on) {
+    if (on < 0 || on > 1) return ESR_EINVAL;
+    const int prev = g_wgrad3_dma;
+    g_wgrad3_dma = on;
+    return prev;
 }
 
 extern "C" int esr_wgrad_set_kernel(int32_t variant) {

@@ -8,7 +8,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('ESR_AMD_LIB', os.path.join(_HERE, 'libesr_amd.so'))
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 c_int = ctypes.c_int32
 c_float = ctypes.c_float
@@ -80,6 +80,7 @@ _SIGNATURES = {
     'esr_axpby_gs': [c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_int,
                      c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     'esr_wgrad_set_kernel': [c_int],
+    'esr_wgrad3_set_dma': [c_int],
     'esr_lrelu_bwd': [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     'esr_lrelu_bwd_split': [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     'esr_axpby': [c_void_p, c_int, c_int, c_float, c_void_p, c_int, c_int, c_float, c_void_p, c_int, c_int, c_int,
@@ -98,6 +99,13 @@ _SIGNATURES = {
                          ctypes.POINTER(c_int), ctypes.POINTER(c_int), c_int, c_void_p, c_void_p],
     'esr_dconv_fwd_splits': [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_int),
                              ctypes.POINTER(c_int)],
+    'esr_dconv_fwd_sd': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                         c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                         ctypes.POINTER(c_int), ctypes.POINTER(c_int), c_int, c_void_p, c_int, c_int, c_int, c_int,
+                         c_void_p],
+    'esr_dconv_uses_halo': [c_int, c_int, c_int, c_int, c_int],
+    'esr_dconv_fwd_splits_sd': [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_int),
+                                ctypes.POINTER(c_int), c_int],
     'esr_dconv_set_halo': [c_int],
     'esr_dconv_wgrad_splits': [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_int),
                                ctypes.POINTER(c_int)],

@@ -31,6 +31,10 @@ PRECISION = os.environ.get('ESR_DCONV_PRECISION', 'x3')
 _LIB_MODE = {'f32': 0, 'x3': 1, 'x6': 3}
 # exact-fp32 forward / data-gradient kernel: the halo-tile implicit GEMM (default) or the per-tap gather ('0', A/B)
 HALO = os.environ.get('ESR_DCONV_HALO', '1') != '0'
+# 4×4 stride-2 convs (and any even k at stride 2) and their data gradients as (k/2)×(k/2)-tap stride-1 convs over the
+# space-to-depth source / into the depth-to-space gradient (esr_dconv_fwd_sd, one launch each); '0' = the direct
+# stride-2 gather and one launch per phase class (A/B)
+S2D = os.environ.get('ESR_DCONV_S2D', '1') != '0'
 _applied = [None]
 
 
@@ -103,24 +107,43 @@ def _packed(w, key, make):
     return val
 
 
-def _gather(src, packed, bias, out, MH, MW, omy, oay, omx, oax, smy, smx, offy, offx):
-    """One esr_dconv_fwd launch: src [B][Hs][Ws][C] and out [B][Ho][Wo][N] contiguous NHWC, `packed` = _pack(wt [T][C][N],
-    N)."""
+def _gather(src, packed, bias, out, MH, MW, omy, oay, omx, oax, smy, smx, offy, offx, s2d_pad=None, d2s_pad=None):
+    """One esr_dconv_fwd launch: src [B][Hs][Ws][C] and out [B][Ho][Wo][N] contiguous NHWC, `packed` = _pack(wt [T][K][N'],
+    N').  s2d_pad: src is read through its space-to-depth view (K = 4C virtual channels); d2s_pad: out is written
+    through its depth-to-space view (N' = 4N virtual channels); include/esr_amd.h esr_dconv_fwd_sd."""
     B, Hs, Ws, C = src.shape
     _, Ho, Wo, N = out.shape
     wp, nck, n_pad = packed
+    kc = 4 * C if s2d_pad is not None else C
+    n = 4 * N if d2s_pad is not None else N
     lib = _lib_for_launch()
     oy, ox = _i32(offy), _i32(offx)
+    sd = s2d_pad is not None or d2s_pad is not None
     # split-K where the grid would fill few CUs and K is long (the 8x8 pseudo-FC layer); the library says how many
-    ks = lib.esr_dconv_fwd_splits(B, MH, MW, N, C, smy, smx, len(offy), oy, ox)
+    ks = lib.esr_dconv_fwd_splits_sd(B, MH, MW, n, kc, smy, smx, len(offy), oy, ox, int(sd))
     if ks < 1:
         raise RuntimeError('esr_dconv_fwd_splits failed with esr_status %d' % ks)
     part = torch.empty(ks * B * MH * MW * n_pad, device=src.device) if ks > 1 else None
-    _lib.check(lib.esr_dconv_fwd_sk(src.data_ptr(), B, Hs, Ws, C, C, wp.data_ptr(), nck, n_pad,
-                                    None if bias is None else bias.data_ptr(), out.data_ptr(), Ho, Wo, N, N, MH, MW,
+    _lib.check(lib.esr_dconv_fwd_sd(src.data_ptr(), B, Hs, Ws, C, kc, wp.data_ptr(), nck, n_pad,
+                                    None if bias is None else bias.data_ptr(), out.data_ptr(), Ho, Wo, N, n, MH, MW,
                                     omy, oay, omx, oax, smy, smx, len(offy), oy, ox, ks,
-                                    None if part is None else part.data_ptr(), _stream(src)),
+                                    None if part is None else part.data_ptr(),
+                                    C if s2d_pad is not None else 0, s2d_pad or 0,
+                                    N if d2s_pad is not None else 0, d2s_pad or 0, _stream(src)),
                'esr_dconv_fwd')
+
+
+def _s2d_form(k, s, C):
+    """Whether a k×k stride-s conv runs in its space-to-depth form ((k/2)² taps, 4C channels)."""
+    return S2D and s == 2 and k % 2 == 0 and C % 4 == 0
+
+
+def _s2d_weights(w):
+    """w [Co][Ci][k][k] -> [(k/2)²][(py, px, ci) = 4Ci][Co]: tap (a, b) of the space-to-depth form holds
+    w[:, :, 2a + py, 2b + px]."""
+    Co, Ci, k, _ = w.shape
+    h = k // 2
+    return w.permute(2, 3, 1, 0).reshape(h, 2, h, 2, Ci, Co).permute(0, 2, 1, 3, 4, 5).reshape(h * h, 4 * Ci, Co)
 
 
 def conv_forward(x, w, b, k, s, p):
@@ -130,6 +153,13 @@ def conv_forward(x, w, b, k, s, p):
     Co = w.shape[0]
     Ho, Wo = out_size(H, k, s, p), out_size(W, k, s, p)
     y = torch.empty(B, Ho, Wo, Co, device=x.device, dtype=torch.float32)
+    # y[yo] = sum over taps (a, b) of W'[a, b] . Z[yo + a, xo + b], Z = s2d(pad(x, p)); only where it is halo-tiled
+    if _s2d_form(k, s, Ci) and _lib_for_launch().esr_dconv_uses_halo(1, 1, (k // 2) ** 2, Wo, 1) == 1:
+        wp = _packed(w, ('fwd_s2d',), lambda: _pack(_s2d_weights(w.detach()), Co))
+        h = k // 2
+        _gather(x, wp, None if b is None else b.detach().contiguous(), y, Ho, Wo, 1, 0, 1, 0, 1, 1,
+                [a for a in range(h) for _ in range(h)], [c for _ in range(h) for c in range(h)], s2d_pad=p)
+        return y
     wp = _packed(w, ('fwd',), lambda: _pack(w.detach().permute(2, 3, 1, 0).reshape(k * k, Ci, Co), Co))
     taps = [(ky, kx) for ky in range(k) for kx in range(k)]
     _gather(x, wp, None if b is None else b.detach().contiguous(), y, Ho, Wo, 1, 0, 1, 0, s, s,
@@ -144,6 +174,13 @@ def conv_dgrad(gy, w, k, s, p, H, W):
     B, Ho, Wo, Co = gy.shape
     Ci = w.shape[1]
     wd = w.detach()
+    if _s2d_form(k, s, Ci):  # dZ[Y, X] = sum over taps (a, b) of W'[a, b]^T . gy[Y - a, X - b]; gx = d2s(dZ) unpadded
+        h = k // 2
+        gx = torch.empty(B, H, W, Ci, device=gy.device, dtype=torch.float32)
+        wp = _packed(w, ('dgrad_s2d',), lambda: _pack(_s2d_weights(wd).transpose(1, 2).contiguous(), 4 * Ci))
+        _gather(gy, wp, None, gx, (H - 1 + p) // 2 + 1, (W - 1 + p) // 2 + 1, 1, 0, 1, 0, 1, 1,
+                [-a for a in range(h) for _ in range(h)], [-c for _ in range(h) for c in range(h)], d2s_pad=p)
+        return gx
     classes = []
     full = True
     for cy in range(s):

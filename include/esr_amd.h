@@ -222,6 +222,10 @@ int esr_wgrad_reduce_gs(const float *partial, int32_t splits, int64_t n, float s
  * kernel (three waves per SIMD, next tile prefetched into registers, XCD-grouped chunks), 0 = the 4-wave kernel.
  * Both are deterministic; they sum the pixels in different orders.  Returns the previous setting, or ESR_EINVAL. */
 int esr_wgrad_set_kernel(int32_t variant);
+/* x3 weight gradient with a split-f16 output gradient (flags bit 8): 1 (default) = both tiles LDS-DMA'd into two LDS
+ * stages (no register staging or per-tile rescale; 4-row pixel tiles for Cout > 32), 0 = the register-staged x3
+ * kernel.  Both deterministic, different summation orders.  Returns the previous setting, or ESR_EINVAL. */
+int esr_wgrad3_set_dma(int32_t on);
 /* LeakyReLU(0.2) backward from the saved output y: d *= (y > 0 ? 1 : 0.2) on a C-channel slice. */
 int esr_lrelu_bwd(float *d, int32_t d_cp, int32_t d_coff, const float *y, int32_t y_cp, int32_t y_coff, int32_t C,
                   int32_t B, int32_t H, int32_t W, esr_stream_t stream);
@@ -296,6 +300,31 @@ int esr_dconv_fwd_sk(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_
  * where its grid has < 512 workgroups (the 8×8 pseudo-FC layer); x3: ~512 workgroups, >= 8 K steps per slice. */
 int esr_dconv_fwd_splits(int32_t B, int32_t MH, int32_t MW, int32_t n_out, int32_t kc, int32_t smy, int32_t smx,
                          int32_t T, const int32_t *offy, const int32_t *offx);
+/* esr_dconv_fwd_sk over a space-to-depth source and/or into a depth-to-space output: a k×k stride-2 conv (k even) as
+ * a (k/2)×(k/2)-tap stride-1 one with 4× the channels, the form the halo-tile kernel stages once per source pixel.
+ *   s2d_c > 0 (forward): src is the REAL [B][Hs][Ws][src_pitch] input with s2d_c channels (a multiple of 4) and
+ *     kc = 4·s2d_c; virtual channel (2·py + px)·s2d_c + c of virtual pixel (sy, sx) = src[b, 2·sy + py - s2d_pad,
+ *     2·sx + px - s2d_pad, c] (zero outside), so with W[(a, b)][(py, px, c)][n] = w[n][c][2a + py][2b + px],
+ *     offy = a, offx = b, smy = smx = 1 this is conv2d(src, w, stride 2, padding s2d_pad).
+ *   d2s_c > 0 (data gradient): n_out = 4·d2s_c, out is the REAL [B][Ho][Wo][out_pitch] input gradient; virtual
+ *     channel (2·py + px)·d2s_c + c of grid point (Y, X) goes to out[b, 2·Y + py - d2s_pad, 2·X + px - d2s_pad, c]
+ *     (dropped outside); omy = omx = 1, oay = oax = 0, no bias.  With src = dL/dy, offy = -a, offx = -b and
+ *     W[(a, b)][co][(py, px, c)] = w[co][c][2a + py][2b + px] over MH × MW = ((H-1+pad)/2 + 1) × ((W-1+pad)/2 + 1)
+ *     this is the transposed conv in one launch (replaces the per-phase-class calls of esr_dconv_fwd).
+ * Replaces: the D's 4×4 stride-2 conv_block convs (architecture.py:232-250, block.py:129-156) and their gradients. */
+int esr_dconv_fwd_sd(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t src_pitch, int32_t kc,
+                     const float *w_packed, int32_t nck, int32_t n_pad, const float *bias, float *out, int32_t Ho,
+                     int32_t Wo, int32_t out_pitch, int32_t n, int32_t MH, int32_t MW, int32_t omy, int32_t oay,
+                     int32_t omx, int32_t oax, int32_t smy, int32_t smx, int32_t T, const int32_t *offy,
+                     const int32_t *offx, int32_t ksplit, float *partial, int32_t s2d_c, int32_t s2d_pad,
+                     int32_t d2s_c, int32_t d2s_pad, esr_stream_t stream);
+/* 1 if an esr_dconv_fwd(_sd) launch of this geometry runs on the halo-tile kernel (sd != 0: an esr_dconv_fwd_sd
+ * launch), 0 if on the per-tap gather kernel.  The host takes the space-to-depth forward only where it is halo-tiled
+ * (on the gather kernel it is no faster than the direct stride-2 gather: profiles/r3_dconv_s2d_ab.txt). */
+int esr_dconv_uses_halo(int32_t smy, int32_t smx, int32_t T, int32_t MW, int32_t sd);
+/* esr_dconv_fwd_splits for an esr_dconv_fwd_sd launch (sd != 0: space-to-depth source or depth-to-space output). */
+int esr_dconv_fwd_splits_sd(int32_t B, int32_t MH, int32_t MW, int32_t n_out, int32_t kc, int32_t smy, int32_t smx,
+                            int32_t T, const int32_t *offy, const int32_t *offx, int32_t sd);
 /* esr_dconv_fwd kernels: 1 (default) = the halo-tile implicit GEMMs (each source pixel of a 32-channel chunk staged
  * in LDS once for all taps; exact fp32, or split x3 / x6 with a per-chunk source scale and a per-step weight scale)
  * for stride-1 launches with one tap or >= 9 taps where the halo fits in LDS, the gather kernels otherwise; 0 = the

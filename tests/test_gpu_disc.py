@@ -33,16 +33,20 @@ pytestmark = pytest.mark.gpu
     (130, 70, 4, 2, 1, 8, 9),      # partial K chunks and N blocks
     (64, 64, 3, 1, 1, 37, 70),     # several halo tiles per image, ragged in both directions
     (32, 64, 4, 2, 1, 41, 75),     # stride-2 halo (column-parity de-interleave), ragged
+    (64, 128, 4, 2, 1, 76, 100),   # space-to-depth form on the halo kernel (MW 50 / 51), two N blocks
     (256, 100, 8, 1, 0, 38, 38),   # the config-3 pseudo-FC geometry: split-K over the channel chunks
 ])
-@pytest.mark.parametrize('precision', ['x3', 'x6', 'f32', 'x3_gather', 'x6_gather', 'f32_gather'])
+@pytest.mark.parametrize('precision', ['x3', 'x6', 'f32', 'x3_gather', 'x6_gather', 'f32_gather', 'x3_direct',
+                                       'f32_direct', 'x3_gather_direct'])
 def test_dconv_ops_vs_float64(gpu_device, ci, co, k, s, p, H, W, precision):
     """x3 / x6 / f32 with the halo-tile forward and tap-row weight-gradient kernels where they apply (default),
-    *_gather = the per-tap kernels everywhere."""
+    *_gather = the per-tap kernels everywhere; the stride-2 convs in their space-to-depth form (default) or, *_direct,
+    as the direct stride-2 gather with one data-gradient launch per phase class."""
     prev = dconv.set_precision(precision.split('_')[0])
     lib = _lib.load()
-    prev_halo = lib.esr_dconv_set_halo(0 if precision.endswith('_gather') else 1)
-    prev_rows = lib.esr_dconv_set_rows(0 if precision.endswith('_gather') else 1)
+    prev_halo = lib.esr_dconv_set_halo(0 if '_gather' in precision else 1)
+    prev_rows = lib.esr_dconv_set_rows(0 if '_gather' in precision else 1)
+    prev_s2d, dconv.S2D = dconv.S2D, not precision.endswith('_direct')
     try:
         _dconv_ops(gpu_device, ci, co, k, s, p, H, W, scale=1.0 if precision.startswith('f32') else 1e-9,
                    tol=1e-5)
@@ -50,6 +54,7 @@ def test_dconv_ops_vs_float64(gpu_device, ci, co, k, s, p, H, W, precision):
         dconv.set_precision(prev)
         lib.esr_dconv_set_halo(prev_halo)
         lib.esr_dconv_set_rows(prev_rows)
+        dconv.S2D = prev_s2d
 
 
 def _dconv_ops(gpu_device, ci, co, k, s, p, H, W, scale, tol=1e-5):

@@ -232,7 +232,7 @@ def test_input_and_parameter_gradients_together_vs_oracle(gpu_device, mode, prec
             assert ok, (n, msg)
 
 
-@pytest.mark.parametrize('variant', [0, 1, 'x3'])
+@pytest.mark.parametrize('variant', [0, 1, 'x3', 'x3_dsplit', 'x3_dsplit_reg'])
 @pytest.mark.parametrize('cin,in_cp,cout,dout_cp,dout_coff,up2,B,H,W,splits', [
     (64, 64, 32, 192, 64, 0, 2, 20, 40, 7),      # RDB growth conv: dout a channel slice of a concat buffer
     (72, 80, 64, 64, 0, 0, 3, 13, 33, 5),        # latent-slot input, cout 64, ragged tiles
@@ -247,7 +247,9 @@ def test_weight_gradient_kernels_vs_float64(gpu_device, variant, cin, in_cp, cou
     torch.nn.grad.conv2d_weight in float64.  The x3 kernel splits the output gradient per pixel tile after a
     power-of-two scaling; here the output gradient is ~2^-30 (a realistic loss-gradient magnitude, far below f16's
     range) and its magnitude changes by 2^3 steps from one 8-row tile / image to the next, so that tiles take
-    different scales (the accumulator is rescaled between them) and every tile still counts in the norm."""
+    different scales (the accumulator is rescaled between them) and every tile still counts in the norm.
+    x3_dsplit: the output gradient split-f16 at one scale S (the x3 backward's layout, flags bit 8) on the LDS-DMA
+    kernel (wgrad3d); x3_dsplit_reg: the same on the register-staged x3 kernel."""
     import ctypes
     from esr_amd import _lib
     lib = _lib.load()
@@ -258,32 +260,44 @@ def test_weight_gradient_kernels_vs_float64(gpu_device, variant, cin, in_cp, cou
     xin = torch.zeros(B, Hi + 2, Wi + 2, in_cp)
     xin[:, 1:-1, 1:-1, :cin] = x.permute(0, 2, 3, 1)
     dbuf = torch.randn(B, H + 2, W + 2, dout_cp, generator=g)  # junk around the slice must be ignored
-    if variant == 'x3':
+    x3 = str(variant).startswith('x3')
+    dsplit = str(variant).startswith('x3_dsplit')
+    if dsplit and (cout % 8 or dout_cp % 8 or dout_coff % 8):
+        pytest.skip('a split-f16 output gradient needs 8-channel groups')
+    if x3:
         if cin % 8 or in_cp % 8:
             pytest.skip('split-f16 activations need 8-channel groups')
         tile = torch.arange(H).view(1, H) // 8 + torch.arange(B).view(B, 1)
         dy = dy * torch.exp2(-30.0 + 3.0 * (tile % 5 - 2)).view(B, 1, H, 1)  # 2^-36 .. 2^-24 by tile
     dbuf[:, 1:-1, 1:-1, dout_coff:dout_coff + cout] = dy.permute(0, 2, 3, 1)
     flags = up2
-    if variant == 'x3':
+    S = 1.0
+    if x3:
         from esr_amd import engine as E
         xin = E.to_split(xin)
         x = E.from_split(E.to_split(x.permute(0, 2, 3, 1).contiguous())).permute(0, 3, 1, 2)  # the values it holds
         flags = up2 | 6
+    if dsplit:
+        S = 2.0 ** 34  # S·dy: largest |S·dy| ~2^12, the smallest tiles' values ~2^-2
+        dbuf = E.to_split(dbuf * S)
+        dy = E.from_split(E.to_split((dy * S).permute(0, 2, 3, 1).contiguous())).permute(0, 3, 1, 2) / S
+        flags |= 8
     cin_pad, cout_pad = 32 * ((cin + 31) // 32), 64 if cout > 32 else 32
     n = 9 * cin_pad * cout_pad + cout_pad
     xin, dbuf = xin.to(gpu_device), dbuf.to(gpu_device)
     partial = torch.full((splits * n,), float('nan'), device=gpu_device)
     out = torch.empty(n, device=gpu_device)
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    prev = lib.esr_wgrad_set_kernel(variant if variant != 'x3' else 1)
+    prev = lib.esr_wgrad_set_kernel(variant if not x3 else 1)
+    prev_dma = lib.esr_wgrad3_set_dma(0 if variant == 'x3_dsplit_reg' else 1)
     try:
         _lib.check(lib.esr_conv3x3_wgrad(xin.data_ptr(), in_cp, cin, flags, dbuf.data_ptr(), dout_cp, dout_coff, cout,
                                          B, H, W, splits, partial.data_ptr(), st), 'wgrad')
-        _lib.check(lib.esr_wgrad_reduce(partial.data_ptr(), splits, n, 1.0, out.data_ptr(), st), 'reduce')
+        _lib.check(lib.esr_wgrad_reduce(partial.data_ptr(), splits, n, 1.0 / S, out.data_ptr(), st), 'reduce')
         torch.cuda.synchronize()
     finally:
         lib.esr_wgrad_set_kernel(prev)
+        lib.esr_wgrad3_set_dma(prev_dma)
     out = out.cpu().double()
     xr = x.double()
     if up2:

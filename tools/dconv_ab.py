@@ -2,7 +2,9 @@
 304², Discriminator_VGG_128_ nb=6): exact fp32, x3 with 64-channel N tiles, x3 with 128 (default).  Order-balanced
 (two rounds, the second reported); µs per launch, TFLOP/s, and the results' normwise difference from the fp32 gather
 kernel.  Variants: f32_gather (the per-tap gather kernel), f32_halo (halo-tile kernel, the fp32 default), x3 with 64-
-and 128-channel N tiles.  Also the data gradient (all phase classes) per variant.
+and 128-channel N tiles.  Also the data gradient (all phase classes) per variant.  *_direct: the 4×4 stride-2 layers
+as the direct stride-2 gather and one data-gradient launch per phase class instead of their space-to-depth form
+(dconv.S2D).  AB_LAYERS (comma list of layer names) and AB_TAGS (comma list of variant tags) select a subset.
 
     python tools/dconv_ab.py
 """
@@ -30,7 +32,16 @@ def main():
     lib = _lib.load()
     dev = torch.device('cuda')
     B = 16
-    for name, ci, co, k, s, p, H in LAYERS:
+    variants = [('f32', 0, 0, 1), ('f32_halo', 0, 1, 1), ('x3_n128', 1, 0, 1), ('x3_halo', 1, 1, 1), ('x6', 3, 0, 1),
+                ('x6_halo', 3, 1, 1), ('f32_halo_direct', 0, 1, 0), ('x3_halo_direct', 1, 1, 0),
+                ('x3_halo_sdall', 1, 2, 1)]
+    if 'AB_TAGS' in os.environ:
+        keep = set(os.environ['AB_TAGS'].split(',')) | {'f32'}
+        variants = [v for v in variants if v[0] in keep]
+    layers = LAYERS
+    if 'AB_LAYERS' in os.environ:
+        layers = [l for l in LAYERS if l[0] in os.environ['AB_LAYERS'].split(',')]
+    for name, ci, co, k, s, p, H in layers:
         x = torch.randn(B, H, H, ci, device=dev)
         w = torch.randn(co, ci, k, k, device=dev) / (ci * k * k) ** 0.5
         b = torch.randn(co, device=dev) * 0.1
@@ -39,14 +50,14 @@ def main():
         row, outs = {}, {}
         gy = torch.randn(B, Ho, Ho, co, device=dev) * 1e-8
         for rnd in range(2):
-            for tag, mode, halo in (('f32', 0, 0), ('f32_halo', 0, 1), ('x3_n128', 1, 0), ('x3_halo', 1, 1),
-                                    ('x6', 3, 0), ('x6_halo', 3, 1)):
+            for tag, mode, halo, s2d in variants:
+                dconv.S2D = bool(s2d)
                 dconv.set_precision({0: 'f32', 3: 'x6'}.get(mode, 'x3'))
                 dconv._applied[0] = None
                 dconv._lib_for_launch()
                 lib.esr_dconv_set_x3(mode)
                 lib.esr_dconv_set_halo(halo)
-                lib.esr_dconv_set_rows(halo)  # *_halo: the halo forward and the tap-row weight gradient
+                lib.esr_dconv_set_rows(min(halo, 1))  # *_halo: the halo forward and the tap-row weight gradient
                 for _ in range(2):
                     dconv.conv_forward(x, w, b, k, s, p)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -78,7 +89,7 @@ def main():
                     row[tag + '_tflops'] = round(flops / us / 1e6, 1)
                     row[tag + '_wgrad_us'] = round(us_w, 1)
                     row[tag + '_dgrad_us'] = round(us_d, 1)
-        for tag in ('f32_halo', 'x3_n128', 'x3_halo', 'x6', 'x6_halo'):
+        for tag in [v[0] for v in variants[1:]]:
             row[tag + '_diff'] = float((outs[tag] - outs['f32']).norm() / outs['f32'].norm())
             row[tag + '_dgrad_diff'] = float((outs[tag + 'd'] - outs['f32d']).norm() / outs['f32d'].norm())
             row[tag + '_wgrad_diff'] = float((outs[tag + 'w'] - outs['f32w']).norm() / outs['f32w'].norm())
@@ -86,6 +97,7 @@ def main():
     lib.esr_dconv_set_x3(0)
     lib.esr_dconv_set_halo(1)
     lib.esr_dconv_set_rows(1)
+    dconv.S2D = True
     dconv._applied[0] = None
 
 

@@ -1,6 +1,7 @@
 """A/B timing of the generator weight-gradient kernels on the config-3 conv shapes (B=16, 96² LR): the exact-fp32
 12-wave kernel reading split-f16 activations (flags 2, the round-1 training path) against the x3 kernel (flags 6),
-the latter also at other split-K counts.  Average µs per esr_conv3x3_wgrad launch (+ its esr_wgrad_reduce) and
+the latter also at other split-K counts, and the x3 kernels on a split-f16 output gradient (flags 14, the x3
+backward's residual blocks): LDS-DMA (wgrad3d, default) vs register-staged (esr_wgrad3_set_dma(0)).  Average µs per esr_conv3x3_wgrad launch (+ its esr_wgrad_reduce) and
 TFLOP/s (2·9·Cin·Cout per output pixel), order-balanced (A, B, A, B; the last pair is reported).
 
     python tools/wgrad_ab.py [--splits-scale 1,0.5,0.25]
@@ -42,6 +43,7 @@ def main():
         Hi, Wi = (H // 2, W // 2) if up2 else (H, W)
         x = E.to_split(torch.randn(B, Hi + 2, Wi + 2, in_cp, device=dev))
         d = torch.randn(B, H + 2, W + 2, d_cp, device=dev) * 1e-7
+        ds = E.to_split(d * 2.0 ** 30) if cout % 8 == 0 and d_cp % 8 == 0 else None  # S·d, split-f16
         chunks = (cin + 31) // 32
         ntiles = B * ((H + 7) // 8) * ((W + 31) // 32)
         splits0 = max(1, min(128, -(-1024 // chunks), ntiles))
@@ -52,15 +54,19 @@ def main():
         flops = 2 * 9 * cin * cout * B * H * W
         variants = [('f32', 2, splits0)] + [('x3_s%d' % max(1, int(splits0 * s)), 6, max(1, int(splits0 * s)))
                                             for s in scales] + [("x3_auto", 6, splits_x3)]
+        if ds is not None:
+            variants += [('x3_dsplit_dma', 14, splits_x3), ('x3_dsplit_reg', 30, splits_x3)]  # 16: tool-local tag
 
         def run(flags, splits, reps, out=None):
+            lib.esr_wgrad3_set_dma(0 if flags & 16 else 1)
+            dd, sc = (ds, 2.0 ** -30) if flags & 8 else (d, 1.0)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(reps):
-                _lib.check(lib.esr_conv3x3_wgrad(x.data_ptr(), in_cp, cin, up2 | flags, d.data_ptr(), d_cp, 0, cout,
-                                                 B, H, W, splits, part.data_ptr(), st), 'wgrad')
+                _lib.check(lib.esr_conv3x3_wgrad(x.data_ptr(), in_cp, cin, up2 | (flags & 15), dd.data_ptr(), d_cp, 0,
+                                                 cout, B, H, W, splits, part.data_ptr(), st), 'wgrad')
                 if out is not None:
-                    _lib.check(lib.esr_wgrad_reduce(part.data_ptr(), splits, n, 1.0, out.data_ptr(), st), 'reduce')
+                    _lib.check(lib.esr_wgrad_reduce(part.data_ptr(), splits, n, sc, out.data_ptr(), st), 'reduce')
             e1.record()
             torch.cuda.synchronize()
             return e0.elapsed_time(e1) * 1000 / reps
@@ -82,6 +88,7 @@ def main():
             if tag != 'f32':
                 row[tag + '_rel_diff'] = float((outs[tag] - ref).norm() / ref.norm())
         print(name, json.dumps(row), flush=True)
+    lib.esr_wgrad3_set_dma(1)
 
 
 if __name__ == '__main__':
