@@ -576,9 +576,12 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_x3_kernel(FwdParams p) {
 // the halo window (a first pass over the window's global loads, values discarded; the second pass scales, splits and
 // stores), per (tap, chunk) step the max |b| of the weight slab; the accumulators are rescaled exactly whenever the
 // sum of the two exponents changes.
-template <int WM, int WN, int NP>
+// NBX = 64 or 128 output channels per workgroup (128: each wave 4 N-tiles, twice the MFMAs per staged B slab and A
+// fragment; taken for x3 where n_pad allows and the grid still fills the chip).  TY = WM·WN·128 / NBX rows.
+template <int WM, int WN, int NP, int NBX = NB>
 __global__ __launch_bounds__(NTH, 2) void dconv_fwd_halo_x_kernel(FwdParams p, HaloParams h) {
-    constexpr int TY = 2 * WM * WN, MWV = TY / WM, XPn = XPitch<NP>::v;
+    constexpr int TY = WM * WN * 128 / NBX, MWV = TY / WM, XPn = XPitch<NP>::v, BX_IT = NBX * KC / 4 / NTH;
+    static_assert((TY / WM) * (NBX / 32 / WN) == NTH / 64, "waves along M x waves along N = 4");
     extern __shared__ __attribute__((aligned(16))) unsigned char xlds[];
     __shared__ float s_reda[NTH / 64], s_redb[2][NTH / 64];  // per-wave max of the halo / of the weight slab
     unsigned char *s_a = xlds, *s_b = xlds + h.b_off;
@@ -588,7 +591,7 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_halo_x_kernel(FwdParams p, H
     id /= h.tiles_x;
     const int tyi = id % h.tiles_y, b = id / h.tiles_y;
     const int Y0 = tyi * TY, X0 = txi * 32;
-    const int n0 = blockIdx.y * NB;
+    const int n0 = blockIdx.y * NBX;
     const int wm = wave % MWV, wn = wave / MWV;
     const bool vec = p.vec != 0;
     const int sy0 = p.smy * Y0 + h.oymin, sx0 = p.smx * X0 + h.oxmin;
@@ -661,17 +664,17 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_halo_x_kernel(FwdParams p, H
         return ea;
     };
 
-    f32x4 rb[B_IT];
+    f32x4 rb[BX_IT];
     auto load_b = [&](int step) {
         const int j = c_begin + step / p.T, t = step - (step / p.T) * p.T;
         const float *wj = p.w + ((long long)(t * p.nck + j) * p.n_pad + n0) * KC;
 #pragma unroll
-        for (int k = 0; k < B_IT; ++k) rb[k] = *reinterpret_cast<const f32x4 *>(wj + (tid + k * NTH) * 4);
+        for (int k = 0; k < BX_IT; ++k) rb[k] = *reinterpret_cast<const f32x4 *>(wj + (tid + k * NTH) * 4);
     };
     auto publish_b = [&](int slot) {
         float mb = 0.f;
 #pragma unroll
-        for (int k = 0; k < B_IT; ++k)
+        for (int k = 0; k < BX_IT; ++k)
 #pragma unroll
             for (int e = 0; e < 4; ++e) mb = fmaxf(mb, fabsf(rb[k][e]));
         mb = wave_max(mb);
@@ -713,7 +716,7 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_halo_x_kernel(FwdParams p, H
         eb = eb2;
         const float sb = ldexpf(1.f, eb);
 #pragma unroll
-        for (int k = 0; k < B_IT; ++k) {
+        for (int k = 0; k < BX_IT; ++k) {
             const int idx = tid + k * NTH;
             split_put(s_b + (idx >> 3) * XPn, idx & 7, rb[k], sb);
         }
@@ -1383,7 +1386,7 @@ bool halo_wanted(int smy, int smx, int T, int MW, bool sd = false) {
 // Halo tiling of an esr_dconv_fwd launch with `pitch` LDS bytes per staged pixel row (144: fp32 / x3, 208: x6):
 // false if the gather kernel has to run it (stride > 2, or a halo that does not fit in LDS even at 2-row tiles).
 bool halo_plan(int MH, int MW, int smy, int smx, int T, const int32_t *offy, const int32_t *offx, HaloParams &h,
-               int &lds, int pitch = PS * 4) {
+               int &lds, int pitch = PS * 4, int nbx = NB) {
     if (smy < 1 || smy > 2 || smx < 1 || smx > 2) return false;
     int ymin = offy[0], ymax = offy[0], xmin = offx[0], xmax = offx[0];
     for (int t = 1; t < T; ++t) {
@@ -1395,7 +1398,7 @@ bool halo_plan(int MH, int MW, int smy, int smx, int T, const int32_t *offy, con
     h.npar = smx;
     h.IXp = smx == 1 ? 32 + (xmax - xmin) : 32 + ((xmax - xmin) >> 1);
     h.IXt = h.npar * h.IXp;
-    const int b_bytes = NB * pitch;
+    const int b_bytes = nbx * pitch;
     for (int pass = 0; pass < 2; ++pass) {
         const int budget = pass == 0 ? HALO_LDS_2PER_CU : HALO_LDS_MAX;
         for (int ty = 8; ty >= 2; ty >>= 1) {
@@ -1491,11 +1494,11 @@ void launch_halo_f32(const FwdParams &p, const HaloParams &h, dim3 grid, int lds
     hipLaunchKernelGGL((dconv_fwd_halo_kernel<WM, WN>), grid, dim3(NTH), lds, st, p, h);
 }
 
-template <int WM, int WN, int NP>
+template <int WM, int WN, int NP, int NBX = NB>
 void launch_halo_x(const FwdParams &p, const HaloParams &h, dim3 grid, int lds, hipStream_t st) {
     static bool attr = false;
-    allow_full_lds(dconv_fwd_halo_x_kernel<WM, WN, NP>, attr);
-    hipLaunchKernelGGL((dconv_fwd_halo_x_kernel<WM, WN, NP>), grid, dim3(NTH), lds, st, p, h);
+    allow_full_lds(dconv_fwd_halo_x_kernel<WM, WN, NP, NBX>, attr);
+    hipLaunchKernelGGL((dconv_fwd_halo_x_kernel<WM, WN, NP, NBX>), grid, dim3(NTH), lds, st, p, h);
 }
 
 }  // namespace
@@ -1558,7 +1561,15 @@ extern "C" int esr_dconv_fwd_sd(const float *src, int32_t B, int32_t Hs, int32_t
             else if (h.TY == 4) launch_halo_f32<1, 2>(p, h, hgrid, lds, st);
             else launch_halo_f32<1, 1>(p, h, hgrid, lds, st);
         } else if (np == 2) {
-            if (h.TY == 8) launch_halo_x<2, 2, 2>(p, h, hgrid, lds, st);
+            // 128-channel N tiles where the plan keeps 8-row tiles under the two-per-CU budget and the grid still
+            // has >= 512 workgroups without a split (profiles/r3_dconv_nb128_ab.txt)
+            HaloParams h2;
+            int lds2 = 0;
+            if (g_dconv_nb != 64 && ksplit == 1 && n_pad % 128 == 0 && h.TY == 8 && hx * (n_pad / 128) >= 512 &&
+                halo_plan(MH, MW, smy, smx, T, offy, offx, h2, lds2, PS * 4, 128) && h2.TY == 8 &&
+                lds2 <= HALO_LDS_2PER_CU) {
+                launch_halo_x<2, 4, 2, 128>(p, h2, dim3((unsigned)hx, (unsigned)(n_pad / 128), 1), lds2, st);
+            } else if (h.TY == 8) launch_halo_x<2, 2, 2>(p, h, hgrid, lds, st);
             else if (h.TY == 4) launch_halo_x<1, 2, 2>(p, h, hgrid, lds, st);
             else launch_halo_x<1, 1, 2>(p, h, hgrid, lds, st);
         } else {

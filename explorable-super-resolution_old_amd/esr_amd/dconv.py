@@ -29,6 +29,9 @@ MAX_TAPS = 64
 # products (each operand to ~33 bits: an fp32 FMA chain's accuracy, esr_dconv.hip), 'f32' = exact fp32 MFMA.
 PRECISION = os.environ.get('ESR_DCONV_PRECISION', 'x3')
 _LIB_MODE = {'f32': 0, 'x3': 1, 'x6': 3}
+# x3: 128-wide N tiles where the grid allows (esr_dconv_set_x3(1)); '0' = 64-wide only (esr_dconv_set_x3(2), A/B)
+if os.environ.get('ESR_DCONV_NB128', '1') == '0':
+    _LIB_MODE['x3'] = 2
 # exact-fp32 forward / data-gradient kernel: the halo-tile implicit GEMM (default) or the per-tap gather ('0', A/B)
 HALO = os.environ.get('ESR_DCONV_HALO', '1') != '0'
 # 4×4 stride-2 convs (and any even k at stride 2) and their data gradients as (k/2)×(k/2)-tap stride-1 convs over the

@@ -57,11 +57,23 @@ def test_dconv_ops_vs_float64(gpu_device, ci, co, k, s, p, H, W, precision):
         dconv.S2D = prev_s2d
 
 
-def _dconv_ops(gpu_device, ci, co, k, s, p, H, W, scale, tol=1e-5):
+@pytest.mark.parametrize('ci,co,k,s,p,H,W,B', [
+    (64, 128, 3, 1, 1, 64, 128, 16),   # forward: 128-wide N tiles (512 workgroups, n_pad 128)
+    (32, 64, 4, 2, 1, 124, 124, 32),   # space-to-depth data gradient: N = 4·32 = 128 on 128-wide tiles
+])
+def test_dconv_ops_wide_halo_tiles(gpu_device, ci, co, k, s, p, H, W, B):
+    """x3 halo kernel with 128 output channels per workgroup (grids of >= 512 workgroups) vs float64."""
+    prev = dconv.set_precision('x3')
+    try:
+        _dconv_ops(gpu_device, ci, co, k, s, p, H, W, scale=1e-9, tol=1e-5, B=B)
+    finally:
+        dconv.set_precision(prev)
+
+
+def _dconv_ops(gpu_device, ci, co, k, s, p, H, W, scale, tol=1e-5, B=3):
     """scale: the output gradient's magnitude (x3: ~1e-9, a realistic loss gradient far below f16's range, which the
     per-step scaling must bring back)."""
     g = torch.Generator().manual_seed(ci * 1000 + co)
-    B = 3
     x = torch.randn(B, ci, H, W, generator=g)
     w = torch.randn(co, ci, k, k, generator=g) / np.sqrt(ci * k * k)
     b = torch.randn(co, generator=g) * 0.1

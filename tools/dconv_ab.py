@@ -34,7 +34,7 @@ def main():
     B = 16
     variants = [('f32', 0, 0, 1), ('f32_halo', 0, 1, 1), ('x3_n128', 1, 0, 1), ('x3_halo', 1, 1, 1), ('x6', 3, 0, 1),
                 ('x6_halo', 3, 1, 1), ('f32_halo_direct', 0, 1, 0), ('x3_halo_direct', 1, 1, 0),
-                ('x3_halo_sdall', 1, 2, 1)]
+                ('x3_halo_sdall', 1, 2, 1), ('x3_halo_n64', 2, 1, 1)]
     if 'AB_TAGS' in os.environ:
         keep = set(os.environ['AB_TAGS'].split(',')) | {'f32'}
         variants = [v for v in variants if v[0] in keep]
