@@ -63,8 +63,8 @@ struct FwdParams {
     int T;
     int offy[MAXT], offx[MAXT];
     float *partial;  // split-K (x3 kernel, gridDim.z > 1): [z][M][n_pad] raw sums, reduced by dconv_splitk_reduce
-    int s2c, s2pad;  // > 0: space-to-depth source (src_quad); 0: plain
-    int d2c, d2pad;  // > 0: depth-to-space output (put_out); 0: plain
+    int s2c, s2pad, s2g;  // > 0: space-to-depth source (src_quad), channel group s2g; 0: plain
+    int d2c, d2pad, d2g;  // > 0: depth-to-space output (put_out), channel group d2g; 0: plain
 };
 
 __device__ __forceinline__ f32x4 load4(const float *row, int c, int kc, bool vec) {
@@ -78,16 +78,19 @@ __device__ __forceinline__ f32x4 load4(const float *row, int c, int kc, bool vec
 
 // The 4-channel quad from channel c of gather point (sy, sx) of image b; zero outside the image (the conv's padding).
 // s2c > 0: the source is the space-to-depth view of a stride-2 conv's input (esr_dconv_fwd_sd): virtual channel
-// c = (2·py + px)·s2c + c' of virtual pixel (sy, sx) is channel c' of real pixel (2·sy + py - s2pad, 2·sx + px - s2pad)
-// of the [B][Hs][Ws][sp] source (s2c % 4 == 0, so a quad never straddles two phases).
+// c = (c' / G)·4G + (2·py + px)·G + c' % G of virtual pixel (sy, sx) is channel c' of real pixel
+// (2·sy + py - s2pad, 2·sx + px - s2pad) of the [B][Hs][Ws][sp] source, G = s2g (32 where s2c % 32 == 0, so that a
+// 32-channel K chunk is 128 contiguous bytes of one real pixel; else s2c).  s2c % 4 == 0: a quad never straddles
+// two phases.
 __device__ __forceinline__ f32x4 src_quad(const FwdParams &p, int b, int sy, int sx, int c, bool vec) {
     int kc = p.kc;
     if (p.s2c) {
-        const int ph = c / p.s2c;
-        c -= ph * p.s2c;
+        const int ph = (c / p.s2g) & 3;
+        c = (c / (4 * p.s2g)) * p.s2g + c % p.s2g;
+        if (c >= p.s2c) c = p.s2c;  // past the last group (kc padding): reads as zero below
         sy = 2 * sy + (ph >> 1) - p.s2pad;
         sx = 2 * sx + (ph & 1) - p.s2pad;
-        kc = ph < 4 ? p.s2c : 0;
+        kc = p.s2c;
     }
     if (c < kc && sy >= 0 && sy < p.Hs && sx >= 0 && sx < p.Ws)
         return load4(p.src + (((long long)b * p.Hs + sy) * p.Ws + sx) * p.sp, c, kc, vec);
@@ -95,14 +98,14 @@ __device__ __forceinline__ f32x4 src_quad(const FwdParams &p, int b, int sy, int
 }
 
 // out at output grid point (Y, X), channel n.  d2c > 0: depth-to-space (the data gradient of a stride-2 conv in its
-// space-to-depth form): channel n = (2·py + px)·d2c + c' of grid point (Y, X) is channel c' of real pixel
-// (2·(omy·Y + oay) + py - d2pad, 2·(omx·X + oax) + px - d2pad); pixels outside [0, Ho) × [0, Wo) (the padding
-// border) are dropped.
+// space-to-depth form): channel n = (c' / G)·4G + (2·py + px)·G + c' % G of grid point (Y, X) (G = d2g, the
+// grouping of src_quad) is channel c' of real pixel (2·(omy·Y + oay) + py - d2pad, 2·(omx·X + oax) + px - d2pad);
+// pixels outside [0, Ho) × [0, Wo) (the padding border) are dropped.
 __device__ __forceinline__ void put_out(const FwdParams &p, int b, int Y, int X, int n, float v) {
     int oy = p.omy * Y + p.oay, ox = p.omx * X + p.oax;
     if (p.d2c) {
-        const int ph = n / p.d2c;
-        n -= ph * p.d2c;
+        const int ph = (n / p.d2g) & 3;
+        n = (n / (4 * p.d2g)) * p.d2g + n % p.d2g;
         oy = 2 * oy + (ph >> 1) - p.d2pad;
         ox = 2 * ox + (ph & 1) - p.d2pad;
         if (oy < 0 || oy >= p.Ho || ox < 0 || ox >= p.Wo) return;
@@ -578,7 +581,9 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_x3_kernel(FwdParams p) {
 // sum of the two exponents changes.
 // NBX = 64 or 128 output channels per workgroup (128: each wave 4 N-tiles, twice the MFMAs per staged B slab and A
 // fragment; taken for x3 where n_pad allows and the grid still fills the chip).  TY = WM·WN·128 / NBX rows.
-template <int WM, int WN, int NP, int NBX = NB>
+// DBG (experiment build only, garbage outputs): 1 = no weight-slab staging (no loads, max, split, stores; one barrier
+// per chunk), 2 = no fragment reads / MFMAs, 4 = the halo window staged for the first chunk only
+template <int WM, int WN, int NP, int NBX = NB, int DBG = 0>
 __global__ __launch_bounds__(NTH, 2) void dconv_fwd_halo_x_kernel(FwdParams p, HaloParams h) {
     constexpr int TY = WM * WN * 128 / NBX, MWV = TY / WM, XPn = XPitch<NP>::v, BX_IT = NBX * KC / 4 / NTH;
     static_assert((TY / WM) * (NBX / 32 / WN) == NTH / 64, "waves along M x waves along N = 4");
@@ -624,7 +629,10 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_halo_x_kernel(FwdParams p, H
         for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
         return m;
     };
-    // stage chunk j's halo window: pass 1 = max |a| (returns the exponent), pass 2 = scaled split into LDS
+    // stage chunk j's halo window: one pass over global memory — each item's fp32 quad goes into its row of the LDS
+    // image (a staged row's 128 fp32 bytes fit in its split pitch) while the max |a| is taken; after the cross-wave
+    // max each thread converts whole rows in place (all 8 quads read before any write), so the window is not read
+    // from L2 twice (the two-pass form cost up to 40 % of a space-to-depth launch: profiles/r3_halo_split.txt)
     auto stage_a = [&](int j, int e_keep) {
         const int total = h.IY * h.IXt * 8;
         float m = 0.f;
@@ -636,9 +644,12 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_halo_x_kernel(FwdParams p, H
                 v[u] = idx < total ? halo_item(idx, j) : f32x4{0.f, 0.f, 0.f, 0.f};
             }
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
+            for (int u = 0; u < 8; ++u) {
+                const int idx = base + u * NTH + tid;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) m = fmaxf(m, fabsf(v[u][e]));
+                if (idx < total) *reinterpret_cast<f32x4 *>(s_a + (idx >> 3) * XPn + (idx & 7) * 16) = v[u];
+            }
         }
         m = wave_max(m);
         if (lane == 0) s_reda[wave] = m;
@@ -648,18 +659,14 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_halo_x_kernel(FwdParams p, H
         for (int w = 0; w < NTH / 64; ++w) mm = fmaxf(mm, s_reda[w]);
         const int ea = tile_exp(mm, e_keep);
         const float sc = ldexpf(1.f, ea);
-        for (int base = 0; base < total; base += 8 * NTH) {
-            f32x4 v[8];
+        const int rows = h.IY * h.IXt;
+        for (int r = tid; r < rows; r += NTH) {
+            unsigned char *row = s_a + r * XPn;
+            f32x4 q[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int idx = base + u * NTH + tid;
-                v[u] = idx < total ? halo_item(idx, j) : f32x4{0.f, 0.f, 0.f, 0.f};
-            }
+            for (int k = 0; k < 8; ++k) q[k] = *reinterpret_cast<const f32x4 *>(row + 16 * k);
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int idx = base + u * NTH + tid;
-                if (idx < total) split_put(s_a + (idx >> 3) * XPn, idx & 7, v[u], sc);
-            }
+            for (int k = 0; k < 8; ++k) split_put(row, k, q[k], sc);
         }
         return ea;
     };
@@ -690,15 +697,15 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_halo_x_kernel(FwdParams p, H
             for (int r = 0; r < 16; ++r) acc[i][k][r] = 0.f;
     int ea = 0, eb = 0;
 
-    if (nsteps > 0) {
+    if (nsteps > 0 && !(DBG & 1)) {
         load_b(0);
         publish_b(0);
     }
     for (int step = 0; step < nsteps; ++step) {
         const int t = step % p.T;
-        __syncthreads();  // the previous step's fragment reads are done; this step's weight max is published
+        if (!(DBG & 1) || t == 0) __syncthreads();  // the previous step's fragment reads are done; weight max published
         int ea2 = ea;
-        if (t == 0) ea2 = stage_a(c_begin + step / p.T, ea);  // (contains a barrier)
+        if (t == 0 && (!(DBG & 4) || step == 0)) ea2 = stage_a(c_begin + step / p.T, ea);  // (contains a barrier)
         float mmb = 0.f;
 #pragma unroll
         for (int w = 0; w < NTH / 64; ++w) mmb = fmaxf(mmb, s_redb[step & 1][w]);
@@ -715,13 +722,15 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_halo_x_kernel(FwdParams p, H
         ea = ea2;
         eb = eb2;
         const float sb = ldexpf(1.f, eb);
+        if constexpr (!(DBG & 1)) {
 #pragma unroll
-        for (int k = 0; k < BX_IT; ++k) {
-            const int idx = tid + k * NTH;
-            split_put(s_b + (idx >> 3) * XPn, idx & 7, rb[k], sb);
+            for (int k = 0; k < BX_IT; ++k) {
+                const int idx = tid + k * NTH;
+                split_put(s_b + (idx >> 3) * XPn, idx & 7, rb[k], sb);
+            }
+            __syncthreads();
+            if (step + 1 < nsteps) load_b(step + 1);
         }
-        __syncthreads();
-        if (step + 1 < nsteps) load_b(step + 1);
         const int dy = p.offy[t] - h.oymin, dx = p.offx[t] - h.oxmin;
         const int col = (h.npar == 1) ? ml + dx : (dx & 1) * h.IXp + ml + (dx >> 1);
         const unsigned char *a_base[WM];
@@ -731,7 +740,7 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_halo_x_kernel(FwdParams p, H
             a_base[i] = s_a + ((p.smy * ty + dy) * h.IXt + col) * XPn + 16 * hl;
         }
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
+        for (int s2 = 0; s2 < ((DBG & 2) ? 0 : 2); ++s2) {
             f16x8 ah[WM], al[WM], al2[WM];
 #pragma unroll
             for (int i = 0; i < WM; ++i) {
@@ -759,7 +768,7 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_halo_x_kernel(FwdParams p, H
                 }
             }
         }
-        if (step + 1 < nsteps) publish_b((step + 1) & 1);
+        if (!(DBG & 1) && step + 1 < nsteps) publish_b((step + 1) & 1);
     }
 
     const long long per_img = (long long)p.MH * p.MW;
@@ -1376,10 +1385,10 @@ constexpr int HALO_LDS_MAX = 160 * 1024;
 // (sd: esr_dconv_fwd_sd) stages each source pixel once per 32 virtual channels — 8 real channels × 4 phases — so its
 // window fits 8-row tiles at two workgroups per CU; it takes the halo kernel under the same width rule.
 int g_dconv_halo = 1; // esr_dconv_set_halo: the halo-tile kernels where they apply (halo_wanted), every precision;
-                      // 2 = also the space-to-depth forms at any width (A/B)
+                      // 2 = also the space-to-depth forms and the >= 9-tap convs at any width (A/B)
 bool halo_wanted(int smy, int smx, int T, int MW, bool sd = false) {
     const int covered = 32 * ((MW + 31) / 32);
-    if (g_dconv_halo == 2 && sd && smy == 1 && smx == 1) return true;
+    if (g_dconv_halo == 2 && (sd || T >= 9) && smy == 1 && smx == 1) return true;
     return smy == 1 && smx == 1 && (T == 1 || T >= 9 || sd) && 10 * (covered - MW) <= 3 * MW;
 }
 
@@ -1494,11 +1503,30 @@ void launch_halo_f32(const FwdParams &p, const HaloParams &h, dim3 grid, int lds
     hipLaunchKernelGGL((dconv_fwd_halo_kernel<WM, WN>), grid, dim3(NTH), lds, st, p, h);
 }
 
+template <int WM, int WN, int NP, int NBX = NB, int DBG = 0>
+void launch_halo_x1(const FwdParams &p, const HaloParams &h, dim3 grid, int lds, hipStream_t st) {
+    static bool attr = false;
+    allow_full_lds(dconv_fwd_halo_x_kernel<WM, WN, NP, NBX, DBG>, attr);
+    hipLaunchKernelGGL((dconv_fwd_halo_x_kernel<WM, WN, NP, NBX, DBG>), grid, dim3(NTH), lds, st, p, h);
+}
+
 template <int WM, int WN, int NP, int NBX = NB>
 void launch_halo_x(const FwdParams &p, const HaloParams &h, dim3 grid, int lds, hipStream_t st) {
-    static bool attr = false;
-    allow_full_lds(dconv_fwd_halo_x_kernel<WM, WN, NP, NBX>, attr);
-    hipLaunchKernelGGL((dconv_fwd_halo_x_kernel<WM, WN, NP, NBX>), grid, dim3(NTH), lds, st, p, h);
+#ifdef ESR_X3_EXPERIMENTS  // ablations (garbage outputs): ESR_HALO_DBG = 1 / 2 / 4 / combinations (the DBG bits)
+    static const int dbg = getenv("ESR_HALO_DBG") ? atoi(getenv("ESR_HALO_DBG")) : 0;
+    if (NP == 2 && WM == 2) {
+        switch (dbg) {
+        case 1: return launch_halo_x1<WM, WN, NP, NBX, 1>(p, h, grid, lds, st);
+        case 2: return launch_halo_x1<WM, WN, NP, NBX, 2>(p, h, grid, lds, st);
+        case 3: return launch_halo_x1<WM, WN, NP, NBX, 3>(p, h, grid, lds, st);
+        case 4: return launch_halo_x1<WM, WN, NP, NBX, 4>(p, h, grid, lds, st);
+        case 5: return launch_halo_x1<WM, WN, NP, NBX, 5>(p, h, grid, lds, st);
+        case 6: return launch_halo_x1<WM, WN, NP, NBX, 6>(p, h, grid, lds, st);
+        default: break;
+        }
+    }
+#endif
+    launch_halo_x1<WM, WN, NP, NBX, 0>(p, h, grid, lds, st);
 }
 
 }  // namespace
@@ -1535,6 +1563,8 @@ extern "C" int esr_dconv_fwd_sd(const float *src, int32_t B, int32_t Hs, int32_t
     const bool sd = s2d_c || d2s_c;
     FwdParams p;
     p.s2c = s2d_c; p.s2pad = s2d_pad; p.d2c = d2s_c; p.d2pad = d2s_pad;
+    p.s2g = s2d_c % 32 == 0 ? 32 : s2d_c;  // the channel grouping of the space-to-depth views (include/esr_amd.h)
+    p.d2g = d2s_c % 32 == 0 ? 32 : d2s_c;
     p.src = src; p.B = B; p.Hs = Hs; p.Ws = Ws; p.sp = src_pitch; p.kc = kc;
     p.vec = (src_pitch % 4 == 0 && aligned16(src)) ? 1 : 0;
     p.w = w_packed; p.nck = nck; p.n_pad = n_pad; p.bias = bias;

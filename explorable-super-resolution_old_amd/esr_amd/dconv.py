@@ -142,11 +142,14 @@ def _s2d_form(k, s, C):
 
 
 def _s2d_weights(w):
-    """w [Co][Ci][k][k] -> [(k/2)²][(py, px, ci) = 4Ci][Co]: tap (a, b) of the space-to-depth form holds
-    w[:, :, 2a + py, 2b + px]."""
+    """w [Co][Ci][k][k] -> [(k/2)²][4Ci][Co]: tap (a, b) of the space-to-depth form holds w[:, :, 2a + py, 2b + px] at
+    virtual channel (ci / G)·4G + (2py + px)·G + ci % G, G = 32 if 32 | Ci else Ci (include/esr_amd.h
+    esr_dconv_fwd_sd: a 32-channel K chunk is then 32 channels of one real pixel)."""
     Co, Ci, k, _ = w.shape
     h = k // 2
-    return w.permute(2, 3, 1, 0).reshape(h, 2, h, 2, Ci, Co).permute(0, 2, 1, 3, 4, 5).reshape(h * h, 4 * Ci, Co)
+    G = 32 if Ci % 32 == 0 else Ci
+    wt = w.permute(2, 3, 1, 0).reshape(h, 2, h, 2, Ci // G, G, Co)  # [a][py][b][px][cb][cg][co]
+    return wt.permute(0, 2, 4, 1, 3, 5, 6).reshape(h * h, 4 * Ci, Co)
 
 
 def conv_forward(x, w, b, k, s, p):

@@ -302,14 +302,16 @@ int esr_dconv_fwd_splits(int32_t B, int32_t MH, int32_t MW, int32_t n_out, int32
                          int32_t T, const int32_t *offy, const int32_t *offx);
 /* esr_dconv_fwd_sk over a space-to-depth source and/or into a depth-to-space output: a k×k stride-2 conv (k even) as
  * a (k/2)×(k/2)-tap stride-1 one with 4× the channels, the form the halo-tile kernel stages once per source pixel.
+ *   Virtual channel order: v(py, px, c) = (c / G)·4G + (2·py + px)·G + c % G with G = 32 where the real channel
+ *   count is a multiple of 32 (a 32-channel K chunk is then 128 contiguous bytes of one real pixel), else G = it.
  *   s2d_c > 0 (forward): src is the REAL [B][Hs][Ws][src_pitch] input with s2d_c channels (a multiple of 4) and
- *     kc = 4·s2d_c; virtual channel (2·py + px)·s2d_c + c of virtual pixel (sy, sx) = src[b, 2·sy + py - s2d_pad,
- *     2·sx + px - s2d_pad, c] (zero outside), so with W[(a, b)][(py, px, c)][n] = w[n][c][2a + py][2b + px],
+ *     kc = 4·s2d_c; virtual channel v(py, px, c) of virtual pixel (sy, sx) = src[b, 2·sy + py - s2d_pad,
+ *     2·sx + px - s2d_pad, c] (zero outside), so with W[(a, b)][v(py, px, c)][n] = w[n][c][2a + py][2b + px],
  *     offy = a, offx = b, smy = smx = 1 this is conv2d(src, w, stride 2, padding s2d_pad).
  *   d2s_c > 0 (data gradient): n_out = 4·d2s_c, out is the REAL [B][Ho][Wo][out_pitch] input gradient; virtual
- *     channel (2·py + px)·d2s_c + c of grid point (Y, X) goes to out[b, 2·Y + py - d2s_pad, 2·X + px - d2s_pad, c]
+ *     channel v(py, px, c) of grid point (Y, X) goes to out[b, 2·Y + py - d2s_pad, 2·X + px - d2s_pad, c]
  *     (dropped outside); omy = omx = 1, oay = oax = 0, no bias.  With src = dL/dy, offy = -a, offx = -b and
- *     W[(a, b)][co][(py, px, c)] = w[co][c][2a + py][2b + px] over MH × MW = ((H-1+pad)/2 + 1) × ((W-1+pad)/2 + 1)
+ *     W[(a, b)][co][v(py, px, c)] = w[co][c][2a + py][2b + px] over MH × MW = ((H-1+pad)/2 + 1) × ((W-1+pad)/2 + 1)
  *     this is the transposed conv in one launch (replaces the per-phase-class calls of esr_dconv_fwd).
  * Replaces: the D's 4×4 stride-2 conv_block convs (architecture.py:232-250, block.py:129-156) and their gradients. */
 int esr_dconv_fwd_sd(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t src_pitch, int32_t kc,
