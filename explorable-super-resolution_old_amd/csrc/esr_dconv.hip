@@ -63,8 +63,8 @@ struct FwdParams {
     int T;
     int offy[MAXT], offx[MAXT];
     float *partial;  // split-K (x3 kernel, gridDim.z > 1): [z][M][n_pad] raw sums, reduced by dconv_splitk_reduce
-    int s2c, s2pad, s2g;  // > 0: space-to-depth source (src_quad), channel group s2g; 0: plain
-    int d2c, d2pad, d2g;  // > 0: depth-to-space output (put_out), channel group d2g; 0: plain
+    int s2c, s2pad, s2g, s2sh;  // > 0: space-to-depth source (src_quad), channel group s2g = 2^s2sh (s2sh < 0: not
+    int d2c, d2pad, d2g, d2sh;  // a power of two); d2*: depth-to-space output (put_out); 0: plain
 };
 
 __device__ __forceinline__ f32x4 load4(const float *row, int c, int kc, bool vec) {
@@ -85,9 +85,14 @@ __device__ __forceinline__ f32x4 load4(const float *row, int c, int kc, bool vec
 __device__ __forceinline__ f32x4 src_quad(const FwdParams &p, int b, int sy, int sx, int c, bool vec) {
     int kc = p.kc;
     if (p.s2c) {
-        const int ph = (c / p.s2g) & 3;
-        c = (c / (4 * p.s2g)) * p.s2g + c % p.s2g;
-        if (c >= p.s2c) c = p.s2c;  // past the last group (kc padding): reads as zero below
+        int ph;
+        if (p.s2sh >= 0) {  // shifts: this runs for every staged quad
+            ph = (c >> p.s2sh) & 3;
+            c = ((c >> (p.s2sh + 2)) << p.s2sh) | (c & (p.s2g - 1));
+        } else {
+            ph = (c / p.s2g) & 3;
+            c = (c / (4 * p.s2g)) * p.s2g + c % p.s2g;
+        }  // (past the last group — kc padding — c >= s2c: reads as zero below)
         sy = 2 * sy + (ph >> 1) - p.s2pad;
         sx = 2 * sx + (ph & 1) - p.s2pad;
         kc = p.s2c;
@@ -104,8 +109,14 @@ __device__ __forceinline__ f32x4 src_quad(const FwdParams &p, int b, int sy, int
 __device__ __forceinline__ void put_out(const FwdParams &p, int b, int Y, int X, int n, float v) {
     int oy = p.omy * Y + p.oay, ox = p.omx * X + p.oax;
     if (p.d2c) {
-        const int ph = (n / p.d2g) & 3;
-        n = (n / (4 * p.d2g)) * p.d2g + n % p.d2g;
+        int ph;
+        if (p.d2sh >= 0) {  // shifts: this runs for every output element
+            ph = (n >> p.d2sh) & 3;
+            n = ((n >> (p.d2sh + 2)) << p.d2sh) | (n & (p.d2g - 1));
+        } else {
+            ph = (n / p.d2g) & 3;
+            n = (n / (4 * p.d2g)) * p.d2g + n % p.d2g;
+        }
         oy = 2 * oy + (ph >> 1) - p.d2pad;
         ox = 2 * ox + (ph & 1) - p.d2pad;
         if (oy < 0 || oy >= p.Ho || ox < 0 || ox >= p.Wo) return;
@@ -198,23 +209,28 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_kernel(FwdParams p) {
         }
     }
 
-    // D layout (32x32 f32 MFMA): lane holds column n = lane & 31, rows m = (r&3) + 8(r>>2) + 4(lane>>5)
+    // D layout (32x32 f32 MFMA): lane holds column n = lane & 31, rows m = (r&3) + 8(r>>2) + 4(lane>>5); the output
+    // pixel of each row is decoded once for all N-tiles (32-bit: M < 2^31 is checked at launch)
+    float bn[2];
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
         const int n = n0 + nt * 32 + ml;
-        if (n >= p.n) continue;
-        const float bn = p.bias ? p.bias[n] : 0.f;
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const long long m = m0 + 64 * wave + 32 * mt + (r & 3) + 8 * (r >> 2) + 4 * hl;
-                if (m >= M) continue;
-                const int b = (int)(m / per_img), rr = (int)(m - (long long)b * per_img);
-                const int Y = rr / p.MW, X = rr - (rr / p.MW) * p.MW;
-                put_out(p, b, Y, X, n, acc[mt][nt][r] + bn);
-            }
+        bn[nt] = (p.bias && n < p.n) ? p.bias[n] : 0.f;
     }
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = (int)m0 + 64 * wave + 32 * mt + (r & 3) + 8 * (r >> 2) + 4 * hl;
+            if (m >= (int)M) continue;
+            const int b = m / per_img, rr = m - b * per_img;
+            const int Y = rr / p.MW, X = rr - Y * p.MW;
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {
+                const int n = n0 + nt * 32 + ml;
+                if (n < p.n) put_out(p, b, Y, X, n, acc[mt][nt][r] + bn[nt]);
+            }
+        }
 }
 
 // ---- halo-tile forward (exact fp32, the default) -----------------------------------------------------------------------
@@ -554,22 +570,26 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_x3_kernel(FwdParams p) {
                 }
         return;
     }
+    float bn[NTN];  // the output pixel of each row is decoded once for all N-tiles (32-bit: M < 2^31 at launch)
 #pragma unroll
     for (int nt = 0; nt < NTN; ++nt) {
         const int n = n0 + nt * 32 + ml;
-        if (n >= p.n) continue;
-        const float bn = p.bias ? p.bias[n] : 0.f;
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const long long m = m0 + 64 * wave + 32 * mt + (r & 3) + 8 * (r >> 2) + 4 * hl;
-                if (m >= M) continue;
-                const int b = (int)(m / per_img), rr = (int)(m - (long long)b * per_img);
-                const int Y = rr / p.MW, X = rr - (rr / p.MW) * p.MW;
-                put_out(p, b, Y, X, n, ldexpf(acc[mt][nt][r], -(ea + eb)) + bn);
-            }
+        bn[nt] = (p.bias && n < p.n) ? p.bias[n] : 0.f;
     }
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = (int)m0 + 64 * wave + 32 * mt + (r & 3) + 8 * (r >> 2) + 4 * hl;
+            if (m >= (int)M) continue;
+            const int b = m / per_img, rr = m - b * per_img;
+            const int Y = rr / p.MW, X = rr - Y * p.MW;
+#pragma unroll
+            for (int nt = 0; nt < NTN; ++nt) {
+                const int n = n0 + nt * 32 + ml;
+                if (n < p.n) put_out(p, b, Y, X, n, ldexpf(acc[mt][nt][r], -(ea + eb)) + bn[nt]);
+            }
+        }
 }
 
 
@@ -583,8 +603,8 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_x3_kernel(FwdParams p) {
 // fragment; taken for x3 where n_pad allows and the grid still fills the chip).  TY = WM·WN·128 / NBX rows.
 // DBG (experiment build only, garbage outputs): 1 = no weight-slab staging (no loads, max, split, stores; one barrier
 // per chunk), 2 = no fragment reads / MFMAs, 4 = the halo window staged for the first chunk only
-template <int WM, int WN, int NP, int NBX = NB, int DBG = 0>
-__global__ __launch_bounds__(NTH, 2) void dconv_fwd_halo_x_kernel(FwdParams p, HaloParams h) {
+template <int WM, int WN, int NP, int NBX = NB, int DBG = 0, int OCC = 2>
+__global__ __launch_bounds__(NTH, OCC) void dconv_fwd_halo_x_kernel(FwdParams p, HaloParams h) {
     constexpr int TY = WM * WN * 128 / NBX, MWV = TY / WM, XPn = XPitch<NP>::v, BX_IT = NBX * KC / 4 / NTH;
     static_assert((TY / WM) * (NBX / 32 / WN) == NTH / 64, "waves along M x waves along N = 4");
     extern __shared__ __attribute__((aligned(16))) unsigned char xlds[];
@@ -1496,6 +1516,8 @@ bool launch_rows_np(const WrowParams &p, const RowsPlan &r, dim3 grid, hipStream
     return true;
 }
 
+int g_dconv_occ3 = 1;  // esr_dconv_set_occ3 (A/B)
+
 template <int WM, int WN>
 void launch_halo_f32(const FwdParams &p, const HaloParams &h, dim3 grid, int lds, hipStream_t st) {
     static bool attr = false;
@@ -1503,11 +1525,11 @@ void launch_halo_f32(const FwdParams &p, const HaloParams &h, dim3 grid, int lds
     hipLaunchKernelGGL((dconv_fwd_halo_kernel<WM, WN>), grid, dim3(NTH), lds, st, p, h);
 }
 
-template <int WM, int WN, int NP, int NBX = NB, int DBG = 0>
+template <int WM, int WN, int NP, int NBX = NB, int DBG = 0, int OCC = 2>
 void launch_halo_x1(const FwdParams &p, const HaloParams &h, dim3 grid, int lds, hipStream_t st) {
     static bool attr = false;
-    allow_full_lds(dconv_fwd_halo_x_kernel<WM, WN, NP, NBX, DBG>, attr);
-    hipLaunchKernelGGL((dconv_fwd_halo_x_kernel<WM, WN, NP, NBX, DBG>), grid, dim3(NTH), lds, st, p, h);
+    allow_full_lds(dconv_fwd_halo_x_kernel<WM, WN, NP, NBX, DBG, OCC>, attr);
+    hipLaunchKernelGGL((dconv_fwd_halo_x_kernel<WM, WN, NP, NBX, DBG, OCC>), grid, dim3(NTH), lds, st, p, h);
 }
 
 template <int WM, int WN, int NP, int NBX = NB>
@@ -1526,6 +1548,10 @@ void launch_halo_x(const FwdParams &p, const HaloParams &h, dim3 grid, int lds, 
         }
     }
 #endif
+    // three workgroups per CU where the window + weight slab fit a third of the LDS (the space-to-depth forms at
+    // 8-row tiles: 52 KB) and the kernel a third of the VGPRs (profiles/r3_dconv_occ3_ab.txt)
+    if (NP == 2 && NBX == 64 && WM == 2 && g_dconv_occ3 && lds <= 160 * 1024 / 3)
+        return launch_halo_x1<WM, WN, NP, NBX, 0, 3>(p, h, grid, lds, st);
     launch_halo_x1<WM, WN, NP, NBX, 0>(p, h, grid, lds, st);
 }
 
@@ -1565,6 +1591,11 @@ extern "C" int esr_dconv_fwd_sd(const float *src, int32_t B, int32_t Hs, int32_t
     p.s2c = s2d_c; p.s2pad = s2d_pad; p.d2c = d2s_c; p.d2pad = d2s_pad;
     p.s2g = s2d_c % 32 == 0 ? 32 : s2d_c;  // the channel grouping of the space-to-depth views (include/esr_amd.h)
     p.d2g = d2s_c % 32 == 0 ? 32 : d2s_c;
+    p.s2sh = p.d2sh = -1;
+    for (int e = 0; e < 31; ++e) {
+        if (p.s2g == (1 << e)) p.s2sh = e;
+        if (p.d2g == (1 << e)) p.d2sh = e;
+    }
     p.src = src; p.B = B; p.Hs = Hs; p.Ws = Ws; p.sp = src_pitch; p.kc = kc;
     p.vec = (src_pitch % 4 == 0 && aligned16(src)) ? 1 : 0;
     p.w = w_packed; p.nck = nck; p.n_pad = n_pad; p.bias = bias;
@@ -1575,7 +1606,7 @@ extern "C" int esr_dconv_fwd_sd(const float *src, int32_t B, int32_t Hs, int32_t
     p.partial = partial;
     const long long M = (long long)B * MH * MW;
     const long long gx = (M + MT - 1) / MT;
-    if (gx > 0x7fffffff) return ESR_EINVAL;
+    if (M + MT >= 0x7fffffffLL) return ESR_EINVAL;  // the kernels index output pixels in 32 bits
     HaloParams h;
     int lds = 0;
     const int np = g_dconv_x3 ? g_dconv_np : 0;
@@ -1706,6 +1737,13 @@ extern "C" int esr_dconv_set_rows(int32_t on) {
     if (on < 0 || on > 1) return ESR_EINVAL;
     const int prev = g_dconv_rows;
     g_dconv_rows = on;
+    return prev;
+}
+
+extern "C" int esr_dconv_set_occ3(int32_t on) {
+    if (on < 0 || on > 1) return ESR_EINVAL;
+    const int prev = g_dconv_occ3;
+    g_dconv_occ3 = on;
     return prev;
 }
 

@@ -107,6 +107,7 @@ _SIGNATURES = {
     'esr_dconv_fwd_splits_sd': [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_int),
                                 ctypes.POINTER(c_int), c_int],
     'esr_dconv_set_halo': [c_int],
+    'esr_dconv_set_occ3': [c_int],
     'esr_dconv_wgrad_splits': [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_int),
                                ctypes.POINTER(c_int)],
     'esr_dconv_set_rows': [c_int],

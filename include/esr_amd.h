@@ -332,6 +332,9 @@ int esr_dconv_fwd_splits_sd(int32_t B, int32_t MH, int32_t MW, int32_t n_out, in
  * for stride-1 launches with one tap or >= 9 taps where the halo fits in LDS, the gather kernels otherwise; 0 = the
  * gather kernels always (A/B).  Returns the previous setting. */
 int esr_dconv_set_halo(int32_t on);
+/* x3 halo kernel with 64-wide N tiles at three workgroups per CU where its LDS allows (the space-to-depth forms):
+ * 1 (default) / 0 (two per CU, A/B).  Bitwise identical.  Returns the previous setting, or ESR_EINVAL. */
+int esr_dconv_set_occ3(int32_t on);
 /* Precision of esr_dconv_fwd (process-wide): 0 (the library default) = exact fp32 MFMA; 1 = x3: both operands split
  * into f16 hi/lo at staging after a power-of-two scaling per K step (one tap × 32 channels) chosen from the
  * workgroup's max |a| and max |b|, products hi·hi + hi·lo + lo·hi on f16 MFMA, the fp32 accumulators rescaled exactly
