@@ -50,11 +50,16 @@ def set_precision(p):
     return prev
 
 
+# x3 halo kernel at three workgroups per CU where its LDS allows (esr_dconv_set_occ3); '0' = two (A/B)
+OCC3 = os.environ.get('ESR_DCONV_OCC3', '1') != '0'
+
+
 def _lib_for_launch():
     lib = _lib.load()
     if _applied[0] != PRECISION:
         lib.esr_dconv_set_x3(_LIB_MODE[PRECISION])
         lib.esr_dconv_set_halo(1 if HALO else 0)
+        lib.esr_dconv_set_occ3(1 if OCC3 else 0)
         _applied[0] = PRECISION
     return lib
 
