@@ -250,6 +250,7 @@ struct HaloParams {
     int IY, IXp, npar, IXt;    // halo rows; columns per parity; parities (= smx); IXt = npar·IXp
     int oymin, oxmin;          // smallest tap offsets
     int b_off;                 // byte offset of the weight slab in LDS
+    int cw;                    // tile columns (32; 16: two rows per M-tile, dconv_fwd_halo_x_kernel CW)
 };
 
 template <int WM, int WN>
@@ -603,9 +604,12 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_x3_kernel(FwdParams p) {
 // fragment; taken for x3 where n_pad allows and the grid still fills the chip).  TY = WM·WN·128 / NBX rows.
 // DBG (experiment build only, garbage outputs): 1 = no weight-slab staging (no loads, max, split, stores; one barrier
 // per chunk), 2 = no fragment reads / MFMAs, 4 = the halo window staged for the first chunk only
-template <int WM, int WN, int NP, int NBX = NB, int DBG = 0, int OCC = 2>
+// CW = 16: an M-tile is 2 rows × 16 columns (stride-1 sources only), for grids whose width 32-column tiles would cover
+// with > 30 % waste (the 38-wide conv2_1 / fc8 layers at config 3); a tile is then 2·TY rows × 16 columns.
+template <int WM, int WN, int NP, int NBX = NB, int DBG = 0, int OCC = 2, int CW = 32>
 __global__ __launch_bounds__(NTH, OCC) void dconv_fwd_halo_x_kernel(FwdParams p, HaloParams h) {
     constexpr int TY = WM * WN * 128 / NBX, MWV = TY / WM, XPn = XPitch<NP>::v, BX_IT = NBX * KC / 4 / NTH;
+    constexpr int RPM = 32 / CW;  // output rows per M-tile
     static_assert((TY / WM) * (NBX / 32 / WN) == NTH / 64, "waves along M x waves along N = 4");
     extern __shared__ __attribute__((aligned(16))) unsigned char xlds[];
     __shared__ float s_reda[NTH / 64], s_redb[2][NTH / 64];  // per-wave max of the halo / of the weight slab
@@ -615,7 +619,7 @@ __global__ __launch_bounds__(NTH, OCC) void dconv_fwd_halo_x_kernel(FwdParams p,
     const int txi = id % h.tiles_x;
     id /= h.tiles_x;
     const int tyi = id % h.tiles_y, b = id / h.tiles_y;
-    const int Y0 = tyi * TY, X0 = txi * 32;
+    const int Y0 = tyi * TY * RPM, X0 = txi * CW;
     const int n0 = blockIdx.y * NBX;
     const int wm = wave % MWV, wn = wave / MWV;
     const bool vec = p.vec != 0;
@@ -752,12 +756,13 @@ __global__ __launch_bounds__(NTH, OCC) void dconv_fwd_halo_x_kernel(FwdParams p,
             if (step + 1 < nsteps) load_b(step + 1);
         }
         const int dy = p.offy[t] - h.oymin, dx = p.offx[t] - h.oxmin;
-        const int col = (h.npar == 1) ? ml + dx : (dx & 1) * h.IXp + ml + (dx >> 1);
+        const int mc = ml % CW, mr = ml / CW;  // the lane's M row: column mc of tile row mr of its M-tile
+        const int col = (h.npar == 1) ? mc + dx : (dx & 1) * h.IXp + mc + (dx >> 1);
         const unsigned char *a_base[WM];
 #pragma unroll
         for (int i = 0; i < WM; ++i) {
             const int ty = wm * WM + i;
-            a_base[i] = s_a + ((p.smy * ty + dy) * h.IXt + col) * XPn + 16 * hl;
+            a_base[i] = s_a + ((p.smy * (RPM * ty + mr) + dy) * h.IXt + col) * XPn + 16 * hl;
         }
 #pragma unroll
         for (int s2 = 0; s2 < ((DBG & 2) ? 0 : 2); ++s2) {
@@ -795,8 +800,8 @@ __global__ __launch_bounds__(NTH, OCC) void dconv_fwd_halo_x_kernel(FwdParams p,
     const int ue = -(ea + eb);
 #pragma unroll
     for (int i = 0; i < WM; ++i) {
-        const int Y = Y0 + wm * WM + i;
-        if (Y >= p.MH) continue;
+        const int Yt = Y0 + RPM * (wm * WM + i);  // first output row of M-tile i
+        if (Yt >= p.MH) continue;
 #pragma unroll
         for (int k = 0; k < WN; ++k) {
             const int n = n0 + (wn * WN + k) * 32 + ml;
@@ -804,8 +809,10 @@ __global__ __launch_bounds__(NTH, OCC) void dconv_fwd_halo_x_kernel(FwdParams p,
                 float *part = p.partial + (long long)blockIdx.z * p.B * per_img * p.n_pad;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    const int X = X0 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-                    if (X < p.MW) part[(b * per_img + (long long)Y * p.MW + X) * p.n_pad + n] = ldexpf(acc[i][k][r], ue);
+                    const int m = (r & 3) + 8 * (r >> 2) + 4 * hl;
+                    const int Y = Yt + m / CW, X = X0 + m % CW;
+                    if (X < p.MW && Y < p.MH)
+                        part[(b * per_img + (long long)Y * p.MW + X) * p.n_pad + n] = ldexpf(acc[i][k][r], ue);
                 }
                 continue;
             }
@@ -813,8 +820,9 @@ __global__ __launch_bounds__(NTH, OCC) void dconv_fwd_halo_x_kernel(FwdParams p,
             const float bn = p.bias ? p.bias[n] : 0.f;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int X = X0 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-                if (X < p.MW) put_out(p, b, Y, X, n, ldexpf(acc[i][k][r], ue) + bn);
+                const int m = (r & 3) + 8 * (r >> 2) + 4 * hl;
+                const int Y = Yt + m / CW, X = X0 + m % CW;
+                if (X < p.MW && Y < p.MH) put_out(p, b, Y, X, n, ldexpf(acc[i][k][r], ue) + bn);
             }
         }
     }
@@ -1412,11 +1420,26 @@ bool halo_wanted(int smy, int smx, int T, int MW, bool sd = false) {
     return smy == 1 && smx == 1 && (T == 1 || T >= 9 || sd) && 10 * (covered - MW) <= 3 * MW;
 }
 
+int g_dconv_cw16 = 1;  // esr_dconv_set_cw16: the 16-column halo tiles where 32-column ones do not pay (A/B)
+
+// Tile width of the halo kernel for a launch: 32, 16 (x3 only: 2 rows × 16 columns per M-tile where a 16-column grid
+// meets the ≤ 30 % waste rule and a 32-column one does not — fc8's data gradient on the 38-wide grid at config 3:
+// 903 -> 651 us, profiles/r3_dconv_cw16_ab.txt), or 0 for the gather kernel.
+int halo_cols(int smy, int smx, int T, int MW, bool sd, int np) {
+    if (!g_dconv_halo) return 0;
+    if (halo_wanted(smy, smx, T, MW, sd)) return 32;
+    const int c16 = 16 * ((MW + 15) / 16);
+    if (np == 2 && g_dconv_cw16 && smy == 1 && smx == 1 && (T == 1 || T >= 9) && 10 * (c16 - MW) <= 3 * MW)
+        return 16;  // (not the 4-tap space-to-depth forms: slower than their gather at MW 38 / 39, r3_dconv_cw16_ab)
+    return 0;
+}
+
 // Halo tiling of an esr_dconv_fwd launch with `pitch` LDS bytes per staged pixel row (144: fp32 / x3, 208: x6):
 // false if the gather kernel has to run it (stride > 2, or a halo that does not fit in LDS even at 2-row tiles).
 bool halo_plan(int MH, int MW, int smy, int smx, int T, const int32_t *offy, const int32_t *offx, HaloParams &h,
-               int &lds, int pitch = PS * 4, int nbx = NB) {
-    if (smy < 1 || smy > 2 || smx < 1 || smx > 2) return false;
+               int &lds, int pitch = PS * 4, int nbx = NB, int cw = 32) {
+    if (smy < 1 || smy > 2 || smx < 1 || smx > 2 || (cw == 16 && smx != 1)) return false;
+    const int rpm = 32 / cw;  // output rows per M-tile
     int ymin = offy[0], ymax = offy[0], xmin = offx[0], xmax = offx[0];
     for (int t = 1; t < T; ++t) {
         ymin = min(ymin, (int)offy[t]); ymax = max(ymax, (int)offy[t]);
@@ -1425,21 +1448,22 @@ bool halo_plan(int MH, int MW, int smy, int smx, int T, const int32_t *offy, con
     h.oymin = ymin;
     h.oxmin = xmin;
     h.npar = smx;
-    h.IXp = smx == 1 ? 32 + (xmax - xmin) : 32 + ((xmax - xmin) >> 1);
+    h.IXp = smx == 1 ? cw + (xmax - xmin) : 32 + ((xmax - xmin) >> 1);
     h.IXt = h.npar * h.IXp;
     const int b_bytes = nbx * pitch;
     for (int pass = 0; pass < 2; ++pass) {
         const int budget = pass == 0 ? HALO_LDS_2PER_CU : HALO_LDS_MAX;
         for (int ty = 8; ty >= 2; ty >>= 1) {
-            if (ty > 2 && MH <= ty / 2) continue;  // a shorter tile wastes fewer rows
-            const int iy = smy * (ty - 1) + (ymax - ymin) + 1;
+            if (ty > 2 && MH <= rpm * ty / 2) continue;  // a shorter tile wastes fewer rows
+            const int iy = smy * (rpm * ty - 1) + (ymax - ymin) + 1;
             const int a_bytes = iy * h.IXt * pitch;
             if (a_bytes + b_bytes <= budget) {
                 h.TY = ty;
                 h.IY = iy;
                 h.b_off = a_bytes;
-                h.tiles_x = (MW + 31) / 32;
-                h.tiles_y = (MH + ty - 1) / ty;
+                h.tiles_x = (MW + cw - 1) / cw;
+                h.tiles_y = (MH + rpm * ty - 1) / (rpm * ty);
+                h.cw = cw;
                 lds = a_bytes + b_bytes;
                 return true;
             }
@@ -1525,15 +1549,22 @@ void launch_halo_f32(const FwdParams &p, const HaloParams &h, dim3 grid, int lds
     hipLaunchKernelGGL((dconv_fwd_halo_kernel<WM, WN>), grid, dim3(NTH), lds, st, p, h);
 }
 
-template <int WM, int WN, int NP, int NBX = NB, int DBG = 0, int OCC = 2>
+template <int WM, int WN, int NP, int NBX = NB, int DBG = 0, int OCC = 2, int CW = 32>
 void launch_halo_x1(const FwdParams &p, const HaloParams &h, dim3 grid, int lds, hipStream_t st) {
     static bool attr = false;
-    allow_full_lds(dconv_fwd_halo_x_kernel<WM, WN, NP, NBX, DBG, OCC>, attr);
-    hipLaunchKernelGGL((dconv_fwd_halo_x_kernel<WM, WN, NP, NBX, DBG, OCC>), grid, dim3(NTH), lds, st, p, h);
+    allow_full_lds(dconv_fwd_halo_x_kernel<WM, WN, NP, NBX, DBG, OCC, CW>, attr);
+    hipLaunchKernelGGL((dconv_fwd_halo_x_kernel<WM, WN, NP, NBX, DBG, OCC, CW>), grid, dim3(NTH), lds, st, p, h);
 }
 
 template <int WM, int WN, int NP, int NBX = NB>
 void launch_halo_x(const FwdParams &p, const HaloParams &h, dim3 grid, int lds, hipStream_t st) {
+    if constexpr (NP == 2 && NBX == 64) {
+        if (h.cw == 16) {  // 16-column tiles (halo_cols)
+            if (g_dconv_occ3 && lds <= 160 * 1024 / 3)
+                return launch_halo_x1<WM, WN, NP, NBX, 0, 3, 16>(p, h, grid, lds, st);
+            return launch_halo_x1<WM, WN, NP, NBX, 0, 2, 16>(p, h, grid, lds, st);
+        }
+    }
 #ifdef ESR_X3_EXPERIMENTS  // ablations (garbage outputs): ESR_HALO_DBG = 1 / 2 / 4 / combinations (the DBG bits)
     static const int dbg = getenv("ESR_HALO_DBG") ? atoi(getenv("ESR_HALO_DBG")) : 0;
     if (NP == 2 && WM == 2) {
@@ -1550,8 +1581,9 @@ void launch_halo_x(const FwdParams &p, const HaloParams &h, dim3 grid, int lds, 
 #endif
     // three workgroups per CU where the window + weight slab fit a third of the LDS (the space-to-depth forms at
     // 8-row tiles: 52 KB) and the kernel a third of the VGPRs (profiles/r3_dconv_occ3_ab.txt)
-    if (NP == 2 && NBX == 64 && WM == 2 && g_dconv_occ3 && lds <= 160 * 1024 / 3)
-        return launch_halo_x1<WM, WN, NP, NBX, 0, 3>(p, h, grid, lds, st);
+    if constexpr (NP == 2 && NBX == 64 && WM == 2) {
+        if (g_dconv_occ3 && lds <= 160 * 1024 / 3) return launch_halo_x1<WM, WN, NP, NBX, 0, 3>(p, h, grid, lds, st);
+    }
     launch_halo_x1<WM, WN, NP, NBX, 0>(p, h, grid, lds, st);
 }
 
@@ -1610,8 +1642,8 @@ extern "C" int esr_dconv_fwd_sd(const float *src, int32_t B, int32_t Hs, int32_t
     HaloParams h;
     int lds = 0;
     const int np = g_dconv_x3 ? g_dconv_np : 0;
-    if (g_dconv_halo && halo_wanted(smy, smx, T, MW, sd) &&
-        halo_plan(MH, MW, smy, smx, T, offy, offx, h, lds, np == 3 ? XPitch<3>::v : PS * 4)) {
+    const int cwh = halo_cols(smy, smx, T, MW, sd, np);
+    if (cwh && halo_plan(MH, MW, smy, smx, T, offy, offx, h, lds, np == 3 ? XPitch<3>::v : PS * 4, NB, cwh)) {
         if (ksplit > nck) return ESR_EINVAL;  // the halo kernels split the channel chunks
         const long long hx = (long long)B * h.tiles_x * h.tiles_y;
         if (hx > 0x7fffffff) return ESR_EINVAL;
@@ -1626,7 +1658,7 @@ extern "C" int esr_dconv_fwd_sd(const float *src, int32_t B, int32_t Hs, int32_t
             // has >= 512 workgroups without a split (profiles/r3_dconv_nb128_ab.txt)
             HaloParams h2;
             int lds2 = 0;
-            if (g_dconv_nb != 64 && ksplit == 1 && n_pad % 128 == 0 && h.TY == 8 && hx * (n_pad / 128) >= 512 &&
+            if (h.cw == 32 && g_dconv_nb != 64 && ksplit == 1 && n_pad % 128 == 0 && h.TY == 8 && hx * (n_pad / 128) >= 512 &&
                 halo_plan(MH, MW, smy, smx, T, offy, offx, h2, lds2, PS * 4, 128) && h2.TY == 8 &&
                 lds2 <= HALO_LDS_2PER_CU) {
                 launch_halo_x<2, 4, 2, 128>(p, h2, dim3((unsigned)hx, (unsigned)(n_pad / 128), 1), lds2, st);
@@ -1692,8 +1724,8 @@ extern "C" int esr_dconv_fwd_splits_sd(int32_t B, int32_t MH, int32_t MW, int32_
     HaloParams h;
     int lds = 0;
     const int np = g_dconv_x3 ? g_dconv_np : 0;
-    if (g_dconv_halo && halo_wanted(smy, smx, T, MW, sd != 0) &&
-        halo_plan(MH, MW, smy, smx, T, offy, offx, h, lds, np == 3 ? XPitch<3>::v : PS * 4))
+    const int cwh = halo_cols(smy, smx, T, MW, sd != 0, np);
+    if (cwh && halo_plan(MH, MW, smy, smx, T, offy, offx, h, lds, np == 3 ? XPitch<3>::v : PS * 4, NB, cwh))
         return halo_splits(h, B, n_pad, nck);
     if (!g_dconv_x3) return 1;
     // x3 gather kernel: ~512 workgroups, at least 8 K steps per slice, for launches that would fill few CUs
@@ -1705,7 +1737,7 @@ extern "C" int esr_dconv_fwd_splits_sd(int32_t B, int32_t MH, int32_t MW, int32_
 
 extern "C" int esr_dconv_uses_halo(int32_t smy, int32_t smx, int32_t T, int32_t MW, int32_t sd) {
     if (T <= 0 || T > ESR_DCONV_MAX_TAPS || MW <= 0) return ESR_EINVAL;
-    return g_dconv_halo && halo_wanted(smy, smx, T, MW, sd != 0) ? 1 : 0;
+    return halo_cols(smy, smx, T, MW, sd != 0, g_dconv_x3 ? g_dconv_np : 0) ? 1 : 0;
 }
 
 extern "C" int esr_dconv_fwd_splits(int32_t B, int32_t MH, int32_t MW, int32_t n, int32_t kc, int32_t smy,
@@ -1737,6 +1769,13 @@ extern "C" int esr_dconv_set_rows(int32_t on) {
     if (on < 0 || on > 1) return ESR_EINVAL;
     const int prev = g_dconv_rows;
     g_dconv_rows = on;
+    return prev;
+}
+
+extern "C" int esr_dconv_set_cw16(int32_t on) {
+    if (on < 0 || on > 1) return ESR_EINVAL;
+    const int prev = g_dconv_cw16;
+    g_dconv_cw16 = on;
     return prev;
 }
 

@@ -108,6 +108,7 @@ _SIGNATURES = {
                                 ctypes.POINTER(c_int), c_int],
     'esr_dconv_set_halo': [c_int],
     'esr_dconv_set_occ3': [c_int],
+    'esr_dconv_set_cw16': [c_int],
     'esr_dconv_wgrad_splits': [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_int),
                                ctypes.POINTER(c_int)],
     'esr_dconv_set_rows': [c_int],

@@ -52,6 +52,8 @@ def set_precision(p):
 
 # x3 halo kernel at three workgroups per CU where its LDS allows (esr_dconv_set_occ3); '0' = two (A/B)
 OCC3 = os.environ.get('ESR_DCONV_OCC3', '1') != '0'
+# x3 halo kernel with 16-column tiles on narrow grids (esr_dconv_set_cw16); '0' = the gather kernel there (A/B)
+CW16 = os.environ.get('ESR_DCONV_CW16', '1') != '0'
 
 
 def _lib_for_launch():
@@ -60,6 +62,7 @@ def _lib_for_launch():
         lib.esr_dconv_set_x3(_LIB_MODE[PRECISION])
         lib.esr_dconv_set_halo(1 if HALO else 0)
         lib.esr_dconv_set_occ3(1 if OCC3 else 0)
+        lib.esr_dconv_set_cw16(1 if CW16 else 0)
         _applied[0] = PRECISION
     return lib
 

@@ -335,6 +335,10 @@ int esr_dconv_set_halo(int32_t on);
 /* x3 halo kernel with 64-wide N tiles at three workgroups per CU where its LDS allows (the space-to-depth forms):
  * 1 (default) / 0 (two per CU, A/B).  Bitwise identical.  Returns the previous setting, or ESR_EINVAL. */
 int esr_dconv_set_occ3(int32_t on);
+/* x3 halo kernel with 16-column tiles (2 rows × 16 columns per MFMA M-tile) where 32-column tiles would waste > 30 %
+ * of the width and 16-column ones do not (the 38-wide layers at config 3): 1 (default) / 0 (the gather kernel there,
+ * A/B).  Returns the previous setting, or ESR_EINVAL. */
+int esr_dconv_set_cw16(int32_t on);
 /* Precision of esr_dconv_fwd (process-wide): 0 (the library default) = exact fp32 MFMA; 1 = x3: both operands split
  * into f16 hi/lo at staging after a power-of-two scaling per K step (one tap × 32 channels) chosen from the
  * workgroup's max |a| and max |b|, products hi·hi + hi·lo + lo·hi on f16 MFMA, the fp32 accumulators rescaled exactly

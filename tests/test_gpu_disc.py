@@ -34,6 +34,7 @@ pytestmark = pytest.mark.gpu
     (64, 64, 3, 1, 1, 37, 70),     # several halo tiles per image, ragged in both directions
     (32, 64, 4, 2, 1, 41, 75),     # stride-2 halo (column-parity de-interleave), ragged
     (64, 128, 4, 2, 1, 76, 100),   # space-to-depth form on the halo kernel (MW 50 / 51), two N blocks
+    (128, 64, 8, 1, 3, 38, 38),    # x3: 16-column halo tiles (MW 37 forward, 38 data gradient: 64 taps)
     (256, 100, 8, 1, 0, 38, 38),   # the config-3 pseudo-FC geometry: split-K over the channel chunks
 ])
 @pytest.mark.parametrize('precision', ['x3', 'x6', 'f32', 'x3_gather', 'x6_gather', 'f32_gather', 'x3_direct',

@@ -34,7 +34,7 @@ def main():
     B = 16
     variants = [('f32', 0, 0, 1), ('f32_halo', 0, 1, 1), ('x3_n128', 1, 0, 1), ('x3_halo', 1, 1, 1), ('x6', 3, 0, 1),
                 ('x6_halo', 3, 1, 1), ('f32_halo_direct', 0, 1, 0), ('x3_halo_direct', 1, 1, 0),
-                ('x3_halo_sdall', 1, 2, 1), ('x3_halo_n64', 2, 1, 1), ('x3_halo_occ2', 1, 1, 1)]
+                ('x3_halo_sdall', 1, 2, 1), ('x3_halo_n64', 2, 1, 1), ('x3_halo_occ2', 1, 1, 1), ('x3_halo_cw32', 1, 1, 1)]
     if 'AB_TAGS' in os.environ:
         keep = set(os.environ['AB_TAGS'].split(',')) | {'f32'}
         variants = [v for v in variants if v[0] in keep]
@@ -59,6 +59,7 @@ def main():
                 lib.esr_dconv_set_halo(halo)
                 lib.esr_dconv_set_rows(min(halo, 1))  # *_halo: the halo forward and the tap-row weight gradient
                 lib.esr_dconv_set_occ3(0 if tag.endswith('_occ2') else 1)
+                lib.esr_dconv_set_cw16(0 if tag.endswith('_cw32') else 1)
                 for _ in range(2):
                     dconv.conv_forward(x, w, b, k, s, p)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
