@@ -48,7 +48,7 @@ def c3_training_step(dev, precision='x3', d_precision=None):
     if not flags == list(d['f64_generator_step']) == list(d['f32_generator_step']):
         fails.append(('generator_step', flags))
     for net, tag in ((model.netG, 'G'), (model.netD, 'D')):
-        errs = []
+        errs, names = [], []
         for i, (k, p) in enumerate(net.named_parameters()):
             key = '%s_gproj:%s' % (tag, k)
             if 'f64_' + key not in d.files:
@@ -65,10 +65,13 @@ def c3_training_step(dev, precision='x3', d_precision=None):
             err, base, norm = np.linalg.norm(mine - p64), np.linalg.norm(p32 - p64), np.linalg.norm(p64)
             bound = FACTOR * base + FLOOR * max(norm, 1e-30)
             errs.append(err / bound)
+            names.append(k)
             if err > bound:
                 fails.append((tag, k, 'err %.3e bound %.3e (ref f32 %.3e, |proj| %.3e)' % (err, bound, base, norm)))
-        lines.append('%s: %d parameter gradients, worst at %.1f %% of its bound, median %.1f %%' % (
-            tag, len(errs), 100 * max(errs), 100 * float(np.median(errs))))
+        order = np.argsort(errs)[::-1][:3]
+        lines.append('%s: %d parameter gradients, worst at %.1f %% of its bound, median %.1f %% (worst: %s)' % (
+            tag, len(errs), 100 * max(errs), 100 * float(np.median(errs)),
+            ', '.join('%s %.1f %%' % (names[j], 100 * errs[j]) for j in order)))
         worst = max(worst, max(errs))
     for f in [f for f in d.files if f.startswith('f64_log:')]:
         key = f[len('f64_log:'):]
