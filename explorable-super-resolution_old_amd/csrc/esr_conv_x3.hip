@@ -1237,6 +1237,7 @@ __global__ __launch_bounds__(NR_THR, 2) void conv_x3_narrow_kernel(X3Params p) {
 }
 
 int g_x3_narrow = 1;  // esr_x3_set_narrow: the narrow-N kernel for cout <= 3 planar outputs (0: the N = 32 tiles)
+int g_x3_nsplit = 0;  // esr_x3_set_nsplit: N = 64 convs on under-filled grids as two N = 32 launches (0: one launch)
 
 int g_x3_kernel = 1;  // esr_x3_set_kernel (include/esr_amd.h)
 int g_x3_map = 1;     // esr_x3_set_tile_map (XCD-grouped: ~1 % per step, profiles/r1_x3_xcdmap_ab.txt)
@@ -1342,6 +1343,30 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
         c.in = p.in; c.B = B; c.H = H; c.W = W; c.in_cp = in_cp; c.cin = cin; c.w = p.w; c.bias = bias;
         c.w_scale_inv = p.w_scale_inv; c.cout = cout; c.tap_y0 = ty0; c.tap_x0 = tx0; c.tiles_x = c.tiles_y = 0;
         c.xcd_map = g_x3_map; c.overflow = overflow; c.o = *o;
+        c.w_ld = c.w_roff = 0;
+        c.w_cstride = 0;
+        // N split: an N = 64 conv whose 16-column grid cannot give every CU two workgroups (config 3 / 5: 294 / 380
+        // tiles for 256 CUs) runs as two N = 32 launches (12-column tiles, three per CU) over the two halves of its
+        // packed weights and output channels — twice the input staging, but the CUs filled (profiles/r3_nsplit_ab.txt)
+        const int tiles16 = ((W + 15) / 16) * ((B * (H + 2) - 2 + 31) / 32);
+        if (g_x3_nsplit && taps_side == 3 && cout > 32 && (g_x3_kernel == 1 || g_x3_kernel == 63) &&
+            tiles16 < 2 * n_cu && !o->out_planar) {
+            for (int h = 0; h < 2; ++h) {
+                X3cParams ch = c;
+                ch.cout = min(32, cout - 32 * h);
+                ch.bias = bias + 32 * h;
+                ch.w_ld = 64;                                    // the N = 64 packing: 64 records per tap
+                ch.w_roff = 32 * h;
+                ch.w_cstride = 9LL * 64 * 64;                    // 9 taps × 64 records × 64 B per 16-channel chunk
+                ch.o.out_coff += 32 * h;
+                if (ch.o.r1) ch.o.r1_coff += 32 * h;
+                if (ch.o.r2) ch.o.r2_coff += 32 * h;
+                if (ch.o.out2) ch.o.out2_coff += 32 * h;
+                const int rc = x3c_launch(ch, taps_side, stream, 128);
+                if (rc != ESR_OK) return rc;
+            }
+            return ESR_OK;
+        }
         if (g_x3_kernel == 60) return x3c_launch(c, taps_side, stream, 16);
         if (g_x3_kernel == 61) return x3c_launch(c, taps_side, stream, 32);
         if (g_x3_kernel == 62) return x3c_launch(c, taps_side, stream, 64);
@@ -1441,6 +1466,13 @@ extern "C" int esr_x3_set_kernel(int32_t variant) {
 #endif
     const int prev = g_x3_kernel;
     g_x3_kernel = variant;
+    return prev;
+}
+
+extern "C" int esr_x3_set_nsplit(int32_t on) {
+    if (on < 0 || on > 1) return ESR_EINVAL;
+    const int prev = g_x3_nsplit;
+    g_x3_nsplit = on;
     return prev;
 }
 

@@ -205,14 +205,16 @@ __global__ __launch_bounds__(64 * (TW / CWV), (TW / CWV) * OCC / 4) void conv_x3
     };
     auto dma_w = [&](int j) {
         if constexpr (!RB) {
-            const unsigned char *wj = p.w + (long long)j * W_B;
+            const unsigned char *wj = p.w + (long long)j * (p.w_cstride ? p.w_cstride : (long long)W_B);
+            const int ld = p.w_ld ? p.w_ld : N;
 #pragma unroll
             for (int i = 0; i < KW; ++i) {
                 const int q = wave + NW * i;
                 if (q >= W_PIECES) break;
                 const int r = 16 * q + sub;
                 const int s = ps ^ ((r >> 2) & 3);
-                __builtin_amdgcn_global_load_lds((glob_void *)(wj + r * REC + (s << 4)),
+                const int rs = (r / N) * ld + p.w_roff + r % N;  // source record (tap r / N, output channel r % N)
+                __builtin_amdgcn_global_load_lds((glob_void *)(wj + rs * REC + (s << 4)),
                                                  (lds_void *)(lds + IN_Bk + q * 1024), 16, 0, 0);
             }
         }

@@ -14,6 +14,11 @@ struct X3cParams {
     int xcd_map;
     int *overflow;
     esr_conv_out o;
+    // weight source layout (0 = the kernel's own: N records per tap, T·N records per chunk): w_ld records per tap,
+    // starting at record w_roff of each tap, w_cstride bytes per chunk — an N = 32 launch over one half of an N = 64
+    // packing (launch_x3's N split)
+    int w_ld, w_roff;
+    long long w_cstride;
 };
 
 // taps_side 3: 3x3 conv (tap_y0 = tap_x0 = 0); 2: one polyphase phase of the nearest-x2 upconv (tap origin py, px)

@@ -51,6 +51,7 @@ _SIGNATURES = {
     'esr_x3_set_kernel': [c_int],
     'esr_x3_set_tile_map': [c_int],
     'esr_x3_set_narrow': [c_int],
+    'esr_x3_set_nsplit': [c_int],
     'esr_cem_set_direct': [c_int],
     'esr_conv_set_tile': [c_int],
     'esr_cem_down': [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int,
@@ -151,6 +152,9 @@ def load():
     if lib.esr_op_size() != ctypes.sizeof(EsrOp):
         raise ESRLibraryError('esr_op layout mismatch: C %d bytes, binding %d' % (lib.esr_op_size(),
                                                                                   ctypes.sizeof(EsrOp)))
+    # process-wide kernel switches for same-box A/B runs (defaults are the library's)
+    if os.environ.get('ESR_X3_NSPLIT') in ('0', '1'):
+        lib.esr_x3_set_nsplit(int(os.environ['ESR_X3_NSPLIT']))
     _lib = lib
     return lib
 

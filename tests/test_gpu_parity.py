@@ -467,6 +467,40 @@ def test_x3_xcd_tile_map_bitwise(gpu_device, cout, cin, B, H, W):
     assert normwise_rel(_nchw(engine.from_split(outs[0]), 0, cout), ref) < 1e-5
 
 
+@pytest.mark.parametrize('cin,cout,B,H,W', [(192, 64, 2, 24, 40), (72, 40, 1, 9, 21)])
+def test_x3_nsplit_bitwise(gpu_device, cin, cout, B, H, W):
+    """An N = 64 conv on an under-filled grid as two N = 32 launches over the halves of its packed weights
+    (esr_x3_set_nsplit, default) against one N = 64 launch: the RDB conv5 epilogue (LeakyReLU off, 0.2 x conv +
+    residual at a channel offset, a dual output at another offset) must land in the same channels, bit for bit."""
+    lib = _lib.load()
+    cp = cin + 8
+    xs = engine.to_split(_padded(B, H, W, cp, cin, gpu_device, 51))
+    rs = engine.to_split(_padded(B, H, W, cp, cp, gpu_device, 52))
+    g = torch.Generator().manual_seed(53)
+    w = torch.randn(cout, cin, 3, 3, generator=g) * 0.05
+    b = (torch.rand(cout, generator=g) - 0.5).to(gpu_device)
+    wx, scale = engine.pack_x3(engine.pack_conv_weight(w.to(gpu_device), list(range(cin)), 64))
+    outs = []
+    prev = lib.esr_x3_set_nsplit(1)
+    try:
+        for mode in (1, 0):
+            lib.esr_x3_set_nsplit(mode)
+            out = torch.zeros(B, H + 2, W + 2, 80, device=gpu_device)
+            out2 = torch.zeros(B, H + 2, W + 2, 88, device=gpu_device)
+            o = engine._conv_out(out, 80, 8, H, W, False, r1=rs, r1_cp=cp, r1_coff=16, s1=0.2, out2=out2, out2_cp=88,
+                                 out2_coff=24)
+            _lib.check(lib.esr_conv3x3_fwd_x3(xs.data_ptr(), B, H, W, cp, cin, wx.data_ptr(), b.data_ptr(), scale,
+                                              cout, ctypes.byref(o), None, _stream()), 'conv_x3')
+            torch.cuda.synchronize()
+            outs.append((out, out2))
+    finally:
+        lib.esr_x3_set_nsplit(prev)
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    ref = F.conv2d(_nchw(engine.from_split(xs), 0, cin), w.double(), b.cpu().double(), padding=1)
+    assert normwise_rel(_nchw(engine.from_split(outs[0][0]), 8, 8 + cout), ref * 0.2 +
+                        _nchw(engine.from_split(rs), 16, 16 + cout)) < 1e-5
+
+
 # default, direct register epilogue 16- / 8-row, classic, column tiles
 @pytest.mark.parametrize('variant', [1, 27, 28, 24, 50, 64])
 def test_conv3x3_x3_planar_output(gpu_device, variant):
