@@ -1237,7 +1237,7 @@ __global__ __launch_bounds__(NR_THR, 2) void conv_x3_narrow_kernel(X3Params p) {
 }
 
 int g_x3_narrow = 1;  // esr_x3_set_narrow: the narrow-N kernel for cout <= 3 planar outputs (0: the N = 32 tiles)
-int g_x3_nsplit = 0;  // esr_x3_set_nsplit: N = 64 convs on under-filled grids as two N = 32 launches (0: one launch)
+int g_x3_nsplit = 1;  // esr_x3_set_nsplit: N = 64 convs on under-filled grids as two N = 32 launches (0: one launch)
 
 int g_x3_kernel = 1;  // esr_x3_set_kernel (include/esr_amd.h)
 int g_x3_map = 1;     // esr_x3_set_tile_map (XCD-grouped: ~1 % per step, profiles/r1_x3_xcdmap_ab.txt)
@@ -1347,7 +1347,7 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
         c.w_cstride = 0;
         // N split: an N = 64 conv whose 16-column grid cannot give every CU two workgroups (config 3 / 5: 294 / 380
         // tiles for 256 CUs) runs as two N = 32 launches (12-column tiles, three per CU) over the two halves of its
-        // packed weights and output channels — twice the input staging, but the CUs filled (profiles/r3_nsplit_ab.txt)
+        // packed weights and output channels — twice the input staging, but the CUs filled (profiles/r3_ab_nsplit.txt)
         const int tiles16 = ((W + 15) / 16) * ((B * (H + 2) - 2 + 31) / 32);
         if (g_x3_nsplit && taps_side == 3 && cout > 32 && (g_x3_kernel == 1 || g_x3_kernel == 63) &&
             tiles16 < 2 * n_cu && !o->out_planar) {

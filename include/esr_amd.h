@@ -171,9 +171,10 @@ int esr_x3_set_tile_map(int32_t mode);
  * columns are padding; 0 = the N = 32 tiles.  Results agree to the x3 rounding (not bitwise: the tap sum order
  * differs).  Returns the previous setting, or ESR_EINVAL. */
 int esr_x3_set_narrow(int32_t on);
-/* N split of esr_conv3x3_fwd_x3 (process-wide): 1 = a 3×3 conv with 32 < cout <= 64 whose 16-column grid
+/* N split of esr_conv3x3_fwd_x3 (process-wide): 1 (default) = a 3×3 conv with 32 < cout <= 64 whose 16-column grid
  * has fewer than two tiles per CU (config 3: 96² × B=16) runs as two N = 32 launches over the halves of its packed
- * weights and output channels; 0 (default until measured on the GPU) = one N = 64 launch.  Bitwise identical (the same products per output channel in
+ * weights and output channels (config 3: 144.6 -> 142.6 ms per step, config 5: 84.5 -> 83.0 ms, profiles/r3_ab_nsplit.txt);
+ * 0 = one N = 64 launch.  Bitwise identical (the same products per output channel in
  * the same order).  Returns the previous setting, or ESR_EINVAL. */
 int esr_x3_set_nsplit(int32_t on);
 
