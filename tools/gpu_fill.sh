@@ -1,6 +1,6 @@
 # x3 conv time split at the config-2 trunk shapes (B=32, 148² = 128² + the CEM pre-pad, the production column-tile kernel): full (1, 50) vs
-# needs the experiment library in the GPU snapshot: make -C explorable-super-resolution_old_amd/csrc exp EXP_OUT=../../exp_lib/libesr_exp.so, and drop ./exp_lib from .gpurunignore for the run
 # LDS-DMA of chunk 0 only (51), no fragment reads / MFMAs (52), no epilogue stores (53), 51+53 (54); experiment build
+# needs the experiment library in the GPU snapshot: make -C explorable-super-resolution_old_amd/csrc exp EXP_OUT=../../exp_lib/libesr_exp.so, and drop ./exp_lib from .gpurunignore for the run
 set -o pipefail
 mkdir -p gpurun_out
 out=gpurun_out/x3_fill.log

@@ -1,6 +1,6 @@
 # time split of the discriminator's x3 halo kernel at the config-3 shapes (experiment build): full (0), no weight-slab
-# needs the experiment library in the GPU snapshot: make -C explorable-super-resolution_old_amd/csrc exp EXP_OUT=../../exp_lib/libesr_exp.so, and drop ./exp_lib from .gpurunignore for the run
 # staging (1), no fragment reads / MFMAs (2), halo window staged once (4), 1+4 (5)
+# needs the experiment library in the GPU snapshot: make -C explorable-super-resolution_old_amd/csrc exp EXP_OUT=../../exp_lib/libesr_exp.so, and drop ./exp_lib from .gpurunignore for the run
 set -o pipefail
 mkdir -p gpurun_out
 out=gpurun_out/halo_split.log
