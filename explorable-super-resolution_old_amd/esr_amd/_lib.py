@@ -155,6 +155,8 @@ def load():
     # process-wide kernel switches for same-box A/B runs (defaults are the library's)
     if os.environ.get('ESR_X3_NSPLIT') in ('0', '1'):
         lib.esr_x3_set_nsplit(int(os.environ['ESR_X3_NSPLIT']))
+    if os.environ.get('ESR_X3_KERNEL', '').isdigit():
+        lib.esr_x3_set_kernel(int(os.environ['ESR_X3_KERNEL']))
     _lib = lib
     return lib
 
