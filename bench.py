@@ -57,7 +57,7 @@ def parse():
     ap.add_argument('--no-cpu-variants', action='store_true', help='skip the latent Z=0 / Z~U[-1,1] CPU baselines')
     ap.add_argument('--no-legs', action='store_true', help='skip the extra legs (exact-fp32 C2, C3/C4 training step, '
                     'C5 Z-optimisation iteration)')
-    ap.add_argument('--leg-steps', type=int, default=3)
+    ap.add_argument('--leg-steps', type=int, default=10)
     ap.add_argument('--x3-kernel', type=int, default=None, help='esr_x3_set_kernel variant (A/B; default automatic)')
     ap.add_argument('--no-op-timers', action='store_true', help='time the steps without the per-launch HIP events '
                     '(no roofline; measures what the events themselves cost)')

@@ -43,7 +43,7 @@ def make_opt(args):
 def leg_args(**kw):
     """Default arguments of this benchmark (BASELINE config 3 per GPU), for callers such as bench.py."""
     # warmup 4: the caching allocator still returns memory to the device (hipFree, ~200 frees) in calls 3-4
-    d = dict(gpus=1, steps=3, warmup=4, batch=16, lr_size=96, nb=23, latent=True)
+    d = dict(gpus=1, steps=10, warmup=4, batch=16, lr_size=96, nb=23, latent=True)
     d.update(kw)
     return argparse.Namespace(**d)
 
@@ -63,20 +63,26 @@ def run(args, dev, world, rank):
     data = {'LR': torch.rand(args.batch, 3, args.lr_size, args.lr_size, generator=g).to(dev),
             'HR': torch.rand(args.batch, 3, hr, hr, generator=g).to(dev)}
     gsteps = 0
+    rrdb = model._rrdb
+    reruns0, a0 = engine.OVERFLOW_RERUNS, engine.act_scale(rrdb)
     for _ in range(args.warmup):
         model.feed_data(data)
         model.optimize_parameters()
+    reruns1, a1 = engine.OVERFLOW_RERUNS, engine.act_scale(rrdb)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    stamps = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         model.feed_data(data)
-        model.optimize_parameters()
+        model.optimize_parameters()  # ends with its deferred overflow-flag read (a device sync)
         gsteps += int(model.generator_step)
+        stamps.append(time.perf_counter())
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    step_ms = [round((b - a) * 1e3, 2) for a, b in zip([t0] + stamps[:-1], stamps)]
     if world > 1:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -98,13 +104,16 @@ def run(args, dev, world, rank):
                                                                       hr - 80, args.nb, args.latent),
                        'global_batch': world * args.batch,
                        'parallelism': 'dp%d (bucketed RCCL all-reduce of G/D grads)' % world},
-            'last_losses': {k: v[-1][1] for k, v in model.log_dict.items() if v}}
+            'last_losses': {k: v[-1][1] for k, v in model.log_dict.items() if v},
+            'step_ms': step_ms,
+            'overflow_reruns': {'warmup': reruns1 - reruns0, 'timed': engine.OVERFLOW_RERUNS - reruns1},
+            'act_scale': {'before_warmup': a0, 'before_timed': a1, 'after_timed': engine.act_scale(rrdb)}}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=4)
     ap.add_argument('--batch', type=int, default=16)
     ap.add_argument('--lr-size', type=int, default=96)

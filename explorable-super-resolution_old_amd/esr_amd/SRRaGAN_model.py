@@ -181,7 +181,7 @@ class SRRaGANModel:
     def __init__(self, opt, accumulation_steps_per_batch=1, kernel=None, device=None):
         self.opt = opt
         self.is_train = bool(opt['is_train'])
-        self.device = device if device is not None else torch.device('cuda', torch.cuda.current_device())
+        self.device = torch.device(device) if device is not None else torch.device('cuda', torch.cuda.current_device())
         opt_G = opt['network_G']
         li = opt_G.get('latent_input')
         self.latent_input = li if li not in (None, 'None') else None
@@ -465,10 +465,17 @@ class SRRaGANModel:
             dev.append((o, o.flat.data.clone(), o.flat.grad.clone(),
                         {k: (v.clone() if torch.is_tensor(v) else v) for k, v in st.items()}))
         bufs = [(b, b.clone()) for n, b in self.netD.named_buffers()]
+        # the RNG streams (the WGAN-GP interpolation points): a redo draws the same points as the undone micro-step
+        host['_rng'] = (torch.get_rng_state(),
+                        torch.cuda.get_rng_state(self.device) if self.device.type == 'cuda' else None)
         return host, dev, bufs
 
     def _restore(self, snap):
         host, dev, bufs = snap
+        cpu_rng, dev_rng = host['_rng']
+        torch.set_rng_state(cpu_rng)
+        if dev_rng is not None:
+            torch.cuda.set_rng_state(dev_rng, self.device)
         for k in self._SNAP_ATTRS:
             if k in host:
                 self.__dict__[k] = host[k]

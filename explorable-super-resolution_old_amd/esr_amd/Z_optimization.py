@@ -404,6 +404,7 @@ class Z_optimizer:
             raise NotImplementedError('auto_set_hist_temperature: not built (second-order through the generator)')
         self.device = model.device
         dev = self.device
+        self.on_iteration = None  # optional callback(z_iter) after each iteration (benchmarks)
         if initial_Z is not None or 'cur_Z' in model.__dict__ or hasattr(model, 'model_input'):
             if initial_Z is None:
                 initial_Z = 1 * model.GetLatent()
@@ -712,17 +713,22 @@ class Z_optimizer:
             if chk.overflowed():
                 E.OVERFLOW_RERUNS += 1
                 self._restore(snap)
-                g = self.model.netG.module.generated_image_model if hasattr(self.model.netG, 'module') else None
-                prev = getattr(g, 'esr_precision', None)
-                if g is not None:
-                    g.esr_precision = 'f32'
+                # every RRDBNet under netG (CEM-wrapped or not, DataParallel or not) in exact fp32 for the redo
+                prev = [(m, m.__dict__.get('esr_precision')) for m in self.model.netG.modules()
+                        if hasattr(m, '_esr_cache')]
+                E.set_precision(self.model.netG, 'f32')
                 try:
                     Z_loss = self._iteration(z_iter)
                 finally:
-                    if g is not None:
-                        g.esr_precision = prev
+                    for m, p in prev:
+                        if p is None:
+                            m.__dict__.pop('esr_precision', None)
+                        else:
+                            m.esr_precision = p
             self.loss_values.append(Z_loss)
             z_iter += 1
+            if self.on_iteration is not None:  # (benchmarks: per-iteration wall times; the check above synchronised)
+                self.on_iteration(z_iter)
         self.loss_values = [float(v) for v in self.loss_values]
         if not self.model_training:
             self.latest_Z_loss_values = [float(v) for v in self.latest_Z_loss_values]

@@ -27,6 +27,7 @@ zero from allocation and never written.
 import ctypes
 import math
 import os
+import warnings
 
 import numpy as np
 import torch
@@ -91,8 +92,21 @@ def act_scale(net):
     return getattr(net, '_esr_act_scale', ACT_SCALE)
 
 
+# Number of activation-scale reductions (observability: each one trades small-activation precision for range, for
+# the rest of the model's life; benchmarks record it, tests/test_gpu_state.py pins the behaviour).
+ACT_SCALE_REDUCTIONS = 0
+
+
 def lower_act_scale(net):
-    net._esr_act_scale = max(1.0, act_scale(net) / 16)
+    """A scaled activation of an x3 forward left f16's range: the model's A drops 16× (floor 1) and stays there — a
+    deliberate one-way ratchet, so a model fed out-of-range inputs does not overflow (and rerun in fp32) again and
+    again; the count is kept in ACT_SCALE_REDUCTIONS and each reduction is reported once per model."""
+    global ACT_SCALE_REDUCTIONS
+    old = act_scale(net)
+    net._esr_act_scale = max(1.0, old / 16)
+    ACT_SCALE_REDUCTIONS += 1
+    warnings.warn('esr_amd: x3 activation scale of %s lowered %g -> %g after an f16-range overflow'
+                  % (type(net).__name__, old, net._esr_act_scale), RuntimeWarning, stacklevel=2)
 
 
 def _prof_begin(prof, tag, flops):

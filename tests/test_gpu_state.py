@@ -80,3 +80,31 @@ def test_retained_graph_second_backward_raises_after_reuse(gpu_device):
     model(torch.flip(x, dims=[2]).contiguous()).sum().backward()
     with pytest.raises(RuntimeError, match='overwritten'):
         y.sum().backward()
+
+
+def test_activation_scale_ratchet(gpu_device):
+    """engine.lower_act_scale: an x3 forward whose scaled activations leave f16's range is redone in
+    exact fp32 (bitwise the f32 output), the model's activation scale A drops 16× and the reduction is counted and
+    warned about; A stays lowered for later in-range forwards (a deliberate one-way ratchet), which still run x3."""
+    from esr_amd import engine
+    d = golden('grad_plain_nb1')
+    _, params = fixture_params(d)
+    x = fixture_input(d).to(gpu_device)
+    model = _model(params, gpu_device).eval()
+    ref = _model(params, gpu_device).eval()
+    engine.set_precision(ref, 'f32')
+    rrdb = model.generated_image_model
+    assert engine.act_scale(rrdb) == engine.ACT_SCALE
+    red0, rer0 = engine.ACT_SCALE_REDUCTIONS, engine.OVERFLOW_RERUNS
+    with torch.no_grad(), pytest.warns(RuntimeWarning, match='activation scale'):
+        big = model(x * 3e5)
+    assert engine.OVERFLOW_RERUNS == rer0 + 1 and engine.ACT_SCALE_REDUCTIONS == red0 + 1
+    assert engine.act_scale(rrdb) == engine.ACT_SCALE / 16
+    with torch.no_grad():
+        assert torch.equal(big, ref(x * 3e5))
+        small = model(x)
+        exact = ref(x)
+    assert engine.act_scale(rrdb) == engine.ACT_SCALE / 16  # not raised again
+    assert engine.OVERFLOW_RERUNS == rer0 + 1
+    err = float((small - exact).abs().max() / exact.abs().max())
+    assert 0 < err < 1e-5, err  # x3 (not bitwise the fp32 path), fp32-level accuracy

@@ -163,7 +163,9 @@ def test_optimize_parameters_vs_reference_loop(gpu_device, name, precision):
 def test_deferred_overflow_redo_equals_fp32_step(gpu_device):
     """optimize_parameters reads the x3 overflow flags once per micro-step (SRRaGANModel.optimize_parameters): an
     input whose activations leave the f16 range must leave the model exactly where the same micro-steps with an
-    exact-fp32 generator leave it — parameters, Adam moments, BatchNorm buffers and logs, bitwise."""
+    exact-fp32 generator leave it — parameters, Adam moments, BatchNorm buffers and logs, bitwise.  The WGAN-GP
+    interpolation points come from the model's own RNG draws: the redo must restore the RNG streams, or it draws
+    different points than the exact-fp32 run (each model runs its steps from the same seed)."""
     from esr_amd import engine
     from esr_amd.SRRaGAN_model import SRRaGANModel
     cfg = dict(TRAIN_CFGS['past_ratio2_acc2'], steps=3)
@@ -175,19 +177,18 @@ def test_deferred_overflow_redo_equals_fp32_step(gpu_device):
         gp = seeded_params([(k, tuple(v.shape)) for k, v in gsd.items()], cfg['seed'], w_scale=1.0)
         model.netG.load_state_dict({k: torch.from_numpy(v) for k, v in gp.items()}, strict=False)
         engine.set_precision(model.netG, prec)
-        pts = torch.full((cfg['batch'], 1, 1, 1), 0.37, device=gpu_device)
-        model._interp_points = lambda n, pts=pts: pts
         models.append(model)
     dsd = {k: v.clone() for k, v in models[0].netD.state_dict().items()}
     models[1].netD.load_state_dict(dsd)
     for m in models:  # the discriminators' flat buffers hold the same weights (load_state_dict copies in place)
         m.optimizer_D._sync_views()
     before = engine.OVERFLOW_RERUNS
-    for k in range(cfg['steps']):
-        lr, hr, z = step_data(cfg, k)
-        lr = lr * 3e4  # activations beyond f16's range: every micro-step of the x3 model is redone in fp32
-        for m in models:
-            t = lambda a: torch.from_numpy(a).to(gpu_device)  # noqa: E731
+    t = lambda a: torch.from_numpy(a).to(gpu_device)  # noqa: E731
+    for m in models:
+        torch.manual_seed(77)
+        for k in range(cfg['steps']):
+            lr, hr, z = step_data(cfg, k)
+            lr = lr * 3e4  # activations beyond f16's range: every micro-step of the x3 model is redone in fp32
             m.feed_data({'LR': t(lr), 'HR': t(hr), 'Z': t(z)})
             m.optimize_parameters()
     assert engine.OVERFLOW_RERUNS >= before + cfg['steps']

@@ -15,9 +15,9 @@ from oracle.recipe import seeded_inputs, seeded_params
 pytestmark = pytest.mark.gpu
 
 
-def _opt(nb):
+def _opt(nb, cem=1):
     return {'is_train': False, 'scale': 4, 'gpu_ids': [0], 'range': [0, 1],
-            'network_G': {'which_model_G': 'RRDB_net', 'CEM_arch': 1, 'latent_input': 'all_layers',
+            'network_G': {'which_model_G': 'RRDB_net', 'CEM_arch': cem, 'latent_input': 'all_layers',
                           'latent_input_domain': 'HR_downscaled', 'latent_channels': 'SVDinNormedOut_structure_tensor',
                           'norm_type': None, 'mode': 'CNA', 'nf': 64, 'nb': nb, 'in_nc': 3, 'out_nc': 3, 'gc': 32}}
 
@@ -66,10 +66,12 @@ def test_z_optimizer_loop_matches_oracle(gpu_device, objective):
     assert len(zo.loss_values) == iters
 
 
-def test_z_optimizer_overflow_redo_equals_fp32_loop(gpu_device):
+@pytest.mark.parametrize('cem', [1, 0])
+def test_z_optimizer_overflow_redo_equals_fp32_loop(gpu_device, cem):
     """Z_optimizer.optimize reads the generator's x3 overflow flags once per iteration: with inputs whose activations
     leave the f16 range, every iteration is redone from its snapshot in exact fp32, so the loop ends bitwise where the
-    same loop with an exact-fp32 generator does."""
+    same loop with an exact-fp32 generator does — with the CEM-wrapped generator and with a bare RRDBNet (define_G
+    without CEM_arch: no generated_image_model to switch)."""
     from esr_amd import engine
     nb, B, h, w, iters = 1, 2, 12, 12, 3
     lr, z0 = seeded_inputs(72, (B, 3, h, w), (B, 3, 4 * h, 4 * w), z_mode='pixel')
@@ -77,7 +79,7 @@ def test_z_optimizer_overflow_redo_equals_fp32_loop(gpu_device):
     before = engine.OVERFLOW_RERUNS
     for prec in ('x3', 'f32'):
         torch.manual_seed(0)
-        model = SRRaGANModel(_opt(nb), device=gpu_device)
+        model = SRRaGANModel(_opt(nb, cem), device=gpu_device)
         sd = model.netG.module.state_dict()
         params = seeded_params([(k, tuple(v.shape)) for k, v in sd.items()], 71, w_scale=0.5)
         model.netG.module.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=False)
