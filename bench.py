@@ -58,7 +58,8 @@ def parse():
     ap.add_argument('--no-legs', action='store_true', help='skip the extra legs (exact-fp32 C2, C3/C4 training step, '
                     'C5 Z-optimisation iteration)')
     ap.add_argument('--leg-steps', type=int, default=10)
-    ap.add_argument('--x3-kernel', type=int, default=None, help='esr_x3_set_kernel variant (A/B; default automatic)')
+    ap.add_argument('--x3-kernel', type=int, default=None, help='esr_x3_set_kernel variant (A/B: needs the ablation '
+                    'library, ESR_AMD_LIB=exp_lib/libesr_exp.so; default automatic)')
     ap.add_argument('--no-op-timers', action='store_true', help='time the steps without the per-launch HIP events '
                     '(no roofline; measures what the events themselves cost)')
     return ap.parse_args()
@@ -255,7 +256,11 @@ def main():
     from esr_amd import engine
     if args.x3_kernel is not None:
         from esr_amd import _lib
-        if _lib.load().esr_x3_set_kernel(args.x3_kernel) < 0:
+        lib = _lib.load()
+        if not hasattr(lib, 'esr_x3_set_kernel'):
+            raise SystemExit('--x3-kernel needs the ablation library (ESR_AMD_LIB=exp_lib/libesr_exp.so); the product '
+                             'library has no kernel-selection state')
+        if lib.esr_x3_set_kernel(args.x3_kernel) < 0:
             raise SystemExit('esr_x3_set_kernel(%d) rejected' % args.x3_kernel)
     model = build_model(args, dev)
     x = make_input(args, dev, rank)

@@ -10,6 +10,7 @@
 // Replicate padding is realised as index clamping (ReplicationPad2d, CEMnet.py:63-64,150,158).
 #include <hip/hip_runtime.h>
 #include "esr_amd.h"
+#include "esr_knobs.h"
 
 namespace {
 
@@ -552,7 +553,6 @@ __global__ __launch_bounds__(NT) void prep_hr_kernel(PrepParams p) {
 }
 
 inline unsigned nblocks(long long n) { return (unsigned)((n + NT - 1) / NT); }
-int g_cem_direct = 0;  // esr_cem_set_direct: 1 = the untiled inverse / up-add kernels and the LDS-tiled down kernel
 inline int launched() { return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH; }
 
 }  // namespace
@@ -636,13 +636,6 @@ extern "C" int esr_cem_up_add(const float *q, const float *gen, float *out, int3
                            W, sf, ph, w_up, kd, M);
     }
     return launched();
-}
-
-extern "C" int esr_cem_set_direct(int32_t direct) {
-    if (direct < 0 || direct > 1) return ESR_EINVAL;
-    const int prev = g_cem_direct;
-    g_cem_direct = direct;
-    return prev;
 }
 
 extern "C" int esr_prep_input_s(const float *x, int32_t B, int32_t nz, int32_t h, int32_t w, int32_t sf, int32_t m,

@@ -14,8 +14,7 @@
 // a CPU fp32 conv only by summation order.
 #include <hip/hip_runtime.h>
 #include "esr_amd.h"
-
-int esr_g_conv_tile_map = 1;  // set with the x3 kernels' order by esr_x3_set_tile_map (esr_conv_x3.hip)
+#include "esr_knobs.h"
 
 namespace {
 
@@ -208,8 +207,6 @@ __global__ __launch_bounds__(NTHREADS, (MT == 1 && NT == 1) ? 2 : 1) void conv_f
     }
 }
 
-int g_conv_tile = 0;  // esr_conv_set_tile: 0 = automatic, 4 or 8 output rows per workgroup
-
 int n_cus() {
     static int n = 0;
     if (!n) {
@@ -235,12 +232,12 @@ int launch_conv(const float *in, int B, int H, int W, int in_cp, int cin, const 
     p.tiles_x = (W + TW - 1) / TW;
     // 4-row tiles for N = 32 (two workgroups per CU fit in LDS: measured 8-35 % faster, profiles/r1_conv_tile_ab.txt)
     // and for N = 64 when 8-row tiles would fill fewer than 8 rounds of one workgroup per CU (the last, partly idle
-    // round then costs up to an eighth; at 8+ rounds the 8-row tile's better weight reuse wins); esr_conv_set_tile
-    // overrides
+    // round then costs up to an eighth; at 8+ rounds the 8-row tile's better weight reuse wins); the ablation
+    // library's esr_conv_set_tile overrides
     const int tiles8 = p.tiles_x * ((H + 7) / 8) * B;
     const int mt = g_conv_tile == 4 ? 1 : g_conv_tile == 8 ? 2 : ((cout <= 32 || tiles8 < 8 * n_cus()) ? 1 : 2);
     p.tiles_y = (H + 4 * mt - 1) / (4 * mt);
-    p.xcd_map = esr_g_conv_tile_map;
+    p.xcd_map = g_tile_map;
     p.o = *o;
     const dim3 grid((unsigned)(p.tiles_x * p.tiles_y * B)), block(NTHREADS);
 #define ESR_CONV_LAUNCH(NT_, TS_, MT_) hipLaunchKernelGGL((conv_fwd_kernel<NT_, TS_, MT_>), grid, block, 0, stream, p)
@@ -276,11 +273,4 @@ extern "C" int esr_upconv2x_phase_fwd(const float *in, int32_t B, int32_t H, int
     return launch_conv(in, B, H, W, in_cp, cin, w_packed, bias, cout, 2, py, px, o, (hipStream_t)stream);
 }
 
-extern "C" int esr_conv_set_tile(int32_t rows) {
-    if (rows != 0 && rows != 4 && rows != 8) return ESR_EINVAL;
-    const int prev = g_conv_tile;
-    g_conv_tile = rows;
-    return prev;
-}
-
-extern "C" int esr_abi_version(void) { return 14; }
+extern "C" int esr_abi_version(void) { return 15; }

@@ -33,8 +33,7 @@
 #include <hip/hip_runtime.h>
 #include "esr_amd.h"
 #include "esr_x3c.h"
-
-extern int esr_g_conv_tile_map;  // esr_conv.hip: the exact-fp32 conv kernel's tile order
+#include "esr_knobs.h"
 
 namespace {
 
@@ -1236,12 +1235,6 @@ __global__ __launch_bounds__(NR_THR, 2) void conv_x3_narrow_kernel(X3Params p) {
     }
 }
 
-int g_x3_narrow = 1;  // esr_x3_set_narrow: the narrow-N kernel for cout <= 3 planar outputs (0: the N = 32 tiles)
-int g_x3_nsplit = 1;  // esr_x3_set_nsplit: N = 64 convs on under-filled grids as two N = 32 launches (0: one launch)
-
-int g_x3_kernel = 1;  // esr_x3_set_kernel (include/esr_amd.h)
-int g_x3_map = 1;     // esr_x3_set_tile_map (XCD-grouped: ~1 % per step, profiles/r1_x3_xcdmap_ab.txt)
-
 int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const void *w, const float *bias,
               float w_scale, int cout, int taps_side, int ty0, int tx0, const esr_conv_out *o, int *overflow,
               hipStream_t stream) {
@@ -1263,7 +1256,7 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
     p.tap_y0 = ty0; p.tap_x0 = tx0;
     p.tiles_x = (W + TWF - 1) / TWF;
     p.tiles_y = (B * (H + 2) - 2 + TH - 1) / TH;
-    p.xcd_map = g_x3_map;
+    p.xcd_map = g_tile_map;
     p.overflow = overflow;
     p.o = *o;
     const dim3 block(NTHR);
@@ -1280,28 +1273,28 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
     // Ring kernel (two tiles per workgroup, esr_x3_set_kernel 2): opt-in only.  With both kernels on counted-wait
     // fragment reads a ring pair cost ~2.0 two-stage classic tiles, and the one-stage classic kernel at two
     // workgroups per CU is faster still (tools/x3_ring_ab.py at config 2 / 3 shapes).
-    const int tiles = p.tiles_x * p.tiles_y, pairs = p.tiles_x * ((p.tiles_y + 1) / 2);
+    const int tiles = p.tiles_x * p.tiles_y;
     static int n_cu = 0;
     if (!n_cu) {
         int dev = 0, v = 0;
         n_cu = (hipGetDevice(&dev) == hipSuccess &&
                 hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
     }
-    // (no longer chosen automatically: the one-stage classic kernel at two workgroups per CU beats it everywhere)
-    const bool ring_pays = false;
     // N = 32 one-stage kernel, 16-row tiles at 2 workgroups per CU vs 8-row tiles at 3: a round of 8-row workgroups
     // takes ~3/4 of a round of 16-row ones (measured: at 148², where both grids fill their last round, 16-row is ~1 %
     // faster over a whole bench step; 8-row is 15-20 % faster at 96², where the 16-row grid's second round is nearly
     // empty), so compare rounds x 3 with rounds x 4, ties to 16-row
     const int tiles8 = p.tiles_x * ((B * (H + 2) - 2 + 7) / 8);
     const bool row8_pays = 3 * ((tiles8 + 3 * n_cu - 1) / (3 * n_cu)) < 4 * ((tiles + 2 * n_cu - 1) / (2 * n_cu));
+#ifdef ESR_X3_EXPERIMENTS  // ring / persistent-ring variants: the ablation library only
+    const int pairs = p.tiles_x * ((p.tiles_y + 1) / 2);
     if (taps_side == 3 && cout <= 32 && (g_x3_kernel == 16 || g_x3_kernel == 17)) {
         const dim3 gridp((unsigned)min(pairs, n_cu));
         if (g_x3_kernel == 16) hipLaunchKernelGGL((conv_x3_pring_kernel<1>), gridp, block, 0, stream, p);
         else hipLaunchKernelGGL((conv_x3_pring_kernel<2>), gridp, block, 0, stream, p);
         return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
     }
-    if (taps_side == 3 && cout <= 32 && ((g_x3_kernel >= 2 && g_x3_kernel < 20) || (g_x3_kernel == 1 && ring_pays))) {
+    if (taps_side == 3 && cout <= 32 && g_x3_kernel >= 2 && g_x3_kernel < 20) {
         const dim3 grid2((unsigned)pairs);
         switch (g_x3_kernel) {
         case 15: hipLaunchKernelGGL((conv_x3_ring_kernel<3, true>), grid2, block, 0, stream, p); break;
@@ -1328,6 +1321,7 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
         }
         return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
     }
+#endif
     const dim3 grid((unsigned)(p.tiles_x * p.tiles_y));
     // Default (variant 1) since round 2: the column-tile kernel (esr_conv_x3c.hip) for 3x3 convs with cout > 32, and
     // with cout <= 32 where the 16-row classic grid fills its rounds (2-6 % faster per launch at the config-2/3
@@ -1342,7 +1336,7 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
         X3cParams c;
         c.in = p.in; c.B = B; c.H = H; c.W = W; c.in_cp = in_cp; c.cin = cin; c.w = p.w; c.bias = bias;
         c.w_scale_inv = p.w_scale_inv; c.cout = cout; c.tap_y0 = ty0; c.tap_x0 = tx0; c.tiles_x = c.tiles_y = 0;
-        c.xcd_map = g_x3_map; c.overflow = overflow; c.o = *o;
+        c.xcd_map = g_tile_map; c.overflow = overflow; c.o = *o;
         c.w_ld = c.w_roff = 0;
         c.w_cstride = 0;
         // N split: an N = 64 conv whose 16-column grid cannot give every CU two workgroups (config 3 / 5: 294 / 380
@@ -1367,9 +1361,11 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
             }
             return ESR_OK;
         }
+#ifdef ESR_X3_EXPERIMENTS
         if (g_x3_kernel == 60) return x3c_launch(c, taps_side, stream, 16);
         if (g_x3_kernel == 61) return x3c_launch(c, taps_side, stream, 32);
         if (g_x3_kernel == 62) return x3c_launch(c, taps_side, stream, 64);
+#endif
         // N = 32 3×3 convs (the RDB growth convs): 12-column tiles of four 3-column waves at three workgroups per CU
         // (variant 64; 0.9 % per config-2 step over the 16-column tiles of variant 50, bitwise equal)
         if (g_x3_kernel == 64 || ((g_x3_kernel == 1 || g_x3_kernel == 63) && taps_side == 3 && cout <= 32))
@@ -1406,6 +1402,7 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
         return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
     }
 #endif
+#ifdef ESR_X3_EXPERIMENTS  // bitwise-identical A/B variants of the classic kernel
     if (taps_side == 3 && g_x3_kernel == 20) {  // A/B: the classic kernel with compiler-scheduled fragment reads
         if (cout > 32) hipLaunchKernelGGL((conv_x3_kernel<2, 3, false>), grid, block, 0, stream, p);
         else hipLaunchKernelGGL((conv_x3_kernel<1, 3, false>), grid, block, 0, stream, p);
@@ -1425,14 +1422,15 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
         } else {
             hipLaunchKernelGGL((conv_x3_kernel<1, 3, true, 1, true, TH, 4, true>), grid, block, 0, stream, p);
         }
-    } else if (taps_side == 3 && cout <= 32 && g_x3_kernel != 22 && g_x3_kernel != 26 &&
-               (g_x3_kernel == 25 || row8_pays)) {
+    } else if (taps_side == 3 && cout <= 32 && g_x3_kernel == 22) {  // A/B: two stages, one workgroup per CU (16 rows)
+        hipLaunchKernelGGL((conv_x3_kernel<1, 3>), grid, block, 0, stream, p);
+    } else
+#endif
+    if (taps_side == 3 && cout <= 32 && g_x3_kernel != 22 && g_x3_kernel != 26 && (g_x3_kernel == 25 || row8_pays)) {
         // N = 32 with 8-row tiles (one 32-pixel M-tile per wave), one stage, three workgroups per CU (<= 80 VGPRs)
         p.tiles_y = (B * (H + 2) - 2 + 7) / 8;
         const dim3 grid8((unsigned)(p.tiles_x * p.tiles_y));
         hipLaunchKernelGGL((conv_x3_kernel<1, 3, true, 1, true, 8, 6>), grid8, block, 0, stream, p);
-    } else if (taps_side == 3 && cout <= 32 && g_x3_kernel == 22) {  // A/B: two stages, one workgroup per CU (16 rows)
-        hipLaunchKernelGGL((conv_x3_kernel<1, 3>), grid, block, 0, stream, p);
     } else if (taps_side == 3) {
         // N = 32 with 16-row tiles (variant 26, or where row8_pays is false): one LDS stage and two workgroups per CU
         // (7-14 % faster than two stages and one workgroup at the config-2/3 shapes, profiles/r1_x3_reads_ab.txt);
@@ -1454,41 +1452,6 @@ extern "C" int esr_conv3x3_fwd_x3(const void *in, int32_t B, int32_t H, int32_t 
                                   const esr_conv_out *o, int32_t *overflow, esr_stream_t stream) {
     return launch_x3(in, B, H, W, in_cp, cin, w_packed, bias, w_scale, cout, 3, 0, 0, o, overflow,
                      (hipStream_t)stream);
-}
-
-extern "C" int esr_x3_set_kernel(int32_t variant) {
-    if (variant < 0 || variant > 64) return ESR_EINVAL;
-#ifndef ESR_X3_EXPERIMENTS
-    // the production library carries the bitwise-identical A/B variants only (include/esr_amd.h)
-    const bool ab = variant <= 2 || variant == 15 || (variant >= 16 && variant <= 18) ||
-                    (variant >= 20 && variant <= 28) || variant == 50 || (variant >= 60 && variant <= 64);
-    if (!ab) return ESR_EINVAL;
-#endif
-    const int prev = g_x3_kernel;
-    g_x3_kernel = variant;
-    return prev;
-}
-
-extern "C" int esr_x3_set_nsplit(int32_t on) {
-    if (on < 0 || on > 1) return ESR_EINVAL;
-    const int prev = g_x3_nsplit;
-    g_x3_nsplit = on;
-    return prev;
-}
-
-extern "C" int esr_x3_set_narrow(int32_t on) {
-    if (on < 0 || on > 1) return ESR_EINVAL;
-    const int prev = g_x3_narrow;
-    g_x3_narrow = on;
-    return prev;
-}
-
-extern "C" int esr_x3_set_tile_map(int32_t mode) {
-    if (mode < 0 || mode > 1) return ESR_EINVAL;
-    const int prev = g_x3_map;
-    g_x3_map = mode;
-    esr_g_conv_tile_map = mode;
-    return prev;
 }
 
 extern "C" int esr_upconv2x_phase_fwd_x3(const void *in, int32_t B, int32_t H, int32_t W, int32_t in_cp, int32_t cin,

@@ -740,6 +740,7 @@ int x3c_launch(const X3cParams &p0, int taps_side, hipStream_t stream, int dbg) 
     p.tiles_y = (p.B * (p.H + 2) - 2 + CT - 1) / CT;
     const dim3 grid((unsigned)(p.tiles_x * p.tiles_y)), block(NTHR);
     const bool n64 = p.cout > 32;
+#ifdef ESR_X3_EXPERIMENTS  // A/B forms (bitwise identical): the ablation library only
     if (dbg == 32) {  // 8 waves of 2 columns (N = 32 only: the per-wave epilogue areas of N = 64 do not fit)
         const dim3 block8(64 * (TWC / 2));
         if (taps_side == 3 && !n64) hipLaunchKernelGGL((conv_x3c_kernel<1, 3, 0, false, 2>), grid, block8, 0, stream, p);
@@ -753,6 +754,7 @@ int x3c_launch(const X3cParams &p0, int taps_side, hipStream_t stream, int dbg) 
         else hipLaunchKernelGGL((conv_x3c_kernel<1, 2, 0, false, 4, true>), grid, block, 0, stream, p);
         return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
     }
+#endif
     if (dbg == 128) {  // N = 32: 12-column tiles of four 3-column waves, three workgroups per CU (48 KB LDS, <= 168 VGPRs)
         if (n64) return x3c_launch(p0, taps_side, stream, 0);
         p.tiles_x = (p.W + 11) / 12;
@@ -761,6 +763,7 @@ int x3c_launch(const X3cParams &p0, int taps_side, hipStream_t stream, int dbg) 
         else hipLaunchKernelGGL((conv_x3c_kernel<1, 2, 0, false, 3, false, 12, 3>), grid12, block, 0, stream, p);
         return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
     }
+#ifdef ESR_X3_EXPERIMENTS
     if (dbg == 16) {  // register-B form
         if (taps_side == 3) {
             if (n64) hipLaunchKernelGGL((conv_x3c_kernel<2, 3, 0, true>), grid, block, 0, stream, p);
@@ -771,7 +774,6 @@ int x3c_launch(const X3cParams &p0, int taps_side, hipStream_t stream, int dbg) 
         }
         return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
     }
-#ifdef ESR_X3_EXPERIMENTS
     if (taps_side == 3 && dbg) {
 #define XD(f) if (n64) hipLaunchKernelGGL((conv_x3c_kernel<2, 3, f>), grid, block, 0, stream, p); \
               else hipLaunchKernelGGL((conv_x3c_kernel<1, 3, f>), grid, block, 0, stream, p)

@@ -24,6 +24,7 @@
 // Numerics: v_mfma_f32_32x32x2_f32 is an exact fp32 FMA chain; only the summation order differs from a CPU conv.
 #include <hip/hip_runtime.h>
 #include "esr_amd.h"
+#include "esr_knobs.h"
 
 namespace {
 
@@ -1412,15 +1413,12 @@ constexpr int HALO_LDS_MAX = 160 * 1024;
 // The 2×2-tap stride-1 form of a 4×4 stride-2 conv over its space-to-depth source / into its depth-to-space output
 // (sd: esr_dconv_fwd_sd) stages each source pixel once per 32 virtual channels — 8 real channels × 4 phases — so its
 // window fits 8-row tiles at two workgroups per CU; it takes the halo kernel under the same width rule.
-int g_dconv_halo = 1; // esr_dconv_set_halo: the halo-tile kernels where they apply (halo_wanted), every precision;
-                      // 2 = also the space-to-depth forms and the >= 9-tap convs at any width (A/B)
 bool halo_wanted(int smy, int smx, int T, int MW, bool sd = false) {
     const int covered = 32 * ((MW + 31) / 32);
     if (g_dconv_halo == 2 && (sd || T >= 9) && smy == 1 && smx == 1) return true;
     return smy == 1 && smx == 1 && (T == 1 || T >= 9 || sd) && 10 * (covered - MW) <= 3 * MW;
 }
 
-int g_dconv_cw16 = 1;  // esr_dconv_set_cw16: the 16-column halo tiles where 32-column ones do not pay (A/B)
 
 // Tile width of the halo kernel for a launch: 32, 16 (x3 only: 2 rows × 16 columns per M-tile where a 16-column grid
 // meets the ≤ 30 % waste rule and a 32-column one does not — fc8's data gradient on the 38-wide grid at config 3:
@@ -1540,7 +1538,6 @@ bool launch_rows_np(const WrowParams &p, const RowsPlan &r, dim3 grid, hipStream
     return true;
 }
 
-int g_dconv_occ3 = 1;  // esr_dconv_set_occ3 (A/B)
 
 template <int WM, int WN>
 void launch_halo_f32(const FwdParams &p, const HaloParams &h, dim3 grid, int lds, hipStream_t st) {
@@ -1589,20 +1586,29 @@ void launch_halo_x(const FwdParams &p, const HaloParams &h, dim3 grid, int lds, 
 
 }  // namespace
 
-int g_dconv_rows = 0; // esr_dconv_set_rows: the tap-row weight-gradient kernel (opt-in: slower than the per-tap
-                      // kernel at config 3 with one resident workgroup per CU, profiles/r3_dconv_ab.txt)
 
-int g_dconv_x3 = 0;   // esr_dconv_set_x3
-int g_dconv_np = 2;   // split pieces of the x3 kernels: 2 = x3, 3 = x6 (esr_dconv_set_x3(3))
-int g_dconv_nb = 128; // x3: widest N tile allowed (esr_dconv_set_x3(2) = 64 only, for A/B)
+
+// Per-call precision of the discriminator convs (include/esr_amd.h `prec`): 0 = exact fp32, 1 = x3 (128-wide N tiles
+// where the grid allows), 2 = x3 with 64-wide N tiles only, 3 = x6.  np = f16 pieces per operand value (0: fp32),
+// nb = widest N tile.
+struct DPrec {
+    int np, nb;
+};
+bool decode_prec(int32_t prec, DPrec &d) {
+    if (prec < 0 || prec > 3) return false;
+    d.np = prec == 0 ? 0 : prec == 3 ? 3 : 2;
+    d.nb = prec == 2 ? 64 : 128;
+    return true;
+}
 
 extern "C" int esr_dconv_fwd_sd(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t src_pitch, int32_t kc,
                                 const float *w_packed, int32_t nck, int32_t n_pad, const float *bias, float *out,
                                 int32_t Ho, int32_t Wo, int32_t out_pitch, int32_t n, int32_t MH, int32_t MW,
                                 int32_t omy, int32_t oay, int32_t omx, int32_t oax, int32_t smy, int32_t smx, int32_t T,
                                 const int32_t *offy, const int32_t *offx, int32_t ksplit, float *partial, int32_t s2d_c,
-                                int32_t s2d_pad, int32_t d2s_c, int32_t d2s_pad, esr_stream_t stream) {
-    if (!src || !w_packed || !out || !offy || !offx) return ESR_EINVAL;
+                                int32_t s2d_pad, int32_t d2s_c, int32_t d2s_pad, int32_t prec, esr_stream_t stream) {
+    DPrec dp;
+    if (!src || !w_packed || !out || !offy || !offx || !decode_prec(prec, dp)) return ESR_EINVAL;
     if (ksplit < 1 || (ksplit > 1 && (!partial || ksplit > T * nck))) return ESR_EINVAL;
     if (s2d_c < 0 || d2s_c < 0 || s2d_pad < 0 || d2s_pad < 0) return ESR_EINVAL;
     const int src_c = s2d_c ? s2d_c : kc, out_c = d2s_c ? d2s_c : n;  // real channels per source / output pixel
@@ -1641,7 +1647,7 @@ extern "C" int esr_dconv_fwd_sd(const float *src, int32_t B, int32_t Hs, int32_t
     if (M + MT >= 0x7fffffffLL) return ESR_EINVAL;  // the kernels index output pixels in 32 bits
     HaloParams h;
     int lds = 0;
-    const int np = g_dconv_x3 ? g_dconv_np : 0;
+    const int np = dp.np;
     const int cwh = halo_cols(smy, smx, T, MW, sd, np);
     if (cwh && halo_plan(MH, MW, smy, smx, T, offy, offx, h, lds, np == 3 ? XPitch<3>::v : PS * 4, NB, cwh)) {
         if (ksplit > nck) return ESR_EINVAL;  // the halo kernels split the channel chunks
@@ -1658,7 +1664,7 @@ extern "C" int esr_dconv_fwd_sd(const float *src, int32_t B, int32_t Hs, int32_t
             // has >= 512 workgroups without a split (profiles/r3_dconv_nb128_ab.txt)
             HaloParams h2;
             int lds2 = 0;
-            if (h.cw == 32 && g_dconv_nb != 64 && ksplit == 1 && n_pad % 128 == 0 && h.TY == 8 && hx * (n_pad / 128) >= 512 &&
+            if (h.cw == 32 && dp.nb != 64 && ksplit == 1 && n_pad % 128 == 0 && h.TY == 8 && hx * (n_pad / 128) >= 512 &&
                 halo_plan(MH, MW, smy, smx, T, offy, offx, h2, lds2, PS * 4, 128) && h2.TY == 8 &&
                 lds2 <= HALO_LDS_2PER_CU) {
                 launch_halo_x<2, 4, 2, 128>(p, h2, dim3((unsigned)hx, (unsigned)(n_pad / 128), 1), lds2, st);
@@ -1677,17 +1683,17 @@ extern "C" int esr_dconv_fwd_sd(const float *src, int32_t B, int32_t Hs, int32_t
     }
     const dim3 grid((unsigned)gx, (unsigned)((n + NB - 1) / NB)), block(NTH);
     // 128-channel N tiles only where the grid still fills the chip (the A tile then feeds twice the MFMAs)
-    const bool wide = n_pad % 128 == 0 && g_dconv_nb != 64 && gx * (n_pad / 128) * ksplit >= 512;
+    const bool wide = n_pad % 128 == 0 && dp.nb != 64 && gx * (n_pad / 128) * ksplit >= 512;
     const dim3 g128((unsigned)gx, (unsigned)(n_pad / 128), (unsigned)ksplit);
     const dim3 g64((unsigned)gx, (unsigned)(n_pad / 64), (unsigned)ksplit);
     const hipStream_t hst = (hipStream_t)stream;
-    if (g_dconv_x3 && g_dconv_np == 3 && wide)
+    if (np == 3 && wide)
         hipLaunchKernelGGL((dconv_fwd_x3_kernel<128, 3>), g128, block, 0, hst, p);
-    else if (g_dconv_x3 && g_dconv_np == 3)
+    else if (np == 3)
         hipLaunchKernelGGL((dconv_fwd_x3_kernel<64, 3>), g64, block, 0, hst, p);
-    else if (g_dconv_x3 && wide)
+    else if (np == 2 && wide)
         hipLaunchKernelGGL((dconv_fwd_x3_kernel<128, 2>), g128, block, 0, hst, p);
-    else if (g_dconv_x3)
+    else if (np == 2)
         hipLaunchKernelGGL((dconv_fwd_x3_kernel<64, 2>), g64, block, 0, hst, p);
     else
         hipLaunchKernelGGL(dconv_fwd_kernel, grid, block, 0, (hipStream_t)stream, p);
@@ -1702,32 +1708,35 @@ extern "C" int esr_dconv_fwd_sk(const float *src, int32_t B, int32_t Hs, int32_t
                                 int32_t Ho, int32_t Wo, int32_t out_pitch, int32_t n, int32_t MH, int32_t MW,
                                 int32_t omy, int32_t oay, int32_t omx, int32_t oax, int32_t smy, int32_t smx, int32_t T,
                                 const int32_t *offy, const int32_t *offx, int32_t ksplit, float *partial,
-                                esr_stream_t stream) {
+                                int32_t prec, esr_stream_t stream) {
     return esr_dconv_fwd_sd(src, B, Hs, Ws, src_pitch, kc, w_packed, nck, n_pad, bias, out, Ho, Wo, out_pitch, n, MH,
-                            MW, omy, oay, omx, oax, smy, smx, T, offy, offx, ksplit, partial, 0, 0, 0, 0, stream);
+                            MW, omy, oay, omx, oax, smy, smx, T, offy, offx, ksplit, partial, 0, 0, 0, 0, prec, stream);
 }
 
 extern "C" int esr_dconv_fwd(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t src_pitch, int32_t kc,
                              const float *w_packed, int32_t nck, int32_t n_pad, const float *bias, float *out,
                              int32_t Ho, int32_t Wo, int32_t out_pitch, int32_t n, int32_t MH, int32_t MW, int32_t omy,
                              int32_t oay, int32_t omx, int32_t oax, int32_t smy, int32_t smx, int32_t T,
-                             const int32_t *offy, const int32_t *offx, esr_stream_t stream) {
+                             const int32_t *offy, const int32_t *offx, int32_t prec, esr_stream_t stream) {
     return esr_dconv_fwd_sk(src, B, Hs, Ws, src_pitch, kc, w_packed, nck, n_pad, bias, out, Ho, Wo, out_pitch, n, MH,
-                            MW, omy, oay, omx, oax, smy, smx, T, offy, offx, 1, nullptr, stream);
+                            MW, omy, oay, omx, oax, smy, smx, T, offy, offx, 1, nullptr, prec, stream);
 }
 
 extern "C" int esr_dconv_fwd_splits_sd(int32_t B, int32_t MH, int32_t MW, int32_t n, int32_t kc, int32_t smy,
-                                       int32_t smx, int32_t T, const int32_t *offy, const int32_t *offx, int32_t sd) {
-    if (B <= 0 || MH <= 0 || MW <= 0 || n <= 0 || kc <= 0 || T <= 0 || T > ESR_DCONV_MAX_TAPS || !offy || !offx)
+                                       int32_t smx, int32_t T, const int32_t *offy, const int32_t *offx, int32_t sd,
+                                       int32_t prec) {
+    DPrec dp;
+    if (B <= 0 || MH <= 0 || MW <= 0 || n <= 0 || kc <= 0 || T <= 0 || T > ESR_DCONV_MAX_TAPS || !offy || !offx ||
+        !decode_prec(prec, dp))
         return ESR_EINVAL;
     const int nck = (kc + KC - 1) / KC, n_pad = NB * ((n + NB - 1) / NB);
     HaloParams h;
     int lds = 0;
-    const int np = g_dconv_x3 ? g_dconv_np : 0;
+    const int np = dp.np;
     const int cwh = halo_cols(smy, smx, T, MW, sd != 0, np);
     if (cwh && halo_plan(MH, MW, smy, smx, T, offy, offx, h, lds, np == 3 ? XPitch<3>::v : PS * 4, NB, cwh))
         return halo_splits(h, B, n_pad, nck);
-    if (!g_dconv_x3) return 1;
+    if (!np) return 1;
     // x3 gather kernel: ~512 workgroups, at least 8 K steps per slice, for launches that would fill few CUs
     const long long wgs = ((long long)B * MH * MW + MT - 1) / MT * (n_pad / NB);
     const int nsteps = T * nck;
@@ -1735,28 +1744,32 @@ extern "C" int esr_dconv_fwd_splits_sd(int32_t B, int32_t MH, int32_t MW, int32_
     return (int)max(1LL, min((512 + wgs - 1) / wgs, (long long)(nsteps / 8)));
 }
 
-extern "C" int esr_dconv_uses_halo(int32_t smy, int32_t smx, int32_t T, int32_t MW, int32_t sd) {
-    if (T <= 0 || T > ESR_DCONV_MAX_TAPS || MW <= 0) return ESR_EINVAL;
-    return halo_cols(smy, smx, T, MW, sd != 0, g_dconv_x3 ? g_dconv_np : 0) ? 1 : 0;
+extern "C" int esr_dconv_uses_halo(int32_t smy, int32_t smx, int32_t T, int32_t MW, int32_t sd, int32_t prec) {
+    DPrec dp;
+    if (T <= 0 || T > ESR_DCONV_MAX_TAPS || MW <= 0 || !decode_prec(prec, dp)) return ESR_EINVAL;
+    return halo_cols(smy, smx, T, MW, sd != 0, dp.np) ? 1 : 0;
 }
 
 extern "C" int esr_dconv_fwd_splits(int32_t B, int32_t MH, int32_t MW, int32_t n, int32_t kc, int32_t smy,
-                                    int32_t smx, int32_t T, const int32_t *offy, const int32_t *offx) {
-    return esr_dconv_fwd_splits_sd(B, MH, MW, n, kc, smy, smx, T, offy, offx, 0);
+                                    int32_t smx, int32_t T, const int32_t *offy, const int32_t *offx, int32_t prec) {
+    return esr_dconv_fwd_splits_sd(B, MH, MW, n, kc, smy, smx, T, offy, offx, 0, prec);
 }
 
 extern "C" int esr_dconv_wgrad_splits(int32_t B, int32_t MH, int32_t MW, int32_t cin, int32_t cout, int32_t smy,
-                                     int32_t smx, int32_t T, const int32_t *offy, const int32_t *offx) {
-    if (B <= 0 || MH <= 0 || MW <= 0 || cin <= 0 || cout <= 0 || T <= 0 || T > ESR_DCONV_MAX_TAPS || !offy || !offx)
+                                     int32_t smx, int32_t T, const int32_t *offy, const int32_t *offx,
+                                     int32_t prec) {
+    DPrec dp;
+    if (B <= 0 || MH <= 0 || MW <= 0 || cin <= 0 || cout <= 0 || T <= 0 || T > ESR_DCONV_MAX_TAPS || !offy || !offx ||
+        !decode_prec(prec, dp))
         return ESR_EINVAL;
     (void)smy;
     const int cin_pad = 64 * ((cin + 63) / 64), cout_pad = 64 * ((cout + 63) / 64);
     const long long n = (long long)T * cin_pad * cout_pad, P = (long long)B * MH * MW;
     const long long pmax = max(1LL, (64LL << 20) / n);
     RowsPlan rp;
-    if (g_dconv_x3 && g_dconv_rows && rows_plan(smx, T, offy, offx, g_dconv_np, rp))
+    if (dp.np && g_dconv_rows != 0 && rows_plan(smx, T, offy, offx, dp.np, rp))
         return rows_splits(rp, B, MH, MW, cin, cout, T);
-    if (g_dconv_x3) {  // per-tap split kernel: 128-channel blocks where the padded widths allow, ~2 workgroups per CU
+    if (dp.np) {  // per-tap split kernel: 128-channel blocks where the padded widths allow, ~2 workgroups per CU
         const int cib = cin_pad % 128 == 0 ? 128 : 64, cob = cout_pad % 128 == 0 ? 128 : 64;
         const long long tiles = (long long)T * (cin_pad / cib) * (cout_pad / cob);
         return (int)max(1LL, min(min((512 + tiles - 1) / tiles, (P + 255) / 256), pmax));
@@ -1765,48 +1778,12 @@ extern "C" int esr_dconv_wgrad_splits(int32_t B, int32_t MH, int32_t MW, int32_t
     return (int)max(1LL, min(min((1024 + tiles - 1) / tiles, (P + 255) / 256), pmax));
 }
 
-extern "C" int esr_dconv_set_rows(int32_t on) {
-    if (on < 0 || on > 1) return ESR_EINVAL;
-    const int prev = g_dconv_rows;
-    g_dconv_rows = on;
-    return prev;
-}
-
-extern "C" int esr_dconv_set_cw16(int32_t on) {
-    if (on < 0 || on > 1) return ESR_EINVAL;
-    const int prev = g_dconv_cw16;
-    g_dconv_cw16 = on;
-    return prev;
-}
-
-extern "C" int esr_dconv_set_occ3(int32_t on) {
-    if (on < 0 || on > 1) return ESR_EINVAL;
-    const int prev = g_dconv_occ3;
-    g_dconv_occ3 = on;
-    return prev;
-}
-
-extern "C" int esr_dconv_set_halo(int32_t on) {
-    if (on < 0 || on > 2) return ESR_EINVAL;
-    const int prev = g_dconv_halo;
-    g_dconv_halo = on;
-    return prev;
-}
-
-extern "C" int esr_dconv_set_x3(int32_t on) {
-    if (on < 0 || on > 3) return ESR_EINVAL;
-    const int prev = g_dconv_x3 ? (g_dconv_np == 3 ? 3 : g_dconv_nb == 64 ? 2 : 1) : 0;
-    g_dconv_x3 = on != 0;
-    g_dconv_nb = on == 2 ? 64 : 128;
-    g_dconv_np = on == 3 ? 3 : 2;
-    return prev;
-}
-
 extern "C" int esr_dconv_wgrad(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t src_pitch, int32_t cin,
                                const float *dy, int32_t MH, int32_t MW, int32_t dy_pitch, int32_t cout, int32_t smy,
                                int32_t smx, int32_t T, const int32_t *offy, const int32_t *offx, int32_t splits,
-                               float *partial, esr_stream_t stream) {
-    if (!src || !dy || !partial || !offy || !offx) return ESR_EINVAL;
+                               float *partial, int32_t prec, esr_stream_t stream) {
+    DPrec dp;
+    if (!src || !dy || !partial || !offy || !offx || !decode_prec(prec, dp)) return ESR_EINVAL;
     if (B <= 0 || Hs <= 0 || Ws <= 0 || cin <= 0 || src_pitch < cin || MH <= 0 || MW <= 0 || cout <= 0 ||
         dy_pitch < cout || T <= 0 || T > ESR_DCONV_MAX_TAPS || splits <= 0)
         return ESR_EINVAL;
@@ -1823,7 +1800,7 @@ extern "C" int esr_dconv_wgrad(const float *src, int32_t B, int32_t Hs, int32_t 
     p.partial = partial;
     for (int t = 0; t < T; ++t) { p.offy[t] = offy[t]; p.offx[t] = offx[t]; }
     RowsPlan rp;
-    if (g_dconv_x3 && g_dconv_rows && rows_plan(smx, T, offy, offx, g_dconv_np, rp)) {
+    if (dp.np && g_dconv_rows != 0 && rows_plan(smx, T, offy, offx, dp.np, rp)) {
         WrowParams q;
         q.src = src; q.B = B; q.Hs = Hs; q.Ws = Ws; q.sp = src_pitch; q.cin = cin; q.svec = p.svec;
         q.dy = dy; q.MH = MH; q.MW = MW; q.dp = dy_pitch; q.cout = cout; q.dvec = p.dvec;
@@ -1837,17 +1814,17 @@ extern "C" int esr_dconv_wgrad(const float *src, int32_t B, int32_t Hs, int32_t 
         for (int t = 0; t < T; ++t) { q.offy[t] = offy[t]; q.offx[t] = offx[t]; }
         const long long gx = (long long)(T / rp.KT) * ((cin + rp.CIB - 1) / rp.CIB) * ((cout + rp.COB - 1) / rp.COB);
         const dim3 grid((unsigned)gx, (unsigned)splits);
-        const bool ok = g_dconv_np == 3 ? launch_rows_np<3>(q, rp, grid, (hipStream_t)stream)
+        const bool ok = dp.np == 3 ? launch_rows_np<3>(q, rp, grid, (hipStream_t)stream)
                                         : launch_rows_np<2>(q, rp, grid, (hipStream_t)stream);
         if (!ok) return ESR_EINVAL;
         return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
     }
-    if (g_dconv_x3) {  // x3: 128-channel blocks where the padded width is a multiple of 128
+    if (dp.np) {  // x3 / x6: 128-channel blocks where the padded width is a multiple of 128
         const int cib = (64 * p.ci_blocks) % 128 == 0 ? 128 : 64, cob = (64 * p.co_blocks) % 128 == 0 ? 128 : 64;
         const long long gx = (long long)T * ((cin + cib - 1) / cib) * ((cout + cob - 1) / cob);
         const dim3 grid((unsigned)gx, (unsigned)splits), block(NTH);
         const hipStream_t st = (hipStream_t)stream;
-        if (g_dconv_np == 3) {
+        if (dp.np == 3) {
             if (cib == 128 && cob == 128) hipLaunchKernelGGL((dconv_wgrad_x3_kernel<128, 128, 3>), grid, block, 0, st, p);
             else if (cib == 128) hipLaunchKernelGGL((dconv_wgrad_x3_kernel<128, 64, 3>), grid, block, 0, st, p);
             else if (cob == 128) hipLaunchKernelGGL((dconv_wgrad_x3_kernel<64, 128, 3>), grid, block, 0, st, p);

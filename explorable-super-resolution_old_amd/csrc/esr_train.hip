@@ -14,6 +14,7 @@
 //                      F^T(g)[k] = Σ_{(o,u): clamp(s·o + c + u - p) = k} w[u] g[o]   (2-D, separable clamp)
 #include <hip/hip_runtime.h>
 #include "esr_amd.h"
+#include "esr_knobs.h"
 
 namespace {
 
@@ -805,9 +806,7 @@ __global__ __launch_bounds__((W3D<NCT, TH>::NT), 1) void wgrad3d_kernel(WgradPar
     }
 }
 
-int g_wgrad3_dma = 1;  // esr_wgrad3_set_dma: wgrad3d for split-f16 output gradients (0: wgrad3, A/B)
 
-int g_wgrad_kernel = 1;  // 0 = wgrad_kernel (4 waves), 1 = wgrad2_kernel (12 waves)
 
 // Gradient scale of the x3 backward (esr_grad_amax): S = 2^(11 - ex) for max|g| < 2^ex, so the largest scaled
 // element lies in [2^10, 2^11) (headroom 2^5 below the f16 range for growth through a residual block); 1 for an
@@ -1028,10 +1027,9 @@ struct AdjParams {
     int K, s, c, Ly, Lx, Oy, Ox, os, oc, Ny, Nx, planes;
     float alpha;      // out = alpha * F^T(g) (+ beta * out when accumulate)
     int accumulate;
-    int fast;         // interior fast path (esr_cem_adjoint_set_generic(0), the default)
+    int fast;         // interior fast path (default; esr_cem_adjoint flags bit 1 = generic)
 };
 
-int g_adjoint_generic = 0;  // esr_cem_adjoint_set_generic
 
 __global__ __launch_bounds__(NT) void cem_adjoint_kernel(AdjParams p) {
     __shared__ float sw[64 * 64];
@@ -1171,20 +1169,6 @@ extern "C" int esr_conv3x3_wgrad(const float *in, int32_t in_cp, int32_t cin, in
     return launched();
 }
 
-extern "C" int esr_wgrad3_set_dma(int32_t on) {
-    if (on < 0 || on > 1) return ESR_EINVAL;
-    const int prev = g_wgrad3_dma;
-    g_wgrad3_dma = on;
-    return prev;
-}
-
-extern "C" int esr_wgrad_set_kernel(int32_t variant) {
-    if (variant < 0 || variant > 1) return ESR_EINVAL;
-    const int prev = g_wgrad_kernel;
-    g_wgrad_kernel = variant;
-    return prev;
-}
-
 extern "C" int esr_wgrad_reduce(const float *partial, int32_t splits, int64_t n, float scale, float *out,
                                 esr_stream_t stream) {
     if (!partial || !out || splits <= 0 || n <= 0) return ESR_EINVAL;
@@ -1274,24 +1258,17 @@ extern "C" int esr_nchw_to_padded(const float *src, int32_t C, int32_t B, int32_
 
 extern "C" int esr_cem_adjoint(const float *g, int32_t planes, int32_t Oy, int32_t Ox, const float *w, int32_t K,
                                int32_t s, int32_t c, int32_t Ly, int32_t Lx, int32_t os, int32_t oc, float alpha,
-                               int32_t accumulate, float *out, esr_stream_t stream) {
+                               int32_t flags, float *out, esr_stream_t stream) {
     if (!g || !w || !out || planes <= 0 || Oy <= 0 || Ox <= 0 || K <= 0 || K > 64 || !(K & 1) || s <= 0 ||
-        Ly <= 0 || Lx <= 0 || os <= 0 || oc < 0 || oc >= os)
+        Ly <= 0 || Lx <= 0 || os <= 0 || oc < 0 || oc >= os || (flags & ~3))
         return ESR_EINVAL;
     AdjParams p;
     p.g = g; p.out = out; p.w = w; p.K = K; p.s = s; p.c = c; p.Ly = Ly; p.Lx = Lx; p.Oy = Oy; p.Ox = Ox;
     p.os = os; p.oc = oc; p.Ny = (Ly - oc + os - 1) / os; p.Nx = (Lx - oc + os - 1) / os; p.planes = planes;
-    p.alpha = alpha; p.accumulate = accumulate; p.fast = !g_adjoint_generic;
+    p.alpha = alpha; p.accumulate = flags & 1; p.fast = !(flags & 2);
     hipLaunchKernelGGL(cem_adjoint_kernel, dim3(nblocks((long long)planes * p.Ny * p.Nx)), dim3(NT), 0,
                        (hipStream_t)stream, p);
     return launched();
-}
-
-extern "C" int esr_cem_adjoint_set_generic(int32_t on) {
-    if (on < 0 || on > 1) return ESR_EINVAL;
-    const int prev = g_adjoint_generic;
-    g_adjoint_generic = on;
-    return prev;
 }
 
 extern "C" int esr_input_adjoint(const float *d_hr, int32_t hr_cp, int32_t hr_coff, const float *d_lr, int32_t lr_cp,

@@ -8,7 +8,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('ESR_AMD_LIB', os.path.join(_HERE, 'libesr_amd.so'))
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 c_int = ctypes.c_int32
 c_float = ctypes.c_float
@@ -48,12 +48,6 @@ _SIGNATURES = {
                            ctypes.POINTER(ConvOut), c_void_p, c_void_p],
     'esr_upconv2x_phase_fwd_x3': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_int,
                                   c_int, c_int, ctypes.POINTER(ConvOut), c_void_p, c_void_p],
-    'esr_x3_set_kernel': [c_int],
-    'esr_x3_set_tile_map': [c_int],
-    'esr_x3_set_narrow': [c_int],
-    'esr_x3_set_nsplit': [c_int],
-    'esr_cem_set_direct': [c_int],
-    'esr_conv_set_tile': [c_int],
     'esr_cem_down': [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int,
                      c_void_p],
     'esr_cem_inv': [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p],
@@ -62,7 +56,6 @@ _SIGNATURES = {
     'esr_conv3x3_wgrad': [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                           c_void_p, c_void_p],
     'esr_wgrad_reduce': [c_void_p, c_int, ctypes.c_int64, c_float, c_void_p, c_void_p],
-    'esr_dconv_set_x3': [c_int],
     'esr_bn_workspace_floats': [ctypes.c_int64, c_int],
     'esr_bn_lrelu_fwd': [c_void_p, ctypes.c_int64, c_int, c_void_p, c_void_p, c_float, c_float, c_void_p, c_void_p,
                          c_void_p, c_void_p, c_void_p, c_void_p],
@@ -80,8 +73,6 @@ _SIGNATURES = {
     'esr_grad_amax': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     'esr_axpby_gs': [c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_int,
                      c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
-    'esr_wgrad_set_kernel': [c_int],
-    'esr_wgrad3_set_dma': [c_int],
     'esr_lrelu_bwd': [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     'esr_lrelu_bwd_split': [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     'esr_axpby': [c_void_p, c_int, c_int, c_float, c_void_p, c_int, c_int, c_float, c_void_p, c_int, c_int, c_int,
@@ -94,28 +85,23 @@ _SIGNATURES = {
                           c_int, c_void_p, c_void_p],
     'esr_dconv_fwd': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
                       c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
-                      ctypes.POINTER(c_int), ctypes.POINTER(c_int), c_void_p],
+                      ctypes.POINTER(c_int), ctypes.POINTER(c_int), c_int, c_void_p],
     'esr_dconv_fwd_sk': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
                          c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
-                         ctypes.POINTER(c_int), ctypes.POINTER(c_int), c_int, c_void_p, c_void_p],
+                         ctypes.POINTER(c_int), ctypes.POINTER(c_int), c_int, c_void_p, c_int, c_void_p],
     'esr_dconv_fwd_splits': [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_int),
-                             ctypes.POINTER(c_int)],
+                             ctypes.POINTER(c_int), c_int],
     'esr_dconv_fwd_sd': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
                          c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                          ctypes.POINTER(c_int), ctypes.POINTER(c_int), c_int, c_void_p, c_int, c_int, c_int, c_int,
-                         c_void_p],
-    'esr_dconv_uses_halo': [c_int, c_int, c_int, c_int, c_int],
+                         c_int, c_void_p],
+    'esr_dconv_uses_halo': [c_int, c_int, c_int, c_int, c_int, c_int],
     'esr_dconv_fwd_splits_sd': [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_int),
-                                ctypes.POINTER(c_int), c_int],
-    'esr_dconv_set_halo': [c_int],
-    'esr_dconv_set_occ3': [c_int],
-    'esr_dconv_set_cw16': [c_int],
+                                ctypes.POINTER(c_int), c_int, c_int],
     'esr_dconv_wgrad_splits': [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_int),
-                               ctypes.POINTER(c_int)],
-    'esr_dconv_set_rows': [c_int],
-    'esr_cem_adjoint_set_generic': [c_int],
+                               ctypes.POINTER(c_int), c_int],
     'esr_dconv_wgrad': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int,
-                        c_int, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int), c_int, c_void_p, c_void_p],
+                        c_int, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int), c_int, c_void_p, c_int, c_void_p],
     'esr_timer_create': [c_int],
     'esr_timer_elapsed': [c_void_p, c_fp],
     'esr_timer_destroy': [c_void_p],
@@ -126,6 +112,14 @@ _SIGNATURES = {
 _RESTYPES = {'esr_timer_create': c_void_p, 'esr_timer_destroy': None, 'esr_bn_workspace_floats': ctypes.c_int64}
 EXPORTED = tuple(_SIGNATURES)
 
+# Extra entry points of the ABLATION library (csrc/esr_ablation.h; `make -C .../csrc exp` -> exp_lib/libesr_exp.so):
+# process-wide kernel-selection setters for same-box A/B runs and the variant-equality tests.  The product library
+# exports none of them (it has no selection state).
+ABLATION_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), 'exp_lib', 'libesr_exp.so')
+ABLATION_SETTERS = ('esr_x3_set_kernel', 'esr_x3_set_tile_map', 'esr_x3_set_narrow', 'esr_x3_set_nsplit',
+                    'esr_conv_set_tile', 'esr_cem_set_direct', 'esr_wgrad_set_kernel', 'esr_wgrad3_set_dma',
+                    'esr_dconv_set_halo', 'esr_dconv_set_occ3', 'esr_dconv_set_cw16', 'esr_dconv_set_rows')
+
 _lib = None
 
 
@@ -133,32 +127,48 @@ class ESRLibraryError(RuntimeError):
     pass
 
 
-def load():
-    """Load libesr_amd.so once and bind prototypes.  Raises ESRLibraryError if absent or ABI-incompatible."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
-        raise ESRLibraryError('libesr_amd.so not found at %s: build it with `make -C explorable-super-resolution_old_amd'
-                              '/csrc` (or __graft_entry__.build()); there is no non-HIP fallback' % LIB_PATH)
-    lib = ctypes.CDLL(LIB_PATH)
+def bind(path):
+    """ctypes handle of the library at `path` with every prototype bound (the product ABI, plus the ablation setters
+    when the library exports them).  Raises ESRLibraryError if absent or ABI-incompatible."""
+    if not os.path.exists(path):
+        raise ESRLibraryError('%s not found: build it with `make -C explorable-super-resolution_old_amd/csrc` (or '
+                              '__graft_entry__.build()); there is no non-HIP fallback' % path)
+    lib = ctypes.CDLL(path)
     for name, argtypes in _SIGNATURES.items():
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = _RESTYPES.get(name, c_int)
     v = lib.esr_abi_version()
     if v != ABI_VERSION:
-        raise ESRLibraryError('libesr_amd.so ABI %d != expected %d (stale build?)' % (v, ABI_VERSION))
+        raise ESRLibraryError('%s ABI %d != expected %d (stale build?)' % (path, v, ABI_VERSION))
     if lib.esr_op_size() != ctypes.sizeof(EsrOp):
         raise ESRLibraryError('esr_op layout mismatch: C %d bytes, binding %d' % (lib.esr_op_size(),
                                                                                   ctypes.sizeof(EsrOp)))
-    # process-wide kernel switches for same-box A/B runs (defaults are the library's)
-    if os.environ.get('ESR_X3_NSPLIT') in ('0', '1'):
-        lib.esr_x3_set_nsplit(int(os.environ['ESR_X3_NSPLIT']))
-    if os.environ.get('ESR_X3_KERNEL', '').isdigit():
-        lib.esr_x3_set_kernel(int(os.environ['ESR_X3_KERNEL']))
-    _lib = lib
+    if hasattr(lib, 'esr_x3_set_kernel'):  # the ablation library
+        for name in ABLATION_SETTERS:
+            fn = getattr(lib, name)
+            fn.argtypes = [c_int]
+            fn.restype = c_int
     return lib
+
+
+def load():
+    """The library of the product path (libesr_amd.so, or ESR_AMD_LIB), loaded once."""
+    global _lib
+    if _lib is None:
+        _lib = bind(LIB_PATH)
+    return _lib
+
+
+_ablation = None
+
+
+def load_ablation():
+    """The ablation library (exp_lib/libesr_exp.so), loaded once; ESRLibraryError if it was not built."""
+    global _ablation
+    if _ablation is None:
+        _ablation = bind(ABLATION_PATH)
+    return _ablation
 
 
 def check(rc, what):

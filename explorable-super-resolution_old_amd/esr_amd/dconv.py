@@ -28,21 +28,20 @@ MAX_TAPS = 64
 # with per-K-step power-of-two scaling on f16 MFMA (3 products, ~2^-22 per product), 'x6' = three f16 pieces and six
 # products (each operand to ~33 bits: an fp32 FMA chain's accuracy, esr_dconv.hip), 'f32' = exact fp32 MFMA.
 PRECISION = os.environ.get('ESR_DCONV_PRECISION', 'x3')
+# esr_dconv_* `prec` argument (include/esr_amd.h): per call, the library keeps no precision state
 _LIB_MODE = {'f32': 0, 'x3': 1, 'x6': 3}
-# x3: 128-wide N tiles where the grid allows (esr_dconv_set_x3(1)); '0' = 64-wide only (esr_dconv_set_x3(2), A/B)
+# x3: 128-wide N tiles where the grid allows (prec 1); '0' = 64-wide only (prec 2, identical results; A/B)
 if os.environ.get('ESR_DCONV_NB128', '1') == '0':
     _LIB_MODE['x3'] = 2
-# exact-fp32 forward / data-gradient kernel: the halo-tile implicit GEMM (default) or the per-tap gather ('0', A/B)
-HALO = os.environ.get('ESR_DCONV_HALO', '1') != '0'
 # 4×4 stride-2 convs (and any even k at stride 2) and their data gradients as (k/2)×(k/2)-tap stride-1 convs over the
 # space-to-depth source / into the depth-to-space gradient (esr_dconv_fwd_sd, one launch each); '0' = the direct
 # stride-2 gather and one launch per phase class (A/B)
 S2D = os.environ.get('ESR_DCONV_S2D', '1') != '0'
-_applied = [None]
 
 
 def set_precision(p):
-    """Select 'x3', 'x6' or 'f32' for the discriminator convolutions (process-wide); returns the previous setting."""
+    """Select 'x3', 'x6' or 'f32' for the discriminator convolutions (the default of every launch that does not name
+    its own); returns the previous setting."""
     global PRECISION
     if p not in _LIB_MODE:
         raise ValueError(p)
@@ -50,21 +49,9 @@ def set_precision(p):
     return prev
 
 
-# x3 halo kernel at three workgroups per CU where its LDS allows (esr_dconv_set_occ3); '0' = two (A/B)
-OCC3 = os.environ.get('ESR_DCONV_OCC3', '1') != '0'
-# x3 halo kernel with 16-column tiles on narrow grids (esr_dconv_set_cw16); '0' = the gather kernel there (A/B)
-CW16 = os.environ.get('ESR_DCONV_CW16', '1') != '0'
-
-
-def _lib_for_launch():
-    lib = _lib.load()
-    if _applied[0] != PRECISION:
-        lib.esr_dconv_set_x3(_LIB_MODE[PRECISION])
-        lib.esr_dconv_set_halo(1 if HALO else 0)
-        lib.esr_dconv_set_occ3(1 if OCC3 else 0)
-        lib.esr_dconv_set_cw16(1 if CW16 else 0)
-        _applied[0] = PRECISION
-    return lib
+def _mode(prec):
+    """The library's `prec` code for a launch: `prec` ('x3' / 'x6' / 'f32') or, if None, the module default."""
+    return _LIB_MODE[PRECISION if prec is None else prec]
 
 
 def _stream(t):
@@ -118,7 +105,8 @@ def _packed(w, key, make):
     return val
 
 
-def _gather(src, packed, bias, out, MH, MW, omy, oay, omx, oax, smy, smx, offy, offx, s2d_pad=None, d2s_pad=None):
+def _gather(src, packed, bias, out, MH, MW, omy, oay, omx, oax, smy, smx, offy, offx, s2d_pad=None, d2s_pad=None,
+            prec=None):
     """One esr_dconv_fwd launch: src [B][Hs][Ws][C] and out [B][Ho][Wo][N] contiguous NHWC, `packed` = _pack(wt [T][K][N'],
     N').  s2d_pad: src is read through its space-to-depth view (K = 4C virtual channels); d2s_pad: out is written
     through its depth-to-space view (N' = 4N virtual channels); include/esr_amd.h esr_dconv_fwd_sd."""
@@ -127,11 +115,12 @@ def _gather(src, packed, bias, out, MH, MW, omy, oay, omx, oax, smy, smx, offy, 
     wp, nck, n_pad = packed
     kc = 4 * C if s2d_pad is not None else C
     n = 4 * N if d2s_pad is not None else N
-    lib = _lib_for_launch()
+    lib = _lib.load()
+    mode = _mode(prec)
     oy, ox = _i32(offy), _i32(offx)
     sd = s2d_pad is not None or d2s_pad is not None
     # split-K where the grid would fill few CUs and K is long (the 8x8 pseudo-FC layer); the library says how many
-    ks = lib.esr_dconv_fwd_splits_sd(B, MH, MW, n, kc, smy, smx, len(offy), oy, ox, int(sd))
+    ks = lib.esr_dconv_fwd_splits_sd(B, MH, MW, n, kc, smy, smx, len(offy), oy, ox, int(sd), mode)
     if ks < 1:
         raise RuntimeError('esr_dconv_fwd_splits failed with esr_status %d' % ks)
     part = torch.empty(ks * B * MH * MW * n_pad, device=src.device) if ks > 1 else None
@@ -140,7 +129,7 @@ def _gather(src, packed, bias, out, MH, MW, omy, oay, omx, oax, smy, smx, offy, 
                                     omy, oay, omx, oax, smy, smx, len(offy), oy, ox, ks,
                                     None if part is None else part.data_ptr(),
                                     C if s2d_pad is not None else 0, s2d_pad or 0,
-                                    N if d2s_pad is not None else 0, d2s_pad or 0, _stream(src)),
+                                    N if d2s_pad is not None else 0, d2s_pad or 0, mode, _stream(src)),
                'esr_dconv_fwd')
 
 
@@ -160,7 +149,7 @@ def _s2d_weights(w):
     return wt.permute(0, 2, 4, 1, 3, 5, 6).reshape(h * h, 4 * Ci, Co)
 
 
-def conv_forward(x, w, b, k, s, p):
+def conv_forward(x, w, b, k, s, p, prec=None):
     """y = conv2d(x, w, b, stride s, zero padding p) on NHWC x [B][H][W][Ci]; w [Co][Ci][k][k]."""
     _check_dev(x, w, b)
     B, H, W, Ci = x.shape
@@ -168,20 +157,20 @@ def conv_forward(x, w, b, k, s, p):
     Ho, Wo = out_size(H, k, s, p), out_size(W, k, s, p)
     y = torch.empty(B, Ho, Wo, Co, device=x.device, dtype=torch.float32)
     # y[yo] = sum over taps (a, b) of W'[a, b] . Z[yo + a, xo + b], Z = s2d(pad(x, p)); only where it is halo-tiled
-    if _s2d_form(k, s, Ci) and _lib_for_launch().esr_dconv_uses_halo(1, 1, (k // 2) ** 2, Wo, 1) == 1:
+    if _s2d_form(k, s, Ci) and _lib.load().esr_dconv_uses_halo(1, 1, (k // 2) ** 2, Wo, 1, _mode(prec)) == 1:
         wp = _packed(w, ('fwd_s2d',), lambda: _pack(_s2d_weights(w.detach()), Co))
         h = k // 2
         _gather(x, wp, None if b is None else b.detach().contiguous(), y, Ho, Wo, 1, 0, 1, 0, 1, 1,
-                [a for a in range(h) for _ in range(h)], [c for _ in range(h) for c in range(h)], s2d_pad=p)
+                [a for a in range(h) for _ in range(h)], [c for _ in range(h) for c in range(h)], s2d_pad=p, prec=prec)
         return y
     wp = _packed(w, ('fwd',), lambda: _pack(w.detach().permute(2, 3, 1, 0).reshape(k * k, Ci, Co), Co))
     taps = [(ky, kx) for ky in range(k) for kx in range(k)]
     _gather(x, wp, None if b is None else b.detach().contiguous(), y, Ho, Wo, 1, 0, 1, 0, s, s,
-            [ky - p for ky, _ in taps], [kx - p for _, kx in taps])
+            [ky - p for ky, _ in taps], [kx - p for _, kx in taps], prec=prec)
     return y
 
 
-def conv_dgrad(gy, w, k, s, p, H, W):
+def conv_dgrad(gy, w, k, s, p, H, W, prec=None):
     """gx = conv_transpose of gy (NHWC [B][Ho][Wo][Co]) back to the [B][H][W][Ci] input grid: one launch per phase
     class (cy, cx) of the stride, each gathering over the taps that land on that class."""
     _check_dev(gy, w)
@@ -193,7 +182,8 @@ def conv_dgrad(gy, w, k, s, p, H, W):
         gx = torch.empty(B, H, W, Ci, device=gy.device, dtype=torch.float32)
         wp = _packed(w, ('dgrad_s2d',), lambda: _pack(_s2d_weights(wd).transpose(1, 2).contiguous(), 4 * Ci))
         _gather(gy, wp, None, gx, (H - 1 + p) // 2 + 1, (W - 1 + p) // 2 + 1, 1, 0, 1, 0, 1, 1,
-                [-a for a in range(h) for _ in range(h)], [-c for _ in range(h) for c in range(h)], d2s_pad=p)
+                [-a for a in range(h) for _ in range(h)], [-c for _ in range(h) for c in range(h)], d2s_pad=p,
+                prec=prec)
         return gx
     classes = []
     full = True
@@ -213,11 +203,11 @@ def conv_dgrad(gy, w, k, s, p, H, W):
         wp = _packed(w, ('dgrad', s, p, cy, cx),
                      lambda taps=taps: _pack(torch.stack([wd[:, :, ky, kx] for ky, kx in taps]), Ci))  # [T][Co][Ci]
         _gather(gy, wp, None, gx, MH, MW, s, cy, s, cx, 1, 1,
-                [(cy + p - ky) // s for ky, _ in taps], [(cx + p - kx) // s for _, kx in taps])
+                [(cy + p - ky) // s for ky, _ in taps], [(cx + p - kx) // s for _, kx in taps], prec=prec)
     return gx
 
 
-def conv_wgrad(x, gy, k, s, p):
+def conv_wgrad(x, gy, k, s, p, prec=None):
     """gw [Co][Ci][k][k] = sum over pixels of x (gathered per tap) * gy; split-K over pixels + deterministic reduce."""
     _check_dev(x, gy)
     B, H, W, Ci = x.shape
@@ -227,15 +217,16 @@ def conv_wgrad(x, gy, k, s, p):
     n = T * cin_pad * cout_pad
     taps = [(ky, kx) for ky in range(k) for kx in range(k)]
     oy, ox = _i32([ky - p for ky, _ in taps]), _i32([kx - p for _, kx in taps])
-    lib = _lib_for_launch()
+    lib = _lib.load()
+    mode = _mode(prec)
     st = _stream(x)
-    splits = lib.esr_dconv_wgrad_splits(B, Ho, Wo, Ci, Co, s, s, T, oy, ox)  # split-K over pixels, library's choice
+    splits = lib.esr_dconv_wgrad_splits(B, Ho, Wo, Ci, Co, s, s, T, oy, ox, mode)  # split-K over pixels
     if splits < 1:
         raise RuntimeError('esr_dconv_wgrad_splits failed with esr_status %d' % splits)
     partial = torch.empty(splits * n, device=x.device, dtype=torch.float32)
     red = torch.empty(n, device=x.device, dtype=torch.float32)
     _lib.check(lib.esr_dconv_wgrad(x.data_ptr(), B, H, W, Ci, Ci, gy.data_ptr(), Ho, Wo, Co, Co, s, s, T, oy, ox,
-                                   splits, partial.data_ptr(), st), 'esr_dconv_wgrad')
+                                   splits, partial.data_ptr(), mode, st), 'esr_dconv_wgrad')
     _lib.check(lib.esr_wgrad_reduce(partial.data_ptr(), splits, n, 1.0, red.data_ptr(), st), 'esr_wgrad_reduce')
     return red.view(k, k, cin_pad, cout_pad)[:, :, :Ci, :Co].permute(3, 2, 0, 1).contiguous()
 

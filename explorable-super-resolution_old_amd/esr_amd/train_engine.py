@@ -33,9 +33,6 @@ USE_GRAPHS = os.environ.get('ESR_TRAIN_GRAPHS', '1') != '0'
 # Weight gradients of an x3 forward (split-f16 activations) on the x3 MFMA kernel (esr_conv3x3_wgrad flag 4); 0 keeps
 # the exact-fp32 weight-gradient kernel reading the same split activations.
 WGRAD_X3 = os.environ.get('ESR_WGRAD_X3', '1') != '0'
-# the x3 weight gradient of a split-f16 output gradient on the LDS-DMA kernel (esr_wgrad3_set_dma); '0' = the
-# register-staged one (A/B: profiles/r3_wgrad_dma_ab.txt)
-WGRAD3_DMA = os.environ.get('ESR_WGRAD3_DMA', '1') != '0'
 # Data gradients inside the residual blocks on the x3 conv (split-f16 gradients scaled per RRDB, include/esr_amd.h
 # "x3 backward") when the forward ran in x3 and only parameter gradients are wanted (training); 0 keeps them fp32.
 DGRAD_X3 = os.environ.get('ESR_DGRAD_X3', '1') != '0'
@@ -369,7 +366,6 @@ def _bwd_packed(net, latent):
 class _Runner:
     def __init__(self, ws, bp, stream, need_params=True, need_input=False, split=False):
         self.lib = _lib.load()
-        self.lib.esr_wgrad3_set_dma(1 if WGRAD3_DMA else 0)
         self.ws = ws
         self.bp = bp
         self.B = ws.B

@@ -2,8 +2,10 @@
  * esr_amd.h — C ABI of the MI355X-native RRDB-23 + CEM ×4 super-resolution hot path (libesr_amd.so).
  *
  * Every entry point is `extern "C"`, takes plain pointers / sizes, enqueues on the given HIP stream and returns 0 or a
- * negative esr_status.  Buffers are caller-allocated device memory; the library holds no persistent allocations and
- * is re-entrant across streams.
+ * negative esr_status.  Buffers are caller-allocated device memory; the library holds no persistent allocations and no
+ * mutable selection state — which kernel a launch runs is a function of its arguments only — so every entry point is
+ * stateless and re-entrant across streams and threads.  The kernel-selection switches used for A/B
+ * measurements live only in the separate ablation build (csrc/esr_ablation.h, `make exp`).
  *
  * Reference = YuvalBahat/Explorable-Super-Resolution_old, paths relative to codes/.  Each entry cites the reference
  * interface it replaces.  The Python host layer (explorable-super-resolution_old_amd/esr_amd) binds these through
@@ -69,10 +71,6 @@ typedef struct esr_conv_out {
  * in: padded NHWC [B][H+2][W+2][in_cp], reads channels [0, cin); cin % 8 == 0; cout <= 64. */
 int esr_conv3x3_fwd(const float *in, int32_t B, int32_t H, int32_t W, int32_t in_cp, int32_t cin,
                     const float *w_packed, const float *bias, int32_t cout, const esr_conv_out *o, esr_stream_t stream);
-/* Tile height of the exact-fp32 convs (esr_conv3x3_fwd, esr_upconv2x_phase_fwd), process-wide: 0 (default) =
- * automatic (4 output rows per workgroup for cout <= 32, and for cout > 32 when 8-row tiles would fill fewer than 8
- * rounds of the CUs; else 8), or force 4 / 8.  Results are identical either way.  Returns the previous setting, or ESR_EINVAL. */
-int esr_conv_set_tile(int32_t rows);
 
 /* One polyphase phase (py, px) in {0,1}² of the nearest-×2 upsample + 3×3 conv (upconv_blcok, block.py:294-301;
  * used twice by RRDBNet, networks.py:91): out[2y+py, 2x+px] = Σ_{a,b∈{0,1}} Wp[a][b] · in[y+py+a-1, x+px+b-1], with
@@ -124,11 +122,6 @@ int esr_cem_inv(const float *r, float *q, int32_t B, int32_t H, int32_t W, const
  * out: NCHW [B][3][sf*H-2M][sf*W-2M]; w_up = sf²·ds_kernel. */
 int esr_cem_up_add(const float *q, const float *gen, float *out, int32_t B, int32_t H, int32_t W, int32_t sf,
                    int32_t ph, const float *w_up, int32_t kd, int32_t M, esr_stream_t stream);
-/* A/B of the CEM stencil kernels (process-wide): 0 (default) = LDS-tiled inverse filter, register-window up-add and
- * down stencils (sf 4, kd 17; LDS-tiled otherwise); 1 = the direct (untiled) inverse / up-add kernels (bitwise equal)
- * and the LDS-tiled down kernel (equal to rounding: FMA contraction differs).  Returns the previous setting, or
- * ESR_EINVAL. */
-int esr_cem_set_direct(int32_t direct);
 
 /* ---- split-precision ("x3") path --------------------------------------------------------------------------------
  * Split activation layout: padded NHWC as above, 4 bytes per channel, channels in groups of 8; group g of a pixel is
@@ -137,46 +130,19 @@ int esr_cem_set_direct(int32_t direct);
  * (64 B per (tap, n)), scaled by `w_scale` (a power of two the epilogue divides out exactly).
  * Products are a_hi·b_hi + a_hi·b_lo + a_lo·b_hi on v_mfma_f32_32x32x16_f16 with fp32 accumulation.
  * Outputs are split unless o->out_planar (fp32 NCHW).  r1/r2 residual inputs are split.  *overflow is OR-ed with 1
- * if any split output is not representable (|v| >= 65504), in which case the caller reruns the exact-fp32 path. */
+ * if any split output is not representable (|v| >= 65504), in which case the caller reruns the exact-fp32 path.
+ * Kernel choice (a function of the shape): the column-tile kernel (esr_conv_x3c.hip; 12-column tiles at three
+ * workgroups per CU for cout <= 32, an N = 64 conv on a grid that cannot give every CU two workgroups as two N = 32
+ * launches over the halves of its weights) or, for small N = 32 grids, the classic 8-row kernel at three workgroups per
+ * CU; a 3×3 conv with cout <= 3, cin <= 80 and a planar output without residuals (HR_conv1) on the narrow-N kernel (the
+ * 9 taps × 3 outputs in the MFMA M dimension).  All are bitwise identical except the narrow-N kernel (tap sums in
+ * another order).  Blocks map to tiles in XCD-grouped order. */
 int esr_conv3x3_fwd_x3(const void *in, int32_t B, int32_t H, int32_t W, int32_t in_cp, int32_t cin,
                        const void *w_packed, const float *bias, float w_scale, int32_t cout, const esr_conv_out *o,
                        int32_t *overflow, esr_stream_t stream);
 int esr_upconv2x_phase_fwd_x3(const void *in, int32_t B, int32_t H, int32_t W, int32_t in_cp, int32_t cin,
                               const void *w_packed, const float *bias, float w_scale, int32_t cout, int32_t py,
                               int32_t px, const esr_conv_out *o, int32_t *overflow, esr_stream_t stream);
-/* Kernel selection for esr_conv3x3_fwd_x3 (process-wide; for A/B tests and benchmarks).  All variants below give
- * bitwise-identical results.
- * 0 / 1 (default) = automatic: the column-tile kernel (32x16 tiles, esr_conv_x3c.hip) for the upconv phases, cout > 32 and, for
- *   cout <= 32, where 16-row classic tiles fill their rounds; otherwise the classic kernel with 8-row tiles at three
- *   workgroups per CU; 24 = the round-1 automatic choice (classic kernel only: 8-row at three per CU or 16-row at two,
- *   by a wave-quantisation cost model; 25 / 26 force one); 50 = column-tile kernel; 63 = same as 1; 60 = column-tile kernel with the
- *   weights read into registers from global memory instead of LDS;
- * 22 = classic with two LDS stages and one workgroup per CU; 23 = cout > 32 with 8-row tiles at two workgroups per
- *   CU; 21 = the same with fragment prefetch distance 1 (default 2); 20 = two-stage classic with compiler-scheduled
- *   fragment reads; 27 / 28 = classic with the register epilogue (16- / 8-row);
- * 2 = ring kernel (two tiles per workgroup, 3-deep LDS-DMA input ring); 15 = ring with staggered DMA issue; 18 = ring
- *   with compiler-scheduled reads; 16 / 17 = persistent ring (one workgroup per CU streaming tile pairs).
- * Diagnostic ablations (garbage outputs) exist only in the experiment build (make exp, -DESR_X3_EXPERIMENTS); the
- * production library returns ESR_EINVAL for them.  Returns the previous setting, or ESR_EINVAL. */
-int esr_x3_set_kernel(int32_t variant);
-
-/* Block -> tile order of the classic x3 conv kernel and the exact-fp32 conv kernel: 1 (default) = XCD-grouped (workgroups run round-robin over the
- * 8 XCDs; each XCD gets one contiguous band of tiles so neighbouring tiles' halos are shared in its L2), 0 = row-major
- * over blockIdx.  Results are bitwise identical.  Returns the previous setting, or ESR_EINVAL. */
-int esr_x3_set_tile_map(int32_t mode);
-
-/* Narrow-N path of esr_conv3x3_fwd_x3 (process-wide): 1 (default) = a 3×3 conv with cout <= 3, cin <= 80 and a planar
- * fp32 output without residuals (HR_conv1 -> CEM, architecture.py:140-141) puts the 9 taps × 3 outputs into the MFMA M
- * dimension (27 of 32 rows) and sums the taps' shifted partial products from LDS, instead of an N = 32 tile of which 29
- * columns are padding; 0 = the N = 32 tiles.  Results agree to the x3 rounding (not bitwise: the tap sum order
- * differs).  Returns the previous setting, or ESR_EINVAL. */
-int esr_x3_set_narrow(int32_t on);
-/* N split of esr_conv3x3_fwd_x3 (process-wide): 1 (default) = a 3×3 conv with 32 < cout <= 64 whose 16-column grid
- * has fewer than two tiles per CU (config 3: 96² × B=16) runs as two N = 32 launches over the halves of its packed
- * weights and output channels (config 3: 144.6 -> 142.6 ms per step, config 5: 84.5 -> 83.0 ms, profiles/r3_ab_nsplit.txt);
- * 0 = one N = 64 launch.  Bitwise identical (the same products per output channel in
- * the same order).  Returns the previous setting, or ESR_EINVAL. */
-int esr_x3_set_nsplit(int32_t on);
 
 /* ---- training / Z-optimisation backward (esr_train.hip) ------------------------------------------------------------
  * The data gradient of every conv is esr_conv3x3_fwd run with rot180, in/out-swapped packed weights (host-side
@@ -224,14 +190,6 @@ int esr_wgrad_reduce2(const float *partial, int32_t splits, int64_t n, int64_t n
 /* out[i] = scale / S(amax) · Σ_s partial[s·n + i]: the weight gradient of a conv whose output gradient was scaled. */
 int esr_wgrad_reduce_gs(const float *partial, int32_t splits, int64_t n, float scale, const uint32_t *amax, float *out,
                         esr_stream_t stream);
-/* Kernel selection for esr_conv3x3_wgrad (process-wide, for A/B tests and benchmarks): 1 (default) = 12-wave
- * kernel (three waves per SIMD, next tile prefetched into registers, XCD-grouped chunks), 0 = the 4-wave kernel.
- * Both are deterministic; they sum the pixels in different orders.  Returns the previous setting, or ESR_EINVAL. */
-int esr_wgrad_set_kernel(int32_t variant);
-/* x3 weight gradient with a split-f16 output gradient (flags bit 8): 1 (default) = both tiles LDS-DMA'd into two LDS
- * stages (no register staging or per-tile rescale; 4-row pixel tiles for Cout > 32), 0 = the register-staged x3
- * kernel.  Both deterministic, different summation orders.  Returns the previous setting, or ESR_EINVAL. */
-int esr_wgrad3_set_dma(int32_t on);
 /* LeakyReLU(0.2) backward from the saved output y: d *= (y > 0 ? 1 : 0.2) on a C-channel slice. */
 int esr_lrelu_bwd(float *d, int32_t d_cp, int32_t d_coff, const float *y, int32_t y_cp, int32_t y_coff, int32_t C,
                   int32_t B, int32_t H, int32_t W, esr_stream_t stream);
@@ -252,14 +210,12 @@ int esr_nchw_to_padded(const float *src, int32_t C, int32_t B, int32_t H, int32_
  * (2-D, same s/c per dimension; x is Ly×Lx, g = F's output shape Oy×Ox, `planes` = B·C images):
  *   out[i][j] (+)= alpha · F^T(g)[os·i + oc][os·j + oc]
  * Used with (s, c, os, oc) = (1, 0, sf, ph) for Upscale_OP (adjoint sampled on the stuffed phase), (1, 0, 1, 0) for
- * Conv_LR_with_Inv_hTh_OP and (sf, ph, 1, 0) for DownscaleOP (CEMnet.py:149-162). */
+ * Conv_LR_with_Inv_hTh_OP and (sf, ph, 1, 0) for DownscaleOP (CEMnet.py:149-162).
+ * flags: bit 0 = accumulate into out (+=); bit 1 = the generic per-tap range search everywhere (default: outputs whose
+ * taps see no replicate clamp visit only the contributing taps, in the generic loop's order — bitwise equal). */
 int esr_cem_adjoint(const float *g, int32_t planes, int32_t Oy, int32_t Ox, const float *w, int32_t K, int32_t s,
-                    int32_t c, int32_t Ly, int32_t Lx, int32_t os, int32_t oc, float alpha, int32_t accumulate,
+                    int32_t c, int32_t Ly, int32_t Lx, int32_t os, int32_t oc, float alpha, int32_t flags,
                     float *out, esr_stream_t stream);
-/* esr_cem_adjoint's interior fast path (outputs whose taps see no replicate clamp visit only the contributing taps,
- * in the generic loop's order: bitwise equal) is the default; 1 = the generic per-tap range search everywhere (A/B,
- * tests).  Returns the previous setting. */
-int esr_cem_adjoint_set_generic(int32_t on);
 
 /* Input gradient of the generator (Z optimisation, Z_optimization.py:574-630): out [B][C][Hp-2M][Wp-2M] (NCHW) =
  *   RepPad_M^T( d_hr  +  d_pl  +  Bilinear↓sf^T(d_lr) )
@@ -273,8 +229,20 @@ int esr_input_adjoint(const float *d_hr, int32_t hr_cp, int32_t hr_coff, const f
 
 /* ---- discriminator convolutions (esr_dconv.hip) -----------------------------------------------------------------
  * Discriminator_VGG_128_ (architecture.py:222-284): the conv_block convolutions (block.py:129-156; k = 3/4/8/1,
- * stride 1/2) of the D step and of the WGAN-GP double backward (SRRaGAN_model.py:360-433, loss.py:244-263), exact fp32
- * (v_mfma_f32_32x32x2_f32), on channels-last (NHWC, no halo) tensors.
+ * stride 1/2) of the D step and of the WGAN-GP double backward (SRRaGAN_model.py:360-433, loss.py:244-263), on
+ * channels-last (NHWC, no halo) tensors.
+ *
+ * `prec` (every esr_dconv_* entry point, per call): 0 = exact fp32 MFMA (v_mfma_f32_32x32x2_f32); 1 = x3: both operands
+ * split into f16 hi/lo at staging after a power-of-two scaling per K step (one tap × 32 channels, or per staged
+ * 32-channel window in the halo kernels) chosen from the workgroup's max |a| and max |b|, products hi·hi + hi·lo +
+ * lo·hi on f16 MFMA, the fp32 accumulators rescaled exactly when the step's scale changes (esr_dconv_wgrad likewise:
+ * per 64-pixel K step); 128 output channels per workgroup where n_pad % 128 == 0 and the grid keeps >= 512 workgroups;
+ * 2 = x3 with 64-channel N tiles only (identical results); 3 = x6: three f16 pieces hi, lo, lo2 per operand value and
+ * the six products hi·hi, hi·lo, lo·hi, lo·lo, hi·lo2, lo2·hi — every dropped term below 2^-33 of the step's scale,
+ * i.e. an fp32 FMA chain's accuracy.
+ * Kernels (a function of the geometry): the halo-tile implicit GEMMs (each source pixel of a 32-channel chunk staged in
+ * LDS once for all taps) for stride-1 launches with one tap or >= 9 taps (and the space-to-depth forms) whose width the
+ * tiles cover with <= 30 % waste and whose halo fits in LDS; the per-tap gather kernels otherwise.
  *
  * esr_dconv_fwd: gather-GEMM
  *   out[b, omy*Y+oay, omx*X+oax, n] = bias[n] + sum_t sum_{c<kc} src[b, smy*Y+offy[t], smx*X+offx[t], c] * W[t][c][n]
@@ -290,7 +258,7 @@ int esr_dconv_fwd(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t s
                   const float *w_packed, int32_t nck, int32_t n_pad, const float *bias, float *out, int32_t Ho,
                   int32_t Wo, int32_t out_pitch, int32_t n_out, int32_t MH, int32_t MW, int32_t omy, int32_t oay,
                   int32_t omx, int32_t oax, int32_t smy, int32_t smx, int32_t T, const int32_t *offy,
-                  const int32_t *offx, esr_stream_t stream);
+                  const int32_t *offx, int32_t prec, esr_stream_t stream);
 /* esr_dconv_fwd with split-K over ksplit workgroup slices of the K steps (x3) or of the 32-channel chunks (fp32
  * halo kernel) — for the small-M,
  * long-K launches — the 8×8 pseudo-FC layer — that would fill few CUs): partial = caller buffer of
@@ -300,12 +268,12 @@ int esr_dconv_fwd_sk(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_
                      const float *w_packed, int32_t nck, int32_t n_pad, const float *bias, float *out, int32_t Ho,
                      int32_t Wo, int32_t out_pitch, int32_t n, int32_t MH, int32_t MW, int32_t omy, int32_t oay,
                      int32_t omx, int32_t oax, int32_t smy, int32_t smx, int32_t T, const int32_t *offy,
-                     const int32_t *offx, int32_t ksplit, float *partial, esr_stream_t stream);
-/* The ksplit esr_dconv_fwd_sk should get for this launch geometry under the current precision setting (1 = no
- * split); the caller allocates `partial` accordingly.  Exact fp32: the halo-tile kernel splits the 32-channel chunks
- * where its grid has < 512 workgroups (the 8×8 pseudo-FC layer); x3: ~512 workgroups, >= 8 K steps per slice. */
+                     const int32_t *offx, int32_t ksplit, float *partial, int32_t prec, esr_stream_t stream);
+/* The ksplit esr_dconv_fwd_sk should get for this launch geometry at precision `prec` (1 = no split); the caller
+ * allocates `partial` accordingly.  Exact fp32: the halo-tile kernel splits the 32-channel chunks where its grid has
+ * < 512 workgroups (the 8×8 pseudo-FC layer); x3: ~512 workgroups, >= 8 K steps per slice. */
 int esr_dconv_fwd_splits(int32_t B, int32_t MH, int32_t MW, int32_t n_out, int32_t kc, int32_t smy, int32_t smx,
-                         int32_t T, const int32_t *offy, const int32_t *offx);
+                         int32_t T, const int32_t *offy, const int32_t *offx, int32_t prec);
 /* esr_dconv_fwd_sk over a space-to-depth source and/or into a depth-to-space output: a k×k stride-2 conv (k even) as
  * a (k/2)×(k/2)-tap stride-1 one with 4× the channels, the form the halo-tile kernel stages once per source pixel.
  *   Virtual channel order: v(py, px, c) = (c / G)·4G + (2·py + px)·G + c % G with G = 32 where the real channel
@@ -325,53 +293,26 @@ int esr_dconv_fwd_sd(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_
                      int32_t Wo, int32_t out_pitch, int32_t n, int32_t MH, int32_t MW, int32_t omy, int32_t oay,
                      int32_t omx, int32_t oax, int32_t smy, int32_t smx, int32_t T, const int32_t *offy,
                      const int32_t *offx, int32_t ksplit, float *partial, int32_t s2d_c, int32_t s2d_pad,
-                     int32_t d2s_c, int32_t d2s_pad, esr_stream_t stream);
+                     int32_t d2s_c, int32_t d2s_pad, int32_t prec, esr_stream_t stream);
 /* 1 if an esr_dconv_fwd(_sd) launch of this geometry runs on the halo-tile kernel (sd != 0: an esr_dconv_fwd_sd
  * launch), 0 if on the per-tap gather kernel.  The host takes the space-to-depth forward only where it is halo-tiled
  * (on the gather kernel it is no faster than the direct stride-2 gather: profiles/r3_dconv_s2d_ab.txt). */
-int esr_dconv_uses_halo(int32_t smy, int32_t smx, int32_t T, int32_t MW, int32_t sd);
+int esr_dconv_uses_halo(int32_t smy, int32_t smx, int32_t T, int32_t MW, int32_t sd, int32_t prec);
 /* esr_dconv_fwd_splits for an esr_dconv_fwd_sd launch (sd != 0: space-to-depth source or depth-to-space output). */
 int esr_dconv_fwd_splits_sd(int32_t B, int32_t MH, int32_t MW, int32_t n_out, int32_t kc, int32_t smy, int32_t smx,
-                            int32_t T, const int32_t *offy, const int32_t *offx, int32_t sd);
-/* esr_dconv_fwd kernels: 1 (default) = the halo-tile implicit GEMMs (each source pixel of a 32-channel chunk staged
- * in LDS once for all taps; exact fp32, or split x3 / x6 with a per-chunk source scale and a per-step weight scale)
- * for stride-1 launches with one tap or >= 9 taps where the halo fits in LDS, the gather kernels otherwise; 0 = the
- * gather kernels always (A/B).  Returns the previous setting. */
-int esr_dconv_set_halo(int32_t on);
-/* x3 halo kernel with 64-wide N tiles at three workgroups per CU where its LDS allows (the space-to-depth forms):
- * 1 (default) / 0 (two per CU, A/B).  Bitwise identical.  Returns the previous setting, or ESR_EINVAL. */
-int esr_dconv_set_occ3(int32_t on);
-/* x3 halo kernel with 16-column tiles (2 rows × 16 columns per MFMA M-tile) where 32-column tiles would waste > 30 %
- * of the width and 16-column ones do not (the 38-wide layers at config 3): 1 (default) / 0 (the gather kernel there,
- * A/B).  Returns the previous setting, or ESR_EINVAL. */
-int esr_dconv_set_cw16(int32_t on);
-/* Precision of esr_dconv_fwd (process-wide): 0 (the library default) = exact fp32 MFMA; 1 = x3: both operands split
- * into f16 hi/lo at staging after a power-of-two scaling per K step (one tap × 32 channels) chosen from the
- * workgroup's max |a| and max |b|, products hi·hi + hi·lo + lo·hi on f16 MFMA, the fp32 accumulators rescaled exactly
- * when the step's scale changes (esr_dconv_wgrad likewise: per 64-pixel K step, 128-channel blocks where the padded
- * widths allow); 128 output channels per workgroup where n_pad % 128 == 0, else 64 (2 = x3 with
- * 64-channel tiles only, for A/B; identical results; 3 = x6: three f16 pieces hi, lo, lo2 per operand value and the
- * six products hi·hi, hi·lo, lo·hi, lo·lo, hi·lo2, lo2·hi — every dropped term below 2^-33 of the step's scale, i.e. an
- * fp32 FMA chain's accuracy).  Returns the previous setting, or ESR_EINVAL. */
-int esr_dconv_set_x3(int32_t on);
+                            int32_t T, const int32_t *offy, const int32_t *offx, int32_t sd, int32_t prec);
 /* esr_dconv_wgrad: weight gradient of the forward conv above (src = its input, dy = dL/dout on the MH x MW grid):
  *   partial[s][t][ci][co] = sum over the pixels of split s of src[b, smy*Y+offy[t], smx*X+offx[t], ci] * dy[b, Y, X, co]
  * partial: [splits][T][cin_pad][cout_pad], cin_pad = 64*ceil(cin/64), cout_pad = 64*ceil(cout/64); reduce the splits
  * with esr_wgrad_reduce (fixed order, deterministic). */
-/* The `splits` esr_dconv_wgrad should get for this geometry under the current precision / kernel settings (the
- * caller sizes `partial` with it).  Returns ESR_EINVAL on bad arguments. */
+/* The `splits` esr_dconv_wgrad should get for this geometry at precision `prec` (the caller sizes `partial` with it).
+ * Returns ESR_EINVAL on bad arguments. */
 int esr_dconv_wgrad_splits(int32_t B, int32_t MH, int32_t MW, int32_t cin, int32_t cout, int32_t smy, int32_t smx,
-                           int32_t T, const int32_t *offy, const int32_t *offx);
-/* Split-precision (x3 / x6) weight gradient kernel: 1 = the tap-row kernel (a workgroup owns one kernel row of taps,
- * a K step is a 64-pixel output-row segment whose output gradient and source row are staged once for all the row's
- * taps) where the taps are (ky, kx) ky-major with kx consecutive and the kernel width is 1, 3, 4 (stride 1 or 2) or
- * 8; 0 (default: the tap-row kernel measured 1.7× slower at config 3) = the per-tap kernel.  Returns the previous
- * setting. */
-int esr_dconv_set_rows(int32_t on);
+                           int32_t T, const int32_t *offy, const int32_t *offx, int32_t prec);
 int esr_dconv_wgrad(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t src_pitch, int32_t cin,
                     const float *dy, int32_t MH, int32_t MW, int32_t dy_pitch, int32_t cout, int32_t smy, int32_t smx,
                     int32_t T, const int32_t *offy, const int32_t *offx, int32_t splits, float *partial,
-                    esr_stream_t stream);
+                    int32_t prec, esr_stream_t stream);
 
 /* ---- op lists (host-side executor, esr_plan.hip) -----------------------------------------------------------------
  * A generator (+CEM) forward is a fixed sequence of the launches above (≈360 for RRDB-23).  The host layer records it

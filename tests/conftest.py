@@ -64,6 +64,30 @@ def gpu_device():
     return torch.device('cuda:0')
 
 
+@pytest.fixture(scope='session')
+def ablation_lib(gpu_device):
+    """The ablation library (exp_lib/libesr_exp.so, csrc/esr_ablation.h): the product ABI built from the same sources
+    plus the process-wide kernel-selection setters and the non-default kernel variants.  Variant-equality tests run
+    the default on the product library and the variants here; the product library has no selection state."""
+    from esr_amd import _lib
+    try:
+        return _lib.load_ablation()
+    except _lib.ESRLibraryError as e:
+        pytest.skip('ablation library not built: %s' % e)
+
+
+@pytest.fixture
+def via_ablation(ablation_lib):
+    """Route the host layer's launches (esr_amd modules call _lib.load()) to the ablation library for one test."""
+    from esr_amd import _lib
+    prev = _lib._lib
+    _lib._lib = ablation_lib
+    try:
+        yield ablation_lib
+    finally:
+        _lib._lib = prev
+
+
 def l2_rel(a, b):
     a = np.asarray(a, dtype=np.float64)
     b = np.asarray(b, dtype=np.float64)

@@ -37,25 +37,29 @@ pytestmark = pytest.mark.gpu
     (128, 64, 8, 1, 3, 38, 38),    # x3: 16-column halo tiles (MW 37 forward, 38 data gradient: 64 taps)
     (256, 100, 8, 1, 0, 38, 38),   # the config-3 pseudo-FC geometry: split-K over the channel chunks
 ])
-@pytest.mark.parametrize('precision', ['x3', 'x6', 'f32', 'x3_gather', 'x6_gather', 'f32_gather', 'x3_direct',
-                                       'f32_direct', 'x3_gather_direct'])
-def test_dconv_ops_vs_float64(gpu_device, ci, co, k, s, p, H, W, precision):
-    """x3 / x6 / f32 with the halo-tile forward and tap-row weight-gradient kernels where they apply (default),
-    *_gather = the per-tap kernels everywhere; the stride-2 convs in their space-to-depth form (default) or, *_direct,
-    as the direct stride-2 gather with one data-gradient launch per phase class."""
+@pytest.mark.parametrize('precision', ['x3', 'x6', 'f32', 'x3_gather', 'x6_gather', 'f32_gather', 'x3_rows',
+                                       'x6_rows', 'x3_direct', 'f32_direct', 'x3_gather_direct'])
+def test_dconv_ops_vs_float64(gpu_device, ci, co, k, s, p, H, W, precision, request):
+    """x3 / x6 / f32 on the product library (the halo-tile forward where it applies, per-tap weight gradients);
+    through the ablation library: *_gather = the per-tap kernels everywhere, *_rows = the tap-row weight-gradient
+    kernel; the stride-2 convs in their space-to-depth form (default) or, *_direct, as the direct stride-2 gather with
+    one data-gradient launch per phase class."""
     prev = dconv.set_precision(precision.split('_')[0])
-    lib = _lib.load()
-    prev_halo = lib.esr_dconv_set_halo(0 if '_gather' in precision else 1)
-    prev_rows = lib.esr_dconv_set_rows(0 if '_gather' in precision else 1)
     prev_s2d, dconv.S2D = dconv.S2D, not precision.endswith('_direct')
+    knobs = []
+    if '_gather' in precision or '_rows' in precision:
+        lib = request.getfixturevalue('via_ablation')
+        knobs = [(lib.esr_dconv_set_halo, 0 if '_gather' in precision else 1),
+                 (lib.esr_dconv_set_rows, 1 if '_rows' in precision else 0)]
+        knobs = [(fn, fn(v)) for fn, v in knobs]
     try:
         _dconv_ops(gpu_device, ci, co, k, s, p, H, W, scale=1.0 if precision.startswith('f32') else 1e-9,
                    tol=1e-5)
     finally:
         dconv.set_precision(prev)
-        lib.esr_dconv_set_halo(prev_halo)
-        lib.esr_dconv_set_rows(prev_rows)
         dconv.S2D = prev_s2d
+        for fn, v in knobs:
+            fn(v)
 
 
 @pytest.mark.parametrize('ci,co,k,s,p,H,W,B', [

@@ -72,8 +72,9 @@ def test_conv3x3_layer(gpu_device, cin, cout, H, W):
 
 
 @pytest.mark.parametrize('cin,cout,H,W', [(72, 32, 13, 37), (136, 64, 30, 70)])
-def test_conv3x3_xcd_tile_map_bitwise(gpu_device, cin, cout, H, W):
-    """Exact-fp32 conv: XCD-grouped tile order (default) against row-major blockIdx order, bit for bit."""
+def test_conv3x3_xcd_tile_map_bitwise(gpu_device, ablation_lib, cin, cout, H, W):
+    """Exact-fp32 conv: XCD-grouped tile order (the product library) against row-major blockIdx order (the ablation
+    library), bit for bit."""
     lib = _lib.load()
     B = 3
     cp = cin + 8
@@ -84,16 +85,17 @@ def test_conv3x3_xcd_tile_map_bitwise(gpu_device, cin, cout, H, W):
     wp = engine.pack_conv_weight(w.to(gpu_device), list(range(cin)), 32 if cout <= 32 else 64)
     outs = []
     try:
-        for mode in (1, 0):
-            lib.esr_x3_set_tile_map(mode)
+        for L in (lib, ablation_lib):
+            if L is ablation_lib:
+                L.esr_x3_set_tile_map(0)
             out = torch.zeros(B, H + 2, W + 2, cout, device=gpu_device)
             o = engine._conv_out(out, cout, 0, H, W, True)
-            _lib.check(lib.esr_conv3x3_fwd(x.data_ptr(), B, H, W, cp, cin, wp.data_ptr(), bd.data_ptr(), cout,
-                                           ctypes.byref(o), _stream()), 'conv')
+            _lib.check(L.esr_conv3x3_fwd(x.data_ptr(), B, H, W, cp, cin, wp.data_ptr(), bd.data_ptr(), cout,
+                                         ctypes.byref(o), _stream()), 'conv')
             torch.cuda.synchronize()
             outs.append(out)
     finally:
-        lib.esr_x3_set_tile_map(1)
+        ablation_lib.esr_x3_set_tile_map(1)
     assert torch.equal(outs[0], outs[1])
     ref = F.leaky_relu(F.conv2d(_nchw(x, 0, cin), w.double(), bd.cpu().double(), padding=1), 0.2)
     assert normwise_rel(_nchw(outs[0], 0, cout), ref) < 1e-5
@@ -370,7 +372,7 @@ def test_conv3x3_layer_x3(gpu_device, cin, cout, H, W):
 
 @pytest.mark.parametrize('cin,cout,B,H,W', [(64, 32, 3, 40, 148), (136, 32, 5, 17, 45), (104, 24, 2, 33, 70),
                                             (16, 32, 1, 1, 1), (160, 32, 4, 96, 33)])
-def test_x3_ring_kernel_bitwise_equals_classic(gpu_device, cin, cout, B, H, W):
+def test_x3_ring_kernel_bitwise_equals_classic(gpu_device, ablation_lib, cin, cout, B, H, W):
     """The N<=32 ring kernels (two tiles per workgroup, 3-deep LDS-DMA ring, counted vmcnt; and the persistent variant
     that streams several tile pairs per workgroup with a per-wave epilogue) run the classic kernel's MFMA sequence per
     accumulator: outputs, residual epilogue and out2 must agree bit for bit, including odd tile counts (the second tile
@@ -389,18 +391,21 @@ def test_x3_ring_kernel_bitwise_equals_classic(gpu_device, cin, cout, B, H, W):
         # fragment reads, two-stage classic with prefetch 1 / 2, the round-1 automatic choice, the column-tile kernel
         # (16-column tiles, LDS / register weights; 12-column tiles at three workgroups per CU, the default where column
         # tiles pay) (none may change a bit)
+        # (the product library's automatic choice first, then the ablation library's variants)
         for variant in (0, 2, 17, 18, 20, 21, 22, 25, 26, 27, 28, 24, 50, 60, 61, 62, 64):
-            lib.esr_x3_set_kernel(variant)
+            L = lib if variant == 0 else ablation_lib
+            if L is ablation_lib:
+                L.esr_x3_set_kernel(variant)
             out = torch.zeros(B, H + 2, W + 2, 40, device=gpu_device)
             out2 = torch.zeros(B, H + 2, W + 2, 32, device=gpu_device)
             o = engine._conv_out(out, 40, 8, H, W, True, r1=rs, r1_cp=40, r1_coff=0, s1=0.2, out2=out2, out2_cp=32,
                                  out2_coff=0)
-            _lib.check(lib.esr_conv3x3_fwd_x3(xs.data_ptr(), B, H, W, cp, cin, wx.data_ptr(), b.data_ptr(), scale,
-                                              cout, ctypes.byref(o), None, _stream()), 'conv_x3')
+            _lib.check(L.esr_conv3x3_fwd_x3(xs.data_ptr(), B, H, W, cp, cin, wx.data_ptr(), b.data_ptr(), scale,
+                                            cout, ctypes.byref(o), None, _stream()), 'conv_x3')
             torch.cuda.synchronize()
             outs.append((out, out2))
     finally:
-        lib.esr_x3_set_kernel(1)
+        ablation_lib.esr_x3_set_kernel(1)
     for k in range(1, len(outs)):
         assert torch.equal(outs[0][0], outs[k][0]) and torch.equal(outs[0][1], outs[k][1]), k
     ref = F.leaky_relu(F.conv2d(_nchw(engine.from_split(xs), 0, cin), w.double(), b.cpu().double(), padding=1), 0.2)
@@ -409,7 +414,7 @@ def test_x3_ring_kernel_bitwise_equals_classic(gpu_device, cin, cout, B, H, W):
 
 
 @pytest.mark.parametrize('cin,B,H,W', [(192, 3, 21, 70), (72, 1, 5, 9)])
-def test_x3_n64_explicit_reads_bitwise(gpu_device, cin, B, H, W):
+def test_x3_n64_explicit_reads_bitwise(gpu_device, ablation_lib, cin, B, H, W):
     """The N = 64 classic kernel with explicit counted-wait fragment reads (default) against the same kernel with the
     compiler-scheduled reads (esr_x3_set_kernel 20): same MFMA order per accumulator, so bit for bit."""
     lib = _lib.load()
@@ -424,22 +429,24 @@ def test_x3_n64_explicit_reads_bitwise(gpu_device, cin, B, H, W):
         # default (column tiles), compiler-scheduled reads, 8-row tiles at two workgroups per CU, the round-1 default,
         # column tiles with register weights
         for variant in (1, 20, 23, 24, 60):
-            lib.esr_x3_set_kernel(variant)
+            L = lib if variant == 1 else ablation_lib
+            if L is ablation_lib:
+                L.esr_x3_set_kernel(variant)
             out = torch.zeros(B, H + 2, W + 2, 64, device=gpu_device)
             o = engine._conv_out(out, 64, 0, H, W, True)
-            _lib.check(lib.esr_conv3x3_fwd_x3(xs.data_ptr(), B, H, W, cp, cin, wx.data_ptr(), b.data_ptr(), scale,
-                                              64, ctypes.byref(o), None, _stream()), 'conv_x3')
+            _lib.check(L.esr_conv3x3_fwd_x3(xs.data_ptr(), B, H, W, cp, cin, wx.data_ptr(), b.data_ptr(), scale,
+                                            64, ctypes.byref(o), None, _stream()), 'conv_x3')
             torch.cuda.synchronize()
             outs.append(out)
     finally:
-        lib.esr_x3_set_kernel(1)
+        ablation_lib.esr_x3_set_kernel(1)
     for k in range(1, len(outs)):
         assert torch.equal(outs[0], outs[k]), k
     assert outs[0].abs().sum() > 0
 
 
 @pytest.mark.parametrize('cout,cin,B,H,W', [(32, 72, 3, 21, 70), (64, 96, 2, 37, 150), (32, 64, 5, 33, 40)])
-def test_x3_xcd_tile_map_bitwise(gpu_device, cout, cin, B, H, W):
+def test_x3_xcd_tile_map_bitwise(gpu_device, ablation_lib, cout, cin, B, H, W):
     """XCD-grouped block -> tile order (default, esr_x3_set_tile_map 1) against row-major blockIdx order (0): a
     renumbering of the same tiles, so bit for bit; grids of 15 / 30 / 45 (16-row) and 8-row tiles are not multiples of
     the 8 XCDs, which exercises the remainder split of xcd_tile."""
@@ -452,23 +459,24 @@ def test_x3_xcd_tile_map_bitwise(gpu_device, cout, cin, B, H, W):
     wx, scale = engine.pack_x3(engine.pack_conv_weight(w.to(gpu_device), list(range(cin)), cout))
     outs = []
     try:
-        for mode in (1, 0):
-            lib.esr_x3_set_tile_map(mode)
+        for L in (lib, ablation_lib):
+            if L is ablation_lib:
+                L.esr_x3_set_tile_map(0)
             out = torch.zeros(B, H + 2, W + 2, cout, device=gpu_device)
             o = engine._conv_out(out, cout, 0, H, W, True)
-            _lib.check(lib.esr_conv3x3_fwd_x3(xs.data_ptr(), B, H, W, cp, cin, wx.data_ptr(), b.data_ptr(), scale,
-                                              cout, ctypes.byref(o), None, _stream()), 'conv_x3')
+            _lib.check(L.esr_conv3x3_fwd_x3(xs.data_ptr(), B, H, W, cp, cin, wx.data_ptr(), b.data_ptr(), scale,
+                                            cout, ctypes.byref(o), None, _stream()), 'conv_x3')
             torch.cuda.synchronize()
             outs.append(out)
     finally:
-        lib.esr_x3_set_tile_map(1)
+        ablation_lib.esr_x3_set_tile_map(1)
     assert torch.equal(outs[0], outs[1])
     ref = F.leaky_relu(F.conv2d(_nchw(engine.from_split(xs), 0, cin), w.double(), b.cpu().double(), padding=1), 0.2)
     assert normwise_rel(_nchw(engine.from_split(outs[0]), 0, cout), ref) < 1e-5
 
 
 @pytest.mark.parametrize('cin,cout,B,H,W', [(192, 64, 2, 24, 40), (72, 40, 1, 9, 21)])
-def test_x3_nsplit_bitwise(gpu_device, cin, cout, B, H, W):
+def test_x3_nsplit_bitwise(gpu_device, ablation_lib, cin, cout, B, H, W):
     """An N = 64 conv on an under-filled grid as two N = 32 launches over the halves of its packed weights
     (esr_x3_set_nsplit, default) against one N = 64 launch: the RDB conv5 epilogue (LeakyReLU off, 0.2 x conv +
     residual at a channel offset, a dual output at another offset) must land in the same channels, bit for bit."""
@@ -481,20 +489,20 @@ def test_x3_nsplit_bitwise(gpu_device, cin, cout, B, H, W):
     b = (torch.rand(cout, generator=g) - 0.5).to(gpu_device)
     wx, scale = engine.pack_x3(engine.pack_conv_weight(w.to(gpu_device), list(range(cin)), 64))
     outs = []
-    prev = lib.esr_x3_set_nsplit(1)
     try:
-        for mode in (1, 0):
-            lib.esr_x3_set_nsplit(mode)
+        for L in (lib, ablation_lib):
+            if L is ablation_lib:
+                L.esr_x3_set_nsplit(0)
             out = torch.zeros(B, H + 2, W + 2, 80, device=gpu_device)
             out2 = torch.zeros(B, H + 2, W + 2, 88, device=gpu_device)
             o = engine._conv_out(out, 80, 8, H, W, False, r1=rs, r1_cp=cp, r1_coff=16, s1=0.2, out2=out2, out2_cp=88,
                                  out2_coff=24)
-            _lib.check(lib.esr_conv3x3_fwd_x3(xs.data_ptr(), B, H, W, cp, cin, wx.data_ptr(), b.data_ptr(), scale,
-                                              cout, ctypes.byref(o), None, _stream()), 'conv_x3')
+            _lib.check(L.esr_conv3x3_fwd_x3(xs.data_ptr(), B, H, W, cp, cin, wx.data_ptr(), b.data_ptr(), scale,
+                                            cout, ctypes.byref(o), None, _stream()), 'conv_x3')
             torch.cuda.synchronize()
             outs.append((out, out2))
     finally:
-        lib.esr_x3_set_nsplit(prev)
+        ablation_lib.esr_x3_set_nsplit(1)
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     ref = F.conv2d(_nchw(engine.from_split(xs), 0, cin), w.double(), b.cpu().double(), padding=1)
     assert normwise_rel(_nchw(engine.from_split(outs[0][0]), 8, 8 + cout), ref * 0.2 +
@@ -503,8 +511,8 @@ def test_x3_nsplit_bitwise(gpu_device, cin, cout, B, H, W):
 
 # default, direct register epilogue 16- / 8-row, classic, column tiles
 @pytest.mark.parametrize('variant', [1, 27, 28, 24, 50, 64])
-def test_conv3x3_x3_planar_output(gpu_device, variant):
-    lib = _lib.load()
+def test_conv3x3_x3_planar_output(gpu_device, variant, request):
+    lib = _lib.load() if variant == 1 else request.getfixturevalue('ablation_lib')
     B, H, W, cin = 2, 19, 45, 72
     x = engine.to_split(_padded(B, H, W, cin, cin, gpu_device, 14))
     w = torch.randn(3, cin, 3, 3, generator=torch.Generator().manual_seed(15)) * 0.05
@@ -513,22 +521,25 @@ def test_conv3x3_x3_planar_output(gpu_device, variant):
     out = torch.full((B, 3, H, W), 7.0, device=gpu_device)
     o = engine._conv_out(out, 0, 0, H, W, False, planar=1)
     try:
-        lib.esr_x3_set_kernel(variant)
+        if variant != 1:
+            lib.esr_x3_set_kernel(variant)
         _lib.check(lib.esr_conv3x3_fwd_x3(x.data_ptr(), B, H, W, cin, cin, wx.data_ptr(),
                                           b.to(gpu_device).data_ptr(), scale, 3, ctypes.byref(o), None, _stream()),
                    'conv_x3')
         torch.cuda.synchronize()
     finally:
-        lib.esr_x3_set_kernel(1)
+        if variant != 1:
+            lib.esr_x3_set_kernel(1)
     ref = F.conv2d(_nchw(engine.from_split(x), 0, cin), w.double(), b.double(), padding=1)
     assert normwise_rel(out.cpu(), ref) < 1e-5
 
 
 @pytest.mark.parametrize('variant', [1, 24])  # column-tile kernel (default), classic kernel
 @pytest.mark.parametrize('H,W', [(6, 9), (16, 40), (37, 21)])
-def test_upconv2x_phases_x3(gpu_device, H, W, variant):
-    lib = _lib.load()
-    lib.esr_x3_set_kernel(variant)
+def test_upconv2x_phases_x3(gpu_device, H, W, variant, request):
+    lib = _lib.load() if variant == 1 else request.getfixturevalue('ablation_lib')
+    if variant != 1:
+        lib.esr_x3_set_kernel(variant)
     B = 2
     x = engine.to_split(_padded(B, H, W, 64, 64, gpu_device, 16))
     w = torch.randn(64, 64, 3, 3, generator=torch.Generator().manual_seed(17)) * 0.05
@@ -543,14 +554,15 @@ def test_upconv2x_phases_x3(gpu_device, H, W, variant):
             _lib.check(lib.esr_upconv2x_phase_fwd_x3(x.data_ptr(), B, H, W, 64, 64, wx.data_ptr(), bd.data_ptr(),
                                                      scale, 64, py, px, ctypes.byref(o), None, _stream()), 'up_x3')
     torch.cuda.synchronize()
-    lib.esr_x3_set_kernel(1)
+    if variant != 1:
+        lib.esr_x3_set_kernel(1)
     ref = F.leaky_relu(F.conv2d(F.interpolate(_nchw(engine.from_split(x), 0, 64), scale_factor=2, mode='nearest'),
                                 w.double(), b.double(), padding=1), 0.2)
     assert normwise_rel(_nchw(engine.from_split(out), 0, 64), ref) < 1e-5
 
 
 @pytest.mark.parametrize('B,H,W,ki,kd,M', [(32, 148, 148, 27, 17, 40), (2, 21, 37, 13, 13, 0), (1, 9, 70, 33, 25, 8)])
-def test_cem_tiled_stencils_bitwise_equal_direct(gpu_device, B, H, W, ki, kd, M):
+def test_cem_tiled_stencils_bitwise_equal_direct(gpu_device, ablation_lib, B, H, W, ki, kd, M):
     """The LDS-tiled inverse-filter and up-add kernels (default) against the direct kernels (esr_cem_set_direct(1)):
     same taps in the same order per output, so bit for bit — at the config-2 shape (B=32, 148² LR) and at ragged
     shapes (tiles past the image edge, windows clamped on every side) — and against float64.  The register-window down
@@ -565,25 +577,27 @@ def test_cem_tiled_stencils_bitwise_equal_direct(gpu_device, B, H, W, ki, kd, M)
     res, downs = {}, {}
     try:
         for direct in (1, 0):
-            lib.esr_cem_set_direct(direct)
+            L = ablation_lib if direct else lib  # the direct kernels: ablation library only
+            if direct:
+                L.esr_cem_set_direct(1)
             downs[direct] = []
             for ph in (1, 2):
                 d = torch.full((B, 3, H, W), 7.0, device=gpu_device)
-                _lib.check(lib.esr_cem_down(gen.data_ptr(), lr.data_ptr(), d.data_ptr(), B, H, W, 4, ph, wu.data_ptr(),
+                _lib.check(L.esr_cem_down(gen.data_ptr(), lr.data_ptr(), d.data_ptr(), B, H, W, 4, ph, wu.data_ptr(),
                                             kd, 0, _stream()), 'down')
                 downs[direct].append(d)
             q = torch.empty_like(r)
-            _lib.check(lib.esr_cem_inv(r.data_ptr(), q.data_ptr(), B, H, W, wi.data_ptr(), ki, _stream()), 'inv')
+            _lib.check(L.esr_cem_inv(r.data_ptr(), q.data_ptr(), B, H, W, wi.data_ptr(), ki, _stream()), 'inv')
             outs = []
             for ph in (1, 2):
                 out = torch.full((B, 3, 4 * H - 2 * M, 4 * W - 2 * M), 7.0, device=gpu_device)
-                _lib.check(lib.esr_cem_up_add(q.data_ptr(), gen.data_ptr(), out.data_ptr(), B, H, W, 4, ph,
+                _lib.check(L.esr_cem_up_add(q.data_ptr(), gen.data_ptr(), out.data_ptr(), B, H, W, 4, ph,
                                               wu.data_ptr(), kd, M, _stream()), 'up_add')
                 outs.append(out)
             torch.cuda.synchronize()
             res[direct] = (q, outs)
     finally:
-        lib.esr_cem_set_direct(0)
+        ablation_lib.esr_cem_set_direct(0)
     assert torch.equal(res[0][0], res[1][0])
     for a, b in zip(res[0][1], res[1][1]):
         assert torch.equal(a, b)
@@ -610,7 +624,7 @@ def test_cem_tiled_stencils_bitwise_equal_direct(gpu_device, B, H, W, ki, kd, M)
 
 @pytest.mark.parametrize('cin,B,H,W', [(64, 2, 19, 45), (72, 3, 17, 61), (64, 1, 1, 1), (72, 2, 40, 30),
                                        (64, 4, 33, 92)])
-def test_conv3x3_x3_narrow_planar(gpu_device, cin, B, H, W):
+def test_conv3x3_x3_narrow_planar(gpu_device, ablation_lib, cin, B, H, W):
     """The narrow-N x3 path (cout 3, planar fp32 output: HR_conv1 -> CEM; taps in the MFMA M dimension, shifted
     partial products summed from LDS) against float64, and against the N = 32 tile path it replaces (same x3 products,
     another tap summation order), over odd sizes, partial 30-column tiles, the latent 72-channel input (a half-filled
@@ -624,16 +638,17 @@ def test_conv3x3_x3_narrow_planar(gpu_device, cin, B, H, W):
     wx, scale = engine.pack_x3(engine.pack_conv_weight(w.to(gpu_device), list(range(cin)), 32))
     outs = []
     try:
-        for narrow in (1, 0):
-            lib.esr_x3_set_narrow(narrow)
+        for L in (lib, ablation_lib):  # narrow-N (product) / N = 32 tiles (ablation library)
+            if L is ablation_lib:
+                L.esr_x3_set_narrow(0)
             out = torch.full((B, 3, H, W), 7.0, device=gpu_device)
             o = engine._conv_out(out, 0, 0, H, W, False, planar=1)
-            _lib.check(lib.esr_conv3x3_fwd_x3(xs.data_ptr(), B, H, W, cp, cin, wx.data_ptr(), b.data_ptr(), scale, 3,
-                                              ctypes.byref(o), None, _stream()), 'conv_x3')
+            _lib.check(L.esr_conv3x3_fwd_x3(xs.data_ptr(), B, H, W, cp, cin, wx.data_ptr(), b.data_ptr(), scale, 3,
+                                            ctypes.byref(o), None, _stream()), 'conv_x3')
             torch.cuda.synchronize()
             outs.append(out.cpu())
     finally:
-        lib.esr_x3_set_narrow(1)
+        ablation_lib.esr_x3_set_narrow(1)
     ref = F.conv2d(_nchw(engine.from_split(xs), 0, cin), w.double(), b.cpu().double(), padding=1)
     for out in outs:
         assert normwise_rel(out, ref) < 2e-6, normwise_rel(out, ref)

@@ -242,17 +242,19 @@ def test_input_and_parameter_gradients_together_vs_oracle(gpu_device, mode, prec
     (64, 64, 32, 36, 2, 0, 2, 9, 31, 4),         # unaligned output-gradient pitch / offset
 ])
 def test_weight_gradient_kernels_vs_float64(gpu_device, variant, cin, in_cp, cout, dout_cp, dout_coff, up2, B, H, W,
-                                            splits):
+                                            splits, request):
     """esr_conv3x3_wgrad (both fp32 kernels, and the x3 kernel on split-f16 activations) + esr_wgrad_reduce against
     torch.nn.grad.conv2d_weight in float64.  The x3 kernel splits the output gradient per pixel tile after a
     power-of-two scaling; here the output gradient is ~2^-30 (a realistic loss-gradient magnitude, far below f16's
     range) and its magnitude changes by 2^3 steps from one 8-row tile / image to the next, so that tiles take
     different scales (the accumulator is rescaled between them) and every tile still counts in the norm.
     x3_dsplit: the output gradient split-f16 at one scale S (the x3 backward's layout, flags bit 8) on the LDS-DMA
-    kernel (wgrad3d); x3_dsplit_reg: the same on the register-staged x3 kernel."""
+    kernel (wgrad3d); x3_dsplit_reg: the same on the register-staged x3 kernel.  Variants 0 and x3_dsplit_reg run on
+    the ablation library (the product library's choices are 1 / the LDS-DMA kernel)."""
     import ctypes
     from esr_amd import _lib
-    lib = _lib.load()
+    ablation = variant in (0, 'x3_dsplit_reg')
+    lib = request.getfixturevalue('ablation_lib') if ablation else _lib.load()
     g = torch.Generator().manual_seed(cin * 7 + cout)
     Hi, Wi = (H // 2, W // 2) if up2 else (H, W)
     x = torch.randn(B, cin, Hi, Wi, generator=g)
@@ -288,16 +290,18 @@ def test_weight_gradient_kernels_vs_float64(gpu_device, variant, cin, in_cp, cou
     partial = torch.full((splits * n,), float('nan'), device=gpu_device)
     out = torch.empty(n, device=gpu_device)
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    prev = lib.esr_wgrad_set_kernel(variant if not x3 else 1)
-    prev_dma = lib.esr_wgrad3_set_dma(0 if variant == 'x3_dsplit_reg' else 1)
+    if ablation:
+        lib.esr_wgrad_set_kernel(variant if not x3 else 1)
+        lib.esr_wgrad3_set_dma(0 if variant == 'x3_dsplit_reg' else 1)
     try:
         _lib.check(lib.esr_conv3x3_wgrad(xin.data_ptr(), in_cp, cin, flags, dbuf.data_ptr(), dout_cp, dout_coff, cout,
                                          B, H, W, splits, partial.data_ptr(), st), 'wgrad')
         _lib.check(lib.esr_wgrad_reduce(partial.data_ptr(), splits, n, 1.0 / S, out.data_ptr(), st), 'reduce')
         torch.cuda.synchronize()
     finally:
-        lib.esr_wgrad_set_kernel(prev)
-        lib.esr_wgrad3_set_dma(prev_dma)
+        if ablation:
+            lib.esr_wgrad_set_kernel(1)
+            lib.esr_wgrad3_set_dma(1)
     out = out.cpu().double()
     xr = x.double()
     if up2:

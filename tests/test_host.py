@@ -5,6 +5,7 @@ import json
 import math
 import os
 import re
+import subprocess
 
 import numpy as np
 import pytest
@@ -127,6 +128,22 @@ def test_library_exports_every_header_symbol():
         assert hasattr(lib, s), s
     assert _lib.load().esr_abi_version() == _lib.ABI_VERSION
     assert lib.esr_op_size() == ctypes.sizeof(_lib.EsrOp)  # op-list record layout matches the binding
+
+
+def test_product_library_is_stateless():
+    """The product library exports no kernel-selection setters (include/esr_amd.h: every entry point stateless); they
+    exist only in the ablation library (csrc/esr_ablation.h), which also exports the whole product ABI."""
+    syms = subprocess.run(['nm', '-D', '--defined-only', _lib.LIB_PATH], capture_output=True, text=True,
+                          check=True).stdout
+    exported = {line.split()[-1] for line in syms.splitlines() if line.split()[-1].startswith('esr_')}
+    assert exported == set(_lib.EXPORTED), sorted(exported ^ set(_lib.EXPORTED))
+    assert not any('_set_' in e for e in exported)
+    if os.path.exists(_lib.ABLATION_PATH):
+        abl = ctypes.CDLL(_lib.ABLATION_PATH)
+        for name in _lib.EXPORTED + _lib.ABLATION_SETTERS:
+            assert hasattr(abl, name), name
+        hdr = open(os.path.join(REPO, 'explorable-super-resolution_old_amd', 'csrc', 'esr_ablation.h')).read()
+        assert set(re.findall(r'^int\s+(esr_\w+)\s*\(', hdr, flags=re.M)) == set(_lib.ABLATION_SETTERS)
 
 
 def test_product_path_refuses_cpu_tensors():

@@ -53,9 +53,7 @@ def main():
             for tag, mode, halo, s2d in variants:
                 dconv.S2D = bool(s2d)
                 dconv.set_precision({0: 'f32', 3: 'x6'}.get(mode, 'x3'))
-                dconv._applied[0] = None
-                dconv._lib_for_launch()
-                lib.esr_dconv_set_x3(mode)
+                dconv._LIB_MODE['x3'] = 2 if mode == 2 else 1  # per-call prec code (x3 with 64-wide tiles: 2)
                 lib.esr_dconv_set_halo(halo)
                 lib.esr_dconv_set_rows(min(halo, 1))  # *_halo: the halo forward and the tap-row weight gradient
                 lib.esr_dconv_set_occ3(0 if tag.endswith('_occ2') else 1)
@@ -96,11 +94,10 @@ def main():
             row[tag + '_dgrad_diff'] = float((outs[tag + 'd'] - outs['f32d']).norm() / outs['f32d'].norm())
             row[tag + '_wgrad_diff'] = float((outs[tag + 'w'] - outs['f32w']).norm() / outs['f32w'].norm())
         print(name, json.dumps(row), flush=True)
-    lib.esr_dconv_set_x3(0)
+    dconv._LIB_MODE['x3'] = 1
     lib.esr_dconv_set_halo(1)
-    lib.esr_dconv_set_rows(1)
+    lib.esr_dconv_set_rows(0)
     dconv.S2D = True
-    dconv._applied[0] = None
 
 
 if __name__ == '__main__':
