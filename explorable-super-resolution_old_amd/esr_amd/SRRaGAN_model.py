@@ -34,6 +34,7 @@ import torch
 import torch.distributed as dist
 
 from . import CEMnet
+from . import dconv as D
 from . import engine as E
 from . import networks
 from . import train_engine as TE
@@ -242,6 +243,9 @@ class SRRaGANModel:
         self.max_accumulation_steps = accumulation_steps_per_batch
         self.l_gan_w = t['gan_weight']
         self.D_exists = self.l_gan_w > 0
+        # precision of the discriminator in the G step (its data gradient into fake_H seeds G's backward); None = the
+        # dconv module default
+        self.d_gstep_precision = os.environ.get('ESR_D_GSTEP_PRECISION') or None
         self.netG.train()
         self.cri_range = CreateRangeLoss(opt.get('range', [0, 1])) if t.get('range_weight', 0) > 0 else None
         self.l_range_w = t.get('range_weight', 0)
@@ -595,7 +599,13 @@ class SRRaGANModel:
                 l_g_range = self.cri_range(self.fake_H)
                 l_g_total = l_g_total + self.l_range_w * l_g_range / self.grad_accumulation_steps_G
             if self.D_exists:
-                pred_g_fake = self.netD(self.fake_H)
+                # (the D's forward here fixes the precision of its backward into fake_H, which seeds G's backward)
+                prev = D.set_precision(self.d_gstep_precision) if self.d_gstep_precision else None
+                try:
+                    pred_g_fake = self.netD(self.fake_H)
+                finally:
+                    if prev is not None:
+                        D.set_precision(prev)
                 if self.relativistic_D:
                     pred_d_real = self.netD(self.var_ref).detach()
                     l_g_gan = self.l_gan_w * (self.cri_gan(pred_d_real - torch.mean(pred_g_fake), False) +

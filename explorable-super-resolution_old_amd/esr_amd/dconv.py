@@ -37,6 +37,8 @@ if os.environ.get('ESR_DCONV_NB128', '1') == '0':
 # space-to-depth source / into the depth-to-space gradient (esr_dconv_fwd_sd, one launch each); '0' = the direct
 # stride-2 gather and one launch per phase class (A/B)
 S2D = os.environ.get('ESR_DCONV_S2D', '1') != '0'
+# conv bias gradients (Σ over pixels of the output gradient) accumulated in float64 ('0': float32 sums)
+BIAS_F64 = os.environ.get('ESR_DCONV_BIAS_F64', '0') != '0'
 
 
 def set_precision(p):
@@ -231,57 +233,62 @@ def conv_wgrad(x, gy, k, s, p, prec=None):
     return red.view(k, k, cin_pad, cout_pad)[:, :, :Ci, :Co].permute(3, 2, 0, 1).contiguous()
 
 
+# The precision of a conv is fixed when its forward runs (the module default, or the layer's own
+# HipConv2d.esr_precision) and travels to every launch of its backward and double backward.
 class DConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, k, s, p):
+    def forward(ctx, x, w, b, k, s, p, prec=None):
+        prec = prec or PRECISION
         ctx.save_for_backward(x, w)
-        ctx.geom = (k, s, p)
+        ctx.geom = (k, s, p, prec)
         ctx.has_bias = b is not None
-        return conv_forward(x, w, b, k, s, p)
+        return conv_forward(x, w, b, k, s, p, prec)
 
     @staticmethod
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
-        k, s, p = ctx.geom
+        k, s, p, prec = ctx.geom
         gy = gy.contiguous()
-        gx = DgradFn.apply(gy, w, k, s, p, x.shape[1], x.shape[2]) if ctx.needs_input_grad[0] else None
-        gw = WgradFn.apply(x, gy, k, s, p) if ctx.needs_input_grad[1] else None
-        gb = gy.sum((0, 1, 2)) if ctx.has_bias and ctx.needs_input_grad[2] else None
-        return gx, gw, gb, None, None, None
+        gx = DgradFn.apply(gy, w, k, s, p, x.shape[1], x.shape[2], prec) if ctx.needs_input_grad[0] else None
+        gw = WgradFn.apply(x, gy, k, s, p, prec) if ctx.needs_input_grad[1] else None
+        gb = None
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = gy.sum((0, 1, 2), dtype=torch.float64).float() if BIAS_F64 else gy.sum((0, 1, 2))
+        return gx, gw, gb, None, None, None, None
 
 
 class DgradFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, gy, w, k, s, p, H, W):
+    def forward(ctx, gy, w, k, s, p, H, W, prec=None):
         ctx.save_for_backward(gy, w)
-        ctx.geom = (k, s, p)
-        return conv_dgrad(gy, w, k, s, p, H, W)
+        ctx.geom = (k, s, p, prec)
+        return conv_dgrad(gy, w, k, s, p, H, W, prec)
 
     @staticmethod
     def backward(ctx, ggx):
         gy, w = ctx.saved_tensors
-        k, s, p = ctx.geom
+        k, s, p, prec = ctx.geom
         ggx = ggx.contiguous()
-        g_gy = DConvFn.apply(ggx, w, None, k, s, p) if ctx.needs_input_grad[0] else None
-        g_w = WgradFn.apply(ggx, gy, k, s, p) if ctx.needs_input_grad[1] else None
-        return g_gy, g_w, None, None, None, None, None
+        g_gy = DConvFn.apply(ggx, w, None, k, s, p, prec) if ctx.needs_input_grad[0] else None
+        g_w = WgradFn.apply(ggx, gy, k, s, p, prec) if ctx.needs_input_grad[1] else None
+        return g_gy, g_w, None, None, None, None, None, None
 
 
 class WgradFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gy, k, s, p):
+    def forward(ctx, x, gy, k, s, p, prec=None):
         ctx.save_for_backward(x, gy)
-        ctx.geom = (k, s, p)
-        return conv_wgrad(x, gy, k, s, p)
+        ctx.geom = (k, s, p, prec)
+        return conv_wgrad(x, gy, k, s, p, prec)
 
     @staticmethod
     def backward(ctx, ggw):
         x, gy = ctx.saved_tensors
-        k, s, p = ctx.geom
+        k, s, p, prec = ctx.geom
         ggw = ggw.contiguous()
-        g_x = DgradFn.apply(gy, ggw, k, s, p, x.shape[1], x.shape[2]) if ctx.needs_input_grad[0] else None
-        g_gy = DConvFn.apply(x, ggw, None, k, s, p) if ctx.needs_input_grad[1] else None
-        return g_x, g_gy, None, None, None
+        g_x = DgradFn.apply(gy, ggw, k, s, p, x.shape[1], x.shape[2], prec) if ctx.needs_input_grad[0] else None
+        g_gy = DConvFn.apply(x, ggw, None, k, s, p, prec) if ctx.needs_input_grad[1] else None
+        return g_x, g_gy, None, None, None, None
 
 
 class _ToNHWC(torch.autograd.Function):
@@ -357,6 +364,7 @@ class HipConv2d(nn.Conv2d):
         # few input channels (conv0: 3 channels x 9 taps = 27): gather the taps into channels once and run a 1x1 conv,
         # one 32-wide K step instead of one (mostly zero) K step per tap
         self._im2col = s[0] == 1 and self.in_channels * k[0] * k[1] <= 32 and self.in_channels < 8
+        self.esr_precision = None  # this layer's precision ('x3' / 'x6' / 'f32'); None = the module default
 
     def forward(self, x):
         _check_dev(x)
@@ -370,7 +378,7 @@ class HipConv2d(nn.Conv2d):
             C = xh.shape[3]
             cols = _Im2ColFn.apply(xh, k, p)  # channel (ky*k + kx)*C + c
             w1 = F.pad(self.weight.permute(0, 2, 3, 1).reshape(self.out_channels, k * k * C), (0, 32 - k * k * C))
-            y = DConvFn.apply(cols, w1.view(self.out_channels, 32, 1, 1), self.bias, 1, 1, 0)
+            y = DConvFn.apply(cols, w1.view(self.out_channels, 32, 1, 1), self.bias, 1, 1, 0, self.esr_precision)
         else:
-            y = DConvFn.apply(xh, self.weight, self.bias, k, self.stride[0], p)
+            y = DConvFn.apply(xh, self.weight, self.bias, k, self.stride[0], p, self.esr_precision)
         return y.permute(0, 3, 1, 2)

@@ -64,6 +64,12 @@ class Discriminator_VGG_128_(nn.Module):
                                         nn.LeakyReLU(LRELU, False),
                                         nn.Sequential(*_conv_block(min(100, nfeat), 1, 1)))
 
+        head = os.environ.get('ESR_D_HEAD_PRECISION')  # (experiment) the classifier's convs in their own precision
+        if head:
+            for m in self.classifier.modules():
+                if isinstance(m, HipConv2d):
+                    m.esr_precision = head
+
     def forward(self, x):
         return _run(self.classifier, _run(self.features, x))
 

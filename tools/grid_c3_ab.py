@@ -1,0 +1,43 @@
+#!/usr/bin/env python3
+"""Config-3 production-grid parity under precision options of the discriminator (round-4 review item 2).
+
+Each variant runs tests/grid_parity.c3_training_step (the reference's own optimize_parameters at B=16 × 96², nb=23,
+bound = 5× the reference's float32 error + 1e-4 floor, unchanged) and prints its worst quantities.
+    usage: python tools/grid_c3_ab.py [variant ...]     variants: base gstep_x6 gstep_f32 head_x6 head_f32 bias64 ...
+    (a variant name joins options with '+': e.g. gstep_x6+bias64)
+"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (REPO, os.path.join(REPO, 'tests'), os.path.join(REPO, 'explorable-super-resolution_old_amd')):
+    sys.path.insert(0, p)
+
+import torch  # noqa: E402
+
+OPTS = {'gstep_x6': ('ESR_D_GSTEP_PRECISION', 'x6'), 'gstep_f32': ('ESR_D_GSTEP_PRECISION', 'f32'),
+        'head_x6': ('ESR_D_HEAD_PRECISION', 'x6'), 'head_f32': ('ESR_D_HEAD_PRECISION', 'f32')}
+
+
+def main():
+    import grid_parity as GP
+    from esr_amd import dconv
+    dev = torch.device('cuda', 0)
+    for name in sys.argv[1:] or ['base']:
+        for k, _ in OPTS.values():
+            os.environ.pop(k, None)
+        dconv.BIAS_F64 = False
+        for opt in name.split('+'):
+            if opt == 'bias64':
+                dconv.BIAS_F64 = True
+            elif opt in OPTS:
+                os.environ[OPTS[opt][0]] = OPTS[opt][1]
+        r = GP.c3_training_step(dev)
+        print('== %s ok %s worst %.4f' % (name, r['ok'], r['worst_frac_of_bound']), flush=True)
+        for line in r['lines'][:2]:
+            print('   ' + line, flush=True)
+        torch.cuda.empty_cache()
+
+
+if __name__ == '__main__':
+    main()
