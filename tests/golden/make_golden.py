@@ -252,7 +252,28 @@ def _digest(v, seed, idx, k):
     return np.random.default_rng([seed, idx]).standard_normal((k, g.size)) @ g
 
 
-def zgrid_fixture(arch, CEMnet):
+def kernelgan_x4_kernel():
+    """A ×4 blur kernel made by the reference's own KernelGAN post-processing (KernelGAN/util.py:123-182, train.py:19-21
+    with conf.X4): post_process_k (zeroize all but the n_filtering = 40 largest taps, re-centre with kernel_shift) of a
+    13×13 ×2 estimate (G_kernel_size = 13, configs.py:25, 41), then analytic_kernel (×2 -> ×4, 37×37 cropped to 25×25).
+    KernelGAN's own training cannot run here (CUDA-only, needs an image dataset): its ×2 estimate is synthetic, an
+    anisotropic Gaussian on a small positive floor from a seeded NumPy stream.  Saved to kernelgan_x4.npz."""
+    import importlib.util
+    np.int = int  # shim: kernel_shift (util.py:204) uses the np.int alias NumPy 2 removed
+    spec = importlib.util.spec_from_file_location('kgan_util', os.path.join(REF, 'KernelGAN', 'util.py'))
+    util = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(util)
+    rng = np.random.default_rng(1313)
+    raw = synthetic_learned_kernel(size=13, sigma=(0.9, 1.5), theta_deg=-25.0, shift=(0.4, 0.1))
+    raw = raw + 2e-3 * rng.random(raw.shape) * raw.max()
+    raw = (raw / raw.sum()).astype(np.float32)
+    k2 = util.post_process_k(torch.from_numpy(raw), n=40)
+    k4 = util.analytic_kernel(k2)
+    np.savez_compressed(os.path.join(HERE, 'kernelgan_x4.npz'), raw_x2=raw, post_x2=k2, kernel_x4=k4)
+    return k4
+
+
+def zgrid_fixture(arch, CEMnet, kernel=None, out='grid_c5_zgrad.npz'):
     """Z-optimisation input gradients (Z_optimization.py:545-630, generator frozen, loss = Σ out·R) at config 5's grid,
     float64 and float32: K seeded random projections + norms of dL/dZ, dL/dLR and of the output per image (the full
     float64 gradients are 6 MB per image).  RRDB.forward (block.py:262-270) runs under torch.utils.checkpoint so that
@@ -262,7 +283,7 @@ def zgrid_fixture(arch, CEMnet):
     fwd = blk.RRDB.forward
     blk.RRDB.forward = lambda self, x: ckpt.checkpoint(fwd, self, x, use_reentrant=False)
     cfg = dict(Z_GRID)
-    k = synthetic_learned_kernel()
+    k = synthetic_learned_kernel() if kernel is None else kernel
     B, h, idx = cfg['B'], cfg['h'], cfg['images']
     lr, z = seeded_inputs(cfg['seed'] + 1, (B, 3, h, h), (B, 3, 4 * h, 4 * h), z_mode='pixel')
     R = np.random.default_rng(cfg['seed'] + 2).standard_normal((B, 3, 4 * h, 4 * h)).astype(np.float32)
@@ -293,7 +314,7 @@ def zgrid_fixture(arch, CEMnet):
         print('zgrid [%s]: |dz| %s' % (tag, [float(zt.grad[j].norm()) for j in range(len(idx))]), flush=True)
         del model, out, zt, lt
     blk.RRDB.forward = fwd
-    np.savez_compressed(os.path.join(HERE, 'grid_c5_zgrad.npz'), **d)
+    np.savez_compressed(os.path.join(HERE, out), **d)
 
 
 def disc_fixture(arch, loss_mod, name, seed):
@@ -383,6 +404,9 @@ def main():
     torch.set_num_threads(8)
     if sys.argv[1:] == ['c5grid']:  # config 5's grid, learned kernel: its own process (imresize's sticky kernel)
         zgrid_fixture(arch, CEMnet)
+        return
+    if sys.argv[1:] == ['c5grid_kgan']:  # config 5's grid with the KernelGAN-recipe ×4 kernel (margins 22/88)
+        zgrid_fixture(arch, CEMnet, kernelgan_x4_kernel(), 'grid_c5_zgrad_kgan.npz')
         return
     if sys.argv[1:] == ['scale2']:  # ×2 generators (architecture.py:113-136) in their own process: imresize's bicubic
         sf = 2                     # kernel is process-global and sticky.  (×3 cannot be built by the reference:

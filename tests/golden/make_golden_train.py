@@ -44,8 +44,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 import make_golden as MG  # noqa: E402
 from oracle.recipe import seeded_params  # noqa: E402
-from train_recipe import (C3_GRID_CFG, CKPT_CFG, LR_CFG, TRAIN_CFGS, drive_lr_schedule, grad_projections,  # noqa: E402
-                          random_points, step_data, train_opt)
+from train_recipe import (C3_GRID_CFG, CKPT_CFG, LR_CFG, TRAIN_CFGS, VAL_CFG, VAL_ZS, drive_lr_schedule,  # noqa: E402
+                          grad_projections, random_points, step_data, train_opt, val_items)
 
 SMALL = 4096  # keys with at most this many elements get their full parameter change stored
 
@@ -280,6 +280,37 @@ def checkpoint_fixtures():
     print('ckpt_save: %s (%d bytes), state for params %s' % (p, os.path.getsize(p), sorted(st['state'])))
 
 
+class ValLoader:
+    """What train.py's val_loader hands perform_validation: batch-1 dicts and .dataset (CHW tensors)."""
+    def __init__(self, items):
+        self.dataset = [{'LR': torch.from_numpy(it['LR']), 'HR': torch.from_numpy(it['HR']), 'HR_path': it['HR_path']}
+                        for it in items]
+
+    def __len__(self):
+        return len(self.dataset)
+
+    def __iter__(self):
+        for it in self.dataset:
+            yield {'LR': it['LR'][None], 'HR': it['HR'][None], 'HR_path': [it['HR_path']]}
+
+
+def validation_fixture():
+    """The reference's own perform_validation (SRRaGAN_model.py:586-635) for three latent values: the returned SR
+    images (HWC BGR float32 0-255) and print_rlt['psnr'] after each call (save_images off: its PNG writer is cv2)."""
+    cfg = dict(VAL_CFG)
+    model = build_reference(cfg, torch.float32)
+    loader = ValLoader(val_items())
+    rlt = {'psnr': 0}
+    d = {'cfg': np.str_(json.dumps(cfg)), 'zs': np.array(VAL_ZS, dtype=np.float64)}
+    for z in VAL_ZS:
+        srs = model.perform_validation(loader, z, rlt, save_GT_HR=False, save_images=False)
+        d['psnr_after:%g' % z] = np.float64(rlt['psnr'])
+        for i, sr in enumerate(srs):
+            d['sr:%g:%d' % (z, i)] = np.asarray(sr, dtype=np.float32)
+        print('validation Z=%g: psnr sum %.6f, SR shapes %s' % (z, rlt['psnr'], [s.shape for s in srs]))
+    np.savez_compressed(os.path.join(HERE, 'validation.npz'), **d)
+
+
 def lr_schedule_fixture():
     import shutil
     cfg = dict(LR_CFG)
@@ -305,6 +336,8 @@ def main():
             checkpoint_fixtures()
         elif name == 'lr':
             lr_schedule_fixture()
+        elif name == 'val':
+            validation_fixture()
         elif name == 'c3':
             c3_grid_fixture()
         else:

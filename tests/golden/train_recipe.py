@@ -67,6 +67,23 @@ CKPT_CFG = dict(nb=1, batch=2, lr_size=40, lr=1e-4, relativistic=0, D_update_rat
 
 
 
+# perform_validation (SRRaGAN_model.py:586-635) as train.py:163-173 calls it: the CKPT_CFG model (nb=1 latent CEM, its
+# own seeded weights) on four batch-1 validation images of different sizes, for latent values 0, -1 and 1
+VAL_CFG = dict(CKPT_CFG, seed=720)
+VAL_SIZES = [(20, 24), (24, 20), (22, 22), (20, 20)]
+VAL_ZS = (0, -1, 1)
+
+
+def val_items():
+    """The validation set: CHW float32 LR / HR pairs (HR 4× the LR) and their paths."""
+    rng = np.random.default_rng(5)
+    items = []
+    for i, (h, w) in enumerate(VAL_SIZES):
+        items.append({'LR': rng.random((3, h, w), dtype=np.float32),
+                      'HR': rng.random((3, 4 * h, 4 * w), dtype=np.float32), 'HR_path': 'val/img%d.png' % i})
+    return items
+
+
 # update_learning_rate (SRRaGAN_model.py:637-683) as train.py:187-189 drives it: one call per gradient step, D losses
 # whose spread jumps at step 10 (std over a 4-step window: ~0.01 before, ~0.5 after, threshold 0.05), checkpoints at
 # gradient steps 2 and 5 (saved only before the first LR drop), lr_gamma 0.05 so that the fourth drop takes the LR

@@ -84,3 +84,34 @@ def test_perform_validation(gpu_device, tmp_path):
     assert os.path.isfile(os.path.join(str(tmp_path), 'GT_HR.png'))
     assert not np.array_equal(outs[-1][0], outs[1][0])  # the latent value reaches the generator
     assert model.netG.training  # test() leaves the model in train mode
+
+
+@pytest.mark.parametrize('precision', ['x3', 'f32'])
+def test_perform_validation_vs_reference(gpu_device, precision):
+    """perform_validation against the reference's own method (tests/golden/validation.npz, made by
+    make_golden_train.py val: the reference's SRRaGANModel with the VAL_CFG seeded weights on the same four images, for
+    Z = 0, -1, 1): the returned SR images (HWC BGR float32 0-255) within 1e-5 normwise of the reference's float32 CPU
+    run, and print_rlt['psnr'] after each call within 1e-4 dB per image."""
+    from esr_amd import engine
+    from esr_amd.SRRaGAN_model import SRRaGANModel
+    from oracle.recipe import seeded_params
+    from train_recipe import VAL_CFG, VAL_ZS, val_items
+    d = np.load(os.path.join(HERE, 'golden', 'validation.npz'))
+    torch.manual_seed(0)
+    model = SRRaGANModel(train_opt(VAL_CFG), device=gpu_device)
+    gsd = model.netG.state_dict()
+    gp = seeded_params([(k, tuple(v.shape)) for k, v in gsd.items()], VAL_CFG['seed'],
+                       w_scale=VAL_CFG.get('w_scale_G', 1.0))
+    model.netG.load_state_dict({k: torch.from_numpy(v) for k, v in gp.items()}, strict=False)
+    engine.set_precision(model.netG, precision)
+    items = [{'LR': torch.from_numpy(it['LR']), 'HR': torch.from_numpy(it['HR']), 'HR_path': it['HR_path']}
+             for it in val_items()]
+    rlt = {'psnr': 0}
+    for z in VAL_ZS:
+        srs = model.perform_validation(_Loader(items), z, rlt, save_GT_HR=False, save_images=False)
+        for i, sr in enumerate(srs):
+            ref = d['sr:%g:%d' % (z, i)]
+            assert sr.shape == ref.shape and sr.dtype == np.float32
+            err = float(np.abs(sr.astype(np.float64) - ref).max() / np.abs(ref).max())
+            assert err < 1e-5, (z, i, err)
+        assert abs(rlt['psnr'] - float(d['psnr_after:%g' % z])) < 1e-4 * len(items), (z, rlt['psnr'])
