@@ -14,7 +14,7 @@ the op-list executor esr_run_ops, so the timing adds no host round trips); `cpu_
 the CPU oracle restatement (oracle/esr_oracle.py, PyTorch-CPU oneDNN convs) on a bounded sample, rank 0 only.
 Extra keys, each timed separately after the headline (--no-legs skips them): `fp32_c2` (the same step in exact fp32),
 `train_c3` / `train_c4` (one SRRaGANModel.optimize_parameters step, bench_train.py), `zopt_c5` (one Z-optimisation
-iteration, bench_zopt.py).
+iteration, bench_zopt.py, with SURVEY §8's KernelGAN-recipe kernel; `zopt_c5_learned13` with the 13×13 learned one).
 """
 import argparse
 import json
@@ -166,7 +166,8 @@ def reference_parity(dev):
         sys.path.insert(0, tests)
     import grid_parity as GP
     out = {}
-    for key, fn in (('train_c3', GP.c3_training_step), ('zopt_c5', GP.c5_z_gradients)):
+    for key, fn in (('train_c3', GP.c3_training_step), ('zopt_c5', lambda d: GP.c5_z_gradients(d, kernel='kgan')),
+                    ('zopt_c5_learned13', lambda d: GP.c5_z_gradients(d, kernel='learned13'))):
         try:
             r = fn(dev)
             out[key] = {'vs': 'reference float64 run (5x its float32 error + 1e-4 floor)', 'ok': r['ok'],
@@ -235,9 +236,11 @@ def run_legs(args, dev, world, rank):
     except Exception as e:  # noqa: BLE001
         legs['fp32_c2'] = {'error': repr(e)}
     torch.cuda.empty_cache()
-    for key, mod in (('train_c4' if world > 1 else 'train_c3', bench_train), ('zopt_c5', bench_zopt)):
+    for key, mod, kw in (('train_c4' if world > 1 else 'train_c3', bench_train, {}),
+                         ('zopt_c5', bench_zopt, {'kernel': 'kgan'}),
+                         ('zopt_c5_learned13', bench_zopt, {'kernel': 'learned13'})):
         try:
-            legs[key] = mod.run(mod.leg_args(steps=args.leg_steps), dev, world, rank)
+            legs[key] = mod.run(mod.leg_args(steps=args.leg_steps, **kw), dev, world, rank)
         except Exception as e:  # noqa: BLE001
             legs[key] = {'error': repr(e)}
         torch.cuda.empty_cache()

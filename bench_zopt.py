@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Z-optimisation benchmark (BASELINE.json config 5): CEM-wrapped latent RRDB-23 with a learned (non-bicubic) 13×13
-blur kernel, batch 8 of 128×128 LR, eval mode (CEM pre-pad), Z_optimizer('max_STD') iterations — each one a
+"""Z-optimisation benchmark (BASELINE.json config 5): CEM-wrapped latent RRDB-23 with a learned (non-bicubic) blur
+kernel — by default the ×4 kernel of the reference's KernelGAN post-processing, --kernel learned13 the 13×13
+one of the CEM fixtures — batch 8 of 128×128 LR, eval mode (CEM pre-pad), Z_optimizer('max_STD') iterations — each one a
 generator forward with retained activations + the HIP input-gradient sweep to Z + Adam on Z.
 
     python bench_zopt.py [--gpus N --steps K --warmup W]      (N>1 via torch.distributed.run: images sharded)
@@ -21,6 +22,18 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 
+def kernelgan_kernel():
+    """SURVEY §8's config-5 kernel: the ×4 kernel of the reference's KernelGAN post-processing (KernelGAN/util.py:
+    123-182, post_process_k + analytic_kernel of a 13×13 ×2 estimate; tests/golden/kernelgan_x4.npz, made by
+    tests/golden/make_golden.py with the reference's own functions).  33×33: CEM's margins are 22 LR / 88 HR pixels, so
+    the generator runs at 172² per image."""
+    with np.load(os.path.join(REPO, 'tests', 'golden', 'kernelgan_x4.npz')) as f:
+        return np.asarray(f['kernel_x4'], dtype=np.float64)
+
+
+KERNELS = {'kgan': 'kernelgan_kernel', 'learned13': 'learned_kernel'}
+
+
 def learned_kernel():
     """The learned (non-bicubic) 13×13 kernel of the reference-made CEM fixture (tests/golden/cem_learned13.npz,
     `input_kernel`: the kernel tests/golden/make_golden.py fed the reference's CEM filter design; no KernelGAN run
@@ -33,7 +46,7 @@ def leg_args(**kw):
     """Default arguments of this benchmark (BASELINE config 5 per GPU), for callers such as bench.py."""
     # warmup 4: the graph captures (2nd call per shape) and the caching allocator's release phase (calls 3-4) stay out
     # of the timed region, as in bench_train.leg_args
-    d = dict(gpus=1, steps=10, warmup=4, batch=8, lr_size=128, nb=23, objective='max_STD')
+    d = dict(gpus=1, steps=10, warmup=4, batch=8, lr_size=128, nb=23, objective='max_STD', kernel='kgan')
     d.update(kw)
     return argparse.Namespace(**d)
 
@@ -51,7 +64,7 @@ def run(args, dev, world, rank):
                          'norm_type': None, 'mode': 'CNA', 'nf': 64, 'nb': args.nb, 'in_nc': 3, 'out_nc': 3,
                          'gc': 32}}
     torch.manual_seed(1234)  # same generator weights on every rank
-    model = SRRaGANModel(opt, kernel=learned_kernel(), device=dev)
+    model = SRRaGANModel(opt, kernel=globals()[KERNELS[args.kernel]](), device=dev)
     networks.init_weights(model.netG.module, scale=0.1)
     g = torch.Generator().manual_seed(99 + rank)
     B, h = args.batch, args.lr_size
@@ -99,9 +112,11 @@ def run(args, dev, world, rank):
             'ms_per_step': round(dt / args.steps * 1e3, 2), 'higher_is_better': True, 'scaling': 'weak',
             'dtype': 'f32', 'fwd_dtype': fwd, 'bwd_dtype': bwd, 'data': 'synthetic',
             'achieved_TFLOPs': round(flop_iter * args.steps / dt / 1e12, 2),
-            'config': {'workload': 'BASELINE config 5: batch %d/GPU of %dx%d LR, learned 13x13 kernel (CEM margins '
-                                   '%d/%d, G at %dx%d), objective %s, nb=%d' % (B, h, h, m, 4 * m, h + 2 * m,
-                                                                                h + 2 * m, args.objective, args.nb),
+            'config': {'workload': 'BASELINE config 5: batch %d/GPU of %dx%d LR, %s kernel (CEM margins %d/%d, G at '
+                                   '%dx%d), objective %s, nb=%d' % (
+                                       B, h, h, {'kgan': 'KernelGAN-recipe x4 33x33',
+                                                 'learned13': 'learned 13x13'}[args.kernel], m, 4 * m, h + 2 * m,
+                                       h + 2 * m, args.objective, args.nb),
                        'global_batch': world * B, 'parallelism': 'images sharded, no collective'},
             'final_loss': zo.loss_values[-1],
             'iter_ms': iter_ms,
@@ -118,6 +133,7 @@ def main():
     ap.add_argument('--lr-size', type=int, default=128)
     ap.add_argument('--nb', type=int, default=23)
     ap.add_argument('--objective', default='max_STD')
+    ap.add_argument('--kernel', choices=sorted(KERNELS), default='kgan')
     args = ap.parse_args()
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))

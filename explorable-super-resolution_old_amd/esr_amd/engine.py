@@ -657,11 +657,7 @@ def generator_forward(net, x, cem=None):
     global OVERFLOW_RERUNS
     _require_device(x, 'generator input')
     if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in param_list(net))):
-        # training step / Z optimisation: retained activations + HIP backward (exact fp32)
-        if getattr(net, 'upscale', SF) != SF:
-            raise NotImplementedError('esr_amd: the HIP backward (training, Z optimisation) implements the ×4 '
-                                      'generator; ×%d runs inference only (torch.no_grad / frozen parameters)'
-                                      % net.upscale)
+        # training step / Z optimisation: retained activations + HIP backward (×4 and ×2)
         from . import train_engine
         return train_engine.generator_forward_train(net, x.contiguous(), cem)
     precision = getattr(net, 'esr_precision', None) or DEFAULT_PRECISION
@@ -690,8 +686,6 @@ def _forward(net, x, cem, precision, train_ws=None, rec=None):
     latent = net.latent_input is not None
     nz = net.nl if latent else 0
     sf = getattr(net, 'upscale', SF)
-    if sf != SF and train_ws is not None:
-        raise NotImplementedError('esr_amd: the training / Z-optimisation backward implements the ×4 generator')
     Bn, C, h, w = x.shape
     if C != 3 + nz * sf * sf:
         raise RuntimeError('esr_amd: expected %d input channels (3 LR + %d rearranged HR latent), got %d'

@@ -113,9 +113,10 @@ class TrainWorkspace:
     """Buffers of one training forward/backward at (B, H, W).  Same attribute names as engine._Workspace for the
     shared forward code, plus one concat buffer per RDB (`Q`) and the gradient buffers."""
 
-    def __init__(self, dev, B, H, W, latent, nb):
+    def __init__(self, dev, B, H, W, latent, nb, sf=4):
         zc = 8 if latent else 0
-        self.B, self.H, self.W, self.zc, self.nb = B, H, W, zc, nb
+        self.B, self.H, self.W, self.zc, self.nb, self.sf = B, H, W, zc, nb, sf
+        S = sf
         self.first_cp = 16 if latent else 8
         self.first_lr_off = 8 if latent else 0
         self.cp = zc + 192
@@ -124,8 +125,8 @@ class TrainWorkspace:
         self.fea = _z(dev, B, H + 2, W + 2, 64)
         self.Q = [_z(dev, B, H + 2, W + 2, self.cp) for _ in range(3 * nb + 1)]
         self.U0 = _z(dev, B, H + 2, W + 2, 64)
-        self.U1 = _z(dev, B, 2 * H + 2, 2 * W + 2, 64)
-        self.HR = [_z(dev, B, 4 * H + 2, 4 * W + 2, self.hr_cp) for _ in range(2)]
+        self.U1 = _z(dev, B, 2 * H + 2, 2 * W + 2, 64) if sf == 4 else None  # between the two ×2 upconvs of ×4
+        self.HR = [_z(dev, B, S * H + 2, S * W + 2, self.hr_cp) for _ in range(2)]
         self.lr = _z(dev, B, 3, H, W)
         self.overflow = torch.zeros(1, device=dev, dtype=torch.int32)
         # backward
@@ -135,14 +136,14 @@ class TrainWorkspace:
         self.D = [_z(dev, B, H + 2, W + 2, self.dcp) for _ in range(2)]
         self.GA = _z(dev, B, H + 2, W + 2, 64)
         self.dU0 = _z(dev, B, H + 2, W + 2, 64)
-        self.dU1 = _z(dev, B, 2 * H + 2, 2 * W + 2, 64)
-        self.dUp1 = _z(dev, B, 2 * H + 2, 2 * W + 2, 64)
-        self.dHR = [_z(dev, B, 4 * H + 2, 4 * W + 2, 64) for _ in range(2)]
-        self.dgen_p = _z(dev, B, 4 * H + 2, 4 * W + 2, 8)
+        self.dU1 = _z(dev, B, 2 * H + 2, 2 * W + 2, 64) if sf == 4 else None
+        self.dUp1 = _z(dev, B, 2 * H + 2, 2 * W + 2, 64) if sf == 4 else None
+        self.dHR = [_z(dev, B, S * H + 2, S * W + 2, 64) for _ in range(2)]
+        self.dgen_p = _z(dev, B, S * H + 2, S * W + 2, 8)
         # generator-input gradient (Z optimisation)
         self.dZl = _z(dev, B, H + 2, W + 2, 8)
         self.dFirst = _z(dev, B, H + 2, W + 2, self.first_cp)
-        self.dZh = _z(dev, B, 4 * H + 2, 4 * W + 2, 8) if latent else None
+        self.dZh = _z(dev, B, S * H + 2, S * W + 2, 8) if latent else None
         self.dzs = _z(dev, B, H + 2, W + 2, 8) if latent else None  # x3 backward: split latent-slot gradient
         # per-RRDB max |gradient| bits (x3 backward), then one slot per x3 trunk-level data gradient (_trunk_dgrad_x3)
         self.gamax = torch.zeros(nb + 4, device=dev, dtype=torch.int32)
@@ -171,16 +172,17 @@ def _train_workspace(net, dev, B, H, W, latent, precision='f32'):
     forward before the first one's backward: two generator calls in one loss, retained graphs) — a fresh one, so that
     no forward overwrites another's activations."""
     # keyed by precision too: an x3 forward leaves split-f16 records where an fp32 forward expects floats
-    key = (str(dev), B, H, W, latent, net.nb, precision)
+    sf = getattr(net, 'upscale', E.SF)
+    key = (str(dev), B, H, W, latent, net.nb, precision, sf)
     c = net._esr_cache.get('train_ws')
     if c is None or c[0] != key:
         if c is not None and _busy(c[1]):
-            return TrainWorkspace(dev, B, H, W, latent, net.nb)  # the cached one is still needed: keep it
+            return TrainWorkspace(dev, B, H, W, latent, net.nb, sf)  # the cached one is still needed: keep it
         net._esr_cache.pop('train_ws', None)
-        c = (key, TrainWorkspace(dev, B, H, W, latent, net.nb))
+        c = (key, TrainWorkspace(dev, B, H, W, latent, net.nb, sf))
         net._esr_cache['train_ws'] = c
     if _busy(c[1]):
-        return TrainWorkspace(dev, B, H, W, latent, net.nb)
+        return TrainWorkspace(dev, B, H, W, latent, net.nb, sf)
     return c[1]
 
 
@@ -248,9 +250,10 @@ class _BwdPacked:
                 self.rdb.append(cv)
                 self.rdb_fused.append(_fused_rdb_weights(plan, cv, zc))
         self.lr_conv = _BwdConv(plan, m[1].sub[net.nb], lr_map(64), dgrad_from=zc, in_width=zc)
-        self.up = [_BwdConv(plan, m[j][1], list(range(64))) for j in (2, 3)]
-        self.hr0 = _BwdConv(plan, m[4], lr_map(64), dgrad_from=zc, in_width=zc)
-        self.hr1 = _BwdConv(plan, m[6], lr_map(64), cin_k=8, dgrad_from=zc, in_width=zc)
+        n_up = getattr(net, 'n_up', 2)  # ×4: two nearest-×2 upconvs (model.2, model.3), ×2: one (architecture.py:132)
+        self.up = [_BwdConv(plan, m[2 + j][1], list(range(64))) for j in range(n_up)]
+        self.hr0 = _BwdConv(plan, m[2 + n_up], lr_map(64), dgrad_from=zc, in_width=zc)
+        self.hr1 = _BwdConv(plan, m[4 + n_up], lr_map(64), cin_k=8, dgrad_from=zc, in_width=zc)
         convs = [self.first, self.lr_conv, self.hr0, self.hr1] + self.up + [c for r in self.rdb for c in r]
         dev = m[0].weight.device
         views = plan.finalize(dev)
@@ -283,7 +286,9 @@ class _BwdPacked:
             views = [(i, k, v) for i, f in enumerate(self.rdb_fused) for k, v in f.items()]
             # the trunk-level data gradients at 2x / 4x resolution (HR_conv0, both upconvs): slices and, for
             # HR_conv0, the latent-slot (input) slice; keyed (conv, kind, slice index) in self._x3_trunk
-            trunk = [(name, kind, j, v) for name, c in (('hr0', self.hr0), ('up1', self.up[1]), ('up0', self.up[0]))
+            tconvs = (('hr0', self.hr0),) + ((('up1', self.up[1]),) if len(self.up) > 1 else ()) + \
+                (('up0', self.up[0]),)
+            trunk = [(name, kind, j, v) for name, c in tconvs
                      for kind, sl in (('s', c.slices), ('in', c.in_slices)) for j, (_, _, v) in enumerate(sl)]
             views += [(None, (name, kind, j), v) for name, kind, j, v in trunk]
             amax = torch.stack([v.abs().max() for _, _, v in views]).cpu().tolist()  # first build only
@@ -571,7 +576,9 @@ def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_in
         if latent:
             ws.dZh.zero_()
     Bn, H, W, zc, cp, hcp = ws.B, ws.H, ws.W, ws.zc, ws.cp, ws.hr_cp
-    HH, WW = E.SF * H, E.SF * W
+    sf = ws.sf
+    ph = E.cem_phase(sf)
+    HH, WW = sf * H, sf * W
     # ---- CEM adjoint: out = crop_M(gen + Up(Inv(LR - Down(gen)))) ----
     if cem is not None:
         g = d_out.contiguous()
@@ -586,12 +593,12 @@ def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_in
         kd, ki = wd.shape[-1], wi.shape[-1]
         a1 = torch.empty(Bn, 3, H, W, device=dev)
         a2 = torch.empty_like(a1)
-        _lib.check(lib.esr_cem_adjoint(gfull.data_ptr(), Bn * 3, HH, WW, wu.data_ptr(), kd, 1, 0, HH, WW, E.SF,
-                                       E.CEM_PHASE, 1.0, 0, a1.data_ptr(), stream), 'cem_adjoint up')
+        _lib.check(lib.esr_cem_adjoint(gfull.data_ptr(), Bn * 3, HH, WW, wu.data_ptr(), kd, 1, 0, HH, WW, sf,
+                                       ph, 1.0, 0, a1.data_ptr(), stream), 'cem_adjoint up')
         _lib.check(lib.esr_cem_adjoint(a1.data_ptr(), Bn * 3, H, W, wi.data_ptr(), ki, 1, 0, H, W, 1, 0, 1.0, 0,
                                        a2.data_ptr(), stream), 'cem_adjoint inv')
         dgen = gfull.clone()
-        _lib.check(lib.esr_cem_adjoint(a2.data_ptr(), Bn * 3, H, W, wd.data_ptr(), kd, E.SF, E.CEM_PHASE, HH, WW, 1,
+        _lib.check(lib.esr_cem_adjoint(a2.data_ptr(), Bn * 3, H, W, wd.data_ptr(), kd, sf, ph, HH, WW, 1,
                                        0, -1.0, 1, dgen.data_ptr(), stream), 'cem_adjoint down')
     else:
         dgen = d_out.contiguous()
@@ -614,24 +621,37 @@ def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_in
     else:
         R.dgrad_in(bp.hr0, dA, 64, 0, 64, HH, WW, ws.dZh, 8)
         R.dgrad(bp.hr0, dA, 64, 0, 64, HH, WW, dB, 64, zc, accumulate=False)
-    # upconv 2: HR0.x = lrelu(conv(nearest2(U1)))
-    R.lrelu(dB, 64, 0, HR0, hcp, zc, 64, HH, WW)
-    R.wgrad(bp.up[1], ws.U1, 64, 64, 1, dB, 64, 0, HH, WW)
-    R.join()
-    if tx3:
-        R.dgrad_trunk_x3('up1', bp.up[1], dB, HH, WW, dA, 0, dA, dB, net.nb + 1)
+    if sf == 4:
+        # upconv 2: HR0.x = lrelu(conv(nearest2(U1)))
+        R.lrelu(dB, 64, 0, HR0, hcp, zc, 64, HH, WW)
+        R.wgrad(bp.up[1], ws.U1, 64, 64, 1, dB, 64, 0, HH, WW)
+        R.join()
+        if tx3:
+            R.dgrad_trunk_x3('up1', bp.up[1], dB, HH, WW, dA, 0, dA, dB, net.nb + 1)
+        else:
+            R.dgrad(bp.up[1], dB, 64, 0, 64, HH, WW, dA, 64, 0, accumulate=False)
+        _lib.check(lib.esr_sum2x2(ws.dU1.data_ptr(), 64, 0, dA.data_ptr(), 64, 0, 64, Bn, 2 * H, 2 * W, stream),
+                   'sum2x2')
+        # upconv 1: U1 = lrelu(conv(nearest2(U0)))
+        R.lrelu(ws.dU1, 64, 0, ws.U1, 64, 0, 64, 2 * H, 2 * W)
+        R.wgrad(bp.up[0], ws.U0, 64, 64, 1, ws.dU1, 64, 0, 2 * H, 2 * W)
+        R.join()
+        if tx3:
+            R.dgrad_trunk_x3('up0', bp.up[0], ws.dU1, 2 * H, 2 * W, ws.dUp1, 0, ws.dUp1, ws.dU1, net.nb + 2)
+        else:
+            R.dgrad(bp.up[0], ws.dU1, 64, 0, 64, 2 * H, 2 * W, ws.dUp1, 64, 0, accumulate=False)
+        _lib.check(lib.esr_sum2x2(ws.dU0.data_ptr(), 64, 0, ws.dUp1.data_ptr(), 64, 0, 64, Bn, H, W, stream),
+                   'sum2x2')
     else:
-        R.dgrad(bp.up[1], dB, 64, 0, 64, HH, WW, dA, 64, 0, accumulate=False)
-    _lib.check(lib.esr_sum2x2(ws.dU1.data_ptr(), 64, 0, dA.data_ptr(), 64, 0, 64, Bn, 2 * H, 2 * W, stream), 'sum2x2')
-    # upconv 1: U1 = lrelu(conv(nearest2(U0)))
-    R.lrelu(ws.dU1, 64, 0, ws.U1, 64, 0, 64, 2 * H, 2 * W)
-    R.wgrad(bp.up[0], ws.U0, 64, 64, 1, ws.dU1, 64, 0, 2 * H, 2 * W)
-    R.join()
-    if tx3:
-        R.dgrad_trunk_x3('up0', bp.up[0], ws.dU1, 2 * H, 2 * W, ws.dUp1, 0, ws.dUp1, ws.dU1, net.nb + 2)
-    else:
-        R.dgrad(bp.up[0], ws.dU1, 64, 0, 64, 2 * H, 2 * W, ws.dUp1, 64, 0, accumulate=False)
-    _lib.check(lib.esr_sum2x2(ws.dU0.data_ptr(), 64, 0, ws.dUp1.data_ptr(), 64, 0, 64, Bn, H, W, stream), 'sum2x2')
+        # ×2: the one upconv, HR0.x = lrelu(conv(nearest2(U0))) (architecture.py:132-136)
+        R.lrelu(dB, 64, 0, HR0, hcp, zc, 64, HH, WW)
+        R.wgrad(bp.up[0], ws.U0, 64, 64, 1, dB, 64, 0, HH, WW)
+        R.join()
+        if tx3:
+            R.dgrad_trunk_x3('up0', bp.up[0], dB, HH, WW, dA, 0, dA, dB, net.nb + 2)
+        else:
+            R.dgrad(bp.up[0], dB, 64, 0, 64, HH, WW, dA, 64, 0, accumulate=False)
+        _lib.check(lib.esr_sum2x2(ws.dU0.data_ptr(), 64, 0, dA.data_ptr(), 64, 0, 64, Bn, H, W, stream), 'sum2x2')
     # LR_conv: U0 = conv(trunk[Z | x]) + fea
     Q = ws.Q
     trunk = Q[3 * net.nb]
@@ -670,7 +690,7 @@ def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_in
     dx = None
     if need_input:
         R.dgrad_in(bp.first, ws.GA, 64, 0, 64, H, W, ws.dFirst, ws.first_cp)
-        m = M // E.SF
+        m = M // sf
         h, w = H - 2 * m, W - 2 * m
         d_lr = torch.empty(Bn, 3, h, w, device=dev)
         _lib.check(lib.esr_input_adjoint(ws.dFirst.data_ptr(), ws.first_cp, ws.first_lr_off, None, 0, 0, 0,
@@ -678,10 +698,10 @@ def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_in
                                          d_lr.data_ptr(), stream), 'input_adjoint lr')
         if latent:  # Z_LR = bilinear↓4(Z_HR) feeds conv_first and every LR conv; Z_HR feeds HR_conv0/1
             R.axpby(ws.dZl, 8, 0, 1.0, ws.dZl, 8, 0, 1.0, ws.dFirst, ws.first_cp, 0, C=8, h=H, w=W)
-            d_z = torch.empty(Bn, 3, E.SF * h, E.SF * w, device=dev)
-            _lib.check(lib.esr_input_adjoint(ws.dZh.data_ptr(), 8, 0, ws.dZl.data_ptr(), 8, 0, E.SF, None, 3, Bn,
+            d_z = torch.empty(Bn, 3, sf * h, sf * w, device=dev)
+            _lib.check(lib.esr_input_adjoint(ws.dZh.data_ptr(), 8, 0, ws.dZl.data_ptr(), 8, 0, sf, None, 3, Bn,
                                              HH, WW, M, d_z.data_ptr(), stream), 'input_adjoint z')
-            dx = torch.cat([d_z.view(Bn, 3 * E.SF * E.SF, h, w), d_lr], 1)  # raw view, SRRaGAN_model.py:252
+            dx = torch.cat([d_z.view(Bn, 3 * sf * sf, h, w), d_lr], 1)  # raw view, SRRaGAN_model.py:252
         else:
             dx = d_lr
     return flat, dx
@@ -765,7 +785,7 @@ class _GeneratorFn(torch.autograd.Function):
                 E.lower_act_scale(net)  # a scaled activation left f16's range: smaller activation scale next time
             ws = _train_workspace(net, x.device, Bn, h + 2 * m, w + 2 * m, latent, 'f32')
             out, graphed, split = E._forward(net, xd, cem, 'f32', train_ws=ws)[0], False, False
-        ctx.net, ctx.cem, ctx.ws, ctx.latent, ctx.M, ctx.split = net, cem, ws, latent, E.SF * m, split
+        ctx.net, ctx.cem, ctx.ws, ctx.latent, ctx.M, ctx.split = net, cem, ws, latent, ws.sf * m, split
         ctx.act_scale = A if split else 1.0  # (after an fp32 rerun the activations are unscaled)
         ctx.params = params
         ctx.owner = _Owner()

@@ -107,7 +107,7 @@ def grad_parity(a, exact, base, factor=5.0, floor=1e-4):
     return e <= max(floor, factor * eb), 'l2 %.2e (fp32 reference %.2e, max-norm %.2e)' % (e, eb, normwise_rel(a, exact))
 
 
-def oracle_grads(params, lr, z, R, nb, latent, design, pre_pad, dtype, want_params=True):
+def oracle_grads(params, lr, z, R, nb, latent, design, pre_pad, dtype, want_params=True, sf=4):
     """Gradients of Σ out·R through the oracle (CEM_PyTorch ∘ RRDBNet) in `dtype`: {'param:<key>', 'dz', 'dlr'}.
     `params` are reference-keyed numpy arrays (prefix stripped here); lr/z numpy NCHW (z = HR latent or None)."""
     import torch
@@ -120,7 +120,7 @@ def oracle_grads(params, lr, z, R, nb, latent, design, pre_pad, dtype, want_para
     if latent:
         z_t = torch.as_tensor(z).to(dtype).requires_grad_(True)
         x = torch.cat([z_t.reshape(B, -1, h, w), lr_t], 1)
-    out = O.sr_forward(x, P, nb, latent, design, pre_pad=pre_pad)
+    out = O.sr_forward(x, P, nb, latent, design, pre_pad=pre_pad, sf=sf)
     (out * torch.as_tensor(R).to(dtype)).sum().backward()
     g = {'dlr': lr_t.grad.double().numpy()}
     if z_t is not None:

@@ -179,46 +179,52 @@ GRAD_KEYS = ('model.0.weight', 'model.0.bias', 'model.1.sub.0.RDB1.convs.0.0.wei
              'model.1.sub.0.RDB3.convs.2.0.weight', 'model.1.sub.0.RDB3.convs.4.0.bias', 'model.1.sub.1.weight',
              'model.2.1.weight', 'model.3.1.bias', 'model.4.weight', 'model.6.weight', 'model.6.bias')
 
+# ×2 (architecture.py:113-136): one upconv, so HR_conv0 / HR_conv1 are model.3 / model.5
+GRAD_KEYS_X2 = GRAD_KEYS[:7] + ('model.2.1.weight', 'model.2.1.bias', 'model.3.weight', 'model.5.weight',
+                                'model.5.bias')
 
-def grad_fixture(arch, CEMnet, name, latent, lr_shape, seed, w_scale):
+
+def grad_fixture(arch, CEMnet, name, latent, lr_shape, seed, w_scale, sf=4):
     """Training-step gradients (SRRaGAN_model.py:347-348, 529): CEM-wrapped RRDBNet(nb=1) in train mode, loss =
     Σ out·R with a seeded R; dumps the gradients of GRAD_KEYS (prefixed 'generated_image_model.')."""
     nl = 3 if latent else 0
-    net = arch.RRDBNet(in_nc=3, out_nc=3, nf=64, nb=1, gc=32, upscale=4, norm_type=None, act_type='leakyrelu',
+    net = arch.RRDBNet(in_nc=3, out_nc=3, nf=64, nb=1, gc=32, upscale=sf, norm_type=None, act_type='leakyrelu',
                        mode='CNA', upsample_mode='upconv',
                        latent_input='all_layers_HR_downscaled' if latent else None, num_latent_channels=nl)
-    model = CEMnet.CEMnet(CEMnet.Get_CEM_Config(4)).WrapArchitecture_PyTorch(net)
+    model = CEMnet.CEMnet(CEMnet.Get_CEM_Config(sf)).WrapArchitecture_PyTorch(net)
     sd = model.state_dict()
     named_shapes = [(k, tuple(v.shape)) for k, v in sd.items()]
     params = seeded_params(named_shapes, seed, w_scale=w_scale)
     model.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=False)
     model.train(True)
     B, _, h, w = lr_shape
-    lr, z = seeded_inputs(seed + 1, lr_shape, (B, 3, 4 * h, 4 * w) if latent else None, z_mode='image')
+    lr, z = seeded_inputs(seed + 1, lr_shape, (B, 3, sf * h, sf * w) if latent else None, z_mode='image')
     x = torch.from_numpy(lr)
     if latent:
-        x = torch.cat([torch.from_numpy(z).contiguous().view(B, 48, h, w), x], 1)
+        x = torch.cat([torch.from_numpy(z).contiguous().view(B, 3 * sf * sf, h, w), x], 1)
     out = model(x)
     R = torch.from_numpy(np.random.default_rng(seed + 2).standard_normal(tuple(out.shape)).astype(np.float32))
     (out * R).sum().backward()
     named = dict(model.named_parameters())
     d = dict(lr=lr, R=R.numpy(), out=out.detach().numpy(), latent=np.int64(latent), seed=np.int64(seed),
              w_scale=np.float64(w_scale), keys=np.str_(json.dumps(named_shapes)), nb=np.int64(1))
+    if sf != 4:
+        d['upscale'] = np.int64(sf)
     if z is not None:
         d['z'] = z
-    for k in GRAD_KEYS:
+    for k in GRAD_KEYS if sf == 4 else GRAD_KEYS_X2:
         d['grad:' + k] = named['generated_image_model.' + k].grad.numpy()
     np.savez_compressed(os.path.join(HERE, 'grad_%s.npz' % name), **d)
     print('grad_%s: %d grads, |g conv_first| %.3e' % (name, len(GRAD_KEYS), np.abs(d['grad:model.0.weight']).mean()))
 
 
-def zgrad_fixture(arch, CEMnet, name, cem_mode, lr_shape, seed, w_scale, kernel=None):
+def zgrad_fixture(arch, CEMnet, name, cem_mode, lr_shape, seed, w_scale, kernel=None, sf=4):
     """Z-optimisation gradients (Z_optimization.py:545-553, 574-630): generator frozen (requires_grad False), latent
-    RRDBNet(nb=1) CEM-wrapped in `cem_mode`, loss = Σ out·R; dumps dL/dZ (HR latent, [B,3,4h,4w]) and dL/dLR."""
-    net = arch.RRDBNet(in_nc=3, out_nc=3, nf=64, nb=1, gc=32, upscale=4, norm_type=None, act_type='leakyrelu',
+    RRDBNet(nb=1) CEM-wrapped in `cem_mode`, loss = Σ out·R; dumps dL/dZ (HR latent, [B,3,sf·h,sf·w]) and dL/dLR."""
+    net = arch.RRDBNet(in_nc=3, out_nc=3, nf=64, nb=1, gc=32, upscale=sf, norm_type=None, act_type='leakyrelu',
                        mode='CNA', upsample_mode='upconv', latent_input='all_layers_HR_downscaled',
                        num_latent_channels=3)
-    model = CEMnet.CEMnet(CEMnet.Get_CEM_Config(4), upscale_kernel=kernel).WrapArchitecture_PyTorch(net)
+    model = CEMnet.CEMnet(CEMnet.Get_CEM_Config(sf), upscale_kernel=kernel).WrapArchitecture_PyTorch(net)
     sd = model.state_dict()
     named_shapes = [(k, tuple(v.shape)) for k, v in sd.items()]
     params = seeded_params(named_shapes, seed, w_scale=w_scale)
@@ -227,15 +233,17 @@ def zgrad_fixture(arch, CEMnet, name, cem_mode, lr_shape, seed, w_scale, kernel=
     for q in model.parameters():
         q.requires_grad = False
     B, _, h, w = lr_shape
-    lr, z = seeded_inputs(seed + 1, lr_shape, (B, 3, 4 * h, 4 * w), z_mode='pixel')
+    lr, z = seeded_inputs(seed + 1, lr_shape, (B, 3, sf * h, sf * w), z_mode='pixel')
     zt = torch.from_numpy(z).requires_grad_(True)
     lt = torch.from_numpy(lr).requires_grad_(True)
-    out = model(torch.cat([zt.view(B, 48, h, w), lt], 1))
+    out = model(torch.cat([zt.view(B, 3 * sf * sf, h, w), lt], 1))
     R = torch.from_numpy(np.random.default_rng(seed + 2).standard_normal(tuple(out.shape)).astype(np.float32))
     (out * R).sum().backward()
     d = dict(lr=lr, z=z, R=R.numpy(), out=out.detach().numpy(), dz=zt.grad.numpy(), dlr=lt.grad.numpy(),
              seed=np.int64(seed), w_scale=np.float64(w_scale), cem_mode=np.str_(cem_mode),
              keys=np.str_(json.dumps(named_shapes)), nb=np.int64(1), latent=np.int64(1))
+    if sf != 4:
+        d['upscale'] = np.int64(sf)
     if isinstance(kernel, np.ndarray):
         d['kernel'] = kernel
     np.savez_compressed(os.path.join(HERE, 'zgrad_%s.npz' % name), **d)
@@ -273,7 +281,7 @@ def kernelgan_x4_kernel():
     return k4
 
 
-def zgrid_fixture(arch, CEMnet, kernel=None, out='grid_c5_zgrad.npz'):
+def zgrid_fixture(arch, CEMnet, kernel=None, fname='grid_c5_zgrad.npz'):
     """Z-optimisation input gradients (Z_optimization.py:545-630, generator frozen, loss = Σ out·R) at config 5's grid,
     float64 and float32: K seeded random projections + norms of dL/dZ, dL/dLR and of the output per image (the full
     float64 gradients are 6 MB per image).  RRDB.forward (block.py:262-270) runs under torch.utils.checkpoint so that
@@ -314,7 +322,7 @@ def zgrid_fixture(arch, CEMnet, kernel=None, out='grid_c5_zgrad.npz'):
         print('zgrid [%s]: |dz| %s' % (tag, [float(zt.grad[j].norm()) for j in range(len(idx))]), flush=True)
         del model, out, zt, lt
     blk.RRDB.forward = fwd
-    np.savez_compressed(os.path.join(HERE, out), **d)
+    np.savez_compressed(os.path.join(HERE, fname), **d)
 
 
 def disc_fixture(arch, loss_mod, name, seed):
@@ -407,6 +415,12 @@ def main():
         return
     if sys.argv[1:] == ['c5grid_kgan']:  # config 5's grid with the KernelGAN-recipe ×4 kernel (margins 22/88)
         zgrid_fixture(arch, CEMnet, kernelgan_x4_kernel(), 'grid_c5_zgrad_kgan.npz')
+        return
+    if sys.argv[1:] == ['scale2grad']:  # ×2 training and Z-optimisation gradients (own process: sticky bicubic)
+        grad_fixture(arch, CEMnet, 'x2_plain_nb1', False, (2, 3, 12, 16), 70, 0.5, sf=2)
+        grad_fixture(arch, CEMnet, 'x2_latent_nb1', True, (2, 3, 12, 12), 71, 0.5, sf=2)
+        zgrad_fixture(arch, CEMnet, 'x2_eval', 'eval', (2, 3, 12, 12), 72, 0.5, sf=2)
+        zgrad_fixture(arch, CEMnet, 'x2_train', 'train', (2, 3, 12, 16), 73, 0.5, sf=2)
         return
     if sys.argv[1:] == ['scale2']:  # ×2 generators (architecture.py:113-136) in their own process: imresize's bicubic
         sf = 2                     # kernel is process-global and sticky.  (×3 cannot be built by the reference:

@@ -97,14 +97,20 @@ def c3_training_step(dev, precision='x3', d_precision=None):
     return _result(fails, worst, lines)
 
 
-def c5_z_gradients(dev, precision='x3'):
-    """Config 5 (latent RRDB-23 + CEM eval with the reference-made learned 13×13 kernel, generator frozen, B=8 × 128²):
-    dL/dZ, dL/dLR and the output of images 0 and 7 against the reference's autograd (make_golden.py c5grid)."""
+C5_FIXTURES = {'learned13': 'grid_c5_zgrad.npz', 'kgan': 'grid_c5_zgrad_kgan.npz'}
+
+
+def c5_z_gradients(dev, precision='x3', kernel='kgan'):
+    """Config 5 (latent RRDB-23 + CEM eval, generator frozen, B=8 × 128²): dL/dZ, dL/dLR and the output of images 0 and
+    7 against the reference's autograd.  kernel 'kgan': the ×4 kernel of the reference's KernelGAN post-processing
+    (post_process_k + analytic_kernel, 33×33 after kernel_shift; CEM margins 22 / 88, G at 172²; make_golden.py
+    c5grid_kgan) — SURVEY §8's config-5 geometry; 'learned13': the 13×13 learned kernel of the CEM fixtures (margins
+    13 / 52, G at 154²; make_golden.py c5grid)."""
     import esr_amd
     from esr_amd import CEMnet as C
     from esr_amd import engine
     from oracle.recipe import seeded_inputs, seeded_params
-    d = np.load(os.path.join(HERE, 'golden', 'grid_c5_zgrad.npz'))
+    d = np.load(os.path.join(HERE, 'golden', C5_FIXTURES[kernel]))
     cfg = json.loads(str(d['cfg']))
     B, h, K = cfg['B'], cfg['h'], cfg['proj']
     net = esr_amd.RRDBNet(3, 3, 64, cfg['nb'], latent_input='all_layers_HR_downscaled', num_latent_channels=3)

@@ -10,8 +10,9 @@ bench_train.py / bench_zopt.py.  The checks live in tests/grid_parity.py (bench.
   floor of 1e-4), the logged D outputs / losses / gradient penalty and the D BatchNorm buffers as in
   test_gpu_train_loop.py.
 * Config 5: dL/dZ, dL/dLR and the output of images 0 and 7 of a B=8 × 128² batch through the latent RRDB-23 + CEM
-  (eval, pre-pad) with the reference-made learned 13×13 kernel, against the reference's autograd
-  (tests/golden/make_golden.py c5grid)."""
+  (eval, pre-pad) against the reference's autograd, with the ×4 kernel of the reference's own KernelGAN
+  post-processing (CEM margins 22 / 88, G at 172²: SURVEY §8's reading; make_golden.py c5grid_kgan) and with the
+  learned 13×13 kernel of the CEM fixtures (margins 13 / 52; make_golden.py c5grid)."""
 import pytest
 
 import grid_parity as GP
@@ -27,8 +28,9 @@ def test_c3_training_step_at_production_grid(gpu_device, precision):
     assert r['ok'], r['fails']
 
 
+@pytest.mark.parametrize('kernel', ['kgan', 'learned13'])
 @pytest.mark.parametrize('precision', ['x3', 'f32'])
-def test_c5_z_gradients_at_production_grid(gpu_device, precision):
-    r = GP.c5_z_gradients(gpu_device, precision)
+def test_c5_z_gradients_at_production_grid(gpu_device, precision, kernel):
+    r = GP.c5_z_gradients(gpu_device, precision, kernel)
     print('\n'.join(r['lines']))
     assert r['ok'], r['fails']

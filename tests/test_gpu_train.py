@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import fixture_input, fixture_params, golden, golden_names, grad_parity, normwise_rel, oracle_grads
+from conftest import fixture_input, fixture_params, fixture_upscale, golden, golden_names, grad_parity, normwise_rel, oracle_grads
 
 import esr_amd
 from esr_amd import CEMnet as C
@@ -18,10 +18,10 @@ from oracle.recipe import seeded_inputs, seeded_params
 pytestmark = pytest.mark.gpu
 
 
-def _model(nb, latent, params, dev):
+def _model(nb, latent, params, dev, sf=4):
     net = esr_amd.RRDBNet(3, 3, 64, nb, latent_input='all_layers_HR_downscaled' if latent else None,
-                          num_latent_channels=3 if latent else 0)
-    model = C.CEMnet(C.Get_CEM_Config(4)).WrapArchitecture_PyTorch(net)
+                          num_latent_channels=3 if latent else 0, upscale=sf)
+    model = C.CEMnet(C.Get_CEM_Config(sf)).WrapArchitecture_PyTorch(net)
     model.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=False)
     return model.to(dev).train(True)
 
@@ -30,12 +30,13 @@ def _model(nb, latent, params, dev):
 def test_training_gradients_vs_reference_golden(gpu_device, name):
     d = golden(name)
     _, params = fixture_params(d)
-    model = _model(int(d['nb']), bool(int(d['latent'])), params, gpu_device)
+    sf = fixture_upscale(d)  # ×4, and ×2 (grad_x2_*: one upconv)
+    model = _model(int(d['nb']), bool(int(d['latent'])), params, gpu_device, sf)
     out = model(fixture_input(d).to(gpu_device))
     assert normwise_rel(out.detach().cpu(), d['out']) < 1e-5
     (out * torch.from_numpy(d['R']).to(gpu_device)).sum().backward()
     exact = oracle_grads(params, d['lr'], d['z'] if 'z' in d.files else None, d['R'], int(d['nb']),
-                         bool(int(d['latent'])), O.cem_design(4), False, torch.float64)
+                         bool(int(d['latent'])), O.cem_design(sf), False, torch.float64, sf=sf)
     named = dict(model.named_parameters())
     for k in [f[len('grad:'):] for f in d.files if f.startswith('grad:')]:
         g = named['generated_image_model.' + k].grad
@@ -173,8 +174,9 @@ def test_z_gradients_vs_reference_golden(gpu_device, name):
     replicate pre-pad adjoint (eval), bilinear ↓4 adjoint, Z slots of every conv, CEM's LR path."""
     d = golden(name)
     _, params = fixture_params(d)
-    net = esr_amd.RRDBNet(3, 3, 64, 1, latent_input='all_layers_HR_downscaled', num_latent_channels=3)
-    cem = C.CEMnet(C.Get_CEM_Config(4), upscale_kernel=d['kernel'] if 'kernel' in d.files else None)
+    sf = fixture_upscale(d)  # ×4, and ×2 (zgrad_x2_*)
+    net = esr_amd.RRDBNet(3, 3, 64, 1, latent_input='all_layers_HR_downscaled', num_latent_channels=3, upscale=sf)
+    cem = C.CEMnet(C.Get_CEM_Config(sf), upscale_kernel=d['kernel'] if 'kernel' in d.files else None)
     model = cem.WrapArchitecture_PyTorch(net)
     model.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=False)
     model = model.to(gpu_device).train(str(d['cem_mode']) == 'train')
@@ -183,12 +185,12 @@ def test_z_gradients_vs_reference_golden(gpu_device, name):
     z = torch.from_numpy(d['z']).to(gpu_device).requires_grad_(True)
     lr = torch.from_numpy(d['lr']).to(gpu_device).requires_grad_(True)
     B, _, h, w = lr.shape
-    out = model(torch.cat([z.view(B, 48, h, w), lr], 1))
+    out = model(torch.cat([z.view(B, 3 * sf * sf, h, w), lr], 1))
     assert normwise_rel(out.detach().cpu(), d['out']) < 1e-5
     (out * torch.from_numpy(d['R']).to(gpu_device)).sum().backward()
-    design = O.cem_design(4, d['kernel'] if 'kernel' in d.files else None)
+    design = O.cem_design(sf, d['kernel'] if 'kernel' in d.files else None)
     exact = oracle_grads(params, d['lr'], d['z'], d['R'], 1, True, design, str(d['cem_mode']) == 'eval',
-                         torch.float64, want_params=False)
+                         torch.float64, want_params=False, sf=sf)
     for g, k in ((z.grad, 'dz'), (lr.grad, 'dlr')):
         ok, msg = grad_parity(g.cpu(), exact[k], d[k])
         assert ok, (k, msg)

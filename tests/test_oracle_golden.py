@@ -73,7 +73,8 @@ def test_oracle_training_gradients(name):
     _, params = fixture_params(d)
     P = {k: v.requires_grad_(True) for k, v in O.strip_prefix(params).items()}
     latent = bool(int(d['latent']))
-    out = O.sr_forward(fixture_input(d), P, int(d['nb']), latent, O.cem_design(4), pre_pad=False)
+    sf = fixture_upscale(d)
+    out = O.sr_forward(fixture_input(d), P, int(d['nb']), latent, O.cem_design(sf), pre_pad=False, sf=sf)
     assert normwise_rel(out.detach().numpy(), d['out']) < 1e-5
     (out * torch.from_numpy(d['R'])).sum().backward()
     for k in [f[len('grad:'):] for f in d.files if f.startswith('grad:')]:
@@ -87,12 +88,13 @@ def test_oracle_z_gradients(name):
     d = golden(name)
     _, params = fixture_params(d)
     P = O.strip_prefix(params)
-    design = O.cem_design(4, d['kernel'] if 'kernel' in d.files else None)
+    sf = fixture_upscale(d)
+    design = O.cem_design(sf, d['kernel'] if 'kernel' in d.files else None)
     z = torch.from_numpy(d['z']).requires_grad_(True)
     lr = torch.from_numpy(d['lr']).requires_grad_(True)
     B, _, h, w = lr.shape
-    out = O.sr_forward(torch.cat([z.view(B, 48, h, w), lr], 1), P, 1, True, design,
-                       pre_pad=str(d['cem_mode']) == 'eval')
+    out = O.sr_forward(torch.cat([z.view(B, 3 * sf * sf, h, w), lr], 1), P, 1, True, design,
+                       pre_pad=str(d['cem_mode']) == 'eval', sf=sf)
     assert normwise_rel(out.detach().numpy(), d['out']) < 1e-5
     (out * torch.from_numpy(d['R'])).sum().backward()
     assert normwise_rel(z.grad.numpy(), d['dz']) < 1e-5
