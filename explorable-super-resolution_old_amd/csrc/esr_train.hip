@@ -1105,7 +1105,7 @@ __global__ void input_adjoint_kernel(const float *d_hr, int hr_cp, int hr_coff, 
         for (int xp = x0; xp <= x1; ++xp) {
             if (d_hr) v += d_hr[(((long long)b * (Hp + 2) + yp + 1) * (Wp + 2) + xp + 1) * hr_cp + hr_coff + c];
             if (d_pl) v += d_pl[(((long long)b * C + c) * Hp + yp) * Wp + xp];
-            if (d_lr) {  // bilinear ↓sf, align_corners=False, sf = 4: mean of the central 2×2 of each 4×4 block
+            if (d_lr) {  // bilinear ↓sf, align_corners=False: sf = 4: mean of the central 2×2 of each 4×4 block; sf = 2: of the 2×2 block
                 const int ry = yp % sf, rx = xp % sf;
                 if ((ry == sf / 2 - 1 || ry == sf / 2) && (rx == sf / 2 - 1 || rx == sf / 2))
                     v += 0.25f * d_lr[(((long long)b * (Hl + 2) + yp / sf + 1) * (Wl + 2) + xp / sf + 1) * lr_cp +
@@ -1276,7 +1276,7 @@ extern "C" int esr_input_adjoint(const float *d_hr, int32_t hr_cp, int32_t hr_co
                                  int32_t Wp, int32_t M, float *out, esr_stream_t stream) {
     if (!out || C <= 0 || B <= 0 || M < 0 || Hp - 2 * M <= 0 || Wp - 2 * M <= 0) return ESR_EINVAL;
     if (d_hr && hr_coff + C > hr_cp) return ESR_EINVAL;
-    if (d_lr && (sf != 4 || Hp % sf || Wp % sf || lr_coff + C > lr_cp)) return ESR_EINVAL;
+    if (d_lr && ((sf != 4 && sf != 2) || Hp % sf || Wp % sf || lr_coff + C > lr_cp)) return ESR_EINVAL;
     const long long n = (long long)B * C * (Hp - 2 * M) * (Wp - 2 * M);
     hipLaunchKernelGGL(input_adjoint_kernel, dim3(nblocks(n)), dim3(NT), 0, (hipStream_t)stream, d_hr, hr_cp, hr_coff,
                        d_lr, lr_cp, lr_coff, sf, d_pl, C, B, Hp, Wp, M, out);

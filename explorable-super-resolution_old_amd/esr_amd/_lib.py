@@ -149,6 +149,11 @@ def bind(path):
             fn = getattr(lib, name)
             fn.argtypes = [c_int]
             fn.restype = c_int
+        # same-box A/B runs of whole benchmarks (tools/gpu_ab_env.sh with ESR_AMD_LIB=exp_lib/libesr_exp.so)
+        if os.environ.get('ESR_X3_NSPLIT') in ('0', '1'):
+            lib.esr_x3_set_nsplit(int(os.environ['ESR_X3_NSPLIT']))
+        if os.environ.get('ESR_X3_KERNEL', '').isdigit():
+            lib.esr_x3_set_kernel(int(os.environ['ESR_X3_KERNEL']))
     return lib
 
 

@@ -220,8 +220,9 @@ int esr_cem_adjoint(const float *g, int32_t planes, int32_t Oy, int32_t Ox, cons
 /* Input gradient of the generator (Z optimisation, Z_optimization.py:574-630): out [B][C][Hp-2M][Wp-2M] (NCHW) =
  *   RepPad_M^T( d_hr  +  d_pl  +  Bilinear↓sf^T(d_lr) )
  * where d_hr is a C-channel slice of a padded NHWC buffer at Hp×Wp, d_pl a planar [B][C][Hp][Wp] array and d_lr a
- * slice of a padded NHWC buffer at (Hp/sf)×(Wp/sf) (bilinear, align_corners=False, sf = 4: each LR pixel is the mean of
- * the central 2×2 of its 4×4 block, architecture.py:153-157); any of the three may be NULL.  RepPad_M is the
+ * slice of a padded NHWC buffer at (Hp/sf)×(Wp/sf) (bilinear, align_corners=False; sf = 4: each LR pixel is the mean
+ * of the central 2×2 of its 4×4 block, sf = 2: of its 2×2 block, architecture.py:153-157); any of the three may be
+ * NULL.  RepPad_M is the
  * ReplicationPad2d(M) of CEM's eval-mode pre-pad (CEMnet.py:170-181; M = 0 for train mode). */
 int esr_input_adjoint(const float *d_hr, int32_t hr_cp, int32_t hr_coff, const float *d_lr, int32_t lr_cp,
                       int32_t lr_coff, int32_t sf, const float *d_pl, int32_t C, int32_t B, int32_t Hp, int32_t Wp,
