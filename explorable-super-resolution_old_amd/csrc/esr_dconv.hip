@@ -32,6 +32,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) const void glob_void;
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -64,6 +66,8 @@ struct FwdParams {
     int T;
     int offy[MAXT], offx[MAXT];
     float *partial;  // split-K (x3 kernel, gridDim.z > 1): [z][M][n_pad] raw sums, reduced by dconv_splitk_reduce
+    const unsigned char *wsx;  // pre-split x3 weights (include/esr_amd.h esr_dconv_fwd_sd w_split) or null
+    const int32_t *wexp;       // their power-of-two exponent E (the stored values are w·2^E)
     int s2c, s2pad, s2g, s2sh;  // > 0: space-to-depth source (src_quad), channel group s2g = 2^s2sh (s2sh < 0: not
     int d2c, d2pad, d2g, d2sh;  // a power of two); d2*: depth-to-space output (put_out); 0: plain
 };
@@ -607,9 +611,15 @@ __global__ __launch_bounds__(NTH, 2) void dconv_fwd_x3_kernel(FwdParams p) {
 // per chunk), 2 = no fragment reads / MFMAs, 4 = the halo window staged for the first chunk only
 // CW = 16: an M-tile is 2 rows × 16 columns (stride-1 sources only), for grids whose width 32-column tiles would cover
 // with > 30 % waste (the 38-wide conv2_1 / fc8 layers at config 3); a tile is then 2·TY rows × 16 columns.
-template <int WM, int WN, int NP, int NBX = NB, int DBG = 0, int OCC = 2, int CW = 32>
+// PB (x3 only): the weights come pre-split (esr_dconv_fwd_sd w_split: hi/lo f16 at one power-of-two scale 2^E per
+// tensor, each 128-byte (t, chunk, n) row's 16-B slots XOR-swizzled by (n >> 1) & 7 so that a linear copy gives a
+// conflict-free LDS image) and are LDS-DMA'd into two slots, the next step's under the current step's MFMAs: no weight
+// loads through registers, no per-step max / split / rescale, one barrier per step instead of two.
+template <int WM, int WN, int NP, int NBX = NB, int DBG = 0, int OCC = 2, int CW = 32, bool PB = false>
 __global__ __launch_bounds__(NTH, OCC) void dconv_fwd_halo_x_kernel(FwdParams p, HaloParams h) {
     constexpr int TY = WM * WN * 128 / NBX, MWV = TY / WM, XPn = XPitch<NP>::v, BX_IT = NBX * KC / 4 / NTH;
+    static_assert(!PB || (NP == 2 && DBG == 0), "pre-split weights: x3");
+    constexpr int RBB = 128, SLOT = NBX * RBB;  // PB: bytes per weight row / per step's slab
     constexpr int RPM = 32 / CW;  // output rows per M-tile
     static_assert((TY / WM) * (NBX / 32 / WN) == NTH / 64, "waves along M x waves along N = 4");
     extern __shared__ __attribute__((aligned(16))) unsigned char xlds[];
@@ -722,11 +732,75 @@ __global__ __launch_bounds__(NTH, OCC) void dconv_fwd_halo_x_kernel(FwdParams p,
             for (int r = 0; r < 16; ++r) acc[i][k][r] = 0.f;
     int ea = 0, eb = 0;
 
-    if (nsteps > 0 && !(DBG & 1)) {
+    if constexpr (PB) {
+        eb = *p.wexp;
+        auto dma_b = [&](int step, int slot) {  // the step's NBX weight rows: one linear copy
+            const int j = c_begin + step / p.T, t = step - (step / p.T) * p.T;
+            const unsigned char *src = p.wsx + ((long long)(t * p.nck + j) * p.n_pad + n0) * RBB + 16 * lane;
+#pragma unroll
+            for (int q = wave; q < SLOT / 1024; q += NTH / 64)
+                __builtin_amdgcn_global_load_lds((glob_void *)(src + q * 1024),
+                                                 (lds_void *)(s_b + slot * SLOT + q * 1024), 16, 0, 0);
+        };
+        if (nsteps > 0) dma_b(0, 0);
+        for (int step = 0; step < nsteps; ++step) {
+            const int t = step % p.T;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's copy of the step's weights landed
+            __syncthreads();  // every copy landed; every wave is done with step - 1 (its slot, and the window at t 0)
+            if (t == 0) {
+                const int ea2 = stage_a(c_begin + step / p.T, ea);  // (contains a barrier)
+                __syncthreads();                                    // the split window is in place
+                if (ea2 != ea) {
+#pragma unroll
+                    for (int i = 0; i < WM; ++i)
+#pragma unroll
+                        for (int k = 0; k < WN; ++k)
+#pragma unroll
+                            for (int r = 0; r < 16; ++r) acc[i][k][r] = ldexpf(acc[i][k][r], ea2 - ea);
+                    ea = ea2;
+                }
+            }
+            if (step + 1 < nsteps) dma_b(step + 1, (step + 1) & 1);  // lands under this step's MFMAs
+            const int dy = p.offy[t] - h.oymin, dx = p.offx[t] - h.oxmin;
+            const int mc = ml % CW, mr = ml / CW;
+            const int col = (h.npar == 1) ? mc + dx : (dx & 1) * h.IXp + mc + (dx >> 1);
+            const unsigned char *a_base[WM];
+#pragma unroll
+            for (int i = 0; i < WM; ++i) {
+                const int ty = wm * WM + i;
+                a_base[i] = s_a + ((p.smy * (RPM * ty + mr) + dy) * h.IXt + col) * XPn + 16 * hl;
+            }
+            const unsigned char *bslot = s_b + (step & 1) * SLOT;
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                f16x8 ah[WM], al[WM];
+#pragma unroll
+                for (int i = 0; i < WM; ++i) {
+                    ah[i] = *reinterpret_cast<const f16x8 *>(a_base[i] + 32 * s2);
+                    al[i] = *reinterpret_cast<const f16x8 *>(a_base[i] + 64 + 32 * s2);
+                }
+#pragma unroll
+                for (int k = 0; k < WN; ++k) {
+                    const int n = (wn * WN + k) * 32 + ml, sw = (n >> 1) & 7;
+                    const unsigned char *brow = bslot + n * RBB;
+                    const f16x8 bh = *reinterpret_cast<const f16x8 *>(brow + (((2 * s2 + hl) ^ sw) << 4));
+                    const f16x8 bl = *reinterpret_cast<const f16x8 *>(brow + (((4 + 2 * s2 + hl) ^ sw) << 4));
+#pragma unroll
+                    for (int i = 0; i < WM; ++i) {
+                        acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh, acc[i][k], 0, 0, 0);
+                        acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl, acc[i][k], 0, 0, 0);
+                        acc[i][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh, acc[i][k], 0, 0, 0);
+                    }
+                }
+            }
+        }
+    }
+
+    if (!PB && nsteps > 0 && !(DBG & 1)) {
         load_b(0);
         publish_b(0);
     }
-    for (int step = 0; step < nsteps; ++step) {
+    for (int step = 0; step < (PB ? 0 : nsteps); ++step) {
         const int t = step % p.T;
         if (!(DBG & 1) || t == 0) __syncthreads();  // the previous step's fragment reads are done; weight max published
         int ea2 = ea;
@@ -1435,7 +1509,7 @@ int halo_cols(int smy, int smx, int T, int MW, bool sd, int np) {
 // Halo tiling of an esr_dconv_fwd launch with `pitch` LDS bytes per staged pixel row (144: fp32 / x3, 208: x6):
 // false if the gather kernel has to run it (stride > 2, or a halo that does not fit in LDS even at 2-row tiles).
 bool halo_plan(int MH, int MW, int smy, int smx, int T, const int32_t *offy, const int32_t *offx, HaloParams &h,
-               int &lds, int pitch = PS * 4, int nbx = NB, int cw = 32) {
+               int &lds, int pitch = PS * 4, int nbx = NB, int cw = 32, bool pb = false) {
     if (smy < 1 || smy > 2 || smx < 1 || smx > 2 || (cw == 16 && smx != 1)) return false;
     const int rpm = 32 / cw;  // output rows per M-tile
     int ymin = offy[0], ymax = offy[0], xmin = offx[0], xmax = offx[0];
@@ -1448,7 +1522,7 @@ bool halo_plan(int MH, int MW, int smy, int smx, int T, const int32_t *offy, con
     h.npar = smx;
     h.IXp = smx == 1 ? cw + (xmax - xmin) : 32 + ((xmax - xmin) >> 1);
     h.IXt = h.npar * h.IXp;
-    const int b_bytes = nbx * pitch;
+    const int b_bytes = pb ? 2 * nbx * 128 : nbx * pitch;  // pb: two slots of pre-split weight rows
     for (int pass = 0; pass < 2; ++pass) {
         const int budget = pass == 0 ? HALO_LDS_2PER_CU : HALO_LDS_MAX;
         for (int ty = 8; ty >= 2; ty >>= 1) {
@@ -1546,11 +1620,27 @@ void launch_halo_f32(const FwdParams &p, const HaloParams &h, dim3 grid, int lds
     hipLaunchKernelGGL((dconv_fwd_halo_kernel<WM, WN>), grid, dim3(NTH), lds, st, p, h);
 }
 
-template <int WM, int WN, int NP, int NBX = NB, int DBG = 0, int OCC = 2, int CW = 32>
+template <int WM, int WN, int NP, int NBX = NB, int DBG = 0, int OCC = 2, int CW = 32, bool PB = false>
 void launch_halo_x1(const FwdParams &p, const HaloParams &h, dim3 grid, int lds, hipStream_t st) {
     static bool attr = false;
-    allow_full_lds(dconv_fwd_halo_x_kernel<WM, WN, NP, NBX, DBG, OCC, CW>, attr);
-    hipLaunchKernelGGL((dconv_fwd_halo_x_kernel<WM, WN, NP, NBX, DBG, OCC, CW>), grid, dim3(NTH), lds, st, p, h);
+    allow_full_lds(dconv_fwd_halo_x_kernel<WM, WN, NP, NBX, DBG, OCC, CW, PB>, attr);
+    hipLaunchKernelGGL((dconv_fwd_halo_x_kernel<WM, WN, NP, NBX, DBG, OCC, CW, PB>), grid, dim3(NTH), lds, st, p, h);
+}
+
+// the pre-split-weight (PB) forms of launch_halo_x's x3 choices
+template <int WM, int WN, int NBX = NB>
+void launch_halo_pb(const FwdParams &p, const HaloParams &h, dim3 grid, int lds, hipStream_t st) {
+    if constexpr (NBX == 64) {
+        if (h.cw == 16) {
+            if (g_dconv_occ3 && lds <= 160 * 1024 / 3)
+                return launch_halo_x1<WM, WN, 2, NBX, 0, 3, 16, true>(p, h, grid, lds, st);
+            return launch_halo_x1<WM, WN, 2, NBX, 0, 2, 16, true>(p, h, grid, lds, st);
+        }
+    }
+    if constexpr (NBX == 64 && WM == 2) {
+        if (g_dconv_occ3 && lds <= 160 * 1024 / 3) return launch_halo_x1<WM, WN, 2, NBX, 0, 3, 32, true>(p, h, grid, lds, st);
+    }
+    launch_halo_x1<WM, WN, 2, NBX, 0, 2, 32, true>(p, h, grid, lds, st);
 }
 
 template <int WM, int WN, int NP, int NBX = NB>
@@ -1606,9 +1696,11 @@ extern "C" int esr_dconv_fwd_sd(const float *src, int32_t B, int32_t Hs, int32_t
                                 int32_t Ho, int32_t Wo, int32_t out_pitch, int32_t n, int32_t MH, int32_t MW,
                                 int32_t omy, int32_t oay, int32_t omx, int32_t oax, int32_t smy, int32_t smx, int32_t T,
                                 const int32_t *offy, const int32_t *offx, int32_t ksplit, float *partial, int32_t s2d_c,
-                                int32_t s2d_pad, int32_t d2s_c, int32_t d2s_pad, int32_t prec, esr_stream_t stream) {
+                                int32_t s2d_pad, int32_t d2s_c, int32_t d2s_pad, int32_t prec, const void *w_split,
+                                const int32_t *w_exp, esr_stream_t stream) {
     DPrec dp;
     if (!src || !w_packed || !out || !offy || !offx || !decode_prec(prec, dp)) return ESR_EINVAL;
+    if ((w_split == nullptr) != (w_exp == nullptr) || (w_split && ((uintptr_t)w_split & 15))) return ESR_EINVAL;
     if (ksplit < 1 || (ksplit > 1 && (!partial || ksplit > T * nck))) return ESR_EINVAL;
     if (s2d_c < 0 || d2s_c < 0 || s2d_pad < 0 || d2s_pad < 0) return ESR_EINVAL;
     const int src_c = s2d_c ? s2d_c : kc, out_c = d2s_c ? d2s_c : n;  // real channels per source / output pixel
@@ -1642,14 +1734,17 @@ extern "C" int esr_dconv_fwd_sd(const float *src, int32_t B, int32_t Hs, int32_t
     p.T = T;
     for (int t = 0; t < T; ++t) { p.offy[t] = offy[t]; p.offx[t] = offx[t]; }
     p.partial = partial;
+    p.wsx = static_cast<const unsigned char *>(w_split);
+    p.wexp = w_exp;
     const long long M = (long long)B * MH * MW;
     const long long gx = (M + MT - 1) / MT;
     if (M + MT >= 0x7fffffffLL) return ESR_EINVAL;  // the kernels index output pixels in 32 bits
     HaloParams h;
     int lds = 0;
     const int np = dp.np;
+    const bool pb = np == 2 && w_split != nullptr;  // x3 halo launches take the pre-split weights when given
     const int cwh = halo_cols(smy, smx, T, MW, sd, np);
-    if (cwh && halo_plan(MH, MW, smy, smx, T, offy, offx, h, lds, np == 3 ? XPitch<3>::v : PS * 4, NB, cwh)) {
+    if (cwh && halo_plan(MH, MW, smy, smx, T, offy, offx, h, lds, np == 3 ? XPitch<3>::v : PS * 4, NB, cwh, pb)) {
         if (ksplit > nck) return ESR_EINVAL;  // the halo kernels split the channel chunks
         const long long hx = (long long)B * h.tiles_x * h.tiles_y;
         if (hx > 0x7fffffff) return ESR_EINVAL;
@@ -1665,9 +1760,15 @@ extern "C" int esr_dconv_fwd_sd(const float *src, int32_t B, int32_t Hs, int32_t
             HaloParams h2;
             int lds2 = 0;
             if (h.cw == 32 && dp.nb != 64 && ksplit == 1 && n_pad % 128 == 0 && h.TY == 8 && hx * (n_pad / 128) >= 512 &&
-                halo_plan(MH, MW, smy, smx, T, offy, offx, h2, lds2, PS * 4, 128) && h2.TY == 8 &&
+                halo_plan(MH, MW, smy, smx, T, offy, offx, h2, lds2, PS * 4, 128, 32, pb) && h2.TY == 8 &&
                 lds2 <= HALO_LDS_2PER_CU) {
-                launch_halo_x<2, 4, 2, 128>(p, h2, dim3((unsigned)hx, (unsigned)(n_pad / 128), 1), lds2, st);
+                const dim3 g2((unsigned)hx, (unsigned)(n_pad / 128), 1);
+                if (pb) launch_halo_pb<2, 4, 128>(p, h2, g2, lds2, st);
+                else launch_halo_x<2, 4, 2, 128>(p, h2, g2, lds2, st);
+            } else if (pb) {
+                if (h.TY == 8) launch_halo_pb<2, 2>(p, h, hgrid, lds, st);
+                else if (h.TY == 4) launch_halo_pb<1, 2>(p, h, hgrid, lds, st);
+                else launch_halo_pb<1, 1>(p, h, hgrid, lds, st);
             } else if (h.TY == 8) launch_halo_x<2, 2, 2>(p, h, hgrid, lds, st);
             else if (h.TY == 4) launch_halo_x<1, 2, 2>(p, h, hgrid, lds, st);
             else launch_halo_x<1, 1, 2>(p, h, hgrid, lds, st);
@@ -1710,7 +1811,8 @@ extern "C" int esr_dconv_fwd_sk(const float *src, int32_t B, int32_t Hs, int32_t
                                 const int32_t *offy, const int32_t *offx, int32_t ksplit, float *partial,
                                 int32_t prec, esr_stream_t stream) {
     return esr_dconv_fwd_sd(src, B, Hs, Ws, src_pitch, kc, w_packed, nck, n_pad, bias, out, Ho, Wo, out_pitch, n, MH,
-                            MW, omy, oay, omx, oax, smy, smx, T, offy, offx, ksplit, partial, 0, 0, 0, 0, prec, stream);
+                            MW, omy, oay, omx, oax, smy, smx, T, offy, offx, ksplit, partial, 0, 0, 0, 0, prec, nullptr,
+                            nullptr, stream);
 }
 
 extern "C" int esr_dconv_fwd(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t src_pitch, int32_t kc,

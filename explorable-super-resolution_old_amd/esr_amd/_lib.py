@@ -8,7 +8,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('ESR_AMD_LIB', os.path.join(_HERE, 'libesr_amd.so'))
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 c_int = ctypes.c_int32
 c_float = ctypes.c_float
@@ -94,7 +94,7 @@ _SIGNATURES = {
     'esr_dconv_fwd_sd': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
                          c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                          ctypes.POINTER(c_int), ctypes.POINTER(c_int), c_int, c_void_p, c_int, c_int, c_int, c_int,
-                         c_int, c_void_p],
+                         c_int, c_void_p, c_void_p, c_void_p],
     'esr_dconv_uses_halo': [c_int, c_int, c_int, c_int, c_int, c_int],
     'esr_dconv_fwd_splits_sd': [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_int),
                                 ctypes.POINTER(c_int), c_int, c_int],

@@ -37,6 +37,9 @@ if os.environ.get('ESR_DCONV_NB128', '1') == '0':
 # space-to-depth source / into the depth-to-space gradient (esr_dconv_fwd_sd, one launch each); '0' = the direct
 # stride-2 gather and one launch per phase class (A/B)
 S2D = os.environ.get('ESR_DCONV_S2D', '1') != '0'
+# x3 halo-tile launches take their weights pre-split (one scale per tensor, LDS-DMA'd: no per-step max / split in the
+# kernel); '0' = the kernel splits the fp32 weight slab per K step (A/B)
+PRESPLIT = os.environ.get('ESR_DCONV_PRESPLIT', '1') != '0'
 # conv bias gradients (Σ over pixels of the output gradient) accumulated in float64 ('0': float32 sums)
 BIAS_F64 = os.environ.get('ESR_DCONV_BIAS_F64', '0') != '0'
 
@@ -75,6 +78,37 @@ def out_size(n, k, s, p):
     return (n + 2 * p - k) // s + 1
 
 
+class _Packed:
+    """Packed weights of one launch: wp [T][nck][n_pad][32] fp32 (esr_dconv_fwd's layout) and, built on first use by an
+    x3 launch, their pre-split form for the halo-tile kernel (include/esr_amd.h esr_dconv_fwd_sd w_split / w_exp)."""
+    __slots__ = ('wp', 'nck', 'n_pad', '_split')
+
+    def __init__(self, wp, nck, n_pad):
+        self.wp, self.nck, self.n_pad, self._split = wp, nck, n_pad, None
+
+    def __iter__(self):
+        return iter((self.wp, self.nck, self.n_pad))
+
+    def split(self):
+        """(f16 rows [T][nck][n_pad][8 slots][8], int32 [1] exponent E): v = wp·2^E with one power of two per tensor
+        (max |v| in [2^14, 2^15)), hi = f16(v), lo = f16(v - hi); logical slot l = piece·4 + k (8 channels each) stored
+        at position l ^ ((n >> 1) & 7).  Device ops only (no host sync)."""
+        if self._split is None:
+            wp = self.wp
+            T, nck, n_pad, _ = wp.shape
+            amax = wp.abs().amax()
+            e = torch.where(amax > 0, 14.0 - torch.floor(torch.log2(amax)), torch.zeros_like(amax))
+            v = wp * torch.exp2(e)
+            hi = v.half()
+            lo = (v - hi.float()).half()
+            logical = torch.stack([hi, lo], 3).view(T, nck, n_pad, 8, 8)
+            n = torch.arange(n_pad, device=wp.device)
+            idx = (torch.arange(8, device=wp.device).view(1, 8) ^ ((n.view(-1, 1) >> 1) & 7))
+            phys = torch.gather(logical, 3, idx.view(1, 1, n_pad, 8, 1).expand(T, nck, n_pad, 8, 8))
+            self._split = (phys.contiguous(), e.to(torch.int32).view(1))
+        return self._split
+
+
 def _pack(wt, n_out):
     """wt [T][K][N] -> packed [T][nck][n_pad][32] (esr_dconv_fwd's weight layout)."""
     T, K, N = wt.shape
@@ -82,7 +116,7 @@ def _pack(wt, n_out):
     n_pad = 64 * ((n_out + 63) // 64)
     buf = wt.new_zeros(T, nck * 32, n_pad)
     buf[:, :K, :N] = wt
-    return buf.view(T, nck, 32, n_pad).permute(0, 1, 3, 2).contiguous(), nck, n_pad
+    return _Packed(buf.view(T, nck, 32, n_pad).permute(0, 1, 3, 2).contiguous(), nck, n_pad)
 
 
 def _packed(w, key, make):
@@ -119,6 +153,7 @@ def _gather(src, packed, bias, out, MH, MW, omy, oay, omx, oax, smy, smx, offy, 
     n = 4 * N if d2s_pad is not None else N
     lib = _lib.load()
     mode = _mode(prec)
+    wsx, wexp = packed.split() if mode in (1, 2) and PRESPLIT else (None, None)
     oy, ox = _i32(offy), _i32(offx)
     sd = s2d_pad is not None or d2s_pad is not None
     # split-K where the grid would fill few CUs and K is long (the 8x8 pseudo-FC layer); the library says how many
@@ -131,7 +166,9 @@ def _gather(src, packed, bias, out, MH, MW, omy, oay, omx, oax, smy, smx, offy, 
                                     omy, oay, omx, oax, smy, smx, len(offy), oy, ox, ks,
                                     None if part is None else part.data_ptr(),
                                     C if s2d_pad is not None else 0, s2d_pad or 0,
-                                    N if d2s_pad is not None else 0, d2s_pad or 0, mode, _stream(src)),
+                                    N if d2s_pad is not None else 0, d2s_pad or 0, mode,
+                                    None if wsx is None else wsx.data_ptr(), None if wexp is None else wexp.data_ptr(),
+                                    _stream(src)),
                'esr_dconv_fwd')
 
 

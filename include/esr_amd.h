@@ -288,13 +288,20 @@ int esr_dconv_fwd_splits(int32_t B, int32_t MH, int32_t MW, int32_t n_out, int32
  *     (dropped outside); omy = omx = 1, oay = oax = 0, no bias.  With src = dL/dy, offy = -a, offx = -b and
  *     W[(a, b)][co][v(py, px, c)] = w[co][c][2a + py][2b + px] over MH × MW = ((H-1+pad)/2 + 1) × ((W-1+pad)/2 + 1)
  *     this is the transposed conv in one launch (replaces the per-phase-class calls of esr_dconv_fwd).
+ * w_split / w_exp (both NULL, or both given; prec 1 / 2): the weights pre-split for the x3 halo-tile kernel — the
+ *   values of w_packed times 2^E (E = *w_exp, one power of two per tensor, |w|·2^E < 2^15) as f16 hi and lo =
+ *   f16(v - hi): per (tap t, chunk j, output channel n) one 128-byte row of eight 16-byte slots, logical slot l =
+ *   piece·4 + k (piece 0 hi, 1 lo; k-th group of 8 channels of the chunk) stored at position l ^ ((n >> 1) & 7),
+ *   rows [T][nck][n_pad].  Halo-tile launches then LDS-DMA them (no per-step max, split or register staging);
+ *   other launches use w_packed.
  * Replaces: the D's 4×4 stride-2 conv_block convs (architecture.py:232-250, block.py:129-156) and their gradients. */
 int esr_dconv_fwd_sd(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t src_pitch, int32_t kc,
                      const float *w_packed, int32_t nck, int32_t n_pad, const float *bias, float *out, int32_t Ho,
                      int32_t Wo, int32_t out_pitch, int32_t n, int32_t MH, int32_t MW, int32_t omy, int32_t oay,
                      int32_t omx, int32_t oax, int32_t smy, int32_t smx, int32_t T, const int32_t *offy,
                      const int32_t *offx, int32_t ksplit, float *partial, int32_t s2d_c, int32_t s2d_pad,
-                     int32_t d2s_c, int32_t d2s_pad, int32_t prec, esr_stream_t stream);
+                     int32_t d2s_c, int32_t d2s_pad, int32_t prec, const void *w_split, const int32_t *w_exp,
+                     esr_stream_t stream);
 /* 1 if an esr_dconv_fwd(_sd) launch of this geometry runs on the halo-tile kernel (sd != 0: an esr_dconv_fwd_sd
  * launch), 0 if on the per-tap gather kernel.  The host takes the space-to-depth forward only where it is halo-tiled
  * (on the gather kernel it is no faster than the direct stride-2 gather: profiles/r3_dconv_s2d_ab.txt). */

@@ -81,3 +81,27 @@ def test_im2col_function_matches_autograd_through_cat_and_pad():
         b, = torch.autograd.grad((gr * v).sum(), g)
         assert (a - b).abs().max() < 1e-12
         assert torch.autograd.gradgradcheck(lambda t: dconv._Im2ColFn.apply(t, k, p), (x,))
+
+
+def test_presplit_weight_layout():
+    """_Packed.split(): the x3 halo kernel's pre-split weights (include/esr_amd.h esr_dconv_fwd_sd w_split): rows of
+    eight 16-byte slots, logical slot piece·4 + k at position ^ ((n >> 1) & 7); hi + lo = w·2^E to f16-pair accuracy
+    with one power of two E per tensor putting max |w|·2^E in [2^14, 2^15)."""
+    import torch
+    g = torch.Generator().manual_seed(3)
+    wt = torch.randn(9, 70, 100, generator=g) * 0.03
+    pk = dconv._pack(wt, 100)
+    wp, nck, n_pad = pk
+    rows, e = pk.split()
+    E = int(e.item())
+    assert 2 ** 14 <= float(wp.abs().max()) * 2 ** E < 2 ** 15
+    assert rows.dtype == torch.float16 and rows.shape == (9, nck, n_pad, 8, 8)
+    n = torch.arange(n_pad)
+    idx = torch.arange(8).view(1, 8) ^ ((n.view(-1, 1) >> 1) & 7)   # position p holds logical slot idx[n, p]
+    logical = torch.empty_like(rows)
+    logical.scatter_(3, idx.view(1, 1, n_pad, 8, 1).expand_as(rows), rows)
+    hi = logical[..., 0:4, :].reshape(9, nck, n_pad, 32).float()
+    lo = logical[..., 4:8, :].reshape(9, nck, n_pad, 32).float()
+    v = wp * 2.0 ** E
+    assert torch.equal(hi, v.half().float())
+    assert float((hi + lo - v).abs().max()) <= 2.0 ** -9  # (|v| < 2^15: the pair carries ~22 bits)
