@@ -17,12 +17,11 @@
 extern "C" {
 #endif
 
-/* esr_conv3x3_fwd_x3 / esr_upconv2x_phase_fwd_x3 kernel (0..66).  All non-diagnostic variants are bitwise identical.
+/* esr_conv3x3_fwd_x3 / esr_upconv2x_phase_fwd_x3 kernel (0..64).  All non-diagnostic variants are bitwise identical.
  * 0 / 1 / 63 = automatic (the product dispatch); 24 = the round-1 automatic choice (classic kernel only: 8-row at three
  *   per CU or 16-row at two; 25 / 26 force one); 50 = column-tile kernel (16 columns); 60 = column tiles with the
  *   weights read into registers from global memory; 61 = 8 waves of 2 columns; 62 = weights copied to registers per
- *   chunk; 64 = 12-column tiles at three workgroups per CU; 65 / 66 = N <= 32 in 24- / 20-column tiles of 4-column
- *   waves (6 / 5 waves) at two workgroups per CU (fewer staged bytes per output than 12-column tiles);
+ *   chunk; 64 = 12-column tiles at three workgroups per CU;
  * 22 = classic with two LDS stages and one workgroup per CU; 23 = cout > 32 with 8-row tiles at two workgroups per CU;
  *   21 = prefetch distance 1; 20 = compiler-scheduled fragment reads; 27 / 28 = register epilogue (16- / 8-row);
  * 2 = ring kernel; 15 = ring with staggered DMA issue; 18 = ring with compiler-scheduled reads; 16 / 17 = persistent

@@ -1332,8 +1332,7 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
     // tiles to look better by rounds (≥ 3 full rounds): HR_conv1 at 592² (1115 -> 1060 us per config-2 launch)
     const int tiles12 = ((W + 11) / 12) * ((B * (H + 2) - 2 + 31) / 32);
     const bool x3c_pays = taps_side == 2 || (taps_side == 3 && (cout > 32 || !row8_pays || tiles12 >= 9 * n_cu));
-    if ((g_x3_kernel >= 50 && g_x3_kernel <= 62) || (g_x3_kernel >= 64 && g_x3_kernel <= 66) ||
-        ((g_x3_kernel == 1 || g_x3_kernel == 63) && x3c_pays)) {
+    if ((g_x3_kernel >= 50 && g_x3_kernel <= 62) || g_x3_kernel == 64 || ((g_x3_kernel == 1 || g_x3_kernel == 63) && x3c_pays)) {
         X3cParams c;
         c.in = p.in; c.B = B; c.H = H; c.W = W; c.in_cp = in_cp; c.cin = cin; c.w = p.w; c.bias = bias;
         c.w_scale_inv = p.w_scale_inv; c.cout = cout; c.tap_y0 = ty0; c.tap_x0 = tx0; c.tiles_x = c.tiles_y = 0;
@@ -1366,8 +1365,6 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
         if (g_x3_kernel == 60) return x3c_launch(c, taps_side, stream, 16);
         if (g_x3_kernel == 61) return x3c_launch(c, taps_side, stream, 32);
         if (g_x3_kernel == 62) return x3c_launch(c, taps_side, stream, 64);
-        if (g_x3_kernel == 65) return x3c_launch(c, taps_side, stream, 24);
-        if (g_x3_kernel == 66) return x3c_launch(c, taps_side, stream, 20);
 #endif
         // N = 32 3×3 convs (the RDB growth convs): 12-column tiles of four 3-column waves at three workgroups per CU
         // (variant 64; 0.9 % per config-2 step over the 16-column tiles of variant 50, bitwise equal)

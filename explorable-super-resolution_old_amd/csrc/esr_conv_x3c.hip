@@ -764,19 +764,6 @@ int x3c_launch(const X3cParams &p0, int taps_side, hipStream_t stream, int dbg) 
         return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
     }
 #ifdef ESR_X3_EXPERIMENTS
-    if (dbg == 20 || dbg == 24) {  // N = 32: 20- / 24-column tiles of 4-column waves (5 / 6 waves), two per CU
-        if (n64) return x3c_launch(p0, taps_side, stream, 0);
-        p.tiles_x = (p.W + dbg - 1) / dbg;
-        const dim3 gridw((unsigned)(p.tiles_x * p.tiles_y)), blockw(64 * (dbg / 4));
-        if (dbg == 24) {
-            if (taps_side == 3) hipLaunchKernelGGL((conv_x3c_kernel<1, 3, 0, false, 4, false, 24, 2>), gridw, blockw, 0, stream, p);
-            else hipLaunchKernelGGL((conv_x3c_kernel<1, 2, 0, false, 4, false, 24, 2>), gridw, blockw, 0, stream, p);
-        } else {
-            if (taps_side == 3) hipLaunchKernelGGL((conv_x3c_kernel<1, 3, 0, false, 4, false, 20, 2>), gridw, blockw, 0, stream, p);
-            else hipLaunchKernelGGL((conv_x3c_kernel<1, 2, 0, false, 4, false, 20, 2>), gridw, blockw, 0, stream, p);
-        }
-        return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
-    }
     if (dbg == 16) {  // register-B form
         if (taps_side == 3) {
             if (n64) hipLaunchKernelGGL((conv_x3c_kernel<2, 3, 0, true>), grid, block, 0, stream, p);
