@@ -40,6 +40,23 @@ def make_opt(args):
     }
 
 
+def observe():
+    """Counters that explain a timed region (record the delta of two calls): x3 overflow reruns, how the training
+    passes ran (eager / graph capture / replay), the caching allocator's device allocations and retries, and Python's
+    generation-2 garbage collections."""
+    import gc
+    from esr_amd import engine, train_engine
+    ms = torch.cuda.memory_stats()
+    return {'overflow_reruns': engine.OVERFLOW_RERUNS, 'act_scale_reductions': engine.ACT_SCALE_REDUCTIONS,
+            **{'graph_' + k: v for k, v in train_engine.GRAPH_COUNTS.items()},
+            'device_allocs': ms.get('num_device_alloc', 0), 'device_frees': ms.get('num_device_free', 0),
+            'alloc_retries': ms.get('num_alloc_retries', 0), 'gc_gen2': gc.get_stats()[2]['collections']}
+
+
+def observed(a, b):
+    return {k: b[k] - a[k] for k in a}
+
+
 def leg_args(**kw):
     """Default arguments of this benchmark (BASELINE config 3 per GPU), for callers such as bench.py."""
     # warmup 4: the caching allocator still returns memory to the device (hipFree, ~200 frees) in calls 3-4
@@ -69,6 +86,7 @@ def run(args, dev, world, rank):
         model.feed_data(data)
         model.optimize_parameters()
     reruns1, a1 = engine.OVERFLOW_RERUNS, engine.act_scale(rrdb)
+    obs0 = observe()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -83,6 +101,7 @@ def run(args, dev, world, rank):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     step_ms = [round((b - a) * 1e3, 2) for a, b in zip([t0] + stamps[:-1], stamps)]
+    obs = observed(obs0, observe())
     if world > 1:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -107,7 +126,8 @@ def run(args, dev, world, rank):
             'last_losses': {k: v[-1][1] for k, v in model.log_dict.items() if v},
             'step_ms': step_ms,
             'overflow_reruns': {'warmup': reruns1 - reruns0, 'timed': engine.OVERFLOW_RERUNS - reruns1},
-            'act_scale': {'before_warmup': a0, 'before_timed': a1, 'after_timed': engine.act_scale(rrdb)}}
+            'act_scale': {'before_warmup': a0, 'before_timed': a1, 'after_timed': engine.act_scale(rrdb)},
+            'timed_region': obs}
 
 
 def main():

@@ -16,6 +16,7 @@ import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, 'explorable-super-resolution_old_amd'))
+sys.path.insert(0, REPO)
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -83,6 +84,8 @@ def run(args, dev, world, rank):
     reruns1 = engine.OVERFLOW_RERUNS
     a1 = engine.act_scale(rrdb)
     zo.max_iters = args.steps
+    from bench_train import observe, observed
+    obs0 = observe()
     stamps = []
     # each iteration ends with its overflow-flag read (a device sync), so these are per-iteration wall times
     zo.on_iteration = lambda _: stamps.append(time.perf_counter())
@@ -96,6 +99,7 @@ def run(args, dev, world, rank):
     dt = time.perf_counter() - t0
     zo.on_iteration = None
     iter_ms = [round((b - a) * 1e3, 2) for a, b in zip([t0] + stamps[:-1], stamps)]
+    obs = observed(obs0, observe())
     if world > 1:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -121,7 +125,8 @@ def run(args, dev, world, rank):
             'final_loss': zo.loss_values[-1],
             'iter_ms': iter_ms,
             'overflow_reruns': {'warmup': reruns1 - reruns0, 'timed': engine.OVERFLOW_RERUNS - reruns1},
-            'act_scale': {'before_warmup': a0, 'before_timed': a1, 'after_timed': engine.act_scale(rrdb)}}
+            'act_scale': {'before_warmup': a0, 'before_timed': a1, 'after_timed': engine.act_scale(rrdb)},
+            'timed_region': obs}
 
 
 def main():

@@ -1678,6 +1678,63 @@ void launch_halo_x(const FwdParams &p, const HaloParams &h, dim3 grid, int lds, 
 
 
 
+// ---- pre-split x3 weights (esr_dconv_presplit) -------------------------------------------------------------------------
+constexpr int PS_BLOCKS = 512;  // partial-max blocks
+
+__global__ __launch_bounds__(NTH) void presplit_amax_kernel(const float *w, long long n, float *partial) {
+    __shared__ float red[NTH / 64];
+    float m = 0.f;
+    for (long long i = (long long)blockIdx.x * NTH + threadIdx.x; i < n; i += (long long)gridDim.x * NTH)
+        m = fmaxf(m, fabsf(w[i]));
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float mm = 0.f;
+#pragma unroll
+        for (int k = 0; k < NTH / 64; ++k) mm = fmaxf(mm, red[k]);
+        partial[blockIdx.x] = mm;
+    }
+}
+
+// One 16-byte output slot per thread: row r = (t, j, n), physical slot p holds logical slot l = p ^ ((n >> 1) & 7) =
+// piece·4 + k: channels 8k..8k+7 of the row, hi (piece 0) or lo (piece 1) of w·2^E (include/esr_amd.h w_split).
+__global__ __launch_bounds__(NTH) void presplit_apply_kernel(const float *wp, long long rows, int n_pad,
+                                                             const float *partial, int nparts, _Float16 *out,
+                                                             int32_t *wexp) {
+    __shared__ float s_e;
+    if (threadIdx.x < 64) {  // the tensor's max |w| from the partials (every block, same order: same result)
+        float m = 0.f;
+        for (int i = threadIdx.x; i < nparts; i += 64) m = fmaxf(m, partial[i]);
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+        if (threadIdx.x == 0) {
+            int e = 0;
+            if (m > 0.f) (void)frexpf(m, &e);  // m = f·2^e, f in [0.5, 1): E = 15 - e puts m·2^E in [2^14, 2^15)
+            const int E = m > 0.f ? 15 - e : 0;
+            s_e = (float)E;
+            if (blockIdx.x == 0) *wexp = E;
+        }
+    }
+    __syncthreads();
+    const float sc = ldexpf(1.f, (int)s_e);
+    const long long q = (long long)blockIdx.x * NTH + threadIdx.x;
+    if (q >= rows * 8) return;
+    const long long r = q >> 3;
+    const int n = (int)(r % n_pad), l = (int)(q & 7) ^ ((n >> 1) & 7), k = l & 3;
+    const f32x4 a = *reinterpret_cast<const f32x4 *>(wp + r * 32 + 8 * k);
+    const f32x4 b = *reinterpret_cast<const f32x4 *>(wp + r * 32 + 8 * k + 4);
+    f16x8 v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const float x = (e < 4 ? a[e] : b[e - 4]) * sc;
+        const _Float16 hi = (_Float16)x;
+        v[e] = (l >> 2) ? (_Float16)(x - (float)hi) : hi;
+    }
+    *reinterpret_cast<f16x8 *>(out + q * 8) = v;
+}
+
 // Per-call precision of the discriminator convs (include/esr_amd.h `prec`): 0 = exact fp32, 1 = x3 (128-wide N tiles
 // where the grid allows), 2 = x3 with 64-wide N tiles only, 3 = x6.  np = f16 pieces per operand value (0: fp32),
 // nb = widest N tile.
@@ -1940,5 +1997,19 @@ extern "C" int esr_dconv_wgrad(const float *src, int32_t B, int32_t Hs, int32_t 
     const long long gx = (long long)T * p.ci_blocks * p.co_blocks;
     const dim3 grid((unsigned)gx, (unsigned)splits), block(NTH);
     hipLaunchKernelGGL(dconv_wgrad_kernel, grid, block, 0, (hipStream_t)stream, p);
+    return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+}
+
+extern "C" int esr_dconv_presplit(const float *w_packed, int64_t rows, int32_t n_pad, float *scratch, void *w_split,
+                                  int32_t *w_exp, esr_stream_t stream) {
+    if (!w_packed || !scratch || !w_split || !w_exp || rows <= 0 || n_pad <= 0 || n_pad % NB || rows % n_pad ||
+        ((uintptr_t)w_packed & 15) || ((uintptr_t)w_split & 15))
+        return ESR_EINVAL;
+    const hipStream_t st = (hipStream_t)stream;
+    const long long n = rows * 32;
+    const int nb = (int)min((long long)PS_BLOCKS, (n + NTH - 1) / NTH);
+    hipLaunchKernelGGL(presplit_amax_kernel, dim3(nb), dim3(NTH), 0, st, w_packed, n, scratch);
+    hipLaunchKernelGGL(presplit_apply_kernel, dim3((unsigned)((rows * 8 + NTH - 1) / NTH)), dim3(NTH), 0, st, w_packed,
+                       (long long)rows, n_pad, (const float *)scratch, nb, static_cast<_Float16 *>(w_split), w_exp);
     return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
 }

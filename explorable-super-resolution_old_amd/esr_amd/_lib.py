@@ -96,6 +96,7 @@ _SIGNATURES = {
                          ctypes.POINTER(c_int), ctypes.POINTER(c_int), c_int, c_void_p, c_int, c_int, c_int, c_int,
                          c_int, c_void_p, c_void_p, c_void_p],
     'esr_dconv_uses_halo': [c_int, c_int, c_int, c_int, c_int, c_int],
+    'esr_dconv_presplit': [c_void_p, ctypes.c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     'esr_dconv_fwd_splits_sd': [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_int),
                                 ctypes.POINTER(c_int), c_int, c_int],
     'esr_dconv_wgrad_splits': [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_int),

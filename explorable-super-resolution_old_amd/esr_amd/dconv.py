@@ -96,16 +96,14 @@ class _Packed:
         if self._split is None:
             wp = self.wp
             T, nck, n_pad, _ = wp.shape
-            amax = wp.abs().amax()
-            e = torch.where(amax > 0, 14.0 - torch.floor(torch.log2(amax)), torch.zeros_like(amax))
-            v = wp * torch.exp2(e)
-            hi = v.half()
-            lo = (v - hi.float()).half()
-            logical = torch.stack([hi, lo], 3).view(T, nck, n_pad, 8, 8)
-            n = torch.arange(n_pad, device=wp.device)
-            idx = (torch.arange(8, device=wp.device).view(1, 8) ^ ((n.view(-1, 1) >> 1) & 7))
-            phys = torch.gather(logical, 3, idx.view(1, 1, n_pad, 8, 1).expand(T, nck, n_pad, 8, 8))
-            self._split = (phys.contiguous(), e.to(torch.int32).view(1))
+            rows = torch.empty(T, nck, n_pad, 8, 8, device=wp.device, dtype=torch.float16)
+            e = torch.empty(1, device=wp.device, dtype=torch.int32)
+            _check_dev(wp)
+            scratch = torch.empty(512, device=wp.device)  # esr_dconv_presplit: two launches, no host sync
+            _lib.check(_lib.load().esr_dconv_presplit(wp.data_ptr(), T * nck * n_pad, n_pad, scratch.data_ptr(),
+                                                      rows.data_ptr(), e.data_ptr(), _stream(wp)),
+                       'esr_dconv_presplit')
+            self._split = (rows, e)
         return self._split
 
 

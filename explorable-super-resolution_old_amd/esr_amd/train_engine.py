@@ -715,15 +715,21 @@ def _split_grads(bp, flat):
     return grads
 
 
+# how the training passes ran (observability: the benchmarks record the deltas of their timed regions)
+GRAPH_COUNTS = {'eager': 0, 'captured': 0, 'replayed': 0}
+
+
 def _run_graphed(ws, key, fn, *inputs):
     """fn(*inputs) eagerly the first time `key` is seen; captured into a HIP graph (static copies of the inputs) the
     second time; replayed from then on.  Returns fn's outputs, which for a graph live in its private pool (the caller
     clones what must outlive the next replay)."""
     if not USE_GRAPHS:
+        GRAPH_COUNTS['eager'] += 1
         return fn(*inputs), False
     ent = ws.graphs.get(key)
     if ent is None:
         ws.graphs[key] = 'seen'
+        GRAPH_COUNTS['eager'] += 1
         return fn(*inputs), False
     if ent == 'seen':
         static = [t.detach().clone() for t in inputs]
@@ -731,6 +737,9 @@ def _run_graphed(ws, key, fn, *inputs):
         with torch.cuda.graph(g):
             out = fn(*static)
         ent = ws.graphs[key] = (g, static, out)
+        GRAPH_COUNTS['captured'] += 1
+    else:
+        GRAPH_COUNTS['replayed'] += 1
     g, static, out = ent
     for st, t in zip(static, inputs):
         st.copy_(t)

@@ -302,6 +302,11 @@ int esr_dconv_fwd_sd(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_
                      const int32_t *offx, int32_t ksplit, float *partial, int32_t s2d_c, int32_t s2d_pad,
                      int32_t d2s_c, int32_t d2s_pad, int32_t prec, const void *w_split, const int32_t *w_exp,
                      esr_stream_t stream);
+/* The w_split / w_exp form of a packed weight tensor (rows = T·nck·n_pad rows of 32 floats): two launches (a partial
+ * max over ESR_DCONV_PRESPLIT_SCRATCH floats of scratch, then the split), no host synchronisation. */
+#define ESR_DCONV_PRESPLIT_SCRATCH 512
+int esr_dconv_presplit(const float *w_packed, int64_t rows, int32_t n_pad, float *scratch, void *w_split,
+                       int32_t *w_exp, esr_stream_t stream);
 /* 1 if an esr_dconv_fwd(_sd) launch of this geometry runs on the halo-tile kernel (sd != 0: an esr_dconv_fwd_sd
  * launch), 0 if on the per-tap gather kernel.  The host takes the space-to-depth forward only where it is halo-tiled
  * (on the gather kernel it is no faster than the direct stride-2 gather: profiles/r3_dconv_s2d_ab.txt). */

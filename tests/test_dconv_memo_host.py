@@ -83,16 +83,33 @@ def test_im2col_function_matches_autograd_through_cat_and_pad():
         assert torch.autograd.gradgradcheck(lambda t: dconv._Im2ColFn.apply(t, k, p), (x,))
 
 
+
+def presplit_reference(wp):
+    """The layout of include/esr_amd.h esr_dconv_fwd_sd w_split / w_exp restated with PyTorch ops (test reference for
+    esr_dconv_presplit): v = wp·2^E, E = 14 - floor(log2 max|wp|), hi = f16(v), lo = f16(v - hi), each 128-byte
+    (t, chunk, n) row's logical 16-B slot piece·4 + k stored at position ^ ((n >> 1) & 7)."""
+    import torch
+    T, nck, n_pad, _ = wp.shape
+    amax = wp.abs().amax()
+    E = torch.where(amax > 0, 14.0 - torch.floor(torch.log2(amax)), torch.zeros_like(amax))
+    v = wp * torch.exp2(E)
+    hi = v.half()
+    lo = (v - hi.float()).half()
+    logical = torch.stack([hi, lo], 3).view(T, nck, n_pad, 8, 8)
+    n = torch.arange(n_pad, device=wp.device)
+    idx = torch.arange(8, device=wp.device).view(1, 8) ^ ((n.view(-1, 1) >> 1) & 7)
+    rows = torch.gather(logical, 3, idx.view(1, 1, n_pad, 8, 1).expand(T, nck, n_pad, 8, 8))
+    return rows, E.to(torch.int32).view(1)
+
+
 def test_presplit_weight_layout():
-    """_Packed.split(): the x3 halo kernel's pre-split weights (include/esr_amd.h esr_dconv_fwd_sd w_split): rows of
-    eight 16-byte slots, logical slot piece·4 + k at position ^ ((n >> 1) & 7); hi + lo = w·2^E to f16-pair accuracy
-    with one power of two E per tensor putting max |w|·2^E in [2^14, 2^15)."""
+    """The reference restatement of the pre-split layout: hi + lo = w·2^E to f16-pair accuracy, max |w|·2^E in
+    [2^14, 2^15), hi exact f16 rounding; tests/test_gpu_disc.py checks esr_dconv_presplit against it bitwise."""
     import torch
     g = torch.Generator().manual_seed(3)
     wt = torch.randn(9, 70, 100, generator=g) * 0.03
-    pk = dconv._pack(wt, 100)
-    wp, nck, n_pad = pk
-    rows, e = pk.split()
+    wp, nck, n_pad = dconv._pack(wt, 100)
+    rows, e = presplit_reference(wp)
     E = int(e.item())
     assert 2 ** 14 <= float(wp.abs().max()) * 2 ** E < 2 ** 15
     assert rows.dtype == torch.float16 and rows.shape == (9, nck, n_pad, 8, 8)

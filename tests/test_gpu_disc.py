@@ -286,3 +286,21 @@ def test_lrelu_nhwc_second_order(gpu_device):
     got = run(lambda t: lrelu_nhwc(t, 0.2), cl(x), cl(gy), cl(r))
     for a, b in zip(got, ref):
         assert normwise_rel(a.double().cpu(), b) < 1e-7
+
+
+@pytest.mark.parametrize('T,K,N', [(9, 70, 100), (16, 256, 64), (1, 32, 1), (64, 256, 100)])
+def test_presplit_kernel_bitwise(gpu_device, T, K, N):
+    """esr_dconv_presplit (two launches) against the PyTorch restatement of the layout
+    (tests/test_dconv_memo_host.py presplit_reference): rows and exponent bitwise."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_dconv_memo_host import presplit_reference
+    g = torch.Generator().manual_seed(T + K + N)
+    wt = (torch.randn(T, K, N, generator=g) * 0.05).to(gpu_device)
+    pk = dconv._pack(wt, N)
+    rows, e = pk.split()
+    ref_rows, ref_e = presplit_reference(pk.wp)
+    torch.cuda.synchronize()
+    assert torch.equal(e.cpu(), ref_e.cpu())
+    assert torch.equal(rows.view(torch.int16).cpu(), ref_rows.view(torch.int16).cpu())
