@@ -668,22 +668,46 @@ __global__ __launch_bounds__(NTH, OCC) void dconv_fwd_halo_x_kernel(FwdParams p,
     // image (a staged row's 128 fp32 bytes fit in its split pitch) while the max |a| is taken; after the cross-wave
     // max each thread converts whole rows in place (all 8 quads read before any write), so the window is not read
     // from L2 twice (the two-pass form cost up to 40 % of a space-to-depth launch: profiles/r3_halo_split.txt)
-    auto stage_a = [&](int j, int e_keep) {
-        const int total = h.IY * h.IXt * 8;
+    const int total_a = h.IY * h.IXt * 8;  // fp32 quads of a chunk's halo window
+    // PB: the next chunk's window is loaded into registers during the last step of the current one when it fits
+    // quads per thread (48 VGPRs); not where the registers run out (128-wide N tiles, three workgroups per CU: spills)
+    constexpr int PFQ = (PB && OCC == 2 && NBX == 64) ? 12 : 0;
+    const bool pf_ok = PFQ > 0 && total_a <= PFQ * NTH;
+    f32x4 pf[PFQ > 0 ? PFQ : 1];
+    auto prefetch_a = [&](int j) {
+#pragma unroll
+        for (int u = 0; u < PFQ; ++u) {
+            const int idx = u * NTH + tid;
+            pf[u] = idx < total_a ? halo_item(idx, j) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    // stage chunk j's window (or, from_pf, the prefetched one) and split it; returns its exponent
+    auto stage_a = [&](int j, int e_keep, bool from_pf = false) {
+        const int total = total_a;
         float m = 0.f;
-        for (int base = 0; base < total; base += 8 * NTH) {
-            f32x4 v[8];
+        if (from_pf) {
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int idx = base + u * NTH + tid;
-                v[u] = idx < total ? halo_item(idx, j) : f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int u = 0; u < PFQ; ++u) {
+                const int idx = u * NTH + tid;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) m = fmaxf(m, fabsf(pf[u][e]));
+                if (idx < total) *reinterpret_cast<f32x4 *>(s_a + (idx >> 3) * XPn + (idx & 7) * 16) = pf[u];
             }
+        } else {
+            for (int base = 0; base < total; base += 8 * NTH) {
+                f32x4 v[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int idx = base + u * NTH + tid;
+                for (int u = 0; u < 8; ++u) {
+                    const int idx = base + u * NTH + tid;
+                    v[u] = idx < total ? halo_item(idx, j) : f32x4{0.f, 0.f, 0.f, 0.f};
+                }
 #pragma unroll
-                for (int e = 0; e < 4; ++e) m = fmaxf(m, fabsf(v[u][e]));
-                if (idx < total) *reinterpret_cast<f32x4 *>(s_a + (idx >> 3) * XPn + (idx & 7) * 16) = v[u];
+                for (int u = 0; u < 8; ++u) {
+                    const int idx = base + u * NTH + tid;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) m = fmaxf(m, fabsf(v[u][e]));
+                    if (idx < total) *reinterpret_cast<f32x4 *>(s_a + (idx >> 3) * XPn + (idx & 7) * 16) = v[u];
+                }
             }
         }
         m = wave_max(m);
@@ -748,8 +772,8 @@ __global__ __launch_bounds__(NTH, OCC) void dconv_fwd_halo_x_kernel(FwdParams p,
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's copy of the step's weights landed
             __syncthreads();  // every copy landed; every wave is done with step - 1 (its slot, and the window at t 0)
             if (t == 0) {
-                const int ea2 = stage_a(c_begin + step / p.T, ea);  // (contains a barrier)
-                __syncthreads();                                    // the split window is in place
+                const int ea2 = stage_a(c_begin + step / p.T, ea, pf_ok && step > 0);  // (contains a barrier)
+                __syncthreads();                                                       // the split window is in place
                 if (ea2 != ea) {
 #pragma unroll
                     for (int i = 0; i < WM; ++i)
@@ -761,6 +785,7 @@ __global__ __launch_bounds__(NTH, OCC) void dconv_fwd_halo_x_kernel(FwdParams p,
                 }
             }
             if (step + 1 < nsteps) dma_b(step + 1, (step + 1) & 1);  // lands under this step's MFMAs
+            if (pf_ok && t == p.T - 1 && step + 1 < nsteps) prefetch_a(c_begin + (step + 1) / p.T);  // next window
             const int dy = p.offy[t] - h.oymin, dx = p.offx[t] - h.oxmin;
             const int mc = ml % CW, mr = ml / CW;
             const int col = (h.npar == 1) ? mc + dx : (dx & 1) * h.IXp + mc + (dx >> 1);
