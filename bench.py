@@ -236,6 +236,7 @@ def run_legs(args, dev, world, rank):
     except Exception as e:  # noqa: BLE001
         legs['fp32_c2'] = {'error': repr(e)}
     torch.cuda.empty_cache()
+    import gc
     for key, mod, kw in (('train_c4' if world > 1 else 'train_c3', bench_train, {}),
                          ('zopt_c5', bench_zopt, {'kernel': 'kgan'}),
                          ('zopt_c5_learned13', bench_zopt, {'kernel': 'learned13'})):
@@ -243,6 +244,7 @@ def run_legs(args, dev, world, rank):
             legs[key] = mod.run(mod.leg_args(steps=args.leg_steps, **kw), dev, world, rank)
         except Exception as e:  # noqa: BLE001
             legs[key] = {'error': repr(e)}
+        gc.collect()  # the leg's model, even inside reference cycles, before the cache is released
         torch.cuda.empty_cache()
     return legs
 

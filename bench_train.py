@@ -40,21 +40,52 @@ def make_opt(args):
     }
 
 
+_GC_PAUSE = [0.0, None]  # total seconds Python's cyclic GC has run, start of the current collection
+
+
+def _gc_timer(phase, info):
+    if phase == 'start':
+        _GC_PAUSE[1] = time.perf_counter()
+    elif _GC_PAUSE[1] is not None:
+        _GC_PAUSE[0] += time.perf_counter() - _GC_PAUSE[1]
+        _GC_PAUSE[1] = None
+
+
+def settle():
+    """End of a leg's warm-up: one full collection, then the surviving objects (models, op lists, packed weights) are
+    frozen out of the collector's generations, as a serving process does after loading its model — a generation-2
+    collection inside the timed region then scans only the objects created since (without it one such collection cost
+    a C5 iteration ≈150 ms: BENCH r4 records, `timed_region.gc_ms`)."""
+    import gc
+    gc.collect()
+    gc.freeze()
+
+
+def unsettle():
+    """After the timed region: the frozen objects rejoin the collector (so that this leg's models, once dropped, are
+    collected even if they sit in reference cycles)."""
+    import gc
+    gc.unfreeze()
+
+
 def observe():
     """Counters that explain a timed region (record the delta of two calls): x3 overflow reruns, how the training
     passes ran (eager / graph capture / replay), the caching allocator's device allocations and retries, and Python's
-    generation-2 garbage collections."""
+    generation-2 garbage collections and the time the collector ran."""
     import gc
     from esr_amd import engine, train_engine
+    if _gc_timer not in gc.callbacks:
+        gc.callbacks.append(_gc_timer)
     ms = torch.cuda.memory_stats()
     return {'overflow_reruns': engine.OVERFLOW_RERUNS, 'act_scale_reductions': engine.ACT_SCALE_REDUCTIONS,
             **{'graph_' + k: v for k, v in train_engine.GRAPH_COUNTS.items()},
             'device_allocs': ms.get('num_device_alloc', 0), 'device_frees': ms.get('num_device_free', 0),
-            'alloc_retries': ms.get('num_alloc_retries', 0), 'gc_gen2': gc.get_stats()[2]['collections']}
+            'alloc_retries': ms.get('num_alloc_retries', 0), 'gc_gen2': gc.get_stats()[2]['collections'],
+            'gc_ms': round(_GC_PAUSE[0] * 1e3, 2)}
 
 
 def observed(a, b):
-    return {k: b[k] - a[k] for k in a}
+    return {k: round(b[k] - a[k], 2) for k in a}
 
 
 def leg_args(**kw):
@@ -86,6 +117,7 @@ def run(args, dev, world, rank):
         model.feed_data(data)
         model.optimize_parameters()
     reruns1, a1 = engine.OVERFLOW_RERUNS, engine.act_scale(rrdb)
+    settle()
     obs0 = observe()
     torch.cuda.synchronize()
     if world > 1:
@@ -102,6 +134,7 @@ def run(args, dev, world, rank):
     dt = time.perf_counter() - t0
     step_ms = [round((b - a) * 1e3, 2) for a, b in zip([t0] + stamps[:-1], stamps)]
     obs = observed(obs0, observe())
+    unsettle()
     if world > 1:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

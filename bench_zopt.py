@@ -84,7 +84,8 @@ def run(args, dev, world, rank):
     reruns1 = engine.OVERFLOW_RERUNS
     a1 = engine.act_scale(rrdb)
     zo.max_iters = args.steps
-    from bench_train import observe, observed
+    from bench_train import observe, observed, settle, unsettle
+    settle()
     obs0 = observe()
     stamps = []
     # each iteration ends with its overflow-flag read (a device sync), so these are per-iteration wall times
@@ -100,6 +101,7 @@ def run(args, dev, world, rank):
     zo.on_iteration = None
     iter_ms = [round((b - a) * 1e3, 2) for a, b in zip([t0] + stamps[:-1], stamps)]
     obs = observed(obs0, observe())
+    unsettle()
     if world > 1:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
