@@ -334,7 +334,10 @@ class SRRaGANModel:
             elif not torch.is_tensor(cur_Z) and np.ndim(cur_Z) < 4:
                 cur_Z = cur_Z * np.ones([1, self.num_latent_channels] + hw)
             elif torch.is_tensor(cur_Z) and cur_Z.size(2) == 1:
-                cur_Z = cur_Z.to(self.device).float().expand(-1, -1, *hw).contiguous()
+                if not cur_Z.is_cuda and self.device.type == 'cuda':
+                    # through a (cached) pinned buffer: a pageable host-to-device copy blocks the host until it is done
+                    cur_Z = cur_Z.float().contiguous().pin_memory()
+                cur_Z = cur_Z.to(self.device, non_blocking=True).float().expand(-1, -1, *hw).contiguous()
             if not torch.is_tensor(cur_Z):
                 cur_Z = torch.from_numpy(np.asarray(cur_Z, dtype=np.float32))
             cur_Z = cur_Z.float().to(self.device)

@@ -161,15 +161,6 @@ def pack_x3(packed):
     return out, scale
 
 
-def _pack_x3_scaled(packed, scale):
-    """pack_x3 with a given power-of-two scale (no host sync)."""
-    n32, T, n_pad, _ = packed.shape
-    p16 = packed.view(n32, T, n_pad, 2, 16).permute(0, 3, 1, 2, 4).reshape(2 * n32, T, n_pad, 16)
-    hi, lo = split_f16(p16 * scale)
-    sh = (2 * n32, T, n_pad, 2, 1, 8)
-    return torch.cat([hi.reshape(sh), lo.reshape(sh)], dim=4).contiguous(), scale
-
-
 def to_split(x_nhwc):
     """fp32 [..., C] (C % 8 == 0) -> split-f16 layout with the same byte size, returned as float32 storage."""
     hi, lo = split_f16(x_nhwc)
@@ -186,12 +177,33 @@ def from_split(buf):
     return (h[..., 0, :] + h[..., 1, :]).reshape(buf.shape)
 
 
+FOLD_TERMS = 4  # a folded phase tap sums at most 2 × 2 of the 3×3 taps
+
+
+def fold_terms(py, px, f=2):
+    """Output phase (py, px) of a nearest-×f upconv: for each of its 2×2 LR taps (a, b), the 3×3 taps (y, x) summed
+    into it, in the fixed order (row-major) in which fold_upconv_phase and GatherPlan.reg_sum add them."""
+    Fy, Fx = _FOLDS[f][py][0], _FOLDS[f][px][0]
+    return [[[(y, x) for y in range(3) for x in range(3) if Fy[a][y] and Fx[b][x]] for b in range(2)] for a in range(2)]
+
+
+def fold_term_images(w, py, px, f=2):
+    """fold_upconv_phase as FOLD_TERMS tensors [Cout][Cin][2][2] whose sum ((t0 + t1) + t2) + t3 is the folded weight:
+    term k holds the k-th summed 3×3 tap of each phase tap, or 0."""
+    terms = fold_terms(py, px, f)
+    out = [w.new_zeros(w.shape[0], w.shape[1], 2, 2) for _ in range(FOLD_TERMS)]
+    for a in range(2):
+        for b in range(2):
+            for k, (y, x) in enumerate(terms[a][b]):
+                out[k][:, :, a, b] = w[:, :, y, x]
+    return out
+
+
 def fold_upconv_phase(w, py, px, f=2):
     """Nearest-×f upsample then 3×3 conv == per output phase (py,px) a 2×2 conv on the LR grid whose taps are sums of
     the 3×3 taps landing on the same source pixel (block.py:294-301)."""
-    Fy = torch.tensor(_FOLDS[f][py][0], dtype=w.dtype, device=w.device)
-    Fx = torch.tensor(_FOLDS[f][px][0], dtype=w.dtype, device=w.device)
-    return torch.einsum('ay,bx,oiyx->oiab', Fy, Fx, w.detach())
+    t = fold_term_images(w.detach(), py, px, f)
+    return ((t[0] + t[1]) + t[2]) + t[3]
 
 
 class _ConvW:
@@ -226,7 +238,9 @@ class GatherPlan:
             self._img[id(p)] = torch.arange(off, off + p.numel(), dtype=torch.float64).view(p.shape)
             off += p.numel()
         self._parts = []
-        self.buf = self.idx = None
+        self._sums = []
+        self.buf = self.idx = self.sidx = None
+        self.n_gather = 0
 
     def w(self, p):
         return self._img[id(p)]
@@ -239,28 +253,51 @@ class GatherPlan:
         self._parts.append(t)
         return t
 
+    def reg_sum(self, terms):
+        """A packed tensor that is the sum ((t0 + t1) + t2) + t3 of FOLD_TERMS gathers (index images of one shape; 0 =
+        a zero term): the nearest-×2 upconv phases (fold_term_images), refreshed with the rest instead of being folded
+        and packed again after every optimiser step.  Returns the key (the first term) that finalize maps to the view."""
+        assert len(terms) == FOLD_TERMS and all(t.shape == terms[0].shape for t in terms)
+        self._sums.append(terms)
+        return terms[0]
+
     def finalize(self, dev):
         """Allocate the packed buffer; returns {id(index tensor): device view} for the caller to swap in."""
         n = sum(t.numel() for t in self._parts)
-        self.buf = torch.empty(n, device=dev, dtype=torch.float32)
+        m = sum(ts[0].numel() for ts in self._sums)
+        self.n_gather = n
+        self.buf = torch.empty(n + m, device=dev, dtype=torch.float32)
         self.idx = torch.cat([t.reshape(-1) for t in self._parts]).to(torch.int64).to(dev)
+        if self._sums:
+            self.sidx = torch.stack([torch.cat([ts[k].reshape(-1) for ts in self._sums])
+                                     for k in range(FOLD_TERMS)]).to(torch.int64).to(dev)
         views, o = {}, 0
         for t in self._parts:
             views[id(t)] = self.buf[o:o + t.numel()].view(t.shape)
             o += t.numel()
-        self._parts = None
+        for ts in self._sums:
+            views[id(ts[0])] = self.buf[o:o + ts[0].numel()].view(ts[0].shape)
+            o += ts[0].numel()
+        self._parts = self._sums = None
         return views
 
     def _flat_source(self):
-        """The FlatAdam buffer (flat_optim.py) if the parameters are exactly its consecutive views, else None."""
+        """The FlatAdam buffer (flat_optim.py) if the parameters are exactly its consecutive views, else None.  The full
+        check runs once per (buffer, parameter addresses); later calls compare the addresses only (~0.1 instead of
+        ~0.4 ms of host time on RRDB-23's 702 parameters, several calls per training step)."""
         fl = getattr(self.params[0], '_esr_flat', None)
         if fl is None or fl.numel() != self.N:
             return None
+        ptrs = [p.data_ptr() for p in self.params]
+        ok = self.__dict__.get('_flat_ok')
+        if ok is not None and ok[0] is fl and ok[1] == ptrs:
+            return fl.detach()
         base, o = fl.data_ptr(), 0
-        for p in self.params:
-            if getattr(p, '_esr_flat', None) is not fl or p.data_ptr() != base + 4 * o or not p.is_contiguous():
+        for p, ptr in zip(self.params, ptrs):
+            if getattr(p, '_esr_flat', None) is not fl or ptr != base + 4 * o or not p.is_contiguous():
                 return None
             o += p.numel()
+        self._flat_ok = (fl, ptrs)
         return fl.detach()
 
     def refresh(self):
@@ -268,7 +305,13 @@ class GatherPlan:
         if flat is None:
             flat = torch.cat([p.detach().reshape(-1) for p in self.params])
         ext = torch.cat([flat.new_zeros(1)] + [flat * s if s != 1.0 else flat for s in self.scales])
-        torch.index_select(ext, 0, self.idx, out=self.buf)
+        torch.index_select(ext, 0, self.idx, out=self.buf[:self.n_gather])
+        if self.sidx is not None:
+            g = ext[self.sidx]
+            out = self.buf[self.n_gather:]
+            torch.add(g[0], g[1], out=out)
+            out.add_(g[2])
+            out.add_(g[3])
 
 
 class _Packed:
@@ -298,11 +341,17 @@ class _Packed:
         i0 = 2 + getattr(net, 'n_up', 2)  # HR_conv0, then its LeakyReLU, then HR_conv1
         self.hr0 = _ConvW(pk(m[i0], lr_map(64), 64), m[i0].bias)
         self.hr1 = _ConvW(pk(m[i0 + 2], lr_map(64), 32), m[i0 + 2].bias)
+        # the upsampler phases: sums of taps (fold_upconv_phase), refreshed by the plan's summed gather
+        self.up = []
+        for j, f in up_stages(net):
+            c = m[j][1]
+            self.up.append([_ConvW(plan.reg_sum([pack_conv_weight(t, list(range(64)), 64)
+                                                 for t in fold_term_images(plan.w(c.weight), py, px, f)]), c.bias)
+                            for py in range(f) for px in range(f)])
         views = plan.finalize(net.model[0].weight.device)
         self.planned = [self.first, self.lr_conv, self.hr0, self.hr1] + [cw for r in self.rdb for cw in r]
-        for cw in self.planned:
+        for cw in self.planned + [c for row in self.up for c in row]:
             cw.f32 = views[id(cw.f32)]
-        self.up = None
 
     def train_x3(self):
         """x3 weights for the training / Z-optimisation forward, rebuilt IN PLACE after every parameter change with no
@@ -317,7 +366,7 @@ class _Packed:
             buf = self.plan.buf
             idx, sc, views, off = [], [], [], 0
             outs = []
-            for cw, scl in zip(self.planned, scales):
+            for cw, scl in zip(convs, scales):  # every layer is a view of the plan's buffer (upsampler phases too)
                 n32, T, n_pad, _ = cw.f32.shape
                 base = cw.f32.storage_offset() - buf.storage_offset()
                 i = torch.arange(base, base + cw.f32.numel(), device=buf.device).view(cw.f32.shape)
@@ -327,13 +376,11 @@ class _Packed:
                 off += 2 * cw.f32.numel()
             self._tx3_idx, self._tx3_scale = torch.cat(idx), torch.cat(sc)
             self._tx3 = torch.empty(off, device=buf.device, dtype=torch.float16)
-            for cw, scl, (o, shp) in zip(self.planned, scales, views):
+            for cw, scl, (o, shp) in zip(convs, scales, views):
                 n = 1
                 for d in shp:
                     n *= d
-                outs.append((cw, self._tx3[o:o + n].view(shp), scl, False))
-            for cw, scl in zip([c for row in self.up for c in row], scales[len(self.planned):]):
-                outs.append((cw, torch.empty_like(_pack_x3_scaled(cw.f32, scl)[0]), scl, True))
+                outs.append((cw, self._tx3[o:o + n].view(shp), scl))
             self._tx3_layers = outs
             self._tx3_bad = torch.zeros(1, device=buf.device, dtype=torch.int32)
             self._tx3_version = None
@@ -343,14 +390,9 @@ class _Packed:
             lo = (g - hi.float()).half()
             G = g.numel() // 8
             self._tx3.view(G, 2, 8).copy_(torch.stack([hi.view(G, 8), lo.view(G, 8)], 1))
-            bad = g.abs().amax() >= 61440.0
-            for cw, view, scl, own in self._tx3_layers:
-                if own:  # upsampler phases (sums of taps, not in the gather plan): fixed-scale split of their own
-                    view.copy_(_pack_x3_scaled(cw.f32, scl)[0])
-                    bad = bad | (cw.f32.abs().amax() * scl >= 61440.0)
-            self._tx3_bad.copy_(bad.to(torch.int32).view(1))
+            self._tx3_bad.copy_((g.abs().amax() >= 61440.0).to(torch.int32).view(1))
             self._tx3_version = getattr(self, 'version', 0)
-        for cw, view, scl, _ in self._tx3_layers:
+        for cw, view, scl in self._tx3_layers:
             cw._x3 = (view, scl)
         return self._tx3_bad
 
@@ -390,25 +432,10 @@ class _Packed:
         self.hr1.bias_s = self.hr1.bias
 
     def refresh(self):
-        self.plan.refresh()
+        self.plan.refresh()  # in place: recorded op lists and captured HIP graphs keep valid pointers
         self.version = getattr(self, 'version', 0) + 1  # invalidates recorded op lists (new x3 weight tensors)
-        for cw in self.planned:
+        for cw in self.planned + [c for row in self.up for c in row]:
             cw._x3 = None
-        # the upsampler phases are sums of taps (not a permutation): packed directly, 8 small tensors, updated in place
-        # after the first build so that recorded op lists and captured HIP graphs keep valid pointers
-        m = self.net.model
-        up = []
-        for j, f in up_stages(self.net):
-            c = m[j][1]
-            up.append([_ConvW(pack_conv_weight(fold_upconv_phase(c.weight, py, px, f), list(range(64)), 64), c.bias)
-                       for py in range(f) for px in range(f)])
-        if self.up is None:
-            self.up = up
-        else:
-            for old_row, new_row in zip(self.up, up):
-                for o, n in zip(old_row, new_row):
-                    o.f32.copy_(n.f32)
-                    o._x3 = None
 
 
 def param_list(m):
@@ -433,20 +460,32 @@ def param_list(m):
 
 
 def _param_key(net):
-    ps = param_list(net)
-    key = tuple((p.data_ptr(), p._version) for p in ps)
-    # parameters bound to a FlatAdam buffer (flat_optim.py) change when the buffer is updated in place, which bumps
-    # the buffer's version counter, not theirs
-    fl = getattr(ps[0], '_esr_flat', None) if ps else None
-    return key + ((id(fl), fl._version),) if fl is not None else key
+    return _keys(net)[1]
 
 
 def _struct_key(net):
-    return tuple((p.data_ptr(), p.shape) for p in param_list(net))
+    return _keys(net)[0]
+
+
+def _keys(net):
+    """(structure key: every parameter's address and shape; value key: their addresses and version counters) in one
+    pass over the parameter list.  Parameters bound to a FlatAdam buffer (flat_optim.py) change when the buffer is
+    updated in place, which bumps the buffer's version counter, not theirs."""
+    ps = param_list(net)
+    sk, vk = [], []
+    for p in ps:
+        ptr = p.data_ptr()
+        sk.append((ptr, p.shape))
+        vk.append((ptr, p._version))
+    fl = getattr(ps[0], '_esr_flat', None) if ps else None
+    if fl is not None:
+        vk.append((id(fl), fl._version))
+    return tuple(sk), tuple(vk)
 
 
 def _packed(net, latent):
-    skey, vkey = (_struct_key(net), latent), _param_key(net)
+    sk, vkey = _keys(net)
+    skey = (sk, latent)
     c = net._esr_cache.get('packed')
     if c is None or c[0] != skey:
         net._esr_cache.pop('packed', None)

@@ -349,7 +349,8 @@ def _fused_rdb_weights(plan, convs, zc):
 
 
 def _bwd_packed(net, latent):
-    skey, vkey = (E._struct_key(net), latent), E._param_key(net)
+    sk, vkey = E._keys(net)
+    skey = (sk, latent)
     c = net._esr_cache.get('packed_bwd')
     if c is None or c[0] != skey:
         net._esr_cache.pop('packed_bwd', None)

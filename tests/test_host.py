@@ -200,6 +200,12 @@ def test_gather_plan_equals_direct_packing(latent):
         conv.weight.mul_(3.0)
     pk = engine._packed(net, latent)
     assert torch.equal(pk.rdb[1][3].f32, engine.pack_conv_weight(conv.weight, lr_map(64 + 96), 32))
+    # the upsampler phases: summed gathers, bitwise equal to folding then packing
+    for row, (j, f) in zip(pk.up, engine.up_stages(net)):
+        w = net.model[j][1].weight
+        for cw, (py, px) in zip(row, [(a, b) for a in range(f) for b in range(f)]):
+            assert torch.equal(cw.f32, engine.pack_conv_weight(engine.fold_upconv_phase(w, py, px, f),
+                                                               list(range(64)), 64)), (j, py, px)
     bp = T._bwd_packed(net, latent)
     # fused RDB data-gradient weights: slice t's rows of rot180/transposed W_i, stacked over the convs i that read t
     rdb = net.model[1].sub[0].RDB3
