@@ -1328,10 +1328,12 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
     // shapes, bitwise identical; profiles/r2_x3c_ab.txt); where 8-row classic tiles at three workgroups per CU pay
     // (small grids), the classic kernel stays.  Variant 24 = the round-1 automatic choice (classic only).
     // the polyphase upconv phases (2x2 taps) too: 341 -> 287 us per config-2 launch (whole-step A/B, 2 rounds)
-    // N = 32 12-column tiles (three workgroups per CU) also where the grid is large enough for the classic 8-row
-    // tiles to look better by rounds (≥ 3 full rounds): HR_conv1 at 592² (1115 -> 1060 us per config-2 launch)
+    // N = 32 12-column tiles (three workgroups per CU) also where the classic 8-row tiles look better by rounds, once
+    // the 12-column grid has a tile per CU: config 3 (B=16 × 96², 392 tiles) 1.00-1.07× per launch, 135.7 -> 133.9-
+    // 134.8 ms per step; config 5 (B=8 × 172², 660 tiles) 1.09-1.12×; HR_conv1 at 592² 1115 -> 1060 us.  Below a tile
+    // per CU (B=8 × 64²: 102 tiles) the 8-row tiles stay (0.70-0.73× there; profiles/r4_x3_n32_grid_ab.txt)
     const int tiles12 = ((W + 11) / 12) * ((B * (H + 2) - 2 + 31) / 32);
-    const bool x3c_pays = taps_side == 2 || (taps_side == 3 && (cout > 32 || !row8_pays || tiles12 >= 9 * n_cu));
+    const bool x3c_pays = taps_side == 2 || (taps_side == 3 && (cout > 32 || !row8_pays || tiles12 >= n_cu));
     if ((g_x3_kernel >= 50 && g_x3_kernel <= 62) || g_x3_kernel == 64 || ((g_x3_kernel == 1 || g_x3_kernel == 63) && x3c_pays)) {
         X3cParams c;
         c.in = p.in; c.B = B; c.H = H; c.W = W; c.in_cp = in_cp; c.cin = cin; c.w = p.w; c.bias = bias;
@@ -1461,4 +1463,32 @@ extern "C" int esr_upconv2x_phase_fwd_x3(const void *in, int32_t B, int32_t H, i
     if (py < 0 || py > 1 || px < 0 || px > 1) return ESR_EINVAL;
     return launch_x3(in, B, H, W, in_cp, cin, w_packed, bias, w_scale, cout, 2, py, px, o, overflow,
                      (hipStream_t)stream);
+}
+
+extern "C" int esr_hr_convs_x3(const void *in, int32_t B, int32_t H, int32_t W, int32_t in_cp, int32_t zc,
+                               const void *w0, const float *bias0, float w0_scale, const void *w1, float *y,
+                               int32_t *overflow, esr_stream_t stream) {
+    if (!in || !w0 || !bias0 || !w1 || !y || B <= 0 || H <= 0 || W <= 0 || (zc != 0 && zc != 8) || in_cp != zc + 64 ||
+        !(w0_scale > 0.f))
+        return ESR_EINVAL;
+    if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(w0) | reinterpret_cast<uintptr_t>(w1) |
+         reinterpret_cast<uintptr_t>(y)) & 15)
+        return ESR_EINVAL;
+    X3cParams c = {};
+    c.in = static_cast<const unsigned char *>(in);
+    c.B = B; c.H = H; c.W = W; c.in_cp = in_cp; c.cin = in_cp;
+    c.w = static_cast<const unsigned char *>(w0);
+    c.bias = bias0; c.w_scale_inv = 1.f / w0_scale; c.cout = 64;
+    c.xcd_map = g_tile_map; c.overflow = overflow;
+    c.o.lrelu = 1;
+    c.w1 = static_cast<const unsigned char *>(w1);
+    c.y1 = y;
+    c.zc1 = zc;
+    return x3c_launch_hr1(c, (hipStream_t)stream);
+}
+
+extern "C" int esr_hr1_sum(const float *y, int32_t B, int32_t H, int32_t W, const float *bias1, float scale_inv,
+                           float *out, esr_stream_t stream) {
+    if (!y || !bias1 || !out || B <= 0 || H <= 0 || W <= 0 || (reinterpret_cast<uintptr_t>(y) & 15)) return ESR_EINVAL;
+    return hr1_sum_launch(y, B, H, W, bias1, scale_inv, out, (hipStream_t)stream);
 }

@@ -138,7 +138,9 @@ __device__ __forceinline__ void sfor(F &&f) {
 // the halo tile's transfer sits between two chunks' MFMAs (the weights are a third of the staged bytes at N = 32).
 // TW: output columns per tile (16 by default); OCC: workgroups per CU the register budget is sized for (A/B: 12-column
 // tiles of 3-column waves at three workgroups per CU, 48 KB of LDS each).
-template <int NT, int TS, int DBG = 0, bool RB = false, int CWV = CW, bool WR = false, int TW = TWC, int OCC = 2>
+// HF: HR_conv0 fused with HR_conv1 (x3c_launch_hr1; the epilogue below the main loop).
+template <int NT, int TS, int DBG = 0, bool RB = false, int CWV = CW, bool WR = false, int TW = TWC, int OCC = 2,
+          bool HF = false>
 __global__ __launch_bounds__(64 * (TW / CWV), (TW / CWV) * OCC / 4) void conv_x3c_kernel(X3cParams p) {
     constexpr int TWk = TW, HXk = TWk + 2, IN_RECSk = HYC * HXk, IN_PIECESk = (IN_RECSk + 15) / 16;
     constexpr int IN_Bk = IN_PIECESk * 16 * REC;
@@ -353,6 +355,70 @@ __global__ __launch_bounds__(64 * (TW / CWV), (TW / CWV) * OCC / 4) void conv_x3
     constexpr int ITEMS = 32 * G / 64;  // (pixel, group) items per lane per column
     const int HP = p.H + 2;
     bool ok = true;
+    if constexpr (HF) {
+        // HR_conv0 (+ LeakyReLU) -> HR_conv1 (architecture.py:140-141) without storing HR_conv0's activations: per
+        // pixel, Y[3t + o] = Σ_c W1[o][c][t] · a[c] over HR_conv1's input channels c = [latent slot | activations]
+        // (t = its 3×3 tap, o = its output channel), on the x3 MFMA with the pixels in M (32 per column, lane row ml)
+        // and the 27 (t, o) pairs in N (of 32); esr_hr1_sum then adds Y over each output pixel's 3×3 neighbours.  The
+        // A operand is split from the fp32 activation exactly as store_group would have stored it (and flagged), the
+        // latent slot is read split from the input (prep_hr wrote it there), B = HR_conv1's x3-packed weights.
+        static_assert(NT == 2 && TS == 3 && !RB && !WR, "fused HR_conv1: HR_conv0 is a 3x3 N = 64 conv");
+        const int zc = p.zc1, nks = (zc + 64 + 15) >> 4;
+        const int n1 = ml < 27 ? ml : 0, t1 = n1 / 3, o1 = n1 - 3 * t1;
+#pragma unroll
+        for (int c = 0; c < CWk; ++c) {
+            if (c >= ncw) break;
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = 8 * (r >> 2) + 4 * hl + (r & 3);
+                    s_ep[m * EP_P + nt * 32 + ml] = acc[c][nt][r];
+                }
+            const int x = x0 + CWk * wave + c;  // interior column; padded column x + 1
+            const int R = r0 + 1 + ml;          // this lane's A row: tall padded row of pixel m = ml
+            const int yb = R - (R / HP) * HP - 1;
+            const bool pv = R < rows_tot && yb >= 0 && yb < p.H;
+            const long long pix = (long long)R * rowp + x + 1;
+            f32x16 y = {};
+            for (int ks = 0; ks < nks; ++ks) {
+                const int bc = 16 * ks + 8 * hl;  // first channel of this lane's 8-channel group (HR_conv1's input)
+                f16x8 ah = {}, al = {}, bh = {}, bl = {};
+                if (pv && bc < zc) {
+                    const unsigned char *zp = p.in + pix * pixb + 4LL * bc;
+                    ah = *reinterpret_cast<const f16x8 *>(zp);
+                    al = *reinterpret_cast<const f16x8 *>(zp + 16);
+                } else if (pv && bc - zc < 64) {
+                    const int f = bc - zc;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const float v = lrelu(s_ep[ml * EP_P + f + e] * p.w_scale_inv + p.bias[f + e]);
+                        ah[e] = (_Float16)v;
+                        al[e] = (_Float16)(v - (float)ah[e]);
+                        ok = ok && (fabsf(v) < 65504.f);
+                    }
+                }
+                if (ml < 27) {
+                    const unsigned char *wp = p.w1 + ((long long)(ks * 9 + t1) * 32 + o1) * REC + 32 * hl;
+                    bh = *reinterpret_cast<const f16x8 *>(wp);
+                    bl = *reinterpret_cast<const f16x8 *>(wp + 16);
+                }
+                y = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, y, 0, 0, 0);
+                y = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, y, 0, 0, 0);
+                y = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, y, 0, 0, 0);
+            }
+            // lane (ml, hl) holds Y[m][n = ml] for m = 8(r>>2) + 4hl + (r&3): 32 lanes store one pixel's 128-B record
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = 8 * (r >> 2) + 4 * hl + (r & 3);
+                const int Rm = r0 + 1 + m;
+                const int ym = Rm - (Rm / HP) * HP - 1;
+                if (Rm < rows_tot && ym >= 0 && ym < p.H) p.y1[((long long)Rm * rowp + x + 1) * 32 + ml] = y[r];
+            }
+        }
+        if (!ok && p.overflow) atomicOr(p.overflow, 1);
+        return;
+    }
     float bk[ITEMS][8];
 #pragma unroll
     for (int k = 0; k < ITEMS; ++k) {
@@ -733,6 +799,79 @@ int x3s_launch(const X3cParams &p0, int taps_side, hipStream_t stream, int dbg) 
     return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
 }
 #endif
+
+int x3c_launch_hr1(const X3cParams &p0, hipStream_t stream) {
+    X3cParams p = p0;
+    p.tiles_x = (p.W + TWC - 1) / TWC;
+    p.tiles_y = (p.B * (p.H + 2) - 2 + CT - 1) / CT;
+    const dim3 grid((unsigned)(p.tiles_x * p.tiles_y)), block(NTHR);
+    hipLaunchKernelGGL((conv_x3c_kernel<2, 3, 0, false, CW, false, TWC, 2, true>), grid, block, 0, stream, p);
+    return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+}
+
+namespace {
+
+// HR_conv1's output from the fused HR_conv0 launch's partial products: out[b][o][y][x] = scale_inv · Σ_t
+// Y[b][y + ty][x + tx][3t + o] + bias[o] over the padded Y grid (zero halo).  A block stages the Y records of its
+// 18 × 34 padded window in LDS (27 floats each at an odd pitch: conflict-free column reads; 66 KB, two blocks per CU;
+// all of a thread's 16-B loads in flight before one barrier), each thread sums two pixels (rows ty and ty + 8).
+constexpr int HS_TY = 16, HS_TX = 32, HS_WY = HS_TY + 2, HS_WX = HS_TX + 2, HS_P = 27;
+constexpr int HS_Q = HS_WY * HS_WX * 7;                 // 16-B pieces of the window (7 per 28-float record prefix)
+constexpr int HS_QT = (HS_Q + 255) / 256;               // per thread
+
+__global__ __launch_bounds__(256) void hr1_sum_kernel(const float *y, int H, int W, const float *bias, float sinv,
+                                                      float *out) {
+    __shared__ float s[HS_WY * HS_WX * HS_P];
+    const int b = blockIdx.z, x0 = blockIdx.x * HS_TX, y0 = blockIdx.y * HS_TY;
+    const long long rowp = W + 2;
+    const float *yb = y + (long long)b * (H + 2) * rowp * 32;
+    f32x4 v[HS_QT];
+#pragma unroll
+    for (int k = 0; k < HS_QT; ++k) {
+        const int i = threadIdx.x + 256 * k;
+        const int q = i % 7, rc = i / 7, c = rc % HS_WX, r = rc / HS_WX;
+        const int py = y0 + r, px = x0 + c;
+        v[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (i < HS_Q && py < H + 2 && px < W + 2)
+            v[k] = *reinterpret_cast<const f32x4 *>(yb + ((long long)py * rowp + px) * 32 + 4 * q);
+    }
+#pragma unroll
+    for (int k = 0; k < HS_QT; ++k) {
+        const int i = threadIdx.x + 256 * k;
+        if (i >= HS_Q) break;
+        const int q = i % 7, rc = i / 7;
+        float *d = s + rc * HS_P + 4 * q;
+        d[0] = v[k][0];
+        d[1] = v[k][1];
+        d[2] = v[k][2];
+        if (q < 6) d[3] = v[k][3];
+    }
+    __syncthreads();
+    const int tx = threadIdx.x % HS_TX, xx = x0 + tx;
+    if (xx >= W) return;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int ty = threadIdx.x / HS_TX + 8 * h, yy = y0 + ty;
+        if (yy >= H) break;
+        float a[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const float *rec = s + ((ty + t / 3) * HS_WX + tx + t % 3) * HS_P + 3 * t;
+#pragma unroll
+            for (int o = 0; o < 3; ++o) a[o] += rec[o];
+        }
+#pragma unroll
+        for (int o = 0; o < 3; ++o) out[(((long long)b * 3 + o) * H + yy) * W + xx] = a[o] * sinv + bias[o];
+    }
+}
+
+}  // namespace
+
+int hr1_sum_launch(const float *y, int B, int H, int W, const float *bias, float sinv, float *out, hipStream_t st) {
+    const dim3 grid((unsigned)((W + HS_TX - 1) / HS_TX), (unsigned)((H + HS_TY - 1) / HS_TY), (unsigned)B);
+    hipLaunchKernelGGL(hr1_sum_kernel, grid, dim3(256), 0, st, y, H, W, bias, sinv, out);
+    return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+}
 
 int x3c_launch(const X3cParams &p0, int taps_side, hipStream_t stream, int dbg) {
     X3cParams p = p0;

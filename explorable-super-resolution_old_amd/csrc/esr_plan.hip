@@ -46,6 +46,11 @@ int dispatch(const esr_op &op, hipStream_t s) {
     case ESR_OP_CEM_UP_ADD:
         return esr_cem_up_add((const float *)p[0], (const float *)p[1], (float *)p[2], i[0], i[1], i[2], i[3], i[4],
                               (const float *)p[3], i[5], i[6], st);
+    case ESR_OP_HR_CONVS_X3:
+        return esr_hr_convs_x3(p[0], i[0], i[1], i[2], i[3], i[4], p[1], (const float *)p[2], op.f[0], p[3],
+                               (float *)p[4], (int32_t *)p[5], st);
+    case ESR_OP_HR1_SUM:
+        return esr_hr1_sum((const float *)p[0], i[0], i[1], i[2], (const float *)p[1], op.f[0], (float *)p[2], st);
     default:
         return ESR_EINVAL;
     }

@@ -8,7 +8,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('ESR_AMD_LIB', os.path.join(_HERE, 'libesr_amd.so'))
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 c_int = ctypes.c_int32
 c_float = ctypes.c_float
@@ -33,7 +33,8 @@ class EsrOp(ctypes.Structure):
                 ('o', ConvOut)]
 
 
-OP_CONV3X3, OP_CONV3X3_X3, OP_UPCONV, OP_UPCONV_X3, OP_PREP, OP_CEM_DOWN, OP_CEM_INV, OP_CEM_UP_ADD = range(1, 9)
+(OP_CONV3X3, OP_CONV3X3_X3, OP_UPCONV, OP_UPCONV_X3, OP_PREP, OP_CEM_DOWN, OP_CEM_INV, OP_CEM_UP_ADD, OP_HR_CONVS_X3,
+ OP_HR1_SUM) = range(1, 11)
 
 # name -> argtypes (all return int32 status unless listed in _RESTYPES)
 _SIGNATURES = {
@@ -48,6 +49,9 @@ _SIGNATURES = {
                            ctypes.POINTER(ConvOut), c_void_p, c_void_p],
     'esr_upconv2x_phase_fwd_x3': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_int,
                                   c_int, c_int, ctypes.POINTER(ConvOut), c_void_p, c_void_p],
+    'esr_hr_convs_x3': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p,
+                        c_void_p, c_void_p],
+    'esr_hr1_sum': [c_void_p, c_int, c_int, c_int, c_void_p, c_float, c_void_p, c_void_p],
     'esr_cem_down': [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int,
                      c_void_p],
     'esr_cem_inv': [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p],

@@ -516,6 +516,7 @@ class _Workspace:
         self.HR = [z(B, sf * H + 2, sf * W + 2, self.hr_cp) for _ in range(2)]
         self.lr = z(B, 3, H, W)
         self.overflow = torch.zeros(1, device=dev, dtype=torch.int32)
+        self.Y = None  # x3 inference: HR_conv1's per-tap partial products (esr_hr_convs_x3), allocated on first use
 
 
 def _workspace(net, dev, B, H, W, latent, precision):
@@ -595,6 +596,12 @@ class _Recorder:
     def esr_cem_up_add(self, q, gen, out, B, H, W, sf, ph, w, kd, M, stream):
         return self._add(_lib.OP_CEM_UP_ADD, [q, gen, out, w], [B, H, W, sf, ph, kd, M])
 
+    def esr_hr_convs_x3(self, inp, B, H, W, in_cp, zc, w0, bias0, w0_scale, w1, y, ovf, stream):
+        return self._add(_lib.OP_HR_CONVS_X3, [inp, w0, bias0, w1, y, ovf], [B, H, W, in_cp, zc], [w0_scale])
+
+    def esr_hr1_sum(self, y, B, H, W, bias1, scale_inv, out, stream):
+        return self._add(_lib.OP_HR1_SUM, [y, bias1, out], [B, H, W], [scale_inv])
+
 
 class _OpPlan:
     """One recorded inference forward.  Between calls only the model-input pointer and the output pointer change;
@@ -661,6 +668,9 @@ def profile_records(prof):
 
 
 USE_OP_LISTS = os.environ.get('ESR_OP_LISTS', '1') != '0'
+# x3 inference: HR_conv0 and HR_conv1 as esr_hr_convs_x3 + esr_hr1_sum (ESR_FUSE_HR1=0: the two convs as launched for
+# training, HR_conv1 on the narrow-N kernel)
+FUSE_HR1 = os.environ.get('ESR_FUSE_HR1', '1') != '0'
 
 
 def _plan_key(net, x, cem, precision, pk):
@@ -671,7 +681,7 @@ def _plan_key(net, x, cem, precision, pk):
         cem_key = (id(cem), pre_pad, int(cem.margins_LR),
                    cem.DownscaleOP.Filter_OP.weight.data_ptr(), cem.Conv_LR_with_Inv_hTh_OP.Filter_OP.weight.data_ptr(),
                    cem.Upscale_OP.Filter_OP.weight.data_ptr())
-    return (id(pk), getattr(pk, 'version', 0), precision, tuple(x.shape), str(x.device), cem_key, a)
+    return (id(pk), getattr(pk, 'version', 0), precision, tuple(x.shape), str(x.device), cem_key, a, FUSE_HR1)
 
 
 def _planned_forward(net, x, cem, precision):
@@ -844,11 +854,36 @@ def _forward(net, x, cem, precision, train_ws=None, rec=None):
             if ev is not None:
                 ev.record()
     HH, WW = sf * H, sf * W
-    conv(HR0, HH, WW, hcp, hcp, pk.hr0, 64, _conv_out(HR1, hcp, zc, HH, WW, True), nl + 64)
     gen = torch.empty(Bn, 3, HH, WW, device=dev, dtype=torch.float32)
     if rec is not None:
         rec.keep.append(gen)
-    conv(HR1, HH, WW, hcp, hcp, pk.hr1, 3, _conv_out(gen, 0, 0, HH, WW, False, planar=1), nl + 64)
+    if x3 and train_ws is None and FUSE_HR1:
+        # HR_conv0 + HR_conv1 without HR_conv0's activations in memory (esr_hr_convs_x3 / esr_hr1_sum); training keeps
+        # them (the backward reads them)
+        if ws.Y is None:
+            ws.Y = torch.zeros(Bn, HH + 2, WW + 2, 32, device=dev, dtype=torch.float32)  # halo stays zero
+        w0x, s0 = pk.hr0.x3()
+        w1x, s1 = pk.hr1.x3()
+        fl0 = 2.0 * Bn * HH * WW * 9 * (nl + 64) * 64
+        fl1 = 2.0 * Bn * HH * WW * 9 * (nl + 64) * 3
+        if rec is not None:
+            rec.keep += [w0x, w1x]
+            rec.tag(tagp + 'hr_conv0_hr1', fl0)
+        ev = _prof_begin(prof, tagp + 'hr_conv0_hr1', fl0) if rec is None and prof is not None else None
+        _lib.check(lib.esr_hr_convs_x3(HR0.data_ptr(), Bn, HH, WW, hcp, zc, w0x.data_ptr(), pk.hr0.bias_s.data_ptr(),
+                                       s0, w1x.data_ptr(), ws.Y.data_ptr(), ovf, stream), 'esr_hr_convs_x3')
+        if ev is not None:
+            ev.record()
+        if rec is not None:
+            rec.tag(tagp + 'hr1_sum', fl1)
+        ev = _prof_begin(prof, tagp + 'hr1_sum', fl1) if rec is None and prof is not None else None
+        _lib.check(lib.esr_hr1_sum(ws.Y.data_ptr(), Bn, HH, WW, pk.hr1.bias.data_ptr(), 1.0 / (s1 * A),
+                                   gen.data_ptr(), stream), 'esr_hr1_sum')
+        if ev is not None:
+            ev.record()
+    else:
+        conv(HR0, HH, WW, hcp, hcp, pk.hr0, 64, _conv_out(HR1, hcp, zc, HH, WW, True), nl + 64)
+        conv(HR1, HH, WW, hcp, hcp, pk.hr1, 3, _conv_out(gen, 0, 0, HH, WW, False, planar=1), nl + 64)
     if cem is None:
         return gen, ws
     return cem_apply(lib, cem, gen, ws.lr, Bn, H, W, sf * m if pre_pad else 0, stream, sf), ws

@@ -144,6 +144,23 @@ int esr_upconv2x_phase_fwd_x3(const void *in, int32_t B, int32_t H, int32_t W, i
                               const void *w_packed, const float *bias, float w_scale, int32_t cout, int32_t py,
                               int32_t px, const esr_conv_out *o, int32_t *overflow, esr_stream_t stream);
 
+/* HR_conv0 + LeakyReLU and HR_conv1 of RRDBNet (architecture.py:140-141, 172-174) in the x3 inference forward,
+ * without HR_conv0's activations ever reaching memory (replaces esr_conv3x3_fwd_x3 of HR_conv0 into a split buffer
+ * followed by HR_conv1's narrow-N launch, which re-read that 4 B/channel buffer).
+ * esr_hr_convs_x3: the HR_conv0 conv (in: the split HR-grid buffer, in_cp = zc + 64 channels = [latent slot of zc
+ * channels (0 or 8, prep_hr's Z) | 64 upsampled features]; w0/bias0/w0_scale as esr_conv3x3_fwd_x3 with cout 64) whose
+ * epilogue computes, per interior pixel p, y[p][3t + o] = Σ_c W1[o][c][t] · a[p][c] for HR_conv1's 9 taps t and 3
+ * outputs o over its input a = [the latent slot of `in` | lrelu(HR_conv0)] (w1: HR_conv1's x3-packed weights, n_pad
+ * 32, scaled like any x3 weight; x3 products on the matrix cores).  y: padded [B][H+2][W+2][32] fp32 (27 used), 16-B
+ * aligned, halo zero (never written).  *overflow |= 1 if an activation is not representable in f16 (as a split store).
+ * esr_hr1_sum: out NCHW [B][3][H][W] = scale_inv · Σ_{ty,tx} y[b][y+ty][x+tx][3(3ty+tx) + o] + bias1[o]
+ * (scale_inv = 1/(w1_scale · activation scale)).  Equal to the unfused pair up to the summation order. */
+int esr_hr_convs_x3(const void *in, int32_t B, int32_t H, int32_t W, int32_t in_cp, int32_t zc, const void *w0,
+                    const float *bias0, float w0_scale, const void *w1, float *y, int32_t *overflow,
+                    esr_stream_t stream);
+int esr_hr1_sum(const float *y, int32_t B, int32_t H, int32_t W, const float *bias1, float scale_inv, float *out,
+                esr_stream_t stream);
+
 /* ---- training / Z-optimisation backward (esr_train.hip) ------------------------------------------------------------
  * The data gradient of every conv is esr_conv3x3_fwd run with rot180, in/out-swapped packed weights (host-side
  * repacking), i.e. the backward of conv_block (block.py:129-156) for loss.backward() in
@@ -340,7 +357,9 @@ int esr_dconv_wgrad(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_t
  *               i: B, nz, h, w, sf, m, first_cp, first_lr_off, zlr_cp[4], n_zlr, zhr_cp[2], n_zhr, split
  *   CEM_DOWN    p: gen, lr, r, w_down    i: B, H, W, sf, ph, kd, negate
  *   CEM_INV     p: r, q, w_inv           i: B, H, W, ki
- *   CEM_UP_ADD  p: q, gen, out, w_up     i: B, H, W, sf, ph, kd, M                              */
+ *   CEM_UP_ADD  p: q, gen, out, w_up     i: B, H, W, sf, ph, kd, M
+ *   HR_CONVS_X3 p: in, w0, bias0, w1, y, overflow   i: B, H, W, in_cp, zc   f0: w0_scale
+ *   HR1_SUM     p: y, bias1, out         i: B, H, W                  f0: scale_inv               */
 enum esr_op_kind {
     ESR_OP_CONV3X3 = 1,
     ESR_OP_CONV3X3_X3 = 2,
@@ -350,6 +369,8 @@ enum esr_op_kind {
     ESR_OP_CEM_DOWN = 6,
     ESR_OP_CEM_INV = 7,
     ESR_OP_CEM_UP_ADD = 8,
+    ESR_OP_HR_CONVS_X3 = 9,
+    ESR_OP_HR1_SUM = 10,
 };
 typedef struct esr_op {
     int32_t kind;

@@ -239,6 +239,35 @@ def test_full_size_rrdb23_cem_vs_oracle(gpu_device, latent, precision):
     assert mse < 1e-8
 
 
+@pytest.mark.parametrize('latent', [False, True])
+@pytest.mark.parametrize('B,h,w', [(2, 9, 13), (3, 16, 5)])
+def test_hr_convs_fused_equals_unfused(gpu_device, monkeypatch, latent, B, h, w):
+    """x3 inference runs HR_conv0 + HR_conv1 as esr_hr_convs_x3 + esr_hr1_sum (HR_conv0's activations never stored;
+    HR_conv1's 27 per-tap partial products from HR_conv0's epilogue, summed over each pixel's 3×3 neighbours): equal to
+    the two convs as the training forward launches them (HR_conv1 on the narrow-N kernel) up to the summation order,
+    and on the float64 oracle.  Ragged widths (tiles past the image edge), the latent slot, the CEM pre-pad."""
+    model, params = _big_model(1, latent, gpu_device, 'x3', seed=41)
+    model.eval()
+    g = torch.Generator().manual_seed(42)
+    x = torch.rand(B, 3, h, w, generator=g)
+    if latent:
+        z = 2 * torch.rand(B, 3, 4 * h, 4 * w, generator=g) - 1
+        x = torch.cat([z.reshape(B, 48, h, w), x], 1)
+    xd = x.to(gpu_device)
+    outs = {}
+    for fuse in (True, False):
+        monkeypatch.setattr(engine, 'FUSE_HR1', fuse)
+        with torch.no_grad():
+            outs[fuse] = model(xd).cpu()
+    err = normwise_rel(outs[True], outs[False])
+    ref = O.sr_forward(x, O.strip_prefix(params), 1, latent, O.cem_design(4), pre_pad=True)
+    err_ref = normwise_rel(outs[True], ref)
+    print('fused vs unfused %.2e, fused vs float64 oracle %.2e, unfused vs oracle %.2e'
+          % (err, err_ref, normwise_rel(outs[False], ref)))
+    assert err < 2e-6
+    assert err_ref < 1e-5
+
+
 @pytest.mark.parametrize('precision', ['x3', 'f32'])
 @pytest.mark.parametrize('latent', [False, True])
 def test_c2_production_grid_vs_oracle_and_batch1(gpu_device, latent, precision):

@@ -67,7 +67,10 @@ def main():
         return
     for ev in prof.events():
         if ev.name not in ('aten::copy_', 'aten::leaky_relu_backward', 'aten::add', 'aten::add_', 'aten::contiguous',
-                           'aten::clone', 'aten::leaky_relu', 'aten::mul', 'aten::sub'):
+                           'aten::clone', 'aten::leaky_relu', 'aten::mul', 'aten::sub', 'aten::cat', 'aten::sum',
+                           'aten::mean', 'aten::norm', 'aten::linalg_vector_norm', 'aten::where', 'aten::pow',
+                           'aten::div', 'aten::abs', 'aten::lerp_', 'aten::addcmul_', 'aten::index_select',
+                           'aten::index', 'aten::mul_', 'aten::zero_', 'aten::fill_', 'aten::sqrt', 'aten::clamp'):
             continue
         shapes = ev.input_shapes or []
         numel = 0

@@ -33,5 +33,5 @@ print('window %.1f ms, busy %.1f ms (%.1f%%), per step: span %.1f busy %.1f' % (
                                                                              span / steps, busy / 1e6 / steps))
 tot = sum(v[1] for v in agg.values())
 print('| kernel | calls/step | ms/step | share |\n|---|---|---|---|')
-for k, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:30]:
+for k, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:int(sys.argv[4]) if len(sys.argv) > 4 else 30]:
     print('| %s | %d | %.2f | %.3f |' % (k, c // steps, t / steps, t / tot))
