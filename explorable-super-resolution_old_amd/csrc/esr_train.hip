@@ -844,18 +844,29 @@ __global__ void wgrad_reduce_kernel(const float *partial, int splits, long long 
 }
 
 // max |x| over a C-channel fp32 slice, OR-ed into *amax as float bits (non-negative floats order as unsigned ints)
+// max |x| over a padded NHWC channel slice.  A block walks whole image rows (blockIdx.x + k·gridDim.x over the B·H
+// rows), each row's W × C slice with 16-B loads where the slice is 4-aligned: the index math is per row, not per
+// element (the per-element 64-bit divisions held it at ~0.5 TB/s, 120 µs per config-5 trunk gradient).
 __global__ void grad_amax_kernel(const float *x, int cp, int coff, int C, int B, int H, int W, unsigned *amax) {
     __shared__ float red[NT / 64];
-    const long long n = (long long)B * H * W * C;
     float m = 0.f;
-    for (long long idx = (long long)blockIdx.x * NT + threadIdx.x; idx < n; idx += (long long)gridDim.x * NT) {
-        const int c = idx % C;
-        long long q = idx / C;
-        const int xx = q % W;
-        q /= W;
-        const int y = q % H;
-        const int b = q / H;
-        m = fmaxf(m, fabsf(x[(((long long)b * (H + 2) + y + 1) * (W + 2) + xx + 1) * cp + coff + c]));
+    const bool v4 = (C % 4 == 0) && (coff % 4 == 0) && (cp % 4 == 0) && ((reinterpret_cast<uintptr_t>(x) & 15) == 0);
+    const int C4 = C / 4;
+    for (long long row = blockIdx.x; row < (long long)B * H; row += gridDim.x) {
+        const long long b = row / H, y = row - b * H;
+        const float *base = x + ((b * (H + 2) + y + 1) * (W + 2) + 1) * cp + coff;
+        if (v4) {
+            for (int k = threadIdx.x; k < W * C4; k += NT) {
+                const int xx = k / C4, c4 = k - xx * C4;
+                const f32x4 v = *reinterpret_cast<const f32x4 *>(base + (long long)xx * cp + 4 * c4);
+                m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+            }
+        } else {
+            for (int k = threadIdx.x; k < W * C; k += NT) {
+                const int xx = k / C, c = k - xx * C;
+                m = fmaxf(m, fabsf(base[(long long)xx * cp + c]));
+            }
+        }
     }
     for (int s = 32; s >= 1; s >>= 1) m = fmaxf(m, __shfl_xor(m, s));
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
@@ -946,6 +957,38 @@ __global__ void lrelu_bwd_kernel(float *d, int d_cp, int d_coff, const float *y,
     if (!(yv > 0.f)) d[pix * d_cp + d_coff + c] *= 0.2f;
 }
 
+// lrelu_bwd_kernel on 8-channel groups (C, offsets and pitches multiples of 8, 16-B aligned; y split or fp32): two
+// 16-B loads of d and of y per thread and one index computation per group instead of per element
+__global__ void lrelu_bwd8_kernel(float *d, int d_cp, int d_coff, const float *y, int y_cp, int y_coff, int C, int B,
+                                  int H, int W, int y_split) {
+    const long long idx = (long long)blockIdx.x * NT + threadIdx.x;
+    const int G = C / 8;
+    if (idx >= (long long)B * H * W * G) return;
+    int g;
+    const long long pix = pix_index(idx, G, B, H, W, &g);
+    float yv[8];
+    if (y_split) {
+        const unsigned char *q = reinterpret_cast<const unsigned char *>(y) + (pix * y_cp + y_coff + 8 * g) * 4;
+        const f16x8 h = *reinterpret_cast<const f16x8 *>(q), l = *reinterpret_cast<const f16x8 *>(q + 16);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) yv[e] = (float)h[e] + (float)l[e];
+    } else {
+        const f32x4 a = *reinterpret_cast<const f32x4 *>(y + pix * y_cp + y_coff + 8 * g);
+        const f32x4 b = *reinterpret_cast<const f32x4 *>(y + pix * y_cp + y_coff + 8 * g + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { yv[e] = a[e]; yv[e + 4] = b[e]; }
+    }
+    f32x4 *dp = reinterpret_cast<f32x4 *>(d + pix * d_cp + d_coff + 8 * g);
+    f32x4 a = dp[0], b = dp[1];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        if (!(yv[e] > 0.f)) a[e] *= 0.2f;
+        if (!(yv[e + 4] > 0.f)) b[e] *= 0.2f;
+    }
+    dp[0] = a;
+    dp[1] = b;
+}
+
 __global__ void axpby_kernel(float *out, int o_cp, int o_coff, float a, const float *x1, int x1_cp, int x1_coff,
                              float b, const float *x2, int x2_cp, int x2_coff, int C, int B, int H, int W) {
     const long long idx = (long long)blockIdx.x * NT + threadIdx.x;
@@ -1030,6 +1073,102 @@ struct AdjParams {
     int fast;         // interior fast path (default; esr_cem_adjoint flags bit 1 = generic)
 };
 
+// The border outputs of the stride-1 adjoint (row or column 0 / L-1, where the replicate clamp lands whole tap rows /
+// columns of g): one block per output, the generic per-tap range sums split over the block's threads (tap q = thread
+// + 256 k) and added in a fixed tree order.  (One thread per border output ran 16 k threads of ~K²·K/2 serial adds each
+// for the 41² inverse filter: ≈5 ms per config-5 iteration.)
+__global__ __launch_bounds__(256) void cem_adjoint_border_kernel(AdjParams p) {
+    __shared__ float red[256];
+    const int nb = 2 * p.Nx + 2 * (p.Ny - 2);
+    const long long plane = blockIdx.x / nb;
+    const int k = (int)(blockIdx.x - plane * nb);
+    int i, j;
+    if (k < 2 * p.Nx) {
+        i = k < p.Nx ? 0 : p.Ny - 1;
+        j = k < p.Nx ? k : k - p.Nx;
+    } else {
+        i = 1 + (k - 2 * p.Nx) / 2;
+        j = ((k - 2 * p.Nx) & 1) ? p.Nx - 1 : 0;
+    }
+    const int ky = p.os * i + p.oc, kx = p.os * j + p.oc, pd = p.K / 2;
+    const float *g = p.g + plane * p.Oy * p.Ox;
+    float acc = 0.f;
+    for (int q = threadIdx.x; q < p.K * p.K; q += 256) {
+        const int uy = q / p.K, ux = q - uy * p.K;
+        int ylo, yhi, xlo, xhi;
+        if (!o_range(ky, uy, p.s, p.c, pd, p.Ly, p.Oy, &ylo, &yhi)) continue;
+        if (!o_range(kx, ux, p.s, p.c, pd, p.Lx, p.Ox, &xlo, &xhi)) continue;
+        float sg = 0.f;
+        for (int oy = ylo; oy <= yhi; ++oy)
+            for (int ox = xlo; ox <= xhi; ++ox) sg += g[(long long)oy * p.Ox + ox];
+        acc += p.w[q] * sg;
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if (threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        float *o = p.out + (plane * p.Ny + i) * p.Nx + j;
+        *o = p.accumulate ? *o + p.alpha * red[0] : p.alpha * red[0];
+    }
+}
+
+// Stride-1 adjoint (the inverse filter's, CEMnet.py:149-151: s = os = 1, oc = 0), interior outputs, tiled as
+// cem_inv_tiled: out[k] = Σ_u w[u] · g0[k - c + pd - u] with g0 = g zero-extended, i.e. a correlation of g0 with the
+// taps reversed.  A 64 × 16 block of outputs stages its (16 + K - 1) × (64 + K - 1) g0 window in LDS once; each thread
+// slides a 4-wide register window along every tap row.  Taps are visited in the generic loop's order (uy, then ux,
+// ascending: window rows and columns descending), so interior outputs are bitwise those of cem_adjoint_kernel; border
+// outputs (where the replicate clamp adds terms) are left to cem_adjoint_border_kernel.  The per-output loop on the
+// inverse filter's 41² taps of the KernelGAN-recipe kernel took 9.6 ms per config-5 iteration.
+__global__ __launch_bounds__(256) void cem_adjoint_s1_tiled(AdjParams p) {
+    extern __shared__ float smem[];
+    const int K = p.K, pd = K / 2, WP = 64 + K - 1, WR = 16 + K - 1;
+    float *sw = smem;                           // [WR][WP]
+    const int j0 = blockIdx.x * 64, i0 = blockIdx.y * 16;
+    const long long plane = blockIdx.z;
+    const float *g = p.g + plane * p.Oy * p.Ox;
+    const int org = -p.c - pd;                  // window origin relative to the output index (k - c + pd - (K - 1))
+    for (int y = threadIdx.x / 64; y < WR; y += 4) {
+        const int gy = i0 + y + org;
+        for (int x = threadIdx.x % 64; x < WP; x += 64) {
+            const int gx = j0 + x + org;
+            sw[y * WP + x] = (gy >= 0 && gy < p.Oy && gx >= 0 && gx < p.Ox) ? g[(long long)gy * p.Ox + gx] : 0.f;
+        }
+    }
+    __syncthreads();
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    for (int uy = 0; uy < K; ++uy) {
+        // window row K-1-uy, columns 4tx + (K-1-ux) (+ e for output e): ux ascending = columns descending
+        const float *sr = sw + (ty + K - 1 - uy) * WP + 4 * tx;
+        const float *wr = p.w + uy * K;  // wave-uniform: scalar loads
+        float r1 = sr[K - 1 + 1], r2 = sr[K - 1 + 2], r3 = sr[K - 1 + 3];
+        for (int ux = 0; ux < K; ++ux) {
+            const int v = K - 1 - ux;
+            const float r0 = sr[v], w = wr[ux];
+            a0 += w * r0;
+            a1 += w * r1;
+            a2 += w * r2;
+            a3 += w * r3;
+            r3 = r2;
+            r2 = r1;
+            r1 = r0;
+        }
+    }
+    const int i = i0 + ty;
+    if (i >= p.Ny || i == 0 || i == p.Ly - 1) return;
+    float *o = p.out + (plane * p.Ny + i) * p.Nx;
+    const float a[4] = {a0, a1, a2, a3};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int j = j0 + 4 * tx + e;
+        if (j >= p.Nx || j == 0 || j == p.Lx - 1) continue;
+        o[j] = p.accumulate ? o[j] + p.alpha * a[e] : p.alpha * a[e];
+    }
+}
+
 
 __global__ __launch_bounds__(NT) void cem_adjoint_kernel(AdjParams p) {
     __shared__ float sw[64 * 64];
@@ -1086,33 +1225,37 @@ __global__ __launch_bounds__(NT) void cem_adjoint_kernel(AdjParams p) {
 // ---------------------------------------------------------------------------------------------------------------------
 // generator input adjoint (Z optimisation): replicate pre-pad adjoint + bilinear ↓sf adjoint
 // ---------------------------------------------------------------------------------------------------------------------
+// One thread per output PIXEL, all C channels (the HR / LR gradient slots are C consecutive channels of a pixel
+// record of hr_cp / lr_cp floats: one sector per pixel instead of one per (pixel, channel) — the per-channel threads
+// re-fetched each 288-B HR record three times, 2.4 ms per config-5 iteration).  Same adds in the same order per output.
 __global__ void input_adjoint_kernel(const float *d_hr, int hr_cp, int hr_coff, const float *d_lr, int lr_cp,
                                      int lr_coff, int sf, const float *d_pl, int C, int B, int Hp, int Wp, int M,
                                      float *out) {
     const int Ho = Hp - 2 * M, Wo = Wp - 2 * M;
     const long long idx = (long long)blockIdx.x * NT + threadIdx.x;
-    if (idx >= (long long)B * C * Ho * Wo) return;
+    if (idx >= (long long)B * Ho * Wo) return;
     const int X = idx % Wo;
     const int Y = (idx / Wo) % Ho;
-    const int c = (idx / ((long long)Wo * Ho)) % C;
-    const int b = idx / ((long long)Wo * Ho * C);
+    const int b = idx / ((long long)Wo * Ho);
     // padded positions that the replicate pad clamps onto (Y, X)
     const int y0 = Y == 0 ? 0 : Y + M, y1 = Y == Ho - 1 ? Hp - 1 : Y + M;
     const int x0 = X == 0 ? 0 : X + M, x1 = X == Wo - 1 ? Wp - 1 : X + M;
     const int Hl = sf > 0 ? Hp / sf : 0, Wl = sf > 0 ? Wp / sf : 0;
-    float v = 0.f;
-    for (int yp = y0; yp <= y1; ++yp)
-        for (int xp = x0; xp <= x1; ++xp) {
-            if (d_hr) v += d_hr[(((long long)b * (Hp + 2) + yp + 1) * (Wp + 2) + xp + 1) * hr_cp + hr_coff + c];
-            if (d_pl) v += d_pl[(((long long)b * C + c) * Hp + yp) * Wp + xp];
-            if (d_lr) {  // bilinear ↓sf, align_corners=False: sf = 4: mean of the central 2×2 of each 4×4 block; sf = 2: of the 2×2 block
-                const int ry = yp % sf, rx = xp % sf;
-                if ((ry == sf / 2 - 1 || ry == sf / 2) && (rx == sf / 2 - 1 || rx == sf / 2))
-                    v += 0.25f * d_lr[(((long long)b * (Hl + 2) + yp / sf + 1) * (Wl + 2) + xp / sf + 1) * lr_cp +
-                                      lr_coff + c];
+    for (int c = 0; c < C; ++c) {
+        float v = 0.f;
+        for (int yp = y0; yp <= y1; ++yp)
+            for (int xp = x0; xp <= x1; ++xp) {
+                if (d_hr) v += d_hr[(((long long)b * (Hp + 2) + yp + 1) * (Wp + 2) + xp + 1) * hr_cp + hr_coff + c];
+                if (d_pl) v += d_pl[(((long long)b * C + c) * Hp + yp) * Wp + xp];
+                if (d_lr) {  // bilinear ↓sf, align_corners=False: sf = 4: mean of the central 2×2 of each 4×4 block; sf = 2: of the 2×2 block
+                    const int ry = yp % sf, rx = xp % sf;
+                    if ((ry == sf / 2 - 1 || ry == sf / 2) && (rx == sf / 2 - 1 || rx == sf / 2))
+                        v += 0.25f * d_lr[(((long long)b * (Hl + 2) + yp / sf + 1) * (Wl + 2) + xp / sf + 1) * lr_cp +
+                                          lr_coff + c];
+                }
             }
-        }
-    out[idx] = v;
+        out[(((long long)b * C + c) * Ho + Y) * Wo + X] = v;
+    }
 }
 
 extern "C" int esr_conv3x3_wgrad(const float *in, int32_t in_cp, int32_t cin, int32_t flags, const float *dout,
@@ -1196,8 +1339,8 @@ extern "C" int esr_wgrad_reduce2(const float *partial, int32_t splits, int64_t n
 extern "C" int esr_grad_amax(const float *x, int32_t cp, int32_t coff, int32_t C, int32_t B, int32_t H, int32_t W,
                              uint32_t *amax, esr_stream_t stream) {
     if (!x || !amax || C <= 0 || B <= 0 || H <= 0 || W <= 0 || coff + C > cp) return ESR_EINVAL;
-    const long long n = (long long)B * H * W * C;
-    const unsigned grid = (unsigned)((n + NT - 1) / NT < 1024 ? (n + NT - 1) / NT : 1024);
+    const long long rows = (long long)B * H;
+    const unsigned grid = (unsigned)(rows < 2048 ? rows : 2048);
     hipLaunchKernelGGL(grad_amax_kernel, dim3(grid), dim3(NT), 0, (hipStream_t)stream, x, cp, coff, C, B, H, W, amax);
     return launched();
 }
@@ -1215,20 +1358,30 @@ extern "C" int esr_axpby_gs(void *out, int32_t o_cp, int32_t o_coff, int32_t o_s
     return launched();
 }
 
+static int lrelu_bwd_launch(float *d, int d_cp, int d_coff, const float *y, int y_cp, int y_coff, int C, int B, int H,
+                            int W, int y_split, hipStream_t st) {
+    const bool g8 = C % 8 == 0 && d_cp % 8 == 0 && d_coff % 8 == 0 && y_cp % 8 == 0 && y_coff % 8 == 0 &&
+                    ((reinterpret_cast<uintptr_t>(d) | reinterpret_cast<uintptr_t>(y)) & 15) == 0;
+    if (g8)
+        hipLaunchKernelGGL(lrelu_bwd8_kernel, dim3(nblocks((long long)B * H * W * (C / 8))), dim3(NT), 0, st, d, d_cp,
+                           d_coff, y, y_cp, y_coff, C, B, H, W, y_split);
+    else
+        hipLaunchKernelGGL(lrelu_bwd_kernel, dim3(nblocks((long long)B * H * W * C)), dim3(NT), 0, st, d, d_cp, d_coff,
+                           y, y_cp, y_coff, C, B, H, W, y_split);
+    return launched();
+}
+
 extern "C" int esr_lrelu_bwd(float *d, int32_t d_cp, int32_t d_coff, const float *y, int32_t y_cp, int32_t y_coff,
                              int32_t C, int32_t B, int32_t H, int32_t W, esr_stream_t stream) {
     if (!d || !y || C <= 0 || B <= 0 || H <= 0 || W <= 0) return ESR_EINVAL;
-    hipLaunchKernelGGL(lrelu_bwd_kernel, dim3(nblocks((long long)B * H * W * C)), dim3(NT), 0, (hipStream_t)stream, d,
-                       d_cp, d_coff, y, y_cp, y_coff, C, B, H, W, 0);
-    return launched();
+    return lrelu_bwd_launch(d, d_cp, d_coff, y, y_cp, y_coff, C, B, H, W, 0, (hipStream_t)stream);
 }
 
 extern "C" int esr_lrelu_bwd_split(float *d, int32_t d_cp, int32_t d_coff, const void *y, int32_t y_cp,
                                    int32_t y_coff, int32_t C, int32_t B, int32_t H, int32_t W, esr_stream_t stream) {
     if (!d || !y || C <= 0 || B <= 0 || H <= 0 || W <= 0 || y_cp % 8) return ESR_EINVAL;
-    hipLaunchKernelGGL(lrelu_bwd_kernel, dim3(nblocks((long long)B * H * W * C)), dim3(NT), 0, (hipStream_t)stream, d,
-                       d_cp, d_coff, static_cast<const float *>(y), y_cp, y_coff, C, B, H, W, 1);
-    return launched();
+    return lrelu_bwd_launch(d, d_cp, d_coff, static_cast<const float *>(y), y_cp, y_coff, C, B, H, W, 1,
+                            (hipStream_t)stream);
 }
 
 extern "C" int esr_axpby(float *out, int32_t o_cp, int32_t o_coff, float a, const float *x1, int32_t x1_cp,
@@ -1266,6 +1419,14 @@ extern "C" int esr_cem_adjoint(const float *g, int32_t planes, int32_t Oy, int32
     p.g = g; p.out = out; p.w = w; p.K = K; p.s = s; p.c = c; p.Ly = Ly; p.Lx = Lx; p.Oy = Oy; p.Ox = Ox;
     p.os = os; p.oc = oc; p.Ny = (Ly - oc + os - 1) / os; p.Nx = (Lx - oc + os - 1) / os; p.planes = planes;
     p.alpha = alpha; p.accumulate = flags & 1; p.fast = !(flags & 2);
+    if (p.fast && s == 1 && os == 1 && oc == 0 && Ly >= 3 && Lx >= 3) {  // the inverse filter's adjoint: tiled
+        const size_t lds = (size_t)(16 + K - 1) * (64 + K - 1) * sizeof(float);
+        hipLaunchKernelGGL(cem_adjoint_s1_tiled, dim3((p.Nx + 63) / 64, (p.Ny + 15) / 16, planes), dim3(256), lds,
+                           (hipStream_t)stream, p);
+        hipLaunchKernelGGL(cem_adjoint_border_kernel, dim3((unsigned)((long long)planes * (2 * p.Nx + 2 * (p.Ny - 2)))),
+                           dim3(256), 0, (hipStream_t)stream, p);
+        return launched();
+    }
     hipLaunchKernelGGL(cem_adjoint_kernel, dim3(nblocks((long long)planes * p.Ny * p.Nx)), dim3(NT), 0,
                        (hipStream_t)stream, p);
     return launched();
@@ -1277,7 +1438,7 @@ extern "C" int esr_input_adjoint(const float *d_hr, int32_t hr_cp, int32_t hr_co
     if (!out || C <= 0 || B <= 0 || M < 0 || Hp - 2 * M <= 0 || Wp - 2 * M <= 0) return ESR_EINVAL;
     if (d_hr && hr_coff + C > hr_cp) return ESR_EINVAL;
     if (d_lr && ((sf != 4 && sf != 2) || Hp % sf || Wp % sf || lr_coff + C > lr_cp)) return ESR_EINVAL;
-    const long long n = (long long)B * C * (Hp - 2 * M) * (Wp - 2 * M);
+    const long long n = (long long)B * (Hp - 2 * M) * (Wp - 2 * M);
     hipLaunchKernelGGL(input_adjoint_kernel, dim3(nblocks(n)), dim3(NT), 0, (hipStream_t)stream, d_hr, hr_cp, hr_coff,
                        d_lr, lr_cp, lr_coff, sf, d_pl, C, B, Hp, Wp, M, out);
     return launched();

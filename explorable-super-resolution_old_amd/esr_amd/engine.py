@@ -182,9 +182,12 @@ FOLD_TERMS = 4  # a folded phase tap sums at most 2 × 2 of the 3×3 taps
 
 def fold_terms(py, px, f=2):
     """Output phase (py, px) of a nearest-×f upconv: for each of its 2×2 LR taps (a, b), the 3×3 taps (y, x) summed
-    into it, in the fixed order (row-major) in which fold_upconv_phase and GatherPlan.reg_sum add them."""
+    into it, in the fixed order in which fold_upconv_phase and GatherPlan.reg_sum add them: x-major, i.e. the order of
+    round 3's einsum fold on the GPU (tools/fold_order_probe.py), so that the folded weights are bitwise the same.  (A
+    near-cancelling discriminator bias gradient of the config-3 grid test, an exact-fp32 run, moved from 81 % to 125 %
+    of its bound under the row-major order: profiles/r4_c3_fold_order.txt.)"""
     Fy, Fx = _FOLDS[f][py][0], _FOLDS[f][px][0]
-    return [[[(y, x) for y in range(3) for x in range(3) if Fy[a][y] and Fx[b][x]] for b in range(2)] for a in range(2)]
+    return [[[(y, x) for x in range(3) for y in range(3) if Fy[a][y] and Fx[b][x]] for b in range(2)] for a in range(2)]
 
 
 def fold_term_images(w, py, px, f=2):

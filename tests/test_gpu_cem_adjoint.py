@@ -30,6 +30,10 @@ def _stencil(x, w, s, c, Oy, Ox):
     (6, 64, 72, 17, 4, 1, 1, 0, -1.0, 1),    # DownscaleOP adjoint (LR -> HR), accumulated with alpha -1
     (3, 13, 11, 17, 4, 1, 1, 0, 1.0, 0),     # tiny HR grid: most outputs on or near the clamped border
     (3, 22, 26, 9, 2, 0, 2, 0, 1.0, 0),      # sf 2 (phase 0)
+    (4, 70, 90, 41, 1, 0, 1, 0, 1.0, 0),     # inverse filter adjoint at the KernelGAN-recipe size (41², tiled path)
+    (2, 37, 130, 41, 1, 0, 1, 0, -0.5, 1),   # ... accumulated, several 64 × 16 output tiles, ragged edges
+    (2, 3, 5, 41, 1, 0, 1, 0, 1.0, 0),       # ... grid far smaller than the taps (one interior output)
+    (2, 2, 9, 13, 1, 0, 1, 0, 1.0, 0),       # ... no interior rows (generic path only)
 ])
 def test_cem_adjoint_vs_float64_vjp(gpu_device, P, Ly, Lx, K, s, c, os_, oc, alpha, acc):
     gen = torch.Generator().manual_seed(K * 100 + Ly)
@@ -52,9 +56,16 @@ def test_cem_adjoint_vs_float64_vjp(gpu_device, P, Ly, Lx, K, s, c, os_, oc, alp
                                    out.data_ptr(), st), 'esr_cem_adjoint')
     torch.cuda.synchronize()
     assert normwise_rel(out.double().cpu(), ref) < 1e-6
-    # the interior fast path (default) is bitwise the generic per-tap range search
+    # the interior fast paths (default: per-output, or the tiled stride-1 kernel) are bitwise the generic per-tap range
+    # search
     out2 = base.float().to(gpu_device) if acc else torch.empty(ref.shape, device=gpu_device)
     _lib.check(lib.esr_cem_adjoint(gd.data_ptr(), P, Oy, Ox, wd.data_ptr(), K, s, c, Ly, Lx, os_, oc, alpha, acc | 2,
                                    out2.data_ptr(), st), 'esr_cem_adjoint generic')
     torch.cuda.synchronize()
-    assert torch.equal(out, out2)
+    if s == 1 and os_ == 1 and oc == 0 and Ly >= 3 and Lx >= 3:
+        # the stride-1 (inverse filter) adjoint: interior outputs tiled, bitwise; the clamped border rows / columns
+        # are summed by a block per output in a tree order
+        assert torch.equal(out[:, 1:-1, 1:-1], out2[:, 1:-1, 1:-1])
+        assert normwise_rel(out.double().cpu(), out2.double().cpu()) < 1e-6
+    else:
+        assert torch.equal(out, out2)
