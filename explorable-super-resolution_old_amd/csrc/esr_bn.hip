@@ -126,9 +126,17 @@ __global__ void bn_finish(const double *partial, int nblk, int K, int C, float *
     }
 }
 
-// mean / invstd from the sums: mode 0 -> mu = s/N; mode 1 -> rs = 1/sqrt(s/N + eps) (and var = s/N)
+// mean / invstd from the sums: mode 0 -> mu = s/N; mode 1 -> rs = 1/sqrt(s/N + eps) (and var = s/N), and, with rm
+// set, nn.BatchNorm2d's running-buffer update (momentum m): rm = rm·(1 - m) + m·mu, rv = rv·(1 - m) + m·N/(N-1)·var,
+// num_batches_tracked + 1 — in this launch instead of five PyTorch ops per layer and call
+struct BnRun {
+    float *rm, *rv;
+    long long *nbt;
+    float m;
+};
+
 __global__ void bn_stats_finish(const float *sum, int C, long long P, float eps, int mode, float *mu, float *rs,
-                                float *var) {
+                                float *var, BnRun run) {
     const int c = blockIdx.x * NT + threadIdx.x;
     if (c >= C) return;
     if (mode == 0) {
@@ -137,6 +145,12 @@ __global__ void bn_stats_finish(const float *sum, int C, long long P, float eps,
         const float v = sum[c] / (float)P;
         var[c] = v;
         rs[c] = 1.f / sqrtf(v + eps);
+        if (run.rm) {
+            const float m = run.m, a = m * (float)P / (float)(P > 1 ? P - 1 : 1);
+            run.rm[c] = run.rm[c] * (1.f - m) + m * mu[c];
+            run.rv[c] = run.rv[c] * (1.f - m) + a * v;
+            if (c == 0 && run.nbt) run.nbt[0] += 1;
+        }
     }
 }
 
@@ -207,16 +221,21 @@ extern "C" int64_t esr_bn_workspace_floats(int64_t P, int32_t C) {
 
 extern "C" int esr_bn_lrelu_fwd(const float *x, int64_t P, int32_t C, const float *gamma, const float *beta, float eps,
                                 float slope, float *y, float *mu, float *rs, float *var, float *ws,
+                                float *running_mean, float *running_var, int64_t *num_batches_tracked, float momentum,
                                 esr_stream_t stream) {
     if (!x || !gamma || !beta || !y || !mu || !rs || !var || !ws || P <= 0 || C <= 0) return ESR_EINVAL;
+    if ((running_mean == nullptr) != (running_var == nullptr) || (running_mean && !(momentum >= 0.f && momentum <= 1.f)))
+        return ESR_EINVAL;
+    const BnRun run = {running_mean, running_var, reinterpret_cast<long long *>(num_batches_tracked), momentum};
+    const BnRun none = {nullptr, nullptr, nullptr, 0.f};
     const hipStream_t st = (hipStream_t)stream;
     BnP p = {};
     p.x = x; p.gamma = gamma; p.beta = beta; p.mu = mu; p.rs = rs; p.P = P; p.C = C; p.slope = slope;
     float *partial = ws, *sums = ws + (long long)MAXB * 3 * C * 2;
     if (colsum<0>(p, partial, sums, st)) return ESR_ELAUNCH;
-    hipLaunchKernelGGL(bn_stats_finish, dim3(grid_of(C)), dim3(NT), 0, st, sums, C, P, eps, 0, mu, rs, var);
+    hipLaunchKernelGGL(bn_stats_finish, dim3(grid_of(C)), dim3(NT), 0, st, sums, C, P, eps, 0, mu, rs, var, none);
     if (colsum<1>(p, partial, sums, st)) return ESR_ELAUNCH;
-    hipLaunchKernelGGL(bn_stats_finish, dim3(grid_of(C)), dim3(NT), 0, st, sums, C, P, eps, 1, mu, rs, var);
+    hipLaunchKernelGGL(bn_stats_finish, dim3(grid_of(C)), dim3(NT), 0, st, sums, C, P, eps, 1, mu, rs, var, run);
     hipLaunchKernelGGL(bn_apply<0>, dim3(grid_of(P * C)), dim3(NT), 0, st, p, y, nullptr);
     return launched();
 }

@@ -2038,3 +2038,76 @@ extern "C" int esr_dconv_presplit(const float *w_packed, int64_t rows, int32_t n
                        (long long)rows, n_pad, (const float *)scratch, nb, static_cast<_Float16 *>(w_split), w_exp);
     return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
 }
+
+// ---- the first conv's tap gather (HipConv2d._im2col: 3 channels × 9 taps -> one 32-wide K step) ------------------------
+namespace {
+
+// out[b][y][x][t·C + c] = x[b][y + ky - p][x + kx - p][c] (zero outside), t = ky·k + kx < k², zero-filled to 32
+// channels: one thread per output pixel, its 128-B record written as 8 16-B stores
+__global__ __launch_bounds__(256) void im2col32_kernel(const float *__restrict__ x, int B, int H, int W, int C, int k,
+                                                       int p, int Ho, int Wo, float *__restrict__ out) {
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (long long)B * Ho * Wo) return;
+    const int xo = idx % Wo;
+    const int yo = (idx / Wo) % Ho;
+    const long long b = idx / ((long long)Wo * Ho);
+    float v[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) v[j] = 0.f;
+    for (int t = 0; t < k * k; ++t) {
+        const int yy = yo + t / k - p, xx = xo + t % k - p;
+        if (yy < 0 || yy >= H || xx < 0 || xx >= W) continue;
+        const float *src = x + ((b * H + yy) * W + xx) * C;
+        for (int c = 0; c < C; ++c) v[t * C + c] = src[c];
+    }
+    float4 *o = reinterpret_cast<float4 *>(out + idx * 32);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = make_float4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
+}
+
+// its adjoint: gx[b][y][x][c] = Σ_t gc[b][y - ky + p][x - kx + p][t·C + c] over the outputs in range, added from 0 in
+// tap order (as the k² shifted in-place adds of the PyTorch form did): one thread per input pixel
+__global__ __launch_bounds__(256) void col2im32_kernel(const float *__restrict__ gc, int B, int Ho, int Wo, int k, int p,
+                                                       int H, int W, int C, float *__restrict__ gx) {
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (long long)B * H * W) return;
+    const int xx = idx % W;
+    const int yy = (idx / W) % H;
+    const long long b = idx / ((long long)W * H);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < k * k; ++t) {
+        const int yo = yy - t / k + p, xo = xx - t % k + p;
+        if (yo < 0 || yo >= Ho || xo < 0 || xo >= Wo) continue;
+        const float *src = gc + ((b * Ho + yo) * Wo + xo) * 32 + t * C;
+        for (int c = 0; c < C; ++c) acc[c] += src[c];
+    }
+    float *o = gx + idx * C;
+    for (int c = 0; c < C; ++c) o[c] = acc[c];
+}
+
+}  // namespace
+
+extern "C" int esr_dconv_im2col(const float *x, int32_t B, int32_t H, int32_t W, int32_t C, int32_t k, int32_t p,
+                                float *out, esr_stream_t stream) {
+    if (!x || !out || B <= 0 || H <= 0 || W <= 0 || C <= 0 || k <= 0 || p < 0 || k * k * C > 32 ||
+        (reinterpret_cast<uintptr_t>(out) & 15))
+        return ESR_EINVAL;
+    const int Ho = H + 2 * p - k + 1, Wo = W + 2 * p - k + 1;
+    if (Ho <= 0 || Wo <= 0) return ESR_EINVAL;
+    const long long n = (long long)B * Ho * Wo;
+    hipLaunchKernelGGL(im2col32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, B, H,
+                       W, C, k, p, Ho, Wo, out);
+    return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+}
+
+extern "C" int esr_dconv_col2im(const float *gc, int32_t B, int32_t H, int32_t W, int32_t C, int32_t k, int32_t p,
+                                float *gx, esr_stream_t stream) {
+    if (!gc || !gx || B <= 0 || H <= 0 || W <= 0 || C <= 0 || C > 8 || k <= 0 || p < 0 || k * k * C > 32)
+        return ESR_EINVAL;
+    const int Ho = H + 2 * p - k + 1, Wo = W + 2 * p - k + 1;
+    if (Ho <= 0 || Wo <= 0) return ESR_EINVAL;
+    const long long n = (long long)B * H * W;
+    hipLaunchKernelGGL(col2im32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, gc, B,
+                       Ho, Wo, k, p, H, W, C, gx);
+    return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+}

@@ -24,14 +24,18 @@ def _ws(lib, P, C, dev):
 
 class _BNLReLUFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x2, gamma, beta, eps, slope):
+    def forward(ctx, x2, gamma, beta, eps, slope, run=None):
+        """run = (running_mean, running_var, num_batches_tracked, momentum): updated by the same launch, or None."""
         lib = _lib.load()
         P, C = x2.shape
         y = torch.empty_like(x2)
         mu, rs, var = (torch.empty(C, device=x2.device) for _ in range(3))
+        rm, rv, nbt, m = run if run is not None else (None, None, None, 0.0)
+        ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
         _lib.check(lib.esr_bn_lrelu_fwd(x2.data_ptr(), P, C, gamma.data_ptr(), beta.data_ptr(), eps, slope,
                                         y.data_ptr(), mu.data_ptr(), rs.data_ptr(), var.data_ptr(),
-                                        _ws(lib, P, C, x2.device).data_ptr(), _stream(x2)), 'esr_bn_lrelu_fwd')
+                                        _ws(lib, P, C, x2.device).data_ptr(), ptr(rm), ptr(rv), ptr(nbt), m,
+                                        _stream(x2)), 'esr_bn_lrelu_fwd')
         ctx.save_for_backward(x2, gamma, beta, mu, rs)
         ctx.slope = slope
         ctx.mark_non_differentiable(mu, var)
@@ -41,7 +45,7 @@ class _BNLReLUFn(torch.autograd.Function):
     def backward(ctx, gy, _gmu, _gvar):
         x2, gamma, beta, mu, rs = ctx.saved_tensors
         gx, gg, gb = _BNLReLUBwdFn.apply(x2, gamma, beta, gy.contiguous(), mu, rs, ctx.slope)
-        return gx, gg, gb, None, None
+        return gx, gg, gb, None, None, None
 
 
 class _BNLReLUBwdFn(torch.autograd.Function):
@@ -83,8 +87,13 @@ def bn_lrelu(x, bn, slope):
     xh = x.permute(0, 2, 3, 1)
     if not xh.is_contiguous():
         xh = xh.contiguous()
-    y, mu, var = _BNLReLUFn.apply(xh.view(B * H * W, C), bn.weight, bn.bias, float(bn.eps), float(slope))
-    if bn.track_running_stats:
+    # running buffers updated by the forward launch itself (momentum; the cumulative average of momentum=None needs
+    # the count on the host and keeps the PyTorch ops)
+    inplace = bn.track_running_stats and bn.momentum is not None and bn.running_mean is not None and \
+        bn.num_batches_tracked is not None and bn.num_batches_tracked.dtype == torch.int64
+    run = (bn.running_mean, bn.running_var, bn.num_batches_tracked, float(bn.momentum)) if inplace else None
+    y, mu, var = _BNLReLUFn.apply(xh.view(B * H * W, C), bn.weight, bn.bias, float(bn.eps), float(slope), run)
+    if bn.track_running_stats and not inplace:
         with torch.no_grad():
             bn.num_batches_tracked.add_(1)
             m = bn.momentum if bn.momentum is not None else 1.0 / float(bn.num_batches_tracked)

@@ -341,23 +341,26 @@ class _ToNHWC(torch.autograd.Function):
 
 def _im2col(xh, k, p):
     """[B][H][W][C] -> [B][Ho][Wo][32] (stride 1): channel (ky*k + kx)*C + c = x[y + ky - p][x + kx - p][c] (zero
-    outside), zero-filled to 32 channels."""
+    outside), zero-filled to 32 channels (esr_dconv_im2col: one pass; the pad + cat of slices took two)."""
+    _check_dev(xh)
+    xh = xh.contiguous()
     B, H, W, C = xh.shape
-    Ho, Wo = out_size(H, k, 1, p), out_size(W, k, 1, p)
-    xp = F.pad(xh, (0, 0, p, p, p, p))
-    return torch.cat([xp[:, ky:ky + Ho, kx:kx + Wo, :] for ky in range(k) for kx in range(k)] +
-                     [xh.new_zeros(B, Ho, Wo, 32 - k * k * C)], dim=3)
+    out = torch.empty(B, out_size(H, k, 1, p), out_size(W, k, 1, p), 32, device=xh.device, dtype=torch.float32)
+    _lib.check(_lib.load().esr_dconv_im2col(xh.data_ptr(), B, H, W, C, k, p, out.data_ptr(), _stream(xh)),
+               'esr_dconv_im2col')
+    return out
 
 
 def _col2im(gc, k, p, H, W, C):
-    """The adjoint of _im2col: every tap's channel group added back at its shift (zeros + k² in-place adds + one
-    copy; autograd through cat / slice / pad made a padded temporary and an add per tap)."""
-    B, Ho, Wo, _ = gc.shape
-    gp = gc.new_zeros(B, H + 2 * p, W + 2 * p, C)
-    for t in range(k * k):
-        ky, kx = divmod(t, k)
-        gp[:, ky:ky + Ho, kx:kx + Wo, :] += gc[..., t * C:(t + 1) * C]
-    return gp[:, p:p + H, p:p + W, :].contiguous()
+    """The adjoint of _im2col: every tap's channel group added back at its shift, in tap order from zero
+    (esr_dconv_col2im: one pass; the zeros + k² shifted in-place adds + copy took 11 launches over the image)."""
+    _check_dev(gc)
+    gc = gc.contiguous()
+    B = gc.shape[0]
+    gx = torch.empty(B, H, W, C, device=gc.device, dtype=torch.float32)
+    _lib.check(_lib.load().esr_dconv_col2im(gc.data_ptr(), B, H, W, C, k, p, gx.data_ptr(), _stream(gc)),
+               'esr_dconv_col2im')
+    return gx
 
 
 class _Im2ColFn(torch.autograd.Function):

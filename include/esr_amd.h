@@ -324,6 +324,16 @@ int esr_dconv_fwd_sd(const float *src, int32_t B, int32_t Hs, int32_t Ws, int32_
 #define ESR_DCONV_PRESPLIT_SCRATCH 512
 int esr_dconv_presplit(const float *w_packed, int64_t rows, int32_t n_pad, float *scratch, void *w_split,
                        int32_t *w_exp, esr_stream_t stream);
+
+/* The discriminator's first conv (3 input channels, 3×3, stride 1: architecture.py:229) runs as a 1×1 conv over its
+ * taps gathered into one 32-wide K step.  esr_dconv_im2col: out [B][Ho][Wo][32] (Ho = H + 2p - k + 1) with
+ * out[..][t·C + c] = x[b][y + ky - p][x + kx - p][c] (zero outside the image), t = ky·k + kx, zero-filled past k²·C
+ * (k²·C <= 32; out 16-B aligned).  esr_dconv_col2im: its adjoint, gx [B][H][W][C] = Σ_t (in tap order, from 0)
+ * gc[b][y - ky + p][x - kx + p][t·C + c] over the outputs in range (C <= 8).  x, gx NHWC [B][H][W][C]. */
+int esr_dconv_im2col(const float *x, int32_t B, int32_t H, int32_t W, int32_t C, int32_t k, int32_t p, float *out,
+                     esr_stream_t stream);
+int esr_dconv_col2im(const float *gc, int32_t B, int32_t H, int32_t W, int32_t C, int32_t k, int32_t p, float *gx,
+                     esr_stream_t stream);
 /* 1 if an esr_dconv_fwd(_sd) launch of this geometry runs on the halo-tile kernel (sd != 0: an esr_dconv_fwd_sd
  * launch), 0 if on the per-tap gather kernel.  The host takes the space-to-depth forward only where it is halo-tiled
  * (on the gather kernel it is no faster than the direct stride-2 gather: profiles/r3_dconv_s2d_ab.txt). */
@@ -390,14 +400,17 @@ int esr_op_size(void);                                  /* sizeof(esr_op), check
 /* ---- discriminator BatchNorm2d (training) + LeakyReLU (esr_bn.hip) ------------------------------------------------
  * conv_block(CNA)'s norm + act (block.py:129-156) fused on channels-last activations x [P][C] (P = B·H·W):
  *   μ, v = batch mean / biased variance per channel, r = 1/sqrt(v + eps), y = lrelu_slope(γ·(x − μ)·r + β).
- * esr_bn_lrelu_fwd writes y and the per-channel mu, rs (= r) and var (the caller updates the running buffers).
+ * esr_bn_lrelu_fwd writes y and the per-channel mu, rs (= r) and var, and, when running_mean / running_var are set,
+ * updates them as nn.BatchNorm2d does (momentum in [0, 1]: r = r·(1 − m) + m·μ, rv = rv·(1 − m) + m·P/(P−1)·v) and adds
+ * 1 to *num_batches_tracked (int64; may be NULL).
  * esr_bn_lrelu_bwd: gx = ∂L/∂x for upstream gy, and sums2 = [Σ gz ; Σ gz·x̂] (= dβ ; dγ), gz = gy·lrelu'.
  * esr_bn_lrelu_bwd2: the backward of (x, γ, gy) -> (gx, dγ, dβ) (the WGAN-GP double backward, loss.py:244-263) for
  * upstream u = ∂/∂gx, ggg = ∂/∂dγ, ggb = ∂/∂dβ (each may be NULL = 0): g_x, g_gy and g_gamma (formulas in
  * esr_bn.hip's header).  ws = scratch of esr_bn_workspace_floats(P, C) floats.  Deterministic (fixed-order sums). */
 int64_t esr_bn_workspace_floats(int64_t P, int32_t C);
 int esr_bn_lrelu_fwd(const float *x, int64_t P, int32_t C, const float *gamma, const float *beta, float eps,
-                     float slope, float *y, float *mu, float *rs, float *var, float *ws, esr_stream_t stream);
+                     float slope, float *y, float *mu, float *rs, float *var, float *ws, float *running_mean,
+                     float *running_var, int64_t *num_batches_tracked, float momentum, esr_stream_t stream);
 int esr_bn_lrelu_bwd(const float *x, const float *gy, int64_t P, int32_t C, const float *gamma, const float *beta,
                      const float *mu, const float *rs, float slope, float *gx, float *sums2, float *ws,
                      esr_stream_t stream);

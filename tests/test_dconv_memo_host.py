@@ -64,26 +64,6 @@ def test_unmarked_tensors_are_not_memoised():
     assert len(calls) == 2 and not hasattr(g, '_esr_packs')
 
 
-def test_im2col_function_matches_autograd_through_cat_and_pad():
-    """HipConv2d's 3-channel path (conv0): _Im2ColFn's gradient (_col2im) and the gradient of that gradient (the
-    WGAN-GP double backward) against autograd through the plain slice / pad / cat ops, float64."""
-    torch.manual_seed(0)
-    for k, p, C in ((3, 1, 3), (3, 0, 3), (5, 2, 1)):
-        x = torch.randn(2, 7, 9, C, dtype=torch.float64, requires_grad=True)
-        c, ref = dconv._Im2ColFn.apply(x, k, p), dconv._im2col(x, k, p)
-        assert torch.equal(c, ref)
-        g = torch.randn_like(c, requires_grad=True)
-        gx, = torch.autograd.grad(c, x, g, create_graph=True)
-        gr, = torch.autograd.grad(ref, x, g, create_graph=True)
-        assert (gx - gr).abs().max() < 1e-12
-        v = torch.randn_like(gx)
-        a, = torch.autograd.grad((gx * v).sum(), g)
-        b, = torch.autograd.grad((gr * v).sum(), g)
-        assert (a - b).abs().max() < 1e-12
-        assert torch.autograd.gradgradcheck(lambda t: dconv._Im2ColFn.apply(t, k, p), (x,))
-
-
-
 def presplit_reference(wp):
     """The layout of include/esr_amd.h esr_dconv_fwd_sd w_split / w_exp restated with PyTorch ops (test reference for
     esr_dconv_presplit): v = wp·2^E, E = 14 - floor(log2 max|wp|), hi = f16(v), lo = f16(v - hi), each 128-byte

@@ -304,3 +304,32 @@ def test_presplit_kernel_bitwise(gpu_device, T, K, N):
     torch.cuda.synchronize()
     assert torch.equal(e.cpu(), ref_e.cpu())
     assert torch.equal(rows.view(torch.int16).cpu(), ref_rows.view(torch.int16).cpu())
+
+
+def _im2col_ref(xh, k, p):
+    """HipConv2d's tap gather restated with PyTorch slice / pad / cat ops (the reference for esr_dconv_im2col)."""
+    B, H, W, C = xh.shape
+    Ho, Wo = H + 2 * p - k + 1, W + 2 * p - k + 1
+    xp = torch.nn.functional.pad(xh, (0, 0, p, p, p, p))
+    return torch.cat([xp[:, ky:ky + Ho, kx:kx + Wo, :] for ky in range(k) for kx in range(k)] +
+                     [xh.new_zeros(B, Ho, Wo, 32 - k * k * C)], dim=3)
+
+
+def test_im2col_col2im_vs_autograd_through_cat_and_pad(gpu_device):
+    """The first conv's 3-channel path: esr_dconv_im2col bitwise the slice / pad / cat restatement; _Im2ColFn's
+    gradient (esr_dconv_col2im) and the gradient of that gradient (the WGAN-GP double backward) bitwise autograd
+    through the restatement (the same adds in the same order), fp32 on the device."""
+    from esr_amd import dconv
+    torch.manual_seed(0)
+    for k, p, C in ((3, 1, 3), (3, 0, 3), (5, 2, 1)):
+        x = torch.randn(2, 7, 9, C, device=gpu_device, requires_grad=True)
+        c, ref = dconv._Im2ColFn.apply(x, k, p), _im2col_ref(x, k, p)
+        assert torch.equal(c, ref)
+        g = torch.randn_like(c, requires_grad=True)
+        gx, = torch.autograd.grad(c, x, g, create_graph=True)
+        gr, = torch.autograd.grad(ref, x, g, create_graph=True)
+        assert (gx - gr).abs().max() < 1e-5
+        v = torch.randn_like(gx)
+        a, = torch.autograd.grad((gx * v).sum(), g)
+        b, = torch.autograd.grad((gr * v).sum(), g)
+        assert torch.equal(a, b)

@@ -20,6 +20,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--min-numel', type=int, default=4_000_000)
     ap.add_argument('--host', action='store_true', help='print the ops by self CPU time instead')
+    ap.add_argument('--device', action='store_true', help='print the aten ops by their device (kernel) time, with the '
+                    'input shapes and the calling Python frames')
     ap.add_argument('--syncs', action='store_true', help='count the Python call sites of tensor -> host scalar '
                     'conversions (item / float / int / bool / iteration) in one step')
     a = ap.parse_args()
@@ -56,6 +58,28 @@ def main():
         torch.cuda.synchronize()
         for (name, st), n in cnt.most_common(12):
             print('%5d x %s\n%s' % (n, name, st), flush=True)
+        return
+    if a.device:
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True,
+                     with_stack=True) as prof:
+            model.feed_data(data)
+            model.optimize_parameters()
+            torch.cuda.synchronize()
+        print(prof.key_averages(group_by_input_shape=True).table(sort_by='self_cuda_time_total', row_limit=45,
+                                                                 max_name_column_width=40, max_shapes_column_width=70),
+              flush=True)
+        agg = {}
+        for ev in prof.events():
+            if not ev.name.startswith('aten::') or ev.self_device_time_total <= 0:
+                continue
+            stack = [f.split('explorable-super-resolution_old_amd/')[-1] for f in (ev.stack or [])
+                     if 'esr_amd' in f][:3]
+            k = (ev.name, str(ev.input_shapes)[:90], ' <- '.join(stack))
+            a = agg.setdefault(k, [0, 0.0])
+            a[0] += 1
+            a[1] += ev.self_device_time_total
+        for (name, shp, st), (n, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:40]:
+            print('%8.1f us %3d x %-28s %-90s | %s' % (t, n, name, shp, st), flush=True)
         return
     with profile(activities=[ProfilerActivity.CPU], record_shapes=True, with_stack=True) as prof:
         model.feed_data(data)
