@@ -17,7 +17,7 @@
 extern "C" {
 #endif
 
-/* esr_conv3x3_fwd_x3 / esr_upconv2x_phase_fwd_x3 kernel (0..64).  All non-diagnostic variants are bitwise identical.
+/* esr_conv3x3_fwd_x3 / esr_upconv2x_phase_fwd_x3 kernel (0..65; 65 = 12-column tiles for N = 64 too, two per CU).  All non-diagnostic variants are bitwise identical.
  * 0 / 1 / 63 = automatic (the product dispatch); 24 = the round-1 automatic choice (classic kernel only: 8-row at three
  *   per CU or 16-row at two; 25 / 26 force one); 50 = column-tile kernel (16 columns); 60 = column tiles with the
  *   weights read into registers from global memory; 61 = 8 waves of 2 columns; 62 = weights copied to registers per
@@ -33,7 +33,7 @@ int esr_x3_set_kernel(int32_t variant);
 int esr_x3_set_tile_map(int32_t mode);
 /* HR_conv1 on the narrow-N kernel: 1 (product) / 0 = N = 32 tiles (equal to the x3 rounding, not bitwise). */
 int esr_x3_set_narrow(int32_t on);
-/* N split of under-filled N = 64 x3 convs: 1 (product) / 0 = one N = 64 launch (bitwise identical). */
+/* N split of under-filled N = 64 x3 convs (round 3): 0 (product) / 1 = two N = 32 launches (bitwise identical). */
 int esr_x3_set_nsplit(int32_t on);
 /* Exact-fp32 conv tile rows: 0 (product: automatic), 4 or 8 (identical results). */
 int esr_conv_set_tile(int32_t rows);

@@ -1334,17 +1334,26 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
     // per CU (B=8 × 64²: 102 tiles) the 8-row tiles stay (0.70-0.73× there; profiles/r4_x3_n32_grid_ab.txt)
     const int tiles12 = ((W + 11) / 12) * ((B * (H + 2) - 2 + 31) / 32);
     const bool x3c_pays = taps_side == 2 || (taps_side == 3 && (cout > 32 || !row8_pays || tiles12 >= n_cu));
-    if ((g_x3_kernel >= 50 && g_x3_kernel <= 62) || g_x3_kernel == 64 || ((g_x3_kernel == 1 || g_x3_kernel == 63) && x3c_pays)) {
+    if ((g_x3_kernel >= 50 && g_x3_kernel <= 62) || g_x3_kernel == 64 || g_x3_kernel == 65 ||
+        ((g_x3_kernel == 1 || g_x3_kernel == 63) && x3c_pays)) {
         X3cParams c;
         c.in = p.in; c.B = B; c.H = H; c.W = W; c.in_cp = in_cp; c.cin = cin; c.w = p.w; c.bias = bias;
         c.w_scale_inv = p.w_scale_inv; c.cout = cout; c.tap_y0 = ty0; c.tap_x0 = tx0; c.tiles_x = c.tiles_y = 0;
         c.xcd_map = g_tile_map; c.overflow = overflow; c.o = *o;
         c.w_ld = c.w_roff = 0;
         c.w_cstride = 0;
-        // N split: an N = 64 conv whose 16-column grid cannot give every CU two workgroups (config 3 / 5: 294 / 380
-        // tiles for 256 CUs) runs as two N = 32 launches (12-column tiles, three per CU) over the two halves of its
-        // packed weights and output channels — twice the input staging, but the CUs filled (profiles/r3_ab_nsplit.txt)
-        const int tiles16 = ((W + 15) / 16) * ((B * (H + 2) - 2 + 31) / 32);
+        // N = 64 3×3 convs: 12-column tiles (four 3-column waves, two workgroups per CU) where their rounds cost less
+        // than the 16-column tiles' (12·⌈t12/2CU⌉ < 16·⌈t16/2CU⌉): 1.08× the N split at config 3's 96², 1.10× at
+        // 154², 1.05–1.24× at smaller grids; 16-column tiles at 172² (one round vs two: 1.18× the split) and 148²
+        // (a tie); profiles/r4_x3_n64_tiles.txt.  Round 3's N split (two N = 32 launches) lost to one of the two at
+        // every measured grid and is the ablation library's option (esr_x3_set_nsplit)
+        const int rows32 = (B * (H + 2) - 2 + 31) / 32;
+        const int tiles16 = ((W + 15) / 16) * rows32;
+        if (taps_side == 3 && cout > 32 && (g_x3_kernel == 1 || g_x3_kernel == 63) && !o->out_planar) {
+            const int t12 = ((W + 11) / 12) * rows32;
+            const int r12 = (t12 + 2 * n_cu - 1) / (2 * n_cu), r16 = (tiles16 + 2 * n_cu - 1) / (2 * n_cu);
+            if (12 * r12 < 16 * r16) return x3c_launch(c, taps_side, stream, 129);
+        }
         if (g_x3_nsplit && taps_side == 3 && cout > 32 && (g_x3_kernel == 1 || g_x3_kernel == 63) &&
             tiles16 < 2 * n_cu && !o->out_planar) {
             for (int h = 0; h < 2; ++h) {
@@ -1364,6 +1373,7 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
             return ESR_OK;
         }
 #ifdef ESR_X3_EXPERIMENTS
+        if (g_x3_kernel == 65) return x3c_launch(c, taps_side, stream, cout > 32 ? 129 : 128);  // N = 64 in 12 columns
         if (g_x3_kernel == 60) return x3c_launch(c, taps_side, stream, 16);
         if (g_x3_kernel == 61) return x3c_launch(c, taps_side, stream, 32);
         if (g_x3_kernel == 62) return x3c_launch(c, taps_side, stream, 64);

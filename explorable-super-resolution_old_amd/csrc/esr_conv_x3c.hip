@@ -158,7 +158,7 @@ __global__ __launch_bounds__(64 * (TW / CWV), (TW / CWV) * OCC / 4) void conv_x3
     constexpr int EP_P = N + 4;                            // epilogue row pitch (floats)
     constexpr int NIC = CWk + TS - 1;                       // halo columns a wave reads (6 for 3×3)
     constexpr int NSTEP = NIC * TS;                        // A steps (halo column, tap row) per sweep
-    static_assert(NW * 32 * EP_P * 4 <= IN_Bk, "per-wave epilogue areas fit in the input region");
+    static_assert(NW * 32 * EP_P * 4 <= LDS_BYTES, "per-wave epilogue areas fit in the (input + weight) stage");
     static_assert(OCC * LDS_BYTES <= 163840, "OCC workgroups per CU");
     __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_BYTES];
 
@@ -347,7 +347,7 @@ __global__ __launch_bounds__(64 * (TW / CWV), (TW / CWV) * OCC / 4) void conv_x3
     }
 
     // ---- epilogue: each wave restages one output column at a time through its own LDS area and stores it ----
-    __builtin_amdgcn_s_barrier();  // all waves are done with the input stage it aliases
+    __builtin_amdgcn_s_barrier();  // all waves are done with the input (and weight) stage it aliases
     if (ncw <= 0) return;
     const esr_conv_out &o = p.o;
     float *s_ep = reinterpret_cast<float *>(lds) + wave * 32 * EP_P;
@@ -894,6 +894,13 @@ int x3c_launch(const X3cParams &p0, int taps_side, hipStream_t stream, int dbg) 
         return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
     }
 #endif
+    if (dbg == 129 && n64) {  // N = 64 in 12-column tiles of four 3-column waves, two workgroups per CU (67.6 KB LDS)
+        p.tiles_x = (p.W + 11) / 12;
+        const dim3 grid12((unsigned)(p.tiles_x * p.tiles_y));
+        if (taps_side == 3) hipLaunchKernelGGL((conv_x3c_kernel<2, 3, 0, false, 3, false, 12, 2>), grid12, block, 0, stream, p);
+        else hipLaunchKernelGGL((conv_x3c_kernel<2, 2, 0, false, 3, false, 12, 2>), grid12, block, 0, stream, p);
+        return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+    }
     if (dbg == 128) {  // N = 32: 12-column tiles of four 3-column waves, three workgroups per CU (48 KB LDS, <= 168 VGPRs)
         if (n64) return x3c_launch(p0, taps_side, stream, 0);
         p.tiles_x = (p.W + 11) / 12;

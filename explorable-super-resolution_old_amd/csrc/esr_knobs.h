@@ -13,7 +13,7 @@
     X(g_conv_tile, 0)    /* exact-fp32 conv tile rows: 0 automatic, 4 or 8                                         */ \
     X(g_x3_kernel, 1)    /* x3 conv kernel variant: 1 = automatic (include/esr_amd.h), others: esr_ablation.h      */ \
     X(g_x3_narrow, 1)    /* narrow-N kernel for HR_conv1 (cout <= 3, planar output)                                */ \
-    X(g_x3_nsplit, 1)    /* N = 64 x3 convs on under-filled grids as two N = 32 launches                           */ \
+    X(g_x3_nsplit, 0)    /* N = 64 x3 convs on under-filled grids as two N = 32 launches (round 3; A/B only)       */ \
     X(g_cem_direct, 0)   /* the untiled CEM inverse / up-add kernels                                               */ \
     X(g_wgrad_kernel, 1) /* 1 = 12-wave weight-gradient kernel, 0 = 4-wave                                         */ \
     X(g_wgrad3_dma, 1)   /* x3 weight gradient of split-f16 output gradients on the LDS-DMA kernel                 */ \

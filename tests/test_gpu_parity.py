@@ -506,9 +506,10 @@ def test_x3_xcd_tile_map_bitwise(gpu_device, ablation_lib, cout, cin, B, H, W):
 
 @pytest.mark.parametrize('cin,cout,B,H,W', [(192, 64, 2, 24, 40), (72, 40, 1, 9, 21)])
 def test_x3_nsplit_bitwise(gpu_device, ablation_lib, cin, cout, B, H, W):
-    """An N = 64 conv on an under-filled grid as two N = 32 launches over the halves of its packed weights
-    (esr_x3_set_nsplit, default) against one N = 64 launch: the RDB conv5 epilogue (LeakyReLU off, 0.2 x conv +
-    residual at a channel offset, a dual output at another offset) must land in the same channels, bit for bit."""
+    """An N = 64 conv on a small grid in the product's choice (12-column N = 64 tiles, two per CU) against the same
+    conv as two N = 32 launches over the halves of its packed weights (round 3's N split, esr_x3_set_nsplit) and in
+    16-column tiles (variant 50): the RDB conv5 epilogue (LeakyReLU off, 0.2 x conv + residual at a channel offset, a
+    dual output at another offset) must land in the same channels, bit for bit."""
     lib = _lib.load()
     cp = cin + 8
     xs = engine.to_split(_padded(B, H, W, cp, cin, gpu_device, 51))
@@ -519,9 +520,10 @@ def test_x3_nsplit_bitwise(gpu_device, ablation_lib, cin, cout, B, H, W):
     wx, scale = engine.pack_x3(engine.pack_conv_weight(w.to(gpu_device), list(range(cin)), 64))
     outs = []
     try:
-        for L in (lib, ablation_lib):
+        for L, nsplit, variant in ((lib, None, None), (ablation_lib, 1, 1), (ablation_lib, 0, 50)):
             if L is ablation_lib:
-                L.esr_x3_set_nsplit(0)
+                L.esr_x3_set_nsplit(nsplit)
+                L.esr_x3_set_kernel(variant)
             out = torch.zeros(B, H + 2, W + 2, 80, device=gpu_device)
             out2 = torch.zeros(B, H + 2, W + 2, 88, device=gpu_device)
             o = engine._conv_out(out, 80, 8, H, W, False, r1=rs, r1_cp=cp, r1_coff=16, s1=0.2, out2=out2, out2_cp=88,
@@ -531,8 +533,10 @@ def test_x3_nsplit_bitwise(gpu_device, ablation_lib, cin, cout, B, H, W):
             torch.cuda.synchronize()
             outs.append((out, out2))
     finally:
-        ablation_lib.esr_x3_set_nsplit(1)
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+        ablation_lib.esr_x3_set_nsplit(0)
+        ablation_lib.esr_x3_set_kernel(1)
+    for k in (1, 2):
+        assert torch.equal(outs[0][0], outs[k][0]) and torch.equal(outs[0][1], outs[k][1]), k
     ref = F.conv2d(_nchw(engine.from_split(xs), 0, cin), w.double(), b.cpu().double(), padding=1)
     assert normwise_rel(_nchw(engine.from_split(outs[0][0]), 8, 8 + cout), ref * 0.2 +
                         _nchw(engine.from_split(rs), 16, 16 + cout)) < 1e-5

@@ -51,9 +51,12 @@ def _close(mine, f32, f64, scale=None, rel=0.0):
     err, base, norm = np.linalg.norm(mine - f64), max(bases), np.linalg.norm(f64)
     scale = norm if scale is None else scale
     bound = FACTOR * base + FLOOR * max(scale, 1e-12) + rel * norm
-    return err <= bound, 'err %.3e  bound %.3e  (%5.1f %% of bound; ref f32 err %.3e (plain %.3e, %d runs), ' \
-        '|ref| %.3e, scale %.3e)' % (err, bound, 100 * err / bound, base, bases[0], len(bases), norm, scale), \
-        err / bound
+    # the same bound on the plain single float32 run alone (no perturbed runs, no projection allowance): printed next
+    # to the ensemble bound so that the widening of the yardstick stays visible (the test asserts the ensemble bound)
+    plain = FACTOR * bases[0] + FLOOR * max(scale, 1e-12)
+    return err <= bound, 'err %.3e  bound %.3e  (%5.1f %% of bound; %5.1f %% of the plain single-run bound; ref f32 ' \
+        'err %.3e (plain %.3e, %d runs), |ref| %.3e, scale %.3e)' % (
+            err, bound, 100 * err / bound, 100 * err / plain, base, bases[0], len(bases), norm, scale), err / bound
 
 
 def _f32s(d, key_fmt):
