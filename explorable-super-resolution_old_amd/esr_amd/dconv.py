@@ -387,6 +387,129 @@ class _Col2ImFn(torch.autograd.Function):
         return _Im2ColFn.apply(gg.contiguous(), *ctx.geom), None, None, None, None, None
 
 
+# ---- the first conv block fused (csrc/esr_dfirst.hip): Conv2d(3, 64, 3, stride 1, padding 1) + LeakyReLU, exact fp32 --
+# (architecture.py:231, block.py:129-156); '0' = HipConv2d (im2col + 1x1 conv at PRECISION) + a separate LeakyReLU
+FUSED_FIRST = os.environ.get('ESR_DFIRST', '1') != '0'
+_DF_LRELU, _DF_MASK, _DF_ACC = 1, 2, 4
+_DF_NW = 64 * 27 + 64  # weight-gradient partial: 64·27 weights (torch order), then 64 biases
+
+
+def _ptr(t):
+    return t.data_ptr() if t is not None else None
+
+
+def _df_fwd(xh, w, b, slope, flags, mask=None, out=None):
+    """esr_dfirst_fwd: [B][H][W][3] -> [B][H][W][64] (flags: LeakyReLU / mask by lrelu'(mask) / accumulate into out)."""
+    B, H, W, _ = xh.shape
+    y = out if out is not None else torch.empty(B, H, W, 64, device=xh.device, dtype=torch.float32)
+    _lib.check(_lib.load().esr_dfirst_fwd(xh.data_ptr(), B, H, W, w.contiguous().data_ptr(), _ptr(b), slope, flags,
+                                          _ptr(mask), y.data_ptr(), _stream(xh)), 'esr_dfirst_fwd')
+    return y
+
+
+def _df_bwd(xh, gy, mask, slope, w, need_x, need_w):
+    """esr_dfirst_bwd + the ordered block reduction: (input gradient or None, [weight grads | bias grads] or None)
+    for g' = gy·lrelu'(mask)."""
+    lib = _lib.load()
+    B, H, W, _ = gy.shape
+    gx = torch.empty(B, H, W, 3, device=gy.device, dtype=torch.float32) if need_x else None
+    part = None
+    if need_w:
+        nb = lib.esr_dfirst_bwd_blocks(B, H, W)
+        part = torch.empty(nb * _DF_NW, device=gy.device, dtype=torch.float32)
+    st = _stream(gy)
+    _lib.check(lib.esr_dfirst_bwd(_ptr(xh), gy.data_ptr(), _ptr(mask), slope, B, H, W, w.contiguous().data_ptr(),
+                                  _ptr(gx), _ptr(part), st), 'esr_dfirst_bwd')
+    gwb = None
+    if need_w:
+        gwb = torch.empty(_DF_NW, device=gy.device, dtype=torch.float32)
+        _lib.check(lib.esr_wgrad_reduce(part.data_ptr(), nb, _DF_NW, 1.0, gwb.data_ptr(), st), 'esr_wgrad_reduce')
+    return gx, gwb
+
+
+class _DFirstFn(torch.autograd.Function):
+    """y = LeakyReLU(conv3x3(x, w) + b) on NHWC tensors (3 -> 64 channels); backward: _DFirstBwdFn."""
+
+    @staticmethod
+    def forward(ctx, xh, w, b, slope):
+        y = _df_fwd(xh, w, b, slope, _DF_LRELU)
+        ctx.save_for_backward(xh, w, y)
+        ctx.slope = slope
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        xh, w, y = ctx.saved_tensors
+        nx, nw, nb = ctx.needs_input_grad[:3]
+        gx, gw, gb = _DFirstBwdFn.apply(xh, gy.contiguous(), y, w, ctx.slope, nx, nw or nb)
+        return gx if nx else None, gw if nw else None, gb if nb else None, None
+
+
+class _DFirstBwdFn(torch.autograd.Function):
+    """(x, gy, y, w) -> (gx, gw, gb) of _DFirstFn with g' = gy·lrelu'(y) (one esr_dfirst_bwd pass).  Its backward (the
+    WGAN-GP double backward, loss.py:244-263): with ggx, ggw, ggb the gradients of the three outputs,
+        d/dgy = lrelu'(y) · (conv(ggx; w) + conv(x; ggw) + ggb)      (esr_dfirst_fwd, masked)
+        d/dw  = wgrad(ggx, g')     d/dx = dgrad(g'; ggw)             (esr_dfirst_bwd)
+    and nothing through y (the mask is piecewise constant)."""
+
+    @staticmethod
+    def forward(ctx, xh, gy, y, w, slope, need_x, need_w):
+        gx, gwb = _df_bwd(xh, gy, y, slope, w, need_x, need_w)
+        ctx.save_for_backward(xh, gy, y, w)
+        ctx.slope, ctx.need = slope, (need_x, need_w)
+        ctx.set_materialize_grads(False)
+        e = gy.new_zeros(0)
+        if gwb is None:
+            return (gx if need_x else e), e, e
+        return (gx if need_x else e), gwb[:64 * 27].view(64, 3, 3, 3).clone(), gwb[64 * 27:].clone()
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, ggx, ggw, ggb):
+        xh, gy, y, w = ctx.saved_tensors
+        need_x, need_w = ctx.need
+        ggx = ggx if need_x and ggx is not None else None
+        ggw = ggw if need_w and ggw is not None else None
+        ggb = ggb if need_w and ggb is not None else None
+        slope = ctx.slope
+        g_x = g_gy = g_w = None
+        if ctx.needs_input_grad[1] and (ggx is not None or ggw is not None or ggb is not None):
+            terms = []
+            if ggx is not None:
+                terms.append((ggx.contiguous(), w))
+            if ggw is not None:
+                terms.append((xh, ggw.contiguous()))
+            if not terms:  # the bias term alone: a conv with zero weights plus ggb
+                terms.append((xh, torch.zeros_like(w)))
+            g_gy = torch.empty_like(gy)
+            for i, (src, wt) in enumerate(terms):
+                last = i == len(terms) - 1
+                _df_fwd(src, wt, ggb.contiguous() if (i == 0 and ggb is not None) else None, slope,
+                        (_DF_ACC if i else 0) | (_DF_MASK if last else 0), mask=y, out=g_gy)
+        if ctx.needs_input_grad[3] and ggx is not None:
+            g_w = _df_bwd(ggx.contiguous(), gy, y, slope, w, False, True)[1][:64 * 27].view(64, 3, 3, 3)
+        if ctx.needs_input_grad[0] and ggw is not None:
+            g_x = _df_bwd(None, gy, y, slope, ggw.contiguous(), True, False)[0]
+        return g_x, g_gy, None, g_w, None, None, None
+
+
+def dfirst_ok(conv):
+    """Whether a HipConv2d is the first conv block's shape the fused kernels take."""
+    return FUSED_FIRST and conv.in_channels == 3 and conv.out_channels == 64 and conv.kernel_size == (3, 3) and \
+        conv.stride == (1, 1) and conv.padding == (1, 1) and conv.bias is not None
+
+
+def dfirst_lrelu(x, conv, slope):
+    """LeakyReLU(slope)(conv(x)) for a HipConv2d passing dfirst_ok, on the fused kernels: NCHW in (any memory format),
+    NCHW with channels-last storage out, differentiable twice (the WGAN-GP penalty)."""
+    _check_dev(x)
+    if x.is_contiguous(memory_format=torch.channels_last):
+        xh = x.permute(0, 2, 3, 1)
+    else:
+        xh = _ToNHWC.apply(x)
+    return _DFirstFn.apply(xh, conv.weight, conv.bias, float(slope)).permute(0, 3, 1, 2)
+
+
 class HipConv2d(nn.Conv2d):
     """nn.Conv2d of the discriminator (same parameters, state_dict and init) whose forward runs esr_dconv.
 

@@ -10,7 +10,9 @@ Every convolution (3×3 s1, 4×4 s2, the 8×8 "pseudo-FC" and the 1×1 head) is 
 and weight gradient on the MFMA kernels of csrc/esr_dconv.hip, differentiable to any order, so the D step and the
 WGAN-GP double backward (loss.py:244-263) run every convolution on HIP.  Their precision is the process-wide
 esr_amd.dconv.PRECISION (default 'x3': split-f16 operands with per-K-step power-of-two scaling on f16 MFMA; 'x6' and
-exact 'f32' via dconv.set_precision or ESR_DCONV_PRECISION).  BatchNorm and LeakyReLU
+exact 'f32' via dconv.set_precision or ESR_DCONV_PRECISION) — except the first conv block (3 -> 64, 3x3, + LeakyReLU),
+which runs fused in exact fp32 on the VALU at every precision (dconv.dfirst_lrelu, csrc/esr_dfirst.hip: 27 MACs per
+output feed no MFMA; the layer's cost is its 64-channel output, now moved once per pass).  BatchNorm and LeakyReLU
 run fused on HIP in training mode (esr_amd/bn.py: forward, backward, double backward); in eval mode they are
 PyTorch ops on the channels-last activations the convolutions produce.
 """
@@ -19,7 +21,7 @@ import os
 import torch.nn as nn
 
 from .bn import bn_lrelu, lrelu_nhwc
-from .dconv import HipConv2d
+from .dconv import HipConv2d, dfirst_lrelu, dfirst_ok
 
 # BatchNorm + LeakyReLU pairs fused on HIP in training mode (esr_amd/bn.py); ESR_FUSED_BN=0 keeps PyTorch's ops
 FUSED_BN = os.environ.get('ESR_FUSED_BN', '1') != '0'
@@ -76,8 +78,9 @@ class Discriminator_VGG_128_(nn.Module):
 
 def _run(seq, x):
     """seq(x), with every training-mode BatchNorm2d -> LeakyReLU pair (conv_block's norm + act) run as the fused HIP
-    layer of bn.py (forward, backward and double backward) and the other LeakyReLUs out of place on the channels-last
-    storage (bn.lrelu_nhwc); nested Sequentials are walked the same way."""
+    layer of bn.py (forward, backward and double backward), the first conv block (3 -> 64 3x3 conv + LeakyReLU) on the
+    fused exact-fp32 kernels of dconv.dfirst_lrelu, and the other LeakyReLUs out of place on the channels-last storage
+    (bn.lrelu_nhwc); nested Sequentials are walked the same way."""
     mods = list(seq.children())
     i = 0
     while i < len(mods):
@@ -85,6 +88,9 @@ def _run(seq, x):
         nxt = mods[i + 1] if i + 1 < len(mods) else None
         if isinstance(m, nn.Sequential):
             x = _run(m, x)
+        elif isinstance(m, HipConv2d) and isinstance(nxt, nn.LeakyReLU) and x.is_cuda and dfirst_ok(m):
+            x = dfirst_lrelu(x, m, nxt.negative_slope)  # conv0 + its LeakyReLU, one fused pass (esr_dfirst_*)
+            i += 1
         elif FUSED_BN and isinstance(m, nn.BatchNorm2d) and m.training and isinstance(nxt, nn.LeakyReLU) and x.is_cuda:
             x = bn_lrelu(x, m, nxt.negative_slope)
             i += 1

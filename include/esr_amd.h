@@ -334,6 +334,27 @@ int esr_dconv_im2col(const float *x, int32_t B, int32_t H, int32_t W, int32_t C,
                      esr_stream_t stream);
 int esr_dconv_col2im(const float *gc, int32_t B, int32_t H, int32_t W, int32_t C, int32_t k, int32_t p, float *gx,
                      esr_stream_t stream);
+/* The discriminator's first conv block fused (architecture.py:231 -> block.py:129-156: Conv2d(3, 64, 3, stride 1,
+ * padding 1) + LeakyReLU(slope), no norm), exact fp32 on the VALU (csrc/esr_dfirst.hip).  x [B][H][W][3] NHWC,
+ * w [64][3][3][3] (torch layout), bias [64] or NULL, y / mask [B][H][W][64] (16-B aligned).
+ * esr_dfirst_fwd: y = conv(x, w) + bias, then per flags: ESR_DFIRST_ACC adds y's previous contents, ESR_DFIRST_LRELU
+ * applies LeakyReLU(slope), ESR_DFIRST_MASK multiplies by lrelu'(mask) (mask: the layer's saved output, its sign the
+ * LeakyReLU mask; the double backward's path).
+ * esr_dfirst_bwd (x may be NULL when partial is): with g' = gy · lrelu'(mask) (mask NULL: g' = gy): gx (if non-NULL) = the input gradient
+ * Σ w[co][ci][ky][kx] g'[y - ky + 1][x - kx + 1][co] (written, not added); partial (if non-NULL) = per block b of
+ * esr_dfirst_bwd_blocks(B, H, W) blocks, ESR_DFIRST_NW floats at b·ESR_DFIRST_NW: the weight gradient
+ * Σ x[y + ky - 1][x + kx - 1][ci] g'[y][x][co] at co·27 + ci·9 + ky·3 + kx, then the bias gradient Σ g'[co] at
+ * 1728 + co, over the block's pixels — sum the blocks with esr_wgrad_reduce(partial, blocks, ESR_DFIRST_NW, 1, out). */
+#define ESR_DFIRST_COUT 64
+#define ESR_DFIRST_NW (64 * 27 + 64)
+#define ESR_DFIRST_LRELU 1
+#define ESR_DFIRST_MASK 2
+#define ESR_DFIRST_ACC 4
+int esr_dfirst_fwd(const float *x, int32_t B, int32_t H, int32_t W, const float *w, const float *bias, float slope,
+                   int32_t flags, const float *mask, float *y, esr_stream_t stream);
+int esr_dfirst_bwd_blocks(int32_t B, int32_t H, int32_t W);
+int esr_dfirst_bwd(const float *x, const float *gy, const float *mask, float slope, int32_t B, int32_t H, int32_t W,
+                   const float *w, float *gx, float *partial, esr_stream_t stream);
 /* 1 if an esr_dconv_fwd(_sd) launch of this geometry runs on the halo-tile kernel (sd != 0: an esr_dconv_fwd_sd
  * launch), 0 if on the per-tap gather kernel.  The host takes the space-to-depth forward only where it is halo-tiled
  * (on the gather kernel it is no faster than the direct stride-2 gather: profiles/r3_dconv_s2d_ab.txt). */

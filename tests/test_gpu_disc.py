@@ -333,3 +333,70 @@ def test_im2col_col2im_vs_autograd_through_cat_and_pad(gpu_device):
         a, = torch.autograd.grad((gx * v).sum(), g)
         b, = torch.autograd.grad((gr * v).sum(), g)
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize('B,H,W', [(2, 20, 37), (1, 8, 32), (2, 33, 70)])
+def test_first_conv_block_fused_vs_float64(gpu_device, B, H, W):
+    """The discriminator's first conv block on the fused kernels (dconv.dfirst_lrelu: esr_dfirst_fwd / esr_dfirst_bwd,
+    Conv2d(3, 64, 3, padding 1) + LeakyReLU(0.2) in exact fp32; architecture.py:231) against float64 PyTorch on the
+    CPU: the forward, the first-order gradients (x, w, b), the WGAN-GP second order (loss.py:244-263: the gradient of
+    (||dD/dx|| - 1)² in w) and the second order through all three first-order outputs at once (gradients of
+    <gx, Vx> + <gw, V> + <gb, u> in x, the upstream gradient and w: every path of _DFirstBwdFn.backward, the
+    accumulate and mask flags).  Ragged shapes against the 8x32 backward tiles; 1e-5 normwise (fp32 sums of 27-576
+    terms vs float64)."""
+    torch.manual_seed(3)
+    conv = dconv.HipConv2d(3, 64, 3, 1, 1).to(gpu_device)
+    assert dconv.dfirst_ok(conv)
+    x64 = torch.randn(B, 3, H, W, dtype=torch.float64)
+    R64 = torch.randn(B, 64, H, W, dtype=torch.float64)
+    Vx, V, u = torch.randn(B, 3, H, W, dtype=torch.float64), torch.randn(64, 3, 3, 3, dtype=torch.float64), \
+        torch.randn(64, dtype=torch.float64)
+
+    def grads(fn, x, R, w, b):
+        y = fn(x, w, b)
+        out = (y * R).sum()
+        gx, gw, gb = torch.autograd.grad(out, (x, w, b), create_graph=True)
+        gp = ((gx.reshape(B, -1).norm(dim=1) - 1) ** 2).mean()
+        gw2, = torch.autograd.grad(gp, w, retain_graph=True)
+        mix = (gx * Vx.to(gx)).sum() + (gw * V.to(gw)).sum() + (gb * u.to(gb)).sum()
+        mx, mR, mw = torch.autograd.grad(mix, (x, R, w))
+        return [t.detach().double().cpu() for t in (y, gx, gw, gb, gw2, mx, mR, mw)]
+
+    def hip(x, w, b):
+        assert w is conv.weight and b is conv.bias
+        return dconv.dfirst_lrelu(x, conv, 0.2)
+
+    w64 = conv.weight.detach().double().cpu().requires_grad_()
+    b64 = conv.bias.detach().double().cpu().requires_grad_()
+    ref = grads(lambda x, w, b: F.leaky_relu(F.conv2d(x, w, b, padding=1), 0.2), x64.clone().requires_grad_(),
+                R64.clone().requires_grad_(), w64, b64)
+    got = grads(hip, x64.float().to(gpu_device).requires_grad_(), R64.float().to(gpu_device).requires_grad_(),
+                conv.weight, conv.bias)
+    names = ('y', 'gx', 'gw', 'gb', 'gp_gw', 'mix_gx', 'mix_gR', 'mix_gw')
+    for n, a, r in zip(names, got, ref):
+        assert a.shape == r.shape, n
+        assert normwise_rel(a, r) < 1e-5, (n, normwise_rel(a, r))
+
+
+def test_first_conv_block_fused_in_discriminator(gpu_device):
+    """Discriminator_VGG_128_ runs its first conv block on the fused kernels (discriminator._run) and agrees with the
+    general path (ESR_DFIRST=0: im2col + the split-f16 1x1 conv + LeakyReLU) to the general path's x3 accuracy, in the
+    output and in the D step's parameter gradients with the WGAN-GP penalty."""
+    torch.manual_seed(5)
+    D = Discriminator_VGG_128_(3, 64, input_patch_size=64, nb=6).to(gpu_device).train()
+    x = torch.randn(2, 3, 64, 64, device=gpu_device, requires_grad=True)
+    runs = []
+    for fused in (True, False):
+        dconv.FUSED_FIRST = fused
+        try:
+            D.zero_grad()
+            y = D(x)
+            gx, = torch.autograd.grad(y.sum(), x, create_graph=True)
+            ((gx.reshape(2, -1).norm(dim=1) - 1) ** 2).mean().add(y.mean()).backward()
+            runs.append([y.detach().clone()] + [p.grad.clone() for p in D.parameters()])
+        finally:
+            dconv.FUSED_FIRST = True
+    assert normwise_rel(runs[0][0].cpu(), runs[1][0].cpu()) < 1e-4
+    # the gradients as one vector (a conv bias in front of a BatchNorm has a zero gradient: rounding noise alone)
+    flat = [torch.cat([g.reshape(-1) for g in r[1:]]).cpu() for r in runs]
+    assert normwise_rel(flat[0], flat[1]) < 1e-4
