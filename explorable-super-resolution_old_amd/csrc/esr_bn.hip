@@ -215,6 +215,15 @@ int colsum(const BnP &p, float *ws, float *out, hipStream_t st) {
 
 }  // namespace
 
+extern "C" int esr_colsum(const float *x, int64_t P, int32_t C, float *out, float *ws, esr_stream_t stream) {
+    if (!x || !out || !ws || P <= 0 || C <= 0) return ESR_EINVAL;
+    BnP p{};
+    p.x = x;
+    p.P = P;
+    p.C = C;
+    return colsum<0>(p, ws, out, (hipStream_t)stream);
+}
+
 extern "C" int64_t esr_bn_workspace_floats(int64_t P, int32_t C) {
     return (int64_t)MAXB * 3 * C * 2 + 8LL * C;  // float64 partials, then [5][C] sums
 }

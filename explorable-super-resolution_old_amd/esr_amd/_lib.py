@@ -8,7 +8,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('ESR_AMD_LIB', os.path.join(_HERE, 'libesr_amd.so'))
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 c_int = ctypes.c_int32
 c_float = ctypes.c_float
@@ -101,6 +101,7 @@ _SIGNATURES = {
                          c_int, c_void_p, c_void_p, c_void_p],
     'esr_dconv_uses_halo': [c_int, c_int, c_int, c_int, c_int, c_int],
     'esr_dconv_presplit': [c_void_p, ctypes.c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+    'esr_colsum': [c_void_p, ctypes.c_int64, c_int, c_void_p, c_void_p, c_void_p],
     'esr_dfirst_fwd': [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_int, c_void_p, c_void_p,
                        c_void_p],
     'esr_dfirst_bwd_blocks': [c_int, c_int, c_int],

@@ -42,6 +42,8 @@ S2D = os.environ.get('ESR_DCONV_S2D', '1') != '0'
 PRESPLIT = os.environ.get('ESR_DCONV_PRESPLIT', '1') != '0'
 # conv bias gradients (Σ over pixels of the output gradient) accumulated in float64 ('0': float32 sums)
 BIAS_F64 = os.environ.get('ESR_DCONV_BIAS_F64', '0') != '0'
+# first-order bias gradients by esr_colsum (float64 partials, one pass); '0' = PyTorch's sum (A/B)
+COLSUM = os.environ.get('ESR_DCONV_COLSUM', '1') != '0'
 
 
 def set_precision(p):
@@ -268,6 +270,20 @@ def conv_wgrad(x, gy, k, s, p, prec=None):
     return red.view(k, k, cin_pad, cout_pad)[:, :, :Ci, :Co].permute(3, 2, 0, 1).contiguous()
 
 
+def colsum(t):
+    """Σ over every dimension but the last of a contiguous float tensor (esr_colsum: float64 partial sums in fixed
+    order, one pass; PyTorch's sum over (0, 1, 2) of an NHWC tensor ran at ~0.2 TB/s)."""
+    _check_dev(t)
+    t = t.contiguous()
+    C = t.shape[-1]
+    P = t.numel() // C
+    lib = _lib.load()
+    out = torch.empty(C, device=t.device, dtype=torch.float32)
+    ws = torch.empty(int(lib.esr_bn_workspace_floats(P, C)), device=t.device, dtype=torch.float32)
+    _lib.check(lib.esr_colsum(t.data_ptr(), P, C, out.data_ptr(), ws.data_ptr(), _stream(t)), 'esr_colsum')
+    return out
+
+
 # The precision of a conv is fixed when its forward runs (the module default, or the layer's own
 # HipConv2d.esr_precision) and travels to every launch of its backward and double backward.
 class DConvFn(torch.autograd.Function):
@@ -288,7 +304,10 @@ class DConvFn(torch.autograd.Function):
         gw = WgradFn.apply(x, gy, k, s, p, prec) if ctx.needs_input_grad[1] else None
         gb = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            gb = gy.sum((0, 1, 2), dtype=torch.float64).float() if BIAS_F64 else gy.sum((0, 1, 2))
+            if torch.is_grad_enabled() or not COLSUM:  # create_graph: a differentiable sum
+                gb = gy.sum((0, 1, 2), dtype=torch.float64).float() if BIAS_F64 else gy.sum((0, 1, 2))
+            else:
+                gb = colsum(gy)
         return gx, gw, gb, None, None, None, None
 
 

@@ -429,6 +429,10 @@ int esr_op_size(void);                                  /* sizeof(esr_op), check
  * upstream u = ∂/∂gx, ggg = ∂/∂dγ, ggb = ∂/∂dβ (each may be NULL = 0): g_x, g_gy and g_gamma (formulas in
  * esr_bn.hip's header).  ws = scratch of esr_bn_workspace_floats(P, C) floats.  Deterministic (fixed-order sums). */
 int64_t esr_bn_workspace_floats(int64_t P, int32_t C);
+/* out[c] = Σ_p x[p][c] over a [P][C] float tensor, float64 partial sums in fixed order (bn_colsum + bn_finish); ws as
+ * above.  The discriminator convs' bias gradients (Σ of the output gradient over batch and pixels): PyTorch's
+ * reduction of an NHWC [B, H, W, C] tensor over (0, 1, 2) ran at ~0.2 TB/s. */
+int esr_colsum(const float *x, int64_t P, int32_t C, float *out, float *ws, esr_stream_t stream);
 int esr_bn_lrelu_fwd(const float *x, int64_t P, int32_t C, const float *gamma, const float *beta, float eps,
                      float slope, float *y, float *mu, float *rs, float *var, float *ws, float *running_mean,
                      float *running_var, int64_t *num_batches_tracked, float momentum, esr_stream_t stream);

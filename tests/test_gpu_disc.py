@@ -400,3 +400,22 @@ def test_first_conv_block_fused_in_discriminator(gpu_device):
     # the gradients as one vector (a conv bias in front of a BatchNorm has a zero gradient: rounding noise alone)
     flat = [torch.cat([g.reshape(-1) for g in r[1:]]).cpu() for r in runs]
     assert normwise_rel(flat[0], flat[1]) < 1e-4
+
+
+def test_colsum_vs_float64(gpu_device):
+    """dconv.colsum (esr_colsum: the D convs' first-order bias gradients) against a float64 sum, on NHWC shapes of the
+    config-3 discriminator and ragged ones; and DConvFn's bias gradient through it equals the differentiable path's
+    (create_graph) to fp32 rounding."""
+    torch.manual_seed(11)
+    for shape in ((16, 38, 38, 256), (2, 31, 31, 100), (3, 7, 5, 64), (1, 1, 1, 1), (5, 9, 3, 300)):
+        t = torch.randn(*shape, device=gpu_device)
+        got = dconv.colsum(t).double().cpu()
+        ref = t.double().sum((0, 1, 2)).cpu()
+        assert (got - ref).abs().max() <= 1e-6 * max(1.0, float(t.abs().sum((0, 1, 2)).max())), shape
+    conv = dconv.HipConv2d(16, 24, 3, 1, 1).to(gpu_device)
+    x = torch.randn(2, 16, 11, 13, device=gpu_device)
+    g = torch.randn(2, 24, 11, 13, device=gpu_device)
+    y = conv(x)
+    gb1, = torch.autograd.grad(y, conv.bias, g)
+    gb2, = torch.autograd.grad(conv(x), conv.bias, g, create_graph=True)
+    assert normwise_rel(gb1.cpu(), gb2.detach().cpu()) < 1e-5

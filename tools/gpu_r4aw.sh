@@ -1,0 +1,7 @@
+# round 4 verification at HEAD: every GPU test, smoke(), the bench line, a torch.profiler view of the config-3 step
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 1500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r4aw_tests.log 2>&1 || exit $?
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r4aw_smoke.log 2>&1 || exit $?
+timeout -k 10 400 python3 bench.py > gpurun_out/r4aw_bench.log 2>&1 || exit $?
+timeout -k 10 300 python -u tools/torch_prof_train.py --device > gpurun_out/r4aw_torchdev.log 2>&1 || exit $?
