@@ -946,6 +946,45 @@ __global__ void axpby_gs_kernel(void *out, int o_cp, int o_coff, int o_split, fl
     }
 }
 
+// out = a·x1 + b·x2 (fp32 out and x1, x2 split at scale S(amax)) on 64-channel slices, with max |out| OR-ed into
+// *out_amax: the closing add of an RRDB's x3 backward, whose result is the next RRDB's gradient-scale source
+// (esr_grad_amax fused).  A block walks whole image rows like grad_amax_kernel (16-B loads, index math per row) and
+// issues ONE atomic (one per wave, on the same word, cost 4 ms per config-3 step).
+__global__ void axpby_amax_kernel(float *out, int o_cp, int o_coff, float a, const float *x1, int x1_cp, int x1_coff,
+                                  float b, const void *x2, int x2_cp, int x2_coff, int x2_split, int C, int B, int H,
+                                  int W, const unsigned *amax, unsigned *out_amax) {
+    __shared__ float red[NT / 64];
+    const float inv_s = 1.f / gscale_of(amax);
+    const int G = C / 8;
+    float mx = 0.f;
+    for (long long row = blockIdx.x; row < (long long)B * H; row += gridDim.x) {
+        const long long bb = row / H, y = row - bb * H;
+        const long long pix0 = (bb * (H + 2) + y + 1) * (W + 2) + 1;
+        for (int k = threadIdx.x; k < W * G; k += NT) {
+            const int xx = k / G, g = k - xx * G;
+            const long long pix = pix0 + xx;
+            float v[8], w[8];
+            ld8(x1, pix, x1_cp, x1_coff + 8 * g, 0, 1.f, v);
+            ld8(x2, pix, x2_cp, x2_coff + 8 * g, x2_split, inv_s, w);
+            float *f = out + pix * o_cp + o_coff + 8 * g;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                float r = v[e] * a;  // (the expression of axpby_gs_kernel: the same rounding)
+                r += b * w[e];
+                f[e] = r;
+                mx = fmaxf(mx, fabsf(r));
+            }
+        }
+    }
+    for (int sh = 32; sh >= 1; sh >>= 1) mx = fmaxf(mx, __shfl_xor(mx, sh));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int wv = 1; wv < NT / 64; ++wv) mx = fmaxf(mx, red[wv]);
+        atomicMax(out_amax, __float_as_uint(mx));
+    }
+}
+
 __global__ void lrelu_bwd_kernel(float *d, int d_cp, int d_coff, const float *y, int y_cp, int y_coff, int C, int B,
                                  int H, int W, int y_split) {
     const long long idx = (long long)blockIdx.x * NT + threadIdx.x;
@@ -1355,6 +1394,21 @@ extern "C" int esr_axpby_gs(void *out, int32_t o_cp, int32_t o_coff, int32_t o_s
     hipLaunchKernelGGL(axpby_gs_kernel, dim3(nblocks((long long)B * H * W * (C / 8))), dim3(NT), 0,
                        (hipStream_t)stream, out, o_cp, o_coff, o_split, a, x1, x1_cp, x1_coff, x1_split, b, x2, x2_cp,
                        x2_coff, x2_split, C, B, H, W, amax, overflow);
+    return launched();
+}
+
+extern "C" int esr_axpby_gs_amax(float *out, int32_t o_cp, int32_t o_coff, float a, const void *x1, int32_t x1_cp,
+                                 int32_t x1_coff, int32_t x1_split, float b, const void *x2, int32_t x2_cp,
+                                 int32_t x2_coff, int32_t x2_split, int32_t C, int32_t B, int32_t H, int32_t W,
+                                 const uint32_t *amax, uint32_t *out_amax, esr_stream_t stream) {
+    if (!out || !x1 || !amax || !out_amax || C <= 0 || C % 8 || B <= 0 || H <= 0 || W <= 0 || (o_cp | o_coff) % 8 ||
+        (x1_cp | x1_coff) % 8 || (x2 && (x2_cp | x2_coff) % 8))
+        return ESR_EINVAL;
+    if (x1_split || !x2) return ESR_EINVAL;  // (the one form the x3 backward uses: fp32 x1, split or fp32 x2)
+    const long long rows = (long long)B * H;
+    hipLaunchKernelGGL(axpby_amax_kernel, dim3((unsigned)(rows < 2048 ? rows : 2048)), dim3(NT), 0,
+                       (hipStream_t)stream, out, o_cp, o_coff, a, static_cast<const float *>(x1), x1_cp, x1_coff, b,
+                       x2, x2_cp, x2_coff, x2_split, C, B, H, W, amax, out_amax);
     return launched();
 }
 

@@ -8,7 +8,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('ESR_AMD_LIB', os.path.join(_HERE, 'libesr_amd.so'))
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 c_int = ctypes.c_int32
 c_float = ctypes.c_float
@@ -75,6 +75,8 @@ _SIGNATURES = {
                          ctypes.POINTER(c_void_p), ctypes.POINTER(c_int), c_int,
                          ctypes.POINTER(c_void_p), ctypes.POINTER(c_int), c_int, c_int, c_float, c_void_p],
     'esr_grad_amax': [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    'esr_axpby_gs_amax': [c_void_p, c_int, c_int, c_float, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_int,
+                          c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     'esr_axpby_gs': [c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_int,
                      c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     'esr_lrelu_bwd': [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],

@@ -44,6 +44,9 @@ TRUNK_X3 = os.environ.get('ESR_TRUNK_X3', '1') != '0'
 # reads).  Opt-in ('1'): on one box, order-balanced, the config-3 step took 159.8 ms with it and 156.3 ms without
 # (profiles/r3_ab_stream.txt) — the concurrent kernels share the CUs and each runs longer than the overlap saves.
 WGRAD_STREAM = os.environ.get('ESR_WGRAD_STREAM', '0') == '1'
+# x3 backward: each RRDB's closing trunk-gradient add also takes the next RRDB's gradient max (esr_axpby_gs_amax: one
+# pass over the trunk gradient fewer per RRDB; bitwise the same scale); '0' = a separate esr_grad_amax (A/B)
+AMAX_FUSED = os.environ.get('ESR_AMAX_FUSED', '1') != '0'
 _SIDE = {}
 
 
@@ -667,14 +670,20 @@ def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_in
         if x3:  # gradient scale of this RRDB from max |trunk gradient| at its output
             amax = ws.gamax.data_ptr() + 4 * k
             ovf = ws.bwd_overflow.data_ptr()
-            _lib.check(lib.esr_grad_amax(ws.GA.data_ptr(), 64, 0, 64, Bn, H, W, amax, stream), 'grad_amax')
+            if k == net.nb - 1 or not AMAX_FUSED:  # (else: taken by the previous RRDB's closing add, below)
+                _lib.check(lib.esr_grad_amax(ws.GA.data_ptr(), 64, 0, 64, Bn, H, W, amax, stream), 'grad_amax')
             _lib.check(lib.esr_axpby_gs(D0.data_ptr(), dcp, d4, 1, 0.2, ws.GA.data_ptr(), 64, 0, 0, 0.0, None, 0, 0,
                                         0, 64, Bn, H, W, amax, ovf, stream), 'axpby_gs')
             for j, (dc, dn) in zip((2, 1, 0), ((D0, D1), (D1, D0), (D0, D1))):
                 _rdb_backward_x3(R, Q[3 * k + j], dc, bp.rdb[3 * k + j], R.x3[0][3 * k + j], zc, cp, H, W,
                                  (dn, dcp, d4), amax, z_first=j == 2)
-            _lib.check(lib.esr_axpby_gs(ws.GA.data_ptr(), 64, 0, 0, 1.0, ws.GA.data_ptr(), 64, 0, 0, 1.0,
-                                        D1.data_ptr(), dcp, d4, 1, 64, Bn, H, W, amax, ovf, stream), 'axpby_gs')
+            if k > 0 and AMAX_FUSED:  # the trunk gradient at this RRDB's input, and its max for the next RRDB's scale
+                _lib.check(lib.esr_axpby_gs_amax(ws.GA.data_ptr(), 64, 0, 1.0, ws.GA.data_ptr(), 64, 0, 0, 1.0,
+                                                 D1.data_ptr(), dcp, d4, 1, 64, Bn, H, W, amax,
+                                                 ws.gamax.data_ptr() + 4 * (k - 1), stream), 'axpby_gs_amax')
+            else:
+                _lib.check(lib.esr_axpby_gs(ws.GA.data_ptr(), 64, 0, 0, 1.0, ws.GA.data_ptr(), 64, 0, 0, 1.0,
+                                            D1.data_ptr(), dcp, d4, 1, 64, Bn, H, W, amax, ovf, stream), 'axpby_gs')
             if need_input and zc:  # latent-slot gradient of this RRDB's blocks, back to fp32
                 _lib.check(lib.esr_axpby_gs(ws.dZl.data_ptr(), 8, 0, 0, 1.0, ws.dZl.data_ptr(), 8, 0, 0, 1.0,
                                             ws.dzs.data_ptr(), 8, 0, 1, 8, Bn, H, W, amax, ovf, stream), 'axpby_gs')

@@ -199,6 +199,12 @@ int esr_axpby_gs(void *out, int32_t o_cp, int32_t o_coff, int32_t o_split, float
                  int32_t x1_coff, int32_t x1_split, float b, const void *x2, int32_t x2_cp, int32_t x2_coff,
                  int32_t x2_split, int32_t C, int32_t B, int32_t H, int32_t W, const uint32_t *amax,
                  int32_t *overflow, esr_stream_t stream);
+/* esr_axpby_gs with an fp32 output that also ORs max |out| into *out_amax (esr_grad_amax of the result, fused: the
+ * x3 backward's trunk gradient at an RRDB's input is the next RRDB's gradient-scale source). */
+int esr_axpby_gs_amax(float *out, int32_t o_cp, int32_t o_coff, float a, const void *x1, int32_t x1_cp, int32_t x1_coff,
+                      int32_t x1_split, float b, const void *x2, int32_t x2_cp, int32_t x2_coff, int32_t x2_split,
+                      int32_t C, int32_t B, int32_t H, int32_t W, const uint32_t *amax, uint32_t *out_amax,
+                      esr_stream_t stream);
 /* esr_wgrad_reduce / _gs with two scales: out[i] = (i < n_w ? scale_w : scale_b) [/ S(amax) if amax] · Σ_s
  * partial[s·n + i] — a conv's weights (first n_w entries) read activations of the x3 forward stored × its activation
  * scale A (scale_w carries 1/A), its bias gradient (the rest) does not. */

@@ -401,3 +401,34 @@ def test_frozen_generator_input_gradient_x3_forward(gpu_device, mode):
         assert normwise_rel(res[prec][0], ref[torch.float64][0]) < 1e-5, prec
     ok, msg = grad_parity(res['x3'][1], ref[torch.float64][1], ref[torch.float32][1])
     assert ok, msg
+
+
+def test_fused_gradient_amax_bitwise(gpu_device):
+    """The x3 backward with each RRDB's gradient max taken by the previous RRDB's closing add (esr_axpby_gs_amax,
+    train_engine.AMAX_FUSED) gives the same parameter and input gradients, bit for bit, as a separate esr_grad_amax
+    pass (max is exact in any order)."""
+    from esr_amd import engine, train_engine as TE
+    from oracle.recipe import seeded_inputs, seeded_params
+    B, h, w, nb = 2, 12, 16, 3
+    kw = dict(latent_input='all_layers_HR_downscaled', num_latent_channels=3)
+    sd = esr_amd.RRDBNet(3, 3, 64, nb, **kw).state_dict()
+    params = seeded_params([(k, tuple(v.shape)) for k, v in sd.items()], 95, w_scale=0.5)
+    lr, z = seeded_inputs(96, (B, 3, h, w), (B, 3, 4 * h, 4 * w), z_mode='pixel')
+    x = torch.cat([torch.from_numpy(z).view(B, 48, h, w), torch.from_numpy(lr)], 1)
+    R = torch.from_numpy(np.random.default_rng(97).standard_normal((B, 3, 4 * h, 4 * w)).astype(np.float32))
+    prev = TE.AMAX_FUSED
+    try:
+        runs = []
+        for fused in (True, False):
+            TE.AMAX_FUSED = fused
+            m = esr_amd.RRDBNet(3, 3, 64, nb, **kw)
+            m.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=False)
+            m = m.to(gpu_device)
+            engine.set_precision(m, 'x3')
+            xi = x.to(gpu_device).requires_grad_()
+            (m(xi) * R.to(gpu_device)).sum().backward()
+            runs.append([q.grad.clone() for q in m.parameters()] + [xi.grad.clone()])
+        for a, b in zip(*runs):
+            assert torch.equal(a, b)
+    finally:
+        TE.AMAX_FUSED = prev
