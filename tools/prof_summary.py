@@ -21,7 +21,7 @@ from collections import defaultdict
 LDS_TAGS = {132096: 'conv3x3_n64', 90624: 'conv3x3_n32', 86016: 'upconv2x_phase', 67584: 'upconv2x_phase_n32'}
 LDS_TAGS_X3 = {153600: 'x3_conv3x3_n64', 116736: 'x3_conv3x3_n32', 73728: 'x3_conv3x3_n32', 40960: 'x3_conv3x3_n32', 139264: 'x3_upconv2x_phase',
                96256: 'x3_upconv2x_phase_n32'}
-LDS_TAGS_X3C = {76800: 'x3_conv3x3_n64', 58368: 'x3_conv3x3_n32', 49152: 'x3_conv3x3_n32', 56320: 'x3_upconv2x_phase',
+LDS_TAGS_X3C = {76800: 'x3_conv3x3_n64', 67584: 'x3_conv3x3_n64', 58368: 'x3_conv3x3_n32', 49152: 'x3_conv3x3_n32', 56320: 'x3_upconv2x_phase',
                 48128: 'x3_upconv2x_phase_n32', 39936: 'x3_conv3x3_regB'}
 
 
