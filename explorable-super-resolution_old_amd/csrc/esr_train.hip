@@ -946,6 +946,52 @@ __global__ void axpby_gs_kernel(void *out, int o_cp, int o_coff, int o_split, fl
     }
 }
 
+// axpby_gs_kernel's per-element arithmetic (bitwise the same results) on whole image rows: a block walks rows
+// row = blockIdx.x + k·gridDim.x, the index math per row instead of a 64-bit division chain per 8-channel group
+// (config-3 step -0.5 ms, profiles/r4_axpby_rows_ab.txt).
+__global__ void axpby_rows_kernel(void *out, int o_cp, int o_coff, int o_split, float a, const void *x1, int x1_cp,
+                                  int x1_coff, int x1_split, float b, const void *x2, int x2_cp, int x2_coff,
+                                  int x2_split, int C, int B, int H, int W, const unsigned *amax, int *overflow) {
+    const float S = gscale_of(amax), inv_s = 1.f / S;
+    const int G = C / 8;
+    bool ok = true;
+    for (long long row = blockIdx.x; row < (long long)B * H; row += gridDim.x) {
+        const long long bb = row / H, y = row - bb * H;
+        const long long pix0 = (bb * (H + 2) + y + 1) * (W + 2) + 1;
+        for (int k = threadIdx.x; k < W * G; k += NT) {
+            const int xx = k / G, g = k - xx * G;
+            const long long pix = pix0 + xx;
+            float v[8], w[8];
+            ld8(x1, pix, x1_cp, x1_coff + 8 * g, x1_split, inv_s, v);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] *= a;
+            if (x2) {
+                ld8(x2, pix, x2_cp, x2_coff + 8 * g, x2_split, inv_s, w);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] += b * w[e];
+            }
+            if (o_split) {
+                f16x8 h, l;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float x = v[e] * S;
+                    h[e] = (_Float16)x;
+                    l[e] = (_Float16)(x - (float)h[e]);
+                    ok = ok && fabsf(x) < 65504.f;
+                }
+                unsigned char *p = static_cast<unsigned char *>(out) + (pix * o_cp + o_coff + 8 * g) * 4;
+                *reinterpret_cast<f16x8 *>(p) = h;
+                *reinterpret_cast<f16x8 *>(p + 16) = l;
+            } else {
+                float *f = static_cast<float *>(out) + pix * o_cp + o_coff + 8 * g;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) f[e] = v[e];
+            }
+        }
+    }
+    if (!ok && overflow) atomicOr(overflow, 1);
+}
+
 // out = a·x1 + b·x2 (fp32 out and x1, x2 split at scale S(amax)) on 64-channel slices, with max |out| OR-ed into
 // *out_amax: the closing add of an RRDB's x3 backward, whose result is the next RRDB's gradient-scale source
 // (esr_grad_amax fused).  A block walks whole image rows like grad_amax_kernel (16-B loads, index math per row) and
@@ -1391,9 +1437,15 @@ extern "C" int esr_axpby_gs(void *out, int32_t o_cp, int32_t o_coff, int32_t o_s
     if (!out || !x1 || !amax || C <= 0 || C % 8 || B <= 0 || H <= 0 || W <= 0 || (o_cp | o_coff) % 8 ||
         (x1_cp | x1_coff) % 8 || (x2 && (x2_cp | x2_coff) % 8))
         return ESR_EINVAL;
-    hipLaunchKernelGGL(axpby_gs_kernel, dim3(nblocks((long long)B * H * W * (C / 8))), dim3(NT), 0,
-                       (hipStream_t)stream, out, o_cp, o_coff, o_split, a, x1, x1_cp, x1_coff, x1_split, b, x2, x2_cp,
-                       x2_coff, x2_split, C, B, H, W, amax, overflow);
+    const long long rows = (long long)B * H;
+    if (g_axpby_rows)
+        hipLaunchKernelGGL(axpby_rows_kernel, dim3((unsigned)(rows < 2048 ? rows : 2048)), dim3(NT), 0,
+                           (hipStream_t)stream, out, o_cp, o_coff, o_split, a, x1, x1_cp, x1_coff, x1_split, b, x2,
+                           x2_cp, x2_coff, x2_split, C, B, H, W, amax, overflow);
+    else
+        hipLaunchKernelGGL(axpby_gs_kernel, dim3(nblocks((long long)B * H * W * (C / 8))), dim3(NT), 0,
+                           (hipStream_t)stream, out, o_cp, o_coff, o_split, a, x1, x1_cp, x1_coff, x1_split, b, x2,
+                           x2_cp, x2_coff, x2_split, C, B, H, W, amax, overflow);
     return launched();
 }
 

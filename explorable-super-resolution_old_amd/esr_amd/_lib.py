@@ -133,7 +133,8 @@ EXPORTED = tuple(_SIGNATURES)
 ABLATION_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), 'exp_lib', 'libesr_exp.so')
 ABLATION_SETTERS = ('esr_x3_set_kernel', 'esr_x3_set_tile_map', 'esr_x3_set_narrow', 'esr_x3_set_nsplit',
                     'esr_conv_set_tile', 'esr_cem_set_direct', 'esr_wgrad_set_kernel', 'esr_wgrad3_set_dma',
-                    'esr_dconv_set_halo', 'esr_dconv_set_occ3', 'esr_dconv_set_cw16', 'esr_dconv_set_rows')
+                    'esr_dconv_set_halo', 'esr_dconv_set_occ3', 'esr_dconv_set_cw16', 'esr_dconv_set_rows',
+                    'esr_axpby_set_rows')
 
 _lib = None
 
@@ -167,6 +168,8 @@ def bind(path):
         # same-box A/B runs of whole benchmarks (tools/gpu_ab_env.sh with ESR_AMD_LIB=exp_lib/libesr_exp.so)
         if os.environ.get('ESR_X3_NSPLIT') in ('0', '1'):
             lib.esr_x3_set_nsplit(int(os.environ['ESR_X3_NSPLIT']))
+        if os.environ.get('ESR_AXPBY_ROWS') in ('0', '1'):
+            lib.esr_axpby_set_rows(int(os.environ['ESR_AXPBY_ROWS']))
         if os.environ.get('ESR_X3_KERNEL', '').isdigit():
             lib.esr_x3_set_kernel(int(os.environ['ESR_X3_KERNEL']))
     return lib

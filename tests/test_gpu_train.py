@@ -432,3 +432,41 @@ def test_fused_gradient_amax_bitwise(gpu_device):
             assert torch.equal(a, b)
     finally:
         TE.AMAX_FUSED = prev
+
+
+def test_axpby_rows_kernel_bitwise(gpu_device, ablation_lib):
+    """esr_axpby_gs on the row-walking kernel (product) against the one-thread-per-8-channel-group kernel (ablation
+    variant): the same results, bit for bit, in every operand form the x3 backward uses (fp32 / split-f16 in and out,
+    with and without x2, an overflow flag)."""
+    import ctypes
+    from esr_amd import engine
+    lib = ablation_lib
+    B, H, W, cp = 2, 9, 13, 72
+    g = torch.Generator(device='cpu').manual_seed(5)
+    amax = torch.tensor([0.0], device=gpu_device)
+    amax.fill_(37.5)
+    amax_u = amax.view(torch.int32)
+    f1 = torch.randn(B, H + 2, W + 2, cp, generator=g).to(gpu_device)
+    f2 = torch.randn(B, H + 2, W + 2, cp, generator=g).to(gpu_device)
+    s2 = engine.to_split(torch.randn(B, H + 2, W + 2, 32, generator=g).to(gpu_device) * 100)  # 32 ch, 32 floats
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    forms = [  # (o_split, x1, x1_split, x2, x2_split, o_cp, C)
+        (0, f1, 0, f2, 0, cp, 64), (0, f1, 0, s2, 1, cp, 32), (1, f1, 0, None, 0, cp, 64), (0, s2, 1, None, 0, cp, 32),
+        (0, f1, 0, None, 0, cp, 8)]
+    try:
+        for o_split, x1, x1s, x2, x2s, o_cp, C in forms:
+            outs = []
+            for rows in (1, 0):
+                lib.esr_axpby_set_rows(rows)
+                out = torch.zeros(B, H + 2, W + 2, o_cp, device=gpu_device)
+                ovf = torch.zeros(1, dtype=torch.int32, device=gpu_device)
+                _lib_check = lib.esr_axpby_gs(out.data_ptr(), o_cp, 8, o_split, 0.7, x1.data_ptr(), x1.shape[-1], 0,
+                                              x1s, -1.3, x2.data_ptr() if x2 is not None else None,
+                                              x2.shape[-1] if x2 is not None else 0, 0, x2s, C, B, H, W,
+                                              amax_u.data_ptr(), ovf.data_ptr(), st)
+                assert _lib_check == 0
+                torch.cuda.synchronize()
+                outs.append((out, ovf))
+            assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1]), (o_split, x1s, x2s, C)
+    finally:
+        lib.esr_axpby_set_rows(1)
