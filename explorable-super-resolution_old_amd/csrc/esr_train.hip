@@ -1313,33 +1313,83 @@ __global__ __launch_bounds__(NT) void cem_adjoint_kernel(AdjParams p) {
 // One thread per output PIXEL, all C channels (the HR / LR gradient slots are C consecutive channels of a pixel
 // record of hr_cp / lr_cp floats: one sector per pixel instead of one per (pixel, channel) — the per-channel threads
 // re-fetched each 288-B HR record three times, 2.4 ms per config-5 iteration).  Same adds in the same order per output.
-__global__ void input_adjoint_kernel(const float *d_hr, int hr_cp, int hr_coff, const float *d_lr, int lr_cp,
-                                     int lr_coff, int sf, const float *d_pl, int C, int B, int Hp, int Wp, int M,
-                                     float *out) {
-    const int Ho = Hp - 2 * M, Wo = Wp - 2 * M;
+// The four corner outputs collect a (M+1)² block of the padded grid each (M = 88 at config 5: 7921 positions × C in
+// one thread held the launch for 2.3 ms): they are left to input_adjoint_corner_kernel, a block per corner.
+struct InAdj {
+    const float *d_hr;
+    int hr_cp, hr_coff;
+    const float *d_lr;
+    int lr_cp, lr_coff, sf;
+    const float *d_pl;
+    int C, B, Hp, Wp, M;
+};
+
+// the gradient reaching padded position (yp, xp), channel c, from the HR slot, the planar term and the LR slot
+__device__ __forceinline__ float in_adj_term(const InAdj &q, int b, int c, int yp, int xp) {
+    float v = 0.f;
+    const int Hl = q.sf > 0 ? q.Hp / q.sf : 0, Wl = q.sf > 0 ? q.Wp / q.sf : 0;
+    if (q.d_hr) v += q.d_hr[(((long long)b * (q.Hp + 2) + yp + 1) * (q.Wp + 2) + xp + 1) * q.hr_cp + q.hr_coff + c];
+    if (q.d_pl) v += q.d_pl[(((long long)b * q.C + c) * q.Hp + yp) * q.Wp + xp];
+    if (q.d_lr) {  // bilinear ↓sf, align_corners=False: sf = 4: mean of the central 2×2 of each 4×4 block; sf = 2: of the 2×2 block
+        const int ry = yp % q.sf, rx = xp % q.sf;
+        if ((ry == q.sf / 2 - 1 || ry == q.sf / 2) && (rx == q.sf / 2 - 1 || rx == q.sf / 2))
+            v += 0.25f * q.d_lr[(((long long)b * (Hl + 2) + yp / q.sf + 1) * (Wl + 2) + xp / q.sf + 1) * q.lr_cp +
+                                q.lr_coff + c];
+    }
+    return v;
+}
+
+__global__ void input_adjoint_kernel(InAdj q, float *out) {
+    const int Ho = q.Hp - 2 * q.M, Wo = q.Wp - 2 * q.M;
     const long long idx = (long long)blockIdx.x * NT + threadIdx.x;
-    if (idx >= (long long)B * Ho * Wo) return;
+    if (idx >= (long long)q.B * Ho * Wo) return;
     const int X = idx % Wo;
     const int Y = (idx / Wo) % Ho;
     const int b = idx / ((long long)Wo * Ho);
+    if (q.M > 0 && (Y == 0 || Y == Ho - 1) && (X == 0 || X == Wo - 1)) return;  // a corner: the corner kernel
     // padded positions that the replicate pad clamps onto (Y, X)
-    const int y0 = Y == 0 ? 0 : Y + M, y1 = Y == Ho - 1 ? Hp - 1 : Y + M;
-    const int x0 = X == 0 ? 0 : X + M, x1 = X == Wo - 1 ? Wp - 1 : X + M;
-    const int Hl = sf > 0 ? Hp / sf : 0, Wl = sf > 0 ? Wp / sf : 0;
-    for (int c = 0; c < C; ++c) {
+    const int y0 = Y == 0 ? 0 : Y + q.M, y1 = Y == Ho - 1 ? q.Hp - 1 : Y + q.M;
+    const int x0 = X == 0 ? 0 : X + q.M, x1 = X == Wo - 1 ? q.Wp - 1 : X + q.M;
+    for (int c = 0; c < q.C; ++c) {
         float v = 0.f;
         for (int yp = y0; yp <= y1; ++yp)
             for (int xp = x0; xp <= x1; ++xp) {
-                if (d_hr) v += d_hr[(((long long)b * (Hp + 2) + yp + 1) * (Wp + 2) + xp + 1) * hr_cp + hr_coff + c];
-                if (d_pl) v += d_pl[(((long long)b * C + c) * Hp + yp) * Wp + xp];
-                if (d_lr) {  // bilinear ↓sf, align_corners=False: sf = 4: mean of the central 2×2 of each 4×4 block; sf = 2: of the 2×2 block
-                    const int ry = yp % sf, rx = xp % sf;
-                    if ((ry == sf / 2 - 1 || ry == sf / 2) && (rx == sf / 2 - 1 || rx == sf / 2))
-                        v += 0.25f * d_lr[(((long long)b * (Hl + 2) + yp / sf + 1) * (Wl + 2) + xp / sf + 1) * lr_cp +
-                                          lr_coff + c];
+                if (q.d_hr) v += q.d_hr[(((long long)b * (q.Hp + 2) + yp + 1) * (q.Wp + 2) + xp + 1) * q.hr_cp +
+                                        q.hr_coff + c];
+                if (q.d_pl) v += q.d_pl[(((long long)b * q.C + c) * q.Hp + yp) * q.Wp + xp];
+                if (q.d_lr) {
+                    const int Hl = q.Hp / q.sf, Wl = q.Wp / q.sf;
+                    const int ry = yp % q.sf, rx = xp % q.sf;
+                    if ((ry == q.sf / 2 - 1 || ry == q.sf / 2) && (rx == q.sf / 2 - 1 || rx == q.sf / 2))
+                        v += 0.25f * q.d_lr[(((long long)b * (Hl + 2) + yp / q.sf + 1) * (Wl + 2) + xp / q.sf + 1) *
+                                                q.lr_cp + q.lr_coff + c];
                 }
             }
-        out[(((long long)b * C + c) * Ho + Y) * Wo + X] = v;
+        out[(((long long)b * q.C + c) * Ho + Y) * Wo + X] = v;
+    }
+}
+
+// block (b, corner k): the (M+1)² padded positions of that corner, per channel: each thread sums its strided share
+// of the positions (whole terms, in position order), then the 256 thread sums are added in thread order
+__global__ void input_adjoint_corner_kernel(InAdj q, float *out) {
+    __shared__ float red[NT];
+    const int Ho = q.Hp - 2 * q.M, Wo = q.Wp - 2 * q.M;
+    const int b = blockIdx.x >> 2, k = blockIdx.x & 3;
+    const int Y = (k & 2) ? Ho - 1 : 0, X = (k & 1) ? Wo - 1 : 0;
+    const int y0 = Y == 0 ? 0 : Y + q.M, y1 = Y == Ho - 1 ? q.Hp - 1 : Y + q.M;
+    const int x0 = X == 0 ? 0 : X + q.M, x1 = X == Wo - 1 ? q.Wp - 1 : X + q.M;
+    const int nx = x1 - x0 + 1, n = (y1 - y0 + 1) * nx;
+    for (int c = 0; c < q.C; ++c) {
+        float v = 0.f;
+        for (int e = threadIdx.x; e < n; e += NT) v += in_adj_term(q, b, c, y0 + e / nx, x0 + e % nx);
+        red[threadIdx.x] = v;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float t = 0.f;
+            for (int r = 0; r < NT; ++r) t += red[r];
+            out[(((long long)b * q.C + c) * Ho + Y) * Wo + X] = t;
+        }
+        __syncthreads();
     }
 }
 
@@ -1545,7 +1595,9 @@ extern "C" int esr_input_adjoint(const float *d_hr, int32_t hr_cp, int32_t hr_co
     if (d_hr && hr_coff + C > hr_cp) return ESR_EINVAL;
     if (d_lr && ((sf != 4 && sf != 2) || Hp % sf || Wp % sf || lr_coff + C > lr_cp)) return ESR_EINVAL;
     const long long n = (long long)B * (Hp - 2 * M) * (Wp - 2 * M);
-    hipLaunchKernelGGL(input_adjoint_kernel, dim3(nblocks(n)), dim3(NT), 0, (hipStream_t)stream, d_hr, hr_cp, hr_coff,
-                       d_lr, lr_cp, lr_coff, sf, d_pl, C, B, Hp, Wp, M, out);
+    const InAdj q{d_hr, hr_cp, hr_coff, d_lr, lr_cp, lr_coff, sf, d_pl, C, B, Hp, Wp, M};
+    hipLaunchKernelGGL(input_adjoint_kernel, dim3(nblocks(n)), dim3(NT), 0, (hipStream_t)stream, q, out);
+    if (M > 0)
+        hipLaunchKernelGGL(input_adjoint_corner_kernel, dim3(4 * B), dim3(NT), 0, (hipStream_t)stream, q, out);
     return launched();
 }
