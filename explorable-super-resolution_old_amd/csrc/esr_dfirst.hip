@@ -35,10 +35,14 @@ __device__ __forceinline__ float lrelu_mask(float m, float slope) { return m > 0
 // saved output: the double backward's data-gradient path); ESR_DFIRST_ACC: the previous contents of y are added
 // to the sum first (before the mask).
 constexpr int F_BLK = 256, F_HALF = CO / 2, F_PITCH = F_HALF + 4;
+// Layouts: pad = 0: x [B][H][W][x_cp], y / m [B][H][W][64] (y_cp = 64, y_coff = 0); pad = 1: the padded NHWC records
+// of the generator's backward, x [B][H+2][W+2][x_cp] (3 channels at 0), y [B][H+2][W+2][y_cp] at channel y_coff (no
+// mask), interior pixels only.
 __global__ __launch_bounds__(F_BLK) void dfirst_fwd_kernel(const float *__restrict__ x, long long P, int H, int W,
                                                            const float *__restrict__ w, const float *__restrict__ bias,
                                                            float slope, int flags, const float *__restrict__ m,
-                                                           float *__restrict__ y) {
+                                                           float *__restrict__ y, int x_cp, int pad, int y_cp,
+                                                           int y_coff) {
     // the outputs restaged through LDS one 32-channel half at a time (36 KB: four blocks per CU)
     __shared__ __attribute__((aligned(16))) float s[F_BLK * F_PITCH];
     const long long p0 = (long long)blockIdx.x * F_BLK;
@@ -55,7 +59,7 @@ __global__ __launch_bounds__(F_BLK) void dfirst_fwd_kernel(const float *__restri
             for (int kx = 0; kx < 3; ++kx) {
                 const int Y = yy + ky - 1, X = xx + kx - 1;
                 const bool in = Y >= 0 && Y < H && X >= 0 && X < W;
-                const float *src = x + ((b * H + Y) * W + X) * 3;
+                const float *src = x + (pad ? ((b * (H + 2) + Y + 1) * (W + 2) + X + 1) : ((b * H + Y) * W + X)) * x_cp;
 #pragma unroll
                 for (int ci = 0; ci < 3; ++ci) xin[ci * 9 + ky * 3 + kx] = in ? src[ci] : 0.f;
             }
@@ -91,7 +95,12 @@ __global__ __launch_bounds__(F_BLK) void dfirst_fwd_kernel(const float *__restri
             const long long q = p0 + px;
             if (q >= P) continue;
             float4 v = *reinterpret_cast<const float4 *>(s + px * F_PITCH + c);
-            float *dst = y + q * CO + F_HALF * h + c;
+            long long rec = q;  // output record of pixel q
+            if (pad) {
+                const long long xx = q % W, r = q / W, yy = r % H, bb = r / H;
+                rec = (bb * (H + 2) + yy + 1) * (W + 2) + xx + 1;
+            }
+            float *dst = y + rec * y_cp + y_coff + F_HALF * h + c;
             if (flags & ESR_DFIRST_ACC) {
                 const float4 o = *reinterpret_cast<const float4 *>(dst);
                 v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
@@ -297,7 +306,19 @@ extern "C" int esr_dfirst_fwd(const float *x, int32_t B, int32_t H, int32_t W, c
     if (((uintptr_t)y & 15) || (mask && ((uintptr_t)mask & 15))) return ESR_EINVAL;
     const long long P = (long long)B * H * W;
     hipLaunchKernelGGL(dfirst_fwd_kernel, dim3((unsigned)((P + F_BLK - 1) / F_BLK)), dim3(F_BLK), 0,
-                       (hipStream_t)stream, x, P, H, W, w, bias, slope, flags, mask, y);
+                       (hipStream_t)stream, x, P, H, W, w, bias, slope, flags, mask, y, 3, 0, CO, 0);
+    return launched();
+}
+
+extern "C" int esr_dfirst_fwd_padded(const float *x, int32_t x_cp, int32_t B, int32_t H, int32_t W, const float *w,
+                                     const float *bias, float slope, int32_t flags, float *y, int32_t y_cp,
+                                     int32_t y_coff, esr_stream_t stream) {
+    if (!x || !w || !y || B <= 0 || H <= 0 || W <= 0 || x_cp < 3 || (flags & ~(ESR_DFIRST_LRELU | ESR_DFIRST_ACC)) ||
+        y_coff < 0 || y_coff + CO > y_cp || (y_cp | y_coff) % 4 || ((uintptr_t)y & 15))
+        return ESR_EINVAL;
+    const long long P = (long long)B * H * W;
+    hipLaunchKernelGGL(dfirst_fwd_kernel, dim3((unsigned)((P + F_BLK - 1) / F_BLK)), dim3(F_BLK), 0,
+                       (hipStream_t)stream, x, P, H, W, w, bias, slope, flags, nullptr, y, x_cp, 1, y_cp, y_coff);
     return launched();
 }
 

@@ -8,7 +8,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('ESR_AMD_LIB', os.path.join(_HERE, 'libesr_amd.so'))
-ABI_VERSION = 21
+ABI_VERSION = 22
 
 c_int = ctypes.c_int32
 c_float = ctypes.c_float
@@ -106,6 +106,8 @@ _SIGNATURES = {
     'esr_colsum': [c_void_p, ctypes.c_int64, c_int, c_void_p, c_void_p, c_void_p],
     'esr_dfirst_fwd': [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_int, c_void_p, c_void_p,
                        c_void_p],
+    'esr_dfirst_fwd_padded': [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_int, c_void_p,
+                              c_int, c_int, c_void_p],
     'esr_dfirst_bwd_blocks': [c_int, c_int, c_int],
     'esr_dfirst_bwd': [c_void_p, c_void_p, c_void_p, c_float, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                        c_void_p],

@@ -44,6 +44,9 @@ TRUNK_X3 = os.environ.get('ESR_TRUNK_X3', '1') != '0'
 # reads).  Opt-in ('1'): on one box, order-balanced, the config-3 step took 159.8 ms with it and 156.3 ms without
 # (profiles/r3_ab_stream.txt) — the concurrent kernels share the CUs and each runs longer than the overlap saves.
 WGRAD_STREAM = os.environ.get('ESR_WGRAD_STREAM', '0') == '1'
+# HR_conv1's data gradient (3 -> 64 channels, 3x3, at HR) on esr_dfirst_fwd_padded (exact fp32 on the VALU; the fp32
+# MFMA conv pads its 3 input channels to a 32-wide K step: 0.86 ms at config 3); '0' = the MFMA conv (A/B)
+HR1_DFIRST = os.environ.get('ESR_HR1_DFIRST', '1') != '0'
 # x3 backward: each RRDB's closing trunk-gradient add also takes the next RRDB's gradient max (esr_axpby_gs_amax: one
 # pass over the trunk gradient fewer per RRDB; bitwise the same scale); '0' = a separate esr_grad_amax (A/B)
 AMAX_FUSED = os.environ.get('ESR_AMAX_FUSED', '1') != '0'
@@ -613,7 +616,12 @@ def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_in
     # HR_conv1 (no act): input HR1 = [Z_HR | x]
     R.wgrad(bp.hr1, HR1, hcp, hcp, 0, ws.dgen_p, 8, 0, HH, WW)
     R.dgrad_in(bp.hr1, ws.dgen_p, 8, 0, 8, HH, WW, ws.dZh, 8)
-    R.dgrad(bp.hr1, ws.dgen_p, 8, 0, 8, HH, WW, dA, 64, zc, accumulate=False)
+    if HR1_DFIRST:  # the 3 -> 64 data gradient on the VALU kernel of the D's first conv (flipped, transposed weights)
+        wt = bp.hr1.conv.weight[:, -64:].detach().flip(2, 3).permute(1, 0, 2, 3).contiguous()
+        _lib.check(lib.esr_dfirst_fwd_padded(ws.dgen_p.data_ptr(), 8, Bn, HH, WW, wt.data_ptr(), None, 0.0, 0,
+                                             dA.data_ptr(), 64, 0, stream), 'hr1 data gradient')
+    else:
+        R.dgrad(bp.hr1, ws.dgen_p, 8, 0, 8, HH, WW, dA, 64, zc, accumulate=False)
     # HR_conv0 + LReLU: output HR1.x
     R.lrelu(dA, 64, 0, HR1, hcp, zc, 64, HH, WW)
     R.wgrad(bp.hr0, HR0, hcp, hcp, 0, dA, 64, 0, HH, WW)

@@ -358,6 +358,12 @@ int esr_dconv_col2im(const float *gc, int32_t B, int32_t H, int32_t W, int32_t C
 #define ESR_DFIRST_ACC 4
 int esr_dfirst_fwd(const float *x, int32_t B, int32_t H, int32_t W, const float *w, const float *bias, float slope,
                    int32_t flags, const float *mask, float *y, esr_stream_t stream);
+/* esr_dfirst_fwd on the padded NHWC records of the generator's backward (halo 1, zero): x [B][H+2][W+2][x_cp] (3
+ * channels at 0), y [B][H+2][W+2][y_cp] at channel y_coff, interior written (flags: LRELU / ACC).  HR_conv1's data
+ * gradient (architecture.py:141) is this 3 -> 64 3×3 conv with its weights flipped and transposed. */
+int esr_dfirst_fwd_padded(const float *x, int32_t x_cp, int32_t B, int32_t H, int32_t W, const float *w,
+                          const float *bias, float slope, int32_t flags, float *y, int32_t y_cp, int32_t y_coff,
+                          esr_stream_t stream);
 int esr_dfirst_bwd_blocks(int32_t B, int32_t H, int32_t W);
 int esr_dfirst_bwd(const float *x, const float *gy, const float *mask, float slope, int32_t B, int32_t H, int32_t W,
                    const float *w, float *gx, float *partial, esr_stream_t stream);

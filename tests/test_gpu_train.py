@@ -470,3 +470,35 @@ def test_axpby_rows_kernel_bitwise(gpu_device, ablation_lib):
             assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1]), (o_split, x1s, x2s, C)
     finally:
         lib.esr_axpby_set_rows(1)
+
+
+@pytest.mark.parametrize('latent', [False, True])
+def test_hr1_data_gradient_on_first_conv_kernel(gpu_device, latent):
+    """HR_conv1's data gradient on esr_dfirst_fwd_padded (train_engine.HR1_DFIRST: exact fp32 on the VALU) against the
+    fp32 MFMA conv it replaces: every parameter gradient and the input gradient agree to fp32 rounding (1e-5)."""
+    from esr_amd import engine, train_engine as TE
+    from oracle.recipe import seeded_inputs, seeded_params
+    B, h, w, nb = 2, 12, 16, 1
+    kw = dict(latent_input='all_layers_HR_downscaled' if latent else None, num_latent_channels=3 if latent else 0)
+    sd = esr_amd.RRDBNet(3, 3, 64, nb, **kw).state_dict()
+    params = seeded_params([(k, tuple(v.shape)) for k, v in sd.items()], 98, w_scale=0.5)
+    lr, z = seeded_inputs(99, (B, 3, h, w), (B, 3, 4 * h, 4 * w), z_mode='pixel')
+    x = torch.from_numpy(lr)
+    if latent:
+        x = torch.cat([torch.from_numpy(z).view(B, 48, h, w), x], 1)
+    R = torch.from_numpy(np.random.default_rng(100).standard_normal((B, 3, 4 * h, 4 * w)).astype(np.float32))
+    prev = TE.HR1_DFIRST
+    try:
+        runs = []
+        for on in (True, False):
+            TE.HR1_DFIRST = on
+            m = esr_amd.RRDBNet(3, 3, 64, nb, **kw)
+            m.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=False)
+            m = m.to(gpu_device)
+            engine.set_precision(m, 'f32')
+            xi = x.to(gpu_device).requires_grad_()
+            (m(xi) * R.to(gpu_device)).sum().backward()
+            runs.append(torch.cat([q.grad.reshape(-1) for q in m.parameters()] + [xi.grad.reshape(-1)]).cpu())
+        assert normwise_rel(runs[0], runs[1]) < 1e-5
+    finally:
+        TE.HR1_DFIRST = prev
