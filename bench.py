@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Benchmark of the RRDB-23 + CEM ×4 super-resolution hot path on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N --steps K --warmup W]        (N>1: launched by torch.distributed.run, one rank per GPU)
+    python bench.py [--gpus N --steps K --warmup W]        (N>1: N ranks, one per GPU — started by this script through
+                                                           torch.distributed.run, or by an external one: bench_launch.py)
 
 A step = one forward of CEM_PyTorch(RRDBNet-23) in eval mode (CEM pre-pad, the reference's test path
 SRRaGANModel.test(), SRRaGAN_model.py:577-584) over one batch of B synthetic 128×128 LR images already resident in
@@ -43,7 +44,9 @@ HBM_PEAK_GBS = 8000.0
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--gpus', type=int, default=None, help='ranks (one per GPU); default: WORLD_SIZE, else 1')
+    ap.add_argument('--launcher-check', action='store_true', help='bring the ranks up on the CPU (gloo), agree on the '
+                    'world size, print it and stop (no GPU)')
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--batch', type=int, default=32, help='images per GPU (BASELINE config 2: 32)')
@@ -251,13 +254,17 @@ def run_legs(args, dev, world, rank):
 
 def main():
     args = parse()
-    world = int(os.environ.get('WORLD_SIZE', '1'))
+    import bench_launch
+    world = bench_launch.ranks(args.gpus, os.path.abspath(__file__), sys.argv[1:],
+                               check_devices=not args.launcher_check)
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if args.launcher_check:
+        bench_launch.launcher_check(world, rank)
+        return
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
-    if world > 1:
-        dist.init_process_group('nccl', device_id=dev)
+    world = bench_launch.init(dev, world)
     from esr_amd import engine
     if args.x3_kernel is not None:
         from esr_amd import _lib
@@ -341,6 +348,8 @@ def main():
                      'flops_per_launch': fl / n_l, 'avg_launch_us': round(ms / n_l * 1e3, 2)},
         'kernels': kernels,
         'gpu_busy_frac': round(tot / (dt * 1e3), 3),
+        'dist': {'world_size': dist.get_world_size() if world > 1 else 1,
+                 'backend': dist.get_backend() if world > 1 else None},
     }
     traffic = pmc_traffic(dom)
     if traffic is not None:

@@ -119,6 +119,7 @@ def run(args, dev, world, rank):
     reruns1, a1 = engine.OVERFLOW_RERUNS, engine.act_scale(rrdb)
     settle()
     obs0 = observe()
+    comm0 = comm_stats(model)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -134,6 +135,7 @@ def run(args, dev, world, rank):
     dt = time.perf_counter() - t0
     step_ms = [round((b - a) * 1e3, 2) for a, b in zip([t0] + stamps[:-1], stamps)]
     obs = observed(obs0, observe())
+    comm = {k: round((v - comm0[k]) / args.steps, 3) for k, v in comm_stats(model).items()}
     unsettle()
     if world > 1:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
@@ -160,12 +162,28 @@ def run(args, dev, world, rank):
             'step_ms': step_ms,
             'overflow_reruns': {'warmup': reruns1 - reruns0, 'timed': engine.OVERFLOW_RERUNS - reruns1},
             'act_scale': {'before_warmup': a0, 'before_timed': a1, 'after_timed': engine.act_scale(rrdb)},
-            'timed_region': obs}
+            'timed_region': obs,
+            'dist': {'world_size': dist.get_world_size() if world > 1 else 1,
+                     'backend': dist.get_backend() if world > 1 else None,
+                     'per_step': comm,
+                     'note': 'G + D gradient buckets: RCCL all-reduces, bytes and the compute-stream time left waiting '
+                             'for them (exposed_ms), averaged over the timed steps'}}
+
+
+def comm_stats(model):
+    """Summed GradBuckets counters of G and D (SRRaGAN_model.GradBuckets.comm_stats)."""
+    tot = {'allreduces': 0, 'allreduce_bytes': 0, 'exposed_ms': 0.0}
+    for b in (model._g_buckets, model._d_buckets):
+        if b is not None:
+            for k, v in b.comm_stats().items():
+                tot[k] += v
+    return tot
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--gpus', type=int, default=None, help='ranks (one per GPU); default: WORLD_SIZE, else 1')
+    ap.add_argument('--launcher-check', action='store_true', help='bring the ranks up on the CPU (gloo) and stop')
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=4)
     ap.add_argument('--batch', type=int, default=16)
@@ -173,13 +191,18 @@ def main():
     ap.add_argument('--nb', type=int, default=23)
     ap.add_argument('--no-latent', dest='latent', action='store_false')
     args = ap.parse_args()
-    world = int(os.environ.get('WORLD_SIZE', '1'))
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import bench_launch
+    world = bench_launch.ranks(args.gpus, os.path.abspath(__file__), sys.argv[1:],
+                               check_devices=not args.launcher_check)
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if args.launcher_check:
+        bench_launch.launcher_check(world, rank)
+        return
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
-    if world > 1:
-        dist.init_process_group('nccl', device_id=dev)
+    world = bench_launch.init(dev, world)
     rec = run(args, dev, world, rank)
     if rank == 0:
         print(json.dumps(rec), flush=True)

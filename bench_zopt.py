@@ -133,7 +133,8 @@ def run(args, dev, world, rank):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--gpus', type=int, default=None, help='ranks (one per GPU); default: WORLD_SIZE, else 1')
+    ap.add_argument('--launcher-check', action='store_true', help='bring the ranks up on the CPU (gloo) and stop')
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=4)
     ap.add_argument('--batch', type=int, default=8)
@@ -142,13 +143,18 @@ def main():
     ap.add_argument('--objective', default='max_STD')
     ap.add_argument('--kernel', choices=sorted(KERNELS), default='kgan')
     args = ap.parse_args()
-    world = int(os.environ.get('WORLD_SIZE', '1'))
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import bench_launch
+    world = bench_launch.ranks(args.gpus, os.path.abspath(__file__), sys.argv[1:],
+                               check_devices=not args.launcher_check)
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if args.launcher_check:
+        bench_launch.launcher_check(world, rank)
+        return
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
-    if world > 1:
-        dist.init_process_group('nccl', device_id=dev)
+    world = bench_launch.init(dev, world)
     rec = run(args, dev, world, rank)
     if rank == 0:
         print(json.dumps(rec), flush=True)

@@ -117,6 +117,22 @@ class GradBuckets:
         self._works = [None] * len(self.buckets)
         self.hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params] \
             if _world() > 1 else []
+        # what went over the wire: collectives, bytes, and the stream time finish() left exposed (device events
+        # around the waits, read lazily by comm_stats so no host sync is added to the step)
+        self.n_allreduce = 0
+        self.allreduce_bytes = 0
+        self._exposed = []
+        self._exposed_ms = 0.0
+
+    def comm_stats(self):
+        """{'allreduces', 'allreduce_bytes', 'exposed_ms'} since construction (exposed_ms: compute-stream time spent
+        waiting in finish() for the collectives, i.e. the part not overlapped with the backward)."""
+        for e0, e1 in self._exposed:
+            e1.synchronize()
+            self._exposed_ms += e0.elapsed_time(e1)
+        self._exposed = []
+        return {'allreduces': self.n_allreduce, 'allreduce_bytes': self.allreduce_bytes,
+                'exposed_ms': round(self._exposed_ms, 3)}
 
     def arm(self):
         self.armed = _world() > 1
@@ -132,6 +148,8 @@ class GradBuckets:
             return
         flat = torch.cat([g.reshape(-1) for g in grads])
         self._works[b] = (dist.all_reduce(flat, async_op=True), flat, grads)
+        self.n_allreduce += 1
+        self.allreduce_bytes += flat.numel() * flat.element_size()
 
     def _on_grad(self, p):
         if not self.armed:
@@ -152,11 +170,20 @@ class GradBuckets:
         for b in range(self._next, len(self.buckets)):  # the rest, still in bucket order
             self._launch(b)
         w = _world()
-        for item in self._works:
-            if not item:
-                continue
-            work, flat, grads = item
+        items = [it for it in self._works if it]
+        ev = None
+        if items and items[0][1].is_cuda:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        for work, _, _ in items:
             work.wait()
+        if ev is not None:
+            ev[1].record()
+            while self._exposed and self._exposed[0][1].query():  # fold the completed ones (no sync): bounded list
+                e0, e1 = self._exposed.pop(0)
+                self._exposed_ms += e0.elapsed_time(e1)
+            self._exposed.append(ev)
+        for _, flat, grads in items:
             flat /= w
             o = 0
             for g in grads:

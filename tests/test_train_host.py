@@ -106,6 +106,9 @@ def _dist_worker(rank, world, port, q):
         net(x).square().sum().backward()
         launched = buckets.launched_in_backward
         buckets.finish()
+        cs = buckets.comm_stats()
+        comm = (cs['allreduces'] == len(buckets.buckets),
+                cs['allreduce_bytes'] == sum(p_.numel() * 4 for p_ in net.parameters()))
         ref_net(x).square().sum().backward()
         M._allreduce_grads(list(ref_net.parameters()))
         same = all(torch.allclose(a.grad, b.grad, rtol=1e-6, atol=1e-7) for a, b in zip(net.parameters(),
@@ -159,7 +162,7 @@ def _dist_worker(rank, world, port, q):
         # tensors travel as NumPy copies: a tensor in a multiprocessing queue is handed over through a file descriptor
         # of the sending process, which may already have exited
         q.put((rank, p[0].grad.numpy().copy(), p[1].grad.numpy().copy(), diff, correct, d_real, d_fake, launched, same,
-               untouched, bufs, gd, gc, cur, past, flat))
+               untouched, bufs, gd, gc, cur, past, flat, comm))
     finally:
         dist.destroy_process_group()
 
@@ -196,3 +199,4 @@ def test_ddp_gradient_average_and_consistent_statistics():
     assert res[0][11:15] == res[1][11:15]
     assert res[0][15][0] and res[1][15][0]  # FlatAdam + buckets == per-tensor Adam + flat average
     assert res[0][15][1] == res[1][15][1]   # and the ranks hold the same parameters
+    assert all(res[0][16]) and all(res[1][16])  # comm_stats: one all-reduce per bucket, every gradient byte once
