@@ -153,9 +153,12 @@ def _gather(src, packed, bias, out, MH, MW, omy, oay, omx, oax, smy, smx, offy, 
     n = 4 * N if d2s_pad is not None else N
     lib = _lib.load()
     mode = _mode(prec)
-    wsx, wexp = packed.split() if mode in (1, 2) and PRESPLIT else (None, None)
-    oy, ox = _i32(offy), _i32(offx)
     sd = s2d_pad is not None or d2s_pad is not None
+    # the pre-split weights feed only the x3 halo kernel: not built for launches the gather kernel takes
+    wsx, wexp = packed.split() if (mode in (1, 2) and PRESPLIT and
+                                   lib.esr_dconv_uses_halo(smy, smx, len(offy), MW, int(sd), mode) == 1) \
+        else (None, None)
+    oy, ox = _i32(offy), _i32(offx)
     # split-K where the grid would fill few CUs and K is long (the 8x8 pseudo-FC layer); the library says how many
     ks = lib.esr_dconv_fwd_splits_sd(B, MH, MW, n, kc, smy, smx, len(offy), oy, ox, int(sd), mode)
     if ks < 1:

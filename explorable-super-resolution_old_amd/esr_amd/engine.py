@@ -100,13 +100,17 @@ ACT_SCALE_REDUCTIONS = 0
 def lower_act_scale(net):
     """A scaled activation of an x3 forward left f16's range: the model's A drops 16× (floor 1) and stays there — a
     deliberate one-way ratchet, so a model fed out-of-range inputs does not overflow (and rerun in fp32) again and
-    again; the count is kept in ACT_SCALE_REDUCTIONS and each reduction is reported once per model."""
+    again; ACT_SCALE_REDUCTIONS counts the reductions that happened and each is reported once (an overflow at the floor
+    A = 1 lowers nothing and reports nothing: the fp32 rerun is counted in OVERFLOW_RERUNS)."""
     global ACT_SCALE_REDUCTIONS
     old = act_scale(net)
-    net._esr_act_scale = max(1.0, old / 16)
+    new = max(1.0, old / 16)
+    if new >= old:
+        return
+    net._esr_act_scale = new
     ACT_SCALE_REDUCTIONS += 1
     warnings.warn('esr_amd: x3 activation scale of %s lowered %g -> %g after an f16-range overflow'
-                  % (type(net).__name__, old, net._esr_act_scale), RuntimeWarning, stacklevel=2)
+                  % (type(net).__name__, old, new), RuntimeWarning, stacklevel=2)
 
 
 def _prof_begin(prof, tag, flops):

@@ -286,3 +286,23 @@ def test_cem_set_upscale_kernel_equals_fresh_design():
     assert int(cem.loss_mask.sum()) == (384 - 2 * M) ** 2
     x = torch.arange(2 * 3 * 5 * 5, dtype=torch.float32).view(2, 3, 5, 5)
     assert torch.equal(model.LR_padder(x), fresh.LR_padder(x))
+
+
+def test_lower_act_scale_counts_only_real_reductions():
+    """at the floor A = 1 an overflow lowers nothing, so neither the counter nor a warning moves."""
+    import warnings
+
+    class Net:
+        pass
+    net = Net()
+    net._esr_act_scale = 256.0
+    r0 = engine.ACT_SCALE_REDUCTIONS
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter('always')
+        engine.lower_act_scale(net)
+    assert net._esr_act_scale == 16.0 and engine.ACT_SCALE_REDUCTIONS == r0 + 1 and len(w) == 1
+    net._esr_act_scale = 1.0
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter('always')
+        engine.lower_act_scale(net)
+    assert net._esr_act_scale == 1.0 and engine.ACT_SCALE_REDUCTIONS == r0 + 1 and not w
