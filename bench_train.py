@@ -40,6 +40,9 @@ def make_opt(args):
     }
 
 
+GC_POLICY = ('Python GC: gc.collect() + gc.freeze() after the warm-up (settle(): the models, op lists and packed '
+             'weights leave the collector, as in a serving process after model load), collector otherwise on; gc_gen2 / '
+             'gc_ms count the collections and time inside the timed steps')
 _GC_PAUSE = [0.0, None]  # total seconds Python's cyclic GC has run, start of the current collection
 
 
@@ -162,7 +165,7 @@ def run(args, dev, world, rank):
             'step_ms': step_ms,
             'overflow_reruns': {'warmup': reruns1 - reruns0, 'timed': engine.OVERFLOW_RERUNS - reruns1},
             'act_scale': {'before_warmup': a0, 'before_timed': a1, 'after_timed': engine.act_scale(rrdb)},
-            'timed_region': obs,
+            'timed_region': dict(obs, gc_policy=GC_POLICY),
             'dist': {'world_size': dist.get_world_size() if world > 1 else 1,
                      'backend': dist.get_backend() if world > 1 else None,
                      'per_step': comm,

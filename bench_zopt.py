@@ -84,7 +84,7 @@ def run(args, dev, world, rank):
     reruns1 = engine.OVERFLOW_RERUNS
     a1 = engine.act_scale(rrdb)
     zo.max_iters = args.steps
-    from bench_train import observe, observed, settle, unsettle
+    from bench_train import GC_POLICY, observe, observed, settle, unsettle
     settle()
     obs0 = observe()
     stamps = []
@@ -128,7 +128,7 @@ def run(args, dev, world, rank):
             'iter_ms': iter_ms,
             'overflow_reruns': {'warmup': reruns1 - reruns0, 'timed': engine.OVERFLOW_RERUNS - reruns1},
             'act_scale': {'before_warmup': a0, 'before_timed': a1, 'after_timed': engine.act_scale(rrdb)},
-            'timed_region': obs}
+            'timed_region': dict(obs, gc_policy=GC_POLICY)}
 
 
 def main():

@@ -174,7 +174,19 @@ def bind(path):
             lib.esr_axpby_set_rows(int(os.environ['ESR_AXPBY_ROWS']))
         if os.environ.get('ESR_X3_KERNEL', '').isdigit():
             lib.esr_x3_set_kernel(int(os.environ['ESR_X3_KERNEL']))
+    else:
+        stale = [k for k in RETIRED_ENV if k in os.environ]
+        if stale:  # switches of earlier rounds: the product library has no selection state, so they change nothing
+            import warnings
+            warnings.warn('esr_amd: %s set but %s is the product library, which has no kernel-selection state: '
+                          'the default kernels run; for an A/B use the ablation library (ESR_AMD_LIB=%s)'
+                          % (', '.join(stale), os.path.basename(path), ABLATION_PATH), RuntimeWarning, stacklevel=2)
     return lib
+
+
+# environment switches that now act only through the ablation library's setters (ignored by the product library)
+RETIRED_ENV = ('ESR_X3_NSPLIT', 'ESR_AXPBY_ROWS', 'ESR_X3_KERNEL', 'ESR_DCONV_HALO', 'ESR_DCONV_OCC3',
+               'ESR_DCONV_CW16', 'ESR_DCONV_ROWS', 'ESR_WGRAD3_DMA', 'ESR_X3_TILE_MAP', 'ESR_X3_NARROW')
 
 
 def load():

@@ -317,8 +317,9 @@ def _im2col_ref(xh, k, p):
 
 def test_im2col_col2im_vs_autograd_through_cat_and_pad(gpu_device):
     """The first conv's 3-channel path: esr_dconv_im2col bitwise the slice / pad / cat restatement; _Im2ColFn's
-    gradient (esr_dconv_col2im) and the gradient of that gradient (the WGAN-GP double backward) bitwise autograd
-    through the restatement (the same adds in the same order), fp32 on the device."""
+    gradient (esr_dconv_col2im) within 1e-5 of autograd through the restatement (each input pixel sums its <= k*k
+    overlapping taps in another order than autograd's adds, so not bitwise), and the gradient of that gradient (the
+    WGAN-GP double backward: im2col of the vector again, a pure gather) bitwise; fp32 on the device."""
     from esr_amd import dconv
     torch.manual_seed(0)
     for k, p, C in ((3, 1, 3), (3, 0, 3), (5, 2, 1)):

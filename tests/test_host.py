@@ -306,3 +306,13 @@ def test_lower_act_scale_counts_only_real_reductions():
         warnings.simplefilter('always')
         engine.lower_act_scale(net)
     assert net._esr_act_scale == 1.0 and engine.ACT_SCALE_REDUCTIONS == r0 + 1 and not w
+
+
+def test_retired_switch_on_product_library_warns(monkeypatch):
+    """an A/B environment switch of an earlier round does nothing on the product library; say so."""
+    import warnings
+    monkeypatch.setenv('ESR_DCONV_HALO', '0')
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter('always')
+        _lib.bind(_lib.LIB_PATH)
+    assert any('ESR_DCONV_HALO' in str(x.message) for x in w)
