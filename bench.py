@@ -87,18 +87,43 @@ def build_model(args, dev):
     return model.to(dev)
 
 
-def make_input(args, dev, rank):
+def make_gt(args, dev, rank):
+    """Seeded synthetic ground-truth HR images (B, 3, 4h, 4w) in [0, 1]: smooth structure (bicubic 16x up of a 32² /
+    8x up of a 64² noise field) plus fine detail, so that an SR result has a meaningful PSNR against them."""
+    import torch.nn.functional as F
     g = torch.Generator().manual_seed(100 + rank)
     B, h = args.batch, args.lr_size
-    x = torch.rand(B, 3, h, h, generator=g)
+    H = 4 * h
+    coarse = torch.rand(B, 3, h // 4, h // 4, generator=g)
+    mid = torch.rand(B, 3, h // 2, h // 2, generator=g)
+    fine = torch.rand(B, 3, H, H, generator=g)
+    gt = (0.6 * F.interpolate(coarse, size=(H, H), mode='bicubic', align_corners=False)
+          + 0.3 * F.interpolate(mid, size=(H, H), mode='bicubic', align_corners=False) + 0.1 * fine)
+    return gt.clamp_(0, 1).to(dev)
+
+
+def make_input(args, dev, rank, model=None):
+    """The LR batch: the CEM's own DownscaleOP (the reference's degradation, CEMnet.py:152,157-162; the build's device
+    stencil) of the seeded ground truth make_gt(), so the SR outputs can be scored against it (PSNR-Δ, SURVEY §8d);
+    without a CEM (--no-cem) seeded U[0, 1) LR images.  Latent variant: per-image constant Z, raw HR view."""
+    g = torch.Generator().manual_seed(200 + rank)
+    B, h = args.batch, args.lr_size
+    if model is not None and hasattr(model, 'DownscaleOP'):
+        with torch.no_grad():
+            x = model.DownscaleOP(make_gt(args, dev, rank)).contiguous()
+    else:
+        x = torch.rand(B, 3, h, h, generator=g).to(dev)
     if args.variant == 'latent':  # per-image constant Z (training-time feed_data), raw HR view (ConcatLatent)
-        z = (2 * torch.rand(B, 3, 1, 1, generator=g) - 1).expand(B, 3, 4 * h, 4 * h).contiguous()
+        z = (2 * torch.rand(B, 3, 1, 1, generator=g) - 1).expand(B, 3, 4 * h, 4 * h).contiguous().to(dev)
         x = torch.cat([z.view(B, 48, h, h), x], 1)
-    return x.to(dev)
+    return x
 
 
-def cpu_baseline(args, model, x_gpu, out_gpu):
-    """The CPU oracle on a bounded sample of the same workload (same weights, same images), rank 0 only."""
+def cpu_baseline(args, model, x_gpu, out_gpu, gt=None):
+    """The CPU oracle on a bounded sample of the same workload (same weights, same images), rank 0 only.  With the
+    ground truth the LR batch was made from (make_gt), also the PSNR-Δ of SURVEY §8(d): |PSNR(build, GT) −
+    PSNR(ref, GT)| with the reference's validation PSNR (0-255 images clamped as tensor2img does, utils/util.py:80-104,
+    168-175; SRRaGAN_model.py:627-634)."""
     from oracle import esr_oracle as O
     threads = min(os.cpu_count() or 1, 16)  # the GPU box gives one GPU a 16-CPU share
     torch.set_num_threads(threads)
@@ -118,11 +143,24 @@ def cpu_baseline(args, model, x_gpu, out_gpu):
     err = float((got - ref.double()).abs().max() / ref.double().abs().max())
     mse = float(((got - ref.double()) ** 2).mean())
     hr = 4 * args.lr_size
+    par = {'normwise_rel_err_vs_cpu_ref': err, 'psnr_vs_ref_db': (10 * np.log10(1.0 / mse)) if mse > 0 else None,
+           'images_compared': n}
+    if gt is not None:
+        from esr_amd.SRRaGAN_model import _psnr
+
+        def img(t):
+            return 255 * t.double().clamp(0, 1).numpy()
+        gts = gt[:n].cpu()
+        pb = [_psnr(img(got[i].float()), img(gts[i])) for i in range(n)]
+        pr = [_psnr(img(ref[i]), img(gts[i])) for i in range(n)]
+        par.update({'psnr_build_vs_gt_db': float(np.mean(pb)), 'psnr_ref_vs_gt_db': float(np.mean(pr)),
+                    'psnr_delta_db': abs(float(np.mean(pb)) - float(np.mean(pr))),
+                    'psnr_delta_max_per_image_db': max(abs(a - b) for a, b in zip(pb, pr)),
+                    'gt': 'seeded synthetic HR images (bench.make_gt), LR = the CEM DownscaleOP of them; '
+                          'random-init weights, so the absolute PSNRs are low and only the delta is the metric'})
     return ({'value': round(n * hr * hr / dt / 1e6, 4), 'unit': 'HR Mpixels/s', 'cores': threads, 'kind': 'port',
              'sample': '%d image(s) of 128x128 LR -> 512x512, same weights/inputs as the GPU run, PyTorch-CPU '
-                       '(oneDNN) restatement oracle/esr_oracle.py, %d threads' % (n, threads)},
-            {'normwise_rel_err_vs_cpu_ref': err, 'psnr_vs_ref_db': (10 * np.log10(1.0 / mse)) if mse > 0 else None,
-             'images_compared': n})
+                       '(oneDNN) restatement oracle/esr_oracle.py, %d threads' % (n, threads)}, par)
 
 
 def cpu_baseline_variants(args):
@@ -173,8 +211,11 @@ def reference_parity(dev):
                     ('zopt_c5_learned13', lambda d: GP.c5_z_gradients(d, kernel='learned13'))):
         try:
             r = fn(dev)
-            out[key] = {'vs': 'reference float64 run (5x its float32 error + 1e-4 floor)', 'ok': r['ok'],
+            out[key] = {'vs': 'reference float64 run (5x its float32 error + 1e-4 floor; config 3: the largest float32 '
+                              'error over the plain and the rounding-perturbed reference runs)', 'ok': r['ok'],
                         'worst_frac_of_bound': r['worst_frac_of_bound'], 'n_fails': len(r['fails'])}
+            if 'worst_frac_of_single_run_bound' in r:
+                out[key]['worst_frac_of_single_run_bound'] = r['worst_frac_of_single_run_bound']
         except Exception as e:  # noqa: BLE001
             out[key] = {'error': repr(e)}
         torch.cuda.empty_cache()
@@ -226,7 +267,7 @@ def run_legs(args, dev, world, rank):
         a = ap_.Namespace(**vars(args))
         a.precision = 'f32'
         model = build_model(a, dev)
-        x = make_input(a, dev, rank)
+        x = make_input(a, dev, rank, model)
         with torch.no_grad():
             model(x)
             dt = _timed(lambda: model(x), args.leg_steps, dev, world)
@@ -275,7 +316,7 @@ def main():
         if lib.esr_x3_set_kernel(args.x3_kernel) < 0:
             raise SystemExit('esr_x3_set_kernel(%d) rejected' % args.x3_kernel)
     model = build_model(args, dev)
-    x = make_input(args, dev, rank)
+    x = make_input(args, dev, rank, model)
     with torch.no_grad():
         # the last warmup forward runs profiled to learn the op-list length(s); their timers are then created up front,
         # outside the timed region
@@ -356,7 +397,7 @@ def main():
         rec['roofline']['traffic'] = traffic[0]
         rec['roofline']['traffic_source'] = traffic[1]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb, parity = cpu_baseline(args, model, x, out)
+        cb, parity = cpu_baseline(args, model, x, out, None if args.no_cem else make_gt(args, dev, rank))
         if not args.no_cpu_variants:
             cb['variants'] = cpu_baseline_variants(args)
         rec['cpu_baseline'] = cb

@@ -5,7 +5,10 @@ inputs come from oracle/recipe.py's NumPy recipe).
 Each check returns {'ok': bool, 'worst_frac_of_bound': float, 'fails': [...], 'lines': [...]} where a quantity's
 bound is the reference's own float32 distance to its float64 run × 5 plus a floor of 1e-4 of the quantity's scale
 (conftest.grad_parity's yardstick), evaluated through K seeded random projections where the fixture cannot hold the
-full float64 tensors."""
+full float64 tensors.  Config 3: the float32 distance is the largest over the plain reference run and its
+rounding-perturbed runs (f32p*, make_golden_train.py c3p), as in the training-loop test; the bound of the plain run
+alone is reported beside it ('worst_frac_of_single_run_bound')."""
+import contextlib
 import json
 import os
 import sys
@@ -26,15 +29,18 @@ def _proj(v, seed, idx, k):
     return np.random.default_rng([seed, idx]).standard_normal((k, g.size)) @ g
 
 
-def _result(fails, worst, lines):
-    return {'ok': not fails, 'worst_frac_of_bound': round(float(worst), 4), 'fails': fails, 'lines': lines}
+def _result(fails, worst, lines, worst_single=None):
+    r = {'ok': not fails, 'worst_frac_of_bound': round(float(worst), 4), 'fails': fails, 'lines': lines}
+    if worst_single is not None:
+        r['worst_frac_of_single_run_bound'] = round(float(worst_single), 4)
+    return r
 
 
 def c3_training_step(dev, precision='x3', d_precision=None):
     """Config 3 (B=16 × 96² LR, RRDB-23, latent, CEM train mode, WGAN-GP): two optimize_parameters micro-steps against
     the reference's own run (tests/golden/make_golden_train.py c3); the step-1 gradient of every G and D parameter,
     the logs and the D BatchNorm buffers."""
-    from test_gpu_train_loop import D_DIFFERENCES, _close, _run_port
+    from test_gpu_train_loop import D_DIFFERENCES, _close, _f32s, _run_port
     from train_recipe import grad_projections
     from esr_amd import dconv
     d = np.load(os.path.join(HERE, 'golden', 'grid_c3_train.npz'))
@@ -44,11 +50,16 @@ def c3_training_step(dev, precision='x3', d_precision=None):
         model, _, _, flags = _run_port(cfg, precision, dev, d_precision)
     finally:
         dconv.set_precision(prev)
-    fails, worst, lines = [], 0.0, []
+    fails, worst, worst1, lines = [], 0.0, 0.0, []
+    n_runs = len(_f32s(d, '%s_generator_step'))
     if not flags == list(d['f64_generator_step']) == list(d['f32_generator_step']):
         fails.append(('generator_step', flags))
+    lines.append('yardstick: %d reference float32 run(s) (the plain run + %d rounding-perturbed ones, '
+                 'make_golden_train.py c3p): bound = %g x the largest float32 distance to the float64 run + %g x |ref|; '
+                 'the single-run bound (plain float32 run only) is printed beside it' % (n_runs, n_runs - 1, FACTOR,
+                                                                                         FLOOR))
     for net, tag in ((model.netG, 'G'), (model.netD, 'D')):
-        errs, names = [], []
+        errs, errs1, names = [], [], []
         for i, (k, p) in enumerate(net.named_parameters()):
             key = '%s_gproj:%s' % (tag, k)
             if 'f64_' + key not in d.files:
@@ -61,18 +72,25 @@ def c3_training_step(dev, precision='x3', d_precision=None):
                 continue
             mine = grad_projections(p.grad.detach().double().cpu().numpy(), cfg['seed'] + (10 if tag == 'G' else 11),
                                     i, cfg['proj'])
-            p64, p32 = d['f64_' + key], d['f32_' + key]
-            err, base, norm = np.linalg.norm(mine - p64), np.linalg.norm(p32 - p64), np.linalg.norm(p64)
+            p64 = d['f64_' + key]
+            bases = [np.linalg.norm(v - p64) for v in _f32s(d, '%s_' + key)]
+            err, base, norm = np.linalg.norm(mine - p64), max(bases), np.linalg.norm(p64)
             bound = FACTOR * base + FLOOR * max(norm, 1e-30)
             errs.append(err / bound)
+            errs1.append(err / (FACTOR * bases[0] + FLOOR * max(norm, 1e-30)))
             names.append(k)
             if err > bound:
-                fails.append((tag, k, 'err %.3e bound %.3e (ref f32 %.3e, |proj| %.3e)' % (err, bound, base, norm)))
+                fails.append((tag, k, 'err %.3e bound %.3e (ref f32 %.3e over %d runs, plain %.3e, |proj| %.3e)' % (
+                    err, bound, base, len(bases), bases[0], norm)))
         order = np.argsort(errs)[::-1][:3]
-        lines.append('%s: %d parameter gradients, worst at %.1f %% of its bound, median %.1f %% (worst: %s)' % (
-            tag, len(errs), 100 * max(errs), 100 * float(np.median(errs)),
-            ', '.join('%s %.1f %%' % (names[j], 100 * errs[j]) for j in order)))
+        order1 = np.argsort(errs1)[::-1][:3]
+        lines.append('%s: %d parameter gradients, worst at %.1f %% of its bound, median %.1f %% (worst: %s); single-run '
+                     'bound: worst %.1f %% (%s)' % (
+                         tag, len(errs), 100 * max(errs), 100 * float(np.median(errs)),
+                         ', '.join('%s %.1f %%' % (names[j], 100 * errs[j]) for j in order), 100 * max(errs1),
+                         ', '.join('%s %.1f %%' % (names[j], 100 * errs1[j]) for j in order1)))
         worst = max(worst, max(errs))
+        worst1 = max(worst1, max(errs1))
     for f in [f for f in d.files if f.startswith('f64_log:')]:
         key = f[len('f64_log:'):]
         mine = np.array(model.log_dict[key], dtype=np.float64)
@@ -83,18 +101,63 @@ def c3_training_step(dev, precision='x3', d_precision=None):
         scale = None
         if key in D_DIFFERENCES:
             scale = 2 * (np.linalg.norm(d['f64_log:D_real'][:, 1]) + np.linalg.norm(d['f64_log:D_fake'][:, 1]))
-        ok, msg, r = _close(mine[:, 1], ref32[:, 1], ref64[:, 1], scale)
+        ok, msg, r = _close(mine[:, 1], [v[:, 1] for v in _f32s(d, '%s_log:' + key)], ref64[:, 1], scale)
         lines.append('log %-24s %s' % (key, msg))
         worst = max(worst, r)
+        worst1 = max(worst1, _close(mine[:, 1], ref32[:, 1], ref64[:, 1], scale)[2])
         if not ok:
             fails.append(('log', key, msg))
     for k, v in model.netD.state_dict().items():
         if 'running' in k:
-            ok, msg, r = _close(v.double().cpu().numpy(), d['f32_Dbuf:' + k], d['f64_Dbuf:' + k])
+            mine = v.double().cpu().numpy()
+            ok, msg, r = _close(mine, _f32s(d, '%s_Dbuf:' + k), d['f64_Dbuf:' + k])
             worst = max(worst, r)
+            worst1 = max(worst1, _close(mine, d['f32_Dbuf:' + k], d['f64_Dbuf:' + k])[2])
             if not ok:
                 fails.append(('D buffer', k, msg))
-    return _result(fails, worst, lines)
+    return _result(fails, worst, lines, worst1)
+
+
+FOLDS = ('product', 'rowmajor', 'f64')
+
+
+@contextlib.contextmanager
+def upsampler_fold(name):
+    """Runs the upsampler phases' folded weights (engine.fold_upconv_phase: nearest-×2 + 3×3 conv as four 2×2 convs,
+    each phase tap a sum of 1, 2 or 4 of the 3×3 taps) summed in another legal order, exact-fp32 path only:
+    'product' = the shipped x-major order (engine.fold_terms), 'rowmajor' = y-major sequential, 'f64' = the exactly
+    rounded sum (profiles/r4_c3_fold_order.txt).  The order changes the folded weights by an ulp, which is the kind of
+    change the config-3 yardstick has to tolerate."""
+    from esr_amd import engine as E
+    if name == 'product':
+        yield
+        return
+
+    def fold(w, py, px, f):
+        t = E.fold_term_images(w.detach().double() if name == 'f64' else w.detach(), py, px, f)
+        if name == 'f64':
+            return (((t[0] + t[1]) + t[2]) + t[3]).float()
+        terms = E.fold_terms(py, px, f)
+        out = torch.zeros_like(t[0])
+        for a in range(2):
+            for b in range(2):
+                for (y, x) in sorted(terms[a][b]):  # row-major: y, then x
+                    out[:, :, a, b] += w.detach()[:, :, y, x]
+        return out
+    refresh = E._Packed.refresh
+
+    def fold_refresh(self):
+        refresh(self)
+        with torch.no_grad():
+            for row, (j, f) in zip(self.up, E.up_stages(self.net)):
+                w = self.net.model[j][1].weight
+                for cw, (py, px) in zip(row, [(a, b) for a in range(f) for b in range(f)]):
+                    cw.f32.copy_(E.pack_conv_weight(fold(w, py, px, f), list(range(64)), 64))
+    E._Packed.refresh = fold_refresh
+    try:
+        yield
+    finally:
+        E._Packed.refresh = refresh
 
 
 C5_FIXTURES = {'learned13': 'grid_c5_zgrad.npz', 'kgan': 'grid_c5_zgrad_kgan.npz'}
