@@ -1335,6 +1335,7 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
     const int tiles12 = ((W + 11) / 12) * ((B * (H + 2) - 2 + 31) / 32);
     const bool x3c_pays = taps_side == 2 || (taps_side == 3 && (cout > 32 || !row8_pays || tiles12 >= n_cu));
     if ((g_x3_kernel >= 50 && g_x3_kernel <= 62) || g_x3_kernel == 64 || g_x3_kernel == 65 ||
+        (g_x3_kernel >= 70 && g_x3_kernel <= 79) ||
         ((g_x3_kernel == 1 || g_x3_kernel == 63) && x3c_pays)) {
         X3cParams c;
         c.in = p.in; c.B = B; c.H = H; c.W = W; c.in_cp = in_cp; c.cin = cin; c.w = p.w; c.bias = bias;
@@ -1347,6 +1348,15 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
         // 154², 1.05–1.24× at smaller grids; 16-column tiles at 172² (one round vs two: 1.18× the split) and 148²
         // (a tie); profiles/r4_x3_n64_tiles.txt.  Round 3's N split (two N = 32 launches) lost to one of the two at
         // every measured grid and is the ablation library's option (esr_x3_set_nsplit)
+#ifdef ESR_X3_EXPERIMENTS  // 70-74: the persistent double-buffered N = 32 kernel (esr_conv_x3p.hip) and its ablations
+        if (g_x3_kernel >= 70 && g_x3_kernel <= 79) {  // 75-79: two-column waves (64 x 8 tiles)
+            static const int dbgp[5] = {0, 1, 2, 4, 5};
+            const int v = g_x3_kernel - 70;
+            if (taps_side == 3 && cout <= 32 && !o->out_planar)
+                return x3p_launch(c, stream, dbgp[v % 5] | (v >= 5 ? 16 : 0));
+            return x3c_launch(c, taps_side, stream, cout > 32 ? 0 : 128);
+        }
+#endif
         const int rows32 = (B * (H + 2) - 2 + 31) / 32;
         const int tiles16 = ((W + 15) / 16) * rows32;
         if (taps_side == 3 && cout > 32 && (g_x3_kernel == 1 || g_x3_kernel == 63) && !o->out_planar) {

@@ -31,6 +31,8 @@ struct X3cParams {
 int x3c_launch(const X3cParams &p, int taps_side, hipStream_t stream, int dbg = 0);
 // warp-specialised persistent form (one workgroup per CU: 8 compute + 4 LDS-DMA loader waves, register epilogue)
 int x3s_launch(const X3cParams &p, int taps_side, hipStream_t stream, int dbg = 0);
+// N = 32 3×3 conv on the persistent double-buffered kernel (esr_conv_x3p.hip; cout <= 32, not planar)
+int x3p_launch(const X3cParams &p, hipStream_t stream, int dbg = 0);
 // HR_conv0 with HR_conv1's partial products as its only output (p.w1, p.y1, p.zc1; N = 64, 3×3, one launch)
 int x3c_launch_hr1(const X3cParams &p, hipStream_t stream);
 // out NCHW [B][3][H][W] = sinv · Σ_t y[b][y + ty][x + tx][3t + o] + bias[o] (y: padded [B][H+2][W+2][32], zero halo)
