@@ -268,7 +268,11 @@ __global__ __launch_bounds__(64 * (TW / CWV), (TW / CWV) * OCC / 4) void conv_x3
                 if constexpr (WR) return;
                 sfor<0, TS>([&](auto Xc) {
                     constexpr int dx = decltype(Xc)::value, t = d * TS + dx;
-                    if constexpr (RB) {  // global (L1/L2) loads; the compiler waits for them before first use
+                    if constexpr ((DBG & 16) != 0) {
+                        bh[d & 1][dx] = f16x8{};
+                        bl[d & 1][dx] = f16x8{};
+                        asm volatile("" : "+v"(bh[d & 1][dx]), "+v"(bl[d & 1][dx]));
+                    } else if constexpr (RB) {  // global (L1/L2) loads; the compiler waits for them before first use
                         bh[d & 1][dx] = wj[(t * N + nt * 32) * (REC / 16)];
                         bl[d & 1][dx] = wj[(t * N + nt * 32) * (REC / 16) + 1];
                     } else {
@@ -279,6 +283,11 @@ __global__ __launch_bounds__(64 * (TW / CWV), (TW / CWV) * OCC / 4) void conv_x3
             };
             auto lda = [&](auto Sc) {
                 constexpr int s = decltype(Sc)::value, d = s / NIC, ic = s % NIC, buf = s % 3;
+                if constexpr ((DBG & 16) != 0) {  // diagnostic: no fragment reads (operands from the registers)
+                    ah[buf] = bh[0][0];
+                    al[buf] = bl[0][0];
+                    return;
+                }
                 ah[buf] = ds_read16<ic * HYC * REC>(a_hi[d]);
                 al[buf] = ds_read16<ic * HYC * REC>(a_lo[d]);
             };
@@ -303,7 +312,7 @@ __global__ __launch_bounds__(64 * (TW / CWV), (TW / CWV) * OCC / 4) void conv_x3
                     constexpr int pr = decltype(Pc)::value;
                     sfor<0, TS>([&](auto Xc) {
                         constexpr int dx = decltype(Xc)::value, c = ic - dx;
-                        if constexpr (c >= 0 && c < CWk) {
+                        if constexpr (c >= 0 && c < CWk && !(DBG & 8)) {  // DBG 8: the reads without the MFMAs
                             const f16x8 &a = pr == 0 ? al[buf] : ah[buf];
                             const f16x8 &b = WR ? (pr == 1 ? bregl[WR ? d * TS + dx : 0] : bregh[WR ? d * TS + dx : 0])
                                                 : (pr == 1 ? bl[d & 1][dx] : bh[d & 1][dx]);
@@ -891,6 +900,22 @@ int x3c_launch(const X3cParams &p0, int taps_side, hipStream_t stream, int dbg) 
         if (n64) return x3c_launch(p0, taps_side, stream, 0);
         if (taps_side == 3) hipLaunchKernelGGL((conv_x3c_kernel<1, 3, 0, false, 4, true>), grid, block, 0, stream, p);
         else hipLaunchKernelGGL((conv_x3c_kernel<1, 2, 0, false, 4, true>), grid, block, 0, stream, p);
+        return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+    }
+#endif
+#ifdef ESR_X3_EXPERIMENTS
+    if (dbg >= 256 && !n64 && taps_side == 3) {  // 12-column N = 32 kernel ablations: DBG = dbg >> 8
+        p.tiles_x = (p.W + 11) / 12;
+        const dim3 grid12((unsigned)(p.tiles_x * p.tiles_y));
+#define X12(D) hipLaunchKernelGGL((conv_x3c_kernel<1, 3, D, false, 3, false, 12, 3>), grid12, block, 0, stream, p)
+        switch (dbg >> 8) {
+        case 5: X12(5); break;
+        case 13: X12(13); break;
+        case 21: X12(21); break;
+        case 29: X12(29); break;
+        default: X12(0);
+        }
+#undef X12
         return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
     }
 #endif
