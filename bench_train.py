@@ -103,12 +103,12 @@ def run(args, dev, world, rank):
     """Build the model, run args.warmup + args.steps optimize_parameters() calls (timed: the steps, bracketed by
     barrier + synchronize, max over ranks), return the JSON record."""
     from esr_amd import engine
-    from esr_amd.SRRaGAN_model import SRRaGANModel
+    from esr_amd.SRRaGAN_model import SRRaGANModel, collective
     torch.manual_seed(1000 + rank)
     model = SRRaGANModel(make_opt(args), device=dev)
     if world > 1:  # identical initial weights on every rank (DataParallel replicates rank 0's)
         for p in list(model.netG.parameters()) + list(model.netD.parameters()):
-            dist.broadcast(p.data, 0)
+            collective(dist.broadcast, p.data, 0)
     g = torch.Generator(device='cpu').manual_seed(7 + rank)
     hr = 4 * args.lr_size
     data = {'LR': torch.rand(args.batch, 3, args.lr_size, args.lr_size, generator=g).to(dev),

@@ -66,6 +66,30 @@ def _world():
     return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
 
+def _host_collectives():
+    """True when the process group is gloo (the CPU test path of the multi-rank code, and ranks sharing one GPU):
+    it moves device tensors through host copies that are not ordered on the device stream the way RCCL's
+    collectives are (tests/test_gpu_ddp.py saw noise-level gradient differences against the single-process run)."""
+    return _world() > 1 and dist.get_backend() == 'gloo'
+
+
+class _Done:
+    def wait(self):
+        return True
+
+
+def collective(fn, t, *args, async_op=False, **kw):
+    """dist.<fn>(t, ...) in place on the backend's terms: RCCL takes device tensors stream-ordered (asynchronous when
+    async_op); with gloo a device tensor goes through an explicit host copy (synchronous: the copy out waits for the
+    stream, the copy back is enqueued on it)."""
+    if t.is_cuda and _host_collectives():
+        c = t.detach().cpu()
+        fn(c, *args, **kw)
+        t.copy_(c)
+        return _Done() if async_op else None
+    return fn(t, *args, async_op=async_op, **kw)
+
+
 def _allreduce_grads(params):
     """Average the .grad of `params` over ranks in one flat bucket (RCCL all-reduce over xGMI)."""
     if _world() == 1:
@@ -74,7 +98,7 @@ def _allreduce_grads(params):
     if not grads:
         return
     flat = torch.cat([g.reshape(-1) for g in grads])
-    dist.all_reduce(flat)
+    collective(dist.all_reduce, flat)
     flat /= _world()
     o = 0
     for g in grads:
@@ -147,7 +171,7 @@ class GradBuckets:
             self._works[b] = ()
             return
         flat = torch.cat([g.reshape(-1) for g in grads])
-        self._works[b] = (dist.all_reduce(flat, async_op=True), flat, grads)
+        self._works[b] = (collective(dist.all_reduce, flat, async_op=True), flat, grads)
         self.n_allreduce += 1
         self.allreduce_bytes += flat.numel() * flat.element_size()
 
@@ -197,7 +221,7 @@ def _broadcast_buffers(module):
     if _world() == 1:
         return
     for b in module.buffers():
-        dist.broadcast(b, 0)
+        collective(dist.broadcast, b, 0)
 
 
 LATENT_WEIGHTS_RELATIVE_STD = 0.  # base_model.py:116
@@ -382,7 +406,7 @@ class SRRaGANModel:
         s = torch.stack([diff.sum(), (diff > 0).float().sum(), diff.new_full((), float(diff.numel())),
                          pred_real.detach().mean(), pred_fake.detach().mean()])
         if _world() > 1:
-            dist.all_reduce(s)
+            collective(dist.all_reduce, s)
             s[3:] /= _world()
         return torch.stack([s[0] / s[2], s[1] / s[2], s[3], s[4]])
 

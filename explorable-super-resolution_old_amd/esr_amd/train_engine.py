@@ -89,7 +89,8 @@ class DeferredOverflow:
                         [b.reshape(()).float() for b, _ in self.resets])
         import torch.distributed as dist
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)  # every rank redoes the step together
+            from .SRRaGAN_model import collective
+            collective(dist.all_reduce, t, op=dist.ReduceOp.MAX)  # every rank redoes the step together
         vals = t.tolist()
         n = len(self.flags)
         for (_, reset), bad in zip(self.resets, vals[n:]):
