@@ -37,7 +37,7 @@ def ranks(gpus, script, argv, check_devices=True):
         raise SystemExit('--gpus must be >= 1')
     if n == 1:
         return 1
-    if check_devices:
+    if check_devices and not share_gpu():
         import torch  # device_count() does not initialise the GPU on this stack
         have = torch.cuda.device_count()
         if have < n:
@@ -48,12 +48,23 @@ def ranks(gpus, script, argv, check_devices=True):
     sys.exit(rc)
 
 
+def share_gpu():
+    """ESR_SHARE_GPU=1 (rehearsal only): every rank on GPU 0, gloo instead of RCCL (RCCL needs one GPU per rank) — runs
+    the N-rank path of a bench on a one-GPU box; its times are not a scaling measurement."""
+    return os.environ.get('ESR_SHARE_GPU') == '1'
+
+
+def local_device_index():
+    return 0 if share_gpu() else int(os.environ.get('LOCAL_RANK', '0'))
+
+
 def init(dev, world):
-    """Join the process group (RCCL on the GPU; gloo for the CPU launcher check) and confirm its size."""
+    """Join the process group (RCCL on the GPU; gloo for the CPU launcher check and ESR_SHARE_GPU) and confirm its
+    size."""
     import torch.distributed as dist
     if world == 1:
         return 1
-    if dev.type == 'cuda':
+    if dev.type == 'cuda' and not share_gpu():
         dist.init_process_group('nccl', device_id=dev)
     else:
         dist.init_process_group('gloo')

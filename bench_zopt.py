@@ -152,6 +152,7 @@ def main():
     if args.launcher_check:
         bench_launch.launcher_check(world, rank)
         return
+    local = bench_launch.local_device_index()
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
     world = bench_launch.init(dev, world)
