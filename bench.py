@@ -222,19 +222,23 @@ def reference_parity(dev):
     return out
 
 
-def pmc_traffic(kernel_tag):
-    """HBM bytes per launch of `kernel_tag` from the committed rocprofv3 PMC passes (profiles/pmc_latest.json, made
-    by tools/prof_summary.py from separate --pmc FETCH_SIZE / WRITE_SIZE runs of this same default bench command,
-    FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM).  PMC counters cannot be read live from inside the process."""
+def pmc_traffic(tags):
+    """HBM bytes per launch, launch-weighted over the kernel tags `tags`, from the committed rocprofv3 PMC passes
+    (profiles/pmc_latest.json, made by tools/prof_summary.py from separate --pmc FETCH_SIZE / WRITE_SIZE runs of this
+    same default bench command, FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM), and the per-launch union time of
+    the x3 family in that run's kernel trace.  PMC counters cannot be read live from inside the process."""
     path = os.path.join(REPO, 'profiles', 'pmc_latest.json')
     if not os.path.exists(path):
         return None
     d = json.load(open(path))
+    n = byt = 0.0
     for r in d['kernels']:
-        if r['kernel'] == kernel_tag and r['hbm_read_bytes_per_launch'] is not None:
-            return (r['hbm_read_bytes_per_launch'] + (r['hbm_write_bytes_per_launch'] or 0.0),
-                    '%s (%s)' % (os.path.relpath(path, REPO), d['source']))
-    return None
+        if r['kernel'] in tags and r['hbm_read_bytes_per_launch'] is not None:
+            n += r['calls']
+            byt += r['calls'] * (r['hbm_read_bytes_per_launch'] + (r['hbm_write_bytes_per_launch'] or 0.0))
+    if not n:
+        return None
+    return byt / n, '%s (%s)' % (os.path.relpath(path, REPO), d['source']), d.get('x3_family_union_us_per_launch')
 
 
 def _timed(fn, steps, dev, world):
@@ -336,6 +340,8 @@ def main():
         torch.cuda.synchronize()
         prof = []
         engine._PROFILE = None if args.no_op_timers else prof
+        origin = engine.ProfileOrigin(dev)
+        origin.record()
         t0 = time.perf_counter()
         for _ in range(args.steps):
             out = model(x)
@@ -352,6 +358,7 @@ def main():
     total_px = world * args.batch * hr * hr * args.steps
     value = total_px / dt / 1e6
     if args.no_op_timers:
+        origin.close()
         if rank == 0:
             print(json.dumps({'metric': METRIC, 'value': round(value, 3), 'unit': 'HR Mpixels/s', 'n_gpus': world,
                               'steps': args.steps, 'ms_per_step': round(dt / args.steps * 1e3, 3),
@@ -359,23 +366,30 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
-    # roofline of the dominant kernel from the per-launch events
+    # roofline from the per-launch events.  With the batch split over engine.STREAMS HIP streams, launches run
+    # concurrently and no single launch's duration is its own: the roofline is that of the x3 MFMA conv family (every
+    # profiled launch of the step: the conv_x3c 3x3 convs, the sub-pixel upconvs, the fused HR convs) — their FLOPs
+    # over the UNION of their HIP-event intervals, i.e. the MFMA rate the GPU sustained while any of them ran; the
+    # per-tag lines beside it give each tag's FLOPs over the union of its own intervals and its mean event duration.
     per = {}
-    for tag, flops, ms in engine.profile_records(prof):
-        a = per.setdefault(tag, [0, 0.0, 0.0])
+    for tag, flops, t_a, t_b in engine.profile_intervals(prof, origin):
+        a = per.setdefault(tag, [0, 0.0, 0.0, []])
         a[0] += 1
         a[1] += flops
-        a[2] += ms
+        a[2] += t_b - t_a
+        a[3].append((t_a, t_b))
+    origin.close()
+    union = {k: engine.union_ms(v[3]) for k, v in per.items()}
+    busy = engine.union_ms([iv for v in per.values() for iv in v[3]])
+    n_all, fl_all = sum(v[0] for v in per.values()), sum(v[1] for v in per.values())
+    achieved = fl_all / (busy / 1e3) / 1e12
     dom = max(per, key=lambda k: per[k][2])
-    n_l, fl, ms = per[dom]
-    achieved = (fl / n_l) / (ms / n_l / 1e3) / 1e12
     peak, peak_note = PEAKS[args.precision]
     kernels = {k: {'launches_per_step': v[0] // args.steps, 'avg_us': round(v[2] / v[0] * 1e3, 2),
-                   'tflops': round(v[1] / (v[2] / 1e3) / 1e12, 2), 'share_of_gpu_time': None}
+                   'tflops_over_own_union': round(v[1] / (union[k] / 1e3) / 1e12, 2),
+                   'share_of_step': round(union[k] / (dt * 1e3), 3)}
                for k, v in per.items()}
-    tot = sum(v[2] for v in per.values())
-    for k in kernels:
-        kernels[k]['share_of_gpu_time'] = round(per[k][2] / (dt * 1e3), 3)
+    streams = engine.STREAMS if (engine.USE_OP_LISTS and args.batch >= engine.STREAM_MIN_B) else 1
     rec = {
         'metric': METRIC, 'value': round(value, 3), 'unit': 'HR Mpixels/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': round(dt / args.steps * 1e3, 3), 'higher_is_better': True,
@@ -385,18 +399,26 @@ def main():
                                   args.lr_size, args.lr_size, hr, hr),
                    'global_batch': world * args.batch, 'nb': args.nb, 'parallelism': 'dp%d (image sharding, no '
                    'data-path collective)' % world},
-        'roofline': {'bound': 'mfma', 'kernel': dom, 'achieved': round(achieved, 2), 'peak': round(peak, 1),
-                     'peak_basis': peak_note, 'unit': 'TFLOP/s', 'frac': round(achieved / peak, 4), 'traffic': None,
-                     'flops_per_launch': fl / n_l, 'avg_launch_us': round(ms / n_l * 1e3, 2)},
+        'roofline': {'bound': 'mfma', 'kernel': 'x3 MFMA conv family (%s), all launches of the step' % ', '.join(sorted(per)),
+                     'achieved': round(achieved, 2), 'peak': round(peak, 1), 'peak_basis': peak_note,
+                     'unit': 'TFLOP/s', 'frac': round(achieved / peak, 4), 'traffic': None,
+                     'flops_per_launch': fl_all / n_all, 'launches_per_step': n_all // args.steps,
+                     'union_us_per_launch': round(busy / n_all * 1e3, 2), 'streams': streams,
+                     'timing': 'achieved = FLOPs of all launches / union of their HIP-event intervals over the timed '
+                               'region (%d stream(s); union / launches is the effective launch time the rocprof '
+                               'kernel-trace union is checked against)' % streams,
+                     'dominant_tag': {'tag': dom, 'flops_per_launch': per[dom][1] / per[dom][0],
+                                      'avg_launch_us': round(per[dom][2] / per[dom][0] * 1e3, 2)}},
         'kernels': kernels,
-        'gpu_busy_frac': round(tot / (dt * 1e3), 3),
+        'gpu_busy_frac': round(busy / (dt * 1e3), 3),
         'dist': {'world_size': dist.get_world_size() if world > 1 else 1,
                  'backend': dist.get_backend() if world > 1 else None},
     }
-    traffic = pmc_traffic(dom)
+    traffic = pmc_traffic(set(per))
     if traffic is not None:
         rec['roofline']['traffic'] = traffic[0]
         rec['roofline']['traffic_source'] = traffic[1]
+        rec['roofline']['rocprof_union_us_per_launch'] = traffic[2]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb, parity = cpu_baseline(args, model, x, out, None if args.no_cem else make_gt(args, dev, rank))
         if not args.no_cpu_variants:

@@ -273,4 +273,4 @@ extern "C" int esr_upconv2x_phase_fwd(const float *in, int32_t B, int32_t H, int
     return launch_conv(in, B, H, W, in_cp, cin, w_packed, bias, cout, 2, py, px, o, (hipStream_t)stream);
 }
 
-extern "C" int esr_abi_version(void) { return 22; }
+extern "C" int esr_abi_version(void) { return 23; }

@@ -87,6 +87,21 @@ extern "C" int esr_timer_elapsed(esr_timer_t timer, float *ms) {
     return ESR_OK;
 }
 
+extern "C" int esr_timer_record(esr_timer_t timer, int32_t k, esr_stream_t stream) {
+    Timer *t = static_cast<Timer *>(timer);
+    if (!t || k < 0 || k > t->n) return ESR_EINVAL;
+    return hipEventRecord(t->ev[k], (hipStream_t)stream) == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+}
+
+extern "C" int esr_timer_stamps(esr_timer_t timer, esr_timer_t ref, float *t_ms) {
+    Timer *t = static_cast<Timer *>(timer), *r = static_cast<Timer *>(ref);
+    if (!t || !r || !t_ms) return ESR_EINVAL;
+    if (hipEventSynchronize(t->ev[t->n]) != hipSuccess) return ESR_ELAUNCH;
+    for (int k = 0; k <= t->n; ++k)
+        if (hipEventElapsedTime(&t_ms[k], r->ev[0], t->ev[k]) != hipSuccess) return ESR_ELAUNCH;
+    return ESR_OK;
+}
+
 extern "C" void esr_timer_destroy(esr_timer_t timer) {
     Timer *t = static_cast<Timer *>(timer);
     if (!t) return;

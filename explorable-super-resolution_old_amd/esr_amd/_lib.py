@@ -8,7 +8,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('ESR_AMD_LIB', os.path.join(_HERE, 'libesr_amd.so'))
-ABI_VERSION = 22
+ABI_VERSION = 23
 
 c_int = ctypes.c_int32
 c_float = ctypes.c_float
@@ -122,6 +122,8 @@ _SIGNATURES = {
     'esr_timer_create': [c_int],
     'esr_timer_elapsed': [c_void_p, c_fp],
     'esr_timer_destroy': [c_void_p],
+    'esr_timer_record': [c_void_p, c_int, c_void_p],
+    'esr_timer_stamps': [c_void_p, c_void_p, c_fp],
     'esr_run_ops': [ctypes.POINTER(EsrOp), c_int, c_void_p, c_void_p],
     'esr_op_size': [],
     'esr_abi_version': [],

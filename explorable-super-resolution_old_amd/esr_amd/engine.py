@@ -526,15 +526,21 @@ class _Workspace:
         self.Y = None  # x3 inference: HR_conv1's per-tap partial products (esr_hr_convs_x3), allocated on first use
 
 
+# workspace slot of the inference forward being built: each batch part of a multi-stream forward (generator_forward)
+# has buffers of its own
+_WS_SLOT = [0]
+
+
 def _workspace(net, dev, B, H, W, latent, precision):
     # keyed by precision too: the zero padding channels of an fp32 workspace are not zero when read as split-f16 pairs
     sf = getattr(net, 'upscale', SF)
     key = (str(dev), B, H, W, latent, precision, sf)
-    c = net._esr_cache.get('ws')
+    name = 'ws' if _WS_SLOT[0] == 0 else 'ws%d' % _WS_SLOT[0]
+    c = net._esr_cache.get(name)
     if c is None or c[0] != key:
-        net._esr_cache.pop('ws', None)  # free the previous shape's buffers first
+        net._esr_cache.pop(name, None)  # free the previous shape's buffers first
         c = (key, _Workspace(dev, B, H, W, latent, sf))
-        net._esr_cache['ws'] = c
+        net._esr_cache[name] = c
     return c[1]
 
 
@@ -634,9 +640,12 @@ class _OpPlan:
         if not self.x_sites or not self.out_sites:
             raise RuntimeError('esr_amd: op-list recording did not find the input/output of the forward')
 
-    def run(self, x):
+    def run(self, x, out=None):
         lib = _lib.load()
-        out = torch.empty(self.out_shape, device=x.device, dtype=torch.float32)
+        if out is None:
+            out = torch.empty(self.out_shape, device=x.device, dtype=torch.float32)
+        elif tuple(out.shape) != self.out_shape or not out.is_contiguous():
+            raise RuntimeError('esr_amd: op-list output view of the wrong shape')
         for k, j in self.x_sites:
             self.ops[k].p[j] = x.data_ptr()
         for k, j in self.out_sites:
@@ -674,6 +683,62 @@ def profile_records(prof):
             yield tag, flops, start.elapsed_time(end)
 
 
+class ProfileOrigin:
+    """A time origin for profile_intervals: one native HIP event and one torch event, recorded back to back on the
+    current stream at the start of a timed region."""
+
+    def __init__(self, dev):
+        lib = _lib.load()
+        self.timer = lib.esr_timer_create(1)
+        if not self.timer:
+            raise RuntimeError('esr_amd: esr_timer_create failed')
+        self.event = torch.cuda.Event(enable_timing=True)
+        self.dev = dev
+
+    def record(self):
+        stream = torch.cuda.current_stream(self.dev)
+        _lib.check(_lib.load().esr_timer_record(self.timer, 0, ctypes.c_void_p(stream.cuda_stream)),
+                   'esr_timer_record')
+        self.event.record(stream)
+
+    def close(self):
+        if self.timer:
+            _lib.load().esr_timer_destroy(self.timer)
+            self.timer = None
+
+
+def profile_intervals(prof, origin):
+    """(tag, flops, start_ms, end_ms) of every profiled launch in `prof`, times from `origin` (a recorded
+    ProfileOrigin): launches of several streams overlap, so a rate over them divides by the union of their intervals,
+    not by the sum of their durations.  Frees the op-list timers like profile_records."""
+    lib = _lib.load()
+    for entry in prof:
+        if entry[0] == 'ops':
+            _, tags, timer, n = entry
+            t = (ctypes.c_float * (n + 1))()
+            _lib.check(lib.esr_timer_stamps(timer, origin.timer, t), 'esr_timer_stamps')
+            lib.esr_timer_destroy(timer)
+            for k in range(n):
+                if tags[k] is not None:
+                    yield tags[k][0], tags[k][1], t[k], t[k + 1]
+        else:
+            tag, flops, start, end = entry
+            yield tag, flops, origin.event.elapsed_time(start), origin.event.elapsed_time(end)
+
+
+def union_ms(intervals):
+    """Length of the union of (start, end) intervals."""
+    tot, hi = 0.0, None
+    for a, b in sorted(intervals):
+        if hi is None or a > hi:
+            tot += b - a
+            hi = b
+        elif b > hi:
+            tot += b - hi
+            hi = b
+    return tot
+
+
 USE_OP_LISTS = os.environ.get('ESR_OP_LISTS', '1') != '0'
 # x3 inference: HR_conv0 and HR_conv1 as esr_hr_convs_x3 + esr_hr1_sum (ESR_FUSE_HR1=0: the two convs as launched for
 # training, HR_conv1 on the narrow-N kernel)
@@ -691,18 +756,66 @@ def _plan_key(net, x, cem, precision, pk):
     return (id(pk), getattr(pk, 'version', 0), precision, tuple(x.shape), str(x.device), cem_key, a, FUSE_HR1)
 
 
-def _planned_forward(net, x, cem, precision):
+def _plan(net, x, cem, precision, slot=0):
     pk = _packed(net, net.latent_input is not None)
     key = _plan_key(net, x, cem, precision, pk)
     if precision == 'x3':
         pk.act_bias(act_scale(net))  # (no-op unless the parameters or the scale changed)
     plans = net._esr_cache.setdefault('plans', {})
-    plan = plans.get(precision)
+    plan = plans.get((precision, slot))
     if plan is None or plan.key != key:
-        plans.pop(precision, None)
-        plan = _OpPlan(key, net, x, cem, precision)
-        plans[precision] = plan
+        plans.pop((precision, slot), None)
+        _WS_SLOT[0] = slot
+        try:
+            plan = _OpPlan(key, net, x, cem, precision)
+        finally:
+            _WS_SLOT[0] = 0
+        plans[(precision, slot)] = plan
+    return plan
+
+
+def _planned_forward(net, x, cem, precision):
+    plan = _plan(net, x, cem, precision)
     return plan.run(x), plan.ws
+
+
+# Inference batches of at least STREAM_MIN_B images run as STREAMS parts on as many HIP streams at once (each part
+# with its own workspace and op list): one part's kernels fill the GPU where another's are in their last, partly empty
+# round of workgroups or between launches.  ESR_STREAMS=1: one stream (A/B).
+STREAMS = int(os.environ.get('ESR_STREAMS', '2'))
+STREAM_MIN_B = 8
+_SIDE_STREAMS = {}
+
+
+def _side_stream(dev, k):
+    key = (str(dev), k)
+    if key not in _SIDE_STREAMS:
+        _SIDE_STREAMS[key] = torch.cuda.Stream(dev)
+    return _SIDE_STREAMS[key]
+
+
+def _multistream_forward(net, x, cem, precision, n):
+    """The batch in n parts, part k on stream k (part 0 on the current stream), results in one output tensor."""
+    B = x.shape[0]
+    bounds = [B * k // n for k in range(n + 1)]
+    parts = [x[bounds[k]:bounds[k + 1]] for k in range(n)]
+    plans = [_plan(net, parts[k], cem, precision, slot=k) for k in range(n)]  # (built once per shape)
+    out = torch.empty((B,) + plans[0].out_shape[1:], device=x.device, dtype=torch.float32)
+    cur = torch.cuda.current_stream(x.device)
+    for k in list(range(1, n)) + [0]:  # the side streams first: each waits for the current stream's work so far only
+        ok = out[bounds[k]:bounds[k + 1]]
+        if k == 0:
+            plans[0].run(parts[0], ok)
+            continue
+        st = _side_stream(x.device, k)
+        st.wait_stream(cur)  # x is ready and out allocated on the current stream
+        with torch.cuda.stream(st):
+            plans[k].run(parts[k], ok)
+        x.record_stream(st)
+        out.record_stream(st)
+    for k in range(1, n):
+        cur.wait_stream(_side_stream(x.device, k))
+    return out, [p.ws for p in plans]
 
 
 # ----------------------------------------------------------------------------------------------------------------------
@@ -720,14 +833,20 @@ def generator_forward(net, x, cem=None):
     if precision not in PRECISIONS:
         raise ValueError('esr_precision must be one of %s' % (PRECISIONS,))
     x = x.contiguous()
-    if USE_OP_LISTS:
+    if USE_OP_LISTS and STREAMS > 1 and x.shape[0] >= STREAM_MIN_B:
+        out, wss = _multistream_forward(net, x, cem, precision, STREAMS)
+    elif USE_OP_LISTS:
         out, ws = _planned_forward(net, x, cem, precision)
+        wss = [ws]
     else:
         out, ws = _forward(net, x, cem, precision)
+        wss = [ws]
     if precision == 'x3':
-        if int(ws.overflow.item()):  # one 4-byte D2H per forward
+        flags = wss[0].overflow if len(wss) == 1 else torch.stack([w.overflow for w in wss]).amax()
+        if int(flags.item()):  # one 4-byte D2H per forward
             OVERFLOW_RERUNS += 1
-            ws.overflow.zero_()
+            for w in wss:
+                w.overflow.zero_()
             lower_act_scale(net)  # an activation (× the activation scale) left f16's range: smaller scale next time
             out, _ = _forward(net, x, cem, 'f32')
     return out

@@ -427,6 +427,11 @@ typedef void *esr_timer_t;
 esr_timer_t esr_timer_create(int32_t n_ops);            /* n_ops + 1 HIP events; NULL on failure */
 int esr_timer_elapsed(esr_timer_t timer, float *ms);    /* waits; ms[k] = duration of op k of the last run */
 void esr_timer_destroy(esr_timer_t timer);
+/* Event k (0..n_ops) of `timer` recorded on `stream` now (a reference mark: a timer of one op, event 0). */
+int esr_timer_record(esr_timer_t timer, int32_t k, esr_stream_t stream);
+/* Waits; t_ms[k] (k = 0..n_ops) = time of event k of the last run relative to event 0 of `ref`: the absolute launch
+ * intervals [t_ms[k], t_ms[k+1]] of op lists run on several streams at once (bench.py's roofline over their union). */
+int esr_timer_stamps(esr_timer_t timer, esr_timer_t ref, float *t_ms);
 int esr_run_ops(const esr_op *ops, int32_t n, esr_timer_t timer, esr_stream_t stream);
 int esr_op_size(void);                                  /* sizeof(esr_op), checked by the binding */
 

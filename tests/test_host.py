@@ -316,3 +316,12 @@ def test_retired_switch_on_product_library_warns(monkeypatch):
         warnings.simplefilter('always')
         _lib.bind(_lib.LIB_PATH)
     assert any('ESR_DCONV_HALO' in str(x.message) for x in w)
+
+
+def test_union_of_launch_intervals():
+    """bench.py's roofline divides a tag's FLOPs by the union of its launch intervals (two streams overlap)."""
+    from esr_amd import engine
+    assert engine.union_ms([]) == 0.0
+    assert engine.union_ms([(0.0, 1.0), (2.0, 3.0)]) == 2.0
+    assert engine.union_ms([(0.0, 2.0), (1.0, 3.0), (2.5, 2.7)]) == 3.0
+    assert engine.union_ms([(1.0, 4.0), (0.0, 1.0), (5.0, 6.0), (3.0, 5.5)]) == 6.0

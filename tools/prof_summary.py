@@ -50,6 +50,24 @@ def load_trace(path):
     return agg
 
 
+def x3_family_union(path):
+    """(launches, union µs) of the x3 MFMA conv family's kernel intervals in a kernel trace — bench.py's roofline
+    divides by the same union (launches of two streams overlap)."""
+    iv = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            t = tag(r['Kernel_Name'], r['LDS_Block_Size'])
+            if t.startswith('x3_') or 'hr1_sum' in t:
+                iv.append((int(r['Start_Timestamp']), int(r['End_Timestamp'])))
+    tot, hi = 0, None
+    for a, b in sorted(iv):
+        if hi is None or a > hi:
+            tot, hi = tot + b - a, b
+        elif b > hi:
+            tot, hi = tot + b - hi, b
+    return len(iv), tot / 1e3
+
+
 def load_pmc(path, counter):
     agg = defaultdict(lambda: [0, 0.0])
     if not os.path.exists(path):
@@ -78,7 +96,9 @@ def main(src, dst):
         rows.append(dict(kernel=k, calls=n, avg_us=us / n, total_ms=us / 1e3, share=us / total,
                          hbm_read_bytes_per_launch=fetch, hbm_write_bytes_per_launch=write))
     os.makedirs(os.path.dirname(dst) or '.', exist_ok=True)
-    json.dump({'source': src, 'kernels': rows}, open(dst + '_pmc.json', 'w'), indent=1)
+    n_x3, u_x3 = x3_family_union(os.path.join(src, 'trace', 'run_kernel_trace.csv'))
+    json.dump({'source': src, 'kernels': rows, 'x3_family_launches': n_x3,
+               'x3_family_union_us_per_launch': u_x3 / n_x3 if n_x3 else None}, open(dst + '_pmc.json', 'w'), indent=1)
     with open(dst + '_kernels.md', 'w') as f:
         f.write('| kernel | calls | avg µs | total ms | share | HBM read B/launch (FETCH_SIZE×2) | HBM write B/launch |\n')
         f.write('|---|---|---|---|---|---|---|\n')
@@ -88,6 +108,9 @@ def main(src, dst):
                                                                      r['total_ms'], r['share'],
                                                                      fmt(r['hbm_read_bytes_per_launch']),
                                                                      fmt(r['hbm_write_bytes_per_launch'])))
+        if n_x3:
+            f.write('\nx3 MFMA conv family: %d launches, union of their intervals %.2f ms = %.2f µs per launch '
+                    '(bench.py roofline: FLOPs / the same union from HIP events)\n' % (n_x3, u_x3 / 1e3, u_x3 / n_x3))
     print(open(dst + '_kernels.md').read())
 
 
