@@ -389,7 +389,7 @@ def main():
                    'tflops_over_own_union': round(v[1] / (union[k] / 1e3) / 1e12, 2),
                    'share_of_step': round(union[k] / (dt * 1e3), 3)}
                for k, v in per.items()}
-    streams = engine.STREAMS if (engine.USE_OP_LISTS and args.batch >= engine.STREAM_MIN_B) else 1
+    streams = engine.STREAMS if (engine.USE_OP_LISTS and engine.use_streams(x.shape, None if args.no_cem else model)) else 1
     rec = {
         'metric': METRIC, 'value': round(value, 3), 'unit': 'HR Mpixels/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': round(dt / args.steps * 1e3, 3), 'higher_is_better': True,

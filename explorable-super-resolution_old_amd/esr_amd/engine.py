@@ -782,8 +782,12 @@ def _planned_forward(net, x, cem, precision):
 # Inference batches of at least STREAM_MIN_B images run as STREAMS parts on as many HIP streams at once (each part
 # with its own workspace and op list): one part's kernels fill the GPU where another's are in their last, partly empty
 # round of workgroups or between launches.  ESR_STREAMS=1: one stream (A/B).
+# Only where each part alone still fills the chip for a round or more: measured at config 2 (two parts of 16 × 148²
+# padded pixels each) +4.7 %; at 4 × 172² and 16 × 96² parts within ±1 %, at 4 × 154² 19 % slower
+# (profiles/r5_streams_shapes.txt).
 STREAMS = int(os.environ.get('ESR_STREAMS', '2'))
 STREAM_MIN_B = 8
+STREAM_MIN_PART_PIXELS = 300000
 _SIDE_STREAMS = {}
 
 
@@ -792,6 +796,14 @@ def _side_stream(dev, k):
     if key not in _SIDE_STREAMS:
         _SIDE_STREAMS[key] = torch.cuda.Stream(dev)
     return _SIDE_STREAMS[key]
+
+
+def use_streams(shape, cem):
+    """Whether an inference forward of an input of `shape` runs as STREAMS batch parts (the padded LR pixels of a part
+    at least STREAM_MIN_PART_PIXELS)."""
+    B, _, h, w = shape
+    m = 2 * int(cem.margins_LR) if (cem is not None and cem.pre_pad) else 0
+    return STREAMS > 1 and B >= STREAM_MIN_B and (B // STREAMS) * (h + m) * (w + m) >= STREAM_MIN_PART_PIXELS
 
 
 def _multistream_forward(net, x, cem, precision, n):
@@ -833,7 +845,7 @@ def generator_forward(net, x, cem=None):
     if precision not in PRECISIONS:
         raise ValueError('esr_precision must be one of %s' % (PRECISIONS,))
     x = x.contiguous()
-    if USE_OP_LISTS and STREAMS > 1 and x.shape[0] >= STREAM_MIN_B:
+    if USE_OP_LISTS and use_streams(x.shape, cem):
         out, wss = _multistream_forward(net, x, cem, precision, STREAMS)
     elif USE_OP_LISTS:
         out, ws = _planned_forward(net, x, cem, precision)

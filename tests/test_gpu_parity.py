@@ -349,6 +349,47 @@ def test_x3_trained_scale_weights_and_small_activations(gpu_device, img_scale):
     assert errs['x3'] < 1e-4
 
 
+@pytest.mark.parametrize('precision', ['x3', 'f32'])
+def test_multistream_forward_bitwise_equals_one_stream(gpu_device, monkeypatch, precision):
+    """engine._multistream_forward (the batch in S parts on S HIP streams, config 2's default) at a small shape with
+    the part-size gate lifted: S = 2 and 3 (ragged parts: 9 images) bitwise equal to one stream, latent slot and CEM
+    pre-pad included; the output is stream-ordered for the caller (read on the current stream right after)."""
+    model, _ = _big_model(1, True, gpu_device, precision, seed=61)
+    model.eval()
+    g = torch.Generator().manual_seed(62)
+    B, h, w = 9, 12, 20
+    z = 2 * torch.rand(B, 3, 1, 1, generator=g) - 1
+    x = torch.cat([z.expand(B, 3, 4 * h, 4 * w).reshape(B, 48, h, w), torch.rand(B, 3, h, w, generator=g)], 1)
+    xd = x.to(gpu_device)
+    monkeypatch.setattr(engine, 'STREAM_MIN_PART_PIXELS', 0)
+    outs = {}
+    with torch.no_grad():
+        for s in (1, 2, 3):
+            monkeypatch.setattr(engine, 'STREAMS', s)
+            assert engine.use_streams(xd.shape, model) == (s > 1)
+            outs[s] = model(xd).cpu()
+    assert torch.equal(outs[1], outs[2])
+    assert torch.equal(outs[1], outs[3])
+
+
+def test_multistream_overflow_in_one_part_reruns_the_batch(gpu_device, monkeypatch):
+    """An f16-range overflow in the second of two stream parts: the whole batch reruns in exact fp32."""
+    model, _ = _big_model(1, False, gpu_device, 'x3', seed=41, w_scale=1.0)
+    model.eval()
+    monkeypatch.setattr(engine, 'STREAM_MIN_PART_PIXELS', 0)
+    monkeypatch.setattr(engine, 'STREAMS', 2)
+    x = torch.rand(8, 3, 16, 16, generator=torch.Generator().manual_seed(43))
+    x[5:] *= 3.0e5  # the second part's inputs drive conv_first beyond 65504
+    xd = x.to(gpu_device)
+    before = engine.OVERFLOW_RERUNS
+    with torch.no_grad():
+        y = model(xd)
+        engine.set_precision(model, 'f32')
+        ref = model(xd)
+    assert engine.OVERFLOW_RERUNS == before + 1
+    assert torch.equal(y, ref)
+
+
 def test_x3_overflow_falls_back_to_exact_f32(gpu_device):
     """Activations beyond the f16 range must not corrupt the x3 path: the overflow flag triggers an exact-fp32 rerun."""
     model, _ = _big_model(1, False, gpu_device, 'x3', seed=41, w_scale=1.0)
