@@ -93,8 +93,10 @@ def observed(a, b):
 
 def leg_args(**kw):
     """Default arguments of this benchmark (BASELINE config 3 per GPU), for callers such as bench.py."""
-    # warmup 4: the caching allocator still returns memory to the device (hipFree, ~200 frees) in calls 3-4
-    d = dict(gpus=1, steps=10, warmup=4, batch=16, lr_size=96, nb=23, latent=True)
+    # warmup 6: the caching allocator grows over the first calls (HIP graph captures in calls 2-3), returns memory to
+    # the device in call 4 and makes its last device allocations (9, in the discriminator's double backward) in calls
+    # 5-6; from call 7 on a step allocates nothing (tools/alloc_probe.py, profiles/r5_c3_alloc_steps.txt)
+    d = dict(gpus=1, steps=10, warmup=6, batch=16, lr_size=96, nb=23, latent=True)
     d.update(kw)
     return argparse.Namespace(**d)
 
@@ -188,7 +190,7 @@ def main():
     ap.add_argument('--gpus', type=int, default=None, help='ranks (one per GPU); default: WORLD_SIZE, else 1')
     ap.add_argument('--launcher-check', action='store_true', help='bring the ranks up on the CPU (gloo) and stop')
     ap.add_argument('--steps', type=int, default=10)
-    ap.add_argument('--warmup', type=int, default=4)
+    ap.add_argument('--warmup', type=int, default=6)
     ap.add_argument('--batch', type=int, default=16)
     ap.add_argument('--lr-size', type=int, default=96)
     ap.add_argument('--nb', type=int, default=23)

@@ -41,9 +41,10 @@ def main():
         model.optimize_parameters()
         torch.cuda.synchronize()
         ms = torch.cuda.memory_stats()
-        print('step %d: device allocs %d, reserved %.1f MB, allocated %.1f MB' % (
+        print('step %d: device allocs %d, reserved %.1f MB, allocated %.1f MB, peak %.1f MB, generator_step %s' % (
             s, ms.get('num_device_alloc', 0) - n0, ms['reserved_bytes.all.current'] / 2**20,
-            ms['allocated_bytes.all.current'] / 2**20), flush=True)
+            ms['allocated_bytes.all.current'] / 2**20, ms['allocated_bytes.all.peak'] / 2**20,
+            bool(model.generator_step)), flush=True)
     snap = torch.cuda.memory._snapshot()
     torch.cuda.memory._record_memory_history(enabled=None)
     for dev_trace in snap['device_traces']:
