@@ -63,6 +63,8 @@ def parse():
     ap.add_argument('--leg-steps', type=int, default=10)
     ap.add_argument('--x3-kernel', type=int, default=None, help='esr_x3_set_kernel variant (A/B: needs the ablation '
                     'library, ESR_AMD_LIB=exp_lib/libesr_exp.so; default automatic)')
+    ap.add_argument('--profile-steps', type=int, default=2, help='timed steps (the last ones) that carry per-launch HIP '
+                    'events for the roofline')
     ap.add_argument('--no-op-timers', action='store_true', help='time the steps without the per-launch HIP events '
                     '(no roofline; measures what the events themselves cost)')
     return ap.parse_args()
@@ -326,24 +328,25 @@ def main():
         # the last warmup forward runs profiled to learn the op-list length(s); their timers are then created up front,
         # outside the timed region
         probe = []
+        n_prof = min(args.steps, max(1, args.profile_steps))
         for i in range(max(args.warmup, 1)):
             engine._PROFILE = probe if i == max(args.warmup, 1) - 1 else None
             out = model(x)
         torch.cuda.synchronize()
         engine._PROFILE = None
         for n_ops in {e[3] for e in probe if e[0] == 'ops'}:
-            engine.reserve_timers(n_ops, args.steps)
+            engine.reserve_timers(n_ops, n_prof)
         list(engine.profile_records(probe))
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         prof = []
-        engine._PROFILE = None if args.no_op_timers else prof
         origin = engine.ProfileOrigin(dev)
         origin.record()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
+        for i in range(args.steps):  # per-launch events on the last n_prof steps only (their cost: ~1.5 % of a step)
+            engine._PROFILE = prof if (not args.no_op_timers and i >= args.steps - n_prof) else None
             out = model(x)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
@@ -385,9 +388,10 @@ def main():
     achieved = fl_all / (busy / 1e3) / 1e12
     dom = max(per, key=lambda k: per[k][2])
     peak, peak_note = PEAKS[args.precision]
-    kernels = {k: {'launches_per_step': v[0] // args.steps, 'avg_us': round(v[2] / v[0] * 1e3, 2),
+    prof_ms = dt * 1e3 * n_prof / args.steps  # wall time of the profiled steps (the steps are alike)
+    kernels = {k: {'launches_per_step': v[0] // n_prof, 'avg_us': round(v[2] / v[0] * 1e3, 2),
                    'tflops_over_own_union': round(v[1] / (union[k] / 1e3) / 1e12, 2),
-                   'share_of_step': round(union[k] / (dt * 1e3), 3)}
+                   'share_of_step': round(union[k] / prof_ms, 3)}
                for k, v in per.items()}
     streams = engine.STREAMS if (engine.USE_OP_LISTS and engine.use_streams(x.shape, None if args.no_cem else model)) else 1
     rec = {
@@ -402,15 +406,17 @@ def main():
         'roofline': {'bound': 'mfma', 'kernel': 'x3 MFMA conv family (%s), all launches of the step' % ', '.join(sorted(per)),
                      'achieved': round(achieved, 2), 'peak': round(peak, 1), 'peak_basis': peak_note,
                      'unit': 'TFLOP/s', 'frac': round(achieved / peak, 4), 'traffic': None,
-                     'flops_per_launch': fl_all / n_all, 'launches_per_step': n_all // args.steps,
+                     'flops_per_launch': fl_all / n_all, 'launches_per_step': n_all // n_prof,
+                     'profiled_steps': n_prof,
                      'union_us_per_launch': round(busy / n_all * 1e3, 2), 'streams': streams,
-                     'timing': 'achieved = FLOPs of all launches / union of their HIP-event intervals over the timed '
-                               'region (%d stream(s); union / launches is the effective launch time the rocprof '
-                               'kernel-trace union is checked against)' % streams,
+                     'timing': 'achieved = FLOPs of all launches / union of their HIP-event intervals, events on '
+                               'every launch of the last %d of the %d timed steps (%d stream(s); union / launches is '
+                               'the effective launch time the rocprof kernel-trace union is checked against)'
+                               % (n_prof, args.steps, streams),
                      'dominant_tag': {'tag': dom, 'flops_per_launch': per[dom][1] / per[dom][0],
                                       'avg_launch_us': round(per[dom][2] / per[dom][0] * 1e3, 2)}},
         'kernels': kernels,
-        'gpu_busy_frac': round(busy / (dt * 1e3), 3),
+        'gpu_busy_frac': round(busy / prof_ms, 3),
         'dist': {'world_size': dist.get_world_size() if world > 1 else 1,
                  'backend': dist.get_backend() if world > 1 else None},
     }
