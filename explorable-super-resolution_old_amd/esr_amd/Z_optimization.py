@@ -21,8 +21,8 @@ switches), evaluated on the device on the generator output, with the reference's
   (loss.py:79,134: KeyError).  'VGG' raises: its feature extractor is unbuildable in the reference (NameError,
   architecture.py:294-300) and torchvision is absent.  Plain 'l1' with an image mask raises as the reference does
   (its masked-L1 closure reads a mask defined only for 'scribble', Z_optimization.py:386-397: NameError).
-  auto_set_hist_temperature raises: its temperature search differentiates the histogram loss's input gradient through
-  the generator a second time (Z_optimization.py:479-499, create_graph=True).
+  auto_set_hist_temperature raises as the reference does with the GUI's data (AttributeError on data['HR'].detach() of a
+  list, Z_optimization.py:485; AssertionError for a 'dict' objective): see Z_optimizer._auto_hist_temperature.
 """
 import numpy as np
 import torch
@@ -400,8 +400,6 @@ class Z_optimizer:
         if masked_l1:
             raise NotImplementedError('Z objective %r with an image mask: the reference\'s masked L1 reads a mask it '
                                       'only defines for "scribble" (NameError)' % objective)
-        if auto_set_hist_temperature and ('hist' in objective or 'dict' in objective):
-            raise NotImplementedError('auto_set_hist_temperature: not built (second-order through the generator)')
         self.device = model.device
         dev = self.device
         self.on_iteration = None  # optional callback(z_iter) after each iteration (benchmarks)
@@ -494,6 +492,8 @@ class Z_optimizer:
         elif 'hist' in o or 'dict' in o:
             self.automatic_temperature = auto_temperature
             self.STD_PRESERVING_WEIGHT = 1e4
+            if auto_temperature:
+                self._auto_hist_temperature(data)
             self.loss = SoftHistogramLoss(
                 bins=256, min=0, max=1, desired_hist_image=data['HR'] if data is not None else None,
                 desired_hist_image_mask=data['Desired_Im_Mask'] if data is not None else None,
@@ -506,6 +506,24 @@ class Z_optimizer:
         elif 'limited' in o:
             self.initial_image = 1 * self.model.fake_H.detach()
             self.rmse_weight = data['rmse_weight']
+
+    def _auto_hist_temperature(self, data):
+        """auto_set_hist_temperature (Z_optimization.py:479-486) fails in the reference before its temperature search
+        starts, and fails here the same way: a 'dict' objective trips its assertion, and a 'hist' objective hands
+        data['HR'].detach() to the search's SoftHistogramLoss while the GUI passes data['HR'] as a LIST of desired
+        images (GUI.py:1549) — AttributeError, recorded by running the reference on the stand-in model
+        (tests/golden/make_golden_zobj.py auto_hist -> zobj_auto_hist.json).  With a single tensor the reference would
+        go on to histogram that tensor's per-row means (its gray-scale branch iterates the tensor's first dimension) and
+        differentiate the loss's input gradient through the generator again (create_graph=True): not built."""
+        assert 'hist' in self.objective, 'Unsupported  for dictionary'
+        hr = None if data is None else data.get('HR')
+        if isinstance(hr, (list, tuple)):
+            raise AttributeError("'list' object has no attribute 'detach' (auto_set_hist_temperature: the reference's "
+                                 "temperature search calls data['HR'].detach() on the GUI's list of desired images, "
+                                 "Z_optimization.py:485)")
+        raise NotImplementedError('auto_set_hist_temperature with a single desired-image tensor: the reference '
+                                  'histograms its per-row means and differentiates through the generator twice; '
+                                  'not built')
 
     def _build_scribble(self, data):
         """Masked L1 to the scribbled image + per-region TV (Z_optimization.py:376-416).  Scribble ids: 1 = match,

@@ -2,7 +2,8 @@
 /root/reference) run here on the CPU over the stand-in model of tests/golden/zobj_recipe.py for every objective the
 GUI builds (zobj_recipe.CASES).  Only the small .npz it writes is committed.
 
-    python tests/golden/make_golden_zobj.py
+    python tests/golden/make_golden_zobj.py [case ...]
+    python tests/golden/make_golden_zobj.py auto_hist     (what auto_set_hist_temperature raises -> zobj_auto_hist.json)
 
 In-memory shims (nothing is written under /root/reference; no reference bytecode is loaded or written), on top of
 make_golden.install_shims():
@@ -121,9 +122,34 @@ def run_case(Zo, name, seed, iters_override=None):
     return out
 
 
+def auto_hist_temperature(Zo):
+    """The reference's auto_set_hist_temperature (Z_optimization.py:476-499) on a 'hist' case with the GUI's data
+    layout (data['HR'] a list of desired images, GUI.py:1549): what it raises, recorded in zobj_auto_hist.json."""
+    out = {}
+    for name in ('hist_localSTD', 'patchhist_noDC_localSTD'):
+        objective, B, data, img_mask, z_mask, z_range, lr, z, iters, lr0 = case_data(name, 1234)
+        torch.manual_seed(0)
+        model = StandInModel(torch.from_numpy(lr), torch.from_numpy(z), 1237, 'cpu')
+        tdata = {'LR': torch.from_numpy(lr), 'HR': [torch.from_numpy(x) for x in data['HR']],
+                 'Desired_Im_Mask': data['Desired_Im_Mask']}
+        try:
+            Zo.Z_optimizer(objective=objective, Z_size=[4 * lr.shape[2], 4 * lr.shape[3]], model=model,
+                           Z_range=z_range, max_iters=iters, data=tdata, initial_LR=lr0, image_mask=img_mask,
+                           Z_mask=z_mask, initial_Z=torch.from_numpy(z), batch_size=B, auto_set_hist_temperature=True)
+            out[name] = {'raises': None}
+        except Exception as e:  # noqa: BLE001
+            out[name] = {'raises': type(e).__name__, 'message': str(e)}
+        print(name, out[name], flush=True)
+    with open(os.path.join(HERE, 'zobj_auto_hist.json'), 'w') as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
 def main():
     install_zobj_shims()
     import Z_optimization as Zo
+    if sys.argv[1:] == ['auto_hist']:
+        auto_hist_temperature(Zo)
+        return
     torch.set_num_threads(8)
     names = sys.argv[1:] or list(CASES)
     path = os.path.join(HERE, 'zobj_cases.npz')

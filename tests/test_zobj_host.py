@@ -94,3 +94,25 @@ def test_patch_extraction_matrix_layout():
     assert win.shape == (8 * 9, 9) and win[0].tolist() == [16, 17, 18, 30, 31, 32, 44, 45, 46]
     mat2, nc = ReturnPatchExtractionMat(mask, 3, 'cpu', patches_overlap=0.5, return_non_covered=True)
     assert mat2.shape[0] % 9 == 0 and mat2.shape[0] < mat.shape[0] and nc is not None
+
+
+@pytest.mark.parametrize('name', ['hist_localSTD', 'patchhist_noDC_localSTD'])
+def test_auto_hist_temperature_fails_as_the_reference(name):
+    """auto_set_hist_temperature with the GUI's data layout (data['HR'] a list of desired images): the reference
+    raises before its temperature search (zobj_auto_hist.json, recorded by make_golden_zobj.py auto_hist), and so does
+    the port, with the same exception type; a 'dict' objective trips the reference's assertion."""
+    from esr_amd.Z_optimization import Z_optimizer
+    ref = json.load(open(os.path.join(HERE, 'golden', 'zobj_auto_hist.json')))[name]
+    objective, B, data, img_mask, z_mask, z_range, lr, z, iters, lr0 = case_data(name, 1234)
+    model = StandInModel(torch.from_numpy(lr), torch.from_numpy(z), 1237, 'cpu')
+    tdata = {'LR': torch.from_numpy(lr), 'HR': [torch.from_numpy(x) for x in data['HR']],
+             'Desired_Im_Mask': data['Desired_Im_Mask']}
+    kw = dict(Z_size=[4 * lr.shape[2], 4 * lr.shape[3]], model=model, Z_range=z_range, max_iters=iters, data=tdata,
+              initial_LR=lr0, image_mask=img_mask, Z_mask=z_mask, initial_Z=torch.from_numpy(z), batch_size=B,
+              auto_set_hist_temperature=True)
+    with pytest.raises(Exception) as ei:
+        Z_optimizer(objective=objective, **kw)
+    assert type(ei.value).__name__ == ref['raises'] == 'AttributeError'
+    assert ref['message'] in str(ei.value)
+    with pytest.raises(AssertionError, match='Unsupported  for dictionary'):
+        Z_optimizer(objective=objective.replace('hist', 'dict'), **kw)
