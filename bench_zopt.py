@@ -88,7 +88,8 @@ def run(args, dev, world, rank):
     settle()
     obs0 = observe()
     stamps = []
-    # each iteration ends with its overflow-flag read (a device sync), so these are per-iteration wall times
+    # host stamps after each iteration is enqueued (the overflow flags are read one iteration later, so the host runs
+    # about one iteration ahead of the GPU; the timed region ends with a synchronize)
     zo.on_iteration = lambda _: stamps.append(time.perf_counter())
     torch.cuda.synchronize()
     if world > 1:

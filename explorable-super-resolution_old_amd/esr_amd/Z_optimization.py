@@ -33,6 +33,10 @@ from . import train_engine as TE
 from .loss import GANLoss
 
 _UNSUPPORTED = ('desired_SVD', 'VGG')
+# Z_optimizer.optimize reads each iteration's x3 overflow flags one iteration later (no stream drain between
+# iterations); ESR_ZOPT_LAG=0: right after the iteration (A/B)
+import os as _os
+LAGGED_OVERFLOW_CHECK = _os.environ.get('ESR_ZOPT_LAG', '1') != '0'
 
 
 # ----------------------------------------------------------------------------------------------------------------
@@ -709,6 +713,10 @@ class Z_optimizer:
             self.model.netG.train(True)
         self.Manage_Model_Grad_Requirements(disable=True)
         self.loss_values = []
+        import torch.distributed as dist
+        lag = LAGGED_OVERFLOW_CHECK and self.device.type == 'cuda' and not (
+            dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
+        pend = None  # (snapshot before the iteration, its overflow flags, its z_iter) awaiting their read
         if self.random_Z_inits and self.cur_iter == 0:
             self.Z_model.Randomize_Z(what_2_shuffle=self.random_Z_inits)
         z_iter = self.cur_iter
@@ -722,31 +730,32 @@ class Z_optimizer:
                 first, last = float(self.loss_values[self.max_iters]), float(self.loss_values[-1])
                 if (first - last) / np.abs(first) < 1e-2 * self.LR:
                     break
-            # one Z iteration with the generator's x3 overflow checks read once at its end (not after the forward
-            # and again after the backward, each a stream drain): from a snapshot of Z and its Adam state the
-            # iteration is redone with the generator in exact fp32 if a flag was set
+            # one Z iteration with the generator's x3 overflow flags collected on the device (TE.DeferredOverflow)
+            # and read one iteration later, so the host enqueues iteration k + 1 while the GPU runs iteration k (no
+            # stream drain between iterations).  If iteration k overflowed, iteration k + 1 (run on k's result) is
+            # dropped: Z and its Adam state go back to the snapshot taken before k, k is redone with the generator in
+            # exact fp32, and k + 1 is enqueued again.  Across ranks the flags are read right away (all-reduced).
             snap = self._snapshot()
-            with TE.deferred_overflow_checks() as chk:
-                Z_loss = self._iteration(z_iter)
-            if chk.overflowed():
-                E.OVERFLOW_RERUNS += 1
+            Z_loss, chk = self._checked_iteration(z_iter, lag)
+            if pend is not None and pend[1].overflowed():
+                self._restore(pend[0])
+                del self.loss_values[-1:]
+                self.loss_values.append(self._redo_f32(pend[2]))
+                snap = self._snapshot()
+                Z_loss, chk = self._checked_iteration(z_iter, lag)
+            if not lag and chk.overflowed():
                 self._restore(snap)
-                # every RRDBNet under netG (CEM-wrapped or not, DataParallel or not) in exact fp32 for the redo
-                prev = [(m, m.__dict__.get('esr_precision')) for m in self.model.netG.modules()
-                        if hasattr(m, '_esr_cache')]
-                E.set_precision(self.model.netG, 'f32')
-                try:
-                    Z_loss = self._iteration(z_iter)
-                finally:
-                    for m, p in prev:
-                        if p is None:
-                            m.__dict__.pop('esr_precision', None)
-                        else:
-                            m.esr_precision = p
+                Z_loss = self._redo_f32(z_iter)
+                pend = None
+            else:
+                pend = (snap, chk, z_iter) if lag else None
             self.loss_values.append(Z_loss)
             z_iter += 1
-            if self.on_iteration is not None:  # (benchmarks: per-iteration wall times; the check above synchronised)
+            if self.on_iteration is not None:  # (benchmarks: per-iteration host stamps)
                 self.on_iteration(z_iter)
+        if pend is not None and pend[1].overflowed():  # the last iteration's flags
+            self._restore(pend[0])
+            self.loss_values[-1] = self._redo_f32(pend[2])
         self.loss_values = [float(v) for v in self.loss_values]
         if not self.model_training:
             self.latest_Z_loss_values = [float(v) for v in self.latest_Z_loss_values]
@@ -764,6 +773,28 @@ class Z_optimizer:
             self.model.feed_data(self.data, need_HR=False)
             self.model.fake_H = self.model.netG(self.model.model_input)
         return Z_2_return
+
+    def _checked_iteration(self, z_iter, lag):
+        with TE.deferred_overflow_checks() as chk:
+            Z_loss = self._iteration(z_iter)
+        if lag:
+            chk.start_read()
+        return Z_loss, chk
+
+    def _redo_f32(self, z_iter):
+        """One iteration with every RRDBNet under netG (CEM-wrapped or not, DataParallel or not) in exact fp32 (after
+        an x3 overflow; the caller restored Z and its Adam state first)."""
+        E.OVERFLOW_RERUNS += 1
+        prev = [(m, m.__dict__.get('esr_precision')) for m in self.model.netG.modules() if hasattr(m, '_esr_cache')]
+        E.set_precision(self.model.netG, 'f32')
+        try:
+            return self._iteration(z_iter)
+        finally:
+            for m, p in prev:
+                if p is None:
+                    m.__dict__.pop('esr_precision', None)
+                else:
+                    m.esr_precision = p
 
     def _snapshot(self):
         params = [p.detach().clone() for p in self.Z_model.parameters()]

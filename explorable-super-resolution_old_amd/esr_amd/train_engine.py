@@ -81,17 +81,36 @@ class DeferredOverflow:
         self.resets.append((bad.clone(), reset))
         self.on_flag.append(on_overflow)
 
+    def _stacked(self):
+        return torch.stack([f.reshape(()).float() for f in self.flags] +
+                           [b.reshape(()).float() for b, _ in self.resets])
+
+    def start_read(self):
+        """Start the flags' device-to-host copy now, stream-ordered after the work that set them (into pinned memory,
+        with an event), so that overflowed() can be asked later — after more work is enqueued — without draining the
+        stream.  Single-process only: across ranks overflowed() all-reduces the flags itself."""
+        self._host = None
+        if self.flags:
+            t = self._stacked()
+            self._host = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+            self._host.copy_(t, non_blocking=True)
+            self._event = torch.cuda.Event()
+            self._event.record()
+
     def overflowed(self):
         """True if any deferred forward or backward overflowed (one device-to-host read; all-reduced over ranks)."""
         if not self.flags:
             return False
-        t = torch.stack([f.reshape(()).float() for f in self.flags] +
-                        [b.reshape(()).float() for b, _ in self.resets])
-        import torch.distributed as dist
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-            from .SRRaGAN_model import collective
-            collective(dist.all_reduce, t, op=dist.ReduceOp.MAX)  # every rank redoes the step together
-        vals = t.tolist()
+        if getattr(self, '_host', None) is not None:  # start_read(): wait for that copy only
+            self._event.synchronize()
+            vals = self._host.tolist()
+        else:
+            t = self._stacked()
+            import torch.distributed as dist
+            if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+                from .SRRaGAN_model import collective
+                collective(dist.all_reduce, t, op=dist.ReduceOp.MAX)  # every rank redoes the step together
+            vals = t.tolist()
         n = len(self.flags)
         for (_, reset), bad in zip(self.resets, vals[n:]):
             if bad:
