@@ -17,7 +17,7 @@
 extern "C" {
 #endif
 
-/* esr_conv3x3_fwd_x3 / esr_upconv2x_phase_fwd_x3 kernel (0..65; 65 = 12-column tiles for N = 64 too, two per CU).  All non-diagnostic variants are bitwise identical.
+/* esr_conv3x3_fwd_x3 / esr_upconv2x_phase_fwd_x3 kernel (0..88; 65 = 12-column tiles for N = 64 too, two per CU; 70-84 the persistent kernel and the time-split ablations; 85 / 86 = N = 32 3x3 convs in 18 / 24-column tiles at two per CU, 87 = the 12-column kernel with per-chunk s_memrealtime stamps (esr_x3c_set_stamps), 88 = N = 32 3x3 convs on the 8-channel double-buffered kernel (not bitwise equal: another summation order); everything else automatic).  All non-diagnostic variants are bitwise identical.
  * 0 / 1 / 63 = automatic (the product dispatch); 24 = the round-1 automatic choice (classic kernel only: 8-row at three
  *   per CU or 16-row at two; 25 / 26 force one); 50 = column-tile kernel (16 columns); 60 = column tiles with the
  *   weights read into registers from global memory; 61 = 8 waves of 2 columns; 62 = weights copied to registers per
@@ -29,6 +29,9 @@ extern "C" {
  * diagnostics (garbage outputs): 3-14, 19 (ring), 29-30, 40-46 (classic), 51-54 (column tiles), 55-59 (warp-
  *   specialised persistent form). */
 int esr_x3_set_kernel(int32_t variant);
+/* Variant 87's stamp buffer: 38 u64 per workgroup (kernel start, per K chunk before DMA / after its wait / after
+ * compute, end); NULL: not stored.  Returns 0, or -1. */
+int esr_x3c_set_stamps(void *buf);
 /* Block -> tile order of the x3 and exact-fp32 generator convs: 1 = XCD-grouped (product), 0 = row-major. */
 int esr_x3_set_tile_map(int32_t mode);
 /* HR_conv1 on the narrow-N kernel: 1 (product) / 0 = N = 32 tiles (equal to the x3 rounding, not bitwise). */

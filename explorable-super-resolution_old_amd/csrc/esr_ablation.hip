@@ -19,7 +19,7 @@ int set_knob(int &knob, int32_t v, int lo, int hi) {
 }
 }  // namespace
 
-extern "C" int esr_x3_set_kernel(int32_t variant) { return set_knob(g_x3_kernel, variant, 0, 84); }
+extern "C" int esr_x3_set_kernel(int32_t variant) { return set_knob(g_x3_kernel, variant, 0, 88); }
 extern "C" int esr_x3_set_tile_map(int32_t mode) { return set_knob(g_tile_map, mode, 0, 1); }
 extern "C" int esr_x3_set_narrow(int32_t on) { return set_knob(g_x3_narrow, on, 0, 1); }
 extern "C" int esr_x3_set_nsplit(int32_t on) { return set_knob(g_x3_nsplit, on, 0, 1); }

@@ -1248,6 +1248,17 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
         (o->out2 && (o->out2_cp % 8 || o->out2_coff % 8)))
         return ESR_EINVAL;
     if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(w)) & 15) return ESR_EINVAL;
+#ifdef ESR_X3_EXPERIMENTS
+    // 85 / 86 (wider N = 32 3x3 tiles, below): every other conv as the automatic choice (variant 1)
+    if ((g_x3_kernel >= 85 && g_x3_kernel <= 88) && !(taps_side == 3 && cout <= 32 && (!o->out_planar || g_x3_kernel == 88))) {
+        const int saved = g_x3_kernel;
+        g_x3_kernel = 1;
+        const int rc = launch_x3(in, B, H, W, in_cp, cin, w, bias, w_scale, cout, taps_side, ty0, tx0, o, overflow,
+                                 stream);
+        g_x3_kernel = saved;
+        return rc;
+    }
+#endif
     X3Params p;
     p.in = static_cast<const unsigned char *>(in);
     p.B = B; p.H = H; p.W = W; p.in_cp = in_cp; p.cin = cin;
@@ -1335,7 +1346,7 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
     const int tiles12 = ((W + 11) / 12) * ((B * (H + 2) - 2 + 31) / 32);
     const bool x3c_pays = taps_side == 2 || (taps_side == 3 && (cout > 32 || !row8_pays || tiles12 >= n_cu));
     if ((g_x3_kernel >= 50 && g_x3_kernel <= 62) || g_x3_kernel == 64 || g_x3_kernel == 65 ||
-        (g_x3_kernel >= 70 && g_x3_kernel <= 84) ||
+        (g_x3_kernel >= 70 && g_x3_kernel <= 88) ||
         ((g_x3_kernel == 1 || g_x3_kernel == 63) && x3c_pays)) {
         X3cParams c;
         c.in = p.in; c.B = B; c.H = H; c.W = W; c.in_cp = in_cp; c.cin = cin; c.w = p.w; c.bias = bias;
@@ -1349,6 +1360,12 @@ int launch_x3(const void *in, int B, int H, int W, int in_cp, int cin, const voi
         // (a tie); profiles/r4_x3_n64_tiles.txt.  Round 3's N split (two N = 32 launches) lost to one of the two at
         // every measured grid and is the ablation library's option (esr_x3_set_nsplit)
 #ifdef ESR_X3_EXPERIMENTS  // 70-74: the persistent double-buffered N = 32 kernel (esr_conv_x3p.hip) and its ablations
+        if ((g_x3_kernel == 85 || g_x3_kernel == 86) && taps_side == 3 && cout <= 32 && !o->out_planar)
+            return x3c_launch(c, taps_side, stream, g_x3_kernel == 85 ? 300 : 301);  // wider N = 32 tiles (A/B)
+        if (g_x3_kernel == 87 && taps_side == 3 && cout <= 32 && !o->out_planar)
+            return x3c_launch(c, taps_side, stream, 302);  // stamped diagnostic build of the 12-column kernel
+        if (g_x3_kernel == 88 && taps_side == 3 && cout <= 32)
+            return x3c_launch(c, taps_side, stream, 303);  // 8-channel double-buffered form (A/B)
         if (g_x3_kernel >= 80 && g_x3_kernel <= 84 && cout <= 32) {  // 12-column time split: 81 = no DMA after chunk 0
             // + no stores, 82 = 81 without MFMAs (reads only), 83 = 81 without reads (MFMAs only), 84 = neither
             static const int dbgt[5] = {64, 5, 13, 21, 29};  // 64: the kernel as built (DBG 0)

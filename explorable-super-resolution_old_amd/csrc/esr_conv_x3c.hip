@@ -22,6 +22,10 @@
 #include "esr_amd.h"
 #include "esr_x3c.h"
 
+#ifdef ESR_X3_EXPERIMENTS
+static void *g_x3c_stamps = nullptr;  // variant 87's stamp buffer (host side; handed to the kernel in X3cParams.y1)
+#endif
+
 namespace {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -45,6 +49,12 @@ constexpr int KIN = (IN_PIECES + NWV - 1) / NWV; // input pieces per wave (10)
 constexpr int N_XCD = 8;
 
 __device__ __attribute__((aligned(16))) unsigned char g_zero64[64];
+// DBG 32 (diagnostic build, variant 87): per-workgroup s_memrealtime stamps (100 MHz) of wave 0 — kernel start, then per
+// K chunk (before its LDS-DMA issue, after its wait + barrier, after its compute), then after the epilogue — written
+// by vector stores into the buffer passed in X3cParams.y1 (unused by this instantiation; X3C_NS stamps per workgroup)
+// and read by tools/x3c_stamps.py.  Only their shares mean anything: the stamps' own waits forbid overlaps the real
+// kernel has.
+constexpr int X3C_NCH = 12, X3C_NS = 2 + 3 * X3C_NCH;  // (stamp slots of the DBG 32 build)
 
 __device__ __forceinline__ float lrelu(float v) { return v > 0.f ? v : 0.2f * v; }
 
@@ -180,6 +190,21 @@ __global__ __launch_bounds__(64 * (TW / CWV), (TW / CWV) * OCC / 4) void conv_x3
     const long long pixb = 4LL * p.in_cp;
     const int nchunk = (p.cin + 15) >> 4;
     const unsigned char *tile_in = p.in + ((long long)r0 * rowp + x0) * pixb;
+#ifdef ESR_X3_EXPERIMENTS
+    unsigned long long stamps[(DBG & 32) ? X3C_NS : 1];
+    auto stamp = [&](int idx) {
+        if constexpr ((DBG & 32) != 0) {
+            __builtin_amdgcn_sched_barrier(0);
+            unsigned long long t;
+            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");  // 100 MHz
+            __builtin_amdgcn_sched_barrier(0);
+            if (idx < X3C_NS) stamps[idx] = t;
+        }
+    };
+    stamp(0);
+#else
+    auto stamp = [&](int) {};
+#endif
 
     // ---- LDS-DMA addressing: input piece q of this wave = records 16 (wave + 4 i) .. +15, lane -> (record, slot) ----
     const int sub = lane >> 2, ps = lane & 3;
@@ -348,10 +373,13 @@ __global__ __launch_bounds__(64 * (TW / CWV), (TW / CWV) * OCC / 4) void conv_x3
     } else {
     for (int j = 0; j < nchunk; ++j) {
         if (j) __builtin_amdgcn_s_barrier();  // every wave is done reading the stage (its reads were waited for)
+        if ((DBG & 32) && j < X3C_NCH) stamp(1 + 3 * j);
         if (!(DBG & 1) || j == 0) dma(j);
         wait_vm0();
         __builtin_amdgcn_s_barrier();
+        if ((DBG & 32) && j < X3C_NCH) stamp(2 + 3 * j);
         if (ncw > 0 && !(DBG & 2)) compute(j);
+        if ((DBG & 32) && j < X3C_NCH) stamp(3 + 3 * j);
     }
     }
 
@@ -507,8 +535,270 @@ __global__ __launch_bounds__(64 * (TW / CWV), (TW / CWV) * OCC / 4) void conv_x3
         }
     }
     if (!ok && p.overflow) atomicOr(p.overflow, 1);
+#ifdef ESR_X3_EXPERIMENTS
+    if constexpr ((DBG & 32) != 0) {
+        stamp(X3C_NS - 1);
+        unsigned long long *sp = reinterpret_cast<unsigned long long *>(p.y1);
+        if (wave == 0 && lane == 0 && sp) {
+            for (int i = 0; i < X3C_NS; ++i) sp[(long long)blockIdx.x * X3C_NS + i] = stamps[i];
+        }
+    }
+#endif
 }
 
+#ifdef ESR_X3_EXPERIMENTS  // measured 4-12 % slower than the one-stage kernel (profiles/r5_x3d_ab.txt): ablation only
+// ---- 8-channel double-buffered form (x3d): N = 32 3×3 convs ------------------------------------------------------
+// The 12-column tile of four 3-column waves at three workgroups per CU (as conv_x3c_kernel<1, 3, 0, false, 3, false,
+// 12, 3>), but its K loop runs over 8-channel chunks in TWO LDS stages of 24 KB (the one-stage kernel's 48 KB): chunk
+// k+1's halo and weights are LDS-DMA'd while chunk k is computed, so a workgroup no longer alternates between waiting
+// for its loads and computing (stamped build, tools/x3c_stamps.py: 3.5 µs load wait + 2.7 µs compute per 16-channel
+// chunk at config 2).  A staged record is one pixel's (or one weight row's) 8 channels, split: [hi 8 | lo 8], 32 B
+// (the global split layout's 8-channel group).  With K = 8 channels the three products a·b = a_hi·b_hi + a_hi·b_lo +
+// a_lo·b_hi go on the K = 16 MFMA as
+//   cross terms  [a_lo | a_hi] · [b_hi ; b_lo]                 one MFMA per tap (9);
+//   hi·hi        [a_hi(col c) | a_hi(col c+1)] · [b_hi(d,0) ; b_hi(d,1)]  per tap row d (3), the taps (d,0) + (d,1);
+//                [a_hi(row 0) | a_hi(row 1)] · [b_hi(0,2) ; b_hi(1,2)]    at tap column 2 (1);
+//                [a_lo | a_hi] · [0 ; b_hi(2,2)]                           the last tap (1);
+// 14 MFMAs per output column and chunk (13.5 for the three products of 72 channel-taps: 3.7 % padding).  The same
+// products as the one-stage kernel, summed in another order (not bitwise equal to it; same fp32-level accuracy).
+// LDS images: column-major records as conv_x3c (halo record (hx, hy) at hx·34 + hy, weight record (t, n) at t·32 + n);
+// the two 16-B slots of a record are swapped when bit 3 of its row is set, which makes every ds_read_b128 lane group
+// conflict-free (rows m and m + 8 share a bank quad otherwise).
+constexpr int XD_REC = 32, XD_HX = 14, XD_HY = 34;
+constexpr int XD_IN_RECS = XD_HX * XD_HY;             // 476
+constexpr int XD_IN_PIECES = (XD_IN_RECS + 31) / 32;  // 15 one-KB LDS-DMA wave-instructions (32 records each)
+constexpr int XD_IN_B = XD_IN_PIECES * 1024;          // 15360
+constexpr int XD_W_PIECES = 9 * 32 / 32;              // 9
+constexpr int XD_STAGE = XD_IN_B + XD_W_PIECES * 1024;  // 24576
+constexpr int XD_PIECES = XD_IN_PIECES + XD_W_PIECES;   // 24
+constexpr int XD_NW = 4, XD_CW = 3, XD_KP = XD_PIECES / XD_NW;  // 6 pieces per wave and chunk
+static_assert(XD_PIECES % XD_NW == 0, "pieces per wave");
+static_assert(XD_NW * 32 * (32 + 4) * 4 <= 2 * XD_STAGE, "epilogue restage areas fit");
+
+__device__ __forceinline__ int xd_sw(int row) { return (row >> 3) & 1; }
+
+// one 16-byte LDS read at a run-time address (the caller waits with lgkm_wait)
+__device__ __forceinline__ f16x8 ds_read16_at(uint32_t a) {
+    f16x8 r;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(a));
+    return r;
+}
+
+__global__ __launch_bounds__(256, 3) void conv_x3d_kernel(X3cParams p) {
+    __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * XD_STAGE];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int hl = lane >> 5;
+    const int ml = lane & 31;
+    const int tile = p.xcd_map ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x;
+    const int tx = tile % p.tiles_x;
+    const int ty = tile / p.tiles_x;
+    const int x0 = tx * 12;
+    const int r0 = ty * CT;
+    const int tw = min(12, p.W - x0);
+    const int ncw = min(XD_CW, max(0, tw - XD_CW * wave));
+    const int rows_tot = p.B * (p.H + 2);
+    const long long rowp = (long long)(p.W + 2);
+    const long long pixb = 4LL * p.in_cp;
+    const int nk = p.cin >> 3;  // 8-channel chunks
+    const unsigned char *tile_in = p.in + ((long long)r0 * rowp + x0) * pixb;
+    const int ld = p.w_ld ? p.w_ld : 32;
+    const long long wcs = p.w_cstride ? p.w_cstride : 9LL * 32 * 64;  // bytes per 16-channel chunk of the packing
+
+    // LDS-DMA sources of this lane: piece q = wave + 4 i -> LDS record 32 q + lane / 2, physical slot lane & 1
+    unsigned src_off[XD_KP];  // halo: byte offset from tile_in (bit 0: zero page); weights: offset in a 16-ch chunk
+#pragma unroll
+    for (int i = 0; i < XD_KP; ++i) {
+        const int q = wave + XD_NW * i;
+        const int ps = lane & 1;
+        if (q < XD_IN_PIECES) {
+            const int r = 32 * q + (lane >> 1);
+            const int hx = r / XD_HY, hy = r - (r / XD_HY) * XD_HY;
+            const int s = ps ^ xd_sw(hy);
+            const bool v = r < XD_IN_RECS && r0 + hy < rows_tot && x0 + hx < p.W + 2;
+            src_off[i] = v ? (unsigned)((hy * rowp + hx) * pixb + 16 * s) : 1u;
+        } else {
+            const int rw = 32 * (q - XD_IN_PIECES) + (lane >> 1);
+            const int t = rw >> 5, n = rw & 31;
+            const int s = ps ^ xd_sw(n);
+            src_off[i] = (unsigned)((t * ld + p.w_roff + n) * 64 + 16 * s);
+        }
+    }
+    auto dma = [&](int k, int stg) {
+        unsigned char *base = lds + stg * XD_STAGE;
+        const unsigned char *wk = p.w + (long long)(k >> 1) * wcs + 32 * (k & 1);
+#pragma unroll
+        for (int i = 0; i < XD_KP; ++i) {
+            const int q = wave + XD_NW * i;
+            const unsigned o = src_off[i];
+            const void *src = q < XD_IN_PIECES ? ((o & 1u) ? (const void *)g_zero64 : (const void *)(tile_in + o + 32LL * k))
+                                                : (const void *)(wk + o);
+            __builtin_amdgcn_global_load_lds((glob_void *)src, (lds_void *)(base + q * 1024), 16, 0, 0);
+        }
+    };
+
+    f32x16 acc[XD_CW];
+#pragma unroll
+    for (int c = 0; c < XD_CW; ++c)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[c][r] = 0.f;
+
+    // fragment addresses (bytes, relative to a stage): halo record (hx, hy) of this wave's columns, weight record (t, n)
+    const int hb = XD_CW * wave * XD_HY;  // first halo record of this wave's columns
+    auto a_at = [&](int ic, int row, int slot) {
+        return (uint32_t)((hb + ic * XD_HY + row) * XD_REC + 16 * (slot ^ xd_sw(row)));
+    };
+    auto b_at = [&](int t, int slot) { return (uint32_t)(XD_IN_B + (t * 32 + ml) * XD_REC + 16 * (slot ^ xd_sw(ml))); };
+
+    auto compute = [&](int stg) {
+        const uint32_t sb = lds_addr(lds) + stg * XD_STAGE;
+        f16x8 zero = {};
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            // tap row d: cross-term A of the 5 halo columns, the hi-pair A of the 3 output columns, its weights
+            f16x8 ax[XD_CW + 2], ap[XD_CW], bx[3], bp, bs;
+#pragma unroll
+            for (int ic = 0; ic < XD_CW + 2; ++ic) ax[ic] = ds_read16_at(sb + a_at(ic, ml + d, 1 - hl));
+#pragma unroll
+            for (int c = 0; c < XD_CW; ++c) ap[c] = ds_read16_at(sb + a_at(c + hl, ml + d, 0));
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx) bx[dx] = ds_read16_at(sb + b_at(3 * d + dx, hl));
+            bp = ds_read16_at(sb + b_at(3 * d + hl, 0));
+            if (d == 2) bs = ds_read16_at(sb + b_at(8, 0));
+            lgkm_wait_arr<0>(ax);
+#pragma unroll
+            for (int c = 0; c < XD_CW; ++c) asm volatile("" : "+v"(ap[c]));
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx) asm volatile("" : "+v"(bx[dx]));
+            asm volatile("" : "+v"(bp));
+            if (d == 2) {
+                asm volatile("" : "+v"(bs));
+                if (!hl) bs = zero;
+            }
+#pragma unroll
+            for (int ic = 0; ic < XD_CW + 2; ++ic)
+#pragma unroll
+                for (int dx = 0; dx < 3; ++dx) {
+                    const int c = ic - dx;
+                    if (c >= 0 && c < XD_CW) acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax[ic], bx[dx], acc[c], 0, 0, 0);
+                }
+#pragma unroll
+            for (int c = 0; c < XD_CW; ++c) acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ap[c], bp, acc[c], 0, 0, 0);
+            if (d == 2) {
+#pragma unroll
+                for (int c = 0; c < XD_CW; ++c) acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax[c + 2], bs, acc[c], 0, 0, 0);
+            }
+        }
+        // tap column 2, rows 0 and 1: [a_hi(row 0) | a_hi(row 1)] · [b_hi(0,2) ; b_hi(1,2)]
+        f16x8 ar[XD_CW], br;
+#pragma unroll
+        for (int c = 0; c < XD_CW; ++c) ar[c] = ds_read16_at(sb + a_at(c + 2, ml + hl, 0));
+        br = ds_read16_at(sb + b_at(2 + 3 * hl, 0));
+        lgkm_wait_arr<0>(ar);
+        asm volatile("" : "+v"(br));
+#pragma unroll
+        for (int c = 0; c < XD_CW; ++c) acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ar[c], br, acc[c], 0, 0, 0);
+    };
+
+    if (nk > 0) dma(0, 0);
+    for (int k = 0; k < nk; ++k) {
+        wait_vm0();                    // this wave's pieces of chunk k have landed
+        __builtin_amdgcn_s_barrier();  // ... every wave's; and every wave is done with chunk k - 1's stage
+        if (k + 1 < nk) dma(k + 1, (k + 1) & 1);
+        if (ncw > 0) compute(k & 1);
+    }
+
+    // ---- epilogue (as conv_x3c_kernel's): each wave restages one output column at a time through its own LDS area
+    __builtin_amdgcn_s_barrier();
+    if (ncw <= 0) return;
+    constexpr int N = 32, EP_P = N + 4, CWk = XD_CW, NT = 1;
+    const esr_conv_out &o = p.o;
+    float *s_ep = reinterpret_cast<float *>(lds) + wave * 32 * EP_P;
+    constexpr int G = N / 8;
+    constexpr int ITEMS = 32 * G / 64;
+    const int HP = p.H + 2;
+    bool ok = true;
+    float bk[ITEMS][8];
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+        const int g = (lane + 64 * k) % G;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bk[k][e] = (8 * g + e < p.cout) ? p.bias[8 * g + e] : 0.f;
+    }
+#pragma unroll
+    for (int c = 0; c < CWk; ++c) {
+        if (c >= ncw) break;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = 8 * (r >> 2) + 4 * hl + (r & 3);
+            s_ep[m * EP_P + ml] = acc[c][r];
+        }
+        const int x = x0 + CWk * wave + c;  // interior column of the output pixel
+        if (o.out_planar) {
+            for (int it = lane; it < 32 * p.cout; it += 64) {
+                const int ch = it / 32, m = it % 32;
+                const int R = r0 + 1 + m;
+                const int b = R / HP, y = R - b * HP - 1;
+                if (R >= rows_tot || y < 0 || y >= p.H) continue;
+                const int oy = o.out_sy * y + o.out_oy, ox = o.out_sx * x + o.out_ox;
+                const long long opix = ((long long)b * (o.out_h + 2) + oy + 1) * (long long)(o.out_w + 2) + ox + 1;
+                float v = s_ep[m * EP_P + ch] * p.w_scale_inv + p.bias[ch];
+                v = epi(o, v, o.r1 ? split_at(o.r1, opix, o.r1_cp, o.r1_coff + ch) : 0.f, o.r2 ? split_at(o.r2, opix, o.r2_cp, o.r2_coff + ch) : 0.f);
+                o.out[(((long long)b * p.cout + ch) * o.out_h + oy) * o.out_w + ox] = v;
+            }
+        } else {
+            long long opix[ITEMS];
+            bool val[ITEMS];
+#pragma unroll
+            for (int k = 0; k < ITEMS; ++k) {
+                const int it = lane + 64 * k, m = it / G, g = it % G;
+                const int R = r0 + 1 + m;
+                const int b = R / HP, y = R - b * HP - 1;
+                const int oy = o.out_sy * y + o.out_oy, ox = o.out_sx * x + o.out_ox;
+                opix[k] = ((long long)b * (o.out_h + 2) + oy + 1) * (long long)(o.out_w + 2) + ox + 1;
+                val[k] = R < rows_tot && y >= 0 && y < p.H && 8 * g < p.cout;
+            }
+            float r1v[ITEMS][8], r2v[ITEMS][8];
+            if (o.r1) {
+#pragma unroll
+                for (int k = 0; k < ITEMS; ++k)
+                    if (val[k])
+                        load_group(reinterpret_cast<const unsigned char *>(o.r1) +
+                                       (opix[k] * o.r1_cp + o.r1_coff + 8 * ((lane + 64 * k) % G)) * 4, r1v[k]);
+            }
+            if (o.r2) {
+#pragma unroll
+                for (int k = 0; k < ITEMS; ++k)
+                    if (val[k])
+                        load_group(reinterpret_cast<const unsigned char *>(o.r2) +
+                                       (opix[k] * o.r2_cp + o.r2_coff + 8 * ((lane + 64 * k) % G)) * 4, r2v[k]);
+            }
+#pragma unroll
+            for (int k = 0; k < ITEMS; ++k) {
+                if (!val[k]) continue;
+                const int it = lane + 64 * k, m = it / G, g = it % G;
+                float v[8];
+                const f32x4 v0 = *reinterpret_cast<const f32x4 *>(s_ep + m * EP_P + 8 * g);
+                const f32x4 v1 = *reinterpret_cast<const f32x4 *>(s_ep + m * EP_P + 8 * g + 4);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { v[e] = v0[e]; v[e + 4] = v1[e]; }
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    v[e] = v[e] * p.w_scale_inv + bk[k][e];
+                    v[e] = epi(o, v[e], o.r1 ? r1v[k][e] : 0.f, o.r2 ? r2v[k][e] : 0.f);
+                }
+                ok &= store_group(reinterpret_cast<unsigned char *>(o.out) + (opix[k] * o.out_cp + o.out_coff + 8 * g) * 4, v);
+                if (o.out2)
+                    store_group(reinterpret_cast<unsigned char *>(o.out2) + (opix[k] * o.out2_cp + o.out2_coff + 8 * g) * 4, v);
+            }
+        }
+    }
+    if (!ok && p.overflow) atomicOr(p.overflow, 1);
+    (void)NT;
+}
+
+#endif  // ESR_X3_EXPERIMENTS (x3d)
 
 #ifdef ESR_X3_EXPERIMENTS  // spills at its register budget and runs 2-5x slower (r2 A/B): experiment library only
 // ---- warp-specialised persistent form --------------------------------------------------------------------------
@@ -904,7 +1194,7 @@ int x3c_launch(const X3cParams &p0, int taps_side, hipStream_t stream, int dbg) 
     }
 #endif
 #ifdef ESR_X3_EXPERIMENTS
-    if (dbg >= 256 && !n64 && taps_side == 3) {  // 12-column N = 32 kernel ablations: DBG = dbg >> 8
+    if (dbg >= 256 && dbg < 300 && !n64 && taps_side == 3) {  // 12-column N = 32 kernel ablations: DBG = dbg >> 8
         p.tiles_x = (p.W + 11) / 12;
         const dim3 grid12((unsigned)(p.tiles_x * p.tiles_y));
 #define X12(D) hipLaunchKernelGGL((conv_x3c_kernel<1, 3, D, false, 3, false, 12, 3>), grid12, block, 0, stream, p)
@@ -916,6 +1206,33 @@ int x3c_launch(const X3cParams &p0, int taps_side, hipStream_t stream, int dbg) 
         default: X12(0);
         }
 #undef X12
+        return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+    }
+#endif
+#ifdef ESR_X3_EXPERIMENTS
+    if (dbg == 303 && !n64 && taps_side == 3) {  // the 8-channel double-buffered form (conv_x3d_kernel)
+        p.tiles_x = (p.W + 11) / 12;
+        const dim3 grid12((unsigned)(p.tiles_x * p.tiles_y));
+        hipLaunchKernelGGL(conv_x3d_kernel, grid12, block, 0, stream, p);
+        return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+    }
+    if (dbg == 302 && !n64 && taps_side == 3) {  // the production 12-column N = 32 kernel with stamps (DBG 32)
+        p.tiles_x = (p.W + 11) / 12;
+        const dim3 grid12((unsigned)(p.tiles_x * p.tiles_y));
+        p.y1 = static_cast<float *>(g_x3c_stamps);
+        hipLaunchKernelGGL((conv_x3c_kernel<1, 3, 32, false, 3, false, 12, 3>), grid12, block, 0, stream, p);
+        return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
+    }
+    if ((dbg == 300 || dbg == 301) && !n64 && taps_side == 3) {  // N = 32 in wider tiles at two workgroups per CU:
+        // 18 columns (six 3-column waves, 62.5 KB LDS) / 24 columns (eight, 75.8 KB): fewer staged bytes per output
+        // pixel (108 / 98 B vs 127 B at 12 columns)
+        const int tw = dbg == 300 ? 18 : 24;
+        p.tiles_x = (p.W + tw - 1) / tw;
+        const dim3 gridw((unsigned)(p.tiles_x * p.tiles_y));
+        if (dbg == 300)
+            hipLaunchKernelGGL((conv_x3c_kernel<1, 3, 0, false, 3, false, 18, 2>), gridw, dim3(64 * 6), 0, stream, p);
+        else
+            hipLaunchKernelGGL((conv_x3c_kernel<1, 3, 0, false, 3, false, 24, 2>), gridw, dim3(64 * 8), 0, stream, p);
         return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
     }
 #endif
@@ -969,3 +1286,11 @@ int x3c_launch(const X3cParams &p0, int taps_side, hipStream_t stream, int dbg) 
     }
     return hipGetLastError() == hipSuccess ? ESR_OK : ESR_ELAUNCH;
 }
+
+#ifdef ESR_X3_EXPERIMENTS
+// variant 87's stamp buffer (X3C_NS u64 per workgroup of the launch; NULL: stamps not stored)
+extern "C" int esr_x3c_set_stamps(void *buf) {
+    g_x3c_stamps = buf;
+    return 0;
+}
+#endif
