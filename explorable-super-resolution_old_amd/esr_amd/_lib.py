@@ -138,7 +138,7 @@ ABLATION_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), 'exp_lib',
 ABLATION_SETTERS = ('esr_x3_set_kernel', 'esr_x3_set_tile_map', 'esr_x3_set_narrow', 'esr_x3_set_nsplit',
                     'esr_conv_set_tile', 'esr_cem_set_direct', 'esr_wgrad_set_kernel', 'esr_wgrad3_set_dma',
                     'esr_dconv_set_halo', 'esr_dconv_set_occ3', 'esr_dconv_set_cw16', 'esr_dconv_set_rows',
-                    'esr_axpby_set_rows')
+                    'esr_axpby_set_rows', 'esr_x3c_set_stamps')
 
 _lib = None
 
@@ -167,7 +167,7 @@ def bind(path):
     if hasattr(lib, 'esr_x3_set_kernel'):  # the ablation library
         for name in ABLATION_SETTERS:
             fn = getattr(lib, name)
-            fn.argtypes = [c_int]
+            fn.argtypes = [c_void_p] if name == 'esr_x3c_set_stamps' else [c_int]  # (a stamp buffer; the rest: ints)
             fn.restype = c_int
         # same-box A/B runs of whole benchmarks (tools/gpu_ab_env.sh with ESR_AMD_LIB=exp_lib/libesr_exp.so)
         if os.environ.get('ESR_X3_NSPLIT') in ('0', '1'):
