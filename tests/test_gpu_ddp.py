@@ -9,7 +9,8 @@ nn.DataParallel over the GPUs (models/networks.py:99-101,125-126) with batch_siz
   ~1e-7 relative in the weights) — except the biases of the discriminator convs that feed a BatchNorm and the BN
   running means: their gradient is analytically zero, its computed value is the rounding noise of a cancelling sum,
   and Adam's m / sqrt(v) turns any change in that noise into a learning-rate-sized step (observed 1e-3..6e-1
-  relative; bounded here by lr per step, and for the running means, which carry those biases, by 1e-3 relative);
+  relative; bounded here by lr per step, and for the running means, which carry those biases, by 1e-3 relative or
+  the same absolute bound);
 * different batches per rank: the ranks end with the same parameters and took the same generator_step decisions.
 """
 import hashlib
@@ -167,6 +168,11 @@ def test_ddp_two_ranks_on_the_gpu(cfg_name):
             assert np.abs(a - b).max() <= 2 * lr * n_steps, (k, np.abs(a - b).max())
             continue
         rel = float(np.linalg.norm(a - b) / max(np.linalg.norm(a), 1e-30))
+        if k.endswith('running_mean'):
+            # a running mean averages (momentum-weighted) batch means that carry those biases' Adam noise: the same
+            # absolute bound, or 1e-3 relative
+            assert rel <= 1e-3 or np.abs(a - b).max() <= 2 * lr * n_steps, (k, rel, np.abs(a - b).max())
+            continue
         assert rel <= 1e-3, (k, rel)
         if not k.endswith('running_mean'):
             worst = max(worst, (rel, k))
