@@ -375,12 +375,13 @@ def main():
     # over the UNION of their HIP-event intervals, i.e. the MFMA rate the GPU sustained while any of them ran; the
     # per-tag lines beside it give each tag's FLOPs over the union of its own intervals and its mean event duration.
     per = {}
-    for tag, flops, t_a, t_b in engine.profile_intervals(prof, origin):
-        a = per.setdefault(tag, [0, 0.0, 0.0, []])
+    for tag, flops, t_a, t_b, nbytes in engine.profile_intervals(prof, origin):
+        a = per.setdefault(tag, [0, 0.0, 0.0, [], 0.0])
         a[0] += 1
         a[1] += flops
         a[2] += t_b - t_a
         a[3].append((t_a, t_b))
+        a[4] += nbytes
     origin.close()
     union = {k: engine.union_ms(v[3]) for k, v in per.items()}
     busy = engine.union_ms([iv for v in per.values() for iv in v[3]])
@@ -407,6 +408,7 @@ def main():
                      'achieved': round(achieved, 2), 'peak': round(peak, 1), 'peak_basis': peak_note,
                      'unit': 'TFLOP/s', 'frac': round(achieved / peak, 4), 'traffic': None,
                      'flops_per_launch': fl_all / n_all, 'launches_per_step': n_all // n_prof,
+                     'algorithmic_bytes_per_launch': sum(v[4] for v in per.values()) / n_all,
                      'profiled_steps': n_prof,
                      'union_us_per_launch': round(busy / n_all * 1e3, 2), 'streams': streams,
                      'timing': 'achieved = FLOPs of all launches / union of their HIP-event intervals, events on '
@@ -423,6 +425,7 @@ def main():
     traffic = pmc_traffic(set(per))
     if traffic is not None:
         rec['roofline']['traffic'] = traffic[0]
+        rec['roofline']['traffic_over_algorithmic'] = round(traffic[0] / rec['roofline']['algorithmic_bytes_per_launch'], 3)
         rec['roofline']['traffic_source'] = traffic[1]
         rec['roofline']['rocprof_union_us_per_launch'] = traffic[2]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -113,10 +113,10 @@ def lower_act_scale(net):
                   % (type(net).__name__, old, new), RuntimeWarning, stacklevel=2)
 
 
-def _prof_begin(prof, tag, flops):
+def _prof_begin(prof, tag, flops, nbytes=0.0):
     start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     start.record()
-    prof.append((tag, flops, start, end))
+    prof.append((tag, flops, start, end, nbytes))
     return end
 
 
@@ -566,8 +566,8 @@ class _Recorder:
         self.ops, self.tags, self.keep = [], [], []
         self._tag = None
 
-    def tag(self, name, flops):
-        self._tag = (name, flops)
+    def tag(self, name, flops, nbytes=0.0):
+        self._tag = (name, flops, nbytes)
 
     def _add(self, kind, p, i, f=(), o=None):
         op = _lib.EsrOp()
@@ -682,7 +682,7 @@ def profile_records(prof):
                 if tags[k] is not None:
                     yield tags[k][0], tags[k][1], ms[k]
         else:
-            tag, flops, start, end = entry
+            tag, flops, start, end = entry[:4]
             yield tag, flops, start.elapsed_time(end)
 
 
@@ -711,7 +711,7 @@ class ProfileOrigin:
 
 
 def profile_intervals(prof, origin):
-    """(tag, flops, start_ms, end_ms) of every profiled launch in `prof`, times from `origin` (a recorded
+    """(tag, flops, start_ms, end_ms, algorithmic bytes) of every profiled launch in `prof`, times from `origin` (a recorded
     ProfileOrigin): launches of several streams overlap, so a rate over them divides by the union of their intervals,
     not by the sum of their durations.  Frees the op-list timers like profile_records."""
     lib = _lib.load()
@@ -723,10 +723,10 @@ def profile_intervals(prof, origin):
             lib.esr_timer_destroy(timer)
             for k in range(n):
                 if tags[k] is not None:
-                    yield tags[k][0], tags[k][1], t[k], t[k + 1]
+                    yield tags[k][0], tags[k][1], t[k], t[k + 1], tags[k][2]
         else:
-            tag, flops, start, end = entry
-            yield tag, flops, origin.event.elapsed_time(start), origin.event.elapsed_time(end)
+            tag, flops, start, end, nbytes = entry
+            yield tag, flops, origin.event.elapsed_time(start), origin.event.elapsed_time(end), nbytes
 
 
 def union_ms(intervals):
@@ -929,10 +929,14 @@ def _forward(net, x, cem, precision, train_ws=None, rec=None):
         ev = None
         # timing tags: the N = 32 / 64 tile classes, and HR_conv1 (cout 3: the narrow-N kernel in x3) on its own
         ntag = '%sconv3x3_n%d' % (tagp, 3 if cout <= 3 else (32 if cout <= 32 else 64))
+        # algorithmic HBM bytes: the input channels read once, the outputs (and residuals) once, the weights once
+        # (4 bytes per value: fp32, or an f16 hi/lo pair)
+        per_px = cin + cout * (1 + bool(o.r1) + bool(o.r2) + bool(o.out2))
+        nbytes = 4.0 * (Bn * h_ * w_ * per_px + 9 * cin * cout)
         if rec is not None:
-            rec.tag(ntag, 2.0 * Bn * h_ * w_ * 9 * cin_ref * cout)
+            rec.tag(ntag, 2.0 * Bn * h_ * w_ * 9 * cin_ref * cout, nbytes)
         elif prof is not None:
-            ev = _prof_begin(prof, ntag, 2.0 * Bn * h_ * w_ * 9 * cin_ref * cout)
+            ev = _prof_begin(prof, ntag, 2.0 * Bn * h_ * w_ * 9 * cin_ref * cout, nbytes)
         if x3:
             wx, scale = cw.x3()
             if rec is not None:  # the op list holds wx's pointer: keep it alive (train_x3 may swap cw._x3 later)
@@ -977,10 +981,11 @@ def _forward(net, x, cem, precision, train_ws=None, rec=None):
             o = _conv_out(dst, dcp, dcoff, f * sh, f * sw, True, sy=f, sx=f, oy=py, ox=px)
             ev = None  # reference FLOPs: a 3×3 conv at f× resolution, 1/f² of it per phase
             fl = 2.0 * Bn * (f * sh) * (f * sw) * 9 * 64 * 64 / (f * f)
+            nb_ = 4.0 * (2 * Bn * sh * sw * 64 + 4 * 64 * 64)  # its LR source, its quarter of the output, weights
             if rec is not None:
-                rec.tag(tagp + 'upconv2x_phase', fl)
+                rec.tag(tagp + 'upconv2x_phase', fl, nb_)
             elif prof is not None:
-                ev = _prof_begin(prof, tagp + 'upconv2x_phase', fl)
+                ev = _prof_begin(prof, tagp + 'upconv2x_phase', fl, nb_)
             if x3:
                 wx, scale = cw.x3()
                 if rec is not None:
@@ -1007,17 +1012,19 @@ def _forward(net, x, cem, precision, train_ws=None, rec=None):
         w1x, s1 = pk.hr1.x3()
         fl0 = 2.0 * Bn * HH * WW * 9 * (nl + 64) * 64
         fl1 = 2.0 * Bn * HH * WW * 9 * (nl + 64) * 3
+        nb0 = 4.0 * (Bn * HH * WW * (zc + 64 + 32) + 9 * (zc + 64) * 64)  # HR0 in, 32 partial products out
+        nb1 = 4.0 * Bn * HH * WW * (32 + 3)
         if rec is not None:
             rec.keep += [w0x, w1x]
-            rec.tag(tagp + 'hr_conv0_hr1', fl0)
-        ev = _prof_begin(prof, tagp + 'hr_conv0_hr1', fl0) if rec is None and prof is not None else None
+            rec.tag(tagp + 'hr_conv0_hr1', fl0, nb0)
+        ev = _prof_begin(prof, tagp + 'hr_conv0_hr1', fl0, nb0) if rec is None and prof is not None else None
         _lib.check(lib.esr_hr_convs_x3(HR0.data_ptr(), Bn, HH, WW, hcp, zc, w0x.data_ptr(), pk.hr0.bias_s.data_ptr(),
                                        s0, w1x.data_ptr(), ws.Y.data_ptr(), ovf, stream), 'esr_hr_convs_x3')
         if ev is not None:
             ev.record()
         if rec is not None:
-            rec.tag(tagp + 'hr1_sum', fl1)
-        ev = _prof_begin(prof, tagp + 'hr1_sum', fl1) if rec is None and prof is not None else None
+            rec.tag(tagp + 'hr1_sum', fl1, nb1)
+        ev = _prof_begin(prof, tagp + 'hr1_sum', fl1, nb1) if rec is None and prof is not None else None
         _lib.check(lib.esr_hr1_sum(ws.Y.data_ptr(), Bn, HH, WW, pk.hr1.bias.data_ptr(), 1.0 / (s1 * A),
                                    gen.data_ptr(), stream), 'esr_hr1_sum')
         if ev is not None:
