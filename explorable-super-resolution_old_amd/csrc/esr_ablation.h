@@ -38,7 +38,8 @@ int esr_x3_set_tile_map(int32_t mode);
 int esr_x3_set_narrow(int32_t on);
 /* N split of under-filled N = 64 x3 convs (round 3): 0 (product) / 1 = two N = 32 launches (bitwise identical). */
 int esr_x3_set_nsplit(int32_t on);
-/* esr_axpby_gs: 1 = row-walking kernel (product), 0 = one thread per 8-channel group (round 3). */
+/* esr_axpby_gs: 2 = row-walking kernel with 4 items in flight per thread (product), 1 = one item, 0 = one thread per
+ * 8-channel group (round 3). */
 int esr_axpby_set_rows(int32_t on);
 /* Exact-fp32 conv tile rows: 0 (product: automatic), 4 or 8 (identical results). */
 int esr_conv_set_tile(int32_t rows);

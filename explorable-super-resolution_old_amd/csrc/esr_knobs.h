@@ -21,7 +21,8 @@
     X(g_dconv_cw16, 1)   /* x3 halo kernel with 16-column tiles on narrow grids                                    */ \
     X(g_dconv_occ3, 1)   /* x3 halo kernel at three workgroups per CU where its LDS allows                         */ \
     X(g_dconv_rows, 0)   /* tap-row discriminator weight-gradient kernel (slower at config 3)                      */ \
-    X(g_axpby_rows, 1)   /* esr_axpby_gs on the row-walking kernel (0: one thread per 8-channel group)             */
+    X(g_axpby_rows, 2)   /* esr_axpby_gs: 1 row-walking kernel, 2 the same with 4 items in flight per thread, 0 one */ \
+                         /* thread per 8-channel group                                                            */
 
 #ifdef ESR_X3_EXPERIMENTS
 #define ESR_KNOB_DECL(name, v) extern int name;

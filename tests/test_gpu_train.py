@@ -434,14 +434,16 @@ def test_fused_gradient_amax_bitwise(gpu_device):
         TE.AMAX_FUSED = prev
 
 
-def test_axpby_rows_kernel_bitwise(gpu_device, ablation_lib):
-    """esr_axpby_gs on the row-walking kernel (product) against the one-thread-per-8-channel-group kernel (ablation
-    variant): the same results, bit for bit, in every operand form the x3 backward uses (fp32 / split-f16 in and out,
-    with and without x2, an overflow flag)."""
+@pytest.mark.parametrize('B,H,W', [(2, 9, 13), (1, 3, 300)])
+def test_axpby_rows_kernel_bitwise(gpu_device, ablation_lib, B, H, W):
+    """esr_axpby_gs on the row-walking kernel with 4 items in flight per thread (product, knob 2) and with one (knob
+    1) against the one-thread-per-8-channel-group kernel (knob 0): the same results, bit for bit, in every operand form
+    the x3 backward uses (fp32 / split-f16 in and out, with and without x2, an overflow flag), including rows whose
+    item count is not a multiple of the 4 x 256 a block covers per pass (W = 13 and W = 300)."""
     import ctypes
     from esr_amd import engine
     lib = ablation_lib
-    B, H, W, cp = 2, 9, 13, 72
+    cp = 72
     g = torch.Generator(device='cpu').manual_seed(5)
     amax = torch.tensor([0.0], device=gpu_device)
     amax.fill_(37.5)
@@ -456,7 +458,7 @@ def test_axpby_rows_kernel_bitwise(gpu_device, ablation_lib):
     try:
         for o_split, x1, x1s, x2, x2s, o_cp, C in forms:
             outs = []
-            for rows in (1, 0):
+            for rows in (2, 1, 0):
                 lib.esr_axpby_set_rows(rows)
                 out = torch.zeros(B, H + 2, W + 2, o_cp, device=gpu_device)
                 ovf = torch.zeros(1, dtype=torch.int32, device=gpu_device)
@@ -467,9 +469,11 @@ def test_axpby_rows_kernel_bitwise(gpu_device, ablation_lib):
                 assert _lib_check == 0
                 torch.cuda.synchronize()
                 outs.append((out, ovf))
-            assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1]), (o_split, x1s, x2s, C)
+            for k in (1, 2):
+                assert torch.equal(outs[0][0], outs[k][0]) and torch.equal(outs[0][1], outs[k][1]), (o_split, x1s, x2s,
+                                                                                                    C, k)
     finally:
-        lib.esr_axpby_set_rows(1)
+        lib.esr_axpby_set_rows(2)
 
 
 @pytest.mark.parametrize('latent', [False, True])
