@@ -224,6 +224,9 @@ def reference_parity(dev):
     return out
 
 
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8 TB/s; 6.3 TB/s measured by a float4 copy)
+
+
 def pmc_traffic(tags):
     """HBM bytes per launch, launch-weighted over the kernel tags `tags`, from the committed rocprofv3 PMC passes
     (profiles/pmc_latest.json, made by tools/prof_summary.py from separate --pmc FETCH_SIZE / WRITE_SIZE runs of this
@@ -426,6 +429,17 @@ def main():
     if traffic is not None:
         rec['roofline']['traffic'] = traffic[0]
         rec['roofline']['traffic_over_algorithmic'] = round(traffic[0] / rec['roofline']['algorithmic_bytes_per_launch'], 3)
+    # the same launches against the HBM roofline (north_star's target is stated there): measured HBM bytes per launch
+    # (PMC) and the algorithmic minimum, each over the effective launch time (union / launches), vs 8 TB/s
+    t_launch = busy / n_all / 1e3  # s
+    alg = rec['roofline']['algorithmic_bytes_per_launch']
+    rec['roofline']['hbm'] = {
+        'peak_GBps': HBM_PEAK_GBPS, 'flop_per_byte_algorithmic': round(fl_all / n_all / alg, 1),
+        'ridge_flop_per_byte': round(peak * 1e12 / (HBM_PEAK_GBPS * 1e9), 1),
+        'algorithmic_GBps': round(alg / t_launch / 1e9, 1), 'algorithmic_frac': round(alg / t_launch / 1e9 / HBM_PEAK_GBPS, 4)}
+    if traffic is not None:
+        rec['roofline']['hbm']['measured_GBps'] = round(traffic[0] / t_launch / 1e9, 1)
+        rec['roofline']['hbm']['measured_frac'] = round(traffic[0] / t_launch / 1e9 / HBM_PEAK_GBPS, 4)
         rec['roofline']['traffic_source'] = traffic[1]
         rec['roofline']['rocprof_union_us_per_launch'] = traffic[2]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
