@@ -886,4 +886,6 @@ class _GeneratorFn(torch.autograd.Function):
 
 def generator_forward_train(net, x, cem):
     params = E.param_list(net)
+    if not any(p.requires_grad for p in params):  # a frozen generator (Z optimisation): only the input gradient, and
+        return _GeneratorFn.apply(x, net, cem)     # no 702-input autograd node (~0.5 ms of host time per forward)
     return _GeneratorFn.apply(x, net, cem, *params)
