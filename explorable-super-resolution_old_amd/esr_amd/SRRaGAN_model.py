@@ -580,7 +580,13 @@ class SRRaGANModel:
             self.var_H, self.var_ref = self.CEM_net.HR_unpadder(self.var_H), self.CEM_net.HR_unpadder(self.var_ref)
         static_Z = self.GetLatent() if self.latent_input is not None else None
         self.ConcatLatent(LR_image=self.var_L, latent_input=static_Z)
-        self.fake_H = self.netG(self.model_input)
+        # single-process: the generator's training forward takes the optimiser's flat parameter as its one autograd
+        # input (its backward returns the flat gradient: train_engine.generator_forward_train) instead of 702 tensors
+        self._rrdb._esr_flat_fwd = self.optimizer_G if _world() == 1 and G_grads_retained else None
+        try:
+            self.fake_H = self.netG(self.model_input)
+        finally:
+            self._rrdb._esr_flat_fwd = None
         if self.CEM_net is not None:
             self.fake_H = self.CEM_net.HR_unpadder(self.fake_H)
         # ---- D step ----

@@ -50,6 +50,9 @@ HR1_DFIRST = os.environ.get('ESR_HR1_DFIRST', '1') != '0'
 # x3 backward: each RRDB's closing trunk-gradient add also takes the next RRDB's gradient max (esr_axpby_gs_amax: one
 # pass over the trunk gradient fewer per RRDB; bitwise the same scale); '0' = a separate esr_grad_amax (A/B)
 AMAX_FUSED = os.environ.get('ESR_AMAX_FUSED', '1') != '0'
+# SRRaGANModel's training forward with the generator optimiser's flat parameter as its one autograd input (the
+# backward returns the flat gradient); '0' = the 702 parameters as inputs (A/B)
+FLAT_FWD = os.environ.get('ESR_FLAT_FWD', '1') != '0'
 _SIDE = {}
 
 
@@ -835,6 +838,8 @@ class _GeneratorFn(torch.autograd.Function):
         ctx.net, ctx.cem, ctx.ws, ctx.latent, ctx.M, ctx.split = net, cem, ws, latent, ws.sf * m, split
         ctx.act_scale = A if split else 1.0  # (after an fp32 rerun the activations are unscaled)
         ctx.params = params
+        ctx.flat_fg = getattr(net, '_esr_flat_fwd', None) if len(params) == 1 and \
+            getattr(getattr(net, '_esr_flat_fwd', None), 'flat', None) is params[0] else None
         ctx.owner = _Owner()
         ws.owner = weakref.ref(ctx.owner)
         return out.clone() if graphed else out
@@ -871,6 +876,13 @@ class _GeneratorFn(torch.autograd.Function):
             dx = dx.clone() if dx is not None else None
         # the generator's FlatAdam, set by SRRaGANModel.optimize_parameters only around its generator loss's
         # .backward() (every parameter's AccumulateGrad runs, no per-parameter hooks wait); None everywhere else
+        if ctx.flat_fg is not None:  # the flat parameter was the input (generator_forward_train)
+            ctx.owner.done = True
+            if flat is not None:
+                ctx.flat_fg._sync_views()  # (parameters / gradients replaced since the last bind are re-attached first)
+                if not ctx.flat_fg.accepts_flat_grad(bp.params):
+                    raise RuntimeError('esr_amd: flat gradient layout differs from the optimiser\'s buffer')
+            return (dx, None, None, flat)
         fg = getattr(ctx.net, '_esr_flat_grad', None)
         if flat is not None and fg is not None and all(ctx.needs_input_grad[3:]) and fg.accepts_flat_grad(bp.params):
             # flat is laid out as the optimiser's buffer: one add instead of 702 per-parameter accumulations (the
@@ -888,4 +900,10 @@ def generator_forward_train(net, x, cem):
     params = E.param_list(net)
     if not any(p.requires_grad for p in params):  # a frozen generator (Z optimisation): only the input gradient, and
         return _GeneratorFn.apply(x, net, cem)     # no 702-input autograd node (~0.5 ms of host time per forward)
+    fg = getattr(net, '_esr_flat_fwd', None)  # SRRaGANModel's own step, single-process: a FlatAdam over `params`
+    if FLAT_FWD and fg is not None and fg.flat.requires_grad and fg.accepts_flat_grad(params) and \
+            all(p.requires_grad for p in params):
+        # one autograd input, the optimiser's flat parameter: the backward returns the flat gradient (laid out as the
+        # flat buffer) and autograd adds it into flat.grad, of which every parameter's .grad is a view
+        return _GeneratorFn.apply(x, net, cem, fg.flat)
     return _GeneratorFn.apply(x, net, cem, *params)
