@@ -26,6 +26,7 @@ zero from allocation and never written.
 """
 import ctypes
 import math
+import operator
 import os
 import warnings
 
@@ -295,7 +296,7 @@ class GatherPlan:
         fl = getattr(self.params[0], '_esr_flat', None)
         if fl is None or fl.numel() != self.N:
             return None
-        ptrs = [p.data_ptr() for p in self.params]
+        ptrs = list(map(_DATA_PTR, self.params))
         ok = self.__dict__.get('_flat_ok')
         if ok is not None and ok[0] is fl and ok[1] == ptrs:
             return fl.detach()
@@ -448,22 +449,28 @@ class _Packed:
 def param_list(m):
     """list(m.parameters()), cached on the module: walking RRDB-23's module tree for its 702 parameters costs ~5 ms
     of host time per call, and a training step needs the list several times.  The cache is revalidated on every
-    call (each cached (module, name) slot must still hold the same Parameter object, ~0.2 ms); adding new submodules
-    after the first call is not detected."""
+    call (each cached (module, name) slot must still hold the same Parameter object: ~0.09 ms for RRDB-23 as one
+    C-level map, 0.13 as a generator expression); adding new submodules after the first call is not detected."""
     c = m.__dict__.get('_esr_plist')
     if c is not None:
-        slots, plist = c
-        if all(mod._parameters.get(n) is q for (mod, n), q in zip(slots, plist)):
+        mods, names, plist = c
+        if all(map(operator.is_, map(dict.get, map(_PARAMS, mods), names), plist)):
             return plist
-    slots, plist, seen = [], [], set()
+    mods, names, plist, seen = [], [], [], set()
     for mod in m.modules():
         for n, q in mod._parameters.items():
             if q is not None and id(q) not in seen:
                 seen.add(id(q))
-                slots.append((mod, n))
+                mods.append(mod)
+                names.append(n)
                 plist.append(q)
-    m.__dict__['_esr_plist'] = (slots, plist)
+    m.__dict__['_esr_plist'] = (mods, names, plist)
     return plist
+
+
+_PARAMS = operator.attrgetter('_parameters')
+_VERSION = operator.attrgetter('_version')
+_DATA_PTR = torch.Tensor.data_ptr
 
 
 def _param_key(net):
@@ -479,14 +486,14 @@ def _keys(net):
     pass over the parameter list.  Parameters bound to a FlatAdam buffer (flat_optim.py) change when the buffer is
     updated in place, which bumps the buffer's version counter, not theirs."""
     ps = param_list(net)
-    ptrs = [p.data_ptr() for p in ps]
+    ptrs = list(map(_DATA_PTR, ps))
     c = net.__dict__.get('_esr_skey')  # the shapes are re-read only when a pointer changed (~0.5 ms per call saved)
     if c is not None and c[0] is ps and c[1] == ptrs:
         sk = c[2]
     else:
         sk = tuple(zip(ptrs, [p.shape for p in ps]))
         net.__dict__['_esr_skey'] = (ps, ptrs, sk)
-    vk = [tuple(ptrs), tuple([p._version for p in ps])]
+    vk = [tuple(ptrs), tuple(map(_VERSION, ps))]
     fl = getattr(ps[0], '_esr_flat', None) if ps else None
     if fl is not None:
         vk.append((id(fl), fl._version))
