@@ -446,7 +446,8 @@ def test_x3_ring_kernel_bitwise_equals_classic(gpu_device, ablation_lib, cin, co
     """The N<=32 ring kernels (two tiles per workgroup, 3-deep LDS-DMA ring, counted vmcnt; and the persistent variant
     that streams several tile pairs per workgroup with a per-wave epilogue) run the classic kernel's MFMA sequence per
     accumulator: outputs, residual epilogue and out2 must agree bit for bit, including odd tile counts (the second tile
-    of the last pair is beyond the batch) and partial column tiles."""
+    of the last pair is beyond the batch) and partial column tiles (W = 148 and 1: a 4- and a 1-column last tile of the
+    default 12-column kernel)."""
     lib = _lib.load()
     cp = cin + 8
     xs = engine.to_split(_padded(B, H, W, cp, cin, gpu_device, 21))
@@ -483,10 +484,11 @@ def test_x3_ring_kernel_bitwise_equals_classic(gpu_device, ablation_lib, cin, co
     assert normwise_rel(_nchw(engine.from_split(outs[1][0]), 8, 8 + cout), ref) < 1e-5
 
 
-@pytest.mark.parametrize('cin,B,H,W', [(192, 3, 21, 70), (72, 1, 5, 9)])
+@pytest.mark.parametrize('cin,B,H,W', [(192, 3, 21, 70), (72, 1, 5, 9), (192, 3, 21, 76), (64, 2, 9, 4)])
 def test_x3_n64_explicit_reads_bitwise(gpu_device, ablation_lib, cin, B, H, W):
     """The N = 64 classic kernel with explicit counted-wait fragment reads (default) against the same kernel with the
-    compiler-scheduled reads (esr_x3_set_kernel 20): same MFMA order per accumulator, so bit for bit."""
+    compiler-scheduled reads (esr_x3_set_kernel 20): same MFMA order per accumulator, so bit for bit.  W = 76 and 4
+    end in a 4-column partial tile of the default 12-column kernel."""
     lib = _lib.load()
     cp = cin + 8
     xs = engine.to_split(_padded(B, H, W, cp, cin, gpu_device, 31))
@@ -609,7 +611,7 @@ def test_conv3x3_x3_planar_output(gpu_device, variant, request):
 
 
 @pytest.mark.parametrize('variant', [1, 24])  # column-tile kernel (default), classic kernel
-@pytest.mark.parametrize('H,W', [(6, 9), (16, 40), (37, 21)])
+@pytest.mark.parametrize('H,W', [(6, 9), (16, 40), (37, 21), (5, 36), (3, 4)])  # 36, 4: a 4-column last tile
 def test_upconv2x_phases_x3(gpu_device, H, W, variant, request):
     lib = _lib.load() if variant == 1 else request.getfixturevalue('ablation_lib')
     if variant != 1:

@@ -7,7 +7,9 @@ later chunks' load waits (B - A), compute (C - B), the barrier before the next c
 epilogue; and how the workgroups' start times spread over the launch (rounds).  Only shares mean anything: the
 stamps' waits forbid overlaps the real kernel has (MI355X guide §7, in-kernel stamps).
 
-    ESR_AMD_LIB=exp_lib/libesr_exp.so python3 tools/x3c_stamps.py [B:H:cin ...]   (default 32:148:128 16:96:128 8:172:128)
+    ESR_AMD_LIB=exp_lib/libesr_exp.so python3 tools/x3c_stamps.py [B:H:cin[:W] ...]   (default 32:148:128 16:96:128 8:172:128)
+
+The last lines compare the workgroups of the last column strip (partial when W is no multiple of 12) with the rest.
 """
 import ctypes
 import os
@@ -32,8 +34,10 @@ def main():
     ovf = torch.zeros(1, dtype=torch.int32, device=dev)
     shapes = sys.argv[1:] or ['32:148:128', '16:96:128', '8:172:128']
     for spec in shapes:
-        B, H, cin = (int(v) for v in spec.split(':'))
-        W, cout, cp = H, 32, 192
+        f = [int(v) for v in spec.split(':')]
+        B, H, cin = f[:3]
+        W = f[3] if len(f) > 3 else H
+        cout, cp = 32, 192
         g = torch.Generator(device='cpu').manual_seed(cin)
         x = torch.zeros(B, H + 2, W + 2, cp)
         x[:, 1:-1, 1:-1, :cin] = torch.rand(B, H, W, cin, generator=g) * 2 - 1
@@ -91,6 +95,12 @@ def main():
         }
         tot = wg.sum()
         print('B=%d %dx%d cin=%d: %d workgroups; production %.1f us, stamped build %.1f us ' % (B, H, W, cin, ntiles, t_prod, t_diag), flush=True)
+        tiles_x = (W + 11) // 12
+        b = np.arange(ntiles)  # stamps are per blockIdx; its tile under the XCD map (esr_conv_x3c.hip xcd_tile)
+        x, l, q, r = b % 8, b // 8, ntiles // 8, ntiles % 8
+        tile = np.where(x < r, x * (q + 1) + l, r * (q + 1) + (x - r) * q + l)
+        tx = tile % tiles_x
+        last = tx == tiles_x - 1
         for k, v in parts.items():
             print('   %-38s %5.1f %%   (%.2f us per workgroup)' % (k, 100 * v / tot, v / ntiles / clk / 1e3))
         rel = (t0 - t0.min()) / span
@@ -99,6 +109,10 @@ def main():
         print('   mean workgroup duration %.1f us; per chunk: load wait %.2f us, compute %.2f us (chunks 1..%d)'
               % (wg.mean() / clk / 1e3, (Bq[:, 1:] - A[:, 1:]).mean() / clk / 1e3,
                  (C[:, 1:] - Bq[:, 1:]).mean() / clk / 1e3, nch - 1), flush=True)
+        for name, m in (('last strip', last), ('other strips', ~last)):
+            print('   %-12s workgroups %4d: duration %.2f us, load wait %.2f, compute %.2f, epilogue %.2f us' % (
+                name, m.sum(), wg[m].mean() / clk / 1e3, (Bq[m][:, 1:] - A[m][:, 1:]).mean() / clk / 1e3,
+                (C[m][:, 1:] - Bq[m][:, 1:]).mean() / clk / 1e3, (tend[m] - C[m][:, -1]).mean() / clk / 1e3), flush=True)
 
 
 if __name__ == '__main__':
