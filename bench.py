@@ -61,6 +61,7 @@ def parse():
     ap.add_argument('--no-legs', action='store_true', help='skip the extra legs (exact-fp32 C2, C3/C4 training step, '
                     'C5 Z-optimisation iteration)')
     ap.add_argument('--leg-steps', type=int, default=10)
+    ap.add_argument('--host-io-steps', type=int, default=3, help='steps of the PCIe-inclusive variant (host_io; 0: skip)')
     ap.add_argument('--x3-kernel', type=int, default=None, help='esr_x3_set_kernel variant (A/B: needs the ablation '
                     'library, ESR_AMD_LIB=exp_lib/libesr_exp.so; default automatic)')
     ap.add_argument('--profile-steps', type=int, default=2, help='timed steps (the last ones) that carry per-launch HIP '
@@ -264,6 +265,27 @@ def _timed(fn, steps, dev, world):
     return dt
 
 
+def host_io(model, x, out, args, dev, world):
+    """The headline step with its batch handed over in host memory, as the reference's feed_data / get_current_visuals
+    do (SRRaGAN_model.py feed_data .to(device), util.tensor2img .cpu()): pinned LR batch -> device, forward, HR output ->
+    pinned host, all on the step's stream, timed like the headline (barrier + synchronize, max over ranks).  The C-ABI
+    boundary itself takes device buffers, so this is never `value`."""
+    xh = torch.empty(x.shape, dtype=x.dtype, pin_memory=True).copy_(x.cpu())
+    oh = torch.empty(out.shape, dtype=out.dtype, pin_memory=True)
+
+    def step():
+        xd = xh.to(dev, non_blocking=True)
+        oh.copy_(model(xd), non_blocking=True)
+    with torch.no_grad():
+        step()
+        dt = _timed(step, args.host_io_steps, dev, world)
+    hr = 4 * args.lr_size
+    return {'value': round(world * args.batch * hr * hr * args.host_io_steps / dt / 1e6, 3), 'unit': 'HR Mpixels/s',
+            'ms_per_step': round(dt / args.host_io_steps * 1e3, 2), 'steps': args.host_io_steps,
+            'h2d_MB_per_step': round(xh.numel() * 4 / 1e6, 2), 'd2h_MB_per_step': round(oh.numel() * 4 / 1e6, 2),
+            'note': 'PCIe-inclusive: pinned host LR batch in, HR output back to pinned host memory, per step'}
+
+
 def run_legs(args, dev, world, rank):
     """Extra legs in the same run, each timed on its own after the headline's timed region (HIP work synchronised,
     barrier, max over ranks): the C2 step in exact fp32, one C3 training step (C4 when N>1: DP over RCCL) and one C5
@@ -442,6 +464,8 @@ def main():
         rec['roofline']['hbm']['measured_frac'] = round(traffic[0] / t_launch / 1e9 / HBM_PEAK_GBPS, 4)
         rec['roofline']['traffic_source'] = traffic[1]
         rec['roofline']['rocprof_union_us_per_launch'] = traffic[2]
+    if args.host_io_steps > 0:
+        rec['host_io'] = host_io(model, x, out, args, dev, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb, parity = cpu_baseline(args, model, x, out, None if args.no_cem else make_gt(args, dev, rank))
         if not args.no_cpu_variants:
