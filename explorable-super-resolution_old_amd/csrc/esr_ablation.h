@@ -41,6 +41,8 @@ int esr_x3_set_nsplit(int32_t on);
 /* esr_axpby_gs: 2 = row-walking kernel with 4 items in flight per thread (product), 1 = one item, 0 = one thread per
  * 8-channel group (round 3). */
 int esr_axpby_set_rows(int32_t on);
+/* BatchNorm forward statistics: 1 (product) = one pass of shifted moments, 0 = mean, then Σ(x − μ)² (round 2-5). */
+int esr_bn_set_onepass(int32_t on);
 /* Exact-fp32 conv tile rows: 0 (product: automatic), 4 or 8 (identical results). */
 int esr_conv_set_tile(int32_t rows);
 /* CEM stencils: 0 (product: LDS-tiled / register-window) / 1 = the direct kernels. */

@@ -35,4 +35,5 @@ extern "C" int esr_dconv_set_occ3(int32_t on) { return set_knob(g_dconv_occ3, on
 extern "C" int esr_dconv_set_cw16(int32_t on) { return set_knob(g_dconv_cw16, on, 0, 1); }
 extern "C" int esr_dconv_set_rows(int32_t on) { return set_knob(g_dconv_rows, on, 0, 1); }
 extern "C" int esr_axpby_set_rows(int32_t on) { return set_knob(g_axpby_rows, on, 0, 2); }
+extern "C" int esr_bn_set_onepass(int32_t on) { return set_knob(g_bn_onepass, on, 0, 1); }
 #endif  // ESR_X3_EXPERIMENTS

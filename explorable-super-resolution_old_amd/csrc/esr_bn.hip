@@ -20,6 +20,7 @@
 // = double): the mean-removal terms then cancel to float64 rounding, not to that of float32 running sums.
 #include <hip/hip_runtime.h>
 #include "esr_amd.h"
+#include "esr_knobs.h"
 
 namespace {
 
@@ -43,10 +44,12 @@ __device__ __forceinline__ float mask_of(const BnP &p, float xh, int c) {
     return z > 0.f ? 1.f : p.slope;
 }
 
-// Column reduction: mode 0: Σx; 1: Σ(x − μ)²; 2: Σgz, Σgz·x̂; 3: Σu, Σu·x̂, Σu·gz.  partial[block][k][C] (float64).
+// Column reduction: mode 0: Σx; 1: Σ(x − μ)²; 2: Σgz, Σgz·x̂; 3: Σu, Σu·x̂, Σu·gz; 4: Σd, Σd² with d = x − x[0][c]
+// (the forward's statistics in one pass: moments about the channel's first value, so the variance does not come from
+// the difference of two large sums).  partial[block][k][C] (float64).
 template <int MODE>
 __global__ __launch_bounds__(NT) void bn_colsum(BnP p, double *partial) {
-    constexpr int K = MODE == 3 ? 3 : (MODE == 2 ? 2 : 1);
+    constexpr int K = MODE == 3 ? 3 : ((MODE == 2 || MODE == 4) ? 2 : 1);
     __shared__ double red[K][NT];
     const int C = p.C, tid = threadIdx.x;
     // thread -> (channel c, row phase) for C <= NT; channel loop otherwise
@@ -61,6 +64,7 @@ __global__ __launch_bounds__(NT) void bn_colsum(BnP p, double *partial) {
         double s[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) s[k] = 0.0;
+        const double shift = (MODE == 4 && act) ? (double)p.x[c] : 0.0;
         if (act) {
 #pragma unroll 4
             for (long long r = r0 + ph; r < r1; r += rpi) {
@@ -68,6 +72,10 @@ __global__ __launch_bounds__(NT) void bn_colsum(BnP p, double *partial) {
                 const float x = p.x[i];
                 if (MODE == 0) {
                     s[0] += x;
+                } else if (MODE == 4) {
+                    const double d = (double)x - shift;
+                    s[0] += d;
+                    s[1] += d * d;
                 } else if (MODE == 1) {
                     const double d = (double)x - (double)p.mu[c];
                     s[0] += d * d;
@@ -106,7 +114,8 @@ __global__ __launch_bounds__(NT) void bn_colsum(BnP p, double *partial) {
 
 // out[k][c] = Σ_b partial[b][k][c]: workgroup = 32 consecutive (k, c) outputs × 8 slices of the blocks, each slice
 // summed in block order, then the slices in slice order (fixed order: deterministic)
-__global__ void bn_finish(const double *partial, int nblk, int K, int C, float *out) {
+template <typename T>
+__global__ void bn_finish(const double *partial, int nblk, int K, int C, T *out) {
     __shared__ double sl[8][32];
     const int o = threadIdx.x & 31, q = threadIdx.x >> 5;
     const int i = blockIdx.x * 32 + o;
@@ -122,7 +131,7 @@ __global__ void bn_finish(const double *partial, int nblk, int K, int C, float *
     if (q == 0 && i < K * C) {
         double t = sl[0][o];
         for (int r = 1; r < 8; ++r) t += sl[r][o];
-        out[i] = (float)t;
+        out[i] = (T)t;
     }
 }
 
@@ -190,6 +199,25 @@ __global__ void bn_apply(BnP p, float *o1, float *o2) {
     o1[i] = r * (Gx - mG - xh * mGx) - Gr * r * r * xh * invN;
 }
 
+// mode 4's sums (float64) -> μ = x[0][c] + Σd/N, var = Σd²/N − (Σd/N)², rs and the running buffers as bn_stats_finish
+__global__ void bn_stats_onepass(const double *sum, const float *x, int C, long long P, float eps, float *mu, float *rs,
+                                 float *var, BnRun run) {
+    const int c = blockIdx.x * NT + threadIdx.x;
+    if (c >= C) return;
+    const double m1 = sum[c] / (double)P, m2 = sum[C + c] / (double)P;
+    const float m = (float)((double)x[c] + m1);
+    const float v = (float)fmax(m2 - m1 * m1, 0.0);
+    mu[c] = m;
+    var[c] = v;
+    rs[c] = 1.f / sqrtf(v + eps);
+    if (run.rm) {
+        const float mo = run.m, a = mo * (float)P / (float)(P > 1 ? P - 1 : 1);
+        run.rm[c] = run.rm[c] * (1.f - mo) + mo * m;
+        run.rv[c] = run.rv[c] * (1.f - mo) + a * v;
+        if (c == 0 && run.nbt) run.nbt[0] += 1;
+    }
+}
+
 // g_γ[c] = r·(Q − s1·U/N − s2·A/N)
 __global__ void bn_ggamma(const float *sums, const float *rs, int C, long long P, float *out) {
     const int c = blockIdx.x * NT + threadIdx.x;
@@ -203,10 +231,10 @@ inline int launched() { return hipGetLastError() == hipSuccess ? ESR_OK : ESR_EL
 inline unsigned grid_of(long long n) { return (unsigned)((n + NT - 1) / NT); }
 inline int nblocks_for(long long P) { return (int)(P / 256 < 1 ? 1 : (P / 256 > MAXB ? MAXB : P / 256)); }
 
-template <int MODE>
-int colsum(const BnP &p, float *ws, float *out, hipStream_t st) {
+template <int MODE, typename T = float>
+int colsum(const BnP &p, float *ws, T *out, hipStream_t st) {
     double *partial = reinterpret_cast<double *>(ws);
-    constexpr int K = MODE == 3 ? 3 : (MODE == 2 ? 2 : 1);
+    constexpr int K = MODE == 3 ? 3 : ((MODE == 2 || MODE == 4) ? 2 : 1);
     const int nb = nblocks_for(p.P);
     hipLaunchKernelGGL(bn_colsum<MODE>, dim3(nb), dim3(NT), 0, st, p, partial);
     hipLaunchKernelGGL(bn_finish, dim3((unsigned)((K * p.C + 31) / 32)), dim3(NT), 0, st, partial, nb, K, p.C, out);
@@ -240,11 +268,17 @@ extern "C" int esr_bn_lrelu_fwd(const float *x, int64_t P, int32_t C, const floa
     const hipStream_t st = (hipStream_t)stream;
     BnP p = {};
     p.x = x; p.gamma = gamma; p.beta = beta; p.mu = mu; p.rs = rs; p.P = P; p.C = C; p.slope = slope;
-    float *partial = ws, *sums = ws + (long long)MAXB * 3 * C * 2;
-    if (colsum<0>(p, partial, sums, st)) return ESR_ELAUNCH;
-    hipLaunchKernelGGL(bn_stats_finish, dim3(grid_of(C)), dim3(NT), 0, st, sums, C, P, eps, 0, mu, rs, var, none);
-    if (colsum<1>(p, partial, sums, st)) return ESR_ELAUNCH;
-    hipLaunchKernelGGL(bn_stats_finish, dim3(grid_of(C)), dim3(NT), 0, st, sums, C, P, eps, 1, mu, rs, var, run);
+    float *partial = ws, *sums = ws + (long long)MAXB * 3 * C * 2;  // (room for [2][C] float64 sums: [8][C] floats)
+    if (g_bn_onepass) {
+        double *sd = reinterpret_cast<double *>(sums);
+        if (colsum<4, double>(p, partial, sd, st)) return ESR_ELAUNCH;
+        hipLaunchKernelGGL(bn_stats_onepass, dim3(grid_of(C)), dim3(NT), 0, st, sd, x, C, P, eps, mu, rs, var, run);
+    } else {
+        if (colsum<0>(p, partial, sums, st)) return ESR_ELAUNCH;
+        hipLaunchKernelGGL(bn_stats_finish, dim3(grid_of(C)), dim3(NT), 0, st, sums, C, P, eps, 0, mu, rs, var, none);
+        if (colsum<1>(p, partial, sums, st)) return ESR_ELAUNCH;
+        hipLaunchKernelGGL(bn_stats_finish, dim3(grid_of(C)), dim3(NT), 0, st, sums, C, P, eps, 1, mu, rs, var, run);
+    }
     hipLaunchKernelGGL(bn_apply<0>, dim3(grid_of(P * C)), dim3(NT), 0, st, p, y, nullptr);
     return launched();
 }

@@ -22,7 +22,8 @@
     X(g_dconv_occ3, 1)   /* x3 halo kernel at three workgroups per CU where its LDS allows                         */ \
     X(g_dconv_rows, 0)   /* tap-row discriminator weight-gradient kernel (slower at config 3)                      */ \
     X(g_axpby_rows, 2)   /* esr_axpby_gs: 1 row-walking kernel, 2 the same with 4 items in flight per thread, 0 one */ \
-                         /* thread per 8-channel group                                                            */
+                         /* thread per 8-channel group                                                            */ \
+    X(g_bn_onepass, 1)   /* BatchNorm forward statistics in one pass (shifted moments; 0: mean, then Σ(x − μ)²)    */
 
 #ifdef ESR_X3_EXPERIMENTS
 #define ESR_KNOB_DECL(name, v) extern int name;

@@ -267,6 +267,48 @@ def test_fused_bn_lrelu_vs_float64(gpu_device, C, B, H, W):
     assert int(bng.num_batches_tracked) == int(bn64.num_batches_tracked) == 1
 
 
+@pytest.mark.parametrize('offset,scale', [(0.0, 1.0), (1e3, 1e-2), (-50.0, 3.0)])
+def test_bn_statistics_one_pass_vs_two_pass(gpu_device, ablation_lib, offset, scale):
+    """The BatchNorm forward's statistics in one pass of shifted moments (product: moments about each channel's first
+    value, float64) against the mean-then-Σ(x − μ)² two-pass form (ablation library, esr_bn_set_onepass(0)), both
+    against float64: μ within 2 float32 ulps of |μ| + σ, the biased variance within 1e-6 relative — also for channels
+    whose mean is 1e5 standard deviations from zero, where the two-pass form's float32 mean biases its Σ(x − μ)²."""
+    import ctypes
+    g = torch.Generator().manual_seed(int(abs(offset)) + 7)
+    P, C = 37 * 41 * 3, 96
+    x = (torch.randn(P, C, generator=g, dtype=torch.float64) * scale + offset).float()
+    gamma, beta = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g) * 0.1
+    x64 = x.double()
+    mu64, var64 = x64.mean(0), x64.var(0, unbiased=False)
+    res = {}
+    for name, lib in (('product', _lib.load()), ('two_pass', ablation_lib)):
+        if lib is ablation_lib:
+            assert lib.esr_bn_set_onepass(0) >= 0
+        try:
+            xd, gd, bd = x.to(gpu_device), gamma.to(gpu_device), beta.to(gpu_device)
+            y = torch.empty_like(xd)
+            mu, rs, var = (torch.empty(C, device=gpu_device) for _ in range(3))
+            ws = torch.empty(int(lib.esr_bn_workspace_floats(P, C)), device=gpu_device)
+            st = ctypes.c_void_p(torch.cuda.current_stream(gpu_device).cuda_stream)
+            _lib.check(lib.esr_bn_lrelu_fwd(xd.data_ptr(), P, C, gd.data_ptr(), bd.data_ptr(), 1e-5, 0.2, y.data_ptr(),
+                                            mu.data_ptr(), rs.data_ptr(), var.data_ptr(), ws.data_ptr(), None, None,
+                                            None, 0.1, st), 'esr_bn_lrelu_fwd')
+            torch.cuda.synchronize()
+        finally:
+            if lib is ablation_lib:
+                lib.esr_bn_set_onepass(1)
+        res[name] = (mu.double().cpu(), var.double().cpu())
+    ulp = torch.finfo(torch.float32).eps * (mu64.abs() + var64.sqrt())
+    mu1, var1 = res['product']
+    assert torch.all((mu1 - mu64).abs() <= 2 * ulp), float(((mu1 - mu64).abs() / ulp).max())
+    assert float(((var1 - var64).abs() / var64).max()) < 1e-6
+    mu2, var2 = res['two_pass']
+    assert torch.all((mu2 - mu64).abs() <= 2 * ulp)
+    if offset == 0.0:
+        assert float(((var2 - var64).abs() / var64).max()) < 1e-6
+        assert float(((var1 - var2).abs() / var64).max()) < 1e-6
+
+
 def test_lrelu_nhwc_second_order(gpu_device):
     """bn.lrelu_nhwc (the discriminator's LeakyReLUs without a norm in front) against F.leaky_relu in float64:
     output, gradient and the gradient's own gradient (w.r.t. the upstream gradient)."""
