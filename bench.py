@@ -18,6 +18,7 @@ Extra keys, each timed separately after the headline (--no-legs skips them): `fp
 iteration, bench_zopt.py, with SURVEY §8's KernelGAN-recipe kernel; `zopt_c5_learned13` with the 13×13 learned one).
 """
 import argparse
+import collections
 import json
 import os
 import sys
@@ -359,8 +360,11 @@ def main():
             out = model(x)
         torch.cuda.synchronize()
         engine._PROFILE = None
-        for n_ops in {e[3] for e in probe if e[0] == 'ops'}:
-            engine.reserve_timers(n_ops, n_prof)
+        # one timer set per op list a profiled step runs: the two stream parts record op lists of the same length,
+        # so reserve per occurrence (a set of lengths reserved half of them and the rest were created in the timed
+        # region)
+        for n_ops, c in collections.Counter(e[3] for e in probe if e[0] == 'ops').items():
+            engine.reserve_timers(n_ops, c * n_prof)
         list(engine.profile_records(probe))
         torch.cuda.synchronize()
         if world > 1:
@@ -370,9 +374,13 @@ def main():
         origin = engine.ProfileOrigin(dev)
         origin.record()
         t0 = time.perf_counter()
+        ev_prof = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         for i in range(args.steps):  # per-launch events on the last n_prof steps only (their cost: ~1.5 % of a step)
             engine._PROFILE = prof if (not args.no_op_timers and i >= args.steps - n_prof) else None
+            if i == args.steps - n_prof:
+                ev_prof[0].record()  # the profiled steps' own wall time on the device (the busy fraction's base)
             out = model(x)
+        ev_prof[1].record()
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         engine._PROFILE = None
@@ -414,7 +422,9 @@ def main():
     achieved = fl_all / (busy / 1e3) / 1e12
     dom = max(per, key=lambda k: per[k][2])
     peak, peak_note = PEAKS[args.precision]
-    prof_ms = dt * 1e3 * n_prof / args.steps  # wall time of the profiled steps (the steps are alike)
+    # wall time of the profiled steps themselves (device events around them: the event-carrying steps run slower than
+    # the average step, so dt * n_prof / steps understated it and the busy fraction could exceed 1)
+    prof_ms = ev_prof[0].elapsed_time(ev_prof[1])
     kernels = {k: {'launches_per_step': v[0] // n_prof, 'avg_us': round(v[2] / v[0] * 1e3, 2),
                    'tflops_over_own_union': round(v[1] / (union[k] / 1e3) / 1e12, 2),
                    'share_of_step': round(union[k] / prof_ms, 3)}
@@ -464,6 +474,8 @@ def main():
         rec['roofline']['hbm']['measured_frac'] = round(traffic[0] / t_launch / 1e9 / HBM_PEAK_GBPS, 4)
         rec['roofline']['traffic_source'] = traffic[1]
         rec['roofline']['rocprof_union_us_per_launch'] = traffic[2]
+        if traffic[2]:  # the same FLOPs over the rocprofv3 kernel-trace union (the committed trace of this bench)
+            rec['roofline']['frac_rocprof_union'] = round(fl_all / n_all / (traffic[2] * 1e-6) / 1e12 / peak, 4)
     if args.host_io_steps > 0:
         rec['host_io'] = host_io(model, x, out, args, dev, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -119,9 +119,17 @@ class GradBuckets:
     backward; buckets go out strictly in bucket order (the same collective sequence on every rank).  `finish()` launches
     the buckets still pending (parameters that got no gradient in this backward: requires_grad toggled off, or not
     reached), waits for every bucket, averages and writes back.  Buckets are ≥ a few MB so that each ring
-    all-reduce runs near the per-link xGMI bandwidth rather than its latency."""
+    all-reduce runs near the per-link xGMI bandwidth rather than its latency.
 
-    def __init__(self, params, cap_bytes=16 << 20):
+    Flat mode (`flat_opt`: a FlatAdam over exactly these parameters, whose .grad are views of flat_opt.flat.grad, so a
+    bucket is one contiguous range of it): a bucket is all-reduced in place on its range (no cat, no copy back).  A
+    producer that writes the flat gradient itself — the HIP generator's backward, one autograd node over the
+    optimiser's flat parameter (train_engine._GeneratorFn) — calls `ready_from(lo)` each time flat.grad[lo:] is final,
+    so that the buckets launch while the rest of its backward runs (`emit_offsets()` tells it where a bucket
+    completes).  A post-accumulate hook on the flat parameter launches everything when the flat gradient arrives
+    through autograd instead."""
+
+    def __init__(self, params, cap_bytes=16 << 20, flat_opt=None):
         self.params = list(params)
         self.buckets, cur, size = [], [], 0
         for p in reversed(self.params):
@@ -134,6 +142,14 @@ class GradBuckets:
         if cur:
             self.buckets.append(cur)
         self.where = {id(p): b for b, ps in enumerate(self.buckets) for p in ps}
+        self.flat_opt = flat_opt if flat_opt is not None and flat_opt.accepts_flat_grad(self.params) else None
+        self.ranges = None
+        if self.flat_opt is not None:
+            off, o = {}, 0
+            for p in self.params:
+                off[id(p)] = o
+                o += p.numel()
+            self.ranges = [(off[id(ps[-1])], off[id(ps[0])] + ps[0].numel()) for ps in self.buckets]
         self.armed = False
         self.launched_in_backward = 0
         self._next = 0
@@ -141,6 +157,8 @@ class GradBuckets:
         self._works = [None] * len(self.buckets)
         self.hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params] \
             if _world() > 1 else []
+        if self.flat_opt is not None and _world() > 1:
+            self.hooks.append(self.flat_opt.flat.register_post_accumulate_grad_hook(lambda _: self.ready_from(0)))
         # what went over the wire: collectives, bytes, and the stream time finish() left exposed (device events
         # around the waits, read lazily by comm_stats so no host sync is added to the step)
         self.n_allreduce = 0
@@ -165,7 +183,19 @@ class GradBuckets:
         self._next = 0
         self.launched_in_backward = 0
 
+    def emit_offsets(self):
+        """Flat mode: the flat-gradient offsets at which a producer finalising the gradient from its end should call
+        ready_from (each bucket's lower end)."""
+        return sorted({lo for lo, _ in self.ranges}) if self.ranges is not None else [0]
+
     def _launch(self, b):
+        if self.ranges is not None:
+            lo, hi = self.ranges[b]
+            g = self.flat_opt.flat.grad[lo:hi]
+            self._works[b] = (collective(dist.all_reduce, g, async_op=True), g, None)
+            self.n_allreduce += 1
+            self.allreduce_bytes += g.numel() * g.element_size()
+            return
         grads = [p.grad for p in self.buckets[b] if p.grad is not None]
         if not grads:
             self._works[b] = ()
@@ -175,17 +205,28 @@ class GradBuckets:
         self.n_allreduce += 1
         self.allreduce_bytes += flat.numel() * flat.element_size()
 
-    def _on_grad(self, p):
-        if not self.armed:
-            return
-        b = self.where[id(p)]
-        self._pending[b].discard(id(p))
+    def _launch_ready(self):
         # launch complete buckets strictly in bucket order (the same sequence of collectives on every rank, as RCCL
         # requires, whatever order the backward finalises the parameters in)
         while self._next < len(self.buckets) and not self._pending[self._next]:
             self._launch(self._next)
             self._next += 1
             self.launched_in_backward += 1
+
+    def _on_grad(self, p):
+        if not self.armed:
+            return
+        self._pending[self.where[id(p)]].discard(id(p))
+        self._launch_ready()
+
+    def ready_from(self, lo):
+        """Flat mode: flat_opt.flat.grad[lo:] holds its final value for this backward (launches the buckets inside)."""
+        if not self.armed:
+            return
+        for b in range(self._next, len(self.buckets)):
+            if self.ranges[b][0] >= lo:
+                self._pending[b].clear()
+        self._launch_ready()
 
     def finish(self):
         if not self.armed:
@@ -207,21 +248,81 @@ class GradBuckets:
                 e0, e1 = self._exposed.pop(0)
                 self._exposed_ms += e0.elapsed_time(e1)
             self._exposed.append(ev)
-        for _, flat, grads in items:
-            flat /= w
-            o = 0
-            for g in grads:
-                n = g.numel()
-                g.copy_(flat[o:o + n].view_as(g))
-                o += n
+        if self.ranges is not None:  # in place on flat.grad: one scaling of the whole buffer
+            self.flat_opt.flat.grad.div_(w)
+        else:
+            for _, flat, grads in items:
+                flat /= w
+                o = 0
+                for g in grads:
+                    n = g.numel()
+                    g.copy_(flat[o:o + n].view_as(g))
+                    o += n
         self._works = [None] * len(self.buckets)
 
 
-def _broadcast_buffers(module):
+class FlatBuffers:
+    """A module's floating-point buffers (the D BatchNorms' running means / variances) as views of one flat tensor, so
+    that rank 0's values reach every rank in ONE broadcast (DataParallel keeps replica 0's buffers).
+    num_batches_tracked stays as it is: every rank increments it identically.  The views are re-bound when something
+    replaced a buffer (module.to(), load_state_dict(assign=True))."""
+
+    def __init__(self, module):
+        self.module = module
+        self.flat = None
+        self._ptrs = []
+
+    def _entries(self):
+        return [(m, n, b) for m in self.module.modules() for n, b in m._buffers.items()
+                if b is not None and b.is_floating_point()]
+
+    def sync(self):
+        ents = self._entries()
+        if self.flat is None or len(ents) != len(self._ptrs) or \
+                any(b.data_ptr() != ptr for (_, _, b), ptr in zip(ents, self._ptrs)):
+            flat = torch.cat([b.detach().reshape(-1) for _, _, b in ents])
+            o = 0
+            for m, n, b in ents:
+                m._buffers[n] = flat[o:o + b.numel()].view_as(b)
+                o += b.numel()
+            self.flat = flat
+            self._ptrs = [b.data_ptr() for _, _, b in self._entries()]
+        return self.flat
+
+
+def _broadcast_buffers(module, flat=None):
+    """Rank 0's buffers everywhere: one broadcast of `flat` (a FlatBuffers of module), else one per buffer."""
     if _world() == 1:
+        return
+    if flat is not None:
+        collective(dist.broadcast, flat.sync(), 0)
         return
     for b in module.buffers():
         collective(dist.broadcast, b, 0)
+
+
+class _GlobalMean(torch.autograd.Function):
+    """mean(t) over the GLOBAL batch (every rank's t, equal sizes), differentiable: the relativistic D terms
+    (SRRaGAN_model.py:380-382, 521-524) subtract the mean over DataParallel's gathered batch.  Backward: the gradient
+    reaching the global mean is all-reduced and spread over the local elements, so that the ranks' averaged parameter
+    gradients are the gradient of the global-batch loss also for non-linear GAN losses (vanilla, lsgan); wgan-gp is
+    linear, where rank-local means give the same average."""
+
+    @staticmethod
+    def forward(ctx, t):
+        ctx.shape = t.shape
+        m = t.detach().mean().reshape(1)
+        collective(dist.all_reduce, m)
+        return (m / _world()).reshape(())
+
+    @staticmethod
+    def backward(ctx, g):
+        gs = g.detach().reshape(1).clone()
+        collective(dist.all_reduce, gs)
+        n = 1
+        for d in ctx.shape:
+            n *= d
+        return (gs / (_world() * n)).reshape(()).expand(ctx.shape)
 
 
 LATENT_WEIGHTS_RELATIVE_STD = 0.  # base_model.py:116
@@ -279,10 +380,25 @@ class SRRaGANModel:
     # ------------------------------------------------------------------------------------------------------------------
     def _init_training(self, opt, accumulation_steps_per_batch):
         t = opt['train']
-        for k in ('pixel_weight', 'feature_weight', 'latent_weight', 'optimalZ_loss_weight', 'highpass_weight',
+        for k in ('feature_weight', 'latent_weight', 'optimalZ_loss_weight', 'highpass_weight',
                   'shift_invariant_weight'):
             if t.get(k):
                 raise NotImplementedError('%s > 0 is not part of the built training path (shipped configs use 0)' % k)
+        # G pixel loss (SRRaGAN_model.py:108-120, 477-483): L1 / L2 between fake_H and var_H, in the HR domain or (not
+        # with CEM_arch: the reference asserts that at construction, :61) between their bilinear resizes to the LR size
+        self.cri_pix = None
+        if (t.get('pixel_weight') or 0) > 0:
+            crit = t.get('pixel_criterion')
+            if crit == 'l1':
+                self.cri_pix = torch.nn.functional.l1_loss
+            elif crit == 'l2':
+                self.cri_pix = torch.nn.functional.mse_loss
+            else:
+                raise NotImplementedError('Loss type [{}] not recognized.'.format(crit))
+            self.l_pix_w = t['pixel_weight']
+        self.pixel_domain = t.get('pixel_domain', 'HR')
+        assert self.pixel_domain == 'HR' or not self.CEM_arch, \
+            'Why should I use CEM_arch AND penalize MSE in the LR domain?'
         if opt['network_D'].get('decomposed_input'):
             raise NotImplementedError('decomposed D input')
         rel = opt['network_D'].get('relativistic')
@@ -316,7 +432,7 @@ class SRRaGANModel:
         g = self.netG.module if isinstance(self.netG, torch.nn.DataParallel) else self.netG
         # the RRDBNet whose backward may add its flat gradient buffer straight into the optimiser's; armed only around
         # the generator loss's .backward() in optimize_parameters (single process: no bucket hooks wait)
-        self._rrdb = g.generated_image_model if self.CEM_net is not None else g
+        self._rrdb = g.generated_image_model if hasattr(g, 'generated_image_model') else g  # (CEM_arch or bare)
         self.optimizers.append(self.optimizer_G)
         if self.D_exists:
             self.netD = networks.define_D(opt, CEM=self.CEM_net).to(self.device)
@@ -336,8 +452,12 @@ class SRRaGANModel:
             self.global_D_update_ratio, self.D_init_iters = 1, 0
         self.schedulers = [torch.optim.lr_scheduler.MultiStepLR(o, t['lr_steps'], t['lr_gamma'])
                            for o in self.optimizers]
-        self._g_buckets = GradBuckets(gparams)
-        self._d_buckets = GradBuckets(list(self.netD.parameters())) if self.D_exists else None
+        # flat mode: the buckets are ranges of the FlatAdams' gradient buffers, all-reduced in place; the generator's
+        # backward launches its buckets itself as it finalises them (train_engine._GeneratorFn, _esr_grad_sink)
+        self._g_buckets = GradBuckets(gparams, flat_opt=self.optimizer_G)
+        self._d_buckets = GradBuckets(list(self.netD.parameters()), flat_opt=self.optimizer_D) \
+            if self.D_exists else None
+        self._d_flat_buffers = FlatBuffers(self.netD) if self.D_exists else None
 
     # ------------------------------------------------------------------------------------------------------------------
     def ConcatLatent(self, LR_image, latent_input):
@@ -398,17 +518,37 @@ class SRRaGANModel:
             self.var_ref = (data['ref'] if 'ref' in data else data['HR']).to(self.device)
 
     # ------------------------------------------------------------------------------------------------------------------
-    def _d_statistics_t(self, pred_real, pred_fake):
+    def _d_statistics_t(self, pred_real, pred_fake, means=()):
         """Per-image D logit differences, summed over ranks (global-batch semantics of DataParallel), as a device
-        tensor [mean diff, fraction correctly distinguished, mean D(real), mean D(fake)] (no host sync)."""
+        tensor [mean diff, fraction correctly distinguished, mean D(real), mean D(fake), *means] (no host sync).
+        `means`: scalars (this micro-step's logged losses) averaged over ranks in the same all-reduce — a loss that
+        is a mean over the local batch averages to the global batch's (equal per-rank batches)."""
         diff = torch.mean(pred_real.detach() - pred_fake.detach(), dim=list(range(1, pred_real.dim())))
         # (the image count as a device fill, not torch.tensor(): a pageable host-to-device copy waits for the stream)
         s = torch.stack([diff.sum(), (diff > 0).float().sum(), diff.new_full((), float(diff.numel())),
-                         pred_real.detach().mean(), pred_fake.detach().mean()])
+                         pred_real.detach().mean(), pred_fake.detach().mean()] +
+                        [m.detach().reshape(()).to(diff.dtype) for m in means])
         if _world() > 1:
             collective(dist.all_reduce, s)
             s[3:] /= _world()
-        return torch.stack([s[0] / s[2], s[1] / s[2], s[3], s[4]])
+        return torch.cat([torch.stack([s[0] / s[2], s[1] / s[2]]), s[3:]])
+
+    def _batch_mean(self, t):
+        """torch.mean(t) over the batch DataParallel would have gathered: across ranks (differentiable) when the GAN
+        loss is not linear in it; rank-local for wgan-gp, whose averaged gradients are then already the global ones
+        and whose logged losses are averaged in _d_statistics_t."""
+        if _world() > 1 and self.cri_gan.gan_type != 'wgan-gp':
+            return _GlobalMean.apply(t)
+        return torch.mean(t)
+
+    def _global_log_means(self, vals):
+        """Logged per-micro-step losses (device scalars) averaged over ranks: the global batch's values."""
+        if _world() > 1 and vals:
+            t = torch.stack([v.detach().reshape(()) for v in vals])
+            collective(dist.all_reduce, t)
+            t /= _world()
+            return list(t.unbind())
+        return [v.detach().reshape(()) for v in vals]
 
     def _d_statistics(self, pred_real, pred_fake):
         return tuple(float(v) for v in self._d_statistics_t(pred_real, pred_fake).tolist())
@@ -580,9 +720,9 @@ class SRRaGANModel:
             self.var_H, self.var_ref = self.CEM_net.HR_unpadder(self.var_H), self.CEM_net.HR_unpadder(self.var_ref)
         static_Z = self.GetLatent() if self.latent_input is not None else None
         self.ConcatLatent(LR_image=self.var_L, latent_input=static_Z)
-        # single-process: the generator's training forward takes the optimiser's flat parameter as its one autograd
-        # input (its backward returns the flat gradient: train_engine.generator_forward_train) instead of 702 tensors
-        self._rrdb._esr_flat_fwd = self.optimizer_G if _world() == 1 and G_grads_retained else None
+        # the generator's training forward takes the optimiser's flat parameter as its one autograd input (its backward
+        # returns the flat gradient, or across ranks writes it in bucket-sized slices: train_engine) instead of 702
+        self._rrdb._esr_flat_fwd = self.optimizer_G if G_grads_retained else None
         try:
             self.fake_H = self.netG(self.model_input)
         finally:
@@ -602,8 +742,8 @@ class SRRaGANModel:
             pred_d_real = self.netD(self.var_ref)
             pred_d_fake = self.netD(self.fake_H.detach())
             if self.relativistic_D:
-                l_d_real = self.cri_gan(pred_d_real - torch.mean(pred_d_fake), True)
-                l_d_fake = self.cri_gan(pred_d_fake - torch.mean(pred_d_real), False)
+                l_d_real = self.cri_gan(pred_d_real - self._batch_mean(pred_d_fake), True)
+                l_d_fake = self.cri_gan(pred_d_fake - self._batch_mean(pred_d_real), False)
             else:
                 l_d_real = 2 * self.cri_gan(pred_d_real, True)
                 l_d_fake = 2 * self.cri_gan(pred_d_fake, False)
@@ -615,9 +755,13 @@ class SRRaGANModel:
                 interp.requires_grad = True
                 l_d_gp = self.l_gp_w * self.cri_gp(interp, self.netD(interp))
                 l_d_total = l_d_total + l_d_gp
-            # [l_d_real, l_d_fake, D_real, D_fake, D_logits_diff, Correctly_distinguished] of this micro-step
-            st = self._d_statistics_t(pred_d_real, pred_d_fake)
-            vals = torch.stack([l_d_real.detach().reshape(()), l_d_fake.detach().reshape(()), st[2], st[3], st[0], st[1]])
+            # [l_d_real, l_d_fake, D_real, D_fake, D_logits_diff, Correctly_distinguished] of this micro-step, the losses
+            # (and l_d_gp) averaged over ranks in the statistics' all-reduce
+            st = self._d_statistics_t(pred_d_real, pred_d_fake,
+                                      (l_d_real, l_d_fake) + ((l_d_gp,) if l_d_gp is not None else ()))
+            vals = torch.stack([st[4], st[5], st[2], st[3], st[0], st[1]])
+            if l_d_gp is not None:
+                l_d_gp_log = st[6]
             if self.D_verification == 'current':  # the gate needs this micro-step's statistics now
                 v = vals.tolist()
                 self._d_logs.append(v)
@@ -634,7 +778,7 @@ class SRRaGANModel:
             if last_acc_D:
                 self._d_buckets.finish()
                 self.optimizer_D.step()
-                _broadcast_buffers(self.netD)
+                _broadcast_buffers(self.netD, self._d_flat_buffers)
 
                 def log_d(_, rows=self._d_logs, g=self.gradient_step_num, ratio=self.cur_D_update_ratio):
                     a = np.mean(np.array(rows), axis=0)
@@ -644,7 +788,7 @@ class SRRaGANModel:
                         self._log_dict[k].append((g, float(v)))
                 self._defer(None, log_d)
                 if l_d_gp is not None:
-                    self._defer(l_d_gp.detach().reshape(1),
+                    self._defer(l_d_gp_log.reshape(1),
                                 lambda v, g=self.gradient_step_num: self._log_dict['l_d_gp'].append((g, v[0])))
         # ---- G step ----
         if self.generator_step:
@@ -653,8 +797,16 @@ class SRRaGANModel:
                     p.requires_grad = False
             if first_acc_G:
                 self.optimizer_G.zero_grad()
-                self._g_logs = {'l_g_range': [], 'l_g_gan': []}
+                self._g_logs = {'l_g_pix': [], 'l_g_range': [], 'l_g_gan': []}
             l_g_total = 0
+            if self.cri_pix is not None:  # :477-483
+                if self.pixel_domain == 'LR':  # Convert_2_LR (:304-305): bilinear resize to the LR size
+                    size = list(self.var_L.size()[-2:])
+                    rs = lambda v: torch.nn.functional.interpolate(v, size=size, mode='bilinear')  # noqa: E731
+                    l_g_pix = self.cri_pix(rs(self.fake_H), rs(self.var_H))
+                else:
+                    l_g_pix = self.cri_pix(self.fake_H, self.var_H)
+                l_g_total = l_g_total + self.l_pix_w * l_g_pix / self.grad_accumulation_steps_G
             if self.cri_range is not None:
                 l_g_range = self.cri_range(self.fake_H)
                 l_g_total = l_g_total + self.l_range_w * l_g_range / self.grad_accumulation_steps_G
@@ -668,8 +820,8 @@ class SRRaGANModel:
                         D.set_precision(prev)
                 if self.relativistic_D:
                     pred_d_real = self.netD(self.var_ref).detach()
-                    l_g_gan = self.l_gan_w * (self.cri_gan(pred_d_real - torch.mean(pred_g_fake), False) +
-                                              self.cri_gan(pred_g_fake - torch.mean(pred_d_real), True)) / 2
+                    l_g_gan = self.l_gan_w * (self.cri_gan(pred_d_real - self._batch_mean(pred_g_fake), False) +
+                                              self.cri_gan(pred_g_fake - self._batch_mean(pred_d_real), True)) / 2
                 else:
                     l_g_gan = self.l_gan_w * self.cri_gan(pred_g_fake, True)
                 l_g_gan = l_g_gan / self.grad_accumulation_steps_G  # logged divided, as the reference (:526, 539)
@@ -677,16 +829,20 @@ class SRRaGANModel:
             if last_acc_G:
                 self._g_buckets.arm()
             # the flat-gradient fast path (train_engine._GeneratorFn.backward) only for this backward: a full
-            # .backward() into every generator parameter, with no per-parameter hooks when single-process
-            self._rrdb._esr_flat_grad = self.optimizer_G if _world() == 1 else None
+            # .backward() into every generator parameter; across ranks the backward also launches the G buckets
+            # itself as it finalises them (flat-mode GradBuckets as its gradient sink)
+            self._rrdb._esr_flat_grad = self.optimizer_G
+            self._rrdb._esr_grad_sink = self._g_buckets if (last_acc_G and _world() > 1) else None
             try:
                 l_g_total.backward()
             finally:
                 self._rrdb._esr_flat_grad = None
-            if self.cri_range is not None:
-                self._defer(l_g_range.detach().reshape(1), lambda v, rows=self._g_logs['l_g_range']: rows.append(v[0]))
-            if self.D_exists:
-                self._defer(l_g_gan.detach().reshape(1), lambda v, rows=self._g_logs['l_g_gan']: rows.append(v[0]))
+                self._rrdb._esr_grad_sink = None
+            logged = [(k, v) for k, v in (('l_g_pix', l_g_pix if self.cri_pix is not None else None),
+                                          ('l_g_range', l_g_range if self.cri_range is not None else None),
+                                          ('l_g_gan', l_g_gan if self.D_exists else None)) if v is not None]
+            for (k, _), v in zip(logged, self._global_log_means([v for _, v in logged])):
+                self._defer(v.reshape(1), lambda x, rows=self._g_logs[k]: rows.append(x[0]))
             if last_acc_G:
                 self._g_buckets.finish()
                 if self.latent_input is not None and self.latent_grads_multiplier != 1:  # :543-546

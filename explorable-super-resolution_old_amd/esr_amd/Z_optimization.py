@@ -727,6 +727,13 @@ class Z_optimizer:
             elif len(self.loss_values) >= -self.max_iters:
                 if z_iter == self.cur_iter - 5 * self.max_iters:
                     break
+                # the convergence test reads the latest loss: settle that iteration's lagged overflow flags first (an
+                # overflowed x3 iteration leaves inf there), so the stop decision is the exact-fp32 loop's
+                if pend is not None:
+                    if pend[1].overflowed():
+                        self._restore(pend[0])
+                        self.loss_values[-1] = self._redo_f32(pend[2])
+                    pend = None
                 first, last = float(self.loss_values[self.max_iters]), float(self.loss_values[-1])
                 if (first - last) / np.abs(first) < 1e-2 * self.LR:
                     break

@@ -816,6 +816,20 @@ def use_streams(shape, cem):
     return STREAMS > 1 and B >= STREAM_MIN_B and (B // STREAMS) * (h + m) * (w + m) >= STREAM_MIN_PART_PIXELS
 
 
+def _trim_slots(net, n):
+    """Free the workspaces and op lists of inference slots >= n (those of a previous multi-stream forward): a later
+    single-stream or smaller forward would otherwise keep a batch part's HR-resolution buffers allocated."""
+    cache = net.__dict__.get('_esr_cache')
+    if not cache:
+        return
+    for name in [k for k in cache if k.startswith('ws') and k[2:].isdigit() and int(k[2:]) >= n]:
+        del cache[name]
+    plans = cache.get('plans')
+    if plans:
+        for k in [k for k in plans if k[1] >= n]:
+            del plans[k]
+
+
 def _multistream_forward(net, x, cem, precision, n):
     """The batch in n parts, part k on stream k (part 0 on the current stream), results in one output tensor."""
     B = x.shape[0]
@@ -855,7 +869,9 @@ def generator_forward(net, x, cem=None):
     if precision not in PRECISIONS:
         raise ValueError('esr_precision must be one of %s' % (PRECISIONS,))
     x = x.contiguous()
-    if USE_OP_LISTS and use_streams(x.shape, cem):
+    multi = USE_OP_LISTS and use_streams(x.shape, cem)
+    _trim_slots(net, STREAMS if multi else 1)
+    if multi:
         out, wss = _multistream_forward(net, x, cem, precision, STREAMS)
     elif USE_OP_LISTS:
         out, ws = _planned_forward(net, x, cem, precision)

@@ -303,6 +303,15 @@ class _BwdPacked:
         self.params = plan.params
         assert all(id(p) in by_param for p in self.params), 'generator parameter without a backward rule'
         self.gidx = torch.cat([by_param[id(p)] for p in self.params]).to(dev)
+        # flat-gradient offsets (reference parameter order) where the backward has finalised a suffix of the flat
+        # gradient: after LR_conv (the convs behind it are done too), after each RRDB (last to first); 0 = all
+        off, o = {}, 0
+        for p in self.params:
+            off[id(p)] = o
+            o += p.numel()
+        self.flat_n = o
+        self.lr_conv_lo = off[id(m[1].sub[net.nb].weight)]
+        self.rrdb_lo = [off[id(m[1].sub[k].RDB1.convs[0][0].weight)] for k in range(net.nb)]
         self._x3 = None
 
     def x3_fused(self):
@@ -585,7 +594,35 @@ def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_in
     """dL/dparams of RRDBNet (+ CEM in train or eval mode) and/or dL/dinput given dL/dout.  x3 (with split, params
     only): the residual blocks' backward in the split-f16 scheme; ws.bwd_overflow then tells whether a scaled gradient
     or a weight left its f16 range (the caller reruns without x3).
-    Returns ({param: grad} or {}, input gradient [B, C_in, h, w] or None)."""
+    Returns (flat parameter gradient in the reference layout or None, input gradient [B, C_in, h, w] or None)."""
+    it = backward_segments(net, cem, ws, d_out, latent, M, need_params, need_input, split, x3, act_scale)
+    while True:
+        try:
+            next(it)
+        except StopIteration as e:
+            return e.value
+
+
+def _emit_points(bp, lows):
+    """The segment boundaries of a sliced backward: for each bucket's lower end `lo` (GradBuckets.emit_offsets), the
+    first point of the backward at which flat[lo:] is final — after LR_conv (with the convs behind it), after RRDB k
+    (last to first) — so that every bucket launches as early as the backward allows.  0 (conv_first) is the end."""
+    cands = [bp.lr_conv_lo] + [bp.rrdb_lo[k] for k in reversed(range(len(bp.rrdb_lo)))]
+    pts = set()
+    for lo in lows:
+        p = next((c for c in cands if c <= lo), 0)
+        if p > 0:
+            pts.add(p)
+    return pts
+
+
+def backward_segments(net, cem, ws, d_out, latent, M, need_params=True, need_input=False, split=False, x3=False,
+                      act_scale=1.0, seg=None):
+    """generator_backward as a generator.  With seg = (flat_grad, lows) (parameter gradients only): the weight
+    gradients go straight into flat_grad (+=, reference layout) in slices — at each boundary of _emit_points(lows)
+    the finished suffix flat_grad[lo:hi] gets its gather-add and the generator yields lo (the caller launches the
+    all-reduces of the buckets now complete while the rest is enqueued); the returned flat gradient is then None and
+    the last slice [0, hi) is added before returning."""
     dev = d_out.device
     stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     bp = _bwd_packed(net, latent)
@@ -693,6 +730,15 @@ def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_in
     R.wgrad(bp.lr_conv, trunk, cp, zc + 64, 0, ws.dU0, 64, 0, H, W)
     R.dgrad_in(bp.lr_conv, ws.dU0, 64, 0, 64, H, W, ws.dZl, 8)
     R.dgrad(bp.lr_conv, ws.dU0, 64, 0, 64, H, W, ws.GA, 64, zc, accumulate=False)
+    pts, hi = (_emit_points(bp, seg[1]), [bp.flat_n]) if seg is not None else (set(), [0])
+
+    def slice_to(lo):  # the finished suffix's weight gradients into the flat gradient, reference layout
+        R.join()
+        seg[0][lo:hi[0]].add_(bp.dw.index_select(0, bp.gidx[lo:hi[0]]))
+        hi[0] = lo
+        return lo
+    if bp.lr_conv_lo in pts:
+        yield slice_to(bp.lr_conv_lo)
     # RRDBs, last to first: o = 0.2·RDB3(RDB2(RDB1(x))) + x
     D0, D1 = ws.D
     dcp, d4 = ws.dcp, zc + 192
@@ -718,16 +764,23 @@ def generator_backward(net, cem, ws, d_out, latent, M, need_params=True, need_in
             if need_input and zc:  # latent-slot gradient of this RRDB's blocks, back to fp32
                 _lib.check(lib.esr_axpby_gs(ws.dZl.data_ptr(), 8, 0, 0, 1.0, ws.dZl.data_ptr(), 8, 0, 0, 1.0,
                                             ws.dzs.data_ptr(), 8, 0, 1, 8, Bn, H, W, amax, ovf, stream), 'axpby_gs')
-            continue
-        R.axpby(D0, dcp, d4, 0.2, ws.GA, 64, 0, C=64, h=H, w=W)
-        for j, (dc, dn) in zip((2, 1, 0), ((D0, D1), (D1, D0), (D0, D1))):
-            _rdb_backward(R, Q[3 * k + j], dc, bp.rdb[3 * k + j], bp.rdb_fused[3 * k + j], zc, cp, H, W, (dn, dcp, d4))
-        R.axpby(ws.GA, 64, 0, 1.0, ws.GA, 64, 0, 1.0, D1, dcp, d4, C=64, h=H, w=W)
+        else:
+            R.axpby(D0, dcp, d4, 0.2, ws.GA, 64, 0, C=64, h=H, w=W)
+            for j, (dc, dn) in zip((2, 1, 0), ((D0, D1), (D1, D0), (D0, D1))):
+                _rdb_backward(R, Q[3 * k + j], dc, bp.rdb[3 * k + j], bp.rdb_fused[3 * k + j], zc, cp, H, W,
+                              (dn, dcp, d4))
+            R.axpby(ws.GA, 64, 0, 1.0, ws.GA, 64, 0, 1.0, D1, dcp, d4, C=64, h=H, w=W)
+        if bp.rrdb_lo[k] in pts:
+            yield slice_to(bp.rrdb_lo[k])
     # conv_first: dL/dfea = trunk gradient + LR_conv skip
     R.axpby(ws.GA, 64, 0, 1.0, ws.GA, 64, 0, 1.0, ws.dU0, 64, 0, C=64, h=H, w=W)
     R.wgrad(bp.first, ws.first, ws.first_cp, ws.first_cp, 0, ws.GA, 64, 0, H, W)
     R.join()
-    flat = bp.dw.index_select(0, bp.gidx) if need_params else None  # all parameter gradients, reference layout
+    if seg is not None:
+        slice_to(0)  # the last slice; the caller launches the rest of the buckets after this segment
+        flat = None
+    else:
+        flat = bp.dw.index_select(0, bp.gidx) if need_params else None  # all parameter gradients, reference layout
     dx = None
     if need_input:
         R.dgrad_in(bp.first, ws.GA, 64, 0, 64, H, W, ws.dFirst, ws.first_cp)
@@ -785,6 +838,54 @@ def _run_graphed(ws, key, fn, *inputs):
     for st, t in zip(static, inputs):
         st.copy_(t)
     g.replay()
+    return out, True
+
+
+def _run_graphed_segments(ws, key, it_fn, d_out, on_seg):
+    """_run_graphed for a backward that yields at segment boundaries (backward_segments with seg): the work up to each
+    yield, and after the last one, is one HIP graph (all in one memory pool), and on_seg(lo) runs on the host after a
+    segment is enqueued — eagerly the first time, captured the second (the captures enqueue nothing: every graph is
+    replayed after them), replayed from then on — then on_seg(0) after the last segment.  Returns the backward's
+    result (flat None, input gradient) and whether it came from graphs."""
+    def eager(x):
+        it = it_fn(x)
+        while True:
+            try:
+                lo = next(it)
+            except StopIteration as e:
+                on_seg(0)
+                return e.value
+            on_seg(lo)
+    if not USE_GRAPHS:
+        GRAPH_COUNTS['eager'] += 1
+        return eager(d_out), False
+    ent = ws.graphs.get(key)
+    if ent is None:
+        ws.graphs[key] = 'seen'
+        GRAPH_COUNTS['eager'] += 1
+        return eager(d_out), False
+    if ent == 'seen':
+        static = d_out.detach().clone()
+        pool = torch.cuda.graph_pool_handle()
+        it = it_fn(static)
+        segs, out = [], None
+        while out is None:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                try:
+                    lo = next(it)
+                except StopIteration as e:
+                    lo, out = 0, (e.value,)
+            segs.append((g, lo))
+        ent = ws.graphs[key] = (segs, static, out[0])
+        GRAPH_COUNTS['captured'] += 1
+    else:
+        GRAPH_COUNTS['replayed'] += 1
+    segs, static, out = ent
+    static.copy_(d_out)
+    for g, lo in segs:
+        g.replay()
+        on_seg(lo)
     return out, True
 
 
@@ -854,6 +955,10 @@ class _GeneratorFn(torch.autograd.Function):
         x3 = DGRAD_X3 and ctx.split and (need_params or need_input)
         if x3:
             bp.x3_fused()  # x3 repack of the data-gradient weights, outside any graph
+        sink = getattr(ctx.net, '_esr_grad_sink', None)
+        if ctx.flat_fg is not None and sink is not None and sink.armed and sink.flat_opt is ctx.flat_fg and \
+                need_params and not need_input and (not x3 or _DEFERRED[0] is not None):
+            return _GeneratorFn._sliced_backward(ctx, d_out, bp, x3, sink)
 
         def run(x3):
             key = ('bwd', tuple(d_out.shape), _cem_key(ctx.cem), ctx.M, need_params, need_input, id(bp), ctx.split,
@@ -890,10 +995,37 @@ class _GeneratorFn(torch.autograd.Function):
             fg._sync_views()
             fg.flat.grad.add_(flat)
             grads = {}
+            sink = getattr(ctx.net, '_esr_grad_sink', None)
+            if sink is not None and sink.flat_opt is fg:
+                sink.ready_from(0)  # (no per-parameter accumulation: the sink's hooks would not see this gradient)
         else:
             grads = _split_grads(bp, flat) if flat is not None else {}
         ctx.owner.done = True  # the workspace may be reused (a retained graph's second backward would then raise)
         return (dx, None, None) + tuple(grads.get(p) for p in ctx.params)
+
+    @staticmethod
+    def _sliced_backward(ctx, d_out, bp, x3, sink):
+        """Across ranks (SRRaGANModel's generator step, last accumulation micro-step): the backward adds its weight
+        gradients into the optimiser's flat gradient itself, slice by slice from the output end, and after each slice
+        hands the finished range to the flat-mode GradBuckets `sink`, whose buckets' all-reduces then run while the
+        rest of the backward does (the whole generator is one autograd node: through autograd the gradient would
+        arrive only after all of it).  Only with the x3 overflow check deferred (a redo restores flat.grad from the
+        step's snapshot) or an exact-fp32 backward."""
+        fg = ctx.flat_fg
+        fg._sync_views()
+        if not fg.accepts_flat_grad(bp.params):
+            raise RuntimeError('esr_amd: flat gradient layout differs from the optimiser\'s buffer')
+        lows = tuple(sink.emit_offsets())
+        key = ('bwdseg', tuple(d_out.shape), _cem_key(ctx.cem), ctx.M, id(bp), ctx.split, x3, ctx.act_scale,
+               fg.flat.grad.data_ptr(), lows)
+        it_fn = lambda g: backward_segments(ctx.net, ctx.cem, ctx.ws, g, ctx.latent, ctx.M, need_params=True,  # noqa
+                                            need_input=False, split=ctx.split, x3=x3, act_scale=ctx.act_scale,
+                                            seg=(fg.flat.grad, lows))
+        _run_graphed_segments(ctx.ws, key, it_fn, d_out.contiguous(), sink.ready_from)
+        if x3:
+            _DEFERRED[0].add(ctx.ws.bwd_overflow, bp._x3_bad, bp.reset_x3)
+        ctx.owner.done = True
+        return (None, None, None, None)
 
 
 def generator_forward_train(net, x, cem):

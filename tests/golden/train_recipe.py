@@ -15,23 +15,23 @@ def train_opt(cfg):
         'path': {'log': '/tmp/esr_golden_train_log', 'models': '/tmp/esr_golden_train_models',
                  'pretrain_model_G': None, 'pretrain_model_D': None},
         'datasets': {'train': {'patch_size': patch, 'batch_size': cfg['batch']}},
-        'network_G': {'which_model_G': 'RRDB_net', 'CEM_arch': 1, 'latent_input': 'all_layers',
+        'network_G': {'which_model_G': 'RRDB_net', 'CEM_arch': cfg.get('cem_arch', 1), 'latent_input': 'all_layers',
                       'latent_input_domain': 'HR_downscaled', 'latent_channels': 'SVDinNormedOut_structure_tensor',
                       'norm_type': None, 'mode': 'CNA', 'nf': 64, 'nb': cfg['nb'], 'in_nc': 3, 'out_nc': 3, 'gc': 32,
                       'group': 1, 'scale': 4},
         'network_D': {'which_model_D': 'discriminator_vgg_128', 'relativistic': cfg['relativistic'],
                       'decomposed_input': 0, 'pre_clipping': 0, 'add_quantization_noise': 0, 'norm_type': 'batch',
                       'act_type': 'leakyrelu', 'mode': 'CNA', 'n_layers': 6, 'nf': 64, 'in_nc': 3},
-        'train': {'resume': 0, 'lr_G': cfg['lr'], 'weight_decay_G': 0, 'beta1_G': 0.9, 'lr_D': cfg['lr'],
+        'train': {'resume': 0, 'lr_G': cfg['lr'], 'weight_decay_G': 0, 'beta1_G': 0.9, 'lr_D': cfg.get('lr_D', cfg['lr']),
                   'lr_E': 1e-4, 'lr_latent': cfg['lr'], 'weight_decay_D': 0, 'beta1_D': 0.9,
                   'lr_scheme': 'MultiStepLR', 'lr_steps': [50000], 'lr_gamma': cfg.get('lr_gamma', 0.5),
                   'steps_4_loss_std': cfg.get('steps_4_loss_std'), 'std_4_lr_drop': cfg.get('std_4_lr_drop'),
-                  'pixel_domain': 'HR',
-                  'pixel_criterion': 'l1', 'feature_domain': 'HR', 'feature_criterion': 'l1', 'gan_type': 'wgan-gp',
+                  'pixel_domain': cfg.get('pixel_domain', 'HR'),
+                  'pixel_criterion': cfg.get('pixel_criterion', 'l1'), 'feature_domain': 'HR', 'feature_criterion': 'l1', 'gan_type': 'wgan-gp',
                   'optimalZ_loss_type': None, 'D_verification': cfg['D_verification'],
                   'min_D_prob_ratio_4_G': cfg['min_D_prob_ratio_4_G'], 'min_mean_D_correct': cfg['min_mean_D_correct'],
                   'D_update_ratio': cfg['D_update_ratio'], 'D_valid_Steps_4_G_update': cfg['D_valid_steps'],
-                  'CEM_exp': 1, 'pixel_weight': 0, 'feature_weight': 0, 'gan_weight': 1, 'latent_weight': 0,
+                  'CEM_exp': 1, 'pixel_weight': cfg.get('pixel_weight', 0), 'feature_weight': 0, 'gan_weight': 1, 'latent_weight': 0,
                   'optimalZ_loss_weight': 0, 'range_weight': 5000, 'highpass_weight': 0, 'shift_invariant_weight': 0,
                   'D_init_iters': 0, 'E_init_iters': 40000, 'gp_weigth': 10,
                   'grad_accumulation_steps_G': cfg['acc'], 'grad_accumulation_steps_D': cfg['acc']},
@@ -61,6 +61,16 @@ TRAIN_CFGS = {
     'adaptive_rel': dict(nb=1, batch=2, lr_size=40, lr=1e-4, relativistic=1, D_update_ratio=0,
                          D_verification=None, D_valid_steps=2, min_D_prob_ratio_4_G=1.0,
                          min_mean_D_correct=0.0, acc=1, steps=8, seed=600),
+    # the G pixel loss (SRRaGAN_model.py:108-120, 477-483) at the JSON's commented default weight 1e-2
+    # (train_esrgan_CEM.json:100): L1 in the HR domain with the CEM generator; L2 in the LR domain ('pixel_domain':
+    # 'LR', bilinear Convert_2_LR) with the plain latent generator (the reference asserts HR with CEM_arch, :61)
+    'pixel_l1_hr': dict(nb=1, batch=2, lr_size=40, lr=1e-4, relativistic=1, D_update_ratio=1,
+                        D_verification=None, D_valid_steps=1, min_D_prob_ratio_4_G=1.0, min_mean_D_correct=0.0,
+                        acc=1, steps=6, seed=650, pixel_weight=1e-2, pixel_criterion='l1', pixel_domain='HR'),
+    'pixel_l2_lr': dict(nb=1, batch=2, lr_size=40, lr=1e-4, relativistic=0, D_update_ratio=1,
+                        D_verification=None, D_valid_steps=1, min_D_prob_ratio_4_G=1.0, min_mean_D_correct=0.0,
+                        acc=1, steps=6, seed=660, pixel_weight=1e-2, pixel_criterion='l2', pixel_domain='LR',
+                        cem_arch=0),
 }
 CKPT_CFG = dict(nb=1, batch=2, lr_size=40, lr=1e-4, relativistic=0, D_update_ratio=1, D_verification=None,
                 D_valid_steps=1, min_D_prob_ratio_4_G=1.0, min_mean_D_correct=0.0, acc=1, steps=0, seed=700)

@@ -7,7 +7,7 @@ bound is the reference's own float32 distance to its float64 run × 5 plus a flo
 (conftest.grad_parity's yardstick), evaluated through K seeded random projections where the fixture cannot hold the
 full float64 tensors.  Config 3: the float32 distance is the largest over the plain reference run and its
 rounding-perturbed runs (f32p*, make_golden_train.py c3p), as in the training-loop test; the bound of the plain run
-alone is reported beside it ('worst_frac_of_single_run_bound')."""
+alone is reported beside it ('worst_frac_of_single_run_bound') and capped at SINGLE_RUN_CEILING."""
 import contextlib
 import json
 import os
@@ -22,6 +22,9 @@ for _p in (HERE, os.path.join(HERE, 'golden'), os.path.dirname(HERE)):
         sys.path.insert(0, _p)
 
 FACTOR, FLOOR = 5.0, 1e-4
+# config 3 also caps the error against the plain single float32 run's bound, so that the wider ensemble yardstick cannot
+# hide a drift (round 5: x3 87.0 %, f32 under the three upsampler folds 80.7 / 104.5 / 80.9 % of it)
+SINGLE_RUN_CEILING = 1.25
 
 
 def _proj(v, seed, idx, k):
@@ -115,6 +118,9 @@ def c3_training_step(dev, precision='x3', d_precision=None):
             worst1 = max(worst1, _close(mine, d['f32_Dbuf:' + k], d['f64_Dbuf:' + k])[2])
             if not ok:
                 fails.append(('D buffer', k, msg))
+    if worst1 > SINGLE_RUN_CEILING:
+        fails.append(('single-run bound', 'worst at %.1f %% of the plain float32 run\'s bound (ceiling %.0f %%)' % (
+            100 * worst1, 100 * SINGLE_RUN_CEILING)))
     return _result(fails, worst, lines, worst1)
 
 

@@ -5,12 +5,13 @@ driver's 8-GPU run takes the same code path with the nccl backend).  The referen
 nn.DataParallel over the GPUs (models/networks.py:99-101,125-126) with batch_size *= nGPU (options/options.py:85-87).
 
 * identical batches on both ranks: the ranks agree bit for bit, and they agree with the single-process run to
-  rounding level (every tensor within 1e-5 relative L2; run to run the two-rank step is not bitwise reproducible,
-  ~1e-7 relative in the weights) — except the biases of the discriminator convs that feed a BatchNorm and the BN
-  running means: their gradient is analytically zero, its computed value is the rounding noise of a cancelling sum,
-  and Adam's m / sqrt(v) turns any change in that noise into a learning-rate-sized step (observed 1e-3..6e-1
-  relative; bounded here by lr per step, and for the running means, which carry those biases, by 1e-3 relative or
-  the same absolute bound);
+  rounding level.  Asserted thresholds: the averaged gradient of each optimiser's FIRST step within 1e-5 relative L2
+  of the single-process one; every parameter after the 6 micro-steps within 1e-3 relative L2 (Adam amplifies
+  rounding-level gradient differences into lr-sized steps for elements whose gradient is ~0; run to run the two-rank
+  step is not bitwise reproducible, ~1e-7 relative in the weights); the biases of the discriminator convs that feed a
+  BatchNorm within 2·lr·steps absolute (their gradient is analytically zero, its computed value the rounding noise
+  of a cancelling sum, observed 1e-3..6e-1 relative), and the BN running means, which carry those biases, within
+  1e-3 relative or that absolute bound;
 * different batches per rank: the ranks end with the same parameters and took the same generator_step decisions.
 """
 import hashlib

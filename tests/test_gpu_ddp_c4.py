@@ -1,0 +1,163 @@
+"""Config 4's data-parallel step at its PER-RANK production shape (B=16 × 96² LR crops per rank, RRDB-23, latent, CEM
+train mode, WGAN-GP as shipped) on the box's one GPU: two ranks on GPU 0 over gloo (as bench_launch's ESR_SHARE_GPU
+rehearsal: RCCL needs a GPU per rank; the driver's 8-GPU run takes the same code with nccl) against single-process
+runs of each rank's half of a B=32 batch.
+
+The reference's counterpart is nn.DataParallel (models/networks.py:99-101,125-126) over a batch of nGPU × 16
+(options/options.py:85-87): each replica's BatchNorm normalises its own 16 images, every loss is a mean over the
+gathered 32 (wgan-gp: linear in the D outputs), so the DataParallel gradient is the average of the gradients each
+replica's half would give alone.  Checked: the first D step's and the first G step's averaged gradients (two ranks)
+against the mean of the two single-process half-batch gradients, ≤ 1e-5 relative L2 (the D learning rate is 0 so
+that the G step of micro-step 1 sees the same D in every run), the generator_step decisions, and that the G
+gradient's all-reduce buckets went out from inside the generator's backward while it still had RRDBs to do
+(train_engine._GeneratorFn._sliced_backward with the flat-mode GradBuckets), with the optimiser's flat buffer as the
+one autograd input (the single-process step's flat path) and one D BatchNorm-buffer broadcast per D step."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _cfg():
+    from train_recipe import C3_GRID_CFG
+    return dict(C3_GRID_CFG, lr_D=0.0)
+
+
+def _run_half(half, dev):
+    """One SRRaGANModel on images [16·half, 16·half + 16) of the B=32 batch, 2 micro-steps: the gradient each
+    optimiser applies first, the generator_step flags, and the sliced-backward / broadcast records."""
+    from train_recipe import step_data, train_opt
+    from oracle.recipe import seeded_params
+    from esr_amd.SRRaGAN_model import SRRaGANModel
+    import torch.distributed as dist
+    cfg = _cfg()
+    B = cfg['batch']
+    torch.manual_seed(0)
+    model = SRRaGANModel(train_opt(cfg), accumulation_steps_per_batch=cfg['acc'], device=dev)
+    gsd, dsd = model.netG.state_dict(), model.netD.state_dict()
+    gp = seeded_params([(k, tuple(v.shape)) for k, v in gsd.items()], cfg['seed'], w_scale=cfg['w_scale_G'])
+    dp = seeded_params([(k, tuple(v.shape)) for k, v in dsd.items() if 'running' not in k and 'num_batches' not in k],
+                       cfg['seed'] + 1, w_scale=1.0)
+    model.netG.load_state_dict({k: torch.from_numpy(v) for k, v in gp.items()}, strict=False)
+    model.netD.load_state_dict({k: torch.from_numpy(v) for k, v in dp.items()}, strict=False)
+    rng = np.random.default_rng(cfg['seed'] + 300 + half)
+    model._interp_points = lambda n: torch.from_numpy(rng.random((n, 1, 1, 1)).astype(np.float32)).to(dev)
+    first = {}
+    for o, tag in ((model.optimizer_G, 'G'), (model.optimizer_D, 'D')):
+        def step(*a, _o=o, _step=o.step, _tag=tag, **kw):
+            if _tag not in first:
+                _o._sync_views()
+                first[_tag] = _o.flat.grad.detach().double().cpu().numpy()
+            return _step(*a, **kw)
+        o.step = step
+    slices = []  # (lo, buckets launched so far) at each ready_from of the G buckets
+    rf = model._g_buckets.ready_from
+
+    def ready_from(lo):  # (also the flat parameter's post-accumulate hook: must return None)
+        rf(lo)
+        slices.append((lo, model._g_buckets.launched_in_backward))
+    model._g_buckets.ready_from = ready_from
+    bcast = []  # torch.distributed.broadcast calls during the steps (the D BatchNorm buffers)
+    bb = dist.broadcast
+    dist.broadcast = lambda *a, **k: (bcast.append(1), bb(*a, **k))[1]
+    flat_in = []
+    import esr_amd.train_engine as TE
+    fwd = TE._GeneratorFn.apply
+    TE._GeneratorFn.apply = lambda *a: (flat_in.append(len(a) == 4), fwd(*a))[1]
+    try:
+        flags = []
+        for k in range(cfg['steps']):
+            lr, hr, z = step_data(dict(cfg, batch=2 * B), k)
+            sl = slice(half * B, (half + 1) * B)
+            t = lambda a: torch.from_numpy(np.ascontiguousarray(a[sl])).to(dev)  # noqa: E731
+            model.feed_data({'LR': t(lr), 'HR': t(hr), 'Z': t(z)})
+            model.optimize_parameters()
+            flags.append(bool(model.generator_step))
+    finally:
+        dist.broadcast = bb
+        TE._GeneratorFn.apply = fwd
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    n_buckets = len(model._g_buckets.buckets)
+    return {'first': first, 'flags': flags, 'slices': slices, 'n_buckets': n_buckets, 'bcast': len(bcast),
+            'flat_in': flat_in, 'world': world, 'comm': model._g_buckets.comm_stats()}
+
+
+def _worker(rank, world, port, q):
+    for p_ in (HERE, os.path.join(HERE, 'golden'), os.path.dirname(HERE),
+               os.path.join(os.path.dirname(HERE), 'explorable-super-resolution_old_amd')):
+        if p_ not in sys.path:
+            sys.path.insert(0, p_)
+    import torch.distributed as dist
+    try:
+        dev = torch.device('cuda', 0)
+        torch.cuda.set_device(dev)
+        if world > 1:
+            os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+            dist.init_process_group('gloo', rank=rank, world_size=world)
+            out = [_run_half(rank, dev)]
+        else:
+            out = []
+            for half in (0, 1):
+                out.append(_run_half(half, dev))
+                torch.cuda.empty_cache()
+        q.put((rank, out, None))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+    finally:
+        if world > 1 and dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def _run(world):
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(60)
+    for r in res:
+        assert r[2] is None, r[2]
+    return res
+
+
+def test_c4_two_ranks_per_rank_production_shape():
+    halves = _run(1)[0][1]
+    ranks = [r[1][0] for r in _run(2)]
+    assert halves[0]['flags'] == halves[1]['flags'] == ranks[0]['flags'] == ranks[1]['flags'] == [False, True]
+    for tag in ('D', 'G'):
+        ref = 0.5 * (halves[0]['first'][tag] + halves[1]['first'][tag])
+        for r in ranks:
+            rel = float(np.linalg.norm(r['first'][tag] - ref) / np.linalg.norm(ref))
+            print('C4 per-rank shape: first %s step, averaged two-rank gradient vs the mean of the single-process '
+                  'half-batch gradients: %.2e relative L2' % (tag, rel))
+            assert rel <= 1e-5, (tag, rel)
+    for r in ranks:
+        # the G buckets went out from inside the generator's backward, most of them while RRDBs were still to come
+        early = max([n for lo, n in r['slices'] if lo > 0] or [0])
+        print('G buckets: %d; launched at the backward\'s slices (lo, count): %s; comm %s' % (
+            r['n_buckets'], r['slices'], r['comm']))
+        assert r['n_buckets'] >= 4 and early >= r['n_buckets'] - 1, (r['slices'], r['n_buckets'])
+        assert r['slices'][-1] == (0, r['n_buckets'])
+        assert r['comm']['allreduces'] == r['n_buckets']  # one G gradient step: every bucket once
+        assert all(r['flat_in']) and r['flat_in']  # the flat parameter as the generator's one autograd input
+        assert r['bcast'] == 2  # one D-buffer broadcast per D step (two D steps), not one per buffer
+    for h in halves:
+        assert all(h['flat_in']) and h['slices'] == [] and h['world'] == 1

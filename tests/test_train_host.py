@@ -200,3 +200,139 @@ def test_ddp_gradient_average_and_consistent_statistics():
     assert res[0][15][0] and res[1][15][0]  # FlatAdam + buckets == per-tensor Adam + flat average
     assert res[0][15][1] == res[1][15][1]   # and the ranks hold the same parameters
     assert all(res[0][16]) and all(res[1][16])  # comm_stats: one all-reduce per bucket, every gradient byte once
+
+
+class _SlicedFlat(torch.autograd.Function):
+    """A stand-in for the HIP generator's sliced backward (train_engine._GeneratorFn._sliced_backward) over a toy
+    linear model y = x @ W: the autograd input is the optimiser's flat parameter, the backward adds its gradient into
+    flat.grad itself from the END of the flat buffer in chunks, calling the flat-mode GradBuckets sink after each, and
+    returns no gradient for the flat parameter."""
+
+    @staticmethod
+    def forward(ctx, x, flat, shape, sink, chunks):
+        ctx.save_for_backward(x)
+        ctx.shape, ctx.sink, ctx.chunks, ctx.flat = shape, sink, chunks, flat
+        return x @ flat.view(shape)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, = ctx.saved_tensors
+        g = (x.t() @ gy).reshape(-1)
+        n = g.numel()
+        hi = n
+        for lo in sorted(ctx.chunks, reverse=True) + [0]:
+            ctx.flat.grad[lo:hi] += g[lo:hi]
+            hi = lo
+            ctx.sink.ready_from(lo)
+            _SlicedFlat.launched_at.append(ctx.sink.launched_in_backward)
+        return None, None, None, None, None
+
+
+def _flat_dist_worker(rank, world, port, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        # (1) flat-mode GradBuckets fed by a producer that writes the flat gradient in slices (the sliced G backward)
+        torch.manual_seed(3)
+        ps = [torch.nn.Parameter(torch.randn(8, 4)) for _ in range(4)]  # 4 x 32 floats = 4 x 128 B
+        ref = [p.detach().clone() for p in ps]
+        opt = FlatAdam(ps, lr=1e-2, foreach=False)
+        sink = M.GradBuckets(ps, cap_bytes=256, flat_opt=opt)  # 2 parameters per bucket: 2 buckets
+        x = torch.randn(5, 32, generator=torch.Generator().manual_seed(20 + rank))
+        opt.zero_grad()
+        sink.arm()
+        _SlicedFlat.launched_at = []  # bucket count after each slice of the backward
+        y = _SlicedFlat.apply(x, opt.flat, (32, 4), sink, [lo for lo in sink.emit_offsets() if lo > 0])
+        y.square().sum().backward()
+        launched = (sink.launched_in_backward, list(_SlicedFlat.launched_at))
+        sink.finish()
+        # reference: autograd through the plain parameters, then one flat average
+        W = torch.cat([r.reshape(-1) for r in ref]).view(32, 4).requires_grad_(True)
+        (x @ W).square().sum().backward()
+        gref = W.grad.reshape(-1).clone()
+        dist.all_reduce(gref)
+        gref /= world
+        flat_ok = torch.allclose(opt.flat.grad, gref, rtol=1e-6, atol=1e-6)
+        views_ok = all(p.grad.data_ptr() == opt.flat.grad[o:o + p.numel()].data_ptr()
+                       for p, o in zip(ps, range(0, 128, 32)))
+        cs = sink.comm_stats()
+        # (2) the D BatchNorm buffers as one flat tensor: ONE broadcast carries all of them (rank 0's values)
+        bnet = torch.nn.Sequential(torch.nn.BatchNorm2d(3), torch.nn.BatchNorm2d(5))
+        for m in bnet:
+            m.running_mean.fill_(rank + 1.0)
+            m.running_var.fill_(10.0 * (rank + 1))
+        fb = M.FlatBuffers(bnet)
+        calls = []
+        orig = dist.broadcast
+        dist.broadcast = lambda *a, **k: (calls.append(1), orig(*a, **k))[1]
+        try:
+            M._broadcast_buffers(bnet, fb)
+        finally:
+            dist.broadcast = orig
+        bufs = (len(calls), [float(m.running_mean[0]) for m in bnet], [float(m.running_var[-1]) for m in bnet],
+                [int(m.num_batches_tracked) for m in bnet])
+        # (3) relativistic vanilla GAN loss with the global-batch means (DataParallel gathers the batch):
+        # the ranks' averaged D gradient equals the single-process gradient over the concatenated batch
+        torch.manual_seed(5)
+        Dnet = torch.nn.Linear(6, 1)
+        Dref = copy.deepcopy(Dnet)
+        real = torch.randn(4, 6, generator=torch.Generator().manual_seed(40 + rank))
+        fake = torch.randn(4, 6, generator=torch.Generator().manual_seed(50 + rank))
+        m = M.SRRaGANModel.__new__(M.SRRaGANModel)
+        m.cri_gan = L.GANLoss('vanilla')
+        pr, pf = Dnet(real), Dnet(fake)
+        l_real = m.cri_gan(pr - m._batch_mean(pf), True)
+        l_fake = m.cri_gan(pf - m._batch_mean(pr), False)
+        ((l_real + l_fake) / 2).backward()
+        M._allreduce_grads(list(Dnet.parameters()))
+        allr = [torch.zeros_like(real) for _ in range(world)]
+        allf = [torch.zeros_like(fake) for _ in range(world)]
+        dist.all_gather(allr, real)
+        dist.all_gather(allf, fake)
+        R_, F_ = torch.cat(allr), torch.cat(allf)
+        prg, pfg = Dref(R_), Dref(F_)
+        lr_g = m.cri_gan(prg - pfg.mean(), True)
+        lf_g = m.cri_gan(pfg - prg.mean(), False)
+        ((lr_g + lf_g) / 2).backward()
+        rel = all(torch.allclose(a.grad, b.grad, rtol=1e-5, atol=1e-7) for a, b in zip(Dnet.parameters(),
+                                                                                       Dref.parameters()))
+        # the logged losses averaged over ranks are the global-batch losses
+        logs = m._global_log_means([l_real, l_fake])
+        log_ok = abs(float(logs[0]) - float(lr_g)) < 1e-6 and abs(float(logs[1]) - float(lf_g)) < 1e-6
+        # rank-local means would NOT give the global gradient for this non-linear loss (the test can tell them apart)
+        Dloc = copy.deepcopy(Dref)
+        Dloc.zero_grad()
+        pr2, pf2 = Dloc(real), Dloc(fake)
+        ((m.cri_gan(pr2 - pf2.mean(), True) + m.cri_gan(pf2 - pr2.mean(), False)) / 2).backward()
+        M._allreduce_grads(list(Dloc.parameters()))
+        local_differs = not all(torch.allclose(a.grad, b.grad, rtol=1e-5, atol=1e-7)
+                                for a, b in zip(Dloc.parameters(), Dref.parameters()))
+        q.put((rank, launched, flat_ok, views_ok, (cs['allreduces'], len(sink.buckets)), bufs, rel, log_ok,
+               local_differs))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ddp_flat_buckets_sliced_backward_global_means():
+    """World size 2 over gloo: (1) flat-mode GradBuckets (the generator's FlatAdam buffer) all-reduced in place by a
+    backward that finalises the flat gradient in slices from its end, with buckets launched before backward() returns;
+    (2) the D BatchNorm buffers in ONE broadcast; (3) relativistic vanilla-GAN terms over the global batch
+    (SRRaGAN_model.py:380-382: torch.mean over DataParallel's gathered batch) give the single-process gradient."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = 31500 + (os.getpid() % 2000)
+    procs = [ctx.Process(target=_flat_dist_worker, args=(r, 2, port, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda t: t[0])
+    for pr in procs:
+        pr.join(60)
+        assert pr.exitcode == 0
+    for r in res:
+        (n_launched, per_slice), flat_ok, views_ok, (n_ar, n_buckets), bufs, rel, log_ok, local_differs = r[1:]
+        assert n_buckets == 2 and n_launched == 2 and per_slice[0] >= 1, (n_launched, per_slice)  # first bucket
+        # went out after the first slice, while the backward still had a slice to produce
+        assert flat_ok and views_ok and n_ar == n_buckets
+        assert bufs == (1, [1.0, 1.0], [10.0, 10.0], [0, 0])
+        assert rel and log_ok and local_differs
