@@ -280,6 +280,12 @@ __global__ __launch_bounds__(256) void cem_inv_tiled(const float *__restrict__ r
     extern __shared__ float smem[];
     const int WP = 64 + ki - 1, WR = 16 + ki - 1;
     float *s = smem;                           // [WR][WP]
+    // The taps are read from LDS (broadcast), not as wave-uniform scalar loads: with SGPR operands the compiler
+    // emitted packed FMAs (v_pk_fma_f32 s[n:n+1]) whose SGPRs the loop's next s_load overwrote, and under concurrent
+    // kernels on the CU the upper lanes of a wave then read the next row's taps (tools/race_probe.py: outputs of two
+    // identical processes in lockstep differed in lanes 48-63 of one packed result).
+    float *sw = smem + WR * WP;
+    for (int k = threadIdx.x; k < ki * ki; k += 256) sw[k] = wi[k];
     const int j0 = blockIdx.x * 64, i0 = blockIdx.y * 16;
     const long long plane = blockIdx.z;
     const float *src = rin + plane * H * W;
@@ -306,7 +312,7 @@ __global__ __launch_bounds__(256) void cem_inv_tiled(const float *__restrict__ r
     float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
     for (int u = 0; u < ki; ++u) {
         const float *sr = s + (ty + u) * WP + 4 * tx;
-        const float *wr = wi + u * ki;  // wave-uniform index: scalar loads through the constant cache
+        const float *wr = sw + u * ki;  // broadcast LDS reads
         float r0 = sr[0], r1 = sr[1], r2 = sr[2];
 #pragma unroll 4
         for (int v = 0; v < ki; ++v) {
@@ -426,6 +432,8 @@ __global__ __launch_bounds__(256) void cem_up_add_win4(const float *__restrict__
     constexpr int sf = 4, kd = KD, pd = KD / 2;
     constexpr int QC = (255 + kd - 1) / sf + 3, QR = (3 + kd - 1) / sf + 3;
     __shared__ float sq[QR * QC];
+    __shared__ float sw[KD * KD];  // the taps, read from LDS (broadcast), not as scalar loads: see cem_inv_tiled
+    for (int k = threadIdx.x; k < KD * KD; k += 256) sw[k] = wu[k];
     const int HH = sf * H, WW = sf * W, OH = HH - 2 * M, OW = WW - 2 * M;
     const int X0 = blockIdx.x * 256, Y0 = blockIdx.y * 4;
     const long long plane = blockIdx.z;
@@ -453,7 +461,7 @@ __global__ __launch_bounds__(256) void cem_up_add_win4(const float *__restrict__
         float qv[5];
 #pragma unroll
         for (int k = 0; k < 5; ++k) qv[k] = qrow[k];
-        const float *wr = wu + u * kd;  // wave-uniform row
+        const float *wr = sw + u * kd;  // wave-uniform row, broadcast LDS reads
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int v0 = (C0 - e) & 3, off = e > C0 ? 1 : 0;
@@ -591,7 +599,7 @@ extern "C" int esr_cem_down(const float *gen, const float *lr, float *r, int32_t
 extern "C" int esr_cem_inv(const float *r, float *q, int32_t B, int32_t H, int32_t W, const float *w_inv, int32_t ki,
                            esr_stream_t stream) {
     if (!r || !q || !w_inv || B <= 0 || H <= 0 || W <= 0 || ki <= 0 || ki > MAXK || !(ki & 1)) return ESR_EINVAL;
-    const size_t lds = 4 * (size_t)(16 + ki - 1) * (64 + ki - 1);
+    const size_t lds = 4 * ((size_t)(16 + ki - 1) * (64 + ki - 1) + (size_t)ki * ki);
     if (lds <= 64 * 1024 && !g_cem_direct) {
         hipLaunchKernelGGL(cem_inv_tiled, dim3((W + 63) / 64, (H + 15) / 16, B * 3), dim3(256), lds,
                            (hipStream_t)stream, r, q, H, W, w_inv, ki);

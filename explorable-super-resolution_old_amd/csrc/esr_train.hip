@@ -1270,6 +1270,8 @@ __global__ __launch_bounds__(256) void cem_adjoint_s1_tiled(AdjParams p) {
     extern __shared__ float smem[];
     const int K = p.K, pd = K / 2, WP = 64 + K - 1, WR = 16 + K - 1;
     float *sw = smem;                           // [WR][WP]
+    float *swt = smem + WR * WP;                // the K × K taps (read from LDS: see cem_inv_tiled)
+    for (int k = threadIdx.x; k < K * K; k += 256) swt[k] = p.w[k];
     const int j0 = blockIdx.x * 64, i0 = blockIdx.y * 16;
     const long long plane = blockIdx.z;
     const float *g = p.g + plane * p.Oy * p.Ox;
@@ -1287,7 +1289,7 @@ __global__ __launch_bounds__(256) void cem_adjoint_s1_tiled(AdjParams p) {
     for (int uy = 0; uy < K; ++uy) {
         // window row K-1-uy, columns 4tx + (K-1-ux) (+ e for output e): ux ascending = columns descending
         const float *sr = sw + (ty + K - 1 - uy) * WP + 4 * tx;
-        const float *wr = p.w + uy * K;  // wave-uniform: scalar loads
+        const float *wr = swt + uy * K;  // broadcast LDS reads (not scalar loads: cem_inv_tiled)
         float r1 = sr[K - 1 + 1], r2 = sr[K - 1 + 2], r3 = sr[K - 1 + 3];
         for (int ux = 0; ux < K; ++ux) {
             const int v = K - 1 - ux;
@@ -1639,7 +1641,7 @@ extern "C" int esr_cem_adjoint(const float *g, int32_t planes, int32_t Oy, int32
     p.os = os; p.oc = oc; p.Ny = (Ly - oc + os - 1) / os; p.Nx = (Lx - oc + os - 1) / os; p.planes = planes;
     p.alpha = alpha; p.accumulate = flags & 1; p.fast = !(flags & 2);
     if (p.fast && s == 1 && os == 1 && oc == 0 && Ly >= 3 && Lx >= 3) {  // the inverse filter's adjoint: tiled
-        const size_t lds = (size_t)(16 + K - 1) * (64 + K - 1) * sizeof(float);
+        const size_t lds = ((size_t)(16 + K - 1) * (64 + K - 1) + (size_t)K * K) * sizeof(float);
         hipLaunchKernelGGL(cem_adjoint_s1_tiled, dim3((p.Nx + 63) / 64, (p.Ny + 15) / 16, planes), dim3(256), lds,
                            (hipStream_t)stream, p);
         hipLaunchKernelGGL(cem_adjoint_border_kernel, dim3((unsigned)((long long)planes * (2 * p.Nx + 2 * (p.Ny - 2)))),

@@ -64,8 +64,15 @@ def _run_half(half, dev):
                 first[_tag] = _o.flat.grad.detach().double().cpu().numpy()
             return _step(*a, **kw)
         o.step = step
+    local = {}  # rank-local flat gradient ranges as each bucket went out (first launch per tag and range)
+    for tag, bk in [(t_, b_) for t_, b_ in (('G', model._g_buckets), ('D', model._d_buckets)) if b_.ranges]:
+        def launch(b, _bk=bk, _tag=tag, _orig=bk._launch):
+            lo, hi = _bk.ranges[b]
+            local.setdefault(_tag, {}).setdefault((lo, hi), _bk.flat_opt.flat.grad[lo:hi].detach().double().cpu().numpy())
+            return _orig(b)
+        bk._launch = launch
     slices = []  # (lo, buckets launched so far) at each ready_from of the G buckets
-    rf = model._g_buckets.ready_from
+    rf = model._g_buckets.ready_from if model._g_buckets.ranges else (lambda lo: None)
 
     def ready_from(lo):  # (also the flat parameter's post-accumulate hook: must return None)
         rf(lo)
@@ -77,9 +84,22 @@ def _run_half(half, dev):
     flat_in = []
     import esr_amd.train_engine as TE
     fwd = TE._GeneratorFn.apply
-    TE._GeneratorFn.apply = lambda *a: (flat_in.append(len(a) == 4), fwd(*a))[1]
+    fwd_in = []  # (input hash, flat parameter hash, activation scale, precision) of each training forward
+    fresh = []  # generator output norms right after each training forward (the step's end may differ: corruption)
+
+    def apply(*a):
+        flat_in.append(len(a) == 4)
+        out = fwd(*a)
+        fresh.append(out.detach().double().flatten(1).norm(dim=1).cpu().numpy())
+        import hashlib
+        from esr_amd import engine as E_
+        fwd_in.append((hashlib.sha256(a[0].detach().cpu().numpy().tobytes()).hexdigest()[:12],
+                       hashlib.sha256(a[3].detach().cpu().numpy().tobytes()).hexdigest()[:12] if len(a) == 4 else None,
+                       E_.act_scale(a[1]), getattr(a[1], 'esr_precision', None)))
+        return out
+    TE._GeneratorFn.apply = apply
     try:
-        flags = []
+        flags, fake = [], []
         for k in range(cfg['steps']):
             lr, hr, z = step_data(dict(cfg, batch=2 * B), k)
             sl = slice(half * B, (half + 1) * B)
@@ -87,16 +107,28 @@ def _run_half(half, dev):
             model.feed_data({'LR': t(lr), 'HR': t(hr), 'Z': t(z)})
             model.optimize_parameters()
             flags.append(bool(model.generator_step))
+            fake.append(model.fake_H.detach().double().flatten(1).norm(dim=1).cpu().numpy())
     finally:
         dist.broadcast = bb
         TE._GeneratorFn.apply = fwd
     world = dist.get_world_size() if dist.is_initialized() else 1
     n_buckets = len(model._g_buckets.buckets)
-    return {'first': first, 'flags': flags, 'slices': slices, 'n_buckets': n_buckets, 'bcast': len(bcast),
+    dshapes = [(k, v.numel()) for k, v in model.netD.named_parameters()]
+    from esr_amd import engine as E
+    loc = {}
+    for tag, d in local.items():
+        n = max(hi for lo, hi in d)
+        v = np.full(n, np.nan)
+        for (lo, hi), x in d.items():
+            v[lo:hi] = x
+        loc[tag] = v
+    return {'first': first, 'flags': flags, 'fake': fake, 'dshapes': dshapes, 'local': loc, 'fresh': fresh, 'fwd_in': fwd_in,
+            'logs': {k: [x[1] for x in v] for k, v in model.log_dict.items() if v},
+            'reruns': (E.OVERFLOW_RERUNS, E.ACT_SCALE_REDUCTIONS), 'slices': slices, 'n_buckets': n_buckets, 'bcast': len(bcast),
             'flat_in': flat_in, 'world': world, 'comm': model._g_buckets.comm_stats()}
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, half, q):
     for p_ in (HERE, os.path.join(HERE, 'golden'), os.path.dirname(HERE),
                os.path.join(os.path.dirname(HERE), 'explorable-super-resolution_old_amd')):
         if p_ not in sys.path:
@@ -108,14 +140,20 @@ def _worker(rank, world, port, q):
         if world > 1:
             os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
             dist.init_process_group('gloo', rank=rank, world_size=world)
-            out = [_run_half(rank, dev)]
-        else:
-            out = []
-            for half in (0, 1):
-                out.append(_run_half(half, dev))
-                torch.cuda.empty_cache()
-        q.put((rank, out, None))
-    except Exception as e:  # noqa: BLE001
+        if os.environ.get('C4_NOFLAT'):  # diagnostic: '1' = no flat-mode buckets (round-5 per-tensor cat buckets)
+            from esr_amd import SRRaGAN_model as SM
+            init = SM.GradBuckets.__init__
+            SM.GradBuckets.__init__ = lambda self, params, cap_bytes=16 << 20, flat_opt=None: init(self, params,
+                                                                                                   cap_bytes, None)
+        if os.environ.get('C4_SYNC') == '1':  # diagnostic: a device-wide synchronize before every collective
+            from esr_amd import SRRaGAN_model as SM
+            coll = SM.collective
+            SM.collective = lambda *a, **k: (torch.cuda.synchronize(), coll(*a, **k))[1]
+        if os.environ.get('C4_NANFILL') == '1':  # diagnostic: every torch.empty filled with NaN
+            torch.use_deterministic_algorithms(True, warn_only=True)
+            torch.utils.deterministic.fill_uninitialized_memory = True
+        q.put((rank, _run_half(half, dev), None))
+    except Exception:  # noqa: BLE001
         import traceback
         q.put((rank, None, traceback.format_exc()))
     finally:
@@ -123,11 +161,12 @@ def _worker(rank, world, port, q):
             dist.destroy_process_group()
 
 
-def _run(world):
+def _run(world, half=None):
+    """world ranks (rank r on half r), or one single-process run on `half`, each in a fresh process."""
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, r if half is None else half, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda r: r[0])
@@ -135,20 +174,43 @@ def _run(world):
         p.join(60)
     for r in res:
         assert r[2] is None, r[2]
-    return res
+    return [r[1] for r in res]
 
 
 def test_c4_two_ranks_per_rank_production_shape():
-    halves = _run(1)[0][1]
-    ranks = [r[1][0] for r in _run(2)]
+    halves = [_run(1, half=h)[0] for h in (0, 1)]
+    ranks = _run(2)
+    again = _run(1, half=0)[0]
+    print('overflow reruns / act-scale reductions: halves', [h['reruns'] for h in halves], 'ranks',
+          [r['reruns'] for r in ranks], 'half 0 again', again['reruns'])
+    print('half 0 run twice: first D grads equal', np.array_equal(again['first']['D'], halves[0]['first']['D']),
+          'fake_H equal', all(np.array_equal(a, b) for a, b in zip(again['fake'], halves[0]['fake'])))
     assert halves[0]['flags'] == halves[1]['flags'] == ranks[0]['flags'] == ranks[1]['flags'] == [False, True]
     for tag in ('D', 'G'):
         ref = 0.5 * (halves[0]['first'][tag] + halves[1]['first'][tag])
-        for r in ranks:
+        for i, r in enumerate(ranks):
             rel = float(np.linalg.norm(r['first'][tag] - ref) / np.linalg.norm(ref))
+            own = float(np.linalg.norm(r['first'][tag] - halves[i]['first'][tag]) / np.linalg.norm(ref))
             print('C4 per-rank shape: first %s step, averaged two-rank gradient vs the mean of the single-process '
-                  'half-batch gradients: %.2e relative L2' % (tag, rel))
-            assert rel <= 1e-5, (tag, rel)
+                  'half-batch gradients: %.2e relative L2 (vs rank %d\'s own half alone: %.2e; the halves differ by '
+                  '%.2e)' % (tag, rel, i, own, float(np.linalg.norm(halves[0]['first'][tag] - halves[1]['first'][tag]) /
+                                                     np.linalg.norm(ref))))
+            if tag in r['local']:
+                lv = r['local'][tag]
+                print('rank %d local %s gradient (as its buckets went out) vs its half alone: bitwise %s, rel %.2e' % (
+                    i, tag, np.array_equal(lv, halves[i]['first'][tag]),
+                    float(np.linalg.norm(lv - halves[i]['first'][tag]) / np.linalg.norm(halves[i]['first'][tag]))))
+            if rel > 1e-5 and tag == 'D':
+                o, rows = 0, []
+                for k, n in r['dshapes']:
+                    a, b = r['first'][tag][o:o + n], ref[o:o + n]
+                    rows.append((float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)), k,
+                                 float(np.linalg.norm(a - halves[i]['first'][tag][o:o + n]) / max(np.linalg.norm(b), 1e-30))))
+                    o += n
+                print('worst D params (rel err vs avg, vs own half):', sorted(rows)[::-1][:8])
+                print('fake_H norms: rank', [f.tolist() for f in r['fake']], 'half', [f.tolist() for f in halves[i]['fake']])
+                print('logs rank', r['logs'], 'halves', halves[0]['logs'], halves[1]['logs'])
+            assert rel <= 1e-5, (tag, rel, own)
     for r in ranks:
         # the G buckets went out from inside the generator's backward, most of them while RRDBs were still to come
         early = max([n for lo, n in r['slices'] if lo > 0] or [0])
