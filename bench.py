@@ -287,6 +287,26 @@ def host_io(model, x, out, args, dev, world):
             'note': 'PCIe-inclusive: pinned host LR batch in, HR output back to pinned host memory, per step'}
 
 
+def lagged_overflow(model, x, args, dev, world, dt_headline):
+    """The headline step with the x3 overflow flag read one forward late (engine.lagged_overflow_checks: forward N + 1
+    is enqueued before N's flag is read, so the host does not wait for the GPU between forwards; an overflowed N is
+    recomputed into its output in exact fp32).  Timed like the headline, without per-launch events; `value` stays the
+    default per-forward check."""
+    from esr_amd import engine
+    with torch.no_grad():
+        dt0 = _timed(lambda: model(x), args.steps, dev, world)  # the default check, no per-launch events
+        with engine.lagged_overflow_checks():
+            model(x)
+            dt = _timed(lambda: model(x), args.steps, dev, world)
+    hr = 4 * args.lr_size
+    return {'value': round(world * args.batch * hr * hr * args.steps / dt / 1e6, 3), 'unit': 'HR Mpixels/s',
+            'ms_per_step': round(dt / args.steps * 1e3, 3), 'steps': args.steps,
+            'default_check_ms_per_step': round(dt0 / args.steps * 1e3, 3),
+            'headline_ms_per_step': round(dt_headline / args.steps * 1e3, 3),
+            'note': 'overflow flag read one forward late (engine.lagged_overflow_checks), no per-launch events; the '
+                    'headline reads each forward\'s flag before returning and carries events on its last steps'}
+
+
 def run_legs(args, dev, world, rank):
     """Extra legs in the same run, each timed on its own after the headline's timed region (HIP work synchronised,
     barrier, max over ranks): the C2 step in exact fp32, one C3 training step (C4 when N>1: DP over RCCL) and one C5
@@ -478,6 +498,8 @@ def main():
             rec['roofline']['frac_rocprof_union'] = round(fl_all / n_all / (traffic[2] * 1e-6) / 1e12 / peak, 4)
     if args.host_io_steps > 0:
         rec['host_io'] = host_io(model, x, out, args, dev, world)
+    if args.precision == 'x3':
+        rec['lagged_overflow'] = lagged_overflow(model, x, args, dev, world, dt)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb, parity = cpu_baseline(args, model, x, out, None if args.no_cem else make_gt(args, dev, rank))
         if not args.no_cpu_variants:

@@ -24,6 +24,7 @@ Memory plan (per (device, B, H, W, latent) — H×W is the LR grid the generator
 Every buffer holds 4 bytes per channel in either mode (fp32, or an f16 hi/lo pair).  Halos and unused channels are
 zero from allocation and never written.
 """
+import contextlib
 import ctypes
 import math
 import operator
@@ -541,11 +542,11 @@ class _Workspace:
 _WS_SLOT = [0]
 
 
-def _workspace(net, dev, B, H, W, latent, precision):
+def _workspace(net, dev, B, H, W, latent, precision, slot=None):
     # keyed by precision too: the zero padding channels of an fp32 workspace are not zero when read as split-f16 pairs
     sf = getattr(net, 'upscale', SF)
     key = (str(dev), B, H, W, latent, precision, sf)
-    name = 'ws' if _WS_SLOT[0] == 0 else 'ws%d' % _WS_SLOT[0]
+    name = ('ws_' + slot) if slot else ('ws' if _WS_SLOT[0] == 0 else 'ws%d' % _WS_SLOT[0])
     c = net._esr_cache.get(name)
     if c is None or c[0] != key:
         net._esr_cache.pop(name, None)  # free the previous shape's buffers first
@@ -881,7 +882,10 @@ def generator_forward(net, x, cem=None):
         wss = [ws]
     if precision == 'x3':
         flags = wss[0].overflow if len(wss) == 1 else torch.stack([w.overflow for w in wss]).amax()
-        if int(flags.item()):  # one 4-byte D2H per forward
+        lag = _LAG[0]
+        if lag is not None:  # lagged_overflow_checks(): read one forward later, after the next one is enqueued
+            lag.push(net, x, cem, out, flags, wss)
+        elif int(flags.item()):  # one 4-byte D2H per forward
             OVERFLOW_RERUNS += 1
             for w in wss:
                 w.overflow.zero_()
@@ -890,7 +894,63 @@ def generator_forward(net, x, cem=None):
     return out
 
 
-def _forward(net, x, cem, precision, train_ws=None, rec=None):
+class _LaggedOverflow:
+    """The x3 overflow flag of inference forward N read after forward N + 1 has been enqueued (lagged_overflow_checks):
+    the host does not wait for the GPU to drain between forwards.  Forward N's flags go to pinned host memory by an
+    async copy (its device flags are then cleared for N + 1) and its input is kept (a device copy: the caller may reuse
+    its buffer); when N + 1 is enqueued, or the block ends, N's flags are read and an overflowed N is recomputed in exact
+    fp32 INTO the tensor forward N returned (stream-ordered: every later read of it on the stream sees the fp32 result).
+    The model's activation scale is lowered then — forward N + 1 was already enqueued at the old scale and is checked
+    the same way."""
+
+    def __init__(self):
+        self.pending = None
+
+    def push(self, net, x, cem, out, flags, wss):
+        host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+        host.copy_(flags.reshape(1).to(torch.int32), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        for w in wss:
+            w.overflow.zero_()
+        prev, self.pending = self.pending, (net, x.clone(), cem, out, host, ev)
+        self._settle(prev)  # N - 1's flag: forward N is enqueued by now
+
+    def _settle(self, item):
+        global OVERFLOW_RERUNS
+        if item is None:
+            return
+        net, x, cem, out, host, ev = item
+        ev.synchronize()
+        if int(host.item()):
+            OVERFLOW_RERUNS += 1
+            lower_act_scale(net)
+            redo, _ = _forward(net, x, cem, 'f32', slot='redo')
+            out.copy_(redo)
+
+    def close(self):
+        item, self.pending = self.pending, None
+        self._settle(item)
+
+
+_LAG = [None]
+
+
+@contextlib.contextmanager
+def lagged_overflow_checks():
+    """Inference forwards in this block read their x3 overflow flag one forward late (_LaggedOverflow): a stream of
+    forwards is enqueued back to back.  A tensor a forward returned holds its final (exact-fp32 if it overflowed) values
+    for every reader that comes after the NEXT forward call or after the block, in stream order; read it earlier only
+    after the block.  Default off: outside the block every forward checks its own flag before returning."""
+    prev, _LAG[0] = _LAG[0], _LaggedOverflow()
+    try:
+        yield _LAG[0]
+    finally:
+        lag, _LAG[0] = _LAG[0], prev
+        lag.close()
+
+
+def _forward(net, x, cem, precision, train_ws=None, rec=None, slot=None):
     """One generator (+CEM) forward.  With `train_ws` (esr_amd.train_engine) every RDB's concat buffer is kept for
     the backward pass instead of the inference ping-pong, and the workspace comes from the caller.  With `rec` (a
     _Recorder) the launches are recorded as an op list instead of issued."""
@@ -909,7 +969,7 @@ def _forward(net, x, cem, precision, train_ws=None, rec=None):
     m = int(cem.margins_LR) if pre_pad else 0
     H, W = h + 2 * m, w + 2 * m
     dev = x.device
-    ws = train_ws if train_ws is not None else _workspace(net, dev, Bn, H, W, latent, precision)
+    ws = train_ws if train_ws is not None else _workspace(net, dev, Bn, H, W, latent, precision, slot)
     pk = _packed(net, latent)
     _require_device(pk.first.bias, 'generator parameters')
     A = act_scale(net) if x3 else 1.0

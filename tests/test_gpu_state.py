@@ -108,3 +108,29 @@ def test_activation_scale_ratchet(gpu_device):
     assert engine.OVERFLOW_RERUNS == rer0 + 1
     err = float((small - exact).abs().max() / exact.abs().max())
     assert 0 < err < 1e-5, err  # x3 (not bitwise the fp32 path), fp32-level accuracy
+
+
+def test_lagged_overflow_check_returns_exact_fp32_output(gpu_device):
+    """engine.lagged_overflow_checks(): forward N's x3 overflow flag is read only after forward N + 1 is enqueued; an
+    overflowed N (inputs × 3e5 leave the f16 range) still returns N's exact-fp32 output — recomputed into the tensor N
+    returned — and N + 1 (enqueued before N was found to overflow, at the old activation scale) its own x3 output;
+    each bitwise equal to a fresh model's forward of the same input with the same precision and scale."""
+    from esr_amd import engine
+    d = golden('grad_plain_nb1')
+    _, params = fixture_params(d)
+    x_ok = fixture_input(d).to(gpu_device)
+    x_big = (x_ok * 3e5).contiguous()
+    with torch.no_grad():
+        ref_ok = _model(params, gpu_device).eval()(x_ok).clone()  # x3 at the default activation scale
+        f32 = _model(params, gpu_device).eval()
+        engine.set_precision(f32, 'f32')
+        ref_big = f32(x_big).clone()
+        model = _model(params, gpu_device).eval()
+        before = engine.OVERFLOW_RERUNS
+        with engine.lagged_overflow_checks():
+            o_big = model(x_big)
+            o_ok = model(x_ok)
+            o_big2 = model(x_big)  # (at the lowered scale: overflows again, redone at the block's end)
+    assert engine.OVERFLOW_RERUNS == before + 2
+    assert torch.equal(o_big, ref_big) and torch.equal(o_big2, ref_big)
+    assert torch.equal(o_ok, ref_ok)
