@@ -158,8 +158,8 @@ __global__ __launch_bounds__(256) void cem_down_tiled(const float *__restrict__ 
 // (77 × 141 values for kd = 17) in LDS de-interleaved by column phase x mod 4, rows padded to P ≡ 8 (mod 16) words.
 // Thread (tx, ty) owns the 4 consecutive outputs j0 + 4 tx + e of row i0 + ty: for every tap row u it reads the 8
 // values [4 tx, 4 tx + 8) of each phase row with two ds_read_b128 (conflict-free: 8 lanes cover 128 B of one row, the
-// next row group starts 32 banks later), i.e. 8 LDS reads per tap row for 4·kd FMAs, and the weights are wave-uniform
-// scalar loads.  Per output the taps are summed u-major, v ascending — the order of cem_down_tiled: bitwise equal.
+// next row group starts 32 banks later), i.e. 8 LDS reads per tap row for 4·kd FMAs, and the weights are broadcast
+// LDS reads.  Per output the taps are summed u-major, v ascending — the order of cem_down_tiled: bitwise equal.
 constexpr int DW_TX = 8, DW_TY = 16;  // 32 × 16 LR outputs, 128 threads
 // The window is staged from the 16-B-aligned column Xa = X0 & ~3 (O = X0 - Xa, a template parameter) with 16-B loads
 // (per-element clamped loads only where a 16-B group crosses the image border), all of a thread's loads in flight
@@ -175,6 +175,8 @@ __global__ __launch_bounds__(128) void cem_down_win4(const float *__restrict__ g
     constexpr int P = ((WC4 + 7) & ~15) + 8;              // >= WC4, ≡ 8 (mod 16) words
     constexpr int NL = (WR * WC4 + 127) / 128;            // 16-B loads per thread
     extern __shared__ __attribute__((aligned(16))) float smem[];
+    __shared__ float sw[KD * KD];  // the taps, read from LDS (broadcast), not as scalar loads: see cem_inv_tiled
+    for (int k = threadIdx.x; k < KD * KD; k += 128) sw[k] = wd[k];
     const int j0 = blockIdx.x * 4 * DW_TX, i0 = blockIdx.y * DW_TY;
     const long long plane = blockIdx.z;
     const int HH = sf * H, WW = sf * W, pd = kd / 2;
@@ -221,7 +223,7 @@ __global__ __launch_bounds__(128) void cem_down_win4(const float *__restrict__ g
             win[q][0] = a.x; win[q][1] = a.y; win[q][2] = a.z; win[q][3] = a.w;
             win[q][4] = b.x; win[q][5] = b.y; win[q][6] = b.z; win[q][7] = b.w;
         }
-        const float *wr = wd + u * kd;  // wave-uniform: scalar loads
+        const float *wr = sw + u * kd;  // wave-uniform row, broadcast LDS reads
 #pragma unroll
         for (int vv = 0; vv < kd; ++vv) {
             const float w = wr[vv];
