@@ -11,7 +11,7 @@ against the mean of the two single-process half-batch gradients, ≤ 1e-5 relati
 that the G step of micro-step 1 sees the same D in every run), the generator_step decisions, and that the G
 gradient's all-reduce buckets went out from inside the generator's backward while it still had RRDBs to do
 (train_engine._GeneratorFn._sliced_backward with the flat-mode GradBuckets), with the optimiser's flat buffer as the
-one autograd input (the single-process step's flat path) and one D BatchNorm-buffer broadcast per D step."""
+one autograd input (the single-process step's flat path) and one D BatchNorm-buffer broadcast per D optimiser step."""
 import os
 import socket
 import sys
@@ -57,8 +57,12 @@ def _run_half(half, dev):
     rng = np.random.default_rng(cfg['seed'] + 300 + half)
     model._interp_points = lambda n: torch.from_numpy(rng.random((n, 1, 1, 1)).astype(np.float32)).to(dev)
     first = {}
+    d_steps = []  # micro-steps with a D optimiser step (none at gradient step 0 with D_init_iters 0: SRRaGAN_model.py:360)
+    cur = [0]
     for o, tag in ((model.optimizer_G, 'G'), (model.optimizer_D, 'D')):
         def step(*a, _o=o, _step=o.step, _tag=tag, **kw):
+            if _tag == 'D':
+                d_steps.append(cur[0])
             if _tag not in first:
                 _o._sync_views()
                 first[_tag] = _o.flat.grad.detach().double().cpu().numpy()
@@ -78,9 +82,15 @@ def _run_half(half, dev):
         rf(lo)
         slices.append((lo, model._g_buckets.launched_in_backward))
     model._g_buckets.ready_from = ready_from
-    bcast = []  # torch.distributed.broadcast calls during the steps (the D BatchNorm buffers)
+    bcast = []  # torch.distributed.broadcast calls during the steps (the D BatchNorm buffers): (micro-step, caller)
     bb = dist.broadcast
-    dist.broadcast = lambda *a, **k: (bcast.append(1), bb(*a, **k))[1]
+
+    def counted(*a, **k):
+        import traceback
+        bcast.append((cur[0], ' <- '.join('%s:%d' % (os.path.basename(f.filename), f.lineno)
+                                          for f in traceback.extract_stack()[-5:-1])))
+        return bb(*a, **k)
+    dist.broadcast = counted
     flat_in = []
     import esr_amd.train_engine as TE
     fwd = TE._GeneratorFn.apply
@@ -101,6 +111,7 @@ def _run_half(half, dev):
     try:
         flags, fake = [], []
         for k in range(cfg['steps']):
+            cur[0] = k
             lr, hr, z = step_data(dict(cfg, batch=2 * B), k)
             sl = slice(half * B, (half + 1) * B)
             t = lambda a: torch.from_numpy(np.ascontiguousarray(a[sl])).to(dev)  # noqa: E731
@@ -124,7 +135,7 @@ def _run_half(half, dev):
         loc[tag] = v
     return {'first': first, 'flags': flags, 'fake': fake, 'dshapes': dshapes, 'local': loc, 'fresh': fresh, 'fwd_in': fwd_in,
             'logs': {k: [x[1] for x in v] for k, v in model.log_dict.items() if v},
-            'reruns': (E.OVERFLOW_RERUNS, E.ACT_SCALE_REDUCTIONS), 'slices': slices, 'n_buckets': n_buckets, 'bcast': len(bcast),
+            'reruns': (E.OVERFLOW_RERUNS, E.ACT_SCALE_REDUCTIONS), 'slices': slices, 'n_buckets': n_buckets, 'bcast': bcast, 'd_steps': d_steps,
             'flat_in': flat_in, 'world': world, 'comm': model._g_buckets.comm_stats()}
 
 
@@ -220,6 +231,8 @@ def test_c4_two_ranks_per_rank_production_shape():
         assert r['slices'][-1] == (0, r['n_buckets'])
         assert r['comm']['allreduces'] == r['n_buckets']  # one G gradient step: every bucket once
         assert all(r['flat_in']) and r['flat_in']  # the flat parameter as the generator's one autograd input
-        assert r['bcast'] == 2  # one D-buffer broadcast per D step (two D steps), not one per buffer
+        print('D steps at micro-steps %s; broadcasts (micro-step, caller): %s' % (r['d_steps'], r['bcast']))
+        # one D-buffer broadcast per D optimiser step, not one per buffer
+        assert r['d_steps'] and [b[0] for b in r['bcast']] == r['d_steps']
     for h in halves:
         assert all(h['flat_in']) and h['slices'] == [] and h['world'] == 1
