@@ -19,6 +19,7 @@ iteration, bench_zopt.py, with SURVEY §8's KernelGAN-recipe kernel; `zopt_c5_le
 """
 import argparse
 import collections
+import contextlib
 import json
 import os
 import sys
@@ -67,6 +68,9 @@ def parse():
                     'library, ESR_AMD_LIB=exp_lib/libesr_exp.so; default automatic)')
     ap.add_argument('--profile-steps', type=int, default=2, help='timed steps (the last ones) that carry per-launch HIP '
                     'events for the roofline')
+    ap.add_argument('--eager-overflow-check', action='store_true',
+                    help='every timed forward reads its own x3 overflow flag before returning (default: one forward '
+                         'late, engine.lagged_overflow_checks, as a serving loop runs)')
     ap.add_argument('--no-op-timers', action='store_true', help='time the steps without the per-launch HIP events '
                     '(no roofline; measures what the events themselves cost)')
     return ap.parse_args()
@@ -287,24 +291,19 @@ def host_io(model, x, out, args, dev, world):
             'note': 'PCIe-inclusive: pinned host LR batch in, HR output back to pinned host memory, per step'}
 
 
-def lagged_overflow(model, x, args, dev, world, dt_headline):
-    """The headline step with the x3 overflow flag read one forward late (engine.lagged_overflow_checks: forward N + 1
-    is enqueued before N's flag is read, so the host does not wait for the GPU between forwards; an overflowed N is
-    recomputed into its output in exact fp32).  Timed like the headline, without per-launch events; `value` stays the
-    default per-forward check."""
-    from esr_amd import engine
+def per_forward_check(model, x, args, dev, world, dt_headline):
+    """The headline step with each forward reading its own x3 overflow flag before it returns (the default outside
+    engine.lagged_overflow_checks: one 4-byte device-to-host read per forward, the host waits for the GPU to drain
+    between forwards).  Timed like the headline, without per-launch events."""
     with torch.no_grad():
-        dt0 = _timed(lambda: model(x), args.steps, dev, world)  # the default check, no per-launch events
-        with engine.lagged_overflow_checks():
-            model(x)
-            dt = _timed(lambda: model(x), args.steps, dev, world)
+        dt = _timed(lambda: model(x), args.steps, dev, world)
     hr = 4 * args.lr_size
     return {'value': round(world * args.batch * hr * hr * args.steps / dt / 1e6, 3), 'unit': 'HR Mpixels/s',
             'ms_per_step': round(dt / args.steps * 1e3, 3), 'steps': args.steps,
-            'default_check_ms_per_step': round(dt0 / args.steps * 1e3, 3),
             'headline_ms_per_step': round(dt_headline / args.steps * 1e3, 3),
-            'note': 'overflow flag read one forward late (engine.lagged_overflow_checks), no per-launch events; the '
-                    'headline reads each forward\'s flag before returning and carries events on its last steps'}
+            'note': 'each forward reads its own overflow flag before returning (no per-launch events); the headline '
+                    'reads forward N\'s flag after forward N + 1 is enqueued (engine.lagged_overflow_checks) and '
+                    'carries events on its last steps'}
 
 
 def run_legs(args, dev, world, rank):
@@ -393,15 +392,21 @@ def main():
         prof = []
         origin = engine.ProfileOrigin(dev)
         origin.record()
+        # A serving loop: each forward's x3 overflow flag is read one forward late (engine.lagged_overflow_checks),
+        # so forward N + 1 is enqueued before the host waits on N; the block's exit settles the last flag (an
+        # overflowed forward is recomputed in exact fp32 into its own output) inside the timed region.
+        lag = contextlib.nullcontext() if args.eager_overflow_check or args.precision != 'x3' \
+            else engine.lagged_overflow_checks()
         t0 = time.perf_counter()
         ev_prof = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-        for i in range(args.steps):  # per-launch events on the last n_prof steps only (their cost: ~1.5 % of a step)
-            engine._PROFILE = prof if (not args.no_op_timers and i >= args.steps - n_prof) else None
-            if i == args.steps - n_prof:
-                ev_prof[0].record()  # the profiled steps' own wall time on the device (the busy fraction's base)
-            out = model(x)
-        ev_prof[1].record()
-        torch.cuda.synchronize()
+        with lag:
+            for i in range(args.steps):  # per-launch events on the last n_prof steps only (~1.5 % of a step)
+                engine._PROFILE = prof if (not args.no_op_timers and i >= args.steps - n_prof) else None
+                if i == args.steps - n_prof:
+                    ev_prof[0].record()  # the profiled steps' own wall time on the device (the busy fraction's base)
+                out = model(x)
+            ev_prof[1].record()
+            torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         engine._PROFILE = None
         engine.release_timers()
@@ -499,7 +504,10 @@ def main():
     if args.host_io_steps > 0:
         rec['host_io'] = host_io(model, x, out, args, dev, world)
     if args.precision == 'x3':
-        rec['lagged_overflow'] = lagged_overflow(model, x, args, dev, world, dt)
+        rec['overflow_check'] = 'per forward' if args.eager_overflow_check else \
+            'lagged by one forward (engine.lagged_overflow_checks), last flag settled inside the timed region'
+        if not args.eager_overflow_check:
+            rec['per_forward_check'] = per_forward_check(model, x, args, dev, world, dt)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb, parity = cpu_baseline(args, model, x, out, None if args.no_cem else make_gt(args, dev, rank))
         if not args.no_cpu_variants:

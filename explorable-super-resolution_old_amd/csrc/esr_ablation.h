@@ -51,6 +51,9 @@ int esr_cem_set_direct(int32_t direct);
 int esr_wgrad_set_kernel(int32_t variant);
 /* x3 weight gradient of split-f16 output gradients: 1 (product) = LDS-DMA kernel, 0 = register-staged kernel. */
 int esr_wgrad3_set_dma(int32_t on);
+/* Diagnostic time split of the LDS-DMA x3 weight-gradient kernel (garbage results): 0 (product), 1 = LDS-DMA of the
+ * first pixel tile only, 2 = no fragment reads / MFMAs, 3 = both (loop skeleton). */
+int esr_wgrad3d_set_dbg(int32_t mode);
 /* Discriminator convs: 1 (product) = halo-tile kernels where they pay, 0 = gather kernels, 2 = halo wherever it fits. */
 int esr_dconv_set_halo(int32_t on);
 /* x3 halo kernel at three workgroups per CU where its LDS allows: 1 (product) / 0 (bitwise identical). */

@@ -50,6 +50,7 @@ struct WgradParams {
     int B, H, W, tiles_x, tiles_y, splits, cin_pad;
     float *partial;  // [splits][9*cin_pad*cout_pad + cout_pad]
     int dsplit;      // output gradient in the split-f16 layout (x3 kernel only)
+    int dbg;         // wgrad3d diagnostic time split (ablation library only: g_wgrad3d_dbg)
 };
 
 __global__ __launch_bounds__(256, 1) void wgrad_kernel(WgradParams p) {
@@ -727,12 +728,17 @@ __global__ __launch_bounds__((W3D<NCT, TH>::NT), 1) void wgrad3d_kernel(WgradPar
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
 
+#ifdef ESR_X3_EXPERIMENTS
+    const int dbg = p.dbg;  // g_wgrad3d_dbg: 1 LDS-DMA of the first tile only, 2 no fragment reads / MFMAs
+#else
+    constexpr int dbg = 0;
+#endif
     if (t_begin < t_end) dma_tile(t_begin, 0);
     for (int t = t_begin; t < t_end; ++t) {
         const int stg = (t - t_begin) & 1;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of tile t are in LDS
         __syncthreads();  // ... every wave's; and every wave is done reading stage stg ^ 1 (tile t - 1)
-        if (t + 1 < t_end) dma_tile(t + 1, stg ^ 1);
+        if (t + 1 < t_end && !(dbg & 1)) dma_tile(t + 1, stg ^ 1);
         const unsigned char *s_in = smem + stg * C::STAGE, *s_d = s_in + C::IN_B;
         if (chunk == 0) {
             for (int px = bp0; px < C::D_PX; px += BST) {
@@ -743,6 +749,7 @@ __global__ __launch_bounds__((W3D<NCT, TH>::NT), 1) void wgrad3d_kernel(WgradPar
             }
         }
         const unsigned char *img_d = s_d + ct * C::D_B;
+        if (dbg & 2) continue;
 #pragma unroll 2
         for (int kk = 0; kk < 2 * TH / NQ; ++kk) {
             const int kb = NQ * kk + q;             // K block: 16 pixels of tile row kb >> 1
@@ -1471,6 +1478,7 @@ extern "C" int esr_conv3x3_wgrad(const float *in, int32_t in_cp, int32_t cin, in
     p.splits = splits; p.cin_pad = (cin + 31) / 32 * 32;
     p.partial = partial;
     p.dsplit = dsplit;
+    p.dbg = g_wgrad3d_dbg;
     const unsigned total = (unsigned)(p.cin_pad / 32 * splits);
     if (x3 && dsplit && g_wgrad3_dma) {
         const unsigned grid = 8 * ((total + 7) / 8);

@@ -138,7 +138,7 @@ ABLATION_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), 'exp_lib',
 ABLATION_SETTERS = ('esr_x3_set_kernel', 'esr_x3_set_tile_map', 'esr_x3_set_narrow', 'esr_x3_set_nsplit',
                     'esr_conv_set_tile', 'esr_cem_set_direct', 'esr_wgrad_set_kernel', 'esr_wgrad3_set_dma',
                     'esr_dconv_set_halo', 'esr_dconv_set_occ3', 'esr_dconv_set_cw16', 'esr_dconv_set_rows',
-                    'esr_axpby_set_rows', 'esr_bn_set_onepass', 'esr_x3c_set_stamps')
+                    'esr_axpby_set_rows', 'esr_bn_set_onepass', 'esr_x3c_set_stamps', 'esr_wgrad3d_set_dbg')
 
 _lib = None
 
