@@ -1,4 +1,4 @@
-"""Bitwise determinism of the discriminator step pieces (tools/loop_determinism.py found ~1e-8 run-to-run differences
+"""Bitwise determinism of the discriminator step pieces (a round-3 loop probe found ~1e-8 run-to-run differences
 in D conv / BN weight gradients): runs each variant 3 times on the same inputs and lists the parameters whose
 gradients differ.  Usage (GPU): python tools/d_determinism.py [H]"""
 import os

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Per-kernel means of the counters of tools/pmc_x3.sh's passes (rocprofv3 counter_collection.csv files)."""
+"""Per-kernel means of the counters of tools/pmc_x3.sh's or tools/pmc_bench_sq.sh's passes (rocprofv3 counter_collection.csv
+files)."""
 import csv
 import glob
 import os

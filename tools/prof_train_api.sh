@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 kernel + HIP API trace of bench_train.py (config 3) -> OUTDIR/trace: which host calls the GPU's idle gaps
-# follow (tools/api_gaps.py)
+# follow (round-4 gap attribution; tools/gap_attrib.py is the torch.profiler form)
 out=$1; shift
 R=$GRAFT_REPO_ROOT; mkdir -p $R/$out
 cd /tmp && export TMPDIR=/tmp
