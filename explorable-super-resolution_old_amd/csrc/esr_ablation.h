@@ -54,6 +54,8 @@ int esr_wgrad3_set_dma(int32_t on);
 /* Diagnostic time split of the LDS-DMA x3 weight-gradient kernel (garbage results): 0 (product), 1 = LDS-DMA of the
  * first pixel tile only, 2 = no fragment reads / MFMAs, 3 = both (loop skeleton). */
 int esr_wgrad3d_set_dbg(int32_t mode);
+/* Unroll of the LDS-DMA x3 weight-gradient kernel's K-block loop: 4 (product, full), 2 or 1 (bitwise identical). */
+int esr_wgrad3d_set_unroll(int32_t u);
 /* Discriminator convs: 1 (product) = halo-tile kernels where they pay, 0 = gather kernels, 2 = halo wherever it fits. */
 int esr_dconv_set_halo(int32_t on);
 /* x3 halo kernel at three workgroups per CU where its LDS allows: 1 (product) / 0 (bitwise identical). */

@@ -31,6 +31,10 @@ extern "C" int esr_cem_set_direct(int32_t direct) { return set_knob(g_cem_direct
 extern "C" int esr_wgrad_set_kernel(int32_t variant) { return set_knob(g_wgrad_kernel, variant, 0, 1); }
 extern "C" int esr_wgrad3_set_dma(int32_t on) { return set_knob(g_wgrad3_dma, on, 0, 1); }
 extern "C" int esr_wgrad3d_set_dbg(int32_t mode) { return set_knob(g_wgrad3d_dbg, mode, 0, 3); }
+extern "C" int esr_wgrad3d_set_unroll(int32_t u) {
+    if (u != 1 && u != 2 && u != 4) return ESR_EINVAL;
+    return set_knob(g_wgrad3d_unroll, u, 1, 4);
+}
 extern "C" int esr_dconv_set_halo(int32_t on) { return set_knob(g_dconv_halo, on, 0, 2); }
 extern "C" int esr_dconv_set_occ3(int32_t on) { return set_knob(g_dconv_occ3, on, 0, 1); }
 extern "C" int esr_dconv_set_cw16(int32_t on) { return set_knob(g_dconv_cw16, on, 0, 1); }

@@ -17,6 +17,7 @@
     X(g_cem_direct, 0)   /* the untiled CEM inverse / up-add kernels                                               */ \
     X(g_wgrad_kernel, 1) /* 1 = 12-wave weight-gradient kernel, 0 = 4-wave                                         */ \
     X(g_wgrad3_dma, 1)   /* x3 weight gradient of split-f16 output gradients on the LDS-DMA kernel                 */ \
+    X(g_wgrad3d_unroll, 4) /* unroll of wgrad3d's K-block loop: 4 (full, round 6: 5-8 % faster), 2, 1; bitwise equal */ \
     X(g_wgrad3d_dbg, 0)  /* diagnostic time split of wgrad3d (garbage results): 1 LDS-DMA of the first tile only,  */ \
                          /* 2 no fragment reads / MFMAs, 3 both                                                    */ \
     X(g_dconv_halo, 1)   /* discriminator convs on the halo-tile kernels where they pay (0: gather; 2: wherever)   */ \

@@ -650,7 +650,7 @@ typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) const void glob_void;
 __device__ __attribute__((aligned(16))) unsigned char g_wzero[64];  // zero page: the DMA source of absent records
 
-template <int NCT, int TH>
+template <int NCT, int TH, int KU = 4>  // KU: unroll of the K-block loop (4 = full; A/B: esr_wgrad3d_set_unroll)
 __global__ __launch_bounds__((W3D<NCT, TH>::NT), 1) void wgrad3d_kernel(WgradParams p) {
     using C = W3D<NCT, TH>;
     constexpr int NT_ = C::NT, NQ = C::NQ;
@@ -750,7 +750,7 @@ __global__ __launch_bounds__((W3D<NCT, TH>::NT), 1) void wgrad3d_kernel(WgradPar
         }
         const unsigned char *img_d = s_d + ct * C::D_B;
         if (dbg & 2) continue;
-#pragma unroll 2
+#pragma unroll(KU)
         for (int kk = 0; kk < 2 * TH / NQ; ++kk) {
             const int kb = NQ * kk + q;             // K block: 16 pixels of tile row kb >> 1
             const int py = kb >> 1, px0 = 16 * (kb & 1) + 8 * hl + rq;
@@ -1485,8 +1485,22 @@ extern "C" int esr_conv3x3_wgrad(const float *in, int32_t in_cp, int32_t cin, in
         const hipStream_t st = (hipStream_t)stream;
         if (p.cout_pad == 64) {
             p.tiles_y = (H + 3) / 4;
+#ifdef ESR_X3_EXPERIMENTS
+            if (g_wgrad3d_unroll == 1)
+                hipLaunchKernelGGL((wgrad3d_kernel<2, 4, 1>), dim3(grid), dim3(W3D<2, 4>::NT), 0, st, p);
+            else if (g_wgrad3d_unroll == 2)
+                hipLaunchKernelGGL((wgrad3d_kernel<2, 4, 2>), dim3(grid), dim3(W3D<2, 4>::NT), 0, st, p);
+            else
+#endif
             hipLaunchKernelGGL((wgrad3d_kernel<2, 4>), dim3(grid), dim3(W3D<2, 4>::NT), 0, st, p);
         } else {
+#ifdef ESR_X3_EXPERIMENTS
+            if (g_wgrad3d_unroll == 1)
+                hipLaunchKernelGGL((wgrad3d_kernel<1, 8, 1>), dim3(grid), dim3(W3D<1, 8>::NT), 0, st, p);
+            else if (g_wgrad3d_unroll == 2)
+                hipLaunchKernelGGL((wgrad3d_kernel<1, 8, 2>), dim3(grid), dim3(W3D<1, 8>::NT), 0, st, p);
+            else
+#endif
             hipLaunchKernelGGL((wgrad3d_kernel<1, 8>), dim3(grid), dim3(W3D<1, 8>::NT), 0, st, p);
         }
     } else if (x3) {

@@ -138,7 +138,8 @@ ABLATION_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), 'exp_lib',
 ABLATION_SETTERS = ('esr_x3_set_kernel', 'esr_x3_set_tile_map', 'esr_x3_set_narrow', 'esr_x3_set_nsplit',
                     'esr_conv_set_tile', 'esr_cem_set_direct', 'esr_wgrad_set_kernel', 'esr_wgrad3_set_dma',
                     'esr_dconv_set_halo', 'esr_dconv_set_occ3', 'esr_dconv_set_cw16', 'esr_dconv_set_rows',
-                    'esr_axpby_set_rows', 'esr_bn_set_onepass', 'esr_x3c_set_stamps', 'esr_wgrad3d_set_dbg')
+                    'esr_axpby_set_rows', 'esr_bn_set_onepass', 'esr_x3c_set_stamps', 'esr_wgrad3d_set_dbg',
+                    'esr_wgrad3d_set_unroll')
 
 _lib = None
 
@@ -176,6 +177,8 @@ def bind(path):
             lib.esr_axpby_set_rows(int(os.environ['ESR_AXPBY_ROWS']))
         if os.environ.get('ESR_X3_KERNEL', '').isdigit():
             lib.esr_x3_set_kernel(int(os.environ['ESR_X3_KERNEL']))
+        if os.environ.get('ESR_WGRAD3D_UNROLL') in ('1', '2', '4'):
+            lib.esr_wgrad3d_set_unroll(int(os.environ['ESR_WGRAD3D_UNROLL']))
     else:
         stale = [k for k in RETIRED_ENV if k in os.environ]
         if stale:  # switches of earlier rounds: the product library has no selection state, so they change nothing
@@ -187,8 +190,8 @@ def bind(path):
 
 
 # environment switches that now act only through the ablation library's setters (ignored by the product library)
-RETIRED_ENV = ('ESR_X3_NSPLIT', 'ESR_AXPBY_ROWS', 'ESR_X3_KERNEL', 'ESR_DCONV_HALO', 'ESR_DCONV_OCC3',
-               'ESR_DCONV_CW16', 'ESR_DCONV_ROWS', 'ESR_WGRAD3_DMA', 'ESR_X3_TILE_MAP', 'ESR_X3_NARROW')
+RETIRED_ENV = ('ESR_X3_NSPLIT', 'ESR_AXPBY_ROWS', 'ESR_X3_KERNEL', 'ESR_WGRAD3D_UNROLL', 'ESR_DCONV_HALO',
+               'ESR_DCONV_OCC3', 'ESR_DCONV_CW16', 'ESR_DCONV_ROWS', 'ESR_WGRAD3_DMA', 'ESR_X3_TILE_MAP', 'ESR_X3_NARROW')
 
 
 def load():

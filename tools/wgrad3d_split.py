@@ -3,7 +3,8 @@ at the config-3 shapes (B=16, 96² LR, latent: concat buffers of 200 channels, c
 ablation library's diagnostic modes (esr_wgrad3d_set_dbg; garbage results): 0 = the kernel as built, 1 = LDS-DMA of
 each workgroup's first pixel tile only ("compute alone"), 2 = no fragment reads / MFMAs ("DMA alone"), 3 = both (loop
 skeleton).  Average µs per launch, order-balanced (two rounds, the second reported), TFLOP/s fp32-equivalent
-(2·9·Cin·Cout per output pixel).
+(2·9·Cin·Cout per output pixel).  Then the K-block loop unroll (esr_wgrad3d_set_unroll 1 / 2 / 4 = product since round 6): µs per
+launch and whether the partials are bitwise the product's.
 
     python tools/wgrad3d_split.py
 """
@@ -36,7 +37,8 @@ def main():
         chunks = (cin + 31) // 32
         ntiles = B * ((H + 7) // 8) * ((W + 31) // 32)
         splits = max(1, min(128, 256 // chunks, ntiles))
-        n = 9 * 32 * chunks * (64 if cout > 32 else 32) + 64
+        cout_pad = 64 if cout > 32 else 32
+        n = 9 * 32 * chunks * cout_pad + cout_pad
         part = torch.empty(splits * n, device=dev)
         flops = 2 * 9 * cin * cout * B * H * W
 
@@ -60,6 +62,19 @@ def main():
                     row['mode%d_us' % mode] = round(us, 2)
                     row['mode%d_tflops' % mode] = round(flops / us / 1e6, 1)
         lib.esr_wgrad3d_set_dbg(0)
+        parts, times = {}, {1: [], 2: [], 4: []}
+        for order in ((2, 4, 1), (4, 1, 2), (1, 2, 4), (2, 4, 1)):  # rotated: each position once, the first twice
+            for u in order:
+                lib.esr_wgrad3d_set_unroll(u)
+                part.fill_(float('nan'))
+                run(0, 3)
+                times[u].append(round(run(0, 30), 2))
+                parts[u] = part.clone()
+        for u in (1, 2, 4):
+            row['unroll%d_us' % u] = times[u]
+        row['unroll1_bitwise'] = bool(torch.equal(parts[1], parts[2]))
+        row['unroll4_bitwise'] = bool(torch.equal(parts[4], parts[2]))
+        lib.esr_wgrad3d_set_unroll(4)
         print(name, json.dumps(row), flush=True)
 
 
