@@ -750,7 +750,7 @@ __global__ __launch_bounds__((W3D<NCT, TH>::NT), 1) void wgrad3d_kernel(WgradPar
         }
         const unsigned char *img_d = s_d + ct * C::D_B;
         if (dbg & 2) continue;
-#pragma unroll(KU)
+#pragma unroll KU
         for (int kk = 0; kk < 2 * TH / NQ; ++kk) {
             const int kb = NQ * kk + q;             // K block: 16 pixels of tile row kb >> 1
             const int py = kb >> 1, px0 = 16 * (kb & 1) + 8 * hl + rq;
